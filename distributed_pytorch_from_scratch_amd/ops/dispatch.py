@@ -1,0 +1,43 @@
+"""Device -> kernel-set selection.
+
+``K(t)`` returns the module implementing the kernel API for tensor ``t``: the native HIP
+extension for GPU tensors (loud failure if it is not built), ``reference`` for CPU tensors.
+Both expose identical function names/signatures (see ``ops/reference.py``).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _ext, reference
+
+
+def K(t: torch.Tensor):
+    if t.is_cuda:
+        return _ext.require()
+    return reference
+
+
+def shadow(p: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """Low-precision compute copy of an fp32 master parameter.
+
+    The copy is cached on the parameter and re-cast only when the parameter's version
+    counter moved (``load_state_dict``, a torch optimizer step, ``copy_``).  The fused HIP
+    Adam (``ops.optim.FusedAdam``) writes the master and the shadow in the same kernel without
+    bumping the version, so the steady state costs no cast kernel at all.
+    """
+    if p.dtype == dtype:
+        return p.detach()
+    c = getattr(p, "_dpfs_shadow", None)
+    if c is not None and c[0] == p._version and c[1].dtype == dtype and c[1].device == p.device \
+            and c[1].shape == p.shape:
+        return c[1]
+    s = p.detach().to(dtype)
+    p._dpfs_shadow = (p._version, s)
+    return s
+
+
+def peek_shadow(p: torch.Tensor):
+    c = getattr(p, "_dpfs_shadow", None)
+    if c is None or c[0] != p._version or c[1].shape != p.shape:
+        return None
+    return c[1]

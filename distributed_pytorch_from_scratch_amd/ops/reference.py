@@ -1,0 +1,284 @@
+"""Pure-PyTorch reference kernels: the CPU compute path and the numerical oracle.
+
+Every function here has the *same signature and semantics* as the HIP kernel of the same
+name in ``csrc/kernels`` (exported by ``_C``).  Tests compare the two; on CPU the model runs
+on these.  Math is done in fp32 and results are cast to the input dtype, matching the GPU
+kernels' accumulate-in-fp32 policy.
+
+Reference parity notes (``/root/reference``):
+
+* ``rmsnorm_fwd``: ``models/layers.py:145-155`` (``scale * (x * rsqrt(mean(x^2)+eps))``).
+* ``rope_``: ``models/model.py:17-46`` (HF rotate-half; cos/sin tables with duplicated
+  halves, angles ``pos * theta`` in fp32).
+* ``attention``: ``models/model.py:73-77`` (causal, softmax(QK^T/sqrt(hd)) V).
+* ``swiglu``: ``models/model.py:94-95``.
+* ``embedding_fwd``: ``models/layers.py:134-141`` without the in-place mutation of the ids.
+* ``vocab-parallel CE``: extension; the reference all-gathers logits and calls
+  ``F.cross_entropy(ignore_index=-1)`` (``train.py:101-104``).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+
+# ------------------------------------------------------------------------------- GEMM ----
+
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """c[M,N] = a[M,K] @ b[N,K]^T (+ bias[N]); output dtype = a.dtype."""
+    c = a.float() @ b.float().t()
+    if bias is not None:
+        c = c + bias.float()
+    return c.to(a.dtype)
+
+
+def gemm_nn(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """c[M,N] = a[M,K] @ b[K,N]; output dtype = a.dtype."""
+    return (a.float() @ b.float()).to(a.dtype)
+
+
+def gemm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
+            accumulate: bool = False) -> torch.Tensor:
+    """c[M,N] (fp32) = a[K,M]^T @ b[K,N]  (+= into ``out`` if ``accumulate``)."""
+    c = a.float().t() @ b.float()
+    if out is None:
+        return c
+    if accumulate:
+        out.add_(c)
+    else:
+        out.copy_(c)
+    return out
+
+
+def add_bias_(y: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    """y[M,N] += bias[N] in place (fp32 add, rounded to y.dtype); returns y."""
+    y.copy_((y.float() + bias.float()).to(y.dtype))
+    return y
+
+
+def bias_grad(dy: torch.Tensor) -> torch.Tensor:
+    """fp32 column sums of dy[M,N]."""
+    return dy.float().sum(0)
+
+
+# -------------------------------------------------------------------------- norms ----
+
+def rmsnorm_fwd(x: torch.Tensor, w: torch.Tensor, eps: float) -> Tuple[torch.Tensor, torch.Tensor]:
+    xf = x.float()
+    rstd = torch.rsqrt(xf.pow(2).mean(-1) + eps)
+    y = (xf * rstd[:, None]).to(x.dtype).float() * w.float()
+    return y.to(x.dtype), rstd
+
+
+def rmsnorm_bwd(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, rstd: torch.Tensor):
+    xf, dyf, wf = x.float(), dy.float(), w.float()
+    xhat = xf * rstd[:, None]
+    dw = (dyf * xhat).sum(0)
+    g = dyf * wf
+    d = xf.size(-1)
+    dx = rstd[:, None] * (g - xhat * (g * xhat).sum(-1, keepdim=True) / d)
+    return dx.to(x.dtype), dw
+
+
+def layernorm_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float):
+    xf = x.float()
+    mean = xf.mean(-1)
+    var = (xf - mean[:, None]).pow(2).mean(-1)
+    rstd = torch.rsqrt(var + eps)
+    y = (xf - mean[:, None]) * rstd[:, None] * w.float() + b.float()
+    return y.to(x.dtype), mean, rstd
+
+
+def layernorm_bwd(dy, x, w, mean, rstd):
+    xf, dyf, wf = x.float(), dy.float(), w.float()
+    xhat = (xf - mean[:, None]) * rstd[:, None]
+    dw = (dyf * xhat).sum(0)
+    db = dyf.sum(0)
+    g = dyf * wf
+    d = xf.size(-1)
+    dx = rstd[:, None] * (g - g.mean(-1, keepdim=True) - xhat * (g * xhat).sum(-1, keepdim=True) / d)
+    return dx.to(x.dtype), dw, db
+
+
+# --------------------------------------------------------------------------- RoPE ----
+
+def rope_table(maxlen: int, head_dim: int, theta: float, device=None) -> torch.Tensor:
+    """fp32 ``(maxlen, head_dim)`` table: columns [cos(pos*inv_freq) | sin(pos*inv_freq)] for
+    the ``head_dim/2`` frequencies (the reference duplicates each half; we store it once).
+    ``inv_freq`` is computed on CPU in fp32 exactly as ``models/model.py:38``."""
+    assert head_dim % 2 == 0
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.int64).float() / head_dim))
+    pos = torch.arange(maxlen).float().unsqueeze(1)
+    ang = pos * inv
+    tab = torch.cat([torch.cos(ang), torch.sin(ang)], dim=1)
+    return tab.to(device) if device is not None else tab
+
+
+def rope_(qkv: torch.Tensor, positions: torch.Tensor, table: torch.Tensor, n_rot_heads: int,
+          head_dim: int, inverse: bool = False) -> torch.Tensor:
+    """Rotate (in place) the first ``n_rot_heads`` heads of each row of ``qkv[M, *]``.
+
+    ``positions[M]`` indexes ``table``.  ``inverse`` applies the transpose rotation (the RoPE
+    backward).  Rotate-half convention: out1 = x1 c - x2 s, out2 = x2 c + x1 s.
+    """
+    M = qkv.size(0)
+    h2 = head_dim // 2
+    tab = table[positions.long()]  # (M, hd)
+    c = tab[:, None, :h2]
+    s = tab[:, None, h2:]
+    if inverse:
+        s = -s
+    view = qkv[:, : n_rot_heads * head_dim].view(M, n_rot_heads, head_dim)
+    x1 = view[..., :h2].float()
+    x2 = view[..., h2:].float()
+    o1 = x1 * c - x2 * s
+    o2 = x2 * c + x1 * s
+    view[..., :h2] = o1.to(qkv.dtype)
+    view[..., h2:] = o2.to(qkv.dtype)
+    return qkv
+
+
+# ---------------------------------------------------------------------- attention ----
+
+def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float,
+             causal: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+    """q,k,v: (B, T, H, hd) (any strides). Returns o (B, T, H, hd) contiguous and the
+    natural-log LSE (B, H, T) fp32 of the scaled scores."""
+    qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))  # B H T hd
+    s = (qf @ kf.transpose(-1, -2)) * scale
+    if causal:
+        T, S = s.shape[-2], s.shape[-1]
+        mask = torch.ones(T, S, dtype=torch.bool, device=s.device).triu(1)
+        s = s.masked_fill(mask, float("-inf"))
+    lse = torch.logsumexp(s, dim=-1)
+    p = torch.exp(s - lse[..., None])
+    o = (p @ vf).transpose(1, 2).contiguous()
+    return o.to(q.dtype), lse
+
+
+def attn_bwd(do, q, k, v, o, lse, scale: float, causal: bool, dq_out, dk_out, dv_out):
+    """Writes dq/dk/dv into the given (B, T, H, hd) views (packed dqkv buffer)."""
+    qf, kf, vf, dof, of = (t.float().transpose(1, 2) for t in (q, k, v, do, o))
+    s = (qf @ kf.transpose(-1, -2)) * scale
+    if causal:
+        T, S = s.shape[-2], s.shape[-1]
+        mask = torch.ones(T, S, dtype=torch.bool, device=s.device).triu(1)
+        s = s.masked_fill(mask, float("-inf"))
+    p = torch.exp(s - lse[..., None])
+    dv = p.transpose(-1, -2) @ dof
+    dp = dof @ vf.transpose(-1, -2)
+    delta = (dof * of).sum(-1, keepdim=True)
+    ds = p * (dp - delta) * scale
+    dq = ds @ kf
+    dk = ds.transpose(-1, -2) @ qf
+    dq_out.copy_(dq.transpose(1, 2))
+    dk_out.copy_(dk.transpose(1, 2))
+    dv_out.copy_(dv.transpose(1, 2))
+
+
+# ------------------------------------------------------------------------- SwiGLU ----
+
+def swiglu_fwd(gu: torch.Tensor) -> torch.Tensor:
+    F_ = gu.size(-1) // 2
+    g, u = gu[..., :F_].float(), gu[..., F_:].float()
+    return (F.silu(g) * u).to(gu.dtype)
+
+
+def swiglu_bwd(dh: torch.Tensor, gu: torch.Tensor) -> torch.Tensor:
+    F_ = gu.size(-1) // 2
+    g, u = gu[..., :F_].float(), gu[..., F_:].float()
+    dhf = dh.float()
+    sig = torch.sigmoid(g)
+    silu = g * sig
+    dg = dhf * u * sig * (1 + g * (1 - sig))
+    du = dhf * silu
+    return torch.cat([dg, du], dim=-1).to(gu.dtype)
+
+
+# ---------------------------------------------------------------------- embedding ----
+
+def embedding_fwd(ids: torch.Tensor, weight: torch.Tensor, vocab_start: int,
+                  out_dtype: torch.dtype) -> torch.Tensor:
+    """Rows of the local vocab shard for ids in [vocab_start, vocab_start+V_local), zeros
+    elsewhere.  Does not mutate ``ids`` (the reference does, ``layers.py:138``)."""
+    vl = weight.size(0)
+    local = ids.long() - vocab_start
+    m = (local >= 0) & (local < vl)
+    out = weight[local.clamp(0, vl - 1)].float() * m[:, None].float()
+    return out.to(out_dtype)
+
+
+def embedding_bwd(dout: torch.Tensor, ids: torch.Tensor, v_local: int, vocab_start: int) -> torch.Tensor:
+    local = ids.long() - vocab_start
+    m = (local >= 0) & (local < v_local)
+    dw = torch.zeros(v_local, dout.size(-1), dtype=torch.float32, device=dout.device)
+    dw.index_add_(0, local[m], dout[m].float())
+    return dw
+
+
+# ------------------------------------------------------------ vocab-parallel CE ----
+
+def ce_fwd_stats(logits: torch.Tensor, targets: torch.Tensor, vocab_start: int,
+                 vocab_valid: int) -> torch.Tensor:
+    """Per-row local statistics of one vocab shard: (M, 3) fp32 = [max, sum(exp(x-max)),
+    target_logit (0 if the target is not in this shard)].  Columns ``>= vocab_valid`` (the
+    padded vocab tail inside this shard) are excluded."""
+    x = logits.float()
+    if vocab_valid < x.size(1):
+        x = x[:, :vocab_valid]
+    mx = x.max(dim=1).values
+    se = torch.exp(x - mx[:, None]).sum(1)
+    local = targets.long() - vocab_start
+    hit = (local >= 0) & (local < x.size(1))
+    tl = torch.where(hit, x.gather(1, local.clamp(0, max(x.size(1) - 1, 0))[:, None]).squeeze(1),
+                     torch.zeros_like(mx))
+    return torch.stack([mx, se, tl], dim=1)
+
+
+def ce_combine(stats: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """stats: (n_shards, M, 3) gathered from every TP rank -> (lse[M], target_logit[M])."""
+    mx = stats[..., 0].max(0).values
+    se = (stats[..., 1] * torch.exp(stats[..., 0] - mx[None])).sum(0)
+    lse = mx + torch.log(se)
+    tl = stats[..., 2].sum(0)
+    return lse, tl
+
+
+def ce_bwd(logits: torch.Tensor, targets: torch.Tensor, lse: torch.Tensor, gscale: torch.Tensor,
+           vocab_start: int, vocab_valid: int, out: torch.Tensor) -> torch.Tensor:
+    """d logits = (softmax - onehot) * gscale[row] (gscale = 0 on ignored rows); padded
+    columns get 0.  Written to ``out`` (may alias ``logits``: the GPU kernel runs in place)."""
+    x = logits.float()
+    p = torch.exp(x - lse[:, None])
+    local = targets.long() - vocab_start
+    hit = (local >= 0) & (local < vocab_valid)
+    p[hit, local[hit]] -= 1.0
+    p = p * gscale[:, None]
+    if vocab_valid < x.size(1):
+        p[:, vocab_valid:] = 0
+    out.copy_(p)
+    return out
+
+
+# -------------------------------------------------------------------------- Adam ----
+
+def adam_step(params, grads, exp_avgs, exp_avg_sqs, shadows, lr: float, beta1: float,
+              beta2: float, eps: float, weight_decay: float, step: int, grad_scale: float = 1.0):
+    """In-place Adam (torch.optim.Adam semantics, L2 ``weight_decay`` added to the gradient
+    as in ``torch.optim.Adam``); also refreshes optional low-precision shadow copies."""
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    for i, p in enumerate(params):
+        g = grads[i].float() * grad_scale
+        if weight_decay != 0:
+            g = g + weight_decay * p
+        m, v = exp_avgs[i], exp_avg_sqs[i]
+        m.mul_(beta1).add_(g, alpha=1 - beta1)
+        v.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+        denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+        p.addcdiv_(m, denom, value=-lr / bc1)
+        if shadows is not None and shadows[i] is not None:
+            shadows[i].copy_(p)

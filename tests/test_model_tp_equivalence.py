@@ -1,0 +1,135 @@
+"""TP is numerically transparent (SURVEY.md §0 key invariant), CPU/gloo.
+
+Same seed => TP=k weights equal the TP=1 / vanilla weights exactly, and the loss trajectory
+over several Adam steps matches to ~1e-5 (fp32).  Also covers uneven head partitions (6
+heads over 4 ranks), a non-divisible vocab, sequence parallelism and the reference
+state-dict layout.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from dist_helpers import run_distributed
+from vanilla_model import VanillaTransformer
+
+
+def _batch(V, B, T, seed=123):
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.randint(0, V, (B, T), generator=g)
+    tgt = torch.randint(0, V, (B, T), generator=g)
+    tgt[0, -3:] = -1  # ignored positions
+    pos = torch.arange(T).unsqueeze(0).repeat(B, 1)
+    return ids, pos, tgt
+
+
+CFG = dict(attn_dim=64, ffn_dim=128, num_heads=4, num_layers=2, vocab_size=96, maxlen=64)
+
+
+def _train_parallel(rank, world, cfg, steps, sp, use_loss_api):
+    from distributed_pytorch_from_scratch_amd.models import Transformer, ModelArgs
+    from distributed_pytorch_from_scratch_amd.utils.dist import set_seed
+    args = ModelArgs(**cfg, vocab_pad_to=1, sequence_parallel=sp)
+    m = Transformer.from_args(args)
+    set_seed(0)
+    m.reset_parameters()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    losses = []
+    for s in range(steps):
+        ids, pos, tgt = _batch(cfg["vocab_size"], 2, 16, seed=100 + s)
+        if use_loss_api:
+            loss = m.loss(ids, pos, tgt)
+        else:
+            logits = m(ids, pos)
+            loss = F.cross_entropy(logits.reshape(-1, logits.size(-1)), tgt.reshape(-1), ignore_index=-1)
+        opt.zero_grad()
+        loss.backward()
+        if sp:
+            from distributed_pytorch_from_scratch_amd.parallel.grad_sync import allreduce_sequence_parallel_grads
+            allreduce_sequence_parallel_grads(m)
+        opt.step()
+        losses.append(loss.item())
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    return losses, sd
+
+
+def _train_vanilla(cfg, steps):
+    m = VanillaTransformer(**cfg)
+    torch.manual_seed(0)      # RNG replay: same state right before reset_parameters()
+    m.reset_parameters()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    losses = []
+    for s in range(steps):
+        ids, pos, tgt = _batch(cfg["vocab_size"], 2, 16, seed=100 + s)
+        logits = m(ids, pos)
+        loss = F.cross_entropy(logits.reshape(-1, logits.size(-1)), tgt.reshape(-1), ignore_index=-1)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    return losses, m
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_tp_matches_vanilla_loss_trajectory(world):
+    van, _ = _train_vanilla(CFG, 3)
+    res = run_distributed(_train_parallel, world, CFG, 3, False, True)
+    for r in range(world):
+        assert torch.allclose(torch.tensor(res[r][0]), torch.tensor(van), atol=2e-5), (res[r][0], van)
+
+
+def test_tp_gathered_logits_api_matches():
+    van, _ = _train_vanilla(CFG, 2)
+    res = run_distributed(_train_parallel, 2, CFG, 2, False, False)
+    assert torch.allclose(torch.tensor(res[0][0]), torch.tensor(van), atol=2e-5)
+
+
+def test_uneven_heads_and_vocab():
+    cfg = dict(CFG, num_heads=8, attn_dim=48, vocab_size=97)   # 8 heads of 6 over 3 ranks
+    van, _ = _train_vanilla(cfg, 2)
+    res = run_distributed(_train_parallel, 3, cfg, 2, False, True)
+    for r in range(3):
+        assert torch.allclose(torch.tensor(res[r][0]), torch.tensor(van), atol=2e-5)
+
+
+def test_sequence_parallel_matches():
+    van, _ = _train_vanilla(CFG, 3)
+    res = run_distributed(_train_parallel, 2, CFG, 3, True, True)
+    for r in range(2):
+        assert torch.allclose(torch.tensor(res[r][0]), torch.tensor(van), atol=2e-5), (res[r][0], van)
+
+
+def test_state_dict_layout_is_reference_layout():
+    cfg = dict(CFG)
+    res = run_distributed(_train_parallel, 2, cfg, 1, False, True)
+    sd = res[0][1]
+    L = cfg["num_layers"]
+    assert len(sd) == 1 + L * 16 + 1 + 2  # emb, 16 per layer, norm, lm_head w+b (196 at L=12)
+    d, f, V = cfg["attn_dim"], cfg["ffn_dim"], cfg["vocab_size"]
+    assert sd["layers.0.attn.wq.weight"].shape == (d // 2, d)
+    assert sd["layers.0.attn.wo.weight"].shape == (d, d // 2)
+    assert sd["layers.0.attn.wo.bias"].shape == (d,)
+    assert sd["layers.0.ffn.gate_proj.weight"].shape == (f // 2, d)
+    assert sd["layers.0.ffn.down_proj.weight"].shape == (d, f // 2)
+    assert sd["embedding.weight"].shape == (V // 2, d)
+    assert sd["lm_head.bias"].shape == (V // 2,)
+    assert "layers.1.norm2.scale" in sd and "norm.scale" in sd
+
+
+def _load_roundtrip(rank, world):
+    from distributed_pytorch_from_scratch_amd.models import Transformer, ModelArgs
+    from distributed_pytorch_from_scratch_amd.utils.dist import set_seed
+    set_seed(0)
+    m = Transformer.from_args(ModelArgs(**CFG, vocab_pad_to=1))
+    m.reset_parameters()
+    sd = m.state_dict()
+    set_seed(1)
+    m2 = Transformer.from_args(ModelArgs(**CFG, vocab_pad_to=1))
+    m2.reset_parameters()
+    m2.load_state_dict(sd)
+    ids, pos, tgt = _batch(CFG["vocab_size"], 2, 8)
+    return (m(ids, pos) - m2(ids, pos)).abs().max().item()
+
+
+def test_state_dict_roundtrip():
+    res = run_distributed(_load_roundtrip, 2)
+    assert res[0] == 0.0 and res[1] == 0.0
