@@ -1,0 +1,178 @@
+#!/usr/bin/env python
+"""Headline benchmark: tokens/sec (whole node) training GPT-2-small-class TP on MI355X.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launched with
+``torch.distributed.run --nproc-per-node N`` (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from env).
+W untimed warmup steps, then EXACTLY K timed steps bracketed by barrier + synchronize on both
+sides, elapsed = MAX over ranks, rank 0 prints ONE JSON line.
+
+Config (BASELINE.json metric "tokens/sec (whole node), GPT-2-small TP at 1/2/4/8 MI355X"):
+GPT-2 small shape in the reference block (d=768, 12 layers, 12 heads, SwiGLU ffn 2048,
+vocab 50257 padded to 50304, untied head; 123.6M matmul params), seq_len 1024, bf16 compute
+with fp32 master weights + Adam, random init, synthetic uniform token data.  Tensor
+parallel degree = N (12 heads over 8 ranks: 2 heads on ranks 0-3, 1 on ranks 4-7).  Weak
+scaling: the global batch is ``--batch-per-gpu x N`` sequences (every rank does the same
+FLOPs per step for every N).
+
+``--impl reference`` times the reference's eager formulation (nn.Linear/autocast, materialised
+causal softmax, full-logit CE, torch.optim.Adam; tests/vanilla_model.py) on one GPU — the
+in-house "reference code on MI355X" baseline recorded in BASELINE.md.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+# Per-GPU throughput of the reference formulation on MI355X at TP=1 (bench.py --impl reference,
+# gpt2-small, seq 1024, batch 16); see BASELINE.md.  None until measured.
+REFERENCE_TOKENS_PER_S_TP1 = None
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="gpt2-small")
+    ap.add_argument("--seq-len", type=int, default=1024)
+    ap.add_argument("--batch-per-gpu", type=int, default=16)
+    ap.add_argument("--global-batch", type=int, default=None, help="override (strong scaling)")
+    ap.add_argument("--sp", action="store_true", help="Megatron sequence parallelism")
+    ap.add_argument("--impl", choices=["ours", "reference"], default="ours")
+    ap.add_argument("--layers", type=int, default=None, help="debug only: not a valid headline number")
+    ap.add_argument("--seed", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    from distributed_pytorch_from_scratch_amd.models import get_preset, Transformer
+    from distributed_pytorch_from_scratch_amd.ops.optim import FusedAdam
+    from distributed_pytorch_from_scratch_amd.engine import TrainStep
+    from distributed_pytorch_from_scratch_amd.utils.dist import init_dist_env, set_seed
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and a.gpus > 1:
+        raise SystemExit("for --gpus > 1 launch with torch.distributed.run --nproc-per-node N")
+    assert world == a.gpus, f"WORLD_SIZE={world} but --gpus {a.gpus}"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29511")
+    p = init_dist_env(rank=None, tp_size=world)
+    rank = dist.get_rank()
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+
+    overrides = dict(sequence_parallel=a.sp)
+    if a.layers:
+        overrides["num_layers"] = a.layers
+    args = get_preset(a.model, **overrides)
+    T = a.seq_len
+    assert T <= args.maxlen
+    gb = a.global_batch or a.batch_per_gpu * world
+    V = args.vocab_size
+
+    set_seed(a.seed)
+    g = torch.Generator(device=dev).manual_seed(1234)  # same synthetic data on every TP rank
+    n_pool = 4
+    pool = [torch.randint(0, V, (gb, T + 1), device=dev, generator=g) for _ in range(n_pool)]
+    pos = torch.arange(T, device=dev).unsqueeze(0).expand(gb, T).contiguous()
+
+    if a.impl == "ours":
+        model = Transformer.from_args(args).to(dev)
+        model.reset_parameters()
+        opt = FusedAdam(model.parameters(), lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.0)
+        step = TrainStep(model, opt)
+
+        def run(i):
+            b = pool[i % n_pool]
+            return step(b[:, :-1], pos, b[:, 1:])
+    else:
+        assert world == 1, "--impl reference is the single-GPU eager baseline"
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from vanilla_model import VanillaTransformer
+        import torch.nn.functional as F
+        model = VanillaTransformer(args.attn_dim, args.ffn_dim, args.num_heads, args.num_layers, V,
+                                   args.maxlen, args.rope_theta).to(dev)
+        model.cos, model.sin = model.cos.to(dev), model.sin.to(dev)
+        model.reset_parameters()
+        opt = torch.optim.Adam(model.parameters(), lr=3e-4)
+
+        def run(i):
+            b = pool[i % n_pool]
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                logits = model(b[:, :-1], pos)
+                loss = F.cross_entropy(logits.float().view(-1, V), b[:, 1:].reshape(-1), ignore_index=-1)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            return loss.detach()
+
+    for i in range(a.warmup):
+        loss = run(i)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        loss = run(a.warmup + i)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    final_loss = float(loss.float().item())
+
+    tokens = gb * T * a.steps
+    value = tokens / elapsed
+    base = REFERENCE_TOKENS_PER_S_TP1
+    vs = None
+    if base:
+        # Reference measured at TP=1; for N>1 compare against ideal linear scaling of it.
+        vs = value / (base * world)
+    mflops = args.flops_per_token(T)
+    out = {
+        "metric": "tokens/sec (whole node), GPT-2-small TP at 1/2/4/8 MI355X",
+        "value": round(value, 1),
+        "unit": "tokens/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(1000 * elapsed / a.steps, 3),
+        "higher_is_better": True,
+        "scaling": "strong" if a.global_batch else "weak",
+        "vs_baseline": round(vs, 4) if vs else None,
+        "dtype": "bf16",
+        "data": "synthetic (uniform random token ids), random-init weights",
+        "config": {
+            "model": a.model + (f"(L={a.layers})" if a.layers else ""),
+            "global_batch": gb,
+            "seq_len": T,
+            "parallelism": f"tp{world}" + ("+sp" if a.sp else ""),
+            "impl": a.impl,
+            "params_matmul": args.matmul_params(),
+        },
+        "tflops_per_gpu": round(value * mflops / world / 1e12, 2),
+        "final_loss": round(final_loss, 4),
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

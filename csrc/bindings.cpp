@@ -1,0 +1,511 @@
+// Python bindings of the gfx950 kernels: torch tensors in, kernels launched on the current
+// HIP stream (so they interleave correctly with RCCL collectives issued by
+// torch.distributed on its own streams and with hipGraph capture).
+//
+// Every function validates device/dtype/shape/stride assumptions of its kernel on the host
+// BEFORE launching (an out-of-bounds wave can reset the whole node), allocates outputs from
+// the PyTorch caching allocator, and mirrors the signature of the pure-PyTorch oracle of
+// the same name in distributed_pytorch_from_scratch_amd/ops/reference.py.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <ATen/DeviceGuard.h>
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+extern "C" {
+void dpfs_gemm_nt(const void*, const void*, void*, const float*, int, int, int, int, int, int, hipStream_t);
+void dpfs_gemm_nn(const void*, const void*, void*, int, int, int, int, int, int, hipStream_t);
+int dpfs_gemm_tn_splits(int, int, int);
+void dpfs_gemm_tn(const void*, const void*, float*, float*, int, int, int, int, int, int, hipStream_t);
+void dpfs_rmsnorm_fwd(int, const void*, const float*, void*, float*, int, int, float, hipStream_t);
+void dpfs_layernorm_fwd(int, const void*, const float*, const float*, void*, float*, float*, int, int, float,
+                        hipStream_t);
+int dpfs_norm_bwd_grid(int);
+void dpfs_norm_bwd(int, int, const void*, const void*, const float*, const float*, const float*, void*, float*, float*,
+                   float*, float*, int, int, hipStream_t);
+void dpfs_swiglu_fwd(int, const void*, void*, int, int, hipStream_t);
+void dpfs_swiglu_bwd(int, const void*, const void*, void*, int, int, hipStream_t);
+void dpfs_rope(int, void*, const int64_t*, const float*, int, int, int, int, int, hipStream_t);
+void dpfs_bias_residual(int, const void*, const float*, const void*, void*, int, int, hipStream_t);
+int dpfs_colsum_groups(int);
+void dpfs_bias_grad(int, const void*, float*, float*, int, int, hipStream_t);
+void dpfs_embedding_fwd(int, const int64_t*, const float*, void*, int, int, long long, int, hipStream_t);
+void dpfs_embedding_bwd(int, const void*, const int64_t*, float*, int, int, long long, int, hipStream_t);
+void dpfs_ce_stats(int, const void*, const int64_t*, float*, int, int, long long, int, hipStream_t);
+void dpfs_ce_bwd(int, const void*, const int64_t*, const float*, const float*, void*, int, int, long long, int,
+                 hipStream_t);
+int dpfs_adam_chunk();
+int dpfs_adam_desc_bytes();
+void dpfs_adam_step(const void*, const int*, int, float, float, float, float, float, float, float, float, const float*,
+                    hipStream_t);
+void dpfs_grad_sumsq(const void*, const int*, int, float*, hipStream_t);
+int dpfs_attn_supported_hd(int);
+void dpfs_attn_fwd(const void*, const void*, const void*, void*, float*, int, int, int, int, long long, long long,
+                   long long, long long, float, int, hipStream_t);
+void dpfs_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, float*, void*, void*,
+                   void*, int, int, int, int, long long, long long, long long, long long, long long, long long,
+                   long long, long long, float, int, hipStream_t);
+}
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+int dcode(const torch::Tensor& t) {
+  if (t.scalar_type() == torch::kBFloat16) return 1;
+  if (t.scalar_type() == torch::kFloat32) return 0;
+  TORCH_CHECK(false, "unsupported dtype ", t.scalar_type(), " (bf16 / fp32 only)");
+  return -1;
+}
+
+void check_cuda(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a HIP (cuda) tensor");
+}
+
+void check_rowmajor(const torch::Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.dim() == 2, name, " must be 2-D, got ", t.dim(), "-D");
+  TORCH_CHECK(t.stride(1) == 1, name, " must have unit inner stride");
+}
+
+const float* opt_f32(const c10::optional<torch::Tensor>& t, int64_t n, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  check_cuda(*t, name);
+  TORCH_CHECK(t->scalar_type() == torch::kFloat32 && t->is_contiguous() && t->numel() == n, name,
+              " must be a contiguous fp32 vector of length ", n);
+  return t->data_ptr<float>();
+}
+
+// -------------------------------------------------------------------------------- GEMM --
+torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> bias) {
+  check_rowmajor(a, "a");
+  check_rowmajor(b, "b");
+  TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "gemm_nt: bf16 operands");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K, "gemm_nt: K mismatch ", K, " vs ", b.size(1));
+  TORCH_CHECK(K % 8 == 0, "gemm_nt: K must be a multiple of 8, got ", K);
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm_nt: row strides must be multiples of 8");
+  const at::DeviceGuard g(a.device());
+  auto c = torch::empty({M, N}, a.options());
+  if (M == 0 || N == 0) return c;
+  if (K == 0) return c.zero_();
+  TORCH_CHECK(N % 2 == 0 || true, "");
+  dpfs_gemm_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), opt_f32(bias, N, "bias"), (int)M, (int)N, (int)K,
+               (int)a.stride(0), (int)b.stride(0), (int)N, stream());
+  return c;
+}
+
+torch::Tensor gemm_nn(torch::Tensor a, torch::Tensor b) {
+  check_rowmajor(a, "a");
+  check_rowmajor(b, "b");
+  TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "gemm_nn: bf16 operands");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(1);
+  TORCH_CHECK(b.size(0) == K, "gemm_nn: K mismatch");
+  TORCH_CHECK(K % 8 == 0 && N % 8 == 0, "gemm_nn: K and N must be multiples of 8, got ", K, " ", N);
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm_nn: row strides must be multiples of 8");
+  const at::DeviceGuard g(a.device());
+  auto c = torch::empty({M, N}, a.options());
+  if (M == 0 || N == 0) return c;
+  if (K == 0) return c.zero_();
+  dpfs_gemm_nn(a.data_ptr(), b.data_ptr(), c.data_ptr(), (int)M, (int)N, (int)K, (int)a.stride(0), (int)b.stride(0),
+               (int)N, stream());
+  return c;
+}
+
+// c[M,N] fp32 = a[K,M]^T b[K,N]
+torch::Tensor gemm_tn(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> out, bool accumulate) {
+  check_rowmajor(a, "a");
+  check_rowmajor(b, "b");
+  TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "gemm_tn: bf16 operands");
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
+  TORCH_CHECK(b.size(0) == K, "gemm_tn: K mismatch");
+  TORCH_CHECK(M % 8 == 0 && N % 8 == 0, "gemm_tn: M and N must be multiples of 8, got ", M, " ", N);
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm_tn: row strides must be multiples of 8");
+  const at::DeviceGuard g(a.device());
+  torch::Tensor c;
+  if (out.has_value() && out->defined()) {
+    c = *out;
+    TORCH_CHECK(c.scalar_type() == torch::kFloat32 && c.is_contiguous() && c.size(0) == M && c.size(1) == N,
+                "gemm_tn: out must be contiguous fp32 [M,N]");
+  } else {
+    c = torch::empty({M, N}, a.options().dtype(torch::kFloat32));
+    accumulate = false;
+  }
+  if (M == 0 || N == 0) return c;
+  if (K == 0) {
+    if (!accumulate) c.zero_();
+    return c;
+  }
+  const int S = dpfs_gemm_tn_splits((int)M, (int)N, (int)K);
+  torch::Tensor ws;
+  if (S > 1 || accumulate) ws = torch::empty({(int64_t)S * M * N}, c.options());
+  dpfs_gemm_tn(a.data_ptr(), b.data_ptr(), c.data_ptr<float>(), ws.defined() ? ws.data_ptr<float>() : nullptr, (int)M,
+               (int)N, (int)K, (int)a.stride(0), (int)b.stride(0), accumulate ? 1 : 0, stream());
+  return c;
+}
+
+torch::Tensor bias_grad(torch::Tensor dy) {
+  check_rowmajor(dy, "dy");
+  TORCH_CHECK(dy.is_contiguous(), "bias_grad: dy must be contiguous");
+  const int64_t M = dy.size(0), N = dy.size(1);
+  const int vec = dcode(dy) == 1 ? 8 : 4;
+  TORCH_CHECK(N % vec == 0, "bias_grad: N must be a multiple of ", vec);
+  const at::DeviceGuard g(dy.device());
+  auto out = torch::empty({N}, dy.options().dtype(torch::kFloat32));
+  if (M == 0) return out.zero_();
+  auto ws = torch::empty({(int64_t)dpfs_colsum_groups((int)M) * N}, out.options());
+  dpfs_bias_grad(dcode(dy), dy.data_ptr(), out.data_ptr<float>(), ws.data_ptr<float>(), (int)M, (int)N, stream());
+  return out;
+}
+
+torch::Tensor add_bias_(torch::Tensor y, torch::Tensor bias) {
+  check_rowmajor(y, "y");
+  TORCH_CHECK(y.is_contiguous(), "add_bias_: y must be contiguous");
+  const int64_t M = y.size(0), N = y.size(1);
+  const int vec = dcode(y) == 1 ? 8 : 4;
+  TORCH_CHECK(N % vec == 0, "add_bias_: N must be a multiple of ", vec);
+  const float* bp = opt_f32(bias, N, "bias");
+  const at::DeviceGuard g(y.device());
+  if (M) dpfs_bias_residual(dcode(y), y.data_ptr(), bp, nullptr, y.data_ptr(), (int)M, (int)N, stream());
+  return y;
+}
+
+// out = residual + y (+ bias)
+torch::Tensor bias_residual(torch::Tensor y, c10::optional<torch::Tensor> bias, torch::Tensor residual) {
+  check_rowmajor(y, "y");
+  TORCH_CHECK(y.is_contiguous() && residual.is_contiguous() && residual.sizes() == y.sizes() &&
+                  residual.scalar_type() == y.scalar_type(),
+              "bias_residual: y and residual must be contiguous, same shape/dtype");
+  const int64_t M = y.size(0), N = y.size(1);
+  const int vec = dcode(y) == 1 ? 8 : 4;
+  TORCH_CHECK(N % vec == 0, "bias_residual: N must be a multiple of ", vec);
+  const at::DeviceGuard g(y.device());
+  auto out = torch::empty_like(y);
+  if (M) dpfs_bias_residual(dcode(y), y.data_ptr(), opt_f32(bias, N, "bias"), residual.data_ptr(), out.data_ptr(),
+                            (int)M, (int)N, stream());
+  return out;
+}
+
+// ------------------------------------------------------------------------------- norms --
+int check_norm_x(const torch::Tensor& x, const torch::Tensor& w) {
+  check_rowmajor(x, "x");
+  TORCH_CHECK(x.is_contiguous(), "norm: x must be contiguous");
+  const int dt = dcode(x);
+  const int64_t D = x.size(1);
+  TORCH_CHECK(D % (dt == 1 ? 8 : 4) == 0 && D <= 16 * 64 * (dt == 1 ? 8 : 4), "norm: unsupported hidden size ", D);
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kFloat32 && w.is_contiguous() && w.numel() == D,
+              "norm: weight must be contiguous fp32 [D]");
+  return dt;
+}
+
+std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, torch::Tensor w, double eps) {
+  const int dt = check_norm_x(x, w);
+  const at::DeviceGuard g(x.device());
+  const int64_t M = x.size(0), D = x.size(1);
+  auto y = torch::empty_like(x);
+  auto rstd = torch::empty({M}, x.options().dtype(torch::kFloat32));
+  if (M) dpfs_rmsnorm_fwd(dt, x.data_ptr(), w.data_ptr<float>(), y.data_ptr(), rstd.data_ptr<float>(), (int)M, (int)D,
+                          (float)eps, stream());
+  return {y, rstd};
+}
+
+std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor rstd) {
+  const int dt = check_norm_x(x, w);
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.is_contiguous() && dy.scalar_type() == x.scalar_type(), "rmsnorm_bwd: dy");
+  const at::DeviceGuard g(x.device());
+  const int64_t M = x.size(0), D = x.size(1);
+  auto dx = torch::empty_like(x);
+  auto dw = torch::empty({D}, w.options());
+  if (M == 0) return {dx, dw.zero_()};
+  auto ws = torch::empty({(int64_t)dpfs_norm_bwd_grid((int)M) * D}, w.options());
+  dpfs_norm_bwd(0, dt, dy.data_ptr(), x.data_ptr(), w.data_ptr<float>(), nullptr, rstd.data_ptr<float>(), dx.data_ptr(),
+                dw.data_ptr<float>(), nullptr, ws.data_ptr<float>(), nullptr, (int)M, (int)D, stream());
+  return {dx, dw};
+}
+
+std::vector<torch::Tensor> layernorm_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor b, double eps) {
+  const int dt = check_norm_x(x, w);
+  TORCH_CHECK(b.is_cuda() && b.scalar_type() == torch::kFloat32 && b.numel() == x.size(1), "layernorm: bias");
+  const at::DeviceGuard g(x.device());
+  const int64_t M = x.size(0), D = x.size(1);
+  auto y = torch::empty_like(x);
+  auto mean = torch::empty({M}, x.options().dtype(torch::kFloat32));
+  auto rstd = torch::empty({M}, x.options().dtype(torch::kFloat32));
+  if (M) dpfs_layernorm_fwd(dt, x.data_ptr(), w.data_ptr<float>(), b.data_ptr<float>(), y.data_ptr(),
+                            mean.data_ptr<float>(), rstd.data_ptr<float>(), (int)M, (int)D, (float)eps, stream());
+  return {y, mean, rstd};
+}
+
+std::vector<torch::Tensor> layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor mean,
+                                         torch::Tensor rstd) {
+  const int dt = check_norm_x(x, w);
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.is_contiguous() && dy.scalar_type() == x.scalar_type(),
+              "layernorm_bwd: dy");
+  const at::DeviceGuard g(x.device());
+  const int64_t M = x.size(0), D = x.size(1);
+  auto dx = torch::empty_like(x);
+  auto dw = torch::empty({D}, w.options());
+  auto db = torch::empty({D}, w.options());
+  if (M == 0) return {dx, dw.zero_(), db.zero_()};
+  const int64_t G = dpfs_norm_bwd_grid((int)M);
+  auto ws = torch::empty({2 * G * D}, w.options());
+  dpfs_norm_bwd(1, dt, dy.data_ptr(), x.data_ptr(), w.data_ptr<float>(), mean.data_ptr<float>(),
+                rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr<float>(), db.data_ptr<float>(),
+                ws.data_ptr<float>(), ws.data_ptr<float>() + G * D, (int)M, (int)D, stream());
+  return {dx, dw, db};
+}
+
+// ------------------------------------------------------------------------ elementwise --
+torch::Tensor swiglu_fwd(torch::Tensor gu) {
+  check_rowmajor(gu, "gu");
+  TORCH_CHECK(gu.is_contiguous(), "swiglu: gu must be contiguous");
+  const int dt = dcode(gu);
+  const int64_t M = gu.size(0), F = gu.size(1) / 2;
+  TORCH_CHECK(gu.size(1) % 2 == 0 && F % (dt == 1 ? 8 : 4) == 0, "swiglu: F must be a multiple of the vector width");
+  const at::DeviceGuard g(gu.device());
+  auto h = torch::empty({M, F}, gu.options());
+  if (M) dpfs_swiglu_fwd(dt, gu.data_ptr(), h.data_ptr(), (int)M, (int)F, stream());
+  return h;
+}
+
+torch::Tensor swiglu_bwd(torch::Tensor dh, torch::Tensor gu) {
+  check_rowmajor(gu, "gu");
+  const int dt = dcode(gu);
+  const int64_t M = gu.size(0), F = gu.size(1) / 2;
+  TORCH_CHECK(dh.is_contiguous() && dh.size(0) == M && dh.size(1) == F && dh.scalar_type() == gu.scalar_type(),
+              "swiglu_bwd: dh");
+  TORCH_CHECK(F % (dt == 1 ? 8 : 4) == 0, "swiglu: F must be a multiple of the vector width");
+  const at::DeviceGuard g(gu.device());
+  auto dgu = torch::empty_like(gu);
+  if (M) dpfs_swiglu_bwd(dt, dh.data_ptr(), gu.data_ptr(), dgu.data_ptr(), (int)M, (int)F, stream());
+  return dgu;
+}
+
+torch::Tensor rope_(torch::Tensor qkv, torch::Tensor positions, torch::Tensor table, int64_t n_rot_heads,
+                    int64_t head_dim, bool inverse) {
+  check_rowmajor(qkv, "qkv");
+  TORCH_CHECK(positions.is_cuda() && positions.scalar_type() == torch::kInt64 && positions.is_contiguous() &&
+                  positions.numel() == qkv.size(0),
+              "rope: positions must be contiguous int64 [M]");
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == torch::kFloat32 && table.is_contiguous() &&
+                  table.dim() == 2 && table.size(1) == head_dim,
+              "rope: table must be fp32 [maxlen, head_dim]");
+  TORCH_CHECK(head_dim % 8 == 0, "rope: head_dim must be a multiple of 8");
+  TORCH_CHECK(n_rot_heads * head_dim <= qkv.size(1), "rope: too many heads for the row");
+  const at::DeviceGuard g(qkv.device());
+  const int64_t M = qkv.size(0);
+  if (M) dpfs_rope(dcode(qkv), qkv.data_ptr(), positions.data_ptr<int64_t>(), table.data_ptr<float>(), (int)M,
+                   (int)qkv.stride(0), (int)n_rot_heads, (int)head_dim, inverse ? 1 : 0, stream());
+  return qkv;
+}
+
+// ---------------------------------------------------------------------------- attention --
+struct View4 {
+  long long ld;
+};
+
+View4 check_bthd(const torch::Tensor& t, const char* name, int64_t B, int64_t T, int64_t H, int64_t hd) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16, name, " must be bf16");
+  TORCH_CHECK(t.dim() == 4 && t.size(0) == B && t.size(1) == T && t.size(2) == H && t.size(3) == hd, name,
+              " must be (B, T, H, hd)");
+  TORCH_CHECK(t.stride(3) == 1 && t.stride(2) == hd && (B == 1 || t.stride(0) == T * t.stride(1)), name,
+              " must be a (B*T, ld) row view with packed heads");
+  TORCH_CHECK(t.stride(1) % 8 == 0, name, " token stride must be a multiple of 8");
+  return {(long long)t.stride(1)};
+}
+
+std::vector<torch::Tensor> attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, double scale, bool causal) {
+  const int64_t B = q.size(0), T = q.size(1), H = q.size(2), hd = q.size(3);
+  TORCH_CHECK(dpfs_attn_supported_hd((int)hd), "attn: head_dim ", hd, " not supported (32/64/128)");
+  auto vq = check_bthd(q, "q", B, T, H, hd), vk = check_bthd(k, "k", B, T, H, hd), vv = check_bthd(v, "v", B, T, H, hd);
+  const at::DeviceGuard g(q.device());
+  auto o = torch::empty({B, T, H, hd}, q.options());
+  auto lse = torch::empty({B, H, T}, q.options().dtype(torch::kFloat32));
+  if (B * T * H)
+    dpfs_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), (int)B, (int)T,
+                  (int)H, (int)hd, vq.ld, vk.ld, vv.ld, H * hd, (float)scale, causal ? 1 : 0, stream());
+  return {o, lse};
+}
+
+void attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Tensor o,
+              torch::Tensor lse, double scale, bool causal, torch::Tensor dq, torch::Tensor dk, torch::Tensor dv) {
+  const int64_t B = q.size(0), T = q.size(1), H = q.size(2), hd = q.size(3);
+  TORCH_CHECK(dpfs_attn_supported_hd((int)hd), "attn: head_dim not supported");
+  auto vq = check_bthd(q, "q", B, T, H, hd), vk = check_bthd(k, "k", B, T, H, hd), vv = check_bthd(v, "v", B, T, H, hd);
+  auto vdo = check_bthd(dout, "dout", B, T, H, hd), vo = check_bthd(o, "o", B, T, H, hd);
+  auto vdq = check_bthd(dq, "dq", B, T, H, hd), vdk = check_bthd(dk, "dk", B, T, H, hd),
+       vdv = check_bthd(dv, "dv", B, T, H, hd);
+  TORCH_CHECK(lse.is_cuda() && lse.scalar_type() == torch::kFloat32 && lse.is_contiguous() && lse.numel() == B * H * T,
+              "attn_bwd: lse must be contiguous fp32 (B, H, T)");
+  const at::DeviceGuard g(q.device());
+  if (B * T * H == 0) return;
+  auto delta = torch::empty({B, H, T}, lse.options());
+  dpfs_attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
+                delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), (int)B, (int)T, (int)H, (int)hd,
+                vdo.ld, vq.ld, vk.ld, vv.ld, vo.ld, vdq.ld, vdk.ld, vdv.ld, (float)scale, causal ? 1 : 0, stream());
+}
+
+// ------------------------------------------------------------------- embedding / CE --
+torch::Tensor embedding_fwd(torch::Tensor ids, torch::Tensor weight, int64_t vocab_start, py::object out_dtype) {
+  check_cuda(ids, "ids");
+  check_cuda(weight, "weight");
+  TORCH_CHECK(ids.scalar_type() == torch::kInt64 && ids.is_contiguous() && ids.dim() == 1, "embedding: ids int64 [M]");
+  TORCH_CHECK(weight.scalar_type() == torch::kFloat32 && weight.is_contiguous() && weight.dim() == 2 &&
+                  weight.size(1) % 4 == 0,
+              "embedding: weight must be contiguous fp32 [V_local, D], D % 4 == 0");
+  const auto odt = torch::python::detail::py_object_to_dtype(out_dtype);
+  TORCH_CHECK(odt == torch::kBFloat16 || odt == torch::kFloat32, "embedding: out dtype bf16/fp32");
+  const at::DeviceGuard g(ids.device());
+  const int64_t M = ids.numel(), D = weight.size(1);
+  auto out = torch::empty({M, D}, weight.options().dtype(odt));
+  if (M) dpfs_embedding_fwd(odt == torch::kBFloat16 ? 1 : 0, ids.data_ptr<int64_t>(), weight.data_ptr<float>(),
+                            out.data_ptr(), (int)M, (int)D, vocab_start, (int)weight.size(0), stream());
+  return out;
+}
+
+torch::Tensor embedding_bwd(torch::Tensor dout, torch::Tensor ids, int64_t v_local, int64_t vocab_start) {
+  check_rowmajor(dout, "dout");
+  TORCH_CHECK(dout.is_contiguous(), "embedding_bwd: dout contiguous");
+  TORCH_CHECK(ids.scalar_type() == torch::kInt64 && ids.is_contiguous() && ids.numel() == dout.size(0),
+              "embedding_bwd: ids");
+  const at::DeviceGuard g(dout.device());
+  const int64_t M = dout.size(0), D = dout.size(1);
+  auto dw = torch::zeros({v_local, D}, dout.options().dtype(torch::kFloat32));
+  if (M) dpfs_embedding_bwd(dcode(dout), dout.data_ptr(), ids.data_ptr<int64_t>(), dw.data_ptr<float>(), (int)M,
+                            (int)D, vocab_start, (int)v_local, stream());
+  return dw;
+}
+
+torch::Tensor ce_fwd_stats(torch::Tensor logits, torch::Tensor targets, int64_t vocab_start, int64_t vocab_valid) {
+  check_rowmajor(logits, "logits");
+  TORCH_CHECK(logits.is_contiguous(), "ce: logits contiguous");
+  TORCH_CHECK(targets.scalar_type() == torch::kInt64 && targets.is_contiguous() && targets.numel() == logits.size(0),
+              "ce: targets int64 [M]");
+  TORCH_CHECK(vocab_valid >= 0 && vocab_valid <= logits.size(1), "ce: vocab_valid out of range");
+  const at::DeviceGuard g(logits.device());
+  const int64_t M = logits.size(0), V = logits.size(1);
+  auto stats = torch::empty({M, 3}, logits.options().dtype(torch::kFloat32));
+  if (M) dpfs_ce_stats(dcode(logits), logits.data_ptr(), targets.data_ptr<int64_t>(), stats.data_ptr<float>(), (int)M,
+                       (int)V, vocab_start, (int)vocab_valid, stream());
+  return stats;
+}
+
+torch::Tensor ce_bwd(torch::Tensor logits, torch::Tensor targets, torch::Tensor lse, torch::Tensor gscale,
+                     int64_t vocab_start, int64_t vocab_valid, torch::Tensor out) {
+  check_rowmajor(logits, "logits");
+  TORCH_CHECK(logits.is_contiguous() && out.is_contiguous() && out.sizes() == logits.sizes() &&
+                  out.scalar_type() == logits.scalar_type(),
+              "ce_bwd: out must match logits");
+  const int64_t M = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(V % (dcode(logits) == 1 ? 8 : 4) == 0, "ce_bwd: V_local must be a multiple of the vector width");
+  TORCH_CHECK(lse.scalar_type() == torch::kFloat32 && lse.numel() == M && gscale.scalar_type() == torch::kFloat32 &&
+                  gscale.numel() == M && lse.is_contiguous() && gscale.is_contiguous(),
+              "ce_bwd: lse/gscale fp32 [M]");
+  const at::DeviceGuard g(logits.device());
+  if (M) dpfs_ce_bwd(dcode(logits), logits.data_ptr(), targets.data_ptr<int64_t>(), lse.data_ptr<float>(),
+                     gscale.data_ptr<float>(), out.data_ptr(), (int)M, (int)V, vocab_start, (int)vocab_valid, stream());
+  return out;
+}
+
+// --------------------------------------------------------------------------------- Adam --
+// Builds the device descriptor table for a fixed list of tensors (done once).
+std::vector<torch::Tensor> adam_build(std::vector<torch::Tensor> params, std::vector<torch::Tensor> grads,
+                                      std::vector<torch::Tensor> m, std::vector<torch::Tensor> v,
+                                      std::vector<c10::optional<torch::Tensor>> shadows) {
+  const size_t n = params.size();
+  TORCH_CHECK(grads.size() == n && m.size() == n && v.size() == n && shadows.size() == n, "adam_build: list sizes");
+  const int db = dpfs_adam_desc_bytes();
+  TORCH_CHECK(db == 48, "unexpected AdamTensor layout");
+  std::vector<int64_t> desc(n * 6);
+  std::vector<int32_t> chunks;
+  const int64_t C = dpfs_adam_chunk();
+  for (size_t i = 0; i < n; ++i) {
+    auto chk = [&](const torch::Tensor& t, const char* nm) {
+      TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kFloat32 && t.is_contiguous() &&
+                      t.numel() == params[i].numel(),
+                  "adam_build: ", nm, " must be contiguous fp32 matching the param");
+    };
+    chk(params[i], "param");
+    chk(grads[i], "grad");
+    chk(m[i], "exp_avg");
+    chk(v[i], "exp_avg_sq");
+    int64_t sh = 0;
+    if (shadows[i].has_value() && shadows[i]->defined()) {
+      TORCH_CHECK(shadows[i]->scalar_type() == torch::kBFloat16 && shadows[i]->is_contiguous() &&
+                      shadows[i]->numel() == params[i].numel(),
+                  "adam_build: shadow must be contiguous bf16");
+      sh = (int64_t)shadows[i]->data_ptr();
+    }
+    desc[i * 6 + 0] = (int64_t)params[i].data_ptr();
+    desc[i * 6 + 1] = (int64_t)grads[i].data_ptr();
+    desc[i * 6 + 2] = (int64_t)m[i].data_ptr();
+    desc[i * 6 + 3] = (int64_t)v[i].data_ptr();
+    desc[i * 6 + 4] = sh;
+    desc[i * 6 + 5] = params[i].numel();
+    const int64_t nc = (params[i].numel() + C - 1) / C;
+    for (int64_t c = 0; c < nc; ++c) {
+      chunks.push_back((int32_t)i);
+      chunks.push_back((int32_t)c);
+    }
+  }
+  auto dev = params.empty() ? torch::Device(torch::kCUDA) : params[0].device();
+  auto d = torch::from_blob(desc.data(), {(int64_t)desc.size()}, torch::kInt64).to(dev);
+  auto c = torch::from_blob(chunks.data(), {(int64_t)chunks.size()}, torch::kInt32).to(dev);
+  return {d, c};
+}
+
+void adam_step(torch::Tensor desc, torch::Tensor chunks, double lr, double b1, double b2, double eps, double wd,
+               int64_t step, double gscale, c10::optional<torch::Tensor> dscale) {
+  TORCH_CHECK(desc.is_cuda() && chunks.is_cuda(), "adam_step: tables must be on the device");
+  const double bc1 = 1.0 - std::pow(b1, (double)step);
+  const double bc2 = 1.0 - std::pow(b2, (double)step);
+  const float* ds = nullptr;
+  if (dscale.has_value() && dscale->defined()) {
+    TORCH_CHECK(dscale->scalar_type() == torch::kFloat32 && dscale->numel() == 1, "adam_step: dscale fp32 scalar");
+    ds = dscale->data_ptr<float>();
+  }
+  const at::DeviceGuard g(desc.device());
+  dpfs_adam_step(desc.data_ptr(), chunks.data_ptr<int32_t>(), (int)(chunks.numel() / 2), (float)lr, (float)b1,
+                 (float)b2, (float)eps, (float)wd, (float)bc1, (float)std::sqrt(bc2), (float)gscale, ds, stream());
+}
+
+torch::Tensor grad_sumsq(torch::Tensor desc, torch::Tensor chunks) {
+  const at::DeviceGuard g(desc.device());
+  const int n = (int)(chunks.numel() / 2);
+  auto partial = torch::empty({n}, desc.options().dtype(torch::kFloat32));
+  dpfs_grad_sumsq(desc.data_ptr(), chunks.data_ptr<int32_t>(), n, partial.data_ptr<float>(), stream());
+  return partial.sum();
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950 (MI355X) HIP kernels of distributed_pytorch_from_scratch_amd";
+  m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("bias") = py::none());
+  m.def("gemm_nn", &gemm_nn);
+  m.def("gemm_tn", &gemm_tn, py::arg("a"), py::arg("b"), py::arg("out") = py::none(), py::arg("accumulate") = false);
+  m.def("bias_grad", &bias_grad);
+  m.def("add_bias_", &add_bias_);
+  m.def("bias_residual", &bias_residual);
+  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("rope_", &rope_, py::arg("qkv"), py::arg("positions"), py::arg("table"), py::arg("n_rot_heads"),
+        py::arg("head_dim"), py::arg("inverse") = false);
+  m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("scale"), py::arg("causal") = true);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("embedding_fwd", &embedding_fwd);
+  m.def("embedding_bwd", &embedding_bwd);
+  m.def("ce_fwd_stats", &ce_fwd_stats);
+  m.def("ce_bwd", &ce_bwd);
+  m.def("adam_build", &adam_build);
+  m.def("adam_step", &adam_step, py::arg("desc"), py::arg("chunks"), py::arg("lr"), py::arg("beta1"),
+        py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"), py::arg("step"), py::arg("grad_scale") = 1.0,
+        py::arg("dscale") = py::none());
+  m.def("grad_sumsq", &grad_sumsq);
+}

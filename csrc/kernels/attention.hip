@@ -1,0 +1,601 @@
+// Causal flash attention (forward + backward) for gfx950, bf16 in / fp32 accumulate.
+//
+// Replaces the reference's materialised attention (models/model.py:73-77: QK^T, a
+// (B,1,T,T) triu mask built every layer and step, masked_fill, softmax, P.V and their
+// autograd backward) with O(T)-memory kernels; the log-sum-exp per query
+// row is the only saved statistic.
+//
+// Layout: q/k/v/do are (B, T, H, hd) views with token stride `ld` (the packed QKV GEMM
+// output: ld = 3*H*hd), o/dq/dk/dv likewise with their own strides; lse/delta are (B, H, T).
+//
+// MFMA orientation (v_mfma_f32_16x16x32_bf16; C/D map col = lane&15, row = 4*(lane>>4)+j):
+//  * forward and dQ compute the TRANSPOSED score tile S^T = K Q^T, so each lane owns one
+//    query column: the row max / row sum / rescale of the online softmax are lane-local
+//    (plus one xor-16/32 butterfly), and P^T in registers is directly the B operand of
+//    O^T = V^T P^T (k-slot permutation shared with the V^T operand, which is fetched with
+//    the CDNA4 transpose read ds_read_b64_tr_b16) — P never touches LDS.
+//  * dK/dV compute S = Q K^T with the block's keys held in registers; P^T/dS^T are then
+//    the A operands of dV = P^T dO and dK = dS^T Q without data movement.
+//  * backward = preprocess (delta = rowsum(dO*O)) + a dK/dV kernel (one block per 64 keys)
+//    + a dQ kernel (one block per 128 queries): no float atomics, bitwise deterministic.
+//  * every LDS tile [rows][hd] uses one XOR swizzle that is conflict-free both for row
+//    reads (ds_read_b128) and for transposed reads (ds_read_b64_tr_b16).
+//  * causal: key tiles above the diagonal are never visited; heaviest q-blocks launch first.
+#include "common.h"
+
+namespace dpfs {
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+// Swizzled byte offset of 16-byte chunk `ch` of row `r` in a [rows][HD] bf16 tile.
+template <int HD>
+__device__ __forceinline__ int sw_off(int r, int ch) {
+  constexpr int RB = HD * 2;
+  int f;
+  if (HD == 32) f = ((r >> 2) & 1) << 1;
+  else if (HD == 64) f = ((r >> 1) & 3) << 1;
+  else f = (r & 7) << 1;
+  return r * RB + ((ch ^ f) << 4);
+}
+
+// Row read: lane holds X[rb + (l&15)][kb + 8(l>>4) + j]  (16x16x32 A/B operand, K-contiguous).
+template <int HD>
+__device__ __forceinline__ bf16x8 row_frag(const char* lds, int rb, int kb) {
+  const int l = lane_id();
+  return *reinterpret_cast<const bf16x8*>(lds + sw_off<HD>(rb + (l & 15), (kb >> 3) + (l >> 4)));
+}
+
+// Transposed read with the permuted k-slots used for P^T / dS^T operands:
+// lane l (g = l>>4) gets X[r0 + 4g + j][c0 + (l&15)] for j<4 and X[r0 + 16 + 4g + j-4][...] for j>=4.
+template <int HD>
+__device__ __forceinline__ bf16x8 tr_frag(const char* lds, int r0, int c0) {
+  const int l = lane_id();
+  const int i = l & 15, q = i >> 2, p = i & 3, g = l >> 4;
+  const int col = c0 + 4 * p;
+  const int ch = col >> 3;
+  const int r_lo = r0 + 4 * g + q;
+  const int r_hi = r_lo + 16;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(lds + sw_off<HD>(r_lo, ch) + (p & 1) * 8));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(lds + sw_off<HD>(r_hi, ch) + (p & 1) * 8));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Pack two 16x16 C tiles (rows 4g+j of tile a, of tile b) into the permuted 8-slot operand.
+__device__ __forceinline__ bf16x8 pack_pt(const f32x4& a, const f32x4& b) {
+  bf16x8 r;
+  r[0] = (bf16)a[0]; r[1] = (bf16)a[1]; r[2] = (bf16)a[2]; r[3] = (bf16)a[3];
+  r[4] = (bf16)b[0]; r[5] = (bf16)b[1]; r[6] = (bf16)b[2]; r[7] = (bf16)b[3];
+  return r;
+}
+
+#define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
+
+// Global -> registers -> swizzled LDS tile of R rows x HD (rows >= nvalid are zero).
+template <int HD, int R>
+struct Stage {
+  static constexpr int CPR = HD / 8;            // chunks per row
+  static constexpr int NC = R * CPR / 256;      // chunks per thread
+  static_assert(NC >= 1, "tile too small");
+  u32x4 reg[NC];
+  __device__ __forceinline__ void load(const bf16* base, long long ld, int nvalid) {
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int r = c / CPR, ch = c % CPR;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (r < nvalid) v = *reinterpret_cast<const u32x4*>(base + r * ld + ch * 8);
+      reg[i] = v;
+    }
+  }
+  __device__ __forceinline__ void store(char* lds) const {
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      *reinterpret_cast<u32x4*>(lds + sw_off<HD>(c / CPR, c % CPR)) = reg[i];
+    }
+  }
+};
+
+// =============================================================================== forward ==
+// Block: 4 waves x 32 queries = 128 queries of one (b, h); K/V tiles of 64 keys, double
+// buffered in LDS.
+template <int HD>
+__global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
+                                                     const bf16* __restrict__ V, bf16* __restrict__ O,
+                                                     float* __restrict__ LSE, int T, int H, long long ldq,
+                                                     long long ldk, long long ldv, long long ldo, float scale,
+                                                     int causal) {
+  constexpr int BQ = 128, BKV = 64, KT = HD / 32, DT = HD / 16;
+  constexpr int TILE = BKV * HD * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
+  const int nqb = (T + BQ - 1) / BQ;
+  const int qb = nqb - 1 - blockIdx.x;  // heaviest first
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int q0 = qb * BQ;
+  const int wave = threadIdx.x >> 6, l = lane_id(), g = l >> 4;
+  const int wq0 = q0 + wave * 32;
+  const float c2 = scale * kLog2e;
+
+  const bf16* qbase = Q + (long long)b * T * ldq + (long long)h * HD;
+  const bf16* kbase = K + (long long)b * T * ldk + (long long)h * HD;
+  const bf16* vbase = V + (long long)b * T * ldv + (long long)h * HD;
+
+  // Q^T operand in registers: lane holds Q[wq0 + 16c + (l&15)][32kk + 8g + j].
+  bf16x8 qf[2][KT];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int qi = wq0 + 16 * c + (l & 15);
+#pragma unroll
+    for (int kk = 0; kk < KT; ++kk) {
+      bf16x8 v = {};
+      if (qi < T) v = *reinterpret_cast<const bf16x8*>(qbase + (long long)qi * ldq + 32 * kk + 8 * g);
+      qf[c][kk] = v;
+    }
+  }
+
+  f32x4 o[2][DT];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int d = 0; d < DT; ++d) o[c][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m[2] = {-INFINITY, -INFINITY}, lsum[2] = {0.f, 0.f};
+
+  const int kv_end = causal ? min(T, q0 + BQ) : T;
+  const int nkv = (kv_end + BKV - 1) / BKV;
+  Stage<HD, BKV> sk, sv;
+  sk.load(kbase, ldk, min(BKV, T));
+  sv.load(vbase, ldv, min(BKV, T));
+  sk.store(smem);
+  sv.store(smem + TILE);
+  __syncthreads();
+
+  for (int t = 0; t < nkv; ++t) {
+    const int cur = t & 1;
+    const char* lk = smem + cur * 2 * TILE;
+    const char* lv = lk + TILE;
+    const int kv0 = t * BKV;
+    const bool more = t + 1 < nkv;
+    if (more) {
+      const int n0 = kv0 + BKV;
+      sk.load(kbase + (long long)n0 * ldk, ldk, min(BKV, T - n0));
+      sv.load(vbase + (long long)n0 * ldv, ldv, min(BKV, T - n0));
+    }
+    const bool wave_active = !causal || kv0 <= wq0 + 31;
+    if (wave_active) {
+      // S^T tiles: s[i][c] = K[kv0+16i..][:] . Q[16c..][:]^T
+      f32x4 s[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        s[i][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        s[i][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < KT; ++kk) {
+          const bf16x8 kf = row_frag<HD>(lk, 16 * i, 32 * kk);
+          s[i][0] = MFMA(kf, qf[0][kk], s[i][0]);
+          s[i][1] = MFMA(kf, qf[1][kk], s[i][1]);
+        }
+      }
+      // Online softmax per query column (lane-local + butterfly over the 4 lane groups).
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int qi = wq0 + 16 * c + (l & 15);
+        float mx = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int ki = kv0 + 16 * i + 4 * g + j;
+            float v = s[i][c][j] * c2;
+            if (ki >= T || (causal && ki > qi)) v = -INFINITY;
+            s[i][c][j] = v;
+            mx = fmaxf(mx, v);
+          }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mnew = fmaxf(m[c], mx);
+        const float alpha = (mnew == -INFINITY) ? 1.f : exp2f(m[c] - mnew);
+        m[c] = mnew;
+        float ps = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float p = (mnew == -INFINITY) ? 0.f : exp2f(s[i][c][j] - mnew);
+            s[i][c][j] = p;
+            ps += p;
+          }
+        lsum[c] = lsum[c] * alpha + ps;
+#pragma unroll
+        for (int d = 0; d < DT; ++d) o[c][d] *= alpha;
+      }
+      // O^T[d][q] += V^T[d][k] P^T[k][q]
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 p0 = pack_pt(s[2 * ks][0], s[2 * ks + 1][0]);
+        const bf16x8 p1 = pack_pt(s[2 * ks][1], s[2 * ks + 1][1]);
+#pragma unroll
+        for (int d = 0; d < DT; ++d) {
+          const bf16x8 vf = tr_frag<HD>(lv, 32 * ks, 16 * d);
+          o[0][d] = MFMA(vf, p0, o[0][d]);
+          o[1][d] = MFMA(vf, p1, o[1][d]);
+        }
+      }
+    }
+    if (more) {
+      char* nk = smem + (cur ^ 1) * 2 * TILE;
+      sk.store(nk);
+      sv.store(nk + TILE);
+    }
+    __syncthreads();
+  }
+
+  // Epilogue: O[q][d] = O^T[d][q] / l ; lse = (m + log2 l) * ln2.
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    float ls = lsum[c];
+    ls += __shfl_xor(ls, 16, 64);
+    ls += __shfl_xor(ls, 32, 64);
+    const int qi = wq0 + 16 * c + (l & 15);
+    if (qi < T) {
+      const float inv = 1.f / ls;
+      bf16* orow = O + ((long long)b * T + qi) * ldo + (long long)h * HD;
+#pragma unroll
+      for (int d = 0; d < DT; ++d) {
+        bf16x4 v = {(bf16)(o[c][d][0] * inv), (bf16)(o[c][d][1] * inv), (bf16)(o[c][d][2] * inv),
+                    (bf16)(o[c][d][3] * inv)};
+        *reinterpret_cast<bf16x4*>(orow + 16 * d + 4 * g) = v;
+      }
+      if (g == 0) LSE[((long long)b * H + h) * T + qi] = (m[c] + __log2f(ls)) * kLn2;
+    }
+  }
+}
+
+// ========================================================================== bwd: delta ==
+// delta[b,h,t] = sum_d dO[b,t,h,d] * O[b,t,h,d]   (one wave per (b,t,h) row)
+template <int HD>
+__global__ __launch_bounds__(256) void attn_bwd_delta_k(const bf16* __restrict__ dO, const bf16* __restrict__ O,
+                                                        float* __restrict__ delta, int B, int T, int H,
+                                                        long long lddo, long long ldo) {
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (long long)B * T * H) return;
+  const int h = (int)(row % H);
+  const long long bt = row / H;
+  const int l = lane_id();
+  float s = 0.f;
+  for (int d = l; d < HD; d += 64)
+    s += to_f(dO[bt * lddo + (long long)h * HD + d]) * to_f(O[bt * ldo + (long long)h * HD + d]);
+  s = wave_sum(s);
+  if (l == 0) {
+    const long long b = bt / T, t = bt % T;
+    delta[(b * H + h) * T + t] = s;
+  }
+}
+
+// ========================================================================= bwd: dK, dV ==
+// Block: 4 waves x 16 keys = 64 keys of one (b,h); query tiles of 64 (Q and dO staged in
+// LDS, double buffered; lse/delta staged alongside).
+template <int HD>
+__global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
+                                                          const bf16* __restrict__ V, const bf16* __restrict__ dO,
+                                                          const float* __restrict__ LSE,
+                                                          const float* __restrict__ DELTA, bf16* __restrict__ dK,
+                                                          bf16* __restrict__ dV, int T, int H, long long ldq,
+                                                          long long ldk, long long ldv, long long lddo,
+                                                          long long lddk, long long lddv, float scale, int causal) {
+  constexpr int BKV = 64, BQ = 64, KT = HD / 32, DT = HD / 16;
+  constexpr int TILE = BQ * HD * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (2 * TILE + 2 * BQ * 4)];
+  constexpr int BUF = 2 * TILE + 2 * BQ * 4;
+  const int nkb = (T + BKV - 1) / BKV;
+  const int kb = blockIdx.x;  // light-to-heavy is fine: causal work per block = T - k0
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int k0 = kb * BKV;
+  const int wave = threadIdx.x >> 6, l = lane_id(), g = l >> 4;
+  const int wk0 = k0 + wave * 16;  // this wave's 16 keys
+  const float c2 = scale * kLog2e;
+  (void)nkb;
+
+  const bf16* qbase = Q + (long long)b * T * ldq + (long long)h * HD;
+  const bf16* dobase = dO + (long long)b * T * lddo + (long long)h * HD;
+  const float* lse_b = LSE + ((long long)b * H + h) * T;
+  const float* del_b = DELTA + ((long long)b * H + h) * T;
+
+  // K^T and V^T B-operands in registers: lane holds K[wk0 + (l&15)][32kk + 8g + j].
+  bf16x8 kf[KT], vf[KT];
+  {
+    const int ki = wk0 + (l & 15);
+#pragma unroll
+    for (int kk = 0; kk < KT; ++kk) {
+      bf16x8 a = {}, c = {};
+      if (ki < T) {
+        a = *reinterpret_cast<const bf16x8*>(K + ((long long)b * T + ki) * ldk + (long long)h * HD + 32 * kk + 8 * g);
+        c = *reinterpret_cast<const bf16x8*>(V + ((long long)b * T + ki) * ldv + (long long)h * HD + 32 * kk + 8 * g);
+      }
+      kf[kk] = a;
+      vf[kk] = c;
+    }
+  }
+  f32x4 dk[DT], dv[DT];
+#pragma unroll
+  for (int d = 0; d < DT; ++d) {
+    dk[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    dv[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+
+  const int qstart = causal ? (k0 / BQ) * BQ : 0;
+  const int nq = (T - qstart + BQ - 1) / BQ;
+  Stage<HD, BQ> sq, sdo;
+  auto stage_stats = [&](char* buf, int qq0) {
+    float* ls = reinterpret_cast<float*>(buf + 2 * TILE);
+    float* ds = ls + BQ;
+    if (threadIdx.x < BQ) {
+      const int qi = qq0 + threadIdx.x;
+      ls[threadIdx.x] = qi < T ? lse_b[qi] * kLog2e : 0.f;
+      ds[threadIdx.x] = qi < T ? del_b[qi] : 0.f;
+    }
+  };
+  if (nq > 0) {
+    sq.load(qbase + (long long)qstart * ldq, ldq, min(BQ, T - qstart));
+    sdo.load(dobase + (long long)qstart * lddo, lddo, min(BQ, T - qstart));
+    sq.store(smem);
+    sdo.store(smem + TILE);
+    stage_stats(smem, qstart);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < nq; ++t) {
+    const int cur = t & 1;
+    const char* lq = smem + cur * BUF;
+    const char* ldo_ = lq + TILE;
+    const float* ls = reinterpret_cast<const float*>(lq + 2 * TILE);
+    const float* ds = ls + BQ;
+    const int qq0 = qstart + t * BQ;
+    const bool more = t + 1 < nq;
+    if (more) {
+      const int n0 = qq0 + BQ;
+      sq.load(qbase + (long long)n0 * ldq, ldq, min(BQ, T - n0));
+      sdo.load(dobase + (long long)n0 * lddo, lddo, min(BQ, T - n0));
+    }
+    const bool wave_active = !causal || (qq0 + BQ - 1 >= wk0);
+    if (wave_active) {
+      // S[q][k] and dP[q][k] for 4 query tiles of 16.
+      f32x4 s[4], dp[4];
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt) {
+        s[qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        dp[qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < KT; ++kk) {
+          s[qt] = MFMA(row_frag<HD>(lq, 16 * qt, 32 * kk), kf[kk], s[qt]);
+          dp[qt] = MFMA(row_frag<HD>(ldo_, 16 * qt, 32 * kk), vf[kk], dp[qt]);
+        }
+      }
+      const int ki = wk0 + (l & 15);
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int qr = 16 * qt + 4 * g + j;
+          const int qi = qq0 + qr;
+          float p = exp2f(s[qt][j] * c2 - ls[qr]);
+          if (qi >= T || ki >= T || (causal && ki > qi)) p = 0.f;
+          s[qt][j] = p;
+          dp[qt][j] = p * (dp[qt][j] - ds[qr]);
+        }
+      }
+      // dV[k][d] += P^T dO ;  dK[k][d] += dS^T Q
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 pa = pack_pt(s[2 * ks], s[2 * ks + 1]);
+        const bf16x8 da = pack_pt(dp[2 * ks], dp[2 * ks + 1]);
+#pragma unroll
+        for (int d = 0; d < DT; ++d) {
+          dv[d] = MFMA(pa, tr_frag<HD>(ldo_, 32 * ks, 16 * d), dv[d]);
+          dk[d] = MFMA(da, tr_frag<HD>(lq, 32 * ks, 16 * d), dk[d]);
+        }
+      }
+    }
+    if (more) {
+      char* nb = smem + (cur ^ 1) * BUF;
+      sq.store(nb);
+      sdo.store(nb + TILE);
+      stage_stats(nb, qq0 + BQ);
+    }
+    __syncthreads();
+  }
+  // Write dK (scaled), dV: C layout col = d (l&15), rows = keys 4g + j.
+#pragma unroll
+  for (int d = 0; d < DT; ++d) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ki = wk0 + 4 * g + j;
+      if (ki < T) {
+        const long long col = (long long)h * HD + 16 * d + (l & 15);
+        dK[((long long)b * T + ki) * lddk + col] = (bf16)(dk[d][j] * scale);
+        dV[((long long)b * T + ki) * lddv + col] = (bf16)dv[d][j];
+      }
+    }
+  }
+}
+
+// ============================================================================ bwd: dQ ==
+// Block: 4 waves x 32 queries = 128 queries; K/V tiles of 64 keys staged in LDS.
+template <int HD>
+__global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
+                                                        const bf16* __restrict__ V, const bf16* __restrict__ dO,
+                                                        const float* __restrict__ LSE,
+                                                        const float* __restrict__ DELTA, bf16* __restrict__ dQ, int T,
+                                                        int H, long long ldq, long long ldk, long long ldv,
+                                                        long long lddo, long long lddq, float scale, int causal) {
+  constexpr int BQ = 128, BKV = 64, KT = HD / 32, DT = HD / 16;
+  constexpr int TILE = BKV * HD * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
+  const int nqb = (T + BQ - 1) / BQ;
+  const int qb = nqb - 1 - blockIdx.x;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int q0 = qb * BQ;
+  const int wave = threadIdx.x >> 6, l = lane_id(), g = l >> 4;
+  const int wq0 = q0 + wave * 32;
+  const float c2 = scale * kLog2e;
+
+  const bf16* kbase = K + (long long)b * T * ldk + (long long)h * HD;
+  const bf16* vbase = V + (long long)b * T * ldv + (long long)h * HD;
+
+  bf16x8 qf[2][KT], dof[2][KT];
+  float lse2[2], del[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int qi = wq0 + 16 * c + (l & 15);
+#pragma unroll
+    for (int kk = 0; kk < KT; ++kk) {
+      bf16x8 a = {}, d = {};
+      if (qi < T) {
+        a = *reinterpret_cast<const bf16x8*>(Q + ((long long)b * T + qi) * ldq + (long long)h * HD + 32 * kk + 8 * g);
+        d = *reinterpret_cast<const bf16x8*>(dO + ((long long)b * T + qi) * lddo + (long long)h * HD + 32 * kk + 8 * g);
+      }
+      qf[c][kk] = a;
+      dof[c][kk] = d;
+    }
+    lse2[c] = qi < T ? LSE[((long long)b * H + h) * T + qi] * kLog2e : 0.f;
+    del[c] = qi < T ? DELTA[((long long)b * H + h) * T + qi] : 0.f;
+  }
+  f32x4 dq[2][DT];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int d = 0; d < DT; ++d) dq[c][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int kv_end = causal ? min(T, q0 + BQ) : T;
+  const int nkv = (kv_end + BKV - 1) / BKV;
+  Stage<HD, BKV> sk, sv;
+  sk.load(kbase, ldk, min(BKV, T));
+  sv.load(vbase, ldv, min(BKV, T));
+  sk.store(smem);
+  sv.store(smem + TILE);
+  __syncthreads();
+
+  for (int t = 0; t < nkv; ++t) {
+    const int cur = t & 1;
+    const char* lk = smem + cur * 2 * TILE;
+    const char* lv = lk + TILE;
+    const int kv0 = t * BKV;
+    const bool more = t + 1 < nkv;
+    if (more) {
+      const int n0 = kv0 + BKV;
+      sk.load(kbase + (long long)n0 * ldk, ldk, min(BKV, T - n0));
+      sv.load(vbase + (long long)n0 * ldv, ldv, min(BKV, T - n0));
+    }
+    const bool wave_active = !causal || kv0 <= wq0 + 31;
+    if (wave_active) {
+      f32x4 s[4][2], dp[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          s[i][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
+          dp[i][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int kk = 0; kk < KT; ++kk) {
+          const bf16x8 kr = row_frag<HD>(lk, 16 * i, 32 * kk);
+          const bf16x8 vr = row_frag<HD>(lv, 16 * i, 32 * kk);
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            s[i][c] = MFMA(kr, qf[c][kk], s[i][c]);
+            dp[i][c] = MFMA(vr, dof[c][kk], dp[i][c]);
+          }
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int qi = wq0 + 16 * c + (l & 15);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int ki = kv0 + 16 * i + 4 * g + j;
+            float p = exp2f(s[i][c][j] * c2 - lse2[c]);
+            if (ki >= T || qi >= T || (causal && ki > qi)) p = 0.f;
+            s[i][c][j] = p * (dp[i][c][j] - del[c]);  // dS^T
+          }
+      }
+      // dQ^T[d][q] += K^T[d][k] dS^T[k][q]
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 d0 = pack_pt(s[2 * ks][0], s[2 * ks + 1][0]);
+        const bf16x8 d1 = pack_pt(s[2 * ks][1], s[2 * ks + 1][1]);
+#pragma unroll
+        for (int d = 0; d < DT; ++d) {
+          const bf16x8 kt = tr_frag<HD>(lk, 32 * ks, 16 * d);
+          dq[0][d] = MFMA(kt, d0, dq[0][d]);
+          dq[1][d] = MFMA(kt, d1, dq[1][d]);
+        }
+      }
+    }
+    if (more) {
+      char* nk = smem + (cur ^ 1) * 2 * TILE;
+      sk.store(nk);
+      sv.store(nk + TILE);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int qi = wq0 + 16 * c + (l & 15);
+    if (qi < T) {
+      bf16* row = dQ + ((long long)b * T + qi) * lddq + (long long)h * HD;
+#pragma unroll
+      for (int d = 0; d < DT; ++d) {
+        bf16x4 v = {(bf16)(dq[c][d][0] * scale), (bf16)(dq[c][d][1] * scale), (bf16)(dq[c][d][2] * scale),
+                    (bf16)(dq[c][d][3] * scale)};
+        *reinterpret_cast<bf16x4*>(row + 16 * d + 4 * g) = v;
+      }
+    }
+  }
+}
+
+}  // namespace dpfs
+
+using namespace dpfs;
+
+#define DPFS_HD_DISPATCH(HDV, ...)                           \
+  do {                                                       \
+    if ((HDV) == 64) { constexpr int HD_ = 64; __VA_ARGS__; } \
+    else if ((HDV) == 128) { constexpr int HD_ = 128; __VA_ARGS__; } \
+    else if ((HDV) == 32) { constexpr int HD_ = 32; __VA_ARGS__; } \
+  } while (0)
+
+extern "C" int dpfs_attn_supported_hd(int hd) { return hd == 32 || hd == 64 || hd == 128; }
+
+extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int T, int H,
+                              int hd, long long ldq, long long ldk, long long ldv, long long ldo, float scale,
+                              int causal, hipStream_t s) {
+  dim3 grid((T + 127) / 128, B * H);
+  DPFS_HD_DISPATCH(hd, attn_fwd_k<HD_><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o,
+                                                            lse, T, H, ldq, ldk, ldv, ldo, scale, causal));
+}
+
+// delta: workspace [B, H, T] fp32.
+extern "C" void dpfs_attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o,
+                              const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int T, int H,
+                              int hd, long long lddo, long long ldq, long long ldk, long long ldv, long long ldo,
+                              long long lddq, long long lddk, long long lddv, float scale, int causal,
+                              hipStream_t s) {
+  const long long rows = (long long)B * T * H;
+  DPFS_HD_DISPATCH(hd, attn_bwd_delta_k<HD_><<<(unsigned)((rows + 3) / 4), 256, 0, s>>>(
+                           (const bf16*)dout, (const bf16*)o, delta, B, T, H, lddo, ldo));
+  dim3 gk((T + 63) / 64, B * H);
+  DPFS_HD_DISPATCH(hd, attn_bwd_dkdv_k<HD_><<<gk, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
+                                                               (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv, T,
+                                                               H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal));
+  dim3 gq((T + 127) / 128, B * H);
+  DPFS_HD_DISPATCH(hd, attn_bwd_dq_k<HD_><<<gq, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
+                                                             (const bf16*)dout, lse, delta, (bf16*)dq, T, H, ldq, ldk,
+                                                             ldv, lddo, lddq, scale, causal));
+}

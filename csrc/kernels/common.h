@@ -1,0 +1,87 @@
+// Shared device helpers for the gfx950 (MI355X, CDNA4) kernels.
+//
+// Conventions used by every kernel in this directory:
+//  * wave64: every reduction is a 64-lane butterfly (__shfl_xor over 64 lanes);
+//  * 16-byte vector memory access per lane (8 x bf16 or 4 x fp32), Guideline 13 of the
+//    CDNA HIP guide: scalar bf16 loads cost 2-2.5x;
+//  * fp32 math / accumulation, bf16 storage; bf16 rounding via the native conversion
+//    (hipcc -O3 emits v_cvt_pk_bf16_f32, which keeps NaNs NaN);
+//  * launchers are extern "C", take raw device pointers + hipStream_t and never
+//    allocate or synchronise (graph-capturable).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dpfs {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+enum DType : int { kF32 = 0, kBF16 = 1 };
+
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f(float x);
+template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+// 16-byte vector of T: 8 bf16 or 4 fp32.
+template <typename T> struct Vec;
+template <> struct Vec<bf16> {
+  static constexpr int N = 8;
+  typedef bf16x8 type;
+};
+template <> struct Vec<float> {
+  static constexpr int N = 4;
+  typedef f32x4 type;
+};
+
+template <typename T>
+__device__ __forceinline__ void load_vec(const T* p, float (&out)[Vec<T>::N]) {
+  typename Vec<T>::type v = *reinterpret_cast<const typename Vec<T>::type*>(p);
+#pragma unroll
+  for (int i = 0; i < Vec<T>::N; ++i) out[i] = to_f(v[i]);
+}
+
+template <typename T>
+__device__ __forceinline__ void store_vec(T* p, const float (&in)[Vec<T>::N]) {
+  typename Vec<T>::type v;
+#pragma unroll
+  for (int i = 0; i < Vec<T>::N; ++i) v[i] = from_f<T>(in[i]);
+  *reinterpret_cast<typename Vec<T>::type*>(p) = v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// Bijective XCD-aware remap of a linear workgroup id (MI355X: 8 XCDs, dispatch deals
+// blocks round-robin over XCDs).  Consecutive remapped ids land on the same XCD, so tiles
+// that share operand panels share an L2.  Valid for any nwg (the q/r form).
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int NX = 8;
+  int xcd = orig % NX;
+  int q = nwg / NX, r = nwg % NX;
+  int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + orig / NX;
+}
+
+}  // namespace dpfs
+
+#define DPFS_LAUNCH_CHECK() (void)hipGetLastError()

@@ -1,0 +1,176 @@
+// Vocab-sharded embedding (fwd/bwd) and vocab-parallel cross-entropy kernels for gfx950.
+//
+// Embedding forward fuses the reference's 5 kernels (two compares + logical_and, two
+// index_put_ on the *caller's* ids, F.embedding, index_put of zeros: models/layers.py:137-140)
+// and the bf16 cast (models/model.py:153-154) into one gather: one wave per token row,
+// 16-byte loads of the fp32 master row, bf16 stores; ids outside [vocab_start, vocab_start
+// + V_local) produce zeros.  The ids are never written.
+//
+// Embedding backward: scatter-add of the output-grad rows into the fp32 table shard with
+// no-return global_atomic_add_f32, shaped as the guide asks (each wave-instruction = 256
+// contiguous bytes of one row; rows spread over the table).
+//
+// Cross-entropy: per-row online max / sum-exp over the local shard in ONE pass (fp32), the
+// target logit if owned; backward writes (softmax - onehot) * g in place over the logits.
+#include "common.h"
+
+namespace dpfs {
+
+template <typename TO>
+__global__ __launch_bounds__(256) void embedding_fwd_k(const int64_t* __restrict__ ids, const float* __restrict__ w,
+                                                       TO* __restrict__ out, int M, int D, long long vstart,
+                                                       int vlocal) {
+  const int lane = threadIdx.x & 63;
+  const int nv = D / 4;
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += gridDim.x * 4) {
+    const long long loc = ids[row] - vstart;
+    const bool hit = loc >= 0 && loc < vlocal;
+    TO* o = out + (long long)row * D;
+    for (int c = lane; c < nv; c += 64) {
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (hit) v = *reinterpret_cast<const f32x4*>(w + loc * D + c * 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[c * 4 + j] = from_f<TO>(v[j]);
+    }
+  }
+}
+
+template <typename TI>
+__global__ __launch_bounds__(256) void embedding_bwd_k(const TI* __restrict__ dout, const int64_t* __restrict__ ids,
+                                                       float* __restrict__ dw, int M, int D, long long vstart,
+                                                       int vlocal) {
+  const int lane = threadIdx.x & 63;
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += gridDim.x * 4) {
+    const long long loc = ids[row] - vstart;
+    if (loc < 0 || loc >= vlocal) continue;
+    const TI* g = dout + (long long)row * D;
+    float* dst = dw + loc * D;
+    for (int c = lane; c < D; c += 64) atomicAdd(dst + c, to_f(g[c]));
+  }
+}
+
+// ------------------------------------------------------------------- cross entropy ----
+struct MaxSum {
+  float m, s;
+};
+__device__ __forceinline__ MaxSum merge(MaxSum a, MaxSum b) {
+  const float m = fmaxf(a.m, b.m);
+  if (m == -INFINITY) return {m, 0.f};
+  return {m, a.s * __expf(a.m - m) + b.s * __expf(b.m - m)};
+}
+
+// One 256-thread block per row.  stats[row] = {max, sum exp(x - max), target logit or 0}.
+template <typename T>
+__global__ __launch_bounds__(256) void ce_stats_k(const T* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                  float* __restrict__ stats, int V, long long vstart, int vvalid) {
+  constexpr int N = Vec<T>::N;
+  __shared__ MaxSum red[4];
+  const int row = blockIdx.x;
+  const T* x = logits + (long long)row * V;
+  MaxSum acc = {-INFINITY, 0.f};
+  const int nvec = vvalid / N;  // full vectors inside the valid range
+  for (int c = threadIdx.x; c < nvec; c += blockDim.x) {
+    float v[N];
+    load_vec<T>(x + c * N, v);
+    float m = v[0];
+#pragma unroll
+    for (int j = 1; j < N; ++j) m = fmaxf(m, v[j]);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) s += __expf(v[j] - m);
+    acc = merge(acc, {m, s});
+  }
+  for (int c = nvec * N + threadIdx.x; c < vvalid; c += blockDim.x) acc = merge(acc, {to_f(x[c]), 1.f});
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    MaxSum other = {__shfl_xor(acc.m, o, 64), __shfl_xor(acc.s, o, 64)};
+    acc = merge(acc, other);
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    MaxSum r = red[0];
+    for (int i = 1; i < 4; ++i) r = merge(r, red[i]);
+    const long long loc = tgt[row] - vstart;
+    const float tl = (loc >= 0 && loc < vvalid) ? to_f(x[loc]) : 0.f;
+    stats[row * 3 + 0] = r.m;
+    stats[row * 3 + 1] = r.s;
+    stats[row * 3 + 2] = tl;
+  }
+}
+
+// out[row, c] = (exp(x - lse[row]) - [c == target]) * g[row]; 0 for c >= vvalid.  out may
+// alias logits (in place).
+template <typename T>
+__global__ __launch_bounds__(256) void ce_bwd_k(const T* logits, const int64_t* __restrict__ tgt,
+                                                const float* __restrict__ lse, const float* __restrict__ gscale,
+                                                T* out, int M, int V, long long vstart, int vvalid) {
+  constexpr int N = Vec<T>::N;
+  const long long per_row = V / N;
+  const long long total = (long long)M * per_row;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / per_row;
+    const int c = (int)(i % per_row) * N;
+    const float l = lse[r], g = gscale[r];
+    const long long loc = tgt[r] - vstart;
+    float v[N];
+    load_vec<T>(logits + r * V + c, v);
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const int col = c + j;
+      float p = col < vvalid ? __expf(v[j] - l) : 0.f;
+      if (col == loc) p -= 1.f;
+      v[j] = p * g;
+    }
+    store_vec<T>(out + r * V + c, v);
+  }
+}
+
+static inline int cap_grid2(long long work, int block) {
+  long long g = (work + block - 1) / block;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace dpfs
+
+using namespace dpfs;
+
+extern "C" void dpfs_embedding_fwd(int out_dtype, const int64_t* ids, const float* w, void* out, int M, int D,
+                                   long long vstart, int vlocal, hipStream_t s) {
+  const int grid = cap_grid2(M, 4);
+  if (out_dtype == kBF16)
+    embedding_fwd_k<bf16><<<grid, 256, 0, s>>>(ids, w, (bf16*)out, M, D, vstart, vlocal);
+  else
+    embedding_fwd_k<float><<<grid, 256, 0, s>>>(ids, w, (float*)out, M, D, vstart, vlocal);
+}
+
+// dw must be zeroed by the caller.
+extern "C" void dpfs_embedding_bwd(int in_dtype, const void* dout, const int64_t* ids, float* dw, int M, int D,
+                                   long long vstart, int vlocal, hipStream_t s) {
+  const int grid = cap_grid2(M, 4);
+  if (in_dtype == kBF16)
+    embedding_bwd_k<bf16><<<grid, 256, 0, s>>>((const bf16*)dout, ids, dw, M, D, vstart, vlocal);
+  else
+    embedding_bwd_k<float><<<grid, 256, 0, s>>>((const float*)dout, ids, dw, M, D, vstart, vlocal);
+}
+
+extern "C" void dpfs_ce_stats(int dtype, const void* logits, const int64_t* tgt, float* stats, int M, int V,
+                              long long vstart, int vvalid, hipStream_t s) {
+  if (M == 0) return;
+  if (dtype == kBF16)
+    ce_stats_k<bf16><<<M, 256, 0, s>>>((const bf16*)logits, tgt, stats, V, vstart, vvalid);
+  else
+    ce_stats_k<float><<<M, 256, 0, s>>>((const float*)logits, tgt, stats, V, vstart, vvalid);
+}
+
+extern "C" void dpfs_ce_bwd(int dtype, const void* logits, const int64_t* tgt, const float* lse, const float* gscale,
+                            void* out, int M, int V, long long vstart, int vvalid, hipStream_t s) {
+  const int vec = dtype == kBF16 ? 8 : 4;
+  const int grid = cap_grid2((long long)M * V / vec, 256);
+  if (dtype == kBF16)
+    ce_bwd_k<bf16><<<grid, 256, 0, s>>>((const bf16*)logits, tgt, lse, gscale, (bf16*)out, M, V, vstart, vvalid);
+  else
+    ce_bwd_k<float><<<grid, 256, 0, s>>>((const float*)logits, tgt, lse, gscale, (float*)out, M, V, vstart, vvalid);
+}

@@ -1,0 +1,278 @@
+// Fused RMSNorm / LayerNorm forward + backward for gfx950.
+//
+// Replaces the ~7 ATen kernels per RMSNorm of the reference (float, pow, mean, add, rsqrt,
+// mul, type_as, mul: models/layers.py:151-155) and their autograd backward with one pass
+// each way.  Layout: x[M, D] row-major, D % (16 B / sizeof(T)) == 0.
+//
+// Forward: one wave64 per row, the row held in registers (VPL x 16-byte vectors per lane),
+// fp32 statistics, 4 rows per 256-thread block.  Memory-bound: 1 read + 1 write of x.
+//
+// Backward: grid-stride waves over rows; dx per row, and the weight gradient accumulated in
+// registers per lane, reduced across the block's 4 waves in a FIXED order through LDS, then
+// across blocks by a second column-sum kernel.  No float atomics anywhere: the replicated
+// norm weights must get bitwise-identical grads on every TP rank.
+#include "common.h"
+
+namespace dpfs {
+
+constexpr int kRowsPerBlock = 4;  // 4 waves
+
+// ------------------------------------------------------------------------- RMSNorm fwd --
+template <typename T, int VPL>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_k(const T* __restrict__ x, const float* __restrict__ w,
+                                                     T* __restrict__ y, float* __restrict__ rstd,
+                                                     int M, int D, float eps) {
+  constexpr int N = Vec<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const T* xr = x + (size_t)row * D;
+  T* yr = y + (size_t)row * D;
+  const int nvec = D / N;
+  float v[VPL][N];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + i * 64;
+    if (c < nvec) {
+      load_vec<T>(xr + c * N, v[i]);
+#pragma unroll
+      for (int j = 0; j < N; ++j) ss += v[i][j] * v[i][j];
+    }
+  }
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / (float)D + eps);
+  if (lane == 0) rstd[row] = r;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + i * 64;
+    if (c < nvec) {
+      float wv[4 * ((N + 3) / 4)];
+      float o[N];
+#pragma unroll
+      for (int j = 0; j < N; j += 4) {
+        f32x4 t = *reinterpret_cast<const f32x4*>(w + c * N + j);
+        wv[j] = t[0]; wv[j + 1] = t[1]; wv[j + 2] = t[2]; wv[j + 3] = t[3];
+      }
+#pragma unroll
+      for (int j = 0; j < N; ++j) o[j] = to_f(from_f<T>(v[i][j] * r)) * wv[j];  // reference rounding
+      store_vec<T>(yr + c * N, o);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------ LayerNorm fwd --
+template <typename T, int VPL>
+__global__ __launch_bounds__(256) void layernorm_fwd_k(const T* __restrict__ x, const float* __restrict__ w,
+                                                       const float* __restrict__ b, T* __restrict__ y,
+                                                       float* __restrict__ mean_out, float* __restrict__ rstd,
+                                                       int M, int D, float eps) {
+  constexpr int N = Vec<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const T* xr = x + (size_t)row * D;
+  T* yr = y + (size_t)row * D;
+  const int nvec = D / N;
+  float v[VPL][N];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + i * 64;
+    if (c < nvec) {
+      load_vec<T>(xr + c * N, v[i]);
+#pragma unroll
+      for (int j = 0; j < N; ++j) s += v[i][j];
+    }
+  }
+  const float mu = wave_sum(s) / (float)D;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + i * 64;
+    if (c < nvec) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) { float d = v[i][j] - mu; ss += d * d; }
+    }
+  }
+  const float r = rsqrtf(wave_sum(ss) / (float)D + eps);
+  if (lane == 0) { rstd[row] = r; mean_out[row] = mu; }
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + i * 64;
+    if (c < nvec) {
+      float o[N];
+#pragma unroll
+      for (int j = 0; j < N; ++j) o[j] = (v[i][j] - mu) * r * w[c * N + j] + b[c * N + j];
+      store_vec<T>(yr + c * N, o);
+    }
+  }
+}
+
+// -------------------------------------------------------------------------- backward --
+// MODE 0 = RMSNorm, 1 = LayerNorm.  partial_w / partial_b: [gridDim.x, D] fp32.
+template <typename T, int VPL, int MODE>
+__global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, const T* __restrict__ x,
+                                                  const float* __restrict__ w, const float* __restrict__ mean_in,
+                                                  const float* __restrict__ rstd, T* __restrict__ dx,
+                                                  float* __restrict__ partial_w, float* __restrict__ partial_b,
+                                                  int M, int D) {
+  constexpr int N = Vec<T>::N;
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [2][D]
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nvec = D / N;
+  float aw[VPL][N], ab[VPL][N];
+#pragma unroll
+  for (int i = 0; i < VPL; ++i)
+#pragma unroll
+    for (int j = 0; j < N; ++j) { aw[i][j] = 0.f; ab[i][j] = 0.f; }
+
+  for (int row = blockIdx.x * kRowsPerBlock + wave; row < M; row += gridDim.x * kRowsPerBlock) {
+    const T* xr = x + (size_t)row * D;
+    const T* dyr = dy + (size_t)row * D;
+    const float r = rstd[row];
+    const float mu = MODE == 1 ? mean_in[row] : 0.f;
+    float xh[VPL][N], g[VPL][N];
+    float dot = 0.f, gs = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane + i * 64;
+      if (c < nvec) {
+        float xv[N], dv[N];
+        load_vec<T>(xr + c * N, xv);
+        load_vec<T>(dyr + c * N, dv);
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          xh[i][j] = (xv[j] - mu) * r;
+          g[i][j] = dv[j] * w[c * N + j];
+          dot += g[i][j] * xh[i][j];
+          gs += g[i][j];
+          aw[i][j] += dv[j] * xh[i][j];
+          ab[i][j] += dv[j];
+        }
+      }
+    }
+    dot = wave_sum(dot) / (float)D;
+    if (MODE == 1) gs = wave_sum(gs) / (float)D;
+    T* dxr = dx + (size_t)row * D;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane + i * 64;
+      if (c < nvec) {
+        float o[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) o[j] = r * (g[i][j] - (MODE == 1 ? gs : 0.f) - xh[i][j] * dot);
+        store_vec<T>(dxr + c * N, o);
+      }
+    }
+  }
+  // Deterministic block reduction of the weight grads: waves add in a fixed order.
+  for (int wv = 0; wv < kRowsPerBlock; ++wv) {
+    if (wave == wv) {
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) {
+        const int c = lane + i * 64;
+        if (c < nvec) {
+#pragma unroll
+          for (int j = 0; j < N; ++j) {
+            const int col = c * N + j;
+            if (wv == 0) {
+              red[col] = aw[i][j];
+              if (MODE == 1) red[D + col] = ab[i][j];
+            } else {
+              red[col] += aw[i][j];
+              if (MODE == 1) red[D + col] += ab[i][j];
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  for (int col = threadIdx.x; col < D; col += blockDim.x) {
+    partial_w[(size_t)blockIdx.x * D + col] = red[col];
+    if (MODE == 1) partial_b[(size_t)blockIdx.x * D + col] = red[D + col];
+  }
+}
+
+// out[c] = sum_g partial[g, c] in a fixed order (g ascending).
+__global__ __launch_bounds__(256) void colsum_partials_k(const float* __restrict__ partial, float* __restrict__ out,
+                                                         int G, int D) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= D) return;
+  float s = 0.f;
+  for (int g = 0; g < G; ++g) s += partial[(size_t)g * D + col];
+  out[col] = s;
+}
+
+template <typename T>
+static int vpl_for(int D) {
+  const int nvec = D / Vec<T>::N;
+  return (nvec + 63) / 64;
+}
+
+#define DPFS_VPL_DISPATCH(VPL_VALUE, ...)                                   \
+  do {                                                                      \
+    const int _v = (VPL_VALUE);                                             \
+    if (_v <= 1) { constexpr int VPL = 1; __VA_ARGS__; }                    \
+    else if (_v <= 2) { constexpr int VPL = 2; __VA_ARGS__; }               \
+    else if (_v <= 4) { constexpr int VPL = 4; __VA_ARGS__; }               \
+    else if (_v <= 8) { constexpr int VPL = 8; __VA_ARGS__; }               \
+    else if (_v <= 12) { constexpr int VPL = 12; __VA_ARGS__; }             \
+    else { constexpr int VPL = 16; __VA_ARGS__; }                           \
+  } while (0)
+
+int norm_bwd_grid(int M) {
+  int g = (M + kRowsPerBlock - 1) / kRowsPerBlock;
+  return g < 512 ? g : 512;
+}
+
+}  // namespace dpfs
+
+using namespace dpfs;
+
+extern "C" int dpfs_norm_bwd_grid(int M) { return norm_bwd_grid(M); }
+
+extern "C" void dpfs_rmsnorm_fwd(int dtype, const void* x, const float* w, void* y, float* rstd, int M, int D,
+                                 float eps, hipStream_t s) {
+  dim3 grid((M + kRowsPerBlock - 1) / kRowsPerBlock);
+  if (dtype == kBF16) {
+    DPFS_VPL_DISPATCH(vpl_for<bf16>(D), rmsnorm_fwd_k<bf16, VPL><<<grid, 256, 0, s>>>(
+        (const bf16*)x, w, (bf16*)y, rstd, M, D, eps));
+  } else {
+    DPFS_VPL_DISPATCH(vpl_for<float>(D), rmsnorm_fwd_k<float, VPL><<<grid, 256, 0, s>>>(
+        (const float*)x, w, (float*)y, rstd, M, D, eps));
+  }
+}
+
+extern "C" void dpfs_layernorm_fwd(int dtype, const void* x, const float* w, const float* b, void* y, float* mean,
+                                   float* rstd, int M, int D, float eps, hipStream_t s) {
+  dim3 grid((M + kRowsPerBlock - 1) / kRowsPerBlock);
+  if (dtype == kBF16) {
+    DPFS_VPL_DISPATCH(vpl_for<bf16>(D), layernorm_fwd_k<bf16, VPL><<<grid, 256, 0, s>>>(
+        (const bf16*)x, w, b, (bf16*)y, mean, rstd, M, D, eps));
+  } else {
+    DPFS_VPL_DISPATCH(vpl_for<float>(D), layernorm_fwd_k<float, VPL><<<grid, 256, 0, s>>>(
+        (const float*)x, w, b, (float*)y, mean, rstd, M, D, eps));
+  }
+}
+
+// mode 0 = rms, 1 = layernorm.  partial_w/partial_b: [dpfs_norm_bwd_grid(M), D] workspace.
+extern "C" void dpfs_norm_bwd(int mode, int dtype, const void* dy, const void* x, const float* w, const float* mean,
+                              const float* rstd, void* dx, float* dw, float* db, float* partial_w, float* partial_b,
+                              int M, int D, hipStream_t s) {
+  const int G = norm_bwd_grid(M);
+  const size_t lds = (size_t)(mode == 1 ? 2 : 1) * D * sizeof(float);
+#define DPFS_NB(T, MODE_)                                                                                  \
+  DPFS_VPL_DISPATCH(vpl_for<T>(D), norm_bwd_k<T, VPL, MODE_><<<G, 256, lds, s>>>(                           \
+      (const T*)dy, (const T*)x, w, mean, rstd, (T*)dx, partial_w, partial_b, M, D))
+  if (dtype == kBF16) {
+    if (mode == 0) DPFS_NB(bf16, 0); else DPFS_NB(bf16, 1);
+  } else {
+    if (mode == 0) DPFS_NB(float, 0); else DPFS_NB(float, 1);
+  }
+#undef DPFS_NB
+  colsum_partials_k<<<(D + 255) / 256, 256, 0, s>>>(partial_w, dw, G, D);
+  if (mode == 1) colsum_partials_k<<<(D + 255) / 256, 256, 0, s>>>(partial_b, db, G, D);
+}

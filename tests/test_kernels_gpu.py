@@ -1,0 +1,241 @@
+"""HIP kernel numerics vs the plain-PyTorch fp32 oracle (``ops/reference.py``), on MI355X.
+
+Every test runs the ``_C`` kernel on ``cuda`` tensors and the reference on the same inputs
+upcast to fp32; tolerances are bf16-rounding sized.  Shapes include ragged edges (M, N not
+multiples of the 128x128 GEMM tile, T not a multiple of the attention tiles).
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from distributed_pytorch_from_scratch_amd.ops import _ext, reference as R  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def C():
+    return _ext.require()
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+DEV = "cuda"
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (1000, 768, 768), (33, 200, 64), (4096, 2304, 768),
+                                   (130, 6288, 768), (512, 96, 1024)])
+def test_gemm_nt(C, M, N, K):
+    torch.manual_seed(0)
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = torch.randn(N, K, device=DEV).bfloat16()
+    bias = torch.randn(N, device=DEV)
+    out = C.gemm_nt(a, b, bias)
+    ref = R.gemm_nt(a.float(), b.float(), bias)
+    assert _rel(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (1000, 768, 2304), (33, 64, 200), (4096, 768, 288)])
+def test_gemm_nn(C, M, N, K):
+    torch.manual_seed(1)
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = torch.randn(K, N, device=DEV).bfloat16()
+    out = C.gemm_nn(a, b)
+    assert _rel(out, R.gemm_nn(a.float(), b.float())) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (2304, 768, 4096), (96, 768, 1000), (200, 64, 33)])
+def test_gemm_tn(C, M, N, K):
+    torch.manual_seed(2)
+    a = torch.randn(K, M, device=DEV).bfloat16()
+    b = torch.randn(K, N, device=DEV).bfloat16()
+    out = C.gemm_tn(a, b)
+    assert out.dtype == torch.float32
+    assert _rel(out, R.gemm_tn(a.float(), b.float())) < 1e-2
+    acc = torch.randn(M, N, device=DEV)
+    acc_ref = acc.clone() + R.gemm_tn(a.float(), b.float())
+    C.gemm_tn(a, b, acc, True)
+    assert _rel(acc, acc_ref) < 1e-2
+
+
+def test_gemm_identity_asymmetric(C):
+    # A = I with an asymmetric B catches a transposed C write (guide §3).
+    n = 128
+    eye = torch.eye(n, device=DEV).bfloat16()
+    b = torch.arange(n * n, device=DEV, dtype=torch.float32).view(n, n).remainder(251).bfloat16()
+    out = C.gemm_nt(eye, b, None)          # = b^T
+    assert torch.equal(out.float(), b.float().t())
+    out = C.gemm_nn(eye, b)                # = b
+    assert torch.equal(out.float(), b.float())
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,D", [(37, 768), (1024, 512), (5, 5120), (64, 128)])
+def test_rmsnorm(C, dt, M, D):
+    torch.manual_seed(3)
+    x = torch.randn(M, D, device=DEV).to(dt)
+    w = torch.rand(D, device=DEV) + 0.5
+    y, rstd = C.rmsnorm_fwd(x, w, 1e-5)
+    yr, rr = R.rmsnorm_fwd(x.float(), w, 1e-5)
+    assert _rel(y, yr) < 1e-2 and _rel(rstd, rr) < 1e-5
+    dy = torch.randn(M, D, device=DEV).to(dt)
+    dx, dw = C.rmsnorm_bwd(dy, x, w, rstd)
+    dxr, dwr = R.rmsnorm_bwd(dy.float(), x.float(), w, rr)
+    assert _rel(dx, dxr) < 1e-2 and _rel(dw, dwr) < 1e-3
+
+
+@pytest.mark.parametrize("M,D", [(37, 768), (300, 1280)])
+def test_layernorm(C, M, D):
+    torch.manual_seed(4)
+    x = torch.randn(M, D, device=DEV).bfloat16()
+    w, b = torch.rand(D, device=DEV) + 0.5, torch.randn(D, device=DEV)
+    y, mu, rs = C.layernorm_fwd(x, w, b, 1e-5)
+    yr, mur, rsr = R.layernorm_fwd(x.float(), w, b, 1e-5)
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn(M, D, device=DEV).bfloat16()
+    dx, dw, db = C.layernorm_bwd(dy, x, w, mu, rs)
+    dxr, dwr, dbr = R.layernorm_bwd(dy.float(), x.float(), w, mur, rsr)
+    assert _rel(dx, dxr) < 1e-2 and _rel(dw, dwr) < 1e-3 and _rel(db, dbr) < 1e-3
+
+
+def test_rmsnorm_bwd_deterministic(C):
+    x = torch.randn(4096, 768, device=DEV).bfloat16()
+    w = torch.rand(768, device=DEV)
+    y, r = C.rmsnorm_fwd(x, w, 1e-5)
+    dy = torch.randn_like(x)
+    a = C.rmsnorm_bwd(dy, x, w, r)[1]
+    b = C.rmsnorm_bwd(dy, x, w, r)[1]
+    assert torch.equal(a, b)
+
+
+def test_swiglu(C):
+    torch.manual_seed(5)
+    gu = torch.randn(333, 2 * 1024, device=DEV).bfloat16()
+    h = C.swiglu_fwd(gu)
+    assert _rel(h, R.swiglu_fwd(gu.float())) < 1e-2
+    dh = torch.randn(333, 1024, device=DEV).bfloat16()
+    assert _rel(C.swiglu_bwd(dh, gu), R.swiglu_bwd(dh.float(), gu.float())) < 1e-2
+
+
+@pytest.mark.parametrize("hd", [32, 64, 128])
+def test_rope(C, hd):
+    torch.manual_seed(6)
+    M, H = 96, 3
+    qkv = torch.randn(M, 3 * H * hd, device=DEV).bfloat16()
+    pos = torch.randint(0, 200, (M,), device=DEV)
+    tab = R.rope_table(256, hd, 10000.0).to(DEV)
+    a = qkv.clone()
+    C.rope_(a, pos, tab, 2 * H, hd, False)
+    b = qkv.float().clone()
+    R.rope_(b, pos, tab, 2 * H, hd, False)
+    assert _rel(a, b) < 1e-2
+    C.rope_(a, pos, tab, 2 * H, hd, True)  # inverse restores
+    assert _rel(a, qkv) < 1e-2
+
+
+def test_bias_grad_and_residual(C):
+    torch.manual_seed(7)
+    dy = torch.randn(1000, 768, device=DEV).bfloat16()
+    assert _rel(C.bias_grad(dy), R.bias_grad(dy.float())) < 1e-4
+    y = torch.randn(1000, 768, device=DEV).bfloat16()
+    res = torch.randn(1000, 768, device=DEV).bfloat16()
+    bias = torch.randn(768, device=DEV)
+    out = C.bias_residual(y, bias, res)
+    assert _rel(out, y.float() + bias + res.float()) < 1e-2
+    y2 = y.clone()
+    C.add_bias_(y2, bias)
+    assert _rel(y2, y.float() + bias) < 1e-2
+
+
+def test_embedding(C):
+    torch.manual_seed(8)
+    V, D, M = 1000, 768, 513
+    w = torch.randn(V, D, device=DEV)
+    ids = torch.randint(0, 3 * V, (M,), device=DEV)
+    for st in (0, V, 2 * V):
+        out = C.embedding_fwd(ids, w, st, torch.bfloat16)
+        ref = R.embedding_fwd(ids, w, st, torch.float32)
+        assert _rel(out, ref) < 1e-2
+        d = torch.randn(M, D, device=DEV).bfloat16()
+        assert _rel(C.embedding_bwd(d, ids, V, st), R.embedding_bwd(d.float(), ids, V, st)) < 1e-3
+
+
+@pytest.mark.parametrize("V,valid,start", [(6288, 6288, 0), (6288, 6241, 6288 * 7), (1024, 1000, 0)])
+def test_cross_entropy_kernels(C, V, valid, start):
+    torch.manual_seed(9)
+    M = 257
+    x = (3 * torch.randn(M, V, device=DEV)).bfloat16()
+    t = torch.randint(start, start + V, (M,), device=DEV)
+    st = C.ce_fwd_stats(x, t, start, valid)
+    sr = R.ce_fwd_stats(x.float(), t, start, valid)
+    assert _rel(st, sr) < 1e-4
+    lse, _ = R.ce_combine(sr.unsqueeze(0))
+    g = torch.rand(M, device=DEV)
+    out = torch.empty_like(x)
+    C.ce_bwd(x, t, lse, g, start, valid, out)
+    ref = torch.empty(M, V, device=DEV)
+    R.ce_bwd(x.float(), t, lse, g, start, valid, ref)
+    assert _rel(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,T,H,hd", [(2, 256, 4, 64), (1, 300, 2, 64), (2, 130, 3, 128), (1, 64, 2, 32),
+                                      (1, 1000, 2, 64)])
+def test_attention(C, B, T, H, hd):
+    torch.manual_seed(10)
+    qkv = torch.randn(B * T, 3 * H * hd, device=DEV).bfloat16()
+    q = qkv[:, : H * hd].view(B, T, H, hd)
+    k = qkv[:, H * hd: 2 * H * hd].view(B, T, H, hd)
+    v = qkv[:, 2 * H * hd:].view(B, T, H, hd)
+    scale = 1 / math.sqrt(hd)
+    o, lse = C.attn_fwd(q, k, v, scale, True)
+    orf, lser = R.attn_fwd(q.float(), k.float(), v.float(), scale, True)
+    assert _rel(o, orf) < 2e-2
+    assert (lse - lser).abs().max().item() < 2e-2
+    do = torch.randn(B, T, H, hd, device=DEV).bfloat16()
+    dqkv = torch.empty_like(qkv)
+    dq = dqkv[:, : H * hd].view(B, T, H, hd)
+    dk = dqkv[:, H * hd: 2 * H * hd].view(B, T, H, hd)
+    dv = dqkv[:, 2 * H * hd:].view(B, T, H, hd)
+    C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv)
+    rq, rk, rv = (torch.empty(B, T, H, hd, device=DEV) for _ in range(3))
+    R.attn_bwd(do.float(), q.float(), k.float(), v.float(), o.float(), lse, scale, True, rq, rk, rv)
+    assert _rel(dq, rq) < 3e-2 and _rel(dk, rk) < 3e-2 and _rel(dv, rv) < 3e-2
+
+
+def test_attention_deterministic(C):
+    B, T, H, hd = 2, 512, 2, 64
+    qkv = torch.randn(B * T, 3 * H * hd, device=DEV).bfloat16()
+    q, k, v = (qkv[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+    o, lse = C.attn_fwd(q, k, v, 0.125, True)
+    do = torch.randn_like(o)
+    outs = []
+    for _ in range(2):
+        d = torch.empty_like(qkv)
+        dq, dk, dv = (d[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+        C.attn_bwd(do, q, k, v, o, lse, 0.125, True, dq, dk, dv)
+        outs.append(d)
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_adam_matches_torch(C):
+    torch.manual_seed(11)
+    ps = [torch.randn(n, device=DEV) for n in (1000, 16384 * 2 + 7, 4096)]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    gs = [torch.randn_like(p) for p in ps]
+    ms = [torch.zeros_like(p) for p in ps]
+    vs = [torch.zeros_like(p) for p in ps]
+    sh = [torch.empty_like(p, dtype=torch.bfloat16) for p in ps]
+    desc, chunks = C.adam_build(ps, gs, ms, vs, sh)
+    opt = torch.optim.Adam(ref, lr=1e-3, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.01)
+    for step in range(1, 4):
+        for r, g in zip(ref, gs):
+            r.grad = g.clone()
+        opt.step()
+        C.adam_step(desc, chunks, 1e-3, 0.9, 0.95, 1e-8, 0.01, step)
+    for p, r, s in zip(ps, ref, sh):
+        assert (p - r.detach()).abs().max().item() < 1e-5
+        assert torch.equal(s, p.bfloat16())
