@@ -155,7 +155,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if a.global_batch else "weak",
         "vs_baseline": round(vs, 4) if vs else None,
-        "dtype": "bf16",
+        "dtype": "bf16" if dev.type == "cuda" else "fp32",
         "data": "synthetic (uniform random token ids), random-init weights",
         "config": {
             "model": a.model + (f"(L={a.layers})" if a.layers else ""),

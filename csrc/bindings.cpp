@@ -28,7 +28,8 @@ void dpfs_swiglu_fwd(int, const void*, void*, int, int, hipStream_t);
 void dpfs_swiglu_bwd(int, const void*, const void*, void*, int, int, hipStream_t);
 void dpfs_rope(int, void*, const int64_t*, const float*, int, int, int, int, int, hipStream_t);
 void dpfs_bias_residual(int, const void*, const float*, const void*, void*, int, int, hipStream_t);
-int dpfs_colsum_groups(int);
+long long dpfs_colsum_ws(int, int);
+long long dpfs_norm_bwd_ws(int, int, int);
 void dpfs_bias_grad(int, const void*, float*, float*, int, int, hipStream_t);
 void dpfs_embedding_fwd(int, const int64_t*, const float*, void*, int, int, long long, int, hipStream_t);
 void dpfs_embedding_bwd(int, const void*, const int64_t*, float*, int, int, long long, int, hipStream_t);
@@ -154,7 +155,7 @@ torch::Tensor bias_grad(torch::Tensor dy) {
   const at::DeviceGuard g(dy.device());
   auto out = torch::empty({N}, dy.options().dtype(torch::kFloat32));
   if (M == 0) return out.zero_();
-  auto ws = torch::empty({(int64_t)dpfs_colsum_groups((int)M) * N}, out.options());
+  auto ws = torch::empty({(int64_t)dpfs_colsum_ws((int)M, (int)N)}, out.options());
   dpfs_bias_grad(dcode(dy), dy.data_ptr(), out.data_ptr<float>(), ws.data_ptr<float>(), (int)M, (int)N, stream());
   return out;
 }
@@ -193,7 +194,7 @@ int check_norm_x(const torch::Tensor& x, const torch::Tensor& w) {
   TORCH_CHECK(x.is_contiguous(), "norm: x must be contiguous");
   const int dt = dcode(x);
   const int64_t D = x.size(1);
-  TORCH_CHECK(D % (dt == 1 ? 8 : 4) == 0 && D <= 16 * 64 * (dt == 1 ? 8 : 4), "norm: unsupported hidden size ", D);
+  TORCH_CHECK(D % (dt == 1 ? 8 : 4) == 0 && D <= 32 * 64 * (dt == 1 ? 8 : 4), "norm: unsupported hidden size ", D);
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kFloat32 && w.is_contiguous() && w.numel() == D,
               "norm: weight must be contiguous fp32 [D]");
   return dt;
@@ -218,7 +219,7 @@ std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch:
   auto dx = torch::empty_like(x);
   auto dw = torch::empty({D}, w.options());
   if (M == 0) return {dx, dw.zero_()};
-  auto ws = torch::empty({(int64_t)dpfs_norm_bwd_grid((int)M) * D}, w.options());
+  auto ws = torch::empty({(int64_t)dpfs_norm_bwd_ws(0, (int)M, (int)D)}, w.options());
   dpfs_norm_bwd(0, dt, dy.data_ptr(), x.data_ptr(), w.data_ptr<float>(), nullptr, rstd.data_ptr<float>(), dx.data_ptr(),
                 dw.data_ptr<float>(), nullptr, ws.data_ptr<float>(), nullptr, (int)M, (int)D, stream());
   return {dx, dw};
@@ -249,7 +250,7 @@ std::vector<torch::Tensor> layernorm_bwd(torch::Tensor dy, torch::Tensor x, torc
   auto db = torch::empty({D}, w.options());
   if (M == 0) return {dx, dw.zero_(), db.zero_()};
   const int64_t G = dpfs_norm_bwd_grid((int)M);
-  auto ws = torch::empty({2 * G * D}, w.options());
+  auto ws = torch::empty({(int64_t)dpfs_norm_bwd_ws(1, (int)M, (int)D)}, w.options());
   dpfs_norm_bwd(1, dt, dy.data_ptr(), x.data_ptr(), w.data_ptr<float>(), mean.data_ptr<float>(),
                 rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr<float>(), db.data_ptr<float>(),
                 ws.data_ptr<float>(), ws.data_ptr<float>() + G * D, (int)M, (int)D, stream());

@@ -120,37 +120,62 @@ __global__ __launch_bounds__(256) void bias_residual_k(const T* __restrict__ y, 
   }
 }
 
-// Bias gradient: column sums of dy[M, N] -> fp32 partials [G, N] (each block a contiguous
-// row range, fixed order), then a fixed-order reduction over G.  Deterministic.
+// Column sums (bias gradient, norm-weight gradient partials).  Two deterministic stages,
+// both 2-D: a block = 32 column vectors x 8 row lanes, each lane strides over rows, then the
+// 8 lanes are reduced through LDS in a fixed order.  Stage 1 reads the bf16/fp32 activation
+// grad [M, N] in row chunks -> fp32 partials [R, N]; stage 2 reduces [R, N] -> [N].
 template <typename T>
-__global__ __launch_bounds__(256) void colsum_rows_k(const T* __restrict__ dy, float* __restrict__ partial,
-                                                     int M, int N_, int rows_per_block) {
+__global__ __launch_bounds__(256) void colsum_stage_k(const T* __restrict__ x, float* __restrict__ out, int M,
+                                                      int N_, int rows_per_chunk) {
   constexpr int N = Vec<T>::N;
-  const int nvec = N_ / N;
-  const int r0 = blockIdx.y * rows_per_block;
-  const int r1 = min(M, r0 + rows_per_block);
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < nvec; c += gridDim.x * blockDim.x) {
-    float acc[N];
+  __shared__ float red[8][32 * N];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int cvec = blockIdx.x * 32 + tx;
+  const int c0 = cvec * N;
+  const int r0 = blockIdx.y * rows_per_chunk;
+  const int r1 = min(M, r0 + rows_per_chunk);
+  float acc[N];
 #pragma unroll
-    for (int j = 0; j < N; ++j) acc[j] = 0.f;
-    for (int r = r0; r < r1; ++r) {
+  for (int j = 0; j < N; ++j) acc[j] = 0.f;
+  if (c0 < N_) {
+    for (int r = r0 + ty; r < r1; r += 8) {
       float v[N];
-      load_vec<T>(dy + (long long)r * N_ + c * N, v);
+      load_vec<T>(x + (long long)r * N_ + c0, v);
 #pragma unroll
       for (int j = 0; j < N; ++j) acc[j] += v[j];
     }
+  }
 #pragma unroll
-    for (int j = 0; j < N; ++j) partial[(long long)blockIdx.y * N_ + c * N + j] = acc[j];
+  for (int j = 0; j < N; ++j) red[ty][tx * N + j] = acc[j];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 32 * N; i += 256) {
+    const int col = blockIdx.x * 32 * N + i;
+    if (col < N_) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += red[k][i];
+      out[(long long)blockIdx.y * N_ + col] = s;
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void colsum_final_k(const float* __restrict__ partial, float* __restrict__ out,
-                                                      int G, int N_) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N_) return;
-  float s = 0.f;
-  for (int g = 0; g < G; ++g) s += partial[(long long)g * N_ + c];
-  out[c] = s;
+template <typename T>
+static void colsum_launch(const T* x, float* out, float* ws, int M, int N_, hipStream_t s) {
+  constexpr int N = Vec<T>::N;
+  const int cblocks = (N_ / N + 31) / 32;
+  int chunks = 1024 / cblocks;
+  const int max_chunks = (M + 63) / 64;
+  if (chunks > max_chunks) chunks = max_chunks;
+  if (chunks < 1) chunks = 1;
+  const int rpc = (M + chunks - 1) / chunks;
+  chunks = (M + rpc - 1) / rpc;
+  if (chunks == 1) {
+    colsum_stage_k<T><<<dim3(cblocks, 1), 256, 0, s>>>(x, out, M, N_, rpc);
+    return;
+  }
+  colsum_stage_k<T><<<dim3(cblocks, chunks), 256, 0, s>>>(x, ws, M, N_, rpc);
+  const int cb2 = (N_ / 4 + 31) / 32;
+  colsum_stage_k<float><<<dim3(cb2, 1), 256, 0, s>>>(ws, out, chunks, N_, chunks);
 }
 
 }  // namespace dpfs
@@ -193,19 +218,14 @@ extern "C" void dpfs_bias_residual(int dtype, const void* y, const float* bias, 
                                                                                  (const float*)res, (float*)out, M, N);
 }
 
-extern "C" int dpfs_colsum_groups(int M) {
-  int g = (M + 255) / 256;  // 256 rows per block
-  return g < 1 ? 1 : g;
+// Workspace (floats) needed by dpfs_bias_grad / dpfs_colsum_f32 for an [M, N] input.
+extern "C" long long dpfs_colsum_ws(int M, int N) { return (long long)((M + 63) / 64) * N; }
+
+extern "C" void dpfs_bias_grad(int dtype, const void* dy, float* out, float* ws, int M, int N, hipStream_t s) {
+  if (dtype == kBF16) colsum_launch<bf16>((const bf16*)dy, out, ws, M, N, s);
+  else colsum_launch<float>((const float*)dy, out, ws, M, N, s);
 }
 
-extern "C" void dpfs_bias_grad(int dtype, const void* dy, float* out, float* partial, int M, int N, hipStream_t s) {
-  const int G = dpfs_colsum_groups(M);
-  const int rows = (M + G - 1) / G;
-  const int vecN = dtype == kBF16 ? 8 : 4;
-  dim3 grid((N / vecN + 255) / 256, G);
-  if (dtype == kBF16)
-    colsum_rows_k<bf16><<<grid, 256, 0, s>>>((const bf16*)dy, partial, M, N, rows);
-  else
-    colsum_rows_k<float><<<grid, 256, 0, s>>>((const float*)dy, partial, M, N, rows);
-  colsum_final_k<<<(N + 255) / 256, 256, 0, s>>>(partial, out, G, N);
+extern "C" void dpfs_colsum_f32(const float* x, float* out, float* ws, int M, int N, hipStream_t s) {
+  colsum_launch<float>(x, out, ws, M, N, s);
 }

@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void ce_bwd_k(const T* logits, const int64_t* 
     for (int j = 0; j < N; ++j) {
       const int col = c + j;
       float p = col < vvalid ? __expf(v[j] - l) : 0.f;
-      if (col == loc) p -= 1.f;
+      if (col == loc && col < vvalid) p -= 1.f;
       v[j] = p * g;
     }
     store_vec<T>(out + r * V + c, v);

@@ -196,16 +196,6 @@ __global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, cons
   }
 }
 
-// out[c] = sum_g partial[g, c] in a fixed order (g ascending).
-__global__ __launch_bounds__(256) void colsum_partials_k(const float* __restrict__ partial, float* __restrict__ out,
-                                                         int G, int D) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= D) return;
-  float s = 0.f;
-  for (int g = 0; g < G; ++g) s += partial[(size_t)g * D + col];
-  out[col] = s;
-}
-
 template <typename T>
 static int vpl_for(int D) {
   const int nvec = D / Vec<T>::N;
@@ -220,19 +210,29 @@ static int vpl_for(int D) {
     else if (_v <= 4) { constexpr int VPL = 4; __VA_ARGS__; }               \
     else if (_v <= 8) { constexpr int VPL = 8; __VA_ARGS__; }               \
     else if (_v <= 12) { constexpr int VPL = 12; __VA_ARGS__; }             \
-    else { constexpr int VPL = 16; __VA_ARGS__; }                           \
+    else if (_v <= 16) { constexpr int VPL = 16; __VA_ARGS__; }             \
+    else if (_v <= 24) { constexpr int VPL = 24; __VA_ARGS__; }             \
+    else { constexpr int VPL = 32; __VA_ARGS__; }                           \
   } while (0)
 
 int norm_bwd_grid(int M) {
   int g = (M + kRowsPerBlock - 1) / kRowsPerBlock;
-  return g < 512 ? g : 512;
+  return g < 1024 ? g : 1024;
 }
 
 }  // namespace dpfs
 
 using namespace dpfs;
 
+extern "C" void dpfs_colsum_f32(const float* x, float* out, float* ws, int M, int N, hipStream_t s);
+extern "C" long long dpfs_colsum_ws(int M, int N);
+
 extern "C" int dpfs_norm_bwd_grid(int M) { return norm_bwd_grid(M); }
+// Total fp32 workspace of dpfs_norm_bwd: block partials (x2 for LayerNorm) + stage-2 partials.
+extern "C" long long dpfs_norm_bwd_ws(int mode, int M, int D) {
+  const int G = norm_bwd_grid(M);
+  return (long long)G * D * (mode == 1 ? 2 : 1) + dpfs_colsum_ws(G, D);
+}
 
 extern "C" void dpfs_rmsnorm_fwd(int dtype, const void* x, const float* w, void* y, float* rstd, int M, int D,
                                  float eps, hipStream_t s) {
@@ -273,6 +273,9 @@ extern "C" void dpfs_norm_bwd(int mode, int dtype, const void* dy, const void* x
     if (mode == 0) DPFS_NB(float, 0); else DPFS_NB(float, 1);
   }
 #undef DPFS_NB
-  colsum_partials_k<<<(D + 255) / 256, 256, 0, s>>>(partial_w, dw, G, D);
-  if (mode == 1) colsum_partials_k<<<(D + 255) / 256, 256, 0, s>>>(partial_b, db, G, D);
+  // Stage 2 (fixed-order 2-D column reduction over the G block partials).  The workspace
+  // for its own partials lives after the G*D block partials (dpfs_norm_bwd_ws).
+  float* ws2 = partial_w + (size_t)G * D * (mode == 1 ? 2 : 1);
+  dpfs_colsum_f32(partial_w, dw, ws2, G, D, s);
+  if (mode == 1) dpfs_colsum_f32(partial_b, db, ws2, G, D, s);
 }

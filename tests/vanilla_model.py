@@ -42,7 +42,7 @@ class VAttention(nn.Module):
         c, s = cos[:, None], sin[:, None]
         q, k = q * c + _rot(q) * s, k * c + _rot(k) * s
         a = (q @ k.transpose(-1, -2)) / math.sqrt(self.hd)
-        mask = torch.triu(torch.ones(t, t, dtype=torch.bool), 1)
+        mask = torch.triu(torch.ones(t, t, dtype=torch.bool, device=x.device), 1)
         a = a.masked_fill(mask, -10000.0).softmax(-1)
         o = (a @ v).transpose(1, 2).reshape(b, t, -1)
         return self.wo(o)
