@@ -17,6 +17,10 @@ extern "C" {
 void dpfs_gemm_nt(const void*, const void*, void*, const float*, int, int, int, int, int, int, hipStream_t);
 void dpfs_gemm_nn(const void*, const void*, void*, int, int, int, int, int, int, hipStream_t);
 int dpfs_gemm_tn_splits(int, int, int);
+void dpfs_gemm_set_impl(int);
+void dpfs_gemm_force(int, int);
+void dpfs_gemm_set_workspace(float*, long long);
+long long dpfs_gemm_bf16_ws(int, int, int);
 void dpfs_gemm_tn(const void*, const void*, float*, float*, int, int, int, int, int, int, hipStream_t);
 void dpfs_rmsnorm_fwd(int, const void*, const float*, void*, float*, int, int, float, hipStream_t);
 void dpfs_layernorm_fwd(int, const void*, const float*, const float*, void*, float*, float*, int, int, float,
@@ -92,8 +96,14 @@ torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
   if (M == 0 || N == 0) return c;
   if (K == 0) return c.zero_();
   TORCH_CHECK(N % 2 == 0 || true, "");
+  TORCH_CHECK(N % 4 == 0, "gemm_nt: N must be a multiple of 4, got ", N);
+  const long long wsn = dpfs_gemm_bf16_ws((int)M, (int)N, (int)K);
+  torch::Tensor ws;
+  if (wsn > 0) ws = torch::empty({wsn}, a.options().dtype(torch::kFloat32));
+  dpfs_gemm_set_workspace(wsn > 0 ? ws.data_ptr<float>() : nullptr, wsn);
   dpfs_gemm_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), opt_f32(bias, N, "bias"), (int)M, (int)N, (int)K,
                (int)a.stride(0), (int)b.stride(0), (int)N, stream());
+  dpfs_gemm_set_workspace(nullptr, 0);
   return c;
 }
 
@@ -109,8 +119,13 @@ torch::Tensor gemm_nn(torch::Tensor a, torch::Tensor b) {
   auto c = torch::empty({M, N}, a.options());
   if (M == 0 || N == 0) return c;
   if (K == 0) return c.zero_();
+  const long long wsn = dpfs_gemm_bf16_ws((int)M, (int)N, (int)K);
+  torch::Tensor ws;
+  if (wsn > 0) ws = torch::empty({wsn}, a.options().dtype(torch::kFloat32));
+  dpfs_gemm_set_workspace(wsn > 0 ? ws.data_ptr<float>() : nullptr, wsn);
   dpfs_gemm_nn(a.data_ptr(), b.data_ptr(), c.data_ptr(), (int)M, (int)N, (int)K, (int)a.stride(0), (int)b.stride(0),
                (int)N, stream());
+  dpfs_gemm_set_workspace(nullptr, 0);
   return c;
 }
 
@@ -486,6 +501,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels of distributed_pytorch_from_scratch_amd";
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("bias") = py::none());
   m.def("gemm_nn", &gemm_nn);
+  m.def("gemm_force", [](int cfg, int splits) { dpfs_gemm_force(cfg, splits); },
+        "force the v2 tile config (-1 auto, 0 = 256x256, 1 = 256x128) and K-splits (0 auto)");
+  m.def("gemm_set_impl", [](int v) { dpfs_gemm_set_impl(v); }, "1 = v1 (128x128 register-staged), 2 = v2 (LDS-DMA)");
   m.def("gemm_tn", &gemm_tn, py::arg("a"), py::arg("b"), py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("bias_grad", &bias_grad);
   m.def("add_bias_", &add_bias_);

@@ -8,7 +8,11 @@
 //   TN      a[k*lda + m]      b[k*ldb + n]      wgrad     dW = dy^T x   (fp32 out, split-K)
 //
 // Reference call sites: models/layers.py:49,93 (F.linear) and their autograd backward
-// (SURVEY.md K8/K9).  Design (CDNA HIP guide §5):
+// (SURVEY.md K8/K9).  Two kernels live here: gemm2_k (v2, the default: 256x256 / 256x128
+// tiles, 8 waves, LDS-DMA staging, split-K; described at its definition) and gemm_k (v1,
+// kept for small-output wgrads where its 128x128 tile fills the chip better).  The
+// selection heuristics below were derived from tools/tune_gemm.py sweeps on MI355X.
+// v1 design (CDNA HIP guide §5):
 //  * 128x128x64 block tile, 256 threads = 4 waves in 2x2, each wave 64x64 = 4x4 tiles of
 //    v_mfma_f32_16x16x32_bf16 (16 accumulators x 4 regs);
 //  * operands staged global -> registers (16-byte loads) -> LDS, double-buffered LDS with the
@@ -204,50 +208,359 @@ __global__ __launch_bounds__(256) void splitk_reduce_k(const float* __restrict__
   }
 }
 
+
+// ======================================================================== GEMM v2 ====
+// 256x256 (or 256x128) x 64 block tile, 512 threads = 8 waves, LDS-DMA staging.
+//  * operands go HBM -> LDS with buffer_load_dwordx4 ... lds (no VGPR round trip, no
+//    ds_write: the register-staged v1 was bound by ds_write_b128 throughput); the LDS image
+//    is lane-linear per 1 KiB DMA piece, so the XOR swizzles are applied on the SOURCE
+//    address (rule 21: linear dest + swizzled source + the same swizzle on read);
+//  * tails: a per-lane offset past the buffer descriptor's num_records returns zeros, so K
+//    tails contribute nothing and out-of-range rows never fault (no branches in the loop);
+//  * 2 LDS stages: the DMA of tile t+1 is in flight while tile t is multiplied; counted
+//    `s_waitcnt vmcnt(pieces of t+1)` + raw s_barrier (never vmcnt(0) in steady state);
+//  * MFMA operands swapped (acc = W-frag x X-frag) so each lane owns 4 consecutive output
+//    columns of one row: bf16x4 / f32x4 vector stores and a vector bias load.
+constexpr unsigned kOOB = 0xFFFFFFF0u;
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, unsigned off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, off, 0,
+                                           0, 0);
+}
+
+template <int N_>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N_ >= 0 && N_ < 64, "vmcnt range");
+  // gfx9 s_waitcnt: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]
+  __builtin_amdgcn_s_waitcnt((N_ & 15) | (7 << 4) | (15 << 8) | ((N_ >> 4) << 14));
+}
+
+// Issue the DMA of one operand tile (R rows/cols x 64 k) into LDS at `tile`.
+template <bool KMAJ, int R>
+__device__ __forceinline__ void issue_tile(__amdgpu_buffer_rsrc_t rs, char* tile, int r0, int k0, int ld, int K) {
+  const int l = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+  for (int i = 0; i < R / 64; ++i) {
+    const int j = wave + 8 * i;  // 1 KiB piece index
+    unsigned off;
+    if (KMAJ) {
+      const int row = 8 * j + (l >> 3);
+      const int c = (l & 7) ^ ((l >> 3) & 7);
+      const int k = k0 + c * 8;
+      off = (k < K) ? (unsigned)(((long long)(r0 + row) * ld + k) * 2) : kOOB;
+    } else {
+      constexpr int CPR = R / 8;
+      const int lin = j * 64 + l;
+      const int row = lin / CPR;
+      const int c = (lin % CPR) ^ (mn_h(row) << 1);
+      const int k = k0 + row;
+      off = (k < K) ? (unsigned)(((long long)k * ld + r0 + c * 8) * 2) : kOOB;
+    }
+    dma16(rs, tile + j * 1024, off);
+  }
+}
+
+template <bool KMAJ, int R>
+__device__ __forceinline__ bf16x8 frag2(const char* lds, int rb, int kb) {
+  const int l = lane_id();
+  if (KMAJ) {
+    const int row = rb + (l & 15);
+    const int chunk = (kb >> 3) + (l >> 4);
+    return *reinterpret_cast<const bf16x8*>(lds + row * 128 + ((chunk ^ (row & 7)) << 4));
+  } else {
+    constexpr int RB = R * 2;
+    const int i = l & 15, q = i >> 2, p = i & 3;
+    const int chunk = (rb + 4 * p) >> 3;
+    const int k_lo = kb + 8 * (l >> 4) + q;
+    const int k_hi = k_lo + 4;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(lds + k_lo * RB + ((chunk ^ (mn_h(k_lo) << 1)) << 4) + (p & 1) * 8));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(lds + k_hi * RB + ((chunk ^ (mn_h(k_hi) << 1)) << 4) + (p & 1) * 8));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+template <int PIECES, int NSTAGE>
+__device__ __forceinline__ void wait_tile(int remaining_after) {
+  // Tiles issued after the one we need: min(NSTAGE-2, remaining_after); each = PIECES DMAs.
+  if (NSTAGE >= 3 && remaining_after >= 1) {
+    if (NSTAGE >= 4 && remaining_after >= 2) wait_vmcnt<2 * PIECES>();
+    else wait_vmcnt<PIECES>();
+  } else {
+    wait_vmcnt<0>();
+  }
+}
+
+// OUT: 0 = bf16 C (+bias); 1 = fp32 C / split-K slab.
+template <int BM_, int BN_, int WAVES_M, int NSTAGE, bool AK, bool BKM, int OUT>
+__global__ __launch_bounds__(512, 2) void gemm2_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                  void* __restrict__ C, const float* __restrict__ bias, int M, int N,
+                                                  int K, int lda, int ldb, int ldc, int k_per_split,
+                                                  long long slab_stride, unsigned a_bytes, unsigned b_bytes) {
+  constexpr int WAVES_N = 8 / WAVES_M;
+  constexpr int WM = BM_ / WAVES_M, WN = BN_ / WAVES_N;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int A_BYTES = BM_ * 128, B_BYTES = BN_ * 128, STAGE = A_BYTES + B_BYTES;
+  constexpr int PIECES = BM_ / 64 + BN_ / 64;  // DMA instructions per wave per K-step
+  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE];
+
+  const int tiles_n = (N + BN_ - 1) / BN_;
+  const int tiles_m = (M + BM_ - 1) / BM_;
+  const int nwg = tiles_m * tiles_n;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int tm = wg / tiles_n, tn = wg % tiles_n;
+  const int m0 = tm * BM_, n0 = tn * BN_;
+  const int kbeg = blockIdx.y * k_per_split;
+  const int kend = min(K, kbeg + k_per_split);
+  const int nk = kend > kbeg ? (kend - kbeg + 63) / 64 : 0;
+
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int l = lane_id();
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (int)b_bytes, 0x00020000);
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // Prologue: NSTAGE-1 tiles in flight.
+#pragma unroll
+  for (int s0 = 0; s0 < NSTAGE - 1; ++s0) {
+    if (s0 < nk) {
+      char* st = smem + s0 * STAGE;
+      issue_tile<AK, BM_>(ra, st, m0, kbeg + s0 * 64, lda, kend);
+      issue_tile<BKM, BN_>(rb, st + A_BYTES, n0, kbeg + s0 * 64, ldb, kend);
+    }
+  }
+  int cur = 0;
+  for (int t = 0; t < nk; ++t) {
+    wait_tile<PIECES, NSTAGE>(nk - 1 - t);
+    __builtin_amdgcn_s_barrier();  // tile t landed for all waves; tile t-1's buffer is free
+    if (t + NSTAGE - 1 < nk) {
+      int nb = cur + NSTAGE - 1;
+      if (nb >= NSTAGE) nb -= NSTAGE;
+      char* st = smem + nb * STAGE;
+      const int k1 = kbeg + (t + NSTAGE - 1) * 64;
+      issue_tile<AK, BM_>(ra, st, m0, k1, lda, kend);
+      issue_tile<BKM, BN_>(rb, st + A_BYTES, n0, k1, ldb, kend);
+    }
+    const char* la = smem + cur * STAGE;
+    const char* lb = la + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = frag2<AK, BM_>(la, wm * WM + 16 * i, 32 * s);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = frag2<BKM, BN_>(lb, wn * WN + 16 * j, 32 * s);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    cur = (cur + 1 == NSTAGE) ? 0 : cur + 1;
+  }
+
+  // Epilogue: acc[i][j] = C^T tile: lane holds C[m = .. + (l&15)][n = .. + 4g + r], r < 4.
+  const int g = l >> 4;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * WM + 16 * i + (l & 15);
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WN + 16 * j + 4 * g;
+      if (n >= N) continue;
+      f32x4 v = acc[i][j];
+      if (OUT == 0) {
+        if (bias) v += *reinterpret_cast<const f32x4*>(bias + n);
+        bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(C) + (long long)m * ldc + n) = o;
+      } else {
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + blockIdx.y * slab_stride + (long long)m * ldc + n) = v;
+      }
+    }
+  }
+}
+
+// bf16 out[m*ldc + n] = sum_s slab[s][m*N + n] (+ bias[n]), fixed order; N % 4 == 0.
+__global__ __launch_bounds__(256) void splitk_reduce_bf16_k(const float* __restrict__ slabs, bf16* __restrict__ out,
+                                                            const float* __restrict__ bias, int M, int N, int ldc,
+                                                            int S) {
+  const long long n4 = (long long)M * N / 4;
+  const long long stride = (long long)M * N;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const long long e = i * 4;
+    const int m = (int)(e / N), n = (int)(e % N);
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < S; ++k) s += *reinterpret_cast<const f32x4*>(slabs + k * stride + e);
+    if (bias) s += *reinterpret_cast<const f32x4*>(bias + n);
+    bf16x4 o = {(bf16)s[0], (bf16)s[1], (bf16)s[2], (bf16)s[3]};
+    *reinterpret_cast<bf16x4*>(out + (long long)m * ldc + n) = o;
+  }
+}
+
 }  // namespace dpfs
 
 using namespace dpfs;
 
 static int tiles_of(int M, int N) { return ((M + BM - 1) / BM) * ((N + BN - 1) / BN); }
+static int tiles2(int M, int N, int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); }
+
+static unsigned span_bytes(long long rows, long long ld, long long cols) {
+  // bytes from the base to the end of the last row of a (rows x cols, stride ld) bf16 view
+  const long long b = rows > 0 ? ((rows - 1) * ld + cols) * 2 : 0;
+  return (unsigned)b;
+}
+
+// v2 configurations: 0 = 256x256 / 2-stage (128 KiB LDS), 1 = 256x128 / 3-stage (144 KiB).
+template <bool AK, bool BKM, int OUT>
+static void launch2(int cfg, const void* A, const void* B, void* C, const float* bias, int M, int N, int K, int lda,
+                    int ldb, int ldc, int splits, int kps, long long slab, unsigned ab, unsigned bb, hipStream_t s) {
+  if (cfg == 0) {
+    gemm2_k<256, 256, 2, 2, AK, BKM, OUT><<<dim3(tiles2(M, N, 256, 256), splits), 512, 0, s>>>(
+        (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, kps, slab, ab, bb);
+  } else {
+    gemm2_k<256, 128, 4, 3, AK, BKM, OUT><<<dim3(tiles2(M, N, 256, 128), splits), 512, 0, s>>>(
+        (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, kps, slab, ab, bb);
+  }
+}
+
+static int g_force_cfg = -1;     // -1 auto, 0 = 256x256, 1 = 256x128 (tuning / A-B runs)
+static int g_force_splits = 0;   // 0 auto
+extern "C" void dpfs_gemm_force(int cfg, int splits) {
+  g_force_cfg = cfg;
+  g_force_splits = splits;
+}
+
+// Tile choice (measured with tools/tune_gemm.py, see profiles/): 256x256 unless the
+// 256x128 tile wastes less of a ragged N (e.g. N = 384 at TP=8).
+static int pick_cfg(int M, int N, int splits) {
+  if (g_force_cfg >= 0) return g_force_cfg;
+  const int w0 = ((N + 255) / 256) * 256 - N, w1 = ((N + 127) / 128) * 128 - N;
+  return (w1 < w0 && w0 * 10 > N) ? 1 : 0;  // only when the 256-wide tile wastes > 10% of N
+}
+
+// K-splits: grow while the grid stays <= ~1300 blocks (~5 waves of 256 CUs) and each split
+// keeps >= 4096 of K (fp32 slab round trip < ~10% of the split's MFMA time).
+static int v2_splits(int M, int N, int K, int cfg) {
+  const int tiles = cfg == 0 ? tiles2(M, N, 256, 256) : tiles2(M, N, 256, 128);
+  int s = 1;
+  while (s < 64 && tiles * s * 2 <= 1300 && K / (s * 2) >= 4096) s *= 2;
+  return s;
+}
+
+// Split-K for bf16-output GEMMs whose tile grid under-fills 256 CUs while K is long
+// (e.g. the lm_head dgrad: N = d_model, K = vocab shard).
+static int bf16_splits(int M, int N, int K) {
+  if (g_force_splits > 0) return g_force_splits;
+  return v2_splits(M, N, K, pick_cfg(M, N, 1));
+}
+
+static int g_gemm_impl = 2;
+extern "C" void dpfs_gemm_set_impl(int v) { g_gemm_impl = v; }
+
+static thread_local float* g_ws = nullptr;  // split-K workspace for bf16 outputs (set by host)
+static thread_local long long g_ws_floats = 0;
+extern "C" void dpfs_gemm_set_workspace(float* ws, long long n) {
+  g_ws = ws;
+  g_ws_floats = n;
+}
+extern "C" long long dpfs_gemm_bf16_ws(int M, int N, int K) {
+  const int S = bf16_splits(M, N, K);
+  return S > 1 ? (long long)S * M * N : 0;
+}
+
+template <bool BKM>
+static void bf16_gemm(const void* A, const void* B, void* C, const float* bias, int M, int N, int K, int lda, int ldb,
+                      int ldc, unsigned ab, unsigned bb, hipStream_t s) {
+  const int S = bf16_splits(M, N, K);
+  if (S > 1 && g_ws && g_ws_floats >= (long long)S * M * N) {
+    int kps = (K + S - 1) / S;
+    kps = ((kps + BKK - 1) / BKK) * BKK;
+    launch2<true, BKM, 1>(pick_cfg(M, N, S), A, B, g_ws, nullptr, M, N, K, lda, ldb, N, S, kps, (long long)M * N, ab,
+                          bb, s);
+    long long g = ((long long)M * N / 4 + 255) / 256;
+    if (g > 4096) g = 4096;
+    splitk_reduce_bf16_k<<<(int)g, 256, 0, s>>>(g_ws, (bf16*)C, bias, M, N, ldc, S);
+    return;
+  }
+  launch2<true, BKM, 0>(pick_cfg(M, N, 1), A, B, C, bias, M, N, K, lda, ldb, ldc, 1, K, 0, ab, bb, s);
+}
 
 // NT: C[M,N] bf16 = A[M,K] B[N,K]^T + bias
 extern "C" void dpfs_gemm_nt(const void* A, const void* B, void* C, const float* bias, int M, int N, int K, int lda,
                              int ldb, int ldc, hipStream_t s) {
-  dim3 grid(tiles_of(M, N), 1);
-  gemm_k<true, true, 0><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, K, 0);
+  if (g_gemm_impl == 1) {
+    gemm_k<true, true, 0><<<dim3(tiles_of(M, N), 1), 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K,
+                                                                 lda, ldb, ldc, K, 0);
+    return;
+  }
+  bf16_gemm<true>(A, B, C, bias, M, N, K, lda, ldb, ldc, span_bytes(M, lda, K), span_bytes(N, ldb, K), s);
 }
 
 // NN: C[M,N] bf16 = A[M,K] B[K,N]
 extern "C" void dpfs_gemm_nn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                              hipStream_t s) {
-  dim3 grid(tiles_of(M, N), 1);
-  gemm_k<true, false, 0><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, nullptr, M, N, K, lda, ldb, ldc, K,
-                                              0);
+  if (g_gemm_impl == 1) {
+    gemm_k<true, false, 0><<<dim3(tiles_of(M, N), 1), 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, nullptr, M, N,
+                                                                  K, lda, ldb, ldc, K, 0);
+    return;
+  }
+  bf16_gemm<false>(A, B, C, nullptr, M, N, K, lda, ldb, ldc, span_bytes(M, lda, K), span_bytes(K, ldb, N), s);
 }
 
 // How many K-splits the TN (wgrad) launch wants; the caller sizes the slab workspace as
 // splits * M * N fp32 when splits > 1.
-extern "C" int dpfs_gemm_tn_splits(int M, int N, int K) {
-  const int tiles = tiles_of(M, N);
-  int s = 1;
-  while (tiles * s < 512 && (K / (s * 2)) >= 4 * BKK && s < 16) s *= 2;
-  return s;
+// TN (wgrad) plan: v2 when the split grid reaches >= 200 blocks, else the 128x128 v1 kernel
+// (small outputs such as the QKV / FFN weight grads at TP=1 run better there).
+static bool tn_use_v1(int M, int N, int K) {
+  if (g_gemm_impl == 1) return true;
+  if (g_force_cfg >= 0 || g_force_splits > 0) return false;
+  const int cfg = pick_cfg(M, N, 1);
+  const int tiles = cfg == 0 ? tiles2(M, N, 256, 256) : tiles2(M, N, 256, 128);
+  return tiles * v2_splits(M, N, K, cfg) < 200;
 }
 
-// TN: C[M,N] fp32 (+)= A[K,M]^T B[K,N].  ws: splits*M*N floats when splits > 1.
+extern "C" int dpfs_gemm_tn_splits(int M, int N, int K) {
+  if (tn_use_v1(M, N, K)) {
+    const int tiles = tiles_of(M, N);
+    int s = 1;
+    while (tiles * s < 256 && (K / (s * 2)) >= 8 * BKK && s < 64) s *= 2;
+    return s;
+  }
+  if (g_force_splits > 0) return g_force_splits;
+  return v2_splits(M, N, K, pick_cfg(M, N, 1));
+}
+
+// TN: C[M,N] fp32 (+)= A[K,M]^T B[K,N].  ws: splits*M*N floats when splits > 1 or accumulate.
 extern "C" void dpfs_gemm_tn(const void* A, const void* B, float* C, float* ws, int M, int N, int K, int lda, int ldb,
                              int accumulate, hipStream_t s) {
   const int S = dpfs_gemm_tn_splits(M, N, K);
   int kps = (K + S - 1) / S;
   kps = ((kps + BKK - 1) / BKK) * BKK;
   const long long n = (long long)M * N;
-  if (S == 1 && !accumulate) {
-    gemm_k<false, false, 1><<<dim3(tiles_of(M, N), 1), 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, nullptr, M, N,
-                                                                   K, lda, ldb, N, K, 0);
-    return;
+  const bool direct = (S == 1 && !accumulate);
+  float* dst = direct ? C : ws;
+  if (tn_use_v1(M, N, K)) {
+    gemm_k<false, false, 1><<<dim3(tiles_of(M, N), S), 256, 0, s>>>((const bf16*)A, (const bf16*)B, dst, nullptr, M,
+                                                                   N, K, lda, ldb, N, direct ? K : kps,
+                                                                   direct ? 0 : n);
+  } else {
+    launch2<false, false, 1>(pick_cfg(M, N, S), A, B, dst, nullptr, M, N, K, lda, ldb, N, S, direct ? K : kps,
+                             direct ? 0 : n, span_bytes(K, lda, M), span_bytes(K, ldb, N), s);
   }
-  gemm_k<false, false, 1><<<dim3(tiles_of(M, N), S), 256, 0, s>>>((const bf16*)A, (const bf16*)B, ws, nullptr, M, N,
-                                                                 K, lda, ldb, N, kps, n);
+  if (direct) return;
   long long g = (n / 4 + 255) / 256;
   if (g > 4096) g = 4096;
   splitk_reduce_k<<<(int)g, 256, 0, s>>>(ws, C, n, S, accumulate);
