@@ -59,9 +59,17 @@ def all_gather_last_dim(x: torch.Tensor, sizes: Optional[Sequence[int]] = None) 
         out = x.new_empty((n * x.size(0),) + tuple(x.shape[1:]))
         dist.all_gather_into_tensor(out, x, group=group)
         return out.view((n,) + tuple(x.shape)).movedim(0, -2).reshape(*x.shape[:-1], n * x.shape[-1])
-    parts = [x.new_empty(tuple(x.shape[:-1]) + (s,)) for s in sizes]
-    dist.all_gather(parts, x, group=group)
-    return torch.cat(parts, dim=-1)
+    # Uneven shards: pad every shard to the largest size, one all_gather_into_tensor (RCCL and
+    # gloo both require equal sizes), then drop the padding.
+    mx = max(sizes)
+    if x.size(-1) < mx:
+        x = torch.nn.functional.pad(x, (0, mx - x.size(-1)))
+    x2 = x.reshape(-1, mx).contiguous()
+    out = x2.new_empty((n * x2.size(0), mx))
+    dist.all_gather_into_tensor(out, x2, group=group)
+    out = out.view(n, -1, mx)
+    parts = [out[i, :, :sizes[i]] for i in range(n)]
+    return torch.cat(parts, dim=-1).view(*x.shape[:-1], sum(sizes))
 
 
 def slice_last_dim(x: torch.Tensor, sizes: Optional[Sequence[int]] = None) -> torch.Tensor:

@@ -1,0 +1,209 @@
+"""Training entrypoint (tensor parallel, optional DP / SP).
+
+Reference parity: ``train.py:25-151`` — same CLI flags (``--tp_size --master_addr
+--master_port --lr --warmup_steps --max_steps --log_interval --save_interval --save_dir
+--reserv_last_n_ckpts --batch_size/-b --bf16 --data_path/-d --random_seed
+--use_vallina_impl``), same launch model (``mp.spawn`` one process per GPU when not started by
+torchrun), Adam + OneCycleLR schedule, per-rank checkpoints ``tprank-{r}_iter-{n}_loss-{x}.pth``
+with keep-last-N rotation, TensorBoard scalars ``train/ce_loss`` (cumulative mean, as the
+reference), ``train/lr`` and ``used_gpu_memory/tprank-{r}`` under ``{save_dir}/tprank-{r}/``.
+
+Extensions: ``--model`` presets (reference / gpt2-small / gpt2-large / llama2-7b / llama-13b),
+``--seq_len``, ``--synthetic`` data, ``--dp_size``, ``--sp`` (sequence parallel),
+``--max_grad_norm``, ``--resume`` (optimizer/scheduler/RNG sidecar), throughput + MFU
+logging, a per-rank heartbeat and ``--fault_inject_step`` for failure-path testing.
+The loss stays on the device between log intervals (the reference syncs every step).
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+import time
+from argparse import ArgumentParser, Namespace
+from dataclasses import replace
+
+import torch
+import torch.distributed as dist
+
+from .constants import IGNORE_INDEX
+from .data.dataset import get_dataloader, get_synthetic_dataloader
+from .engine import TrainStep
+from .models import Transformer, get_preset
+from .ops.optim import FusedAdam
+from .parallel import process_manager as pm
+from .utils import checkpoint as ck
+from .utils.dist import destroy_dist_env, init_dist_env, set_seed, free_port
+from .utils.fault import Heartbeat, maybe_inject_fault
+from .utils.tb import SummaryWriter
+
+
+def get_train_args(argv=None) -> Namespace:
+    p = ArgumentParser()
+    g = p.add_argument_group("distributed")
+    g.add_argument("--tp_size", type=int, default=2)
+    g.add_argument("--dp_size", type=int, default=1)
+    g.add_argument("--sp", action="store_true", help="Megatron sequence parallelism")
+    g.add_argument("--master_addr", type=str, default="127.0.0.1")
+    g.add_argument("--master_port", type=str, default="25555")
+    g = p.add_argument_group("training")
+    g.add_argument("--lr", type=float, default=3e-4)
+    g.add_argument("--warmup_steps", type=int, default=2000)
+    g.add_argument("--max_steps", type=int, default=20000)
+    g.add_argument("--log_interval", type=int, default=100)
+    g.add_argument("--save_interval", type=int, default=1000)
+    g.add_argument("--save_dir", type=str, default="./checkpoints")
+    g.add_argument("--reserv_last_n_ckpts", type=int, default=-1)
+    g.add_argument("--batch_size", "-b", type=int, default=32)
+    g.add_argument("--bf16", action="store_true", help="bf16 compute (always on for the GPU kernels)")
+    g.add_argument("--max_grad_norm", type=float, default=None)
+    g.add_argument("--resume", type=str, default=None, help="checkpoint path, or 'latest'")
+    g = p.add_argument_group("model")
+    g.add_argument("--model", type=str, default="reference")
+    g.add_argument("--seq_len", type=int, default=None, help="synthetic sequence length (default maxlen)")
+    g = p.add_argument_group("data")
+    g.add_argument("--data_path", "-d", type=str, default=None)
+    g.add_argument("--synthetic", action="store_true")
+    g = p.add_argument_group("other")
+    g.add_argument("--random_seed", type=int, default=0)
+    g.add_argument("--use_vallina_impl", action="store_true", help="only changes the log tag (reference)")
+    g.add_argument("--fault_inject_step", type=int, default=-1)
+    g.add_argument("--device", type=str, default=None, help="cuda|cpu (default: cuda if available)")
+    a = p.parse_args(argv)
+    if a.data_path is None and not a.synthetic:
+        p.error("--data_path is required unless --synthetic")
+    return a
+
+
+def train(rank, args: Namespace):
+    set_seed(args.random_seed)
+    world = args.tp_size * args.dp_size
+    use_cuda = (args.device or ("cuda" if torch.cuda.is_available() else "cpu")) == "cuda"
+    if rank is None:
+        p = init_dist_env(rank=None, tp_size=args.tp_size, dp_size=args.dp_size,
+                          backend="nccl" if use_cuda else "gloo")
+    else:
+        p = init_dist_env(args, rank, world_size=world, backend="nccl" if use_cuda else "gloo")
+    grank = dist.get_rank()
+    dev = torch.device("cuda", torch.cuda.current_device()) if use_cuda else torch.device("cpu")
+    compute_dtype = torch.bfloat16 if (use_cuda or args.bf16) else torch.float32
+    log0 = (lambda *a_: print(*a_, flush=True)) if grank == 0 else (lambda *a_: None)
+    log0(f"{'Enable' if compute_dtype == torch.bfloat16 else 'Disable'} bf16 training  [{p}]")
+
+    margs = replace(get_preset(args.model), sequence_parallel=args.sp)
+    model = Transformer.from_args(margs).to(dev)
+    model.set_compute_dtype(compute_dtype)
+    model.reset_parameters()
+    model.train()
+    nparam = model.num_parameters(global_count=True)
+    log0(model)
+    log0(f"Number of parameters: {nparam / 1e6:.4f} million (global)")
+
+    seq_len = args.seq_len or margs.maxlen
+    if args.synthetic:
+        loader = get_synthetic_dataloader(margs.vocab_size, seq_len, args.batch_size,
+                                          seed=args.random_seed + 17 * p.dp_rank)
+    else:
+        loader = get_dataloader(args.data_path, args.batch_size, IGNORE_INDEX, split="train",
+                                maxlen=margs.maxlen, shuffle=True, seed=args.random_seed + 17 * p.dp_rank)
+        assert loader.dataset.vocab_size == margs.vocab_size, "vocab size of dataset and model should be the same"
+
+    dist.barrier()
+    replicated = [q for n_, q in model.named_parameters() if ck.shard_dim(n_) is None]
+    opt = FusedAdam(model.parameters(), lr=args.lr, max_grad_norm=args.max_grad_norm,
+                    norm_group=p.tp_group, replicated_params=replicated)
+    sched = torch.optim.lr_scheduler.OneCycleLR(opt, args.lr, total_steps=args.max_steps,
+                                                pct_start=min(0.99, args.warmup_steps / max(1, args.max_steps)))
+    step_fn = TrainStep(model, opt, sched)
+    writer = SummaryWriter(os.path.join(args.save_dir, f"tprank-{p.tp_rank}")) if p.dp_rank == 0 else None
+    hb = Heartbeat(interval_s=30.0)
+
+    start_step = 0
+    if args.resume:
+        path = args.resume
+        if path == "latest":
+            cands = ck.list_checkpoints(args.save_dir, p.tp_rank)
+            path = cands[-1] if cands else None
+        if path:
+            ck.load_model(model, path)
+            st = ck.load_resume(path, opt, None)
+            start_step = ck.parse_iter(path) if st is None else int(st["step"])
+            # Re-derive the LR schedule for this run's --max_steps and fast-forward it.
+            import warnings
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")
+                for _ in range(min(start_step, args.max_steps - 1)):
+                    sched.step()
+            log0(f"resumed from {path} at step {start_step}")
+
+    tag = "vanilla" if args.use_vallina_impl else f"TP-{p.tp_rank}"
+    n = start_step
+    accum = torch.zeros((), device=dev, dtype=torch.float64)
+    accum_host = 0.0
+    t_last, n_last = time.time(), n
+    max_epoch = math.ceil(max(1, args.max_steps - n) / max(1, len(loader)))
+    flops_tok = margs.flops_per_token(seq_len)
+    dist.barrier()
+    done = False
+    for epoch in range(max_epoch):
+        for batch in loader:
+            ids = batch["input_ids"].to(dev, non_blocking=True)
+            tgt = batch["target_ids"].to(dev, non_blocking=True)
+            pos = batch["position_ids"].to(dev, non_blocking=True)
+            maybe_inject_fault(args.fault_inject_step, n + 1, grank)
+            loss = step_fn(ids, pos, tgt)
+            accum += loss.double()
+            n += 1
+            hb.beat(n)
+            if n % args.log_interval == 0:
+                accum_host += float(accum.item())
+                accum.zero_()
+                avg = accum_host / (n - start_step)
+                lr = opt.param_groups[0]["lr"]
+                now = time.time()
+                tps = ids.numel() * (n - n_last) * p.dp_size / (now - t_last)
+                t_last, n_last = now, n
+                mem = torch.cuda.memory_reserved(dev) / 1024 ** 3 if use_cuda else 0.0
+                log0(f"[{tag}] Step {n}/{args.max_steps} -> Avg Loss {avg:.4f}, Lr {lr:.8f}, "
+                     f"{tps:,.0f} tok/s, {tps * flops_tok / p.world_size / 1e12:.1f} TFLOP/s/GPU")
+                if writer is not None:
+                    writer.add_scalar("train/ce_loss", avg, n)
+                    writer.add_scalar("train/lr", lr, n)
+                    writer.add_scalar(f"used_gpu_memory/tprank-{p.tp_rank}", mem, n)
+                    writer.add_scalar("throughput/tokens_per_s", tps, n)
+                    writer.flush()
+            if n % args.save_interval == 0:
+                accum_host += float(accum.item())
+                accum.zero_()
+                avg = accum_host / (n - start_step)
+                if p.dp_rank == 0:
+                    path = ck.save_checkpoint(model, args.save_dir, p.tp_rank, n, avg, opt, sched,
+                                              keep_last_n=args.reserv_last_n_ckpts)
+                    print(f"[TP rank {p.tp_rank}]: Model saved to {path}", flush=True)
+                dist.barrier()
+            if n >= args.max_steps:
+                done = True
+                break
+        log0(f"Epoch {epoch + 1}/{max_epoch} finished.")
+        if done:
+            break
+    log0(f"Training finished (total steps: {n}).")
+    if writer is not None:
+        writer.close()
+    hb.stop()
+    dist.barrier()
+    destroy_dist_env()
+
+
+def main(argv=None):
+    args = get_train_args(argv)
+    if "WORLD_SIZE" in os.environ and "RANK" in os.environ:
+        train(None, args)   # torchrun: one process per GPU already
+        return
+    import torch.multiprocessing as mp
+    os.environ.setdefault("MASTER_ADDR", args.master_addr)
+    mp.spawn(train, args=(args,), nprocs=args.tp_size * args.dp_size, join=True)
+
+
+if __name__ == "__main__":
+    main()
