@@ -34,7 +34,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 # Per-GPU throughput of the reference formulation on MI355X at TP=1 (bench.py --impl reference,
-# gpt2-small, seq 1024, batch 16); see BASELINE.md.  None until measured.
+# gpt2-small, seq 1024, batch 32); see BASELINE.md.  None until measured.
 REFERENCE_TOKENS_PER_S_TP1 = None
 
 
@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="gpt2-small")
     ap.add_argument("--seq-len", type=int, default=1024)
-    ap.add_argument("--batch-per-gpu", type=int, default=16)
+    ap.add_argument("--batch-per-gpu", type=int, default=32)
     ap.add_argument("--global-batch", type=int, default=None, help="override (strong scaling)")
     ap.add_argument("--sp", action="store_true", help="Megatron sequence parallelism")
     ap.add_argument("--impl", choices=["ours", "reference"], default="ours")

@@ -1,0 +1,302 @@
+"""Explicit-schedule forward/backward of the whole TP decoder (the training fast path).
+
+``Transformer.loss()`` runs through :class:`DecoderTrainFn`: one autograd Function whose
+forward and hand-written backward call the kernel API directly (``ops.dispatch.K``: HIP
+kernels on MI355X, the PyTorch oracle on CPU) in an explicit order.  Same math as the modular
+layers (``parallel/layers.py``; the CPU/gloo equivalence tests run this path), but:
+
+* **comm/compute overlap by ping-pong chunks.**  With TP > 1 the batch is split into
+  ``chunks`` halves.  Every tensor-parallel all-reduce (row-parallel outputs in forward,
+  column-parallel input-grads in backward) is launched ``async_op=True`` (RCCL runs on its own
+  HIP stream) and waited only by the *next* segment of the *same* half, after the other half's
+  segment has been enqueued on the compute stream:
+
+      fwd  seg1(A) seg1(B) seg2(A)* seg2(B)* ...     seg1 = norm1,QKV,RoPE,attn,Wo -> AR
+                                                     seg2 = *wait+bias+residual, norm2,
+                                                            gate|up, SwiGLU, down -> AR
+      bwd  b2(A) b2(B) b1(A)* b1(B)* ...             b2 = down/SwiGLU/gate|up grads -> AR(dh2)
+                                                     b1 = *wait, norm2 bwd, Wo/attn/QKV grads
+                                                          -> AR(dh)
+
+  so each all-reduce is hidden behind the other half's GEMMs / attention (the reference issues
+  every collective synchronously).  Inside a segment the weight-gradient GEMMs
+  are issued after the all-reduce launch, so they overlap it too.
+* fp32 weight-gradient accumulation across chunks inside the wgrad GEMM epilogue/reduce,
+  norm/bias gradients from deterministic reductions (replicated params stay bitwise identical
+  across TP ranks).
+* bias + residual add fused in one kernel after the all-reduce; the logits all-gather is
+  replaced by the vocab-parallel cross-entropy (one (M,3) stats all-gather per chunk).
+* activations saved per chunk: x, normed inputs, roped QKV, attention output + LSE, gate|up,
+  SwiGLU output — no (B,H,T,T) tensors.
+
+Supported: RMSNorm blocks without sequence parallelism (the reference architecture and all
+presets).  ``ModelArgs.sequence_parallel`` / LayerNorm models use the modular autograd path.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops.dispatch import K, shadow
+from ..parallel import process_manager as pm
+
+
+def _ar(t: torch.Tensor):
+    p = pm.pgm
+    if p is None or p.tp_size == 1:
+        return None
+    return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=p.tp_group, async_op=True)
+
+
+def _wait(h):
+    if h is not None:
+        h.wait()
+
+
+def _addg(acc, g):
+    if g is None:
+        return acc
+    if acc is None:
+        return g.float().clone() if g.dtype != torch.float32 else g.clone()
+    return acc.add_(g)
+
+
+class _Layer:
+    """Parameter views of one DecoderLayer."""
+
+    def __init__(self, layer):
+        a, f = layer.attn, layer.ffn
+        self.s1, self.s2 = layer.norm1.scale, layer.norm2.scale
+        self.eps1, self.eps2 = layer.norm1.eps, layer.norm2.eps
+        self.wqkv, self.bqkv = a.wqkv.weight, a.wqkv.bias
+        self.wo, self.bo = a.wo.weight, a.wo.bias
+        self.wgu, self.bgu = f.gate_up.weight, f.gate_up.bias
+        self.wd, self.bd = f.down_proj.weight, f.down_proj.bias
+        self.h, self.hd = a.num_local_heads, a.head_dim
+
+    def params(self):
+        return [self.s1, self.wqkv, self.bqkv, self.wo, self.bo, self.s2, self.wgu, self.bgu, self.wd, self.bd]
+
+
+def collect_params(model) -> List[Optional[torch.Tensor]]:
+    ps = [model.embedding.weight]
+    for layer in model.layers:
+        ps += _Layer(layer).params()
+    ps += [model.norm.scale, model.lm_head.weight, model.lm_head.bias]
+    return ps
+
+
+class DecoderTrainFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, model, ids, pos, tgt, chunks: int, ignore_index: int, *params):
+        dev = ids.device
+        dt = model.act_dtype(dev)
+        k = K(model.embedding.weight)
+        p = pm.pgm
+        tp = 1 if p is None else p.tp_size
+        B, T = ids.shape
+        C = max(1, min(chunks, B))
+        bounds = [(B * i) // C for i in range(C + 1)]
+        layers = [_Layer(l) for l in model.layers]
+        tab = model.rope_table(dev)
+        emb = model.embedding
+        head = model.lm_head
+        vst = head.odim_start
+        vvalid = max(0, min(model.vocab_size - vst, head.odim_partition))
+        d = model.args.attn_dim
+
+        W = lambda w: shadow(w, dt) if w is not None else None  # bf16 compute copies
+        st = []  # per-chunk saved state
+        for c in range(C):
+            b0, b1 = bounds[c], bounds[c + 1]
+            ids_c = ids[b0:b1].reshape(-1).contiguous()
+            x = k.embedding_fwd(ids_c, emb.weight, emb.vocab_st_idx, dt)
+            st.append(dict(B=b1 - b0, ids=ids_c, pos=pos[b0:b1].reshape(-1).contiguous(),
+                           tgt=tgt[b0:b1].reshape(-1).contiguous(), x=x, h=_ar(x), pend=None,
+                           pend_bias=None, layers=[]))
+        for li, L in enumerate(layers):
+            # seg1: (wait + residual), norm1, QKV, RoPE, attention, Wo -> async all-reduce
+            for s in st:
+                if s["pend"] is not None:
+                    _wait(s["h"])
+                    s["x"] = k.bias_residual(s["pend"], s["pend_bias"], s["x"])
+                else:
+                    _wait(s["h"])
+                x = s["x"]
+                h1, r1 = k.rmsnorm_fwd(x, L.s1, L.eps1)
+                qkv = k.gemm_nt(h1, W(L.wqkv), L.bqkv)
+                Mc = x.size(0)
+                Bc = s["B"]
+                k.rope_(qkv, s["pos"], tab, 2 * L.h, L.hd, False)
+                q, kk, v = _split(qkv, Bc, T, L.h, L.hd)
+                o, lse = k.attn_fwd(q, kk, v, 1.0 / math.sqrt(L.hd), True)
+                o2 = o.view(Mc, L.h * L.hd)
+                pout = k.gemm_nt(o2, W(L.wo), None)
+                s["layers"].append(dict(x=x, r1=r1, h1=h1, qkv=qkv, o=o, lse=lse))
+                s["pend"], s["pend_bias"], s["h"] = pout, L.bo, _ar(pout)
+            # seg2: wait + bias + residual, norm2, gate|up, SwiGLU, down -> async all-reduce
+            for s in st:
+                _wait(s["h"])
+                x2 = k.bias_residual(s["pend"], s["pend_bias"], s["x"])
+                h2, r2 = k.rmsnorm_fwd(x2, L.s2, L.eps2)
+                gu = k.gemm_nt(h2, W(L.wgu), L.bgu)
+                sw = k.swiglu_fwd(gu)
+                qout = k.gemm_nt(sw, W(L.wd), None)
+                s["layers"][-1].update(x2=x2, r2=r2, h2=h2, gu=gu, sw=sw)
+                s["x"] = x2
+                s["pend"], s["pend_bias"], s["h"] = qout, L.bd, _ar(qout)
+        # head: residual, final norm, lm_head shard, vocab-parallel CE statistics
+        losses_sum = torch.zeros((), device=dev, dtype=torch.float32)
+        n_valid_total = torch.zeros((), device=dev, dtype=torch.float32)
+        for s in st:
+            _wait(s["h"])
+            xf = k.bias_residual(s["pend"], s["pend_bias"], s["x"])
+            hf, rf = k.rmsnorm_fwd(xf, model.norm.scale, model.norm.eps)
+            logits = k.gemm_nt(hf, W(head.weight), head.bias)
+            stats = k.ce_fwd_stats(logits, s["tgt"], vst, vvalid)
+            if tp > 1:
+                allst = stats.new_empty((tp * stats.size(0), 3))
+                dist.all_gather_into_tensor(allst, stats, group=p.tp_group)
+                allst = allst.view(tp, -1, 3)
+            else:
+                allst = stats.unsqueeze(0)
+            mx = allst[..., 0].amax(0)
+            lse = mx + torch.log((allst[..., 1] * torch.exp(allst[..., 0] - mx)).sum(0))
+            tl = allst[..., 2].sum(0)
+            valid = s["tgt"] != ignore_index
+            losses_sum = losses_sum + torch.where(valid, lse - tl, torch.zeros_like(lse)).sum()
+            n_valid_total = n_valid_total + valid.sum()
+            s.update(xf=xf, hf=hf, rf=rf, logits=logits, ce_lse=lse, valid=valid)
+            del s["pend"], s["h"]
+        n_valid_total = n_valid_total.clamp_min(1.0)
+        loss = losses_sum / n_valid_total
+        ctx.model, ctx.st, ctx.layers, ctx.meta = model, st, layers, (T, dt, vst, vvalid, C, d)
+        ctx.n_valid = n_valid_total
+        ctx.nparams = len(params)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        model, st, layers = ctx.model, ctx.st, ctx.layers
+        T, dt, vst, vvalid, C, d = ctx.meta
+        k = K(model.embedding.weight)
+        head = model.lm_head
+        W = lambda w: shadow(w, dt) if w is not None else None
+        gscale_all = (gloss.float() / ctx.n_valid)
+        nL = len(layers)
+        # fp32 grad accumulators
+        g = {"emb": None, "nf": None, "lm_w": None, "lm_b": None}
+        gl = [dict() for _ in range(nL)]
+
+        def tn(key_dict, key, dy, x):
+            acc = key_dict.get(key)
+            if acc is None:
+                key_dict[key] = k.gemm_tn(dy, x)
+            else:
+                k.gemm_tn(dy, x, acc, True)
+
+        def bias_acc(key_dict, key, dy, present):
+            if present is None:
+                return
+            key_dict[key] = _addg(key_dict.get(key), k.bias_grad(dy))
+
+        # ---- head: CE backward in place over the logits, lm_head dgrad -> async AR
+        for s in st:
+            gs = s["valid"].float() * gscale_all
+            dl = s["logits"]
+            k.ce_bwd(dl, s["tgt"], s["ce_lse"], gs, vst, vvalid, dl)
+            dh = k.gemm_nn(dl, W(head.weight))
+            s["bh"] = _ar(dh)
+            s["dpend"] = dh
+            tn(g, "lm_w", dl, s["hf"])
+            if head.bias is not None:
+                g["lm_b"] = _addg(g["lm_b"], k.bias_grad(dl))
+            del s["logits"]
+        for s in st:
+            _wait(s["bh"])
+            dxf, dsf = k.rmsnorm_bwd(s["dpend"], s["xf"], model.norm.scale, s["rf"])
+            g["nf"] = _addg(g["nf"], dsf)
+            s["g"] = dxf            # grad wrt the last layer's output (residual stream)
+            s["dpend"] = None
+            del s["xf"], s["hf"]
+        # ---- layers, reversed
+        for li in range(nL - 1, -1, -1):
+            L, G = layers[li], gl[li]
+            # b2: down / SwiGLU / gate|up grads -> AR(dh2)
+            for s in st:
+                if s["dpend"] is not None:     # finish the upper layer: wait, norm1 bwd, residual
+                    _finish_norm1(k, s, layers[li + 1], gl[li + 1], li + 1)
+                a = s["layers"][li]
+                gq = s["g"]
+                bias_acc(G, "bd", gq, L.bd)
+                ds = k.gemm_nn(gq, W(L.wd))
+                tn(G, "wd", gq, a["sw"])
+                dgu = k.swiglu_bwd(ds, a["gu"])
+                dh2 = k.gemm_nn(dgu, W(L.wgu))
+                s["bh"], s["dpend"] = _ar(dh2), dh2
+                tn(G, "wgu", dgu, a["h2"])
+                bias_acc(G, "bgu", dgu, L.bgu)
+                del a["sw"], a["gu"]
+            # b1: wait, norm2 bwd, Wo / attention / QKV grads -> AR(dh)
+            for s in st:
+                a = s["layers"][li]
+                _wait(s["bh"])
+                dx2n, ds2 = k.rmsnorm_bwd(s["dpend"], a["x2"], L.s2, a["r2"])
+                G["s2"] = _addg(G.get("s2"), ds2)
+                g2 = s["g"].add_(dx2n) if s["g"].dtype == dx2n.dtype else s["g"] + dx2n
+                bias_acc(G, "bo", g2, L.bo)
+                do = k.gemm_nn(g2, W(L.wo))
+                tn(G, "wo", g2, a["o"].view(g2.size(0), -1))
+                Bc = s["B"]
+                q, kk, v = _split(a["qkv"], Bc, T, L.h, L.hd)
+                dqkv = torch.empty_like(a["qkv"])
+                dq, dk, dv = _split(dqkv, Bc, T, L.h, L.hd)
+                k.attn_bwd(do.view(Bc, T, L.h, L.hd), q, kk, v, a["o"], a["lse"], 1.0 / math.sqrt(L.hd), True,
+                           dq, dk, dv)
+                k.rope_(dqkv, s["pos"], model.rope_table(dqkv.device), 2 * L.h, L.hd, True)
+                dh = k.gemm_nn(dqkv, W(L.wqkv))
+                s["bh"], s["dpend"] = _ar(dh), dh
+                tn(G, "wqkv", dqkv, a["h1"])
+                bias_acc(G, "bqkv", dqkv, L.bqkv)
+                s["g"] = g2
+                for key in ("x2", "r2", "h2", "qkv", "o", "lse"):
+                    a.pop(key, None)
+        for s in st:
+            _finish_norm1(k, s, layers[0], gl[0], 0)
+            dwe = k.embedding_bwd(s["g"], s["ids"], model.embedding.weight.size(0), model.embedding.vocab_st_idx)
+            g["emb"] = _addg(g["emb"], dwe)
+        ctx.st = None
+        grads = [g["emb"]]
+        for li, L in enumerate(layers):
+            G = gl[li]
+            grads += [G.get("s1"), G.get("wqkv"), G.get("bqkv") if L.bqkv is not None else None,
+                      G.get("wo"), G.get("bo") if L.bo is not None else None, G.get("s2"), G.get("wgu"),
+                      G.get("bgu") if L.bgu is not None else None, G.get("wd"),
+                      G.get("bd") if L.bd is not None else None]
+        grads += [g["nf"], g["lm_w"], g["lm_b"] if head.bias is not None else None]
+        return (None, None, None, None, None, None) + tuple(grads)
+
+
+def _finish_norm1(k, s, L, G, li):
+    """Wait for the all-reduce of layer li's norm1 input-grad, run the norm1 backward and add
+    it to the residual-stream grad (-> grad wrt layer li's input)."""
+    a = s["layers"][li]
+    _wait(s["bh"])
+    dxn, ds1 = k.rmsnorm_bwd(s["dpend"], a["x"], L.s1, a["r1"])
+    G["s1"] = _addg(G.get("s1"), ds1)
+    s["g"] = s["g"].add_(dxn)
+    s["dpend"] = None
+    for key in ("x", "r1", "h1"):
+        a.pop(key, None)
+
+
+def _split(qkv, B, T, h, hd):
+    q = qkv[:, : h * hd].view(B, T, h, hd)
+    k = qkv[:, h * hd: 2 * h * hd].view(B, T, h, hd)
+    v = qkv[:, 2 * h * hd: 3 * h * hd].view(B, T, h, hd)
+    return q, k, v
+
+

@@ -151,6 +151,8 @@ class Transformer(nn.Module):
                                             gather_output=False, sizes=vsizes, sequence_parallel=sp)
         self.compute_dtype: Optional[torch.dtype] = None
         self._rope = {}
+        self.use_fused_engine = True   # explicit-schedule fast path for loss()
+        self.chunks: Optional[int] = None  # ping-pong chunks (default: 2 when TP > 1)
 
     @classmethod
     def from_args(cls, args: ModelArgs) -> "Transformer":
@@ -227,9 +229,27 @@ class Transformer(nn.Module):
         logits = comm_ops.Gather.apply(logits, self.lm_head.sizes)
         return logits[..., : self.vocab_size].reshape(B, T, self.vocab_size)
 
+    def fused_supported(self) -> bool:
+        return (not self.args.sequence_parallel) and self.args.norm == "rmsnorm" and self.use_fused_engine
+
+    def overlap_chunks(self) -> int:
+        p = pm.pgm
+        if self.chunks is not None:
+            return self.chunks
+        return 2 if (p is not None and p.tp_size > 1) else 1
+
     def loss(self, input_ids: torch.Tensor, position_ids: torch.Tensor, target_ids: torch.Tensor,
              ignore_index: int = IGNORE_INDEX) -> torch.Tensor:
-        """Mean next-token CE via the vocab-parallel cross-entropy (no logits all-gather)."""
+        """Mean next-token CE via the vocab-parallel cross-entropy (no logits all-gather).
+
+        Runs the explicit-schedule engine (``models/fused_engine.py``: ping-pong chunks with
+        all-reduces overlapped by the other chunk's compute) when supported, else the modular
+        autograd path."""
+        if self.fused_supported():
+            from .fused_engine import DecoderTrainFn, collect_params
+            assert input_ids.size(1) <= self.args.maxlen
+            return DecoderTrainFn.apply(self, input_ids, position_ids, target_ids.reshape(input_ids.shape),
+                                        self.overlap_chunks(), ignore_index, *collect_params(self))
         h, B, T = self._trunk(input_ids, position_ids)
         logits = self._lm_head_local(h)
         st = self.lm_head.odim_start

@@ -59,6 +59,14 @@ def add_bias_(y: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
     return y
 
 
+def bias_residual(y: torch.Tensor, bias: Optional[torch.Tensor], residual: torch.Tensor) -> torch.Tensor:
+    """out = residual + y (+ bias), fp32 math, rounded once to y.dtype."""
+    out = y.float() + residual.float()
+    if bias is not None:
+        out = out + bias.float()
+    return out.to(y.dtype)
+
+
 def bias_grad(dy: torch.Tensor) -> torch.Tensor:
     """fp32 column sums of dy[M,N]."""
     return dy.float().sum(0)
