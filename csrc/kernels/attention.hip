@@ -16,8 +16,9 @@
 //    the CDNA4 transpose read ds_read_b64_tr_b16) — P never touches LDS.
 //  * dK/dV compute S = Q K^T with the block's keys held in registers; P^T/dS^T are then
 //    the A operands of dV = P^T dO and dK = dS^T Q without data movement.
-//  * backward = preprocess (delta = rowsum(dO*O)) + a dK/dV kernel (one block per 64 keys)
-//    + a dQ kernel (one block per 128 queries): no float atomics, bitwise deterministic.
+//  * backward = a dQ kernel (one block per 128 queries; it also computes and stores
+//    delta = rowsum(dO*O)) then a dK/dV kernel (one block per 64 keys): no float atomics,
+//    bitwise deterministic.
 //  * every LDS tile [rows][hd] uses one XOR swizzle that is conflict-free both for row
 //    reads (ds_read_b128) and for transposed reads (ds_read_b64_tr_b16).
 //  * causal: key tiles above the diagonal are never visited; heaviest q-blocks launch first.
@@ -182,33 +183,40 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd_k(const bf16*
         }
       }
       // Online softmax per query column (lane-local + butterfly over the 4 lane groups).
+      // The causal / tail mask is evaluated only on tiles that need it (wave-uniform), the
+      // 1/sqrt(hd)*log2(e) scale is folded into the exp2 argument with one FMA, and every
+      // visited tile has >= 1 valid key per query (key kv0 <= wq0), so no -inf guards.
+      const bool need_mask = (causal && kv0 + BKV - 1 > wq0) || (kv0 + BKV > T);
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int qi = wq0 + 16 * c + (l & 15);
-        float mx = -INFINITY;
+        if (need_mask) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int ki = kv0 + 16 * i + 4 * g + j;
+              if (ki >= T || (causal && ki > qi)) s[i][c][j] = -INFINITY;
+            }
+        }
+        float mx = s[0][c][0];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int ki = kv0 + 16 * i + 4 * g + j;
-            float v = s[i][c][j] * c2;
-            if (ki >= T || (causal && ki > qi)) v = -INFINITY;
-            s[i][c][j] = v;
-            mx = fmaxf(mx, v);
-          }
+          for (int j = 0; j < 4; ++j) mx = fmaxf(mx, s[i][c][j]);
         mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mnew = fmaxf(m[c], mx);
-        const float alpha = (mnew == -INFINITY) ? 1.f : exp2f(m[c] - mnew);
+        const float mnew = fmaxf(m[c], mx * c2);
+        const float alpha = exp2f(m[c] - mnew);
         m[c] = mnew;
         float ps = 0.f;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float p = (mnew == -INFINITY) ? 0.f : exp2f(s[i][c][j] - mnew);
-            s[i][c][j] = p;
-            ps += p;
+            const float pv = exp2f(fmaf(s[i][c][j], c2, -mnew));
+            s[i][c][j] = pv;
+            ps += pv;
           }
         lsum[c] = lsum[c] * alpha + ps;
 #pragma unroll
@@ -377,16 +385,20 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv_k(const 
         }
       }
       const int ki = wk0 + (l & 15);
+      const bool need_mask = (causal && wk0 + 15 > qq0) || (qq0 + BQ > T) || (wk0 + 16 > T);
 #pragma unroll
       for (int qt = 0; qt < 4; ++qt) {
+        const f32x4 lsv = *reinterpret_cast<const f32x4*>(ls + 16 * qt + 4 * g);
+        const f32x4 dsv = *reinterpret_cast<const f32x4*>(ds + 16 * qt + 4 * g);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int qr = 16 * qt + 4 * g + j;
-          const int qi = qq0 + qr;
-          float p = exp2f(s[qt][j] * c2 - ls[qr]);
-          if (qi >= T || ki >= T || (causal && ki > qi)) p = 0.f;
+          float p = exp2f(fmaf(s[qt][j], c2, -lsv[j]));
+          if (need_mask) {
+            const int qi = qq0 + 16 * qt + 4 * g + j;
+            if (qi >= T || ki >= T || (causal && ki > qi)) p = 0.f;
+          }
           s[qt][j] = p;
-          dp[qt][j] = p * (dp[qt][j] - ds[qr]);
+          dp[qt][j] = p * (dp[qt][j] - dsv[j]);
         }
       }
       // dV[k][d] += P^T dO ;  dK[k][d] += dS^T Q
@@ -429,10 +441,11 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv_k(const 
 template <int HD>
 __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                         const bf16* __restrict__ V, const bf16* __restrict__ dO,
-                                                        const float* __restrict__ LSE,
-                                                        const float* __restrict__ DELTA, bf16* __restrict__ dQ, int T,
+                                                        const bf16* __restrict__ Og, const float* __restrict__ LSE,
+                                                        float* __restrict__ DELTA_OUT, bf16* __restrict__ dQ, int T,
                                                         int H, long long ldq, long long ldk, long long ldv,
-                                                        long long lddo, long long lddq, float scale, int causal) {
+                                                        long long lddo, long long ldo, long long lddq, float scale,
+                                                        int causal) {
   constexpr int BQ = 128, BKV = 64, KT = HD / 32, DT = HD / 16;
   constexpr int TILE = BKV * HD * 2;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
@@ -463,7 +476,21 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
       dof[c][kk] = d;
     }
     lse2[c] = qi < T ? LSE[((long long)b * H + h) * T + qi] * kLog2e : 0.f;
-    del[c] = qi < T ? DELTA[((long long)b * H + h) * T + qi] : 0.f;
+    // delta = rowsum(dO * O), fused here (written for the dK/dV kernel that runs next).
+    float dsum = 0.f;
+    if (qi < T) {
+#pragma unroll
+      for (int kk = 0; kk < KT; ++kk) {
+        const bf16x8 ov = *reinterpret_cast<const bf16x8*>(Og + ((long long)b * T + qi) * ldo + (long long)h * HD +
+                                                           32 * kk + 8 * g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dsum += (float)dof[c][kk][j] * (float)ov[j];
+      }
+    }
+    dsum += __shfl_xor(dsum, 16, 64);
+    dsum += __shfl_xor(dsum, 32, 64);
+    del[c] = dsum;
+    if (g == 0 && qi < T) DELTA_OUT[((long long)b * H + h) * T + qi] = dsum;
   }
   f32x4 dq[2][DT];
 #pragma unroll
@@ -512,6 +539,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
           }
         }
       }
+      const bool need_mask = (causal && kv0 + BKV - 1 > wq0) || (kv0 + BKV > T);
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int qi = wq0 + 16 * c + (l & 15);
@@ -519,9 +547,11 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const int ki = kv0 + 16 * i + 4 * g + j;
-            float p = exp2f(s[i][c][j] * c2 - lse2[c]);
-            if (ki >= T || qi >= T || (causal && ki > qi)) p = 0.f;
+            float p = exp2f(fmaf(s[i][c][j], c2, -lse2[c]));
+            if (need_mask) {
+              const int ki = kv0 + 16 * i + 4 * g + j;
+              if (ki >= T || (causal && ki > qi)) p = 0.f;
+            }
             s[i][c][j] = p * (dp[i][c][j] - del[c]);  // dS^T
           }
       }
@@ -587,15 +617,12 @@ extern "C" void dpfs_attn_bwd(const void* dout, const void* q, const void* k, co
                               int hd, long long lddo, long long ldq, long long ldk, long long ldv, long long ldo,
                               long long lddq, long long lddk, long long lddv, float scale, int causal,
                               hipStream_t s) {
-  const long long rows = (long long)B * T * H;
-  DPFS_HD_DISPATCH(hd, attn_bwd_delta_k<HD_><<<(unsigned)((rows + 3) / 4), 256, 0, s>>>(
-                           (const bf16*)dout, (const bf16*)o, delta, B, T, H, lddo, ldo));
+  dim3 gq((T + 127) / 128, B * H);
+  DPFS_HD_DISPATCH(hd, attn_bwd_dq_k<HD_><<<gq, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
+                                                             (const bf16*)dout, (const bf16*)o, lse, delta, (bf16*)dq,
+                                                             T, H, ldq, ldk, ldv, lddo, ldo, lddq, scale, causal));
   dim3 gk((T + 63) / 64, B * H);
   DPFS_HD_DISPATCH(hd, attn_bwd_dkdv_k<HD_><<<gk, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
                                                                (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv, T,
                                                                H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal));
-  dim3 gq((T + 127) / 128, B * H);
-  DPFS_HD_DISPATCH(hd, attn_bwd_dq_k<HD_><<<gq, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
-                                                             (const bf16*)dout, lse, delta, (bf16*)dq, T, H, ldq, ldk,
-                                                             ldv, lddo, lddq, scale, causal));
 }
