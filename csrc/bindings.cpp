@@ -18,6 +18,9 @@ void dpfs_gemm_nt(const void*, const void*, void*, const float*, int, int, int, 
 void dpfs_gemm_nn(const void*, const void*, void*, int, int, int, int, int, int, hipStream_t);
 int dpfs_gemm_tn_splits(int, int, int);
 void dpfs_gemm_set_impl(int);
+int dpfs_gemm_rope_fusable(int, int, int, int);
+void dpfs_gemm_nt_rope(const void*, const void*, void*, const float*, int, int, int, int, int, int, const int64_t*,
+                       const float*, int, hipStream_t);
 void dpfs_gemm_force(int, int);
 void dpfs_gemm_set_workspace(float*, long long);
 long long dpfs_gemm_bf16_ws(int, int, int);
@@ -26,10 +29,15 @@ void dpfs_rmsnorm_fwd(int, const void*, const float*, void*, float*, int, int, f
 void dpfs_layernorm_fwd(int, const void*, const float*, const float*, void*, float*, float*, int, int, float,
                         hipStream_t);
 int dpfs_norm_bwd_grid(int);
-void dpfs_norm_bwd(int, int, const void*, const void*, const float*, const float*, const float*, void*, float*, float*,
-                   float*, float*, int, int, hipStream_t);
+void dpfs_norm_bwd(int, int, const void*, const void*, const float*, const float*, const float*, const void*, void*,
+                   float*, float*, float*, float*, int, int, hipStream_t);
 void dpfs_swiglu_fwd(int, const void*, void*, int, int, hipStream_t);
 void dpfs_swiglu_bwd(int, const void*, const void*, void*, int, int, hipStream_t);
+long long dpfs_swiglu_bwd_dbias_ws(int, int);
+void dpfs_swiglu_bwd_dbias(int, const void*, const void*, void*, float*, float*, int, int, hipStream_t);
+long long dpfs_ce_bwd_dbias_ws(int, int, int);
+void dpfs_ce_bwd_dbias(int, const void*, const int64_t*, const float*, const float*, void*, float*, float*, int, int,
+                       long long, int, hipStream_t);
 void dpfs_rope(int, void*, const int64_t*, const float*, int, int, int, int, int, hipStream_t);
 void dpfs_bias_residual(int, const void*, const float*, const void*, void*, int, int, hipStream_t);
 long long dpfs_colsum_ws(int, int);
@@ -50,7 +58,7 @@ void dpfs_attn_fwd(const void*, const void*, const void*, void*, float*, int, in
                    long long, long long, float, int, hipStream_t);
 void dpfs_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, float*, void*, void*,
                    void*, int, int, int, int, long long, long long, long long, long long, long long, long long,
-                   long long, long long, float, int, hipStream_t);
+                   long long, long long, float, int, const int64_t*, const float*, hipStream_t);
 }
 
 namespace {
@@ -83,7 +91,12 @@ const float* opt_f32(const c10::optional<torch::Tensor>& t, int64_t n, const cha
 }
 
 // -------------------------------------------------------------------------------- GEMM --
-torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> bias) {
+torch::Tensor rope_(torch::Tensor qkv, torch::Tensor positions, torch::Tensor table, int64_t n_rot_heads,
+                    int64_t head_dim, bool inverse);
+
+torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> bias,
+                      c10::optional<torch::Tensor> rope_pos, c10::optional<torch::Tensor> rope_tab,
+                      int64_t rope_heads, int64_t rope_hd) {
   check_rowmajor(a, "a");
   check_rowmajor(b, "b");
   TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "gemm_nt: bf16 operands");
@@ -101,8 +114,21 @@ torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
   torch::Tensor ws;
   if (wsn > 0) ws = torch::empty({wsn}, a.options().dtype(torch::kFloat32));
   dpfs_gemm_set_workspace(wsn > 0 ? ws.data_ptr<float>() : nullptr, wsn);
-  dpfs_gemm_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), opt_f32(bias, N, "bias"), (int)M, (int)N, (int)K,
-               (int)a.stride(0), (int)b.stride(0), (int)N, stream());
+  const bool want_rope = rope_pos.has_value() && rope_pos->defined() && rope_heads > 0;
+  if (want_rope && dpfs_gemm_rope_fusable((int)M, (int)N, (int)K, (int)rope_hd)) {
+    TORCH_CHECK(rope_pos->scalar_type() == torch::kInt64 && rope_pos->is_contiguous() && rope_pos->numel() == M,
+                "gemm_nt: rope_pos must be contiguous int64 [M]");
+    TORCH_CHECK(rope_tab.has_value() && rope_tab->scalar_type() == torch::kFloat32 && rope_tab->is_contiguous() &&
+                    rope_tab->size(1) == rope_hd,
+                "gemm_nt: rope_tab must be fp32 [maxlen, hd]");
+    dpfs_gemm_nt_rope(a.data_ptr(), b.data_ptr(), c.data_ptr(), opt_f32(bias, N, "bias"), (int)M, (int)N, (int)K,
+                      (int)a.stride(0), (int)b.stride(0), (int)N, rope_pos->data_ptr<int64_t>(),
+                      rope_tab->data_ptr<float>(), (int)(rope_heads * rope_hd), stream());
+  } else {
+    dpfs_gemm_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), opt_f32(bias, N, "bias"), (int)M, (int)N, (int)K,
+                 (int)a.stride(0), (int)b.stride(0), (int)N, stream());
+    if (want_rope) rope_(c, *rope_pos, *rope_tab, rope_heads, rope_hd, false);
+  }
   dpfs_gemm_set_workspace(nullptr, 0);
   return c;
 }
@@ -226,16 +252,23 @@ std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, torch::Tensor w, double 
   return {y, rstd};
 }
 
-std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor rstd) {
+std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor rstd,
+                                       c10::optional<torch::Tensor> dres) {
   const int dt = check_norm_x(x, w);
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.is_contiguous() && dy.scalar_type() == x.scalar_type(), "rmsnorm_bwd: dy");
+  const void* rp = nullptr;
+  if (dres.has_value() && dres->defined()) {
+    TORCH_CHECK(dres->sizes() == x.sizes() && dres->is_contiguous() && dres->scalar_type() == x.scalar_type(),
+                "rmsnorm_bwd: dres must match x");
+    rp = dres->data_ptr();
+  }
   const at::DeviceGuard g(x.device());
   const int64_t M = x.size(0), D = x.size(1);
   auto dx = torch::empty_like(x);
   auto dw = torch::empty({D}, w.options());
   if (M == 0) return {dx, dw.zero_()};
   auto ws = torch::empty({(int64_t)dpfs_norm_bwd_ws(0, (int)M, (int)D)}, w.options());
-  dpfs_norm_bwd(0, dt, dy.data_ptr(), x.data_ptr(), w.data_ptr<float>(), nullptr, rstd.data_ptr<float>(), dx.data_ptr(),
+  dpfs_norm_bwd(0, dt, dy.data_ptr(), x.data_ptr(), w.data_ptr<float>(), nullptr, rstd.data_ptr<float>(), rp, dx.data_ptr(),
                 dw.data_ptr<float>(), nullptr, ws.data_ptr<float>(), nullptr, (int)M, (int)D, stream());
   return {dx, dw};
 }
@@ -267,7 +300,7 @@ std::vector<torch::Tensor> layernorm_bwd(torch::Tensor dy, torch::Tensor x, torc
   const int64_t G = dpfs_norm_bwd_grid((int)M);
   auto ws = torch::empty({(int64_t)dpfs_norm_bwd_ws(1, (int)M, (int)D)}, w.options());
   dpfs_norm_bwd(1, dt, dy.data_ptr(), x.data_ptr(), w.data_ptr<float>(), mean.data_ptr<float>(),
-                rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr<float>(), db.data_ptr<float>(),
+                rstd.data_ptr<float>(), nullptr, dx.data_ptr(), dw.data_ptr<float>(), db.data_ptr<float>(),
                 ws.data_ptr<float>(), ws.data_ptr<float>() + G * D, (int)M, (int)D, stream());
   return {dx, dw, db};
 }
@@ -285,7 +318,16 @@ torch::Tensor swiglu_fwd(torch::Tensor gu) {
   return h;
 }
 
-torch::Tensor swiglu_bwd(torch::Tensor dh, torch::Tensor gu) {
+static float* dbias_out(const c10::optional<torch::Tensor>& db, int64_t n, const char* what) {
+  if (!db.has_value() || !db->defined()) return nullptr;
+  TORCH_CHECK(db->is_cuda() && db->scalar_type() == torch::kFloat32 && db->is_contiguous() && db->numel() == n, what,
+              ": dbias must be contiguous fp32 [", n, "]");
+  return db->data_ptr<float>();
+}
+
+// dgu = SwiGLU'(gu) * dh; with `dbias` the gate|up bias gradient (column sums of dgu) is
+// written there by the same pass.
+torch::Tensor swiglu_bwd(torch::Tensor dh, torch::Tensor gu, c10::optional<torch::Tensor> dbias) {
   check_rowmajor(gu, "gu");
   const int dt = dcode(gu);
   const int64_t M = gu.size(0), F = gu.size(1) / 2;
@@ -294,7 +336,18 @@ torch::Tensor swiglu_bwd(torch::Tensor dh, torch::Tensor gu) {
   TORCH_CHECK(F % (dt == 1 ? 8 : 4) == 0, "swiglu: F must be a multiple of the vector width");
   const at::DeviceGuard g(gu.device());
   auto dgu = torch::empty_like(gu);
-  if (M) dpfs_swiglu_bwd(dt, dh.data_ptr(), gu.data_ptr(), dgu.data_ptr(), (int)M, (int)F, stream());
+  float* db = dbias_out(dbias, 2 * F, "swiglu_bwd");
+  if (db && M == 0) dbias->zero_();
+  if (M == 0) return dgu;
+  if (db) {
+    TORCH_CHECK(gu.is_contiguous(), "swiglu_bwd: gu must be contiguous");
+    const long long wsn = dpfs_swiglu_bwd_dbias_ws((int)M, (int)F);
+    auto ws = torch::empty({std::max<long long>(wsn, 1)}, gu.options().dtype(torch::kFloat32));
+    dpfs_swiglu_bwd_dbias(dt, dh.data_ptr(), gu.data_ptr(), dgu.data_ptr(), db, ws.data_ptr<float>(), (int)M, (int)F,
+                          stream());
+  } else {
+    dpfs_swiglu_bwd(dt, dh.data_ptr(), gu.data_ptr(), dgu.data_ptr(), (int)M, (int)F, stream());
+  }
   return dgu;
 }
 
@@ -346,7 +399,8 @@ std::vector<torch::Tensor> attn_fwd(torch::Tensor q, torch::Tensor k, torch::Ten
 }
 
 void attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Tensor o,
-              torch::Tensor lse, double scale, bool causal, torch::Tensor dq, torch::Tensor dk, torch::Tensor dv) {
+              torch::Tensor lse, double scale, bool causal, torch::Tensor dq, torch::Tensor dk, torch::Tensor dv,
+              c10::optional<torch::Tensor> rope_pos, c10::optional<torch::Tensor> rope_tab) {
   const int64_t B = q.size(0), T = q.size(1), H = q.size(2), hd = q.size(3);
   TORCH_CHECK(dpfs_attn_supported_hd((int)hd), "attn: head_dim not supported");
   auto vq = check_bthd(q, "q", B, T, H, hd), vk = check_bthd(k, "k", B, T, H, hd), vv = check_bthd(v, "v", B, T, H, hd);
@@ -357,10 +411,21 @@ void attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tenso
               "attn_bwd: lse must be contiguous fp32 (B, H, T)");
   const at::DeviceGuard g(q.device());
   if (B * T * H == 0) return;
+  const int64_t* rp = nullptr;
+  const float* rt = nullptr;
+  if (rope_pos.has_value() && rope_pos->defined()) {
+    TORCH_CHECK(rope_pos->scalar_type() == torch::kInt64 && rope_pos->is_contiguous() && rope_pos->numel() == B * T,
+                "attn_bwd: rope_pos must be contiguous int64 [B*T]");
+    TORCH_CHECK(rope_tab.has_value() && rope_tab->scalar_type() == torch::kFloat32 && rope_tab->is_contiguous() &&
+                    rope_tab->dim() == 2 && rope_tab->size(1) == hd,
+                "attn_bwd: rope_tab must be contiguous fp32 [maxlen, hd]");
+    rp = rope_pos->data_ptr<int64_t>();
+    rt = rope_tab->data_ptr<float>();
+  }
   auto delta = torch::empty({B, H, T}, lse.options());
   dpfs_attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
                 delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), (int)B, (int)T, (int)H, (int)hd,
-                vdo.ld, vq.ld, vk.ld, vv.ld, vo.ld, vdq.ld, vdk.ld, vdv.ld, (float)scale, causal ? 1 : 0, stream());
+                vdo.ld, vq.ld, vk.ld, vv.ld, vo.ld, vdq.ld, vdk.ld, vdv.ld, (float)scale, causal ? 1 : 0, rp, rt, stream());
 }
 
 // ------------------------------------------------------------------- embedding / CE --
@@ -409,7 +474,8 @@ torch::Tensor ce_fwd_stats(torch::Tensor logits, torch::Tensor targets, int64_t 
 }
 
 torch::Tensor ce_bwd(torch::Tensor logits, torch::Tensor targets, torch::Tensor lse, torch::Tensor gscale,
-                     int64_t vocab_start, int64_t vocab_valid, torch::Tensor out) {
+                     int64_t vocab_start, int64_t vocab_valid, torch::Tensor out,
+                     c10::optional<torch::Tensor> dbias) {
   check_rowmajor(logits, "logits");
   TORCH_CHECK(logits.is_contiguous() && out.is_contiguous() && out.sizes() == logits.sizes() &&
                   out.scalar_type() == logits.scalar_type(),
@@ -420,8 +486,19 @@ torch::Tensor ce_bwd(torch::Tensor logits, torch::Tensor targets, torch::Tensor 
                   gscale.numel() == M && lse.is_contiguous() && gscale.is_contiguous(),
               "ce_bwd: lse/gscale fp32 [M]");
   const at::DeviceGuard g(logits.device());
-  if (M) dpfs_ce_bwd(dcode(logits), logits.data_ptr(), targets.data_ptr<int64_t>(), lse.data_ptr<float>(),
-                     gscale.data_ptr<float>(), out.data_ptr(), (int)M, (int)V, vocab_start, (int)vocab_valid, stream());
+  float* db = dbias_out(dbias, V, "ce_bwd");
+  if (db && M == 0) dbias->zero_();
+  if (M == 0) return out;
+  if (db) {
+    const long long wsn = dpfs_ce_bwd_dbias_ws(dcode(logits), (int)M, (int)V);
+    auto ws = torch::empty({std::max<long long>(wsn, 1)}, lse.options());
+    dpfs_ce_bwd_dbias(dcode(logits), logits.data_ptr(), targets.data_ptr<int64_t>(), lse.data_ptr<float>(),
+                      gscale.data_ptr<float>(), out.data_ptr(), db, ws.data_ptr<float>(), (int)M, (int)V, vocab_start,
+                      (int)vocab_valid, stream());
+  } else {
+    dpfs_ce_bwd(dcode(logits), logits.data_ptr(), targets.data_ptr<int64_t>(), lse.data_ptr<float>(),
+                gscale.data_ptr<float>(), out.data_ptr(), (int)M, (int)V, vocab_start, (int)vocab_valid, stream());
+  }
   return out;
 }
 
@@ -499,7 +576,9 @@ torch::Tensor grad_sumsq(torch::Tensor desc, torch::Tensor chunks) {
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels of distributed_pytorch_from_scratch_amd";
-  m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("bias") = py::none());
+  m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("bias") = py::none(),
+        py::arg("rope_pos") = py::none(), py::arg("rope_tab") = py::none(), py::arg("rope_heads") = 0,
+        py::arg("rope_hd") = 0);
   m.def("gemm_nn", &gemm_nn);
   m.def("gemm_force", [](int cfg, int splits) { dpfs_gemm_force(cfg, splits); },
         "force the v2 tile config (-1 auto, 0 = 256x256, 1 = 256x128) and K-splits (0 auto)");
@@ -509,19 +588,23 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("add_bias_", &add_bias_);
   m.def("bias_residual", &bias_residual);
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
-  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("rstd"),
+        py::arg("dres") = py::none());
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("swiglu_fwd", &swiglu_fwd);
-  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("swiglu_bwd", &swiglu_bwd, py::arg("dh"), py::arg("gu"), py::arg("dbias") = py::none());
   m.def("rope_", &rope_, py::arg("qkv"), py::arg("positions"), py::arg("table"), py::arg("n_rot_heads"),
         py::arg("head_dim"), py::arg("inverse") = false);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("scale"), py::arg("causal") = true);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
+        py::arg("lse"), py::arg("scale"), py::arg("causal"), py::arg("dq"), py::arg("dk"), py::arg("dv"),
+        py::arg("rope_pos") = py::none(), py::arg("rope_tab") = py::none());
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("ce_fwd_stats", &ce_fwd_stats);
-  m.def("ce_bwd", &ce_bwd);
+  m.def("ce_bwd", &ce_bwd, py::arg("logits"), py::arg("targets"), py::arg("lse"), py::arg("gscale"),
+        py::arg("vocab_start"), py::arg("vocab_valid"), py::arg("out"), py::arg("dbias") = py::none());
   m.def("adam_build", &adam_build);
   m.def("adam_step", &adam_step, py::arg("desc"), py::arg("chunks"), py::arg("lr"), py::arg("beta1"),
         py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"), py::arg("step"), py::arg("grad_scale") = 1.0,

@@ -264,27 +264,10 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd_k(const bf16*
   }
 }
 
-// ========================================================================== bwd: delta ==
-// delta[b,h,t] = sum_d dO[b,t,h,d] * O[b,t,h,d]   (one wave per (b,t,h) row)
-template <int HD>
-__global__ __launch_bounds__(256) void attn_bwd_delta_k(const bf16* __restrict__ dO, const bf16* __restrict__ O,
-                                                        float* __restrict__ delta, int B, int T, int H,
-                                                        long long lddo, long long ldo) {
-  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= (long long)B * T * H) return;
-  const int h = (int)(row % H);
-  const long long bt = row / H;
-  const int l = lane_id();
-  float s = 0.f;
-  for (int d = l; d < HD; d += 64)
-    s += to_f(dO[bt * lddo + (long long)h * HD + d]) * to_f(O[bt * ldo + (long long)h * HD + d]);
-  s = wave_sum(s);
-  if (l == 0) {
-    const long long b = bt / T, t = bt % T;
-    delta[(b * H + h) * T + t] = s;
-  }
-}
-
+// Optional inverse RoPE fused into the dQ / dK stores: tab[pos][HD] = [cos | sin] of the
+// HD/2 frequencies; column d < HD/2 pairs with d + HD/2, which lives in the same lane
+// (accumulator tile d + DT/2), so the transpose rotation is applied in registers.
+//   dx1 = dy1 c + dy2 s ;  dx2 = dy2 c - dy1 s
 // ========================================================================= bwd: dK, dV ==
 // Block: 4 waves x 16 keys = 64 keys of one (b,h); query tiles of 64 (Q and dO staged in
 // LDS, double buffered; lse/delta staged alongside).
@@ -295,7 +278,8 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv_k(const 
                                                           const float* __restrict__ DELTA, bf16* __restrict__ dK,
                                                           bf16* __restrict__ dV, int T, int H, long long ldq,
                                                           long long ldk, long long ldv, long long lddo,
-                                                          long long lddk, long long lddv, float scale, int causal) {
+                                                          long long lddk, long long lddv, float scale, int causal,
+                                                          const int64_t* __restrict__ rpos, const float* __restrict__ rtab) {
   constexpr int BKV = 64, BQ = 64, KT = HD / 32, DT = HD / 16;
   constexpr int TILE = BQ * HD * 2;
   __shared__ __attribute__((aligned(16))) char smem[2 * (2 * TILE + 2 * BQ * 4)];
@@ -423,13 +407,33 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv_k(const 
   }
   // Write dK (scaled), dV: C layout col = d (l&15), rows = keys 4g + j.
 #pragma unroll
+  for (int d = 0; d < DT; ++d)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dk[d][j] *= scale;
+  if (rpos) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ki = wk0 + 4 * g + j;
+      if (ki < T) {
+        const float* tr = rtab + rpos[(long long)b * T + ki] * HD;
+#pragma unroll
+        for (int d = 0; d < DT / 2; ++d) {
+          const float c = tr[16 * d + (l & 15)], sn = tr[HD / 2 + 16 * d + (l & 15)];
+          const float x1 = dk[d][j], x2 = dk[d + DT / 2][j];
+          dk[d][j] = x1 * c + x2 * sn;
+          dk[d + DT / 2][j] = x2 * c - x1 * sn;
+        }
+      }
+    }
+  }
+#pragma unroll
   for (int d = 0; d < DT; ++d) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int ki = wk0 + 4 * g + j;
       if (ki < T) {
         const long long col = (long long)h * HD + 16 * d + (l & 15);
-        dK[((long long)b * T + ki) * lddk + col] = (bf16)(dk[d][j] * scale);
+        dK[((long long)b * T + ki) * lddk + col] = (bf16)dk[d][j];
         dV[((long long)b * T + ki) * lddv + col] = (bf16)dv[d][j];
       }
     }
@@ -445,7 +449,8 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
                                                         float* __restrict__ DELTA_OUT, bf16* __restrict__ dQ, int T,
                                                         int H, long long ldq, long long ldk, long long ldv,
                                                         long long lddo, long long ldo, long long lddq, float scale,
-                                                        int causal) {
+                                                        int causal, const int64_t* __restrict__ rpos,
+                                                        const float* __restrict__ rtab) {
   constexpr int BQ = 128, BKV = 64, KT = HD / 32, DT = HD / 16;
   constexpr int TILE = BKV * HD * 2;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
@@ -581,9 +586,21 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
     if (qi < T) {
       bf16* row = dQ + ((long long)b * T + qi) * lddq + (long long)h * HD;
 #pragma unroll
+      for (int d = 0; d < DT; ++d) dq[c][d] *= scale;
+      if (rpos) {
+        const float* tr = rtab + rpos[(long long)b * T + qi] * HD;
+#pragma unroll
+        for (int d = 0; d < DT / 2; ++d) {
+          const f32x4 cs = *reinterpret_cast<const f32x4*>(tr + 16 * d + 4 * g);
+          const f32x4 sn = *reinterpret_cast<const f32x4*>(tr + HD / 2 + 16 * d + 4 * g);
+          const f32x4 x1 = dq[c][d], x2 = dq[c][d + DT / 2];
+          dq[c][d] = x1 * cs + x2 * sn;
+          dq[c][d + DT / 2] = x2 * cs - x1 * sn;
+        }
+      }
+#pragma unroll
       for (int d = 0; d < DT; ++d) {
-        bf16x4 v = {(bf16)(dq[c][d][0] * scale), (bf16)(dq[c][d][1] * scale), (bf16)(dq[c][d][2] * scale),
-                    (bf16)(dq[c][d][3] * scale)};
+        bf16x4 v = {(bf16)dq[c][d][0], (bf16)dq[c][d][1], (bf16)dq[c][d][2], (bf16)dq[c][d][3]};
         *reinterpret_cast<bf16x4*>(row + 16 * d + 4 * g) = v;
       }
     }
@@ -616,13 +633,15 @@ extern "C" void dpfs_attn_bwd(const void* dout, const void* q, const void* k, co
                               const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int T, int H,
                               int hd, long long lddo, long long ldq, long long ldk, long long ldv, long long ldo,
                               long long lddq, long long lddk, long long lddv, float scale, int causal,
-                              hipStream_t s) {
+                              const int64_t* rope_pos, const float* rope_tab, hipStream_t s) {
   dim3 gq((T + 127) / 128, B * H);
   DPFS_HD_DISPATCH(hd, attn_bwd_dq_k<HD_><<<gq, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
                                                              (const bf16*)dout, (const bf16*)o, lse, delta, (bf16*)dq,
-                                                             T, H, ldq, ldk, ldv, lddo, ldo, lddq, scale, causal));
+                                                             T, H, ldq, ldk, ldv, lddo, ldo, lddq, scale, causal,
+                                                             rope_pos, rope_tab));
   dim3 gk((T + 63) / 64, B * H);
   DPFS_HD_DISPATCH(hd, attn_bwd_dkdv_k<HD_><<<gk, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
                                                                (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv, T,
-                                                               H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal));
+                                                               H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal,
+                                                               rope_pos, rope_tab));
 }

@@ -159,6 +159,71 @@ __global__ __launch_bounds__(256) void colsum_stage_k(const T* __restrict__ x, f
   }
 }
 
+// Row-chunk plan shared by the fused "elementwise + column-sum" kernels: ~2048 blocks of
+// (32 column vectors x 8 row lanes); returns the chunk count, *rpc = rows per chunk.
+static int colsum_plan(int M, int cblocks, int target_blocks, int* rpc) {
+  int chunks = target_blocks / (cblocks > 0 ? cblocks : 1);
+  const int max_chunks = (M + 63) / 64;
+  if (chunks > max_chunks) chunks = max_chunks;
+  if (chunks < 1) chunks = 1;
+  *rpc = (M + chunks - 1) / chunks;
+  return (M + *rpc - 1) / *rpc;
+}
+
+// SwiGLU backward fused with the gate|up bias gradient: each thread owns one gate column
+// vector and its up partner, walks its row chunk, stores dgu and accumulates both column
+// sums in fp32; the block's 8 row lanes are reduced through LDS in a fixed order and
+// written as partials[chunk][2F] (deterministic; stage 2 = colsum_stage_k<float>).
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_bwd_colsum_k(const T* __restrict__ dh, const T* __restrict__ gu,
+                                                           T* __restrict__ dgu, float* __restrict__ partial, int M,
+                                                           int F, int rows_per_chunk) {
+  constexpr int N = Vec<T>::N;
+  __shared__ float red[8][2][32 * N];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int c0 = (blockIdx.x * 32 + tx) * N;
+  const int r0 = blockIdx.y * rows_per_chunk;
+  const int r1 = min(M, r0 + rows_per_chunk);
+  float ag[N], au[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) ag[j] = au[j] = 0.f;
+  if (c0 < F) {
+    for (int r = r0 + ty; r < r1; r += 8) {
+      const long long rr = r;
+      float g[N], u[N], d[N], og[N], ou[N];
+      load_vec<T>(gu + rr * 2 * F + c0, g);
+      load_vec<T>(gu + rr * 2 * F + F + c0, u);
+      load_vec<T>(dh + rr * F + c0, d);
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const float sg = 1.f / (1.f + __expf(-g[j]));
+        og[j] = d[j] * u[j] * sg * (1.f + g[j] * (1.f - sg));
+        ou[j] = d[j] * g[j] * sg;
+        ag[j] += og[j];
+        au[j] += ou[j];
+      }
+      store_vec<T>(dgu + rr * 2 * F + c0, og);
+      store_vec<T>(dgu + rr * 2 * F + F + c0, ou);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    red[ty][0][tx * N + j] = ag[j];
+    red[ty][1][tx * N + j] = au[j];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * 32 * N; i += 256) {
+    const int half = i / (32 * N), k = i % (32 * N);
+    const int col = blockIdx.x * 32 * N + k;
+    if (col < F) {
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) sum += red[w][half][k];
+      partial[(long long)blockIdx.y * 2 * F + half * F + col] = sum;
+    }
+  }
+}
+
 template <typename T>
 static void colsum_launch(const T* x, float* out, float* ws, int M, int N_, hipStream_t s) {
   constexpr int N = Vec<T>::N;
@@ -196,6 +261,42 @@ extern "C" void dpfs_swiglu_bwd(int dtype, const void* dh, const void* gu, void*
   else
     swiglu_bwd_k<float><<<cap_grid((long long)M * F / 4, 256), 256, 0, s>>>((const float*)dh, (const float*)gu,
                                                                                (float*)dgu, M, F);
+}
+
+// Workspace (floats) for dpfs_swiglu_bwd_dbias: partials [chunks, 2F].
+extern "C" long long dpfs_swiglu_bwd_dbias_ws(int M, int F) {
+  int rpc;
+  const int chunks = colsum_plan(M, (F / 8 + 31) / 32, 2048, &rpc);
+  return chunks > 1 ? (long long)chunks * 2 * F : 0;
+}
+
+extern "C" void dpfs_swiglu_bwd_dbias(int dtype, const void* dh, const void* gu, void* dgu, float* dbias, float* ws,
+                                      int M, int F, hipStream_t s) {
+  const int vec = dtype == kBF16 ? 8 : 4;
+  const int cblocks = (F / vec + 31) / 32;
+  int rpc;
+  const int chunks = colsum_plan(M, cblocks, 2048, &rpc);
+  float* part = chunks > 1 ? ws : dbias;
+  if (dtype == kBF16)
+    swiglu_bwd_colsum_k<bf16><<<dim3(cblocks, chunks), 256, 0, s>>>((const bf16*)dh, (const bf16*)gu, (bf16*)dgu,
+                                                                    part, M, F, rpc);
+  else
+    swiglu_bwd_colsum_k<float><<<dim3(cblocks, chunks), 256, 0, s>>>((const float*)dh, (const float*)gu, (float*)dgu,
+                                                                     part, M, F, rpc);
+  if (chunks > 1) {
+    const int cb2 = (2 * F / 4 + 31) / 32;
+    colsum_stage_k<float><<<dim3(cb2, 1), 256, 0, s>>>(ws, dbias, chunks, 2 * F, chunks);
+  }
+}
+
+// Stage 2 of a fused column sum: out[N] = sum over `rows` rows of part[rows, N] (fixed order).
+extern "C" void dpfs_colsum_rows_small(const float* part, float* out, int rows, int N, hipStream_t s) {
+  const int cb2 = (N / 4 + 31) / 32;
+  colsum_stage_k<float><<<dim3(cb2, 1), 256, 0, s>>>(part, out, rows, N, rows);
+}
+
+extern "C" int dpfs_colsum_plan(int M, int cblocks, int target_blocks, int* rpc) {
+  return colsum_plan(M, cblocks, target_blocks, rpc);
 }
 
 extern "C" void dpfs_rope(int dtype, void* qkv, const int64_t* pos, const float* table, int M, int ld, int n_heads,

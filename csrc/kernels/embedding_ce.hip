@@ -126,6 +126,55 @@ __global__ __launch_bounds__(256) void ce_bwd_k(const T* logits, const int64_t* 
   }
 }
 
+// CE backward fused with the lm_head bias gradient (column sums of dlogits): 2-D blocks of
+// 32 column vectors x 8 row lanes over a row chunk; fp32 partials [chunk][V], reduced in a
+// fixed order (deterministic).  Saves one full re-read of the [M, V_local] logits.
+template <typename T>
+__global__ __launch_bounds__(256) void ce_bwd_colsum_k(const T* logits, const int64_t* __restrict__ tgt,
+                                                       const float* __restrict__ lse,
+                                                       const float* __restrict__ gscale, T* out,
+                                                       float* __restrict__ partial, int M, int V, long long vstart,
+                                                       int vvalid, int rows_per_chunk) {
+  constexpr int N = Vec<T>::N;
+  __shared__ float red[8][32 * N];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int c = (blockIdx.x * 32 + tx) * N;
+  const int r0 = blockIdx.y * rows_per_chunk;
+  const int r1 = min(M, r0 + rows_per_chunk);
+  float acc[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) acc[j] = 0.f;
+  if (c < V) {
+    for (int r = r0 + ty; r < r1; r += 8) {
+      const float l = lse[r], g = gscale[r];
+      const long long loc = tgt[r] - vstart;
+      float v[N];
+      load_vec<T>(logits + (long long)r * V + c, v);
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const int col = c + j;
+        float p = col < vvalid ? __expf(v[j] - l) : 0.f;
+        if (col == loc && col < vvalid) p -= 1.f;
+        v[j] = p * g;
+        acc[j] += v[j];
+      }
+      store_vec<T>(out + (long long)r * V + c, v);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) red[ty][tx * N + j] = acc[j];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 32 * N; i += 256) {
+    const int col = blockIdx.x * 32 * N + i;
+    if (col < V) {
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) sum += red[w][i];
+      partial[(long long)blockIdx.y * V + col] = sum;
+    }
+  }
+}
+
 static inline int cap_grid2(long long work, int block) {
   long long g = (work + block - 1) / block;
   if (g > 2048) g = 2048;
@@ -136,6 +185,31 @@ static inline int cap_grid2(long long work, int block) {
 }  // namespace dpfs
 
 using namespace dpfs;
+
+extern "C" int dpfs_colsum_plan(int M, int cblocks, int target_blocks, int* rpc);
+extern "C" void dpfs_colsum_rows_small(const float* part, float* out, int rows, int N, hipStream_t s);
+
+extern "C" long long dpfs_ce_bwd_dbias_ws(int dtype, int M, int V) {
+  int rpc;
+  const int chunks = dpfs_colsum_plan(M, (V / (dtype == kBF16 ? 8 : 4) + 31) / 32, 2048, &rpc);
+  return chunks > 1 ? (long long)chunks * V : 0;
+}
+
+extern "C" void dpfs_ce_bwd_dbias(int dtype, const void* logits, const int64_t* tgt, const float* lse,
+                                  const float* gscale, void* out, float* dbias, float* ws, int M, int V,
+                                  long long vstart, int vvalid, hipStream_t s) {
+  const int cblocks = (V / (dtype == kBF16 ? 8 : 4) + 31) / 32;
+  int rpc;
+  const int chunks = dpfs_colsum_plan(M, cblocks, 2048, &rpc);
+  float* part = chunks > 1 ? ws : dbias;
+  if (dtype == kBF16)
+    ce_bwd_colsum_k<bf16><<<dim3(cblocks, chunks), 256, 0, s>>>((const bf16*)logits, tgt, lse, gscale, (bf16*)out,
+                                                                part, M, V, vstart, vvalid, rpc);
+  else
+    ce_bwd_colsum_k<float><<<dim3(cblocks, chunks), 256, 0, s>>>((const float*)logits, tgt, lse, gscale,
+                                                                 (float*)out, part, M, V, vstart, vvalid, rpc);
+  if (chunks > 1) dpfs_colsum_rows_small(ws, dbias, chunks, V, s);
+}
 
 extern "C" void dpfs_embedding_fwd(int out_dtype, const int64_t* ids, const float* w, void* out, int M, int D,
                                    long long vstart, int vlocal, hipStream_t s) {

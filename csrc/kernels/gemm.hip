@@ -284,6 +284,17 @@ __device__ __forceinline__ bf16x8 frag2(const char* lds, int rb, int kb) {
   }
 }
 
+// Optional RoPE (rotate-half, head_dim 64) applied in the NT epilogue to output columns
+// < cols (the q and k heads of a packed QKV projection); pos[m] indexes tab[maxlen][64]
+// = [cos | sin].  Each wave's 64 output columns are exactly one head, and with the swapped
+// MFMA layout the rotation partner of column d (d + 32) sits in the same lane (tile j+2), so
+// the rotation is pure register math — no separate RoPE pass over the QKV activations.
+struct RopeArgs {
+  const int64_t* pos;
+  const float* tab;
+  int cols;
+};
+
 template <int PIECES, int NSTAGE>
 __device__ __forceinline__ void wait_tile(int remaining_after) {
   // Tiles issued after the one we need: min(NSTAGE-2, remaining_after); each = PIECES DMAs.
@@ -300,7 +311,8 @@ template <int BM_, int BN_, int WAVES_M, int NSTAGE, bool AK, bool BKM, int OUT>
 __global__ __launch_bounds__(512, 2) void gemm2_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                   void* __restrict__ C, const float* __restrict__ bias, int M, int N,
                                                   int K, int lda, int ldb, int ldc, int k_per_split,
-                                                  long long slab_stride, unsigned a_bytes, unsigned b_bytes) {
+                                                  long long slab_stride, unsigned a_bytes, unsigned b_bytes,
+                                                  RopeArgs rope) {
   constexpr int WAVES_N = 8 / WAVES_M;
   constexpr int WM = BM_ / WAVES_M, WN = BN_ / WAVES_N;
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -373,21 +385,41 @@ __global__ __launch_bounds__(512, 2) void gemm2_k(const bf16* __restrict__ A, co
 
   // Epilogue: acc[i][j] = C^T tile: lane holds C[m = .. + (l&15)][n = .. + 4g + r], r < 4.
   const int g = l >> 4;
+  const int wcol0 = n0 + wn * WN;
+  const bool do_rope = (OUT == 0) && (WN == 64) && (TN == 4) && rope.cols > 0 && wcol0 < rope.cols;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = m0 + wm * WM + 16 * i + (l & 15);
     if (m >= M) continue;
+    f32x4 v[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * WN + 16 * j + 4 * g;
+      v[j] = acc[i][j];
+      const int n = wcol0 + 16 * j + 4 * g;
+      if (OUT == 0 && bias && n < N) v[j] += *reinterpret_cast<const f32x4*>(bias + n);
+    }
+    if constexpr (OUT == 0 && TN == 4) {
+      if (do_rope) {
+        const float* tr = rope.tab + rope.pos[m] * 64;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const f32x4 cs = *reinterpret_cast<const f32x4*>(tr + 16 * j + 4 * g);
+          const f32x4 sn = *reinterpret_cast<const f32x4*>(tr + 32 + 16 * j + 4 * g);
+          const f32x4 x1 = v[j], x2 = v[j + 2];
+          v[j] = x1 * cs - x2 * sn;
+          v[j + 2] = x2 * cs + x1 * sn;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = wcol0 + 16 * j + 4 * g;
       if (n >= N) continue;
-      f32x4 v = acc[i][j];
       if (OUT == 0) {
-        if (bias) v += *reinterpret_cast<const f32x4*>(bias + n);
-        bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        bf16x4 o = {(bf16)v[j][0], (bf16)v[j][1], (bf16)v[j][2], (bf16)v[j][3]};
         *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(C) + (long long)m * ldc + n) = o;
       } else {
-        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + blockIdx.y * slab_stride + (long long)m * ldc + n) = v;
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + blockIdx.y * slab_stride + (long long)m * ldc + n) = v[j];
       }
     }
   }
@@ -426,13 +458,14 @@ static unsigned span_bytes(long long rows, long long ld, long long cols) {
 // v2 configurations: 0 = 256x256 / 2-stage (128 KiB LDS), 1 = 256x128 / 3-stage (144 KiB).
 template <bool AK, bool BKM, int OUT>
 static void launch2(int cfg, const void* A, const void* B, void* C, const float* bias, int M, int N, int K, int lda,
-                    int ldb, int ldc, int splits, int kps, long long slab, unsigned ab, unsigned bb, hipStream_t s) {
+                    int ldb, int ldc, int splits, int kps, long long slab, unsigned ab, unsigned bb, hipStream_t s,
+                    RopeArgs rope = RopeArgs{nullptr, nullptr, 0}) {
   if (cfg == 0) {
     gemm2_k<256, 256, 2, 2, AK, BKM, OUT><<<dim3(tiles2(M, N, 256, 256), splits), 512, 0, s>>>(
-        (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, kps, slab, ab, bb);
+        (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, kps, slab, ab, bb, rope);
   } else {
     gemm2_k<256, 128, 4, 3, AK, BKM, OUT><<<dim3(tiles2(M, N, 256, 128), splits), 512, 0, s>>>(
-        (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, kps, slab, ab, bb);
+        (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, kps, slab, ab, bb, rope);
   }
 }
 
@@ -483,7 +516,7 @@ extern "C" long long dpfs_gemm_bf16_ws(int M, int N, int K) {
 
 template <bool BKM>
 static void bf16_gemm(const void* A, const void* B, void* C, const float* bias, int M, int N, int K, int lda, int ldb,
-                      int ldc, unsigned ab, unsigned bb, hipStream_t s) {
+                      int ldc, unsigned ab, unsigned bb, hipStream_t s, RopeArgs rope = RopeArgs{nullptr, nullptr, 0}) {
   const int S = bf16_splits(M, N, K);
   if (S > 1 && g_ws && g_ws_floats >= (long long)S * M * N) {
     int kps = (K + S - 1) / S;
@@ -495,7 +528,20 @@ static void bf16_gemm(const void* A, const void* B, void* C, const float* bias, 
     splitk_reduce_bf16_k<<<(int)g, 256, 0, s>>>(g_ws, (bf16*)C, bias, M, N, ldc, S);
     return;
   }
-  launch2<true, BKM, 0>(pick_cfg(M, N, 1), A, B, C, bias, M, N, K, lda, ldb, ldc, 1, K, 0, ab, bb, s);
+  launch2<true, BKM, 0>(pick_cfg(M, N, 1), A, B, C, bias, M, N, K, lda, ldb, ldc, 1, K, 0, ab, bb, s, rope);
+}
+
+// Whether dpfs_gemm_nt_rope can fuse the rotation for this problem (else the caller runs the
+// separate RoPE kernel after the GEMM).
+extern "C" int dpfs_gemm_rope_fusable(int M, int N, int K, int hd) {
+  return g_gemm_impl != 1 && hd == 64 && bf16_splits(M, N, K) == 1 && N % 64 == 0;
+}
+
+extern "C" void dpfs_gemm_nt_rope(const void* A, const void* B, void* C, const float* bias, int M, int N, int K,
+                                  int lda, int ldb, int ldc, const int64_t* pos, const float* tab, int rope_cols,
+                                  hipStream_t s) {
+  bf16_gemm<true>(A, B, C, bias, M, N, K, lda, ldb, ldc, span_bytes(M, lda, K), span_bytes(N, ldb, K), s,
+                  RopeArgs{pos, tab, rope_cols});
 }
 
 // NT: C[M,N] bf16 = A[M,K] B[N,K]^T + bias

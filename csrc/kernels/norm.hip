@@ -114,9 +114,9 @@ __global__ __launch_bounds__(256) void layernorm_fwd_k(const T* __restrict__ x, 
 template <typename T, int VPL, int MODE>
 __global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, const T* __restrict__ x,
                                                   const float* __restrict__ w, const float* __restrict__ mean_in,
-                                                  const float* __restrict__ rstd, T* __restrict__ dx,
-                                                  float* __restrict__ partial_w, float* __restrict__ partial_b,
-                                                  int M, int D) {
+                                                  const float* __restrict__ rstd, const T* __restrict__ dres,
+                                                  T* __restrict__ dx, float* __restrict__ partial_w,
+                                                  float* __restrict__ partial_b, int M, int D) {
   constexpr int N = Vec<T>::N;
   extern __shared__ __attribute__((aligned(16))) float red[];  // [2][D]
   const int lane = threadIdx.x & 63;
@@ -163,6 +163,12 @@ __global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, cons
         float o[N];
 #pragma unroll
         for (int j = 0; j < N; ++j) o[j] = r * (g[i][j] - (MODE == 1 ? gs : 0.f) - xh[i][j] * dot);
+        if (dres) {  // fused residual-stream gradient add (dx += dres)
+          float rv[N];
+          load_vec<T>(dres + (size_t)row * D + c * N, rv);
+#pragma unroll
+          for (int j = 0; j < N; ++j) o[j] += rv[j];
+        }
         store_vec<T>(dxr + c * N, o);
       }
     }
@@ -260,13 +266,13 @@ extern "C" void dpfs_layernorm_fwd(int dtype, const void* x, const float* w, con
 
 // mode 0 = rms, 1 = layernorm.  partial_w/partial_b: [dpfs_norm_bwd_grid(M), D] workspace.
 extern "C" void dpfs_norm_bwd(int mode, int dtype, const void* dy, const void* x, const float* w, const float* mean,
-                              const float* rstd, void* dx, float* dw, float* db, float* partial_w, float* partial_b,
-                              int M, int D, hipStream_t s) {
+                              const float* rstd, const void* dres, void* dx, float* dw, float* db, float* partial_w,
+                              float* partial_b, int M, int D, hipStream_t s) {
   const int G = norm_bwd_grid(M);
   const size_t lds = (size_t)(mode == 1 ? 2 : 1) * D * sizeof(float);
 #define DPFS_NB(T, MODE_)                                                                                  \
   DPFS_VPL_DISPATCH(vpl_for<T>(D), norm_bwd_k<T, VPL, MODE_><<<G, 256, lds, s>>>(                           \
-      (const T*)dy, (const T*)x, w, mean, rstd, (T*)dx, partial_w, partial_b, M, D))
+      (const T*)dy, (const T*)x, w, mean, rstd, (const T*)dres, (T*)dx, partial_w, partial_b, M, D))
   if (dtype == kBF16) {
     if (mode == 0) DPFS_NB(bf16, 0); else DPFS_NB(bf16, 1);
   } else {

@@ -60,7 +60,7 @@ def _addg(acc, g):
     if g is None:
         return acc
     if acc is None:
-        return g.float().clone() if g.dtype != torch.float32 else g.clone()
+        return g.float() if g.dtype != torch.float32 else g   # fresh kernel output: take ownership
     return acc.add_(g)
 
 
@@ -127,10 +127,9 @@ class DecoderTrainFn(torch.autograd.Function):
                     _wait(s["h"])
                 x = s["x"]
                 h1, r1 = k.rmsnorm_fwd(x, L.s1, L.eps1)
-                qkv = k.gemm_nt(h1, W(L.wqkv), L.bqkv)
+                qkv = k.gemm_nt(h1, W(L.wqkv), L.bqkv, s["pos"], tab, 2 * L.h, L.hd)  # RoPE in the epilogue
                 Mc = x.size(0)
                 Bc = s["B"]
-                k.rope_(qkv, s["pos"], tab, 2 * L.h, L.hd, False)
                 q, kk, v = _split(qkv, Bc, T, L.h, L.hd)
                 o, lse = k.attn_fwd(q, kk, v, 1.0 / math.sqrt(L.hd), True)
                 o2 = o.view(Mc, L.h * L.hd)
@@ -175,6 +174,7 @@ class DecoderTrainFn(torch.autograd.Function):
         loss = losses_sum / n_valid_total
         ctx.model, ctx.st, ctx.layers, ctx.meta = model, st, layers, (T, dt, vst, vvalid, C, d)
         ctx.n_valid = n_valid_total
+        ctx.tab = tab
         ctx.nparams = len(params)
         return loss
 
@@ -185,6 +185,7 @@ class DecoderTrainFn(torch.autograd.Function):
         k = K(model.embedding.weight)
         head = model.lm_head
         W = lambda w: shadow(w, dt) if w is not None else None
+        tab = ctx.tab
         gscale_all = (gloss.float() / ctx.n_valid)
         nL = len(layers)
         # fp32 grad accumulators
@@ -207,13 +208,14 @@ class DecoderTrainFn(torch.autograd.Function):
         for s in st:
             gs = s["valid"].float() * gscale_all
             dl = s["logits"]
-            k.ce_bwd(dl, s["tgt"], s["ce_lse"], gs, vst, vvalid, dl)
+            db = dl.new_empty(dl.size(1), dtype=torch.float32) if head.bias is not None else None
+            k.ce_bwd(dl, s["tgt"], s["ce_lse"], gs, vst, vvalid, dl, db)    # + lm_head bias grad
             dh = k.gemm_nn(dl, W(head.weight))
             s["bh"] = _ar(dh)
             s["dpend"] = dh
             tn(g, "lm_w", dl, s["hf"])
-            if head.bias is not None:
-                g["lm_b"] = _addg(g["lm_b"], k.bias_grad(dl))
+            if db is not None:
+                g["lm_b"] = _addg(g["lm_b"], db)
             del s["logits"]
         for s in st:
             _wait(s["bh"])
@@ -234,19 +236,20 @@ class DecoderTrainFn(torch.autograd.Function):
                 bias_acc(G, "bd", gq, L.bd)
                 ds = k.gemm_nn(gq, W(L.wd))
                 tn(G, "wd", gq, a["sw"])
-                dgu = k.swiglu_bwd(ds, a["gu"])
+                dbgu = ds.new_empty(a["gu"].size(1), dtype=torch.float32) if L.bgu is not None else None
+                dgu = k.swiglu_bwd(ds, a["gu"], dbgu)     # + gate|up bias grad in the same pass
                 dh2 = k.gemm_nn(dgu, W(L.wgu))
                 s["bh"], s["dpend"] = _ar(dh2), dh2
                 tn(G, "wgu", dgu, a["h2"])
-                bias_acc(G, "bgu", dgu, L.bgu)
+                if dbgu is not None:
+                    G["bgu"] = _addg(G.get("bgu"), dbgu)
                 del a["sw"], a["gu"]
             # b1: wait, norm2 bwd, Wo / attention / QKV grads -> AR(dh)
             for s in st:
                 a = s["layers"][li]
                 _wait(s["bh"])
-                dx2n, ds2 = k.rmsnorm_bwd(s["dpend"], a["x2"], L.s2, a["r2"])
+                g2, ds2 = k.rmsnorm_bwd(s["dpend"], a["x2"], L.s2, a["r2"], s["g"])  # + residual grad
                 G["s2"] = _addg(G.get("s2"), ds2)
-                g2 = s["g"].add_(dx2n) if s["g"].dtype == dx2n.dtype else s["g"] + dx2n
                 bias_acc(G, "bo", g2, L.bo)
                 do = k.gemm_nn(g2, W(L.wo))
                 tn(G, "wo", g2, a["o"].view(g2.size(0), -1))
@@ -255,8 +258,7 @@ class DecoderTrainFn(torch.autograd.Function):
                 dqkv = torch.empty_like(a["qkv"])
                 dq, dk, dv = _split(dqkv, Bc, T, L.h, L.hd)
                 k.attn_bwd(do.view(Bc, T, L.h, L.hd), q, kk, v, a["o"], a["lse"], 1.0 / math.sqrt(L.hd), True,
-                           dq, dk, dv)
-                k.rope_(dqkv, s["pos"], model.rope_table(dqkv.device), 2 * L.h, L.hd, True)
+                           dq, dk, dv, s["pos"], tab)   # inverse RoPE fused into the dq/dk stores
                 dh = k.gemm_nn(dqkv, W(L.wqkv))
                 s["bh"], s["dpend"] = _ar(dh), dh
                 tn(G, "wqkv", dqkv, a["h1"])
@@ -285,9 +287,8 @@ def _finish_norm1(k, s, L, G, li):
     it to the residual-stream grad (-> grad wrt layer li's input)."""
     a = s["layers"][li]
     _wait(s["bh"])
-    dxn, ds1 = k.rmsnorm_bwd(s["dpend"], a["x"], L.s1, a["r1"])
+    s["g"], ds1 = k.rmsnorm_bwd(s["dpend"], a["x"], L.s1, a["r1"], s["g"])   # fused residual-grad add
     G["s1"] = _addg(G.get("s1"), ds1)
-    s["g"] = s["g"].add_(dxn)
     s["dpend"] = None
     for key in ("x", "r1", "h1"):
         a.pop(key, None)

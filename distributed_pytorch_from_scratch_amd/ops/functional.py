@@ -88,8 +88,8 @@ class CausalSelfAttentionFn(torch.autograd.Function):
 
     Forward rotates q and k in place (the buffer is a fresh GEMM output nobody else saved),
     runs the flash-attention forward (O(T) memory, LSE saved), returns ``o[B*T, hq*hd]``.
-    Backward runs the flash backward into one packed ``dqkv`` buffer and applies the inverse
-    rotation to dq/dk in place, so the QKV dgrad GEMM consumes it directly.
+    Backward runs the flash backward into one packed ``dqkv`` buffer with the inverse rotation
+    fused into the dq/dk stores, so the QKV dgrad GEMM consumes it directly.
     """
 
     @staticmethod
@@ -114,9 +114,8 @@ class CausalSelfAttentionFn(torch.autograd.Function):
         do4 = do.contiguous().view(B, T, hq, hd)
         dqkv = torch.empty_like(qkv)
         dq, dk, dv = _split_qkv(dqkv, B, T, hq, hkv, hd)
-        k_.attn_bwd(do4, q, k, v, o, lse, scale, causal, dq, dk, dv)
-        if rope_table is not None:
-            k_.rope_(dqkv, positions, rope_table, hq + hkv, hd, True)
+        rp = positions.reshape(-1).long().contiguous() if rope_table is not None else None
+        k_.attn_bwd(do4, q, k, v, o, lse, scale, causal, dq, dk, dv, rp, rope_table)  # + inverse RoPE
         return dqkv, None, None, None, None, None, None, None, None
 
 

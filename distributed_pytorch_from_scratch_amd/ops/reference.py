@@ -27,12 +27,18 @@ import torch.nn.functional as F
 
 # ------------------------------------------------------------------------------- GEMM ----
 
-def gemm_nt(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """c[M,N] = a[M,K] @ b[N,K]^T (+ bias[N]); output dtype = a.dtype."""
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None, rope_pos=None, rope_tab=None,
+            rope_heads: int = 0, rope_hd: int = 0) -> torch.Tensor:
+    """c[M,N] = a[M,K] @ b[N,K]^T (+ bias[N]); output dtype = a.dtype.  With ``rope_pos`` the first
+    ``rope_heads`` heads of each row are then rotated (the GPU kernel fuses this into its
+    epilogue)."""
     c = a.float() @ b.float().t()
     if bias is not None:
         c = c + bias.float()
-    return c.to(a.dtype)
+    c = c.to(a.dtype)
+    if rope_pos is not None and rope_heads > 0:
+        rope_(c, rope_pos, rope_tab, rope_heads, rope_hd, False)
+    return c
 
 
 def gemm_nn(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -81,13 +87,17 @@ def rmsnorm_fwd(x: torch.Tensor, w: torch.Tensor, eps: float) -> Tuple[torch.Ten
     return y.to(x.dtype), rstd
 
 
-def rmsnorm_bwd(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, rstd: torch.Tensor):
+def rmsnorm_bwd(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, rstd: torch.Tensor,
+                dres: Optional[torch.Tensor] = None):
+    """Returns (dx [+ dres if given, fused residual-grad add], dw fp32)."""
     xf, dyf, wf = x.float(), dy.float(), w.float()
     xhat = xf * rstd[:, None]
     dw = (dyf * xhat).sum(0)
     g = dyf * wf
     d = xf.size(-1)
     dx = rstd[:, None] * (g - xhat * (g * xhat).sum(-1, keepdim=True) / d)
+    if dres is not None:
+        dx = dx + dres.float()
     return dx.to(x.dtype), dw
 
 
@@ -167,8 +177,22 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float,
     return o.to(q.dtype), lse
 
 
-def attn_bwd(do, q, k, v, o, lse, scale: float, causal: bool, dq_out, dk_out, dv_out):
-    """Writes dq/dk/dv into the given (B, T, H, hd) views (packed dqkv buffer)."""
+def _rot_bthd(x: torch.Tensor, positions: torch.Tensor, table: torch.Tensor, inverse: bool) -> torch.Tensor:
+    """Rotate-half RoPE of an fp32 (B, T, H, hd) tensor; ``positions`` is flat [B*T]."""
+    B, T, H, hd = x.shape
+    h2 = hd // 2
+    tab = table[positions.long()].view(B, T, 1, hd)
+    c, s = tab[..., :h2], tab[..., h2:]
+    if inverse:
+        s = -s
+    x1, x2 = x[..., :h2], x[..., h2:]
+    return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1)
+
+
+def attn_bwd(do, q, k, v, o, lse, scale: float, causal: bool, dq_out, dk_out, dv_out, rope_pos=None,
+             rope_tab=None):
+    """Writes dq/dk/dv into the given (B, T, H, hd) views (packed dqkv buffer).  With
+    ``rope_pos`` the inverse RoPE is applied to dq and dk (fused into the stores on the GPU)."""
     qf, kf, vf, dof, of = (t.float().transpose(1, 2) for t in (q, k, v, do, o))
     s = (qf @ kf.transpose(-1, -2)) * scale
     if causal:
@@ -182,8 +206,12 @@ def attn_bwd(do, q, k, v, o, lse, scale: float, causal: bool, dq_out, dk_out, dv
     ds = p * (dp - delta) * scale
     dq = ds @ kf
     dk = ds.transpose(-1, -2) @ qf
-    dq_out.copy_(dq.transpose(1, 2))
-    dk_out.copy_(dk.transpose(1, 2))
+    dq, dk = dq.transpose(1, 2), dk.transpose(1, 2)
+    if rope_pos is not None:
+        dq = _rot_bthd(dq, rope_pos, rope_tab, True)
+        dk = _rot_bthd(dk, rope_pos, rope_tab, True)
+    dq_out.copy_(dq)
+    dk_out.copy_(dk)
     dv_out.copy_(dv.transpose(1, 2))
 
 
@@ -195,7 +223,8 @@ def swiglu_fwd(gu: torch.Tensor) -> torch.Tensor:
     return (F.silu(g) * u).to(gu.dtype)
 
 
-def swiglu_bwd(dh: torch.Tensor, gu: torch.Tensor) -> torch.Tensor:
+def swiglu_bwd(dh: torch.Tensor, gu: torch.Tensor, dbias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """d gate|up; with ``dbias`` (fp32 [2F]) also writes the bias gradient (column sums)."""
     F_ = gu.size(-1) // 2
     g, u = gu[..., :F_].float(), gu[..., F_:].float()
     dhf = dh.float()
@@ -203,7 +232,10 @@ def swiglu_bwd(dh: torch.Tensor, gu: torch.Tensor) -> torch.Tensor:
     silu = g * sig
     dg = dhf * u * sig * (1 + g * (1 - sig))
     du = dhf * silu
-    return torch.cat([dg, du], dim=-1).to(gu.dtype)
+    d = torch.cat([dg, du], dim=-1)
+    if dbias is not None:
+        dbias.copy_(d.sum(0))
+    return d.to(gu.dtype)
 
 
 # ---------------------------------------------------------------------- embedding ----
@@ -256,7 +288,8 @@ def ce_combine(stats: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
 
 
 def ce_bwd(logits: torch.Tensor, targets: torch.Tensor, lse: torch.Tensor, gscale: torch.Tensor,
-           vocab_start: int, vocab_valid: int, out: torch.Tensor) -> torch.Tensor:
+           vocab_start: int, vocab_valid: int, out: torch.Tensor,
+           dbias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """d logits = (softmax - onehot) * gscale[row] (gscale = 0 on ignored rows); padded
     columns get 0.  Written to ``out`` (may alias ``logits``: the GPU kernel runs in place)."""
     x = logits.float()
@@ -267,6 +300,8 @@ def ce_bwd(logits: torch.Tensor, targets: torch.Tensor, lse: torch.Tensor, gscal
     p = p * gscale[:, None]
     if vocab_valid < x.size(1):
         p[:, vocab_valid:] = 0
+    if dbias is not None:
+        dbias.copy_(p.sum(0))
     out.copy_(p)
     return out
 

@@ -239,3 +239,83 @@ def test_adam_matches_torch(C):
     for p, r, s in zip(ps, ref, sh):
         assert (p - r.detach()).abs().max().item() < 1e-5
         assert torch.equal(s, p.bfloat16())
+
+
+@pytest.mark.parametrize("M,N,K,heads", [(2048, 2304, 768, 24), (300, 1152, 768, 12), (4096, 576, 768, 6)])
+def test_gemm_nt_fused_rope(C, M, N, K, heads):
+    """QKV projection with the RoPE rotation in the GEMM epilogue (hd=64) vs GEMM + reference RoPE."""
+    torch.manual_seed(12)
+    hd = 64
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
+    bias = torch.randn(N, device=DEV)
+    pos = torch.randint(0, 1024, (M,), device=DEV)
+    tab = R.rope_table(1024, hd, 10000.0).to(DEV)
+    c = C.gemm_nt(a, b, bias, pos, tab, heads, hd)
+    ref = a.float() @ b.float().t() + bias
+    R.rope_(ref, pos, tab, heads, hd, False)
+    assert _rel(c, ref) < 1e-2
+    # unrotated tail (v heads) untouched by the rotation
+    assert _rel(c[:, heads * hd:], (a.float() @ b.float().t() + bias)[:, heads * hd:]) < 1e-2
+
+
+@pytest.mark.parametrize("hd", [64, 128])
+def test_attention_bwd_fused_inverse_rope(C, hd):
+    torch.manual_seed(13)
+    B, T, H = 2, 192, 3
+    qkv = torch.randn(B * T, 3 * H * hd, device=DEV).bfloat16()
+    q, k, v = (qkv[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+    o, lse = C.attn_fwd(q, k, v, hd ** -0.5, True)
+    do = torch.randn_like(o)
+    pos = torch.randint(0, 512, (B * T,), device=DEV)
+    tab = R.rope_table(512, hd, 10000.0).to(DEV)
+    d = torch.empty_like(qkv)
+    dq, dk, dv = (d[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+    C.attn_bwd(do, q, k, v, o, lse, hd ** -0.5, True, dq, dk, dv, pos, tab)
+    r = torch.empty(B * T, 3 * H * hd, device=DEV)
+    rq, rk, rv = (r[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+    R.attn_bwd(do.float(), q.float(), k.float(), v.float(), o.float(), lse, hd ** -0.5, True, rq, rk, rv)
+    R.rope_(r, pos, tab, 2 * H, hd, True)
+    assert _rel(d, r) < 3e-2
+
+
+def test_rmsnorm_bwd_fused_residual_grad(C):
+    torch.manual_seed(14)
+    M, D = 513, 768
+    x = torch.randn(M, D, device=DEV).bfloat16()
+    w = torch.randn(D, device=DEV)
+    dy = torch.randn(M, D, device=DEV).bfloat16()
+    dres = torch.randn(M, D, device=DEV).bfloat16()
+    _, rstd = C.rmsnorm_fwd(x, w, 1e-5)
+    dx, dw = C.rmsnorm_bwd(dy, x, w, rstd, dres)
+    rdx, rdw = R.rmsnorm_bwd(dy.float(), x.float(), w, rstd, dres.float())
+    assert _rel(dx, rdx) < 1e-2 and _rel(dw, rdw) < 1e-2
+
+
+@pytest.mark.parametrize("M,F", [(4096, 3072), (333, 1024), (40, 64)])
+def test_swiglu_bwd_fused_bias_grad(C, M, F):
+    torch.manual_seed(15)
+    gu = torch.randn(M, 2 * F, device=DEV).bfloat16()
+    dh = torch.randn(M, F, device=DEV).bfloat16()
+    db = torch.empty(2 * F, device=DEV)
+    dgu = C.swiglu_bwd(dh, gu, db)
+    rdb = torch.empty(2 * F, device=DEV)
+    rdgu = R.swiglu_bwd(dh.float(), gu.float(), rdb)
+    assert _rel(dgu, rdgu) < 1e-2 and _rel(db, rdb) < 1e-3
+    assert torch.equal(dgu, C.swiglu_bwd(dh, gu))
+
+
+@pytest.mark.parametrize("M,V,valid,start", [(2048, 6288, 6241, 6288 * 7), (100, 50304, 50257, 0)])
+def test_ce_bwd_fused_bias_grad(C, M, V, valid, start):
+    torch.manual_seed(16)
+    logits = torch.randn(M, V, device=DEV).bfloat16()
+    tgt = torch.randint(start, start + valid, (M,), device=DEV)
+    lse = torch.logsumexp(logits.float()[:, :valid], -1)
+    gs = torch.rand(M, device=DEV)
+    out = torch.empty_like(logits)
+    db = torch.empty(V, device=DEV)
+    C.ce_bwd(logits, tgt, lse, gs, start, valid, out, db)
+    rout = torch.empty(M, V, device=DEV)
+    rdb = torch.empty(V, device=DEV)
+    R.ce_bwd(logits.float(), tgt, lse, gs, start, valid, rout, rdb)
+    assert _rel(out, rout) < 1e-2 and _rel(db, rdb) < 1e-3
