@@ -17,11 +17,13 @@ extern "C" {
 void dpfs_gemm_nt(const void*, const void*, void*, const float*, int, int, int, int, int, int, hipStream_t);
 void dpfs_gemm_nn(const void*, const void*, void*, int, int, int, int, int, int, hipStream_t);
 int dpfs_gemm_tn_splits(int, int, int);
+long long dpfs_gemm_tn_ws(int, int, int, int);
 void dpfs_gemm_set_impl(int);
 int dpfs_gemm_rope_fusable(int, int, int, int);
 void dpfs_gemm_nt_rope(const void*, const void*, void*, const float*, int, int, int, int, int, int, const int64_t*,
                        const float*, int, hipStream_t);
 void dpfs_gemm_force(int, int);
+void dpfs_gemm_v2_sched(int);
 void dpfs_gemm_set_workspace(float*, long long);
 long long dpfs_gemm_bf16_ws(int, int, int);
 void dpfs_gemm_tn(const void*, const void*, float*, float*, int, int, int, int, int, int, hipStream_t);
@@ -179,9 +181,9 @@ torch::Tensor gemm_tn(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
     if (!accumulate) c.zero_();
     return c;
   }
-  const int S = dpfs_gemm_tn_splits((int)M, (int)N, (int)K);
+  const long long wsn = dpfs_gemm_tn_ws((int)M, (int)N, (int)K, accumulate ? 1 : 0);
   torch::Tensor ws;
-  if (S > 1 || accumulate) ws = torch::empty({(int64_t)S * M * N}, c.options());
+  if (wsn > 0) ws = torch::empty({(int64_t)wsn}, c.options());
   dpfs_gemm_tn(a.data_ptr(), b.data_ptr(), c.data_ptr<float>(), ws.defined() ? ws.data_ptr<float>() : nullptr, (int)M,
                (int)N, (int)K, (int)a.stride(0), (int)b.stride(0), accumulate ? 1 : 0, stream());
   return c;
@@ -582,7 +584,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nn", &gemm_nn);
   m.def("gemm_force", [](int cfg, int splits) { dpfs_gemm_force(cfg, splits); },
         "force the v2 tile config (-1 auto, 0 = 256x256, 1 = 256x128) and K-splits (0 auto)");
-  m.def("gemm_set_impl", [](int v) { dpfs_gemm_set_impl(v); }, "1 = v1 (128x128 register-staged), 2 = v2 (LDS-DMA)");
+  m.def("gemm_v2_sched", [](int v) { dpfs_gemm_v2_sched(v); }, "v2 256x256 schedule (-1 per-layout default, 0..4 see gemm2_k SCHED)");
+  m.def("gemm_set_impl", [](int v) { dpfs_gemm_set_impl(v); }, "1 = v1 (128x128 register-staged), 2 = v2 (LDS-DMA, default)");
   m.def("gemm_tn", &gemm_tn, py::arg("a"), py::arg("b"), py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("bias_grad", &bias_grad);
   m.def("add_bias_", &add_bias_);

@@ -261,6 +261,31 @@ __device__ __forceinline__ void issue_tile(__amdgpu_buffer_rsrc_t rs, char* tile
   }
 }
 
+// One 1 KiB DMA piece (index i < R/64) of issue_tile, for schedules that spread the
+// pieces between MFMAs.
+template <bool KMAJ, int R>
+__device__ __forceinline__ void issue_piece(__amdgpu_buffer_rsrc_t rs, char* tile, int r0, int k0, int ld, int K,
+                                            int i) {
+  const int l = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = wave + 8 * i;
+  unsigned off;
+  if (KMAJ) {
+    const int row = 8 * j + (l >> 3);
+    const int c = (l & 7) ^ ((l >> 3) & 7);
+    const int k = k0 + c * 8;
+    off = (k < K) ? (unsigned)(((long long)(r0 + row) * ld + k) * 2) : kOOB;
+  } else {
+    constexpr int CPR = R / 8;
+    const int lin = j * 64 + l;
+    const int row = lin / CPR;
+    const int c = (lin % CPR) ^ (mn_h(row) << 1);
+    const int k = k0 + row;
+    off = (k < K) ? (unsigned)(((long long)k * ld + r0 + c * 8) * 2) : kOOB;
+  }
+  dma16(rs, tile + j * 1024, off);
+}
+
 template <bool KMAJ, int R>
 __device__ __forceinline__ bf16x8 frag2(const char* lds, int rb, int kb) {
   const int l = lane_id();
@@ -307,7 +332,9 @@ __device__ __forceinline__ void wait_tile(int remaining_after) {
 }
 
 // OUT: 0 = bf16 C (+bias); 1 = fp32 C / split-K slab.
-template <int BM_, int BN_, int WAVES_M, int NSTAGE, bool AK, bool BKM, int OUT>
+// SCHED: 0 = all DMA pieces right after the barrier; 1 = after the first k-half's MFMAs;
+// 2 = one piece after each MFMA row of the first k-half (spreads the DMA issue cost).
+template <int BM_, int BN_, int WAVES_M, int NSTAGE, bool AK, bool BKM, int OUT, int SCHED = 0>
 __global__ __launch_bounds__(512, 2) void gemm2_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                   void* __restrict__ C, const float* __restrict__ bias, int M, int N,
                                                   int K, int lda, int ldb, int ldc, int k_per_split,
@@ -356,16 +383,49 @@ __global__ __launch_bounds__(512, 2) void gemm2_k(const bf16* __restrict__ A, co
   for (int t = 0; t < nk; ++t) {
     wait_tile<PIECES, NSTAGE>(nk - 1 - t);
     __builtin_amdgcn_s_barrier();  // tile t landed for all waves; tile t-1's buffer is free
-    if (t + NSTAGE - 1 < nk) {
-      int nb = cur + NSTAGE - 1;
-      if (nb >= NSTAGE) nb -= NSTAGE;
-      char* st = smem + nb * STAGE;
-      const int k1 = kbeg + (t + NSTAGE - 1) * 64;
-      issue_tile<AK, BM_>(ra, st, m0, k1, lda, kend);
-      issue_tile<BKM, BN_>(rb, st + A_BYTES, n0, k1, ldb, kend);
+    const bool more = t + NSTAGE - 1 < nk;
+    int nb = cur + NSTAGE - 1;
+    if (nb >= NSTAGE) nb -= NSTAGE;
+    char* nst = smem + nb * STAGE;
+    const int k1 = kbeg + (t + NSTAGE - 1) * 64;
+    if (SCHED == 0 && more) {
+      issue_tile<AK, BM_>(ra, nst, m0, k1, lda, kend);
+      issue_tile<BKM, BN_>(rb, nst + A_BYTES, n0, k1, ldb, kend);
     }
     const char* la = smem + cur * STAGE;
     const char* lb = la + A_BYTES;
+    auto piece = [&](int q) {
+      if (q < BM_ / 64) issue_piece<AK, BM_>(ra, nst, m0, k1, lda, kend, q);
+      else issue_piece<BKM, BN_>(rb, nst + A_BYTES, n0, k1, ldb, kend, q - BM_ / 64);
+    };
+    if constexpr (SCHED == 4) {
+      // both k-halves' fragments read up front (the second half's reads land under the
+      // first half's MFMAs); DMA pieces spread over the first half's MFMA rows.
+      bf16x8 fa[2][TM], fb[2][TN];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[s][j] = frag2<BKM, BN_>(lb, wn * WN + 16 * j, 32 * s);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[s][i] = frag2<AK, BM_>(la, wm * WM + 16 * i, 32 * s);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[s][j], fa[s][i], acc[i][j], 0, 0, 0);
+          if (s == 0 && more) {
+#pragma unroll
+            for (int q = 0; q < PIECES; ++q)
+              if ((q * TM) / PIECES == i) piece(q);
+          }
+        }
+        __builtin_amdgcn_s_setprio(0);
+      }
+    } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8 fa[TM], fb[TN];
@@ -375,10 +435,28 @@ __global__ __launch_bounds__(512, 2) void gemm2_k(const bf16* __restrict__ A, co
       for (int j = 0; j < TN; ++j) fb[j] = frag2<BKM, BN_>(lb, wn * WN + 16 * j, 32 * s);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+        if (SCHED == 2 && s == 0 && more) {
+          // spread PIECES DMA instructions over the TM MFMA rows of this k-half
+#pragma unroll
+          for (int q = 0; q < PIECES; ++q)
+            if ((q * TM) / PIECES == i) piece(q);
+        }
+        if (SCHED == 3 && more) {
+          // spread them over the MFMA rows of both k-halves
+#pragma unroll
+          for (int q = 0; q < PIECES; ++q)
+            if ((q * 2 * TM) / PIECES == s * TM + i) piece(q);
+        }
+      }
       __builtin_amdgcn_s_setprio(0);
+      if (SCHED == 1 && s == 0 && more) {
+        issue_tile<AK, BM_>(ra, nst, m0, k1, lda, kend);
+        issue_tile<BKM, BN_>(rb, nst + A_BYTES, n0, k1, ldb, kend);
+      }
+    }
     }
     cur = (cur + 1 == NSTAGE) ? 0 : cur + 1;
   }
@@ -455,14 +533,40 @@ static unsigned span_bytes(long long rows, long long ld, long long cols) {
   return (unsigned)b;
 }
 
+// DMA-issue / fragment-read schedule of the 256x256 tile (gemm2_k SCHED), per layout, from
+// tools/gemm_probe.py sweeps on MI355X (profiles/r1_gemm_sched_sweep.log): NT 2 (+7 %),
+// NN and TN 4 (+16..30 % over issuing every DMA piece right after the barrier).
+static int g_v2_sched = -1;  // -1 = per-layout default
+extern "C" void dpfs_gemm_v2_sched(int v) { g_v2_sched = v; }
+template <bool AK, bool BKM>
+static int v2_sched() {
+  if (g_v2_sched >= 0) return g_v2_sched;
+  return (AK && BKM) ? 2 : 4;
+}
+
 // v2 configurations: 0 = 256x256 / 2-stage (128 KiB LDS), 1 = 256x128 / 3-stage (144 KiB).
 template <bool AK, bool BKM, int OUT>
 static void launch2(int cfg, const void* A, const void* B, void* C, const float* bias, int M, int N, int K, int lda,
                     int ldb, int ldc, int splits, int kps, long long slab, unsigned ab, unsigned bb, hipStream_t s,
                     RopeArgs rope = RopeArgs{nullptr, nullptr, 0}) {
   if (cfg == 0) {
-    gemm2_k<256, 256, 2, 2, AK, BKM, OUT><<<dim3(tiles2(M, N, 256, 256), splits), 512, 0, s>>>(
-        (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, kps, slab, ab, bb, rope);
+    const dim3 grid(tiles2(M, N, 256, 256), splits);
+    const int sched = v2_sched<AK, BKM>();
+    if (sched == 1)
+      gemm2_k<256, 256, 2, 2, AK, BKM, OUT, 1><<<grid, 512, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K,
+                                                                  lda, ldb, ldc, kps, slab, ab, bb, rope);
+    else if (sched == 2)
+      gemm2_k<256, 256, 2, 2, AK, BKM, OUT, 2><<<grid, 512, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K,
+                                                                  lda, ldb, ldc, kps, slab, ab, bb, rope);
+    else if (sched == 3)
+      gemm2_k<256, 256, 2, 2, AK, BKM, OUT, 3><<<grid, 512, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K,
+                                                                  lda, ldb, ldc, kps, slab, ab, bb, rope);
+    else if (sched == 4)
+      gemm2_k<256, 256, 2, 2, AK, BKM, OUT, 4><<<grid, 512, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K,
+                                                                  lda, ldb, ldc, kps, slab, ab, bb, rope);
+    else
+      gemm2_k<256, 256, 2, 2, AK, BKM, OUT, 0><<<grid, 512, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K,
+                                                                  lda, ldb, ldc, kps, slab, ab, bb, rope);
   } else {
     gemm2_k<256, 128, 4, 3, AK, BKM, OUT><<<dim3(tiles2(M, N, 256, 128), splits), 512, 0, s>>>(
         (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, kps, slab, ab, bb, rope);
@@ -500,7 +604,7 @@ static int bf16_splits(int M, int N, int K) {
   return v2_splits(M, N, K, pick_cfg(M, N, 1));
 }
 
-static int g_gemm_impl = 2;
+static int g_gemm_impl = 2;  // 2 = v2 (default), 1 = v1
 extern "C" void dpfs_gemm_set_impl(int v) { g_gemm_impl = v; }
 
 static thread_local float* g_ws = nullptr;  // split-K workspace for bf16 outputs (set by host)
@@ -509,6 +613,12 @@ extern "C" void dpfs_gemm_set_workspace(float* ws, long long n) {
   g_ws = ws;
   g_ws_floats = n;
 }
+extern "C" void dpfs_rope(int dtype, void* qkv, const int64_t* pos, const float* table, int M, int ld, int n_heads,
+                          int hd, int inverse, hipStream_t s);
+static void dpfs_rope_after_gemm(void* C, RopeArgs r, int M, int ldc, hipStream_t s) {
+  dpfs_rope(1, C, r.pos, r.tab, M, ldc, r.cols / 64, 64, 0, s);
+}
+
 extern "C" long long dpfs_gemm_bf16_ws(int M, int N, int K) {
   const int S = bf16_splits(M, N, K);
   return S > 1 ? (long long)S * M * N : 0;
@@ -526,15 +636,16 @@ static void bf16_gemm(const void* A, const void* B, void* C, const float* bias, 
     long long g = ((long long)M * N / 4 + 255) / 256;
     if (g > 4096) g = 4096;
     splitk_reduce_bf16_k<<<(int)g, 256, 0, s>>>(g_ws, (bf16*)C, bias, M, N, ldc, S);
+    if (rope.cols > 0) dpfs_rope_after_gemm(C, rope, M, ldc, s);
     return;
   }
   launch2<true, BKM, 0>(pick_cfg(M, N, 1), A, B, C, bias, M, N, K, lda, ldb, ldc, 1, K, 0, ab, bb, s, rope);
 }
 
-// Whether dpfs_gemm_nt_rope can fuse the rotation for this problem (else the caller runs the
-// separate RoPE kernel after the GEMM).
+// Whether dpfs_gemm_nt_rope fuses the rotation into the GEMM epilogue (hd 64; otherwise it
+// runs the separate RoPE kernel after the GEMM — same result).
 extern "C" int dpfs_gemm_rope_fusable(int M, int N, int K, int hd) {
-  return g_gemm_impl != 1 && hd == 64 && bf16_splits(M, N, K) == 1 && N % 64 == 0;
+  return g_gemm_impl != 1 && hd == 64 && N % 64 == 0;
 }
 
 extern "C" void dpfs_gemm_nt_rope(const void* A, const void* B, void* C, const float* bias, int M, int N, int K,
@@ -544,7 +655,7 @@ extern "C" void dpfs_gemm_nt_rope(const void* A, const void* B, void* C, const f
                   RopeArgs{pos, tab, rope_cols});
 }
 
-// NT: C[M,N] bf16 = A[M,K] B[N,K]^T + bias
+// NT: C[M,N] bf16 = A[M,K] B[N,K]^T (+ bias)
 extern "C" void dpfs_gemm_nt(const void* A, const void* B, void* C, const float* bias, int M, int N, int K, int lda,
                              int ldb, int ldc, hipStream_t s) {
   if (g_gemm_impl == 1) {
@@ -589,13 +700,19 @@ extern "C" int dpfs_gemm_tn_splits(int M, int N, int K) {
   return v2_splits(M, N, K, pick_cfg(M, N, 1));
 }
 
+// Floats of slab workspace dpfs_gemm_tn needs (0: none).
+extern "C" long long dpfs_gemm_tn_ws(int M, int N, int K, int accumulate) {
+  const int S = dpfs_gemm_tn_splits(M, N, K);
+  return (S > 1 || accumulate) ? (long long)S * M * N : 0;
+}
+
 // TN: C[M,N] fp32 (+)= A[K,M]^T B[K,N].  ws: splits*M*N floats when splits > 1 or accumulate.
 extern "C" void dpfs_gemm_tn(const void* A, const void* B, float* C, float* ws, int M, int N, int K, int lda, int ldb,
                              int accumulate, hipStream_t s) {
+  const long long n = (long long)M * N;
   const int S = dpfs_gemm_tn_splits(M, N, K);
   int kps = (K + S - 1) / S;
   kps = ((kps + BKK - 1) / BKK) * BKK;
-  const long long n = (long long)M * N;
   const bool direct = (S == 1 && !accumulate);
   float* dst = direct ? C : ws;
   if (tn_use_v1(M, N, K)) {

@@ -23,6 +23,7 @@ MI355X-first differences (same math):
 """
 from __future__ import annotations
 
+import os
 from dataclasses import asdict
 from typing import Optional
 
@@ -175,9 +176,17 @@ class Transformer(nn.Module):
         return self
 
     def act_dtype(self, device: torch.device) -> torch.dtype:
+        """Activation dtype: explicit ``set_compute_dtype`` > bf16 on the GPU (the MFMA kernels
+        are bf16-in / fp32-accumulate) > the reference's ``DTYPE`` env var (``model.py:153``)
+        on the CPU oracle path > the parameter dtype."""
         if self.compute_dtype is not None:
             return self.compute_dtype
-        return torch.bfloat16 if device.type == "cuda" else self.embedding.weight.dtype
+        if device.type == "cuda":
+            return torch.bfloat16
+        env = os.environ.get("DTYPE")
+        if env in ("bfloat16", "float32"):
+            return torch.bfloat16 if env == "bfloat16" else torch.float32
+        return self.embedding.weight.dtype
 
     def rope_table(self, device) -> torch.Tensor:
         key = str(device)

@@ -319,3 +319,34 @@ def test_ce_bwd_fused_bias_grad(C, M, V, valid, start):
     rdb = torch.empty(V, device=DEV)
     R.ce_bwd(logits.float(), tgt, lse, gs, start, valid, rout, rdb)
     assert _rel(out, rout) < 1e-2 and _rel(db, rdb) < 1e-3
+
+
+@pytest.mark.parametrize("impl,cfg,splits,sched", [(2, -1, 0, -1), (2, 0, 1, 0), (2, 0, 1, 1), (2, 0, 1, 2),
+                                                  (2, 0, 1, 3), (2, 0, 1, 4), (2, 1, 1, -1), (2, 0, 3, -1),
+                                                  (2, 1, 2, -1), (2, 0, 7, 4), (1, -1, 0, -1)])
+def test_gemm_plans(C, impl, cfg, splits, sched):
+    """Every GEMM variant (tile configs, K-splits, DMA schedules, v1) on ragged shapes, all
+    three layouts, TN with and without accumulate."""
+    torch.manual_seed(17)
+    M, N, K = 8200, 2104, 712
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    bt = torch.randn(N, K, device=DEV).bfloat16()
+    bn = torch.randn(K, N, device=DEV).bfloat16()
+    bias = torch.randn(N, device=DEV)
+    at = torch.randn(K, M, device=DEV).bfloat16()
+    try:
+        C.gemm_set_impl(impl)
+        C.gemm_force(cfg, splits)
+        C.gemm_v2_sched(sched)
+        assert _rel(C.gemm_nt(a, bt, bias), R.gemm_nt(a.float(), bt.float(), bias)) < 1e-2
+        assert _rel(C.gemm_nn(a, bn), R.gemm_nn(a.float(), bn.float())) < 1e-2
+        ref = R.gemm_tn(at.float(), bn.float())
+        assert _rel(C.gemm_tn(at, bn), ref) < 1e-2
+        acc = torch.randn(M, N, device=DEV)
+        want = acc + ref
+        C.gemm_tn(at, bn, acc, True)
+        assert _rel(acc, want) < 1e-2
+    finally:
+        C.gemm_set_impl(2)
+        C.gemm_force(-1, 0)
+        C.gemm_v2_sched(-1)

@@ -60,16 +60,16 @@ def main():
             w = torch.randn(nn_, k, device=dev).bfloat16()
             dy = torch.randn(m, nn_, device=dev).bfloat16()
             fl = 2.0 * m * nn_ * k
-            def v1(f):
+            def old(f, impl=1):
                 def g():
-                    C.gemm_set_impl(1)
+                    C.gemm_set_impl(impl)
                     f()
                     C.gemm_set_impl(2)
                 return g
             t = timeit({
                 "nt": lambda: C.gemm_nt(x, w, None), "nt_ref": lambda: x @ w.t(),
-                "nt_v1": v1(lambda: C.gemm_nt(x, w, None)), "nn_v1": v1(lambda: C.gemm_nn(dy, w)),
-                "tn_v1": v1(lambda: C.gemm_tn(dy, x)),
+                "nt_v1": old(lambda: C.gemm_nt(x, w, None)), "nn_v1": old(lambda: C.gemm_nn(dy, w)),
+                "tn_v1": old(lambda: C.gemm_tn(dy, x)),
                 "nn": lambda: C.gemm_nn(dy, w), "nn_ref": lambda: dy @ w,
                 "tn": lambda: C.gemm_tn(dy, x), "tn_ref": lambda: dy.t() @ x,
             })

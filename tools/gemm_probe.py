@@ -1,0 +1,50 @@
+"""Run one GEMM layout/shape repeatedly with a chosen implementation (for rocprofv3 PMC runs).
+
+    python tools/gemm_probe.py --layout nt --M 32768 --N 4096 --K 768 --impl 2 --sched 0 2 4 --iters 20
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_pytorch_from_scratch_amd.ops import _ext  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layout", default="nt", choices=["nt", "nn", "tn"])
+    ap.add_argument("--M", type=int, default=32768)
+    ap.add_argument("--N", type=int, default=4096)
+    ap.add_argument("--K", type=int, default=768)
+    ap.add_argument("--impl", type=int, nargs="+", default=[2])
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--sched", type=int, nargs="+", default=[-1])
+    a = ap.parse_args()
+    C = _ext.require()
+    M, N, K = a.M, a.N, a.K
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    w = torch.randn(N, K, device="cuda").bfloat16()
+    dy = torch.randn(M, N, device="cuda").bfloat16()
+    fn = {"nt": lambda: C.gemm_nt(x, w, None), "nn": lambda: C.gemm_nn(dy, w), "tn": lambda: C.gemm_tn(dy, x)}[a.layout]
+    for impl, sched in [(i, sc) for i in a.impl for sc in (a.sched if i == 2 else [0])]:
+        C.gemm_set_impl(impl)
+        C.gemm_v2_sched(sched)
+        for _ in range(a.iters):
+            fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / a.iters
+        print(f"impl {impl} sched {sched} {a.layout} {M}x{N}x{K}: {ms:.4f} ms {2.0 * M * N * K / ms / 1e9:.1f} TF", flush=True)
+    C.gemm_set_impl(2)
+    C.gemm_v2_sched(-1)
+
+
+if __name__ == "__main__":
+    main()

@@ -32,6 +32,8 @@ def main():
             flops = 2.0 * m * nn_ * k
             for lay, fn in ops.items():
                 variants = {}
+                if m * nn_ * 4 * 16 > 24e9:  # split-K slabs beyond a few GiB: skip the sweep
+                    continue
                 def mk(impl, cfg, sp):
                     def g():
                         C.gemm_set_impl(impl); C.gemm_force(cfg, sp)
