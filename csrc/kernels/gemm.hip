@@ -568,8 +568,13 @@ static void launch2(int cfg, const void* A, const void* B, void* C, const float*
       gemm2_k<256, 256, 2, 2, AK, BKM, OUT, 0><<<grid, 512, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K,
                                                                   lda, ldb, ldc, kps, slab, ab, bb, rope);
   } else {
-    gemm2_k<256, 128, 4, 3, AK, BKM, OUT><<<dim3(tiles2(M, N, 256, 128), splits), 512, 0, s>>>(
-        (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, kps, slab, ab, bb, rope);
+    const dim3 grid(tiles2(M, N, 256, 128), splits);
+    if (v2_sched<AK, BKM>() == 4)
+      gemm2_k<256, 128, 4, 3, AK, BKM, OUT, 4><<<grid, 512, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K,
+                                                                  lda, ldb, ldc, kps, slab, ab, bb, rope);
+    else
+      gemm2_k<256, 128, 4, 3, AK, BKM, OUT, 2><<<grid, 512, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K,
+                                                                  lda, ldb, ldc, kps, slab, ab, bb, rope);
   }
 }
 
@@ -677,16 +682,35 @@ extern "C" void dpfs_gemm_nn(const void* A, const void* B, void* C, int M, int N
   bf16_gemm<false>(A, B, C, nullptr, M, N, K, lda, ldb, ldc, span_bytes(M, lda, K), span_bytes(K, ldb, N), s);
 }
 
-// How many K-splits the TN (wgrad) launch wants; the caller sizes the slab workspace as
-// splits * M * N fp32 when splits > 1.
-// TN (wgrad) plan: v2 when the split grid reaches >= 200 blocks, else the 128x128 v1 kernel
-// (small outputs such as the QKV / FFN weight grads at TP=1 run better there).
+// TN (wgrad) plan.  Outputs are small (weight shards) and K = tokens is long, so the K-split
+// count S sets the grid.  v2 256x256: S (power of 2, K/S >= 512) minimising a makespan model
+// calibrated on MI355X sweeps (profiles/r1_gemm_tn_sweep.log, within ~10 % on every TP1-8
+// GPT-2 wgrad shape):  ceil(tiles*S / 256 CUs) * ceil(K/S / 64) * 1.95 us   (one 256x256x64
+// K-step per CU)  +  S*M*N*8 B / 4 TB/s  (fp32 slabs written + reduced).  The 128x128 v1
+// kernel when the 256-granular tiles waste > 30 % of the output (e.g. 576- or 384-row
+// shards at TP 4 / 8).
+static int tn_v2_splits(int M, int N, int K) {
+  const long long tiles = tiles2(M, N, 256, 256);
+  int best = 1;
+  double best_t = 1e300;
+  for (int S = 1; S <= 64; S *= 2) {
+    if (S > 1 && K / S < 512) break;
+    const long long kps = ((K + S - 1) / S + 63) / 64;
+    const long long rounds = (tiles * S + 255) / 256;
+    const double t = (double)rounds * kps * 1.95 + (S > 1 ? (double)S * M * N * 8.0 / 4.0e6 : 0.0);
+    if (t < best_t * 0.97) {
+      best_t = t;
+      best = S;
+    }
+  }
+  return best;
+}
+
 static bool tn_use_v1(int M, int N, int K) {
   if (g_gemm_impl == 1) return true;
   if (g_force_cfg >= 0 || g_force_splits > 0) return false;
-  const int cfg = pick_cfg(M, N, 1);
-  const int tiles = cfg == 0 ? tiles2(M, N, 256, 256) : tiles2(M, N, 256, 128);
-  return tiles * v2_splits(M, N, K, cfg) < 200;
+  const double waste = (double)tiles2(M, N, 256, 256) * 65536.0 / ((double)M * N);
+  return waste > 1.3;
 }
 
 extern "C" int dpfs_gemm_tn_splits(int M, int N, int K) {
@@ -697,7 +721,7 @@ extern "C" int dpfs_gemm_tn_splits(int M, int N, int K) {
     return s;
   }
   if (g_force_splits > 0) return g_force_splits;
-  return v2_splits(M, N, K, pick_cfg(M, N, 1));
+  return tn_v2_splits(M, N, K);
 }
 
 // Floats of slab workspace dpfs_gemm_tn needs (0: none).
@@ -720,7 +744,7 @@ extern "C" void dpfs_gemm_tn(const void* A, const void* B, float* C, float* ws, 
                                                                    N, K, lda, ldb, N, direct ? K : kps,
                                                                    direct ? 0 : n);
   } else {
-    launch2<false, false, 1>(pick_cfg(M, N, S), A, B, dst, nullptr, M, N, K, lda, ldb, N, S, direct ? K : kps,
+    launch2<false, false, 1>(g_force_cfg >= 0 ? g_force_cfg : 0, A, B, dst, nullptr, M, N, K, lda, ldb, N, S, direct ? K : kps,
                              direct ? 0 : n, span_bytes(K, lda, M), span_bytes(K, ldb, N), s);
   }
   if (direct) return;

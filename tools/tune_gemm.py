@@ -14,6 +14,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tp", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--tokens-per-tp", type=int, default=16384)
+    ap.add_argument("--layouts", nargs="+", default=["nt", "nn", "tn"])
+    ap.add_argument("--gemms", nargs="+", default=["qkv", "wo", "gate_up", "down", "lm_head"])
     a = ap.parse_args()
     C = _ext.require()
     d, f, V, H = 768, 2048, 50304, 12
@@ -30,9 +32,14 @@ def main():
             ops = {"nt": lambda: C.gemm_nt(x, w, None), "nn": lambda: C.gemm_nn(dy, w),
                    "tn": lambda: C.gemm_tn(dy, x)}
             flops = 2.0 * m * nn_ * k
+            if name not in a.gemms:
+                continue
             for lay, fn in ops.items():
+                if lay not in a.layouts:
+                    continue
                 variants = {}
-                if m * nn_ * 4 * 16 > 24e9:  # split-K slabs beyond a few GiB: skip the sweep
+                out_elems = nn_ * k if lay == "tn" else m * nn_
+                if out_elems * 4 * (32 if lay == "tn" else 4) > 24e9:  # split-K slabs beyond ~24 GB
                     continue
                 def mk(impl, cfg, sp):
                     def g():
@@ -43,7 +50,7 @@ def main():
                 variants["v1"] = mk(1, -1, 0)
                 variants["auto"] = mk(2, -1, 0)
                 for cfg in (0, 1):
-                    for sp in ((1, 2, 4) if lay != "tn" else (1, 2, 4, 8, 16)):
+                    for sp in ((1, 2, 4) if lay != "tn" else (1, 2, 4, 8, 16, 32)):
                         variants[f"c{cfg}s{sp}"] = mk(2, cfg, sp)
                 t = timeit(variants, iters=10, rounds=3)
                 best = min(t, key=t.get)
