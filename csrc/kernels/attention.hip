@@ -67,6 +67,42 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* lds, int r0, int c0) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// tr_frag through inline asm.  hipcc puts an `s_waitcnt vmcnt(0)` in front of the
+// ds_read_b64_tr_b16 builtin whenever any LDS-DMA is in flight (it cannot tell the DMA's LDS
+// destination from the read's), which drains a prefetch ring.  The asm form is invisible to
+// its bookkeeping: the caller retires the reads with tr_wait (one `s_waitcnt lgkmcnt(0)`
+// statement naming every destination "+v", guide §5.7 item 1 form (ii)) before any use,
+// and orders the LDS-DMA data with its own vmcnt + barrier.  EXEC must be all ones.
+__device__ __forceinline__ unsigned lds_u32(const char* p) {
+  return (unsigned)(size_t)((__attribute__((address_space(3))) const char*)p);
+}
+__device__ __forceinline__ s16x4 ds_tr16(const char* p) {
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_u32(p)));
+  return r;
+}
+template <int HD>
+__device__ __forceinline__ void tr_frag_asm(const char* lds, int r0, int c0, s16x4& lo, s16x4& hi) {
+  const int l = lane_id();
+  const int i = l & 15, q = i >> 2, p = i & 3, g = l >> 4;
+  const int col = c0 + 4 * p;
+  const int ch = col >> 3;
+  const int r_lo = r0 + 4 * g + q;
+  lo = ds_tr16(lds + sw_off<HD>(r_lo, ch) + (p & 1) * 8);
+  hi = ds_tr16(lds + sw_off<HD>(r_lo + 16, ch) + (p & 1) * 8);
+}
+__device__ __forceinline__ bf16x8 tr_join(const s16x4& lo, const s16x4& hi) {
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+// Retire every outstanding LDS read and pin the 8 fragments (16 halves) behind the wait.
+__device__ __forceinline__ void tr_wait8(s16x4 (&x)[16]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
+                 "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]),
+                 "+v"(x[15]));
+}
+
 // Pack two 16x16 C tiles (rows 4g+j of tile a, of tile b) into the permuted 8-slot operand.
 __device__ __forceinline__ bf16x8 pack_pt(const f32x4& a, const f32x4& b) {
   bf16x8 r;
@@ -207,14 +243,14 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd_k(const bf16*
         mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
         const float mnew = fmaxf(m[c], mx * c2);
-        const float alpha = exp2f(m[c] - mnew);
+        const float alpha = __builtin_amdgcn_exp2f(m[c] - mnew);
         m[c] = mnew;
         float ps = 0.f;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float pv = exp2f(fmaf(s[i][c][j], c2, -mnew));
+            const float pv = __builtin_amdgcn_exp2f(fmaf(s[i][c][j], c2, -mnew));
             s[i][c][j] = pv;
             ps += pv;
           }
@@ -244,6 +280,201 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd_k(const bf16*
   }
 
   // Epilogue: O[q][d] = O^T[d][q] / l ; lse = (m + log2 l) * ln2.
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    float ls = lsum[c];
+    ls += __shfl_xor(ls, 16, 64);
+    ls += __shfl_xor(ls, 32, 64);
+    const int qi = wq0 + 16 * c + (l & 15);
+    if (qi < T) {
+      const float inv = 1.f / ls;
+      bf16* orow = O + ((long long)b * T + qi) * ldo + (long long)h * HD;
+#pragma unroll
+      for (int d = 0; d < DT; ++d) {
+        bf16x4 v = {(bf16)(o[c][d][0] * inv), (bf16)(o[c][d][1] * inv), (bf16)(o[c][d][2] * inv),
+                    (bf16)(o[c][d][3] * inv)};
+        *reinterpret_cast<bf16x4*>(orow + 16 * d + 4 * g) = v;
+      }
+      if (g == 0) LSE[((long long)b * H + h) * T + qi] = (m[c] + __log2f(ls)) * kLn2;
+    }
+  }
+}
+
+// ==================================================================== forward (LDS-DMA) ==
+// NW waves x 32 queries per block; K/V tiles of 64 keys arrive by LDS-DMA
+// (buffer_load ... lds, 1 KiB per wave-instruction, swizzle applied on the source address)
+// into a 3-deep ring: tile t+2 is in flight while tile t is computed, one barrier per tile,
+// counted vmcnt (never 0 in steady state).  Rows >= T get an out-of-range offset -> zeros.
+template <int HD, int NW>
+__device__ __forceinline__ void kv_dma(__amdgpu_buffer_rsrc_t rk, __amdgpu_buffer_rsrc_t rv, char* stage, int kv0,
+                                       int T, long long ldk, long long ldv) {
+  constexpr int CPR = HD / 8;                 // 16-byte chunks per row
+  constexpr int TILE = 64 * HD * 2;
+  constexpr int P = 2 * TILE / 1024;          // pieces per K+V tile
+  constexpr int PW = P / NW;                  // per wave
+  static_assert(PW >= 1 && PW * NW == P, "pieces must divide over the waves");
+  const int l = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int j = wave + NW * i;              // piece index
+    const bool isv = j >= P / 2;
+    const int jj = isv ? j - P / 2 : j;
+    const int pos = jj * 64 + l;              // physical chunk position in the tile
+    const int r = pos / CPR, cp = pos % CPR;
+    const int ch = ((sw_off<HD>(r, cp) - r * HD * 2) >> 4);  // XOR swizzle is an involution
+    const int row = kv0 + r;
+    const long long ld = isv ? ldv : ldk;
+    const unsigned off = row < T ? (unsigned)(((long long)row * ld + ch * 8) * 2) : kOOB;
+    dma16(isv ? rv : rk, stage + (isv ? TILE : 0) + jj * 1024, off);
+  }
+}
+
+template <int HD, int NW>
+__global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd2_k(
+    const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V, bf16* __restrict__ O,
+    float* __restrict__ LSE, int T, int H, long long ldq, long long ldk, long long ldv, long long ldo, float scale,
+    int causal) {
+  constexpr int BQ = 32 * NW, BKV = 64, KT = HD / 32, DT = HD / 16;
+  constexpr int TILE = BKV * HD * 2, STAGE = 2 * TILE, NST = 3;
+  constexpr int PW = 2 * TILE / 1024 / NW;
+  __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
+  const int nqb = (T + BQ - 1) / BQ;
+  const int qb = nqb - 1 - blockIdx.x;  // heaviest first
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int q0 = qb * BQ;
+  const int wave = threadIdx.x >> 6, l = lane_id(), g = l >> 4;
+  const int wq0 = q0 + wave * 32;
+  const float c2 = scale * kLog2e;
+
+  const bf16* qbase = Q + (long long)b * T * ldq + (long long)h * HD;
+  const bf16* kbase = K + (long long)b * T * ldk + (long long)h * HD;
+  const bf16* vbase = V + (long long)b * T * ldv + (long long)h * HD;
+  const unsigned kspan = (unsigned)(((long long)(T - 1) * ldk + HD) * 2);
+  const unsigned vspan = (unsigned)(((long long)(T - 1) * ldv + HD) * 2);
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, (short)0, (int)kspan, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, (short)0, (int)vspan, 0x00020000);
+
+  const int kv_end = causal ? min(T, q0 + BQ) : T;
+  const int nkv = (kv_end + BKV - 1) / BKV;
+  kv_dma<HD, NW>(rk, rv, smem, 0, T, ldk, ldv);
+  if (nkv > 1) kv_dma<HD, NW>(rk, rv, smem + STAGE, BKV, T, ldk, ldv);
+
+  // Q^T operand in registers: lane holds Q[wq0 + 16c + (l&15)][32kk + 8g + j].
+  bf16x8 qf[2][KT];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int qi = wq0 + 16 * c + (l & 15);
+#pragma unroll
+    for (int kk = 0; kk < KT; ++kk) {
+      bf16x8 v = {};
+      if (qi < T) v = *reinterpret_cast<const bf16x8*>(qbase + (long long)qi * ldq + 32 * kk + 8 * g);
+      qf[c][kk] = v;
+    }
+  }
+
+  f32x4 o[2][DT];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int d = 0; d < DT; ++d) o[c][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m[2] = {-INFINITY, -INFINITY}, lsum[2] = {0.f, 0.f};
+
+  int cur = 0;
+  for (int t = 0; t < nkv; ++t) {
+    // tile t landed (tile t+1's pieces may still be in flight), then one barrier.
+    if (t + 1 < nkv) wait_vmcnt<PW>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    const char* lk = smem + cur * STAGE;
+    const char* lv = lk + TILE;
+    int nb = cur + 2;
+    if (nb >= NST) nb -= NST;
+    cur = (cur + 1 == NST) ? 0 : cur + 1;
+    const int kv0 = t * BKV;
+    const bool active = !causal || kv0 <= wq0 + 31;  // wave-uniform
+    bf16x8 kf[4][KT];
+    if (active) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kk = 0; kk < KT; ++kk) kf[i][kk] = row_frag<HD>(lk, 16 * i, 32 * kk);
+    }
+    if (t + 2 < nkv) kv_dma<HD, NW>(rk, rv, smem + nb * STAGE, (t + 2) * BKV, T, ldk, ldv);
+    if (!active) continue;
+    f32x4 s[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      s[i][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      s[i][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KT; ++kk) {
+        s[i][0] = MFMA(kf[i][kk], qf[0][kk], s[i][0]);
+        s[i][1] = MFMA(kf[i][kk], qf[1][kk], s[i][1]);
+      }
+    }
+    // V^T fragments via asm transposed reads (no compiler vmcnt(0) in front of them, see
+    // tr_frag_asm), issued after QK^T is under way so they land during the softmax; the
+    // sched_barrier keeps them below the compiler's lgkmcnt wait for the K reads.
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr int NVH = 4 * DT;                // s16x4 halves of the 2*DT V^T fragments
+    s16x4 vh[(NVH + 15) / 16 * 16];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int d = 0; d < DT; ++d) tr_frag_asm<HD>(lv, 32 * ks, 16 * d, vh[2 * (ks * DT + d)], vh[2 * (ks * DT + d) + 1]);
+    const bool need_mask = (causal && kv0 + BKV - 1 > wq0) || (kv0 + BKV > T);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int qi = wq0 + 16 * c + (l & 15);
+      if (need_mask) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int ki = kv0 + 16 * i + 4 * g + j;
+            if (ki >= T || (causal && ki > qi)) s[i][c][j] = -INFINITY;
+          }
+      }
+      float mx = s[0][c][0];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mx = fmaxf(mx, s[i][c][j]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m[c], mx * c2);
+      const float alpha = __builtin_amdgcn_exp2f(m[c] - mnew);
+      m[c] = mnew;
+      float ps = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float pv = __builtin_amdgcn_exp2f(fmaf(s[i][c][j], c2, -mnew));
+          s[i][c][j] = pv;
+          ps += pv;
+        }
+      lsum[c] = lsum[c] * alpha + ps;
+#pragma unroll
+      for (int d = 0; d < DT; ++d) o[c][d] *= alpha;
+    }
+#pragma unroll
+    for (int w = 0; w < (NVH + 15) / 16; ++w) tr_wait8(*reinterpret_cast<s16x4(*)[16]>(&vh[16 * w]));
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 p0 = pack_pt(s[2 * ks][0], s[2 * ks + 1][0]);
+      const bf16x8 p1 = pack_pt(s[2 * ks][1], s[2 * ks + 1][1]);
+#pragma unroll
+      for (int d = 0; d < DT; ++d) {
+        const bf16x8 vf = tr_join(vh[2 * (ks * DT + d)], vh[2 * (ks * DT + d) + 1]);
+        o[0][d] = MFMA(vf, p0, o[0][d]);
+        o[1][d] = MFMA(vf, p1, o[1][d]);
+      }
+    }
+  }
+
+
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     float ls = lsum[c];
@@ -376,7 +607,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv_k(const 
         const f32x4 dsv = *reinterpret_cast<const f32x4*>(ds + 16 * qt + 4 * g);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          float p = exp2f(fmaf(s[qt][j], c2, -lsv[j]));
+          float p = __builtin_amdgcn_exp2f(fmaf(s[qt][j], c2, -lsv[j]));
           if (need_mask) {
             const int qi = qq0 + 16 * qt + 4 * g + j;
             if (qi >= T || ki >= T || (causal && ki > qi)) p = 0.f;
@@ -552,7 +783,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            float p = exp2f(fmaf(s[i][c][j], c2, -lse2[c]));
+            float p = __builtin_amdgcn_exp2f(fmaf(s[i][c][j], c2, -lse2[c]));
             if (need_mask) {
               const int ki = kv0 + 16 * i + 4 * g + j;
               if (ki >= T || (causal && ki > qi)) p = 0.f;
@@ -620,9 +851,26 @@ using namespace dpfs;
 
 extern "C" int dpfs_attn_supported_hd(int hd) { return hd == 32 || hd == 64 || hd == 128; }
 
+static int g_attn_impl = 1;  // 1 = register-staged (default, fastest measured), 2 / 3 = LDS-DMA ring with 8 / 4 waves
+extern "C" void dpfs_attn_set_impl(int v) { g_attn_impl = v; }
+
 extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int T, int H,
                               int hd, long long ldq, long long ldk, long long ldv, long long ldo, float scale,
                               int causal, hipStream_t s) {
+  if (g_attn_impl == 2) {
+    dim3 g8((T + 255) / 256, B * H);
+    DPFS_HD_DISPATCH(hd, attn_fwd2_k<HD_, 8><<<g8, 512, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
+                                                                (bf16*)o, lse, T, H, ldq, ldk, ldv, ldo, scale,
+                                                                causal));
+    return;
+  }
+  if (g_attn_impl == 3) {
+    dim3 g4((T + 127) / 128, B * H);
+    DPFS_HD_DISPATCH(hd, attn_fwd2_k<HD_, 4><<<g4, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
+                                                                (bf16*)o, lse, T, H, ldq, ldk, ldv, ldo, scale,
+                                                                causal));
+    return;
+  }
   dim3 grid((T + 127) / 128, B * H);
   DPFS_HD_DISPATCH(hd, attn_fwd_k<HD_><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o,
                                                             lse, T, H, ldq, ldk, ldv, ldo, scale, causal));

@@ -83,6 +83,22 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return base + orig / NX;
 }
 
+// ---- LDS-DMA (buffer_load ... lds) helpers shared by the GEMM and attention kernels.
+// A per-lane source offset past the descriptor's num_records returns zeros.
+constexpr unsigned kOOB = 0xFFFFFFF0u;
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, unsigned off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, off, 0,
+                                           0, 0);
+}
+
+template <int N_>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N_ >= 0 && N_ < 64, "vmcnt range");
+  // gfx9 s_waitcnt: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]
+  __builtin_amdgcn_s_waitcnt((N_ & 15) | (7 << 4) | (15 << 8) | ((N_ >> 4) << 14));
+}
+
 }  // namespace dpfs
 
 #define DPFS_LAUNCH_CHECK() (void)hipGetLastError()

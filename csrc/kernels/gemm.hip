@@ -221,20 +221,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_k(const float* __restrict__
 //    `s_waitcnt vmcnt(pieces of t+1)` + raw s_barrier (never vmcnt(0) in steady state);
 //  * MFMA operands swapped (acc = W-frag x X-frag) so each lane owns 4 consecutive output
 //    columns of one row: bf16x4 / f32x4 vector stores and a vector bias load.
-constexpr unsigned kOOB = 0xFFFFFFF0u;
-
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, unsigned off) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, off, 0,
-                                           0, 0);
-}
-
-template <int N_>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N_ >= 0 && N_ < 64, "vmcnt range");
-  // gfx9 s_waitcnt: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]
-  __builtin_amdgcn_s_waitcnt((N_ & 15) | (7 << 4) | (15 << 8) | ((N_ >> 4) << 14));
-}
-
 // Issue the DMA of one operand tile (R rows/cols x 64 k) into LDS at `tile`.
 template <bool KMAJ, int R>
 __device__ __forceinline__ void issue_tile(__amdgpu_buffer_rsrc_t rs, char* tile, int r0, int k0, int ld, int K) {

@@ -184,7 +184,16 @@ def test_cross_entropy_kernels(C, V, valid, start):
 
 @pytest.mark.parametrize("B,T,H,hd", [(2, 256, 4, 64), (1, 300, 2, 64), (2, 130, 3, 128), (1, 64, 2, 32),
                                       (1, 1000, 2, 64)])
-def test_attention(C, B, T, H, hd):
+@pytest.mark.parametrize("impl", [2, 3, 1])
+def test_attention(C, B, T, H, hd, impl):
+    C.attn_set_impl(impl)
+    try:
+        _check_attention(C, B, T, H, hd)
+    finally:
+        C.attn_set_impl(1)
+
+
+def _check_attention(C, B, T, H, hd):
     torch.manual_seed(10)
     qkv = torch.randn(B * T, 3 * H * hd, device=DEV).bfloat16()
     q = qkv[:, : H * hd].view(B, T, H, hd)

@@ -1,0 +1,55 @@
+"""Run the attention kernels repeatedly with chosen implementations (for rocprofv3 PMC runs).
+
+    python tools/attn_probe.py --B 32 --T 1024 --H 12 --hd 64 --impl 1 2 --iters 10 [--bwd]
+"""
+import argparse
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_pytorch_from_scratch_amd.ops import _ext  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=32)
+    ap.add_argument("--T", type=int, default=1024)
+    ap.add_argument("--H", type=int, default=12)
+    ap.add_argument("--hd", type=int, default=64)
+    ap.add_argument("--impl", type=int, nargs="+", default=[2])
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--bwd", action="store_true")
+    a = ap.parse_args()
+    C = _ext.require()
+    B, T, H, hd = a.B, a.T, a.H, a.hd
+    qkv = torch.randn(B * T, 3 * H * hd, device="cuda").bfloat16()
+    q, k, v = (qkv[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+    scale = 1 / math.sqrt(hd)
+    o, lse = C.attn_fwd(q, k, v, scale, True)
+    do = torch.randn_like(o)
+    d = torch.empty_like(qkv)
+    dq, dk, dv = (d[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+    fl = 4.0 * B * H * T * T * hd / 2 * (2.5 if a.bwd else 1.0)
+    for impl in a.impl:
+        C.attn_set_impl(impl)
+        fn = (lambda: C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv)) if a.bwd else \
+            (lambda: C.attn_fwd(q, k, v, scale, True))
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / a.iters
+        print(f"impl {impl} {'bwd' if a.bwd else 'fwd'}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF", flush=True)
+    C.attn_set_impl(1)
+
+
+if __name__ == "__main__":
+    main()
