@@ -34,8 +34,8 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 # Per-GPU throughput of the reference formulation on MI355X at TP=1 (bench.py --impl reference,
-# gpt2-small, seq 1024, batch 32); see BASELINE.md.  None until measured.
-REFERENCE_TOKENS_PER_S_TP1 = None
+# gpt2-small, seq 1024, batch 32, measured on MI355X: 183.7 ms/step); see BASELINE.md.
+REFERENCE_TOKENS_PER_S_TP1 = 178376.0
 
 
 def parse():
