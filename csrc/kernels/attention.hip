@@ -114,41 +114,41 @@ __device__ __forceinline__ bf16x8 pack_pt(const f32x4& a, const f32x4& b) {
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
 // Global -> registers -> swizzled LDS tile of R rows x HD (rows >= nvalid are zero).
-template <int HD, int R>
+template <int HD, int R, int NT = 256>
 struct Stage {
   static constexpr int CPR = HD / 8;            // chunks per row
-  static constexpr int NC = R * CPR / 256;      // chunks per thread
-  static_assert(NC >= 1, "tile too small");
+  static constexpr int NCH = R * CPR;          // chunks per tile
+  static constexpr int NC = (NCH + NT - 1) / NT;  // chunks per thread (last round may be partial)
   u32x4 reg[NC];
   __device__ __forceinline__ void load(const bf16* base, long long ld, int nvalid) {
 #pragma unroll
     for (int i = 0; i < NC; ++i) {
-      const int c = threadIdx.x + 256 * i;
+      const int c = threadIdx.x + NT * i;
       const int r = c / CPR, ch = c % CPR;
       u32x4 v = {0u, 0u, 0u, 0u};
-      if (r < nvalid) v = *reinterpret_cast<const u32x4*>(base + r * ld + ch * 8);
+      if ((NCH % NT == 0 || c < NCH) && r < nvalid) v = *reinterpret_cast<const u32x4*>(base + r * ld + ch * 8);
       reg[i] = v;
     }
   }
   __device__ __forceinline__ void store(char* lds) const {
 #pragma unroll
     for (int i = 0; i < NC; ++i) {
-      const int c = threadIdx.x + 256 * i;
-      *reinterpret_cast<u32x4*>(lds + sw_off<HD>(c / CPR, c % CPR)) = reg[i];
+      const int c = threadIdx.x + NT * i;
+      if (NCH % NT == 0 || c < NCH) *reinterpret_cast<u32x4*>(lds + sw_off<HD>(c / CPR, c % CPR)) = reg[i];
     }
   }
 };
 
 // =============================================================================== forward ==
-// Block: 4 waves x 32 queries = 128 queries of one (b, h); K/V tiles of 64 keys, double
-// buffered in LDS.
-template <int HD>
-__global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
+// Block: NW waves x 32 queries of one (b, h); K/V tiles of 64 keys, double buffered in LDS
+// (measured: 4 waves beat 8, and issuing the next tile's loads after QK^T gained nothing).
+template <int HD, int NW = 4>
+__global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ V, bf16* __restrict__ O,
                                                      float* __restrict__ LSE, int T, int H, long long ldq,
                                                      long long ldk, long long ldv, long long ldo, float scale,
                                                      int causal) {
-  constexpr int BQ = 128, BKV = 64, KT = HD / 32, DT = HD / 16;
+  constexpr int BQ = 32 * NW, BKV = 64, KT = HD / 32, DT = HD / 16;
   constexpr int TILE = BKV * HD * 2;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
   const int nqb = (T + BQ - 1) / BQ;
@@ -185,7 +185,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd_k(const bf16*
 
   const int kv_end = causal ? min(T, q0 + BQ) : T;
   const int nkv = (kv_end + BKV - 1) / BKV;
-  Stage<HD, BKV> sk, sv;
+  Stage<HD, BKV, 64 * NW> sk, sv;
   sk.load(kbase, ldk, min(BKV, T));
   sv.load(vbase, ldv, min(BKV, T));
   sk.store(smem);

@@ -33,20 +33,18 @@ def main():
     d = torch.empty_like(qkv)
     dq, dk, dv = (d[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
     fl = 4.0 * B * H * T * T * hd / 2 * (2.5 if a.bwd else 1.0)
-    for impl in a.impl:
-        C.attn_set_impl(impl)
-        fn = (lambda: C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv)) if a.bwd else \
-            (lambda: C.attn_fwd(q, k, v, scale, True))
-        for _ in range(3):
-            fn()
-        torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(a.iters):
-            fn()
-        e.record()
-        torch.cuda.synchronize()
-        ms = s.elapsed_time(e) / a.iters
+    from tools.bench_kernels import timeit
+
+    def mk(impl):
+        def g():
+            C.attn_set_impl(impl)
+            if a.bwd:
+                C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv)
+            else:
+                C.attn_fwd(q, k, v, scale, True)
+        return g
+    res = timeit({impl: mk(impl) for impl in a.impl}, iters=a.iters, rounds=5)  # interleaved, median
+    for impl, ms in res.items():
         print(f"impl {impl} {'bwd' if a.bwd else 'fwd'}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF", flush=True)
     C.attn_set_impl(1)
 
