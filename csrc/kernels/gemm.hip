@@ -222,13 +222,13 @@ __global__ __launch_bounds__(256) void splitk_reduce_k(const float* __restrict__
 //  * MFMA operands swapped (acc = W-frag x X-frag) so each lane owns 4 consecutive output
 //    columns of one row: bf16x4 / f32x4 vector stores and a vector bias load.
 // Issue the DMA of one operand tile (R rows/cols x 64 k) into LDS at `tile`.
-template <bool KMAJ, int R>
+template <bool KMAJ, int R, int NWV = 8>
 __device__ __forceinline__ void issue_tile(__amdgpu_buffer_rsrc_t rs, char* tile, int r0, int k0, int ld, int K) {
   const int l = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
-  for (int i = 0; i < R / 64; ++i) {
-    const int j = wave + 8 * i;  // 1 KiB piece index
+  for (int i = 0; i < R / 8 / NWV; ++i) {
+    const int j = wave + NWV * i;  // 1 KiB piece index
     unsigned off;
     if (KMAJ) {
       const int row = 8 * j + (l >> 3);
@@ -249,12 +249,12 @@ __device__ __forceinline__ void issue_tile(__amdgpu_buffer_rsrc_t rs, char* tile
 
 // One 1 KiB DMA piece (index i < R/64) of issue_tile, for schedules that spread the
 // pieces between MFMAs.
-template <bool KMAJ, int R>
+template <bool KMAJ, int R, int NWV = 8>
 __device__ __forceinline__ void issue_piece(__amdgpu_buffer_rsrc_t rs, char* tile, int r0, int k0, int ld, int K,
                                             int i) {
   const int l = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int j = wave + 8 * i;
+  const int j = wave + NWV * i;
   unsigned off;
   if (KMAJ) {
     const int row = 8 * j + (l >> 3);
@@ -320,17 +320,22 @@ __device__ __forceinline__ void wait_tile(int remaining_after) {
 // OUT: 0 = bf16 C (+bias); 1 = fp32 C / split-K slab.
 // SCHED: 0 = all DMA pieces right after the barrier; 1 = after the first k-half's MFMAs;
 // 2 = one piece after each MFMA row of the first k-half (spreads the DMA issue cost).
-template <int BM_, int BN_, int WAVES_M, int NSTAGE, bool AK, bool BKM, int OUT, int SCHED = 0>
-__global__ __launch_bounds__(512, 2) void gemm2_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                  void* __restrict__ C, const float* __restrict__ bias, int M, int N,
-                                                  int K, int lda, int ldb, int ldc, int k_per_split,
-                                                  long long slab_stride, unsigned a_bytes, unsigned b_bytes,
-                                                  RopeArgs rope) {
-  constexpr int WAVES_N = 8 / WAVES_M;
+// NWV: waves per workgroup.  8 (two waves per SIMD) is what runs: a 4-wave variant with
+// 128x128 wave tiles (accumulators in AGPRs, one wave per SIMD) measured 20-30 % slower
+// without hand-placed software pipelining (profiles/r1_gemm_sched_sweep.log).
+template <int BM_, int BN_, int WAVES_M, int NSTAGE, bool AK, bool BKM, int OUT, int SCHED = 0, int NWV = 8>
+__global__ __launch_bounds__(64 * NWV, NWV == 8 ? 2 : 1) void gemm2_k(const bf16* __restrict__ A,
+                                                                  const bf16* __restrict__ B, void* __restrict__ C,
+                                                                  const float* __restrict__ bias, int M, int N, int K,
+                                                                  int lda, int ldb, int ldc, int k_per_split,
+                                                                  long long slab_stride, unsigned a_bytes,
+                                                                  unsigned b_bytes, RopeArgs rope) {
+  constexpr int WAVES_N = NWV / WAVES_M;
   constexpr int WM = BM_ / WAVES_M, WN = BN_ / WAVES_N;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int A_BYTES = BM_ * 128, B_BYTES = BN_ * 128, STAGE = A_BYTES + B_BYTES;
-  constexpr int PIECES = BM_ / 64 + BN_ / 64;  // DMA instructions per wave per K-step
+  constexpr int PA = BM_ / 8 / NWV, PB = BN_ / 8 / NWV;  // DMA pieces per wave per K-step
+  constexpr int PIECES = PA + PB;
   __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE];
 
   const int tiles_n = (N + BN_ - 1) / BN_;
@@ -361,8 +366,8 @@ __global__ __launch_bounds__(512, 2) void gemm2_k(const bf16* __restrict__ A, co
   for (int s0 = 0; s0 < NSTAGE - 1; ++s0) {
     if (s0 < nk) {
       char* st = smem + s0 * STAGE;
-      issue_tile<AK, BM_>(ra, st, m0, kbeg + s0 * 64, lda, kend);
-      issue_tile<BKM, BN_>(rb, st + A_BYTES, n0, kbeg + s0 * 64, ldb, kend);
+      issue_tile<AK, BM_, NWV>(ra, st, m0, kbeg + s0 * 64, lda, kend);
+      issue_tile<BKM, BN_, NWV>(rb, st + A_BYTES, n0, kbeg + s0 * 64, ldb, kend);
     }
   }
   int cur = 0;
@@ -375,14 +380,14 @@ __global__ __launch_bounds__(512, 2) void gemm2_k(const bf16* __restrict__ A, co
     char* nst = smem + nb * STAGE;
     const int k1 = kbeg + (t + NSTAGE - 1) * 64;
     if (SCHED == 0 && more) {
-      issue_tile<AK, BM_>(ra, nst, m0, k1, lda, kend);
-      issue_tile<BKM, BN_>(rb, nst + A_BYTES, n0, k1, ldb, kend);
+      issue_tile<AK, BM_, NWV>(ra, nst, m0, k1, lda, kend);
+      issue_tile<BKM, BN_, NWV>(rb, nst + A_BYTES, n0, k1, ldb, kend);
     }
     const char* la = smem + cur * STAGE;
     const char* lb = la + A_BYTES;
     auto piece = [&](int q) {
-      if (q < BM_ / 64) issue_piece<AK, BM_>(ra, nst, m0, k1, lda, kend, q);
-      else issue_piece<BKM, BN_>(rb, nst + A_BYTES, n0, k1, ldb, kend, q - BM_ / 64);
+      if (q < PA) issue_piece<AK, BM_, NWV>(ra, nst, m0, k1, lda, kend, q);
+      else issue_piece<BKM, BN_, NWV>(rb, nst + A_BYTES, n0, k1, ldb, kend, q - PA);
     };
     if constexpr (SCHED == 4) {
       // both k-halves' fragments read up front (the second half's reads land under the
@@ -439,8 +444,8 @@ __global__ __launch_bounds__(512, 2) void gemm2_k(const bf16* __restrict__ A, co
       }
       __builtin_amdgcn_s_setprio(0);
       if (SCHED == 1 && s == 0 && more) {
-        issue_tile<AK, BM_>(ra, nst, m0, k1, lda, kend);
-        issue_tile<BKM, BN_>(rb, nst + A_BYTES, n0, k1, ldb, kend);
+        issue_tile<AK, BM_, NWV>(ra, nst, m0, k1, lda, kend);
+        issue_tile<BKM, BN_, NWV>(rb, nst + A_BYTES, n0, k1, ldb, kend);
       }
     }
     }
@@ -450,7 +455,9 @@ __global__ __launch_bounds__(512, 2) void gemm2_k(const bf16* __restrict__ A, co
   // Epilogue: acc[i][j] = C^T tile: lane holds C[m = .. + (l&15)][n = .. + 4g + r], r < 4.
   const int g = l >> 4;
   const int wcol0 = n0 + wn * WN;
-  const bool do_rope = (OUT == 0) && (WN == 64) && (TN == 4) && rope.cols > 0 && wcol0 < rope.cols;
+  // RoPE needs each 64-column head inside one wave (WN % 64 == 0): head hg of the wave is
+  // tiles 4hg..4hg+3 and column d's partner d + 32 is tile + 2 in the same lane.
+  const bool do_rope = (OUT == 0) && (WN % 64 == 0) && rope.cols > 0 && wcol0 < rope.cols;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = m0 + wm * WM + 16 * i + (l & 15);
@@ -462,16 +469,20 @@ __global__ __launch_bounds__(512, 2) void gemm2_k(const bf16* __restrict__ A, co
       const int n = wcol0 + 16 * j + 4 * g;
       if (OUT == 0 && bias && n < N) v[j] += *reinterpret_cast<const f32x4*>(bias + n);
     }
-    if constexpr (OUT == 0 && TN == 4) {
+    if constexpr (OUT == 0 && WN % 64 == 0) {
       if (do_rope) {
         const float* tr = rope.tab + rope.pos[m] * 64;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const f32x4 cs = *reinterpret_cast<const f32x4*>(tr + 16 * j + 4 * g);
-          const f32x4 sn = *reinterpret_cast<const f32x4*>(tr + 32 + 16 * j + 4 * g);
-          const f32x4 x1 = v[j], x2 = v[j + 2];
-          v[j] = x1 * cs - x2 * sn;
-          v[j + 2] = x2 * cs + x1 * sn;
+        for (int hg = 0; hg < WN / 64; ++hg) {
+          if (wcol0 + 64 * hg >= rope.cols) break;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const f32x4 cs = *reinterpret_cast<const f32x4*>(tr + 16 * j + 4 * g);
+            const f32x4 sn = *reinterpret_cast<const f32x4*>(tr + 32 + 16 * j + 4 * g);
+            const f32x4 x1 = v[4 * hg + j], x2 = v[4 * hg + j + 2];
+            v[4 * hg + j] = x1 * cs - x2 * sn;
+            v[4 * hg + j + 2] = x2 * cs + x1 * sn;
+          }
         }
       }
     }

@@ -1,0 +1,44 @@
+"""bench.py driver contract on CPU/gloo: one JSON line from rank 0 with the required fields,
+for a single process and for a torch.distributed.run launch with 2 ranks (TP = 2)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config"}
+
+
+def _env():
+    e = dict(os.environ, PYTHONPATH=ROOT, MASTER_ADDR="127.0.0.1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        e.pop(k, None)
+    return e
+
+
+def _json_lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_bench_prints_one_json_line(world):
+    from dist_helpers import _free_port
+    args = ["--gpus", str(world), "--model", "plumbing", "--steps", "2", "--warmup", "1", "--seq-len", "64",
+            "--batch-per-gpu", "2"]
+    if world == 1:
+        cmd = [sys.executable, "bench.py"] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py"] + args
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    d = lines[0]
+    assert REQUIRED <= d.keys()
+    assert d["n_gpus"] == world and d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "weak"
+    assert d["config"]["parallelism"] == f"tp{world}" and d["config"]["global_batch"] == 2 * world
+    assert d["value"] > 0 and d["higher_is_better"] is True

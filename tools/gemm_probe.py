@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--impl", type=int, nargs="+", default=[2])
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--sched", type=int, nargs="+", default=[-1])
+    ap.add_argument("--cfg", type=int, nargs="+", default=[-1])
     a = ap.parse_args()
     C = _ext.require()
     M, N, K = a.M, a.N, a.K
@@ -28,9 +29,10 @@ def main():
     w = torch.randn(N, K, device="cuda").bfloat16()
     dy = torch.randn(M, N, device="cuda").bfloat16()
     fn = {"nt": lambda: C.gemm_nt(x, w, None), "nn": lambda: C.gemm_nn(dy, w), "tn": lambda: C.gemm_tn(dy, x)}[a.layout]
-    for impl, sched in [(i, sc) for i in a.impl for sc in (a.sched if i == 2 else [0])]:
+    for impl, sched, cfg in [(i, sc, cf) for i in a.impl for sc in (a.sched if i == 2 else [0]) for cf in a.cfg]:
         C.gemm_set_impl(impl)
         C.gemm_v2_sched(sched)
+        C.gemm_force(cfg, 0)
         for _ in range(a.iters):
             fn()
         torch.cuda.synchronize()
@@ -41,9 +43,10 @@ def main():
         e.record()
         torch.cuda.synchronize()
         ms = s.elapsed_time(e) / a.iters
-        print(f"impl {impl} sched {sched} {a.layout} {M}x{N}x{K}: {ms:.4f} ms {2.0 * M * N * K / ms / 1e9:.1f} TF", flush=True)
+        print(f"impl {impl} sched {sched} cfg {cfg} {a.layout} {M}x{N}x{K}: {ms:.4f} ms {2.0 * M * N * K / ms / 1e9:.1f} TF", flush=True)
     C.gemm_set_impl(2)
     C.gemm_v2_sched(-1)
+    C.gemm_force(-1, 0)
 
 
 if __name__ == "__main__":
