@@ -170,6 +170,10 @@ def main():
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
+        if os.environ.get("DPFS_BENCH_VERBOSE"):
+            from distributed_pytorch_from_scratch_amd.ops import gemm_select
+            for key, c in sorted(gemm_select.choices().items(), key=str):
+                print(f"gemm {key}: {c}", file=sys.stderr, flush=True)
     dist.barrier()
     dist.destroy_process_group()
 

@@ -40,6 +40,7 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
+from ..ops import gemm_select as GS
 from ..ops.dispatch import K, shadow
 from ..parallel import process_manager as pm
 
@@ -133,7 +134,7 @@ class DecoderTrainFn(torch.autograd.Function):
                 q, kk, v = _split(qkv, Bc, T, L.h, L.hd)
                 o, lse = k.attn_fwd(q, kk, v, 1.0 / math.sqrt(L.hd), True)
                 o2 = o.view(Mc, L.h * L.hd)
-                pout = k.gemm_nt(o2, W(L.wo), None)
+                pout = GS.gemm_nt(k, o2, W(L.wo), None)
                 s["layers"].append(dict(x=x, r1=r1, h1=h1, qkv=qkv, o=o, lse=lse))
                 s["pend"], s["pend_bias"], s["h"] = pout, L.bo, _ar(pout)
             # seg2: wait + bias + residual, norm2, gate|up, SwiGLU, down -> async all-reduce
@@ -141,9 +142,9 @@ class DecoderTrainFn(torch.autograd.Function):
                 _wait(s["h"])
                 x2 = k.bias_residual(s["pend"], s["pend_bias"], s["x"])
                 h2, r2 = k.rmsnorm_fwd(x2, L.s2, L.eps2)
-                gu = k.gemm_nt(h2, W(L.wgu), L.bgu)
+                gu = GS.gemm_nt(k, h2, W(L.wgu), L.bgu)
                 sw = k.swiglu_fwd(gu)
-                qout = k.gemm_nt(sw, W(L.wd), None)
+                qout = GS.gemm_nt(k, sw, W(L.wd), None)
                 s["layers"][-1].update(x2=x2, r2=r2, h2=h2, gu=gu, sw=sw)
                 s["x"] = x2
                 s["pend"], s["pend_bias"], s["h"] = qout, L.bd, _ar(qout)
@@ -154,7 +155,7 @@ class DecoderTrainFn(torch.autograd.Function):
             _wait(s["h"])
             xf = k.bias_residual(s["pend"], s["pend_bias"], s["x"])
             hf, rf = k.rmsnorm_fwd(xf, model.norm.scale, model.norm.eps)
-            logits = k.gemm_nt(hf, W(head.weight), head.bias)
+            logits = GS.gemm_nt(k, hf, W(head.weight), head.bias)
             stats = k.ce_fwd_stats(logits, s["tgt"], vst, vvalid)
             if tp > 1:
                 allst = stats.new_empty((tp * stats.size(0), 3))
@@ -210,7 +211,7 @@ class DecoderTrainFn(torch.autograd.Function):
             dl = s["logits"]
             db = dl.new_empty(dl.size(1), dtype=torch.float32) if head.bias is not None else None
             k.ce_bwd(dl, s["tgt"], s["ce_lse"], gs, vst, vvalid, dl, db)    # + lm_head bias grad
-            dh = k.gemm_nn(dl, W(head.weight))
+            dh = GS.gemm_nn(k, dl, W(head.weight))
             s["bh"] = _ar(dh)
             s["dpend"] = dh
             tn(g, "lm_w", dl, s["hf"])
@@ -234,11 +235,11 @@ class DecoderTrainFn(torch.autograd.Function):
                 a = s["layers"][li]
                 gq = s["g"]
                 bias_acc(G, "bd", gq, L.bd)
-                ds = k.gemm_nn(gq, W(L.wd))
+                ds = GS.gemm_nn(k, gq, W(L.wd))
                 tn(G, "wd", gq, a["sw"])
                 dbgu = ds.new_empty(a["gu"].size(1), dtype=torch.float32) if L.bgu is not None else None
                 dgu = k.swiglu_bwd(ds, a["gu"], dbgu)     # + gate|up bias grad in the same pass
-                dh2 = k.gemm_nn(dgu, W(L.wgu))
+                dh2 = GS.gemm_nn(k, dgu, W(L.wgu))
                 s["bh"], s["dpend"] = _ar(dh2), dh2
                 tn(G, "wgu", dgu, a["h2"])
                 if dbgu is not None:
@@ -251,7 +252,7 @@ class DecoderTrainFn(torch.autograd.Function):
                 g2, ds2 = k.rmsnorm_bwd(s["dpend"], a["x2"], L.s2, a["r2"], s["g"])  # + residual grad
                 G["s2"] = _addg(G.get("s2"), ds2)
                 bias_acc(G, "bo", g2, L.bo)
-                do = k.gemm_nn(g2, W(L.wo))
+                do = GS.gemm_nn(k, g2, W(L.wo))
                 tn(G, "wo", g2, a["o"].view(g2.size(0), -1))
                 Bc = s["B"]
                 q, kk, v = _split(a["qkv"], Bc, T, L.h, L.hd)
@@ -259,7 +260,7 @@ class DecoderTrainFn(torch.autograd.Function):
                 dq, dk, dv = _split(dqkv, Bc, T, L.h, L.hd)
                 k.attn_bwd(do.view(Bc, T, L.h, L.hd), q, kk, v, a["o"], a["lse"], 1.0 / math.sqrt(L.hd), True,
                            dq, dk, dv, s["pos"], tab)   # inverse RoPE fused into the dq/dk stores
-                dh = k.gemm_nn(dqkv, W(L.wqkv))
+                dh = GS.gemm_nn(k, dqkv, W(L.wqkv))
                 s["bh"], s["dpend"] = _ar(dh), dh
                 tn(G, "wqkv", dqkv, a["h1"])
                 bias_acc(G, "bqkv", dqkv, L.bqkv)

@@ -83,7 +83,11 @@ class FusedAdam(torch.optim.Optimizer):
             coef = self._clip_coef(params) if self.max_grad_norm else None
             if params[0].is_cuda:
                 C = _ext.require()
-                shadows = [self._shadow_for(p) if p.dim() >= 2 else None for p in params]
+                from .dispatch import peek_shadow
+                # 2-D weights always carry a bf16 compute shadow; 1-D params only when a GEMM
+                # epilogue reads one (a hipBLASLt bias, ops.gemm_select).
+                shadows = [self._shadow_for(p) if (p.dim() >= 2 or peek_shadow(p) is not None) else None
+                           for p in params]
                 key = tuple((p.data_ptr(), p.grad.data_ptr(), s.data_ptr() if s is not None else 0)
                             for p, s in zip(params, shadows))
                 tab = self._tables.get(gi)

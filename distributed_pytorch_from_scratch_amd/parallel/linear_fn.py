@@ -30,6 +30,7 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+from ..ops import gemm_select as GS
 from ..ops.dispatch import K, shadow
 from . import comm_ops
 from . import process_manager as pm
@@ -53,7 +54,7 @@ class ColumnParallelLinearFn(torch.autograd.Function):
         if sequence_parallel:
             x = comm_ops.all_gather_rows(x)
         w = _compute_w(weight, x)
-        y = k.gemm_nt(x, w, bias)
+        y = GS.gemm_nt(k, x, w, bias)
         # In SP mode keep only the shard; the full activation is re-gathered in backward.
         ctx.save_for_backward(x_in, weight, bias)
         ctx.sp = sequence_parallel
@@ -69,13 +70,13 @@ class ColumnParallelLinearFn(torch.autograd.Function):
         handle = None
         if ctx.sp:
             xg, hg = comm_ops.all_gather_rows(x2, async_op=True)
-            dx_full = k.gemm_nn(dy2, w)
+            dx_full = GS.gemm_nn(k, dy2, w)
             if hg is not None:
                 hg.wait()
             dx = comm_ops.reduce_scatter_rows(dx_full)
             x_for_w = xg
         else:
-            dx = k.gemm_nn(dy2, w)
+            dx = GS.gemm_nn(k, dy2, w)
             if ctx.ar:
                 handle = comm_ops.all_reduce_(dx, async_op=True)
             x_for_w = x2
@@ -91,7 +92,7 @@ class RowParallelLinearFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, sequence_parallel: bool, reduce_output: bool):
         k = K(x)
         w = _compute_w(weight, x)
-        y = k.gemm_nt(x, w, None)
+        y = GS.gemm_nt(k, x, w, None)
         if sequence_parallel:
             y = comm_ops.reduce_scatter_rows(y)
         elif reduce_output:
@@ -111,7 +112,7 @@ class RowParallelLinearFn(torch.autograd.Function):
         if ctx.sp:
             dy2 = comm_ops.all_gather_rows(dy2)
         w = _compute_w(weight, dy2)
-        dx = k.gemm_nn(dy2, w)
+        dx = GS.gemm_nn(k, dy2, w)
         dw = k.gemm_tn(dy2, x2).to(weight.dtype) if weight.requires_grad else None
         return dx, dw, db, None, None
 

@@ -121,3 +121,30 @@ def test_fused_engine_matches_modular_path_and_chunks(dist1):
         for n, g in res["modular"][1].items():
             rel = ((res[mode][1][n] - g).norm() / (g.norm() + 1e-12)).item()
             assert rel < 2e-2, (mode, n, rel)
+
+
+def test_gemm_backend_selection_agrees(dist1, monkeypatch):
+    """Plain GEMMs may run on hipBLASLt when it measures faster (ops.gemm_select); every
+    backend choice gives the same loss and gradients within bf16 tolerance."""
+    from distributed_pytorch_from_scratch_amd.models import get_preset, Transformer
+    from distributed_pytorch_from_scratch_amd.ops import gemm_select
+    from distributed_pytorch_from_scratch_amd.utils.dist import set_seed
+    args = get_preset("gpt2-small", num_layers=2)
+    m = Transformer.from_args(args).cuda()
+    set_seed(0)
+    m.reset_parameters()
+    ids = torch.randint(0, args.vocab_size, (4, 256), device="cuda")
+    pos = torch.arange(256, device="cuda").repeat(4, 1)
+    res = {}
+    for backend in ("ours", "blas", "auto"):
+        monkeypatch.setenv("DPFS_GEMM_BACKEND", backend)
+        m.zero_grad(set_to_none=True)
+        loss = m.loss(ids, pos, ids)
+        loss.backward()
+        res[backend] = (loss.item(), m.lm_head.weight.grad.clone(), m.layers[0].ffn.gate_up.weight.grad.clone())
+    assert gemm_select.choices(), "auto mode recorded no per-shape decision"
+    for b in ("blas", "auto"):
+        assert abs(res[b][0] - res["ours"][0]) < 1e-2
+        for i in (1, 2):
+            rel = ((res[b][i] - res["ours"][i]).norm() / res["ours"][i].norm()).item()
+            assert rel < 2e-2, (b, i, rel)
