@@ -58,6 +58,7 @@ def get_test_args(argv=None):
     g = p.add_argument_group("decode")
     g.add_argument("--max_decode_len", type=int, default=128)
     g.add_argument("--synthetic_prompts", action="store_true")
+    g.add_argument("--no_kv_cache", action="store_true", help="re-run the full prefix per token (reference)")
     g = p.add_argument_group("other")
     g.add_argument("--random_seed", type=int, default=0)
     g.add_argument("--device", type=str, default=None)
@@ -80,7 +81,20 @@ def calc_loss(model: Transformer, dataloader, dev) -> float:
 
 
 @torch.inference_mode()
-def greedy_decode(model: Transformer, prompt_ids, bos: int, eos: int, max_len: int, dev):
+def greedy_decode(model: Transformer, prompt_ids, bos: int, eos: int, max_len: int, dev, kv_cache: bool = True):
+    """Greedy continuation of ``[bos] + prompt`` until EOS or ``max_len + 1`` tokens (the
+    reference's stopping rule, ``test.py:144-150``); returns the ids after BOS without EOS.
+    ``kv_cache`` decodes one token per step against cached keys/values
+    (``models/generation.py``); ``False`` re-runs the whole prefix per token like the reference."""
+    if kv_cache:
+        from .models.generation import generate
+        n0 = 1 + len(prompt_ids)
+        tokens = torch.tensor([bos] + list(prompt_ids), dtype=torch.long, device=dev).view(1, -1)
+        out = generate(model, tokens, max_new_tokens=max(1, max_len + 1 - n0), eos_id=eos)[0]
+        out = out[1:]
+        if out and out[-1] == eos and len(out) > len(prompt_ids):
+            out = out[:-1]
+        return out
     tokens = torch.tensor([bos] + list(prompt_ids), dtype=torch.long, device=dev).view(1, -1)
     while True:
         pos = torch.arange(tokens.size(1), device=dev).unsqueeze(0)
@@ -135,7 +149,7 @@ def test(rank, args):
         for i in range(4):
             g = torch.Generator().manual_seed(i)
             ids = torch.randint(3, margs.vocab_size, (8,), generator=g).tolist()
-            out = greedy_decode(model, ids, ds.bos, ds.eos, args.max_decode_len, dev)
+            out = greedy_decode(model, ids, ds.bos, ds.eos, args.max_decode_len, dev, not args.no_kv_cache)
             assert out[:len(ids)] == ids
             decoded.append((str(ids), str(out[len(ids):])))
     else:
@@ -145,7 +159,7 @@ def test(rank, args):
         for t in PROMPTS:
             t = t.strip()
             ids = tok.encode(t).ids
-            out = greedy_decode(model, ids, ds.bos, ds.eos, args.max_decode_len, dev)
+            out = greedy_decode(model, ids, ds.bos, ds.eos, args.max_decode_len, dev, not args.no_kv_cache)
             text = tok.decode(out).strip()
             decoded.append((t, text[len(t):] if text.startswith(t) else text))
     with open(save_path, "a") as fp:
