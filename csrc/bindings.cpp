@@ -44,6 +44,9 @@ void dpfs_rope(int, void*, const int64_t*, const float*, int, int, int, int, int
 void dpfs_bias_residual(int, const void*, const float*, const void*, void*, int, int, hipStream_t);
 long long dpfs_colsum_ws(int, int);
 long long dpfs_norm_bwd_ws(int, int, int);
+void dpfs_add_rmsnorm_fwd(int, const void*, const float*, const void*, const float*, void*, void*, float*, int, int,
+                          float, hipStream_t);
+int dpfs_norm_bwd_grid(int);
 void dpfs_bias_grad(int, const void*, float*, float*, int, int, hipStream_t);
 void dpfs_embedding_fwd(int, const int64_t*, const float*, void*, int, int, long long, int, hipStream_t);
 void dpfs_embedding_bwd(int, const void*, const int64_t*, float*, int, int, long long, int, hipStream_t);
@@ -255,8 +258,36 @@ std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, torch::Tensor w, double 
   return {y, rstd};
 }
 
+// (x = y + bias + res, RMSNorm(x), rstd) in one pass: the residual epilogue of a row-parallel
+// projection fused into the next norm.
+std::vector<torch::Tensor> add_rmsnorm_fwd(torch::Tensor y, c10::optional<torch::Tensor> bias, torch::Tensor res,
+                                           torch::Tensor w, double eps) {
+  const int dt = check_norm_x(res, w);
+  TORCH_CHECK(y.sizes() == res.sizes() && y.is_contiguous() && y.scalar_type() == res.scalar_type(),
+              "add_rmsnorm_fwd: y must match res");
+  const at::DeviceGuard g(res.device());
+  const int64_t M = res.size(0), D = res.size(1);
+  const float* bp = opt_f32(bias, D, "bias");
+  auto x = torch::empty_like(res);
+  auto h = torch::empty_like(res);
+  auto rstd = torch::empty({M}, res.options().dtype(torch::kFloat32));
+  if (M)
+    dpfs_add_rmsnorm_fwd(dt, y.data_ptr(), bp, res.data_ptr(), w.data_ptr<float>(), x.data_ptr(), h.data_ptr(),
+                         rstd.data_ptr<float>(), (int)M, (int)D, (float)eps, stream());
+  return {x, h, rstd};
+}
+
+static float* dbias_out(const c10::optional<torch::Tensor>& db, int64_t n, const char* what) {
+  if (!db.has_value() || !db->defined()) return nullptr;
+  TORCH_CHECK(db->is_cuda() && db->scalar_type() == torch::kFloat32 && db->is_contiguous() && db->numel() == n, what,
+              ": dbias must be contiguous fp32 [", n, "]");
+  return db->data_ptr<float>();
+}
+
+// dx = RMSNorm'(dy) (+ dres); with `dbias` also the column sums of dx (the bias grad of the
+// projection whose output gradient dx is), from the same pass.
 std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor rstd,
-                                       c10::optional<torch::Tensor> dres) {
+                                       c10::optional<torch::Tensor> dres, c10::optional<torch::Tensor> dbias) {
   const int dt = check_norm_x(x, w);
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.is_contiguous() && dy.scalar_type() == x.scalar_type(), "rmsnorm_bwd: dy");
   const void* rp = nullptr;
@@ -267,12 +298,20 @@ std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch:
   }
   const at::DeviceGuard g(x.device());
   const int64_t M = x.size(0), D = x.size(1);
+  float* db = dbias_out(dbias, x.size(1), "rmsnorm_bwd");
   auto dx = torch::empty_like(x);
   auto dw = torch::empty({D}, w.options());
-  if (M == 0) return {dx, dw.zero_()};
-  auto ws = torch::empty({(int64_t)dpfs_norm_bwd_ws(0, (int)M, (int)D)}, w.options());
-  dpfs_norm_bwd(0, dt, dy.data_ptr(), x.data_ptr(), w.data_ptr<float>(), nullptr, rstd.data_ptr<float>(), rp, dx.data_ptr(),
-                dw.data_ptr<float>(), nullptr, ws.data_ptr<float>(), nullptr, (int)M, (int)D, stream());
+  if (M == 0) {
+    if (db) dbias->zero_();
+    return {dx, dw.zero_()};
+  }
+  const int mode = db ? 2 : 0;
+  const int G = dpfs_norm_bwd_grid((int)M);
+  auto ws = torch::empty({(int64_t)dpfs_norm_bwd_ws(mode, (int)M, (int)D)}, w.options());
+  float* pw = ws.data_ptr<float>();
+  dpfs_norm_bwd(mode, dt, dy.data_ptr(), x.data_ptr(), w.data_ptr<float>(), nullptr, rstd.data_ptr<float>(), rp,
+                dx.data_ptr(), dw.data_ptr<float>(), db, pw, db ? pw + (int64_t)G * D : nullptr, (int)M, (int)D,
+                stream());
   return {dx, dw};
 }
 
@@ -321,12 +360,6 @@ torch::Tensor swiglu_fwd(torch::Tensor gu) {
   return h;
 }
 
-static float* dbias_out(const c10::optional<torch::Tensor>& db, int64_t n, const char* what) {
-  if (!db.has_value() || !db->defined()) return nullptr;
-  TORCH_CHECK(db->is_cuda() && db->scalar_type() == torch::kFloat32 && db->is_contiguous() && db->numel() == n, what,
-              ": dbias must be contiguous fp32 [", n, "]");
-  return db->data_ptr<float>();
-}
 
 // dgu = SwiGLU'(gu) * dh; with `dbias` the gate|up bias gradient (column sums of dgu) is
 // written there by the same pass.
@@ -592,8 +625,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("add_bias_", &add_bias_);
   m.def("bias_residual", &bias_residual);
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("add_rmsnorm_fwd", &add_rmsnorm_fwd, py::arg("y"), py::arg("bias"), py::arg("res"), py::arg("w"),
+        py::arg("eps"));
   m.def("rmsnorm_bwd", &rmsnorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("rstd"),
-        py::arg("dres") = py::none());
+        py::arg("dres") = py::none(), py::arg("dbias") = py::none());
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("swiglu_fwd", &swiglu_fwd);

@@ -61,6 +61,54 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_k(const T* __restrict__ x, co
   }
 }
 
+// Residual add fused into the norm: xo = y + bias + res (the post-all-reduce epilogue of a
+// row-parallel projection), written once; then RMSNorm of the rounded xo.
+// Same rounding as bias_residual followed by rmsnorm_fwd.
+template <typename T, int VPL>
+__global__ __launch_bounds__(256) void add_rmsnorm_fwd_k(const T* __restrict__ yin, const float* __restrict__ bias,
+                                                         const T* __restrict__ res, const float* __restrict__ w,
+                                                         T* __restrict__ xo, T* __restrict__ y,
+                                                         float* __restrict__ rstd, int M, int D, float eps) {
+  constexpr int N = Vec<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const size_t off = (size_t)row * D;
+  const int nvec = D / N;
+  float v[VPL][N];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + i * 64;
+    if (c < nvec) {
+      float a[N], b[N];
+      load_vec<T>(yin + off + c * N, a);
+      load_vec<T>(res + off + c * N, b);
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        float t = a[j] + b[j];
+        if (bias) t += bias[c * N + j];
+        v[i][j] = to_f(from_f<T>(t));
+        ss += v[i][j] * v[i][j];
+      }
+      store_vec<T>(xo + off + c * N, v[i]);
+    }
+  }
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / (float)D + eps);
+  if (lane == 0) rstd[row] = r;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + i * 64;
+    if (c < nvec) {
+      float o[N];
+#pragma unroll
+      for (int j = 0; j < N; ++j) o[j] = to_f(from_f<T>(v[i][j] * r)) * w[c * N + j];
+      store_vec<T>(y + off + c * N, o);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------ LayerNorm fwd --
 template <typename T, int VPL>
 __global__ __launch_bounds__(256) void layernorm_fwd_k(const T* __restrict__ x, const float* __restrict__ w,
@@ -149,7 +197,7 @@ __global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, cons
           dot += g[i][j] * xh[i][j];
           gs += g[i][j];
           aw[i][j] += dv[j] * xh[i][j];
-          ab[i][j] += dv[j];
+          if (MODE == 1) ab[i][j] += dv[j];
         }
       }
     }
@@ -169,6 +217,10 @@ __global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, cons
 #pragma unroll
           for (int j = 0; j < N; ++j) o[j] += rv[j];
         }
+        if (MODE == 2) {  // column sums of the output: the bias grad of the layer below
+#pragma unroll
+          for (int j = 0; j < N; ++j) ab[i][j] += o[j];
+        }
         store_vec<T>(dxr + c * N, o);
       }
     }
@@ -185,10 +237,10 @@ __global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, cons
             const int col = c * N + j;
             if (wv == 0) {
               red[col] = aw[i][j];
-              if (MODE == 1) red[D + col] = ab[i][j];
+              if (MODE != 0) red[D + col] = ab[i][j];
             } else {
               red[col] += aw[i][j];
-              if (MODE == 1) red[D + col] += ab[i][j];
+              if (MODE != 0) red[D + col] += ab[i][j];
             }
           }
         }
@@ -198,7 +250,7 @@ __global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, cons
   }
   for (int col = threadIdx.x; col < D; col += blockDim.x) {
     partial_w[(size_t)blockIdx.x * D + col] = red[col];
-    if (MODE == 1) partial_b[(size_t)blockIdx.x * D + col] = red[D + col];
+    if (MODE != 0) partial_b[(size_t)blockIdx.x * D + col] = red[D + col];
   }
 }
 
@@ -237,7 +289,7 @@ extern "C" int dpfs_norm_bwd_grid(int M) { return norm_bwd_grid(M); }
 // Total fp32 workspace of dpfs_norm_bwd: block partials (x2 for LayerNorm) + stage-2 partials.
 extern "C" long long dpfs_norm_bwd_ws(int mode, int M, int D) {
   const int G = norm_bwd_grid(M);
-  return (long long)G * D * (mode == 1 ? 2 : 1) + dpfs_colsum_ws(G, D);
+  return (long long)G * D * (mode != 0 ? 2 : 1) + dpfs_colsum_ws(G, D);
 }
 
 extern "C" void dpfs_rmsnorm_fwd(int dtype, const void* x, const float* w, void* y, float* rstd, int M, int D,
@@ -249,6 +301,18 @@ extern "C" void dpfs_rmsnorm_fwd(int dtype, const void* x, const float* w, void*
   } else {
     DPFS_VPL_DISPATCH(vpl_for<float>(D), rmsnorm_fwd_k<float, VPL><<<grid, 256, 0, s>>>(
         (const float*)x, w, (float*)y, rstd, M, D, eps));
+  }
+}
+
+extern "C" void dpfs_add_rmsnorm_fwd(int dtype, const void* yin, const float* bias, const void* res, const float* w,
+                                     void* xo, void* y, float* rstd, int M, int D, float eps, hipStream_t s) {
+  dim3 grid((M + kRowsPerBlock - 1) / kRowsPerBlock);
+  if (dtype == kBF16) {
+    DPFS_VPL_DISPATCH(vpl_for<bf16>(D), add_rmsnorm_fwd_k<bf16, VPL><<<grid, 256, 0, s>>>(
+        (const bf16*)yin, bias, (const bf16*)res, w, (bf16*)xo, (bf16*)y, rstd, M, D, eps));
+  } else {
+    DPFS_VPL_DISPATCH(vpl_for<float>(D), add_rmsnorm_fwd_k<float, VPL><<<grid, 256, 0, s>>>(
+        (const float*)yin, bias, (const float*)res, w, (float*)xo, (float*)y, rstd, M, D, eps));
   }
 }
 
@@ -264,24 +328,25 @@ extern "C" void dpfs_layernorm_fwd(int dtype, const void* x, const float* w, con
   }
 }
 
-// mode 0 = rms, 1 = layernorm.  partial_w/partial_b: [dpfs_norm_bwd_grid(M), D] workspace.
+// mode 0 = rms, 1 = layernorm, 2 = rms + column sums of dx (the bias grad of the layer whose
+// output grad dx is) into db.  partial_w/partial_b: [dpfs_norm_bwd_grid(M), D] workspace.
 extern "C" void dpfs_norm_bwd(int mode, int dtype, const void* dy, const void* x, const float* w, const float* mean,
                               const float* rstd, const void* dres, void* dx, float* dw, float* db, float* partial_w,
                               float* partial_b, int M, int D, hipStream_t s) {
   const int G = norm_bwd_grid(M);
-  const size_t lds = (size_t)(mode == 1 ? 2 : 1) * D * sizeof(float);
+  const size_t lds = (size_t)(mode != 0 ? 2 : 1) * D * sizeof(float);
 #define DPFS_NB(T, MODE_)                                                                                  \
   DPFS_VPL_DISPATCH(vpl_for<T>(D), norm_bwd_k<T, VPL, MODE_><<<G, 256, lds, s>>>(                           \
       (const T*)dy, (const T*)x, w, mean, rstd, (const T*)dres, (T*)dx, partial_w, partial_b, M, D))
   if (dtype == kBF16) {
-    if (mode == 0) DPFS_NB(bf16, 0); else DPFS_NB(bf16, 1);
+    if (mode == 0) DPFS_NB(bf16, 0); else if (mode == 1) DPFS_NB(bf16, 1); else DPFS_NB(bf16, 2);
   } else {
-    if (mode == 0) DPFS_NB(float, 0); else DPFS_NB(float, 1);
+    if (mode == 0) DPFS_NB(float, 0); else if (mode == 1) DPFS_NB(float, 1); else DPFS_NB(float, 2);
   }
 #undef DPFS_NB
   // Stage 2 (fixed-order 2-D column reduction over the G block partials).  The workspace
   // for its own partials lives after the G*D block partials (dpfs_norm_bwd_ws).
-  float* ws2 = partial_w + (size_t)G * D * (mode == 1 ? 2 : 1);
+  float* ws2 = partial_w + (size_t)G * D * (mode != 0 ? 2 : 1);
   dpfs_colsum_f32(partial_w, dw, ws2, G, D, s);
-  if (mode == 1) dpfs_colsum_f32(partial_b, db, ws2, G, D, s);
+  if (mode != 0) dpfs_colsum_f32(partial_b, db, ws2, G, D, s);
 }

@@ -121,13 +121,12 @@ class DecoderTrainFn(torch.autograd.Function):
         for li, L in enumerate(layers):
             # seg1: (wait + residual), norm1, QKV, RoPE, attention, Wo -> async all-reduce
             for s in st:
-                if s["pend"] is not None:
-                    _wait(s["h"])
-                    s["x"] = k.bias_residual(s["pend"], s["pend_bias"], s["x"])
+                _wait(s["h"])
+                if s["pend"] is not None:   # residual epilogue of the previous layer fused into norm1
+                    s["x"], h1, r1 = k.add_rmsnorm_fwd(s["pend"], s["pend_bias"], s["x"], L.s1, L.eps1)
                 else:
-                    _wait(s["h"])
+                    h1, r1 = k.rmsnorm_fwd(s["x"], L.s1, L.eps1)
                 x = s["x"]
-                h1, r1 = k.rmsnorm_fwd(x, L.s1, L.eps1)
                 qkv = k.gemm_nt(h1, W(L.wqkv), L.bqkv, s["pos"], tab, 2 * L.h, L.hd)  # RoPE in the epilogue
                 Mc = x.size(0)
                 Bc = s["B"]
@@ -140,8 +139,7 @@ class DecoderTrainFn(torch.autograd.Function):
             # seg2: wait + bias + residual, norm2, gate|up, SwiGLU, down -> async all-reduce
             for s in st:
                 _wait(s["h"])
-                x2 = k.bias_residual(s["pend"], s["pend_bias"], s["x"])
-                h2, r2 = k.rmsnorm_fwd(x2, L.s2, L.eps2)
+                x2, h2, r2 = k.add_rmsnorm_fwd(s["pend"], s["pend_bias"], s["x"], L.s2, L.eps2)
                 gu = GS.gemm_nt(k, h2, W(L.wgu), L.bgu)
                 sw = k.swiglu_fwd(gu)
                 qout = GS.gemm_nt(k, sw, W(L.wd), None)
@@ -153,8 +151,7 @@ class DecoderTrainFn(torch.autograd.Function):
         n_valid_total = torch.zeros((), device=dev, dtype=torch.float32)
         for s in st:
             _wait(s["h"])
-            xf = k.bias_residual(s["pend"], s["pend_bias"], s["x"])
-            hf, rf = k.rmsnorm_fwd(xf, model.norm.scale, model.norm.eps)
+            xf, hf, rf = k.add_rmsnorm_fwd(s["pend"], s["pend_bias"], s["x"], model.norm.scale, model.norm.eps)
             logits = GS.gemm_nt(k, hf, W(head.weight), head.bias)
             stats = k.ce_fwd_stats(logits, s["tgt"], vst, vvalid)
             if tp > 1:
@@ -220,7 +217,12 @@ class DecoderTrainFn(torch.autograd.Function):
             del s["logits"]
         for s in st:
             _wait(s["bh"])
-            dxf, dsf = k.rmsnorm_bwd(s["dpend"], s["xf"], model.norm.scale, s["rf"])
+            Lt = layers[-1]
+            dbd = s["dpend"].new_empty(s["dpend"].size(1), dtype=torch.float32) if Lt.bd is not None else None
+            dxf, dsf = k.rmsnorm_bwd(s["dpend"], s["xf"], model.norm.scale, s["rf"], None, dbd)
+            if dbd is not None:   # bias grad of the last layer's down projection, same pass
+                gl[nL - 1]["bd"] = _addg(gl[nL - 1].get("bd"), dbd)
+                s["bd_done"] = True
             g["nf"] = _addg(g["nf"], dsf)
             s["g"] = dxf            # grad wrt the last layer's output (residual stream)
             s["dpend"] = None
@@ -231,10 +233,11 @@ class DecoderTrainFn(torch.autograd.Function):
             # b2: down / SwiGLU / gate|up grads -> AR(dh2)
             for s in st:
                 if s["dpend"] is not None:     # finish the upper layer: wait, norm1 bwd, residual
-                    _finish_norm1(k, s, layers[li + 1], gl[li + 1], li + 1)
+                    _finish_norm1(k, s, layers[li + 1], gl[li + 1], li + 1, (G, L.bd))
                 a = s["layers"][li]
                 gq = s["g"]
-                bias_acc(G, "bd", gq, L.bd)
+                if not s.pop("bd_done", False):
+                    bias_acc(G, "bd", gq, L.bd)
                 ds = GS.gemm_nn(k, gq, W(L.wd))
                 tn(G, "wd", gq, a["sw"])
                 dbgu = ds.new_empty(a["gu"].size(1), dtype=torch.float32) if L.bgu is not None else None
@@ -249,9 +252,13 @@ class DecoderTrainFn(torch.autograd.Function):
             for s in st:
                 a = s["layers"][li]
                 _wait(s["bh"])
-                g2, ds2 = k.rmsnorm_bwd(s["dpend"], a["x2"], L.s2, a["r2"], s["g"])  # + residual grad
+                dbo = None
+                if L.bo is not None:
+                    dbo = s["dpend"].new_empty(s["dpend"].size(1), dtype=torch.float32)
+                g2, ds2 = k.rmsnorm_bwd(s["dpend"], a["x2"], L.s2, a["r2"], s["g"], dbo)  # + residual grad, bo grad
                 G["s2"] = _addg(G.get("s2"), ds2)
-                bias_acc(G, "bo", g2, L.bo)
+                if dbo is not None:
+                    G["bo"] = _addg(G.get("bo"), dbo)
                 do = GS.gemm_nn(k, g2, W(L.wo))
                 tn(G, "wo", g2, a["o"].view(g2.size(0), -1))
                 Bc = s["B"]
@@ -283,12 +290,20 @@ class DecoderTrainFn(torch.autograd.Function):
         return (None, None, None, None, None, None) + tuple(grads)
 
 
-def _finish_norm1(k, s, L, G, li):
+def _finish_norm1(k, s, L, G, li, below=None):
     """Wait for the all-reduce of layer li's norm1 input-grad, run the norm1 backward and add
-    it to the residual-stream grad (-> grad wrt layer li's input)."""
+    it to the residual-stream grad (-> grad wrt layer li's input).  ``below`` = (grad dict,
+    bias) of layer li-1's down projection: its bias grad (column sums of that residual grad)
+    comes out of the same norm-backward pass."""
     a = s["layers"][li]
     _wait(s["bh"])
-    s["g"], ds1 = k.rmsnorm_bwd(s["dpend"], a["x"], L.s1, a["r1"], s["g"])   # fused residual-grad add
+    db = None
+    if below is not None and below[1] is not None:
+        db = s["g"].new_empty(s["g"].size(1), dtype=torch.float32)
+    s["g"], ds1 = k.rmsnorm_bwd(s["dpend"], a["x"], L.s1, a["r1"], s["g"], db)   # fused residual-grad add
+    if db is not None:
+        below[0]["bd"] = _addg(below[0].get("bd"), db)
+        s["bd_done"] = True
     G["s1"] = _addg(G.get("s1"), ds1)
     s["dpend"] = None
     for key in ("x", "r1", "h1"):

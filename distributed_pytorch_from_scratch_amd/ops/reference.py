@@ -88,8 +88,9 @@ def rmsnorm_fwd(x: torch.Tensor, w: torch.Tensor, eps: float) -> Tuple[torch.Ten
 
 
 def rmsnorm_bwd(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, rstd: torch.Tensor,
-                dres: Optional[torch.Tensor] = None):
-    """Returns (dx [+ dres if given, fused residual-grad add], dw fp32)."""
+                dres: Optional[torch.Tensor] = None, dbias: Optional[torch.Tensor] = None):
+    """Returns (dx [+ dres if given, fused residual-grad add], dw fp32); with ``dbias`` (fp32
+    [D]) also writes the column sums of dx there (the bias grad of the layer below)."""
     xf, dyf, wf = x.float(), dy.float(), w.float()
     xhat = xf * rstd[:, None]
     dw = (dyf * xhat).sum(0)
@@ -98,7 +99,17 @@ def rmsnorm_bwd(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, rstd: torch.
     dx = rstd[:, None] * (g - xhat * (g * xhat).sum(-1, keepdim=True) / d)
     if dres is not None:
         dx = dx + dres.float()
+    if dbias is not None:
+        dbias.copy_(dx.sum(0))
     return dx.to(x.dtype), dw
+
+
+def add_rmsnorm_fwd(y: torch.Tensor, bias: Optional[torch.Tensor], res: torch.Tensor, w: torch.Tensor,
+                    eps: float):
+    """(x = y + bias + res rounded to y.dtype, rmsnorm_fwd(x)) — the fused residual epilogue."""
+    x = bias_residual(y, bias, res)
+    h, rstd = rmsnorm_fwd(x, w, eps)
+    return x, h, rstd
 
 
 def layernorm_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float):

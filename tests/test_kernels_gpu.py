@@ -359,3 +359,36 @@ def test_gemm_plans(C, impl, cfg, splits, sched):
         C.gemm_set_impl(2)
         C.gemm_force(-1, 0)
         C.gemm_v2_sched(-1)
+
+
+@pytest.mark.parametrize("with_bias", [True, False])
+def test_add_rmsnorm_fwd_fused(C, with_bias):
+    torch.manual_seed(18)
+    M, D = 777, 768
+    y = torch.randn(M, D, device=DEV).bfloat16()
+    res = torch.randn(M, D, device=DEV).bfloat16()
+    b = torch.randn(D, device=DEV) if with_bias else None
+    w = torch.rand(D, device=DEV) + 0.5
+    x, h, r = C.add_rmsnorm_fwd(y, b, res, w, 1e-5)
+    x2 = C.bias_residual(y, b, res)
+    h2, r2 = C.rmsnorm_fwd(x2, w, 1e-5)
+    # same math as bias_residual + rmsnorm_fwd (fp32 add order may differ by one bf16 ulp)
+    assert (x.float() - x2.float()).abs().max().item() <= 2 ** -7 * x2.float().abs().max().item()
+    assert _rel(h, h2) < 1e-2 and torch.allclose(r, r2, rtol=1e-3)
+    rx, rh, rr = R.add_rmsnorm_fwd(y.float(), b, res.float(), w, 1e-5)
+    assert _rel(h, rh) < 1e-2
+
+
+def test_rmsnorm_bwd_fused_output_colsum(C):
+    torch.manual_seed(19)
+    M, D = 1500, 768
+    x = torch.randn(M, D, device=DEV).bfloat16()
+    w = torch.rand(D, device=DEV) + 0.5
+    dy = torch.randn(M, D, device=DEV).bfloat16()
+    dres = torch.randn(M, D, device=DEV).bfloat16()
+    _, rstd = C.rmsnorm_fwd(x, w, 1e-5)
+    db = torch.empty(D, device=DEV)
+    dx, dw = C.rmsnorm_bwd(dy, x, w, rstd, dres, db)
+    dx2, dw2 = C.rmsnorm_bwd(dy, x, w, rstd, dres)
+    assert torch.equal(dx, dx2) and torch.equal(dw, dw2)
+    assert _rel(db, dx.float().sum(0)) < 5e-3   # db sums the fp32 values before the bf16 store
