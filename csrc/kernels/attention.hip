@@ -140,15 +140,17 @@ struct Stage {
 };
 
 // =============================================================================== forward ==
-// Block: NW waves x 32 queries of one (b, h); K/V tiles of 64 keys, double buffered in LDS
-// (measured: 4 waves beat 8, and issuing the next tile's loads after QK^T gained nothing).
-template <int HD, int NW = 4>
+// Block: NW waves x QW queries of one (b, h); K/V tiles of 64 keys, double buffered in LDS
+// (measured at hd 64: 4 waves x 32 queries beats 8 waves, 16-query waves (occupancy 4) and
+// issuing the next tile's loads after QK^T; profiles/r1_v4_attn_fwd_pmc.txt).
+template <int HD, int NW = 4, int QW = 32>
 __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ V, bf16* __restrict__ O,
                                                      float* __restrict__ LSE, int T, int H, long long ldq,
                                                      long long ldk, long long ldv, long long ldo, float scale,
                                                      int causal) {
-  constexpr int BQ = 32 * NW, BKV = 64, KT = HD / 32, DT = HD / 16;
+  constexpr int QC = QW / 16;  // 16-query column tiles per wave
+  constexpr int BQ = QW * NW, BKV = 64, KT = HD / 32, DT = HD / 16;
   constexpr int TILE = BKV * HD * 2;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
   const int nqb = (T + BQ - 1) / BQ;
@@ -156,7 +158,7 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd_k(const b
   const int bh = blockIdx.y, b = bh / H, h = bh % H;
   const int q0 = qb * BQ;
   const int wave = threadIdx.x >> 6, l = lane_id(), g = l >> 4;
-  const int wq0 = q0 + wave * 32;
+  const int wq0 = q0 + wave * QW;
   const float c2 = scale * kLog2e;
 
   const bf16* qbase = Q + (long long)b * T * ldq + (long long)h * HD;
@@ -164,9 +166,9 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd_k(const b
   const bf16* vbase = V + (long long)b * T * ldv + (long long)h * HD;
 
   // Q^T operand in registers: lane holds Q[wq0 + 16c + (l&15)][32kk + 8g + j].
-  bf16x8 qf[2][KT];
+  bf16x8 qf[QC][KT];
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
+  for (int c = 0; c < QC; ++c) {
     const int qi = wq0 + 16 * c + (l & 15);
 #pragma unroll
     for (int kk = 0; kk < KT; ++kk) {
@@ -176,12 +178,17 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd_k(const b
     }
   }
 
-  f32x4 o[2][DT];
+  f32x4 o[QC][DT];
 #pragma unroll
-  for (int c = 0; c < 2; ++c)
+  for (int c = 0; c < QC; ++c)
 #pragma unroll
     for (int d = 0; d < DT; ++d) o[c][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float m[2] = {-INFINITY, -INFINITY}, lsum[2] = {0.f, 0.f};
+  float m[QC], lsum[QC];
+#pragma unroll
+  for (int c = 0; c < QC; ++c) {
+    m[c] = -INFINITY;
+    lsum[c] = 0.f;
+  }
 
   const int kv_end = causal ? min(T, q0 + BQ) : T;
   const int nkv = (kv_end + BKV - 1) / BKV;
@@ -203,19 +210,19 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd_k(const b
       sk.load(kbase + (long long)n0 * ldk, ldk, min(BKV, T - n0));
       sv.load(vbase + (long long)n0 * ldv, ldv, min(BKV, T - n0));
     }
-    const bool wave_active = !causal || kv0 <= wq0 + 31;
+    const bool wave_active = !causal || kv0 <= wq0 + QW - 1;
     if (wave_active) {
       // S^T tiles: s[i][c] = K[kv0+16i..][:] . Q[16c..][:]^T
-      f32x4 s[4][2];
+      f32x4 s[4][QC];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        s[i][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        s[i][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < QC; ++c) s[i][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kk = 0; kk < KT; ++kk) {
           const bf16x8 kf = row_frag<HD>(lk, 16 * i, 32 * kk);
-          s[i][0] = MFMA(kf, qf[0][kk], s[i][0]);
-          s[i][1] = MFMA(kf, qf[1][kk], s[i][1]);
+#pragma unroll
+          for (int c = 0; c < QC; ++c) s[i][c] = MFMA(kf, qf[c][kk], s[i][c]);
         }
       }
       // Online softmax per query column (lane-local + butterfly over the 4 lane groups).
@@ -224,7 +231,7 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd_k(const b
       // visited tile has >= 1 valid key per query (key kv0 <= wq0), so no -inf guards.
       const bool need_mask = (causal && kv0 + BKV - 1 > wq0) || (kv0 + BKV > T);
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
+      for (int c = 0; c < QC; ++c) {
         const int qi = wq0 + 16 * c + (l & 15);
         if (need_mask) {
 #pragma unroll
@@ -261,13 +268,14 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd_k(const b
       // O^T[d][q] += V^T[d][k] P^T[k][q]
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 p0 = pack_pt(s[2 * ks][0], s[2 * ks + 1][0]);
-        const bf16x8 p1 = pack_pt(s[2 * ks][1], s[2 * ks + 1][1]);
+        bf16x8 pc[QC];
+#pragma unroll
+        for (int c = 0; c < QC; ++c) pc[c] = pack_pt(s[2 * ks][c], s[2 * ks + 1][c]);
 #pragma unroll
         for (int d = 0; d < DT; ++d) {
           const bf16x8 vf = tr_frag<HD>(lv, 32 * ks, 16 * d);
-          o[0][d] = MFMA(vf, p0, o[0][d]);
-          o[1][d] = MFMA(vf, p1, o[1][d]);
+#pragma unroll
+          for (int c = 0; c < QC; ++c) o[c][d] = MFMA(vf, pc[c], o[c][d]);
         }
       }
     }
@@ -281,7 +289,7 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd_k(const b
 
   // Epilogue: O[q][d] = O^T[d][q] / l ; lse = (m + log2 l) * ln2.
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
+  for (int c = 0; c < QC; ++c) {
     float ls = lsum[c];
     ls += __shfl_xor(ls, 16, 64);
     ls += __shfl_xor(ls, 32, 64);

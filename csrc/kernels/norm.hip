@@ -85,10 +85,17 @@ __global__ __launch_bounds__(256) void add_rmsnorm_fwd_k(const T* __restrict__ y
       load_vec<T>(yin + off + c * N, a);
       load_vec<T>(res + off + c * N, b);
 #pragma unroll
+      for (int j = 0; j < N; ++j) v[i][j] = a[j];
+      if (bias) {  // same add order as bias_residual_k: (y + bias) + res
+#pragma unroll
+        for (int j = 0; j < N; j += 4) {
+          const f32x4 t = *reinterpret_cast<const f32x4*>(bias + c * N + j);
+          v[i][j] += t[0]; v[i][j + 1] += t[1]; v[i][j + 2] += t[2]; v[i][j + 3] += t[3];
+        }
+      }
+#pragma unroll
       for (int j = 0; j < N; ++j) {
-        float t = a[j] + b[j];
-        if (bias) t += bias[c * N + j];
-        v[i][j] = to_f(from_f<T>(t));
+        v[i][j] = to_f(from_f<T>(v[i][j] + b[j]));
         ss += v[i][j] * v[i][j];
       }
       store_vec<T>(xo + off + c * N, v[i]);
@@ -103,7 +110,13 @@ __global__ __launch_bounds__(256) void add_rmsnorm_fwd_k(const T* __restrict__ y
     if (c < nvec) {
       float o[N];
 #pragma unroll
-      for (int j = 0; j < N; ++j) o[j] = to_f(from_f<T>(v[i][j] * r)) * w[c * N + j];
+      for (int j = 0; j < N; j += 4) {
+        const f32x4 t = *reinterpret_cast<const f32x4*>(w + c * N + j);
+        o[j] = to_f(from_f<T>(v[i][j] * r)) * t[0];
+        o[j + 1] = to_f(from_f<T>(v[i][j + 1] * r)) * t[1];
+        o[j + 2] = to_f(from_f<T>(v[i][j + 2] * r)) * t[2];
+        o[j + 3] = to_f(from_f<T>(v[i][j + 3] * r)) * t[3];
+      }
       store_vec<T>(y + off + c * N, o);
     }
   }
