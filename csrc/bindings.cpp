@@ -60,6 +60,7 @@ void dpfs_adam_step(const void*, const int*, int, float, float, float, float, fl
 void dpfs_grad_sumsq(const void*, const int*, int, float*, hipStream_t);
 int dpfs_attn_supported_hd(int);
 void dpfs_attn_set_impl(int);
+void dpfs_attn_set_bwd_impl(int);
 void dpfs_attn_fwd(const void*, const void*, const void*, void*, float*, int, int, int, int, long long, long long,
                    long long, long long, float, int, hipStream_t);
 void dpfs_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, float*, void*, void*,
@@ -637,6 +638,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("head_dim"), py::arg("inverse") = false);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("scale"), py::arg("causal") = true);
   m.def("attn_set_impl", [](int v) { dpfs_attn_set_impl(v); }, "1 = register-staged (default), 2 = LDS-DMA ring 8-wave, 3 = LDS-DMA ring 4-wave");
+  m.def("attn_set_bwd_impl", [](int v) { dpfs_attn_set_bwd_impl(v); }, "dK/dV kernel: 2 = LDS-DMA ring (default), 1 = register-staged");
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("scale"), py::arg("causal"), py::arg("dq"), py::arg("dk"), py::arg("dv"),
         py::arg("rope_pos") = py::none(), py::arg("rope_tab") = py::none());

@@ -679,6 +679,215 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv_k(const 
   }
 }
 
+// ================================================================ bwd: dK, dV (LDS-DMA) ==
+// Same math and block shape as attn_bwd_dkdv_k (4 waves x 16 keys, query tiles of 64), but
+// Q / dO tiles and their LSE / delta rows arrive by LDS-DMA into a 3-deep ring: tile t+2
+// is in flight while tile t is computed (the register-staged kernel waited ~45 % of its
+// wave cycles on the one-tile-ahead loads, profiles/r1_v5_attn_bwd_pmc.txt).  Every wave
+// issues the same 5 DMA instructions per tile (4 x 1 KiB pieces of Q/dO, one 256-B row of
+// LSE or delta or an out-of-range dummy), so one counted vmcnt serves all waves.
+template <int HD>
+__device__ __forceinline__ void qdo_dma(__amdgpu_buffer_rsrc_t rq, __amdgpu_buffer_rsrc_t rdo,
+                                        __amdgpu_buffer_rsrc_t rl, __amdgpu_buffer_rsrc_t rd, char* stage, int q0,
+                                        int T, long long ldq, long long lddo) {
+  constexpr int CPR = HD / 8;
+  constexpr int TILE = 64 * HD * 2;
+  constexpr int P = 2 * TILE / 1024;          // 1 KiB pieces per Q + dO tile
+  constexpr int PW = P / 4;                   // per wave (4 waves)
+  const int l = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int j = wave + 4 * i;
+    const bool isdo = j >= P / 2;
+    const int jj = isdo ? j - P / 2 : j;
+    const int pos = jj * 64 + l;
+    const int r = pos / CPR, cp = pos % CPR;
+    const int ch = ((sw_off<HD>(r, cp) - r * HD * 2) >> 4);
+    const int row = q0 + r;
+    const long long ld = isdo ? lddo : ldq;
+    const unsigned off = row < T ? (unsigned)(((long long)row * ld + ch * 8) * 2) : kOOB;
+    dma16(isdo ? rdo : rq, stage + (isdo ? TILE : 0) + jj * 1024, off);
+  }
+  // stats: wave 0 -> LSE[q0..q0+63], wave 1 -> delta, waves 2/3 -> dummy (OOB) into a pad slot
+  char* st = stage + 2 * TILE;
+  const unsigned soff = (wave < 2 && q0 + l < T) ? (unsigned)((q0 + l) * 4) : kOOB;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(wave == 1 ? rd : rl,
+                                           (__attribute__((address_space(3))) void*)(st + (wave < 2 ? wave : 2) * 256),
+                                           4, soff, 0, 0, 0);
+}
+
+template <int HD>
+__global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv2_k(
+    const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V, const bf16* __restrict__ dO,
+    const float* __restrict__ LSE, const float* __restrict__ DELTA, bf16* __restrict__ dK, bf16* __restrict__ dV,
+    int T, int H, long long ldq, long long ldk, long long ldv, long long lddo, long long lddk, long long lddv,
+    float scale, int causal, const int64_t* __restrict__ rpos, const float* __restrict__ rtab) {
+  constexpr int BKV = 64, BQ = 64, KT = HD / 32, DT = HD / 16;
+  constexpr int TILE = BQ * HD * 2;
+  constexpr int BUF = 2 * TILE + 1024;        // Q, dO, lse, delta, dummy slot (1 KiB aligned stages)
+  constexpr int NST = 3;
+  constexpr int PWV = 2 * TILE / 1024 / 4 + 1;  // DMA instructions per wave per tile
+  __shared__ __attribute__((aligned(1024))) char smem[NST * BUF];
+  const int kb = blockIdx.x;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int k0 = kb * BKV;
+  const int wave = threadIdx.x >> 6, l = lane_id(), g = l >> 4;
+  const int wk0 = k0 + wave * 16;
+  const float c2 = scale * kLog2e;
+
+  const bf16* qbase = Q + (long long)b * T * ldq + (long long)h * HD;
+  const bf16* dobase = dO + (long long)b * T * lddo + (long long)h * HD;
+  const float* lse_b = LSE + ((long long)b * H + h) * T;
+  const float* del_b = DELTA + ((long long)b * H + h) * T;
+  const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)qbase, (short)0, (int)(((long long)(T - 1) * ldq + HD) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rdo = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)dobase, (short)0, (int)(((long long)(T - 1) * lddo + HD) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)lse_b, (short)0, T * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)del_b, (short)0, T * 4, 0x00020000);
+
+  const int qstart = causal ? (k0 / BQ) * BQ : 0;
+  const int nq = (T - qstart + BQ - 1) / BQ;
+  if (nq > 0) qdo_dma<HD>(rq, rdo, rl, rd, smem, qstart, T, ldq, lddo);
+  if (nq > 1) qdo_dma<HD>(rq, rdo, rl, rd, smem + BUF, qstart + BQ, T, ldq, lddo);
+
+  bf16x8 kf[KT], vf[KT];
+  {
+    const int ki = wk0 + (l & 15);
+#pragma unroll
+    for (int kk = 0; kk < KT; ++kk) {
+      bf16x8 a = {}, c = {};
+      if (ki < T) {
+        a = *reinterpret_cast<const bf16x8*>(K + ((long long)b * T + ki) * ldk + (long long)h * HD + 32 * kk + 8 * g);
+        c = *reinterpret_cast<const bf16x8*>(V + ((long long)b * T + ki) * ldv + (long long)h * HD + 32 * kk + 8 * g);
+      }
+      kf[kk] = a;
+      vf[kk] = c;
+    }
+  }
+  f32x4 dk[DT], dv[DT];
+#pragma unroll
+  for (int d = 0; d < DT; ++d) {
+    dk[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    dv[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+
+  int cur = 0;
+  for (int t = 0; t < nq; ++t) {
+    if (t + 1 < nq) wait_vmcnt<PWV>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    const char* lq = smem + cur * BUF;
+    const char* ldo_ = lq + TILE;
+    const float* ls = reinterpret_cast<const float*>(lq + 2 * TILE);
+    const float* ds = ls + BQ;
+    int nb = cur + 2;
+    if (nb >= NST) nb -= NST;
+    cur = (cur + 1 == NST) ? 0 : cur + 1;
+    const int qq0 = qstart + t * BQ;
+    if (t + 2 < nq) qdo_dma<HD>(rq, rdo, rl, rd, smem + nb * BUF, qq0 + 2 * BQ, T, ldq, lddo);
+    const bool wave_active = !causal || (qq0 + BQ - 1 >= wk0);
+    if (!wave_active) continue;
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      s[qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      dp[qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KT; ++kk) {
+        s[qt] = MFMA(row_frag<HD>(lq, 16 * qt, 32 * kk), kf[kk], s[qt]);
+        dp[qt] = MFMA(row_frag<HD>(ldo_, 16 * qt, 32 * kk), vf[kk], dp[qt]);
+      }
+    }
+    // transposed dO fragments for dV (asm reads: see tr_frag_asm) land during the softmax; the
+    // Q fragments for dK are read after the dV MFMAs are issued (two batches of 2*DT halves
+    // keep the kernel at 3 waves/SIMD instead of holding both across the softmax).
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr int NH = 2 * DT * 2;             // 2 k-slots x DT fragments x 2 halves
+    constexpr int NHP = (NH + 15) / 16 * 16;
+    s16x4 th[NHP];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int d = 0; d < DT; ++d) tr_frag_asm<HD>(ldo_, 32 * ks, 16 * d, th[2 * (ks * DT + d)], th[2 * (ks * DT + d) + 1]);
+    const int ki = wk0 + (l & 15);
+    const bool need_mask = (causal && wk0 + 15 > qq0) || (qq0 + BQ > T) || (wk0 + 16 > T);
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      const f32x4 lsv = *reinterpret_cast<const f32x4*>(ls + 16 * qt + 4 * g);
+      const f32x4 dsv = *reinterpret_cast<const f32x4*>(ds + 16 * qt + 4 * g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float p = __builtin_amdgcn_exp2f(fmaf(s[qt][j], c2, -lsv[j] * kLog2e));
+        if (need_mask) {
+          const int qi = qq0 + 16 * qt + 4 * g + j;
+          if (qi >= T || ki >= T || (causal && ki > qi)) p = 0.f;
+        }
+        s[qt][j] = p;
+        dp[qt][j] = p * (dp[qt][j] - dsv[j]);
+      }
+    }
+    bf16x8 pa[2], da[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      pa[ks] = pack_pt(s[2 * ks], s[2 * ks + 1]);
+      da[ks] = pack_pt(dp[2 * ks], dp[2 * ks + 1]);
+    }
+#pragma unroll
+    for (int w = 0; w < NHP / 16; ++w) tr_wait8(*reinterpret_cast<s16x4(*)[16]>(&th[16 * w]));
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int d = 0; d < DT; ++d) dv[d] = MFMA(pa[ks], tr_join(th[2 * (ks * DT + d)], th[2 * (ks * DT + d) + 1]), dv[d]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int d = 0; d < DT; ++d) tr_frag_asm<HD>(lq, 32 * ks, 16 * d, th[2 * (ks * DT + d)], th[2 * (ks * DT + d) + 1]);
+#pragma unroll
+    for (int w = 0; w < NHP / 16; ++w) tr_wait8(*reinterpret_cast<s16x4(*)[16]>(&th[16 * w]));
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int d = 0; d < DT; ++d) dk[d] = MFMA(da[ks], tr_join(th[2 * (ks * DT + d)], th[2 * (ks * DT + d) + 1]), dk[d]);
+  }
+  wait_vmcnt<0>();
+  // Write dK (scaled, inverse RoPE), dV: C layout col = d (l&15), rows = keys 4g + j.
+#pragma unroll
+  for (int d = 0; d < DT; ++d)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dk[d][j] *= scale;
+  if (rpos) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ki = wk0 + 4 * g + j;
+      if (ki < T) {
+        const float* tr = rtab + rpos[(long long)b * T + ki] * HD;
+#pragma unroll
+        for (int d = 0; d < DT / 2; ++d) {
+          const float c = tr[16 * d + (l & 15)], sn = tr[HD / 2 + 16 * d + (l & 15)];
+          const float x1 = dk[d][j], x2 = dk[d + DT / 2][j];
+          dk[d][j] = x1 * c + x2 * sn;
+          dk[d + DT / 2][j] = x2 * c - x1 * sn;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < DT; ++d) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ki = wk0 + 4 * g + j;
+      if (ki < T) {
+        const long long col = (long long)h * HD + 16 * d + (l & 15);
+        dK[((long long)b * T + ki) * lddk + col] = (bf16)dk[d][j];
+        dV[((long long)b * T + ki) * lddv + col] = (bf16)dv[d][j];
+      }
+    }
+  }
+}
+
 // ============================================================================ bwd: dQ ==
 // Block: 4 waves x 32 queries = 128 queries; K/V tiles of 64 keys staged in LDS.
 template <int HD>
@@ -861,6 +1070,8 @@ extern "C" int dpfs_attn_supported_hd(int hd) { return hd == 32 || hd == 64 || h
 
 static int g_attn_impl = 1;  // 1 = register-staged (default, fastest measured), 2 / 3 = LDS-DMA ring with 8 / 4 waves
 extern "C" void dpfs_attn_set_impl(int v) { g_attn_impl = v; }
+static int g_attn_bwd_impl = 2;  // dK/dV kernel: 2 = LDS-DMA ring (default), 1 = register-staged
+extern "C" void dpfs_attn_set_bwd_impl(int v) { g_attn_bwd_impl = v; }
 
 extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int T, int H,
                               int hd, long long ldq, long long ldk, long long ldv, long long ldo, float scale,
@@ -896,6 +1107,13 @@ extern "C" void dpfs_attn_bwd(const void* dout, const void* q, const void* k, co
                                                              T, H, ldq, ldk, ldv, lddo, ldo, lddq, scale, causal,
                                                              rope_pos, rope_tab));
   dim3 gk((T + 63) / 64, B * H);
+  if (g_attn_bwd_impl == 2) {
+    DPFS_HD_DISPATCH(hd, attn_bwd_dkdv2_k<HD_><<<gk, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
+                                                                  (const bf16*)dout, lse, delta, (bf16*)dk,
+                                                                  (bf16*)dv, T, H, ldq, ldk, ldv, lddo, lddk, lddv,
+                                                                  scale, causal, rope_pos, rope_tab));
+    return;
+  }
   DPFS_HD_DISPATCH(hd, attn_bwd_dkdv_k<HD_><<<gk, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
                                                                (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv, T,
                                                                H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal,

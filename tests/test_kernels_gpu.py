@@ -186,11 +186,13 @@ def test_cross_entropy_kernels(C, V, valid, start):
                                       (1, 1000, 2, 64)])
 @pytest.mark.parametrize("impl", [2, 3, 1])
 def test_attention(C, B, T, H, hd, impl):
-    C.attn_set_impl(impl)
+    C.attn_set_impl(impl)            # forward variants
+    C.attn_set_bwd_impl(1 if impl == 3 else 2)   # dK/dV: register-staged and LDS-DMA ring
     try:
         _check_attention(C, B, T, H, hd)
     finally:
         C.attn_set_impl(1)
+        C.attn_set_bwd_impl(2)
 
 
 def _check_attention(C, B, T, H, hd):

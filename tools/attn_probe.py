@@ -38,6 +38,7 @@ def main():
     def mk(impl):
         def g():
             C.attn_set_impl(impl)
+            C.attn_set_bwd_impl(impl if a.bwd else 2)
             if a.bwd:
                 C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv)
             else:
@@ -47,6 +48,7 @@ def main():
     for impl, ms in res.items():
         print(f"impl {impl} {'bwd' if a.bwd else 'fwd'}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF", flush=True)
     C.attn_set_impl(1)
+    C.attn_set_bwd_impl(2)
 
 
 if __name__ == "__main__":
