@@ -401,13 +401,6 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd2_k(
     cur = (cur + 1 == NST) ? 0 : cur + 1;
     const int kv0 = t * BKV;
     const bool active = !causal || kv0 <= wq0 + 31;  // wave-uniform
-    bf16x8 kf[4][KT];
-    if (active) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int kk = 0; kk < KT; ++kk) kf[i][kk] = row_frag<HD>(lk, 16 * i, 32 * kk);
-    }
     if (t + 2 < nkv) kv_dma<HD, NW>(rk, rv, smem + nb * STAGE, (t + 2) * BKV, T, ldk, ldv);
     if (!active) continue;
     f32x4 s[4][2];
@@ -417,8 +410,9 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd2_k(
       s[i][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < KT; ++kk) {
-        s[i][0] = MFMA(kf[i][kk], qf[0][kk], s[i][0]);
-        s[i][1] = MFMA(kf[i][kk], qf[1][kk], s[i][1]);
+        const bf16x8 kf = row_frag<HD>(lk, 16 * i, 32 * kk);  // b128 reads: no compiler vmcnt(0)
+        s[i][0] = MFMA(kf, qf[0][kk], s[i][0]);
+        s[i][1] = MFMA(kf, qf[1][kk], s[i][1]);
       }
     }
     // V^T fragments via asm transposed reads (no compiler vmcnt(0) in front of them, see
