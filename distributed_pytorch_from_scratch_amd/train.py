@@ -171,6 +171,8 @@ def train(rank, args: Namespace):
                     writer.add_scalar("train/lr", lr, n)
                     writer.add_scalar(f"used_gpu_memory/tprank-{p.tp_rank}", mem, n)
                     writer.add_scalar("throughput/tokens_per_s", tps, n)
+                    for k_, v_ in step_fn.timings().items():
+                        writer.add_scalar(f"time/{k_}", v_, n)
                     writer.flush()
             if n % args.save_interval == 0:
                 accum_host += float(accum.item())
