@@ -51,7 +51,9 @@ class TrainStep:
         self.scheduler = scheduler
         self.sp = model.args.sequence_parallel
         p = pm.pgm
-        self.dp = DataParallelGradSync(model, dp_bucket_mb) if (p is not None and p.dp_size > 1) else None
+        # The fused engine averages DP gradients itself, overlapped with its backward.
+        use_hooks = p is not None and p.dp_size > 1 and not model.fused_supported()
+        self.dp = DataParallelGradSync(model, dp_bucket_mb) if use_hooks else None
         self.checker = comm_check.from_env()
         self.steps = 0
         self._ev = None

@@ -202,6 +202,23 @@ class DecoderTrainFn(torch.autograd.Function):
                 return
             key_dict[key] = _addg(key_dict.get(key), k.bias_grad(dy))
 
+        # DP: each layer's gradients are averaged over the data-parallel group by one async
+        # all-reduce of a flat fp32 buffer, issued as soon as the layer's backward completes,
+        # so it overlaps the remaining layers (DataParallelGradSync's hooks would only fire
+        # after this Function returns).
+        pg = pm.pgm
+        dp = pg.dp_size if pg is not None else 1
+        dp_pending = []
+
+        def dp_reduce(d: dict, keys=None):
+            if dp <= 1:
+                return
+            keys = [key for key in (keys or sorted(d)) if d.get(key) is not None]
+            if not keys:
+                return
+            flat = torch.cat([d[key].reshape(-1) for key in keys])
+            dp_pending.append((dist.all_reduce(flat, group=pg.dp_group, async_op=True), flat, d, keys))
+
         # ---- head: CE backward in place over the logits, lm_head dgrad -> async AR
         for s in st:
             gs = s["valid"].float() * gscale_all
@@ -227,6 +244,7 @@ class DecoderTrainFn(torch.autograd.Function):
             s["g"] = dxf            # grad wrt the last layer's output (residual stream)
             s["dpend"] = None
             del s["xf"], s["hf"]
+        dp_reduce(g, ("nf", "lm_w", "lm_b"))
         # ---- layers, reversed
         for li in range(nL - 1, -1, -1):
             L, G = layers[li], gl[li]
@@ -248,6 +266,8 @@ class DecoderTrainFn(torch.autograd.Function):
                 if dbgu is not None:
                     G["bgu"] = _addg(G.get("bgu"), dbgu)
                 del a["sw"], a["gu"]
+            if li + 1 < nL:
+                dp_reduce(gl[li + 1])           # layer li+1 is complete (its norm1 grad just landed)
             # b1: wait, norm2 bwd, Wo / attention / QKV grads -> AR(dh)
             for s in st:
                 a = s["layers"][li]
@@ -278,6 +298,18 @@ class DecoderTrainFn(torch.autograd.Function):
             _finish_norm1(k, s, layers[0], gl[0], 0)
             dwe = k.embedding_bwd(s["g"], s["ids"], model.embedding.weight.size(0), model.embedding.vocab_st_idx)
             g["emb"] = _addg(g["emb"], dwe)
+        dp_reduce(gl[0])
+        dp_reduce(g, ("emb",))
+        if dp_pending:
+            model._dpfs_dp_reduced = True   # DataParallelGradSync hooks skip this step
+        for h, flat, d, keys in dp_pending:
+            h.wait()
+            flat /= dp
+            off = 0
+            for key in keys:
+                n = d[key].numel()
+                d[key] = flat[off:off + n].view_as(d[key])
+                off += n
         ctx.st = None
         grads = [g["emb"]]
         for li, L in enumerate(layers):

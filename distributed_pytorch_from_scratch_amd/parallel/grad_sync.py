@@ -49,6 +49,7 @@ class DataParallelGradSync:
     """Overlapped, bucketed DP gradient averaging (no-op when ``dp_size == 1``)."""
 
     def __init__(self, model: torch.nn.Module, bucket_mb: float = 32.0):
+        self.model = model
         self.p = pm.get_pgm()
         self.params = [q for q in model.parameters() if q.requires_grad]
         self.enabled = self.p.dp_size > 1
@@ -80,6 +81,8 @@ class DataParallelGradSync:
         self._flat = {}
 
     def _hook(self, param):
+        if getattr(self.model, "_dpfs_dp_reduced", False):
+            return   # the fused engine already averaged this step's grads (overlapped)
         bi = self._index[id(param)]
         self._pending[bi] -= 1
         if self._pending[bi] == 0:
@@ -91,6 +94,11 @@ class DataParallelGradSync:
     def finish(self) -> None:
         """Wait for all buckets (call after backward, before the optimizer step)."""
         if not self.enabled:
+            return
+        if getattr(self.model, "_dpfs_dp_reduced", False):
+            self.model._dpfs_dp_reduced = False
+            self._handles = []
+            self._reset()
             return
         # Buckets whose params got no grad this step are reduced here synchronously.
         for bi, n in self._pending.items():

@@ -79,9 +79,10 @@ def test_vocab_parallel_ce(world, V, valid, ign):
     run_distributed(_ce, world, V, valid, ign)
 
 
-def _dp(rank, world):
+def _dp(rank, world, fused):
     """DP=2 x TP=2 grid: DP gradient averaging gives the same step as the full batch on one
-    replica; the TP groups are {0,1} and {2,3}."""
+    replica; the TP groups are {0,1} and {2,3}.  ``fused``: the engine averages inside its
+    backward (overlapped) and the hooks stand down; else the bucketed hooks do it."""
     from distributed_pytorch_from_scratch_amd.parallel import process_manager as pm
     from distributed_pytorch_from_scratch_amd.parallel.grad_sync import DataParallelGradSync
     from distributed_pytorch_from_scratch_amd.models import Transformer, ModelArgs
@@ -90,6 +91,7 @@ def _dp(rank, world):
     assert (p.dp_size, p.tp_size) == (2, 2) and p.tp_ranks == [2 * p.dp_rank, 2 * p.dp_rank + 1]
     args = ModelArgs(attn_dim=32, ffn_dim=64, num_heads=4, num_layers=1, vocab_size=64, maxlen=16, vocab_pad_to=1)
     m = Transformer.from_args(args)
+    m.use_fused_engine = fused
     set_seed(0)
     m.reset_parameters()
     sync = DataParallelGradSync(m, bucket_mb=0.01)
@@ -101,12 +103,14 @@ def _dp(rank, world):
     loss = m.loss(ids[half], pos[half], tgt[half])
     loss.backward()
     sync.finish()
-    gw = m.layers[0].attn.wqkv.weight.grad.clone()
+    got = {n: q.grad.clone() for n, q in m.named_parameters()}
     m.zero_grad()
     m.loss(ids, pos, tgt).backward()
-    return (gw - m.layers[0].attn.wqkv.weight.grad).abs().max().item()
+    sync.finish()
+    return max((got[n] - q.grad).abs().max().item() for n, q in m.named_parameters())
 
 
-def test_data_parallel_grad_sync():
-    res = run_distributed(_dp, 4, tp_size=2)
+@pytest.mark.parametrize("fused", [True, False])
+def test_data_parallel_grad_sync(fused):
+    res = run_distributed(_dp, 4, fused, tp_size=2)
     assert max(res.values()) < 1e-6
