@@ -33,14 +33,25 @@ def available() -> bool:
     return _C is not None
 
 
+_PROXY = None
+
+
 def require():
-    """Return the native module or raise a loud error (used by every GPU op)."""
+    """Return the native module or raise a loud error (used by every GPU op).
+
+    With ``DPFS_SYNC_DEBUG=1`` or ``DPFS_NAN_CHECK=1`` the module comes wrapped in
+    :class:`_DebugProxy`."""
+    global _PROXY
     _load()
     if _C is None:
         raise RuntimeError(
             "distributed_pytorch_from_scratch_amd._C (HIP kernels for gfx950) is not built or "
             f"failed to load: {_ERR!r}. Run `python setup.py build_ext --inplace` "
             "(or __graft_entry__.build()).")
+    if debug_sync() or nan_check():
+        if _PROXY is None:
+            _PROXY = _DebugProxy(_C)
+        return _PROXY
     return _C
 
 
@@ -51,3 +62,50 @@ def so_path() -> str | None:
 
 def debug_sync() -> bool:
     return os.environ.get("DPFS_SYNC_DEBUG", "0") == "1"
+
+
+def nan_check() -> bool:
+    return os.environ.get("DPFS_NAN_CHECK", "0") == "1"
+
+
+class _DebugProxy:
+    """Kernel-level debug mode (SURVEY.md §5 "race detection / sanitizers").
+
+    * ``DPFS_SYNC_DEBUG=1``: every op synchronises the device after its launch. A fault or
+      launch error is reported against the op that caused it, with its argument shapes,
+      instead of surfacing at some later synchronisation. This is the launch-blocking mode.
+    * ``DPFS_NAN_CHECK=1``: the floating-point tensor outputs of every op are checked, and
+      so are its in-place-written arguments. The first op that produces a NaN/Inf raises.
+
+    Both modes are slow and meant for debugging only.
+    """
+
+    def __init__(self, mod):
+        self._mod = mod
+
+    def __getattr__(self, name):
+        fn = getattr(self._mod, name)
+        if not callable(fn):
+            return fn
+        import torch
+
+        def desc(args):
+            return ", ".join(f"{tuple(a.shape)}:{str(a.dtype).replace('torch.', '')}"
+                             if isinstance(a, torch.Tensor) else type(a).__name__ for a in args)
+
+        def wrapped(*args, **kw):
+            out = fn(*args, **kw)
+            if debug_sync():
+                try:
+                    torch.cuda.synchronize()
+                except RuntimeError as e:
+                    raise RuntimeError(f"HIP kernel op `{name}`({desc(args)}) failed: {e}") from e
+            if nan_check():
+                outs = list(out) if isinstance(out, (list, tuple)) else [out]
+                cands = outs + [a for a in args if isinstance(a, torch.Tensor)]
+                for t in cands:
+                    if isinstance(t, torch.Tensor) and t.is_floating_point() and t.numel() and \
+                            not bool(torch.isfinite(t).all()):
+                        raise FloatingPointError(f"op `{name}`({desc(args)}) produced non-finite values")
+            return out
+        return wrapped

@@ -173,3 +173,26 @@ def test_kv_cache_generation_on_gpu(dist1):
         assert rel < 3e-2, rel
     out = generate(m, prompt, max_new_tokens=20)
     assert len(out) == 2 and all(len(o) == 120 for o in out)
+
+
+def test_kernel_debug_modes_run_clean_and_catch_nan(dist1, monkeypatch):
+    """DPFS_SYNC_DEBUG / DPFS_NAN_CHECK: a clean step raises nothing; a NaN weight is
+    reported against the first kernel op that produces non-finite values."""
+    from distributed_pytorch_from_scratch_amd.models import get_preset, Transformer
+    from distributed_pytorch_from_scratch_amd.ops import _ext
+    monkeypatch.setenv("DPFS_SYNC_DEBUG", "1")
+    monkeypatch.setenv("DPFS_NAN_CHECK", "1")
+    args = get_preset("gpt2-small", num_layers=1)
+    m = Transformer.from_args(args).cuda()
+    m.reset_parameters()
+    ids = torch.randint(0, args.vocab_size, (2, 64), device="cuda")
+    pos = torch.arange(64, device="cuda").repeat(2, 1)
+    assert isinstance(_ext.require(), _ext._DebugProxy)
+    m.loss(ids, pos, ids).backward()
+    with torch.no_grad():
+        m.layers[0].norm2.scale[3] = float("nan")
+    with pytest.raises(FloatingPointError, match="non-finite"):
+        m.loss(ids, pos, ids)
+    monkeypatch.delenv("DPFS_SYNC_DEBUG")
+    monkeypatch.delenv("DPFS_NAN_CHECK")
+    assert not isinstance(_ext.require(), _ext._DebugProxy)
