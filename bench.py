@@ -166,6 +166,7 @@ def main():
             "params_matmul": args.matmul_params(),
         },
         "tflops_per_gpu": round(value * mflops / world / 1e12, 2),
+        "mfu_vs_2.5pf_dense_bf16": round(value * mflops / world / 2.5e15, 4),
         "final_loss": round(final_loss, 4),
     }
     if rank == 0:

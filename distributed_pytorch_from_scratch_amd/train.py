@@ -38,6 +38,10 @@ from .utils.fault import Heartbeat, maybe_inject_fault
 from .utils.tb import SummaryWriter
 
 
+# Dense (no sparsity) bf16 MFMA peak of one MI355X, FLOP/s.
+MI355X_BF16_PEAK = 2.5e15
+
+
 def get_train_args(argv=None) -> Namespace:
     p = ArgumentParser()
     g = p.add_argument_group("distributed")
@@ -171,6 +175,8 @@ def train(rank, args: Namespace):
                     writer.add_scalar("train/lr", lr, n)
                     writer.add_scalar(f"used_gpu_memory/tprank-{p.tp_rank}", mem, n)
                     writer.add_scalar("throughput/tokens_per_s", tps, n)
+                    # model FLOPs utilisation vs the MI355X dense bf16 peak (2.5 PFLOP/s per GPU)
+                    writer.add_scalar("throughput/mfu", tps * flops_tok / p.world_size / MI355X_BF16_PEAK, n)
                     for k_, v_ in step_fn.timings().items():
                         writer.add_scalar(f"time/{k_}", v_, n)
                     writer.flush()
