@@ -66,6 +66,17 @@ void dpfs_attn_fwd(const void*, const void*, const void*, void*, float*, int, in
 void dpfs_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, float*, void*, void*,
                    void*, int, int, int, int, long long, long long, long long, long long, long long, long long,
                    long long, long long, float, int, const int64_t*, const float*, hipStream_t);
+// comm/xgmi.hip
+const char* dpfs_xgmi_last_error();
+long long dpfs_xgmi_handle_bytes();
+void* dpfs_xgmi_create(int, int, long long, void*);
+int dpfs_xgmi_open(void*, const void*);
+void dpfs_xgmi_set_blocks(void*, int);
+long long dpfs_xgmi_capacity(void*);
+int dpfs_xgmi_error(void*);
+void dpfs_xgmi_clear_error(void*);
+int dpfs_xgmi_run(void*, int, int, const void*, void*, long long, long long, double, hipStream_t);
+void dpfs_xgmi_destroy(void*);
 }
 
 namespace {
@@ -518,7 +529,6 @@ torch::Tensor ce_bwd(torch::Tensor logits, torch::Tensor targets, torch::Tensor 
                   out.scalar_type() == logits.scalar_type(),
               "ce_bwd: out must match logits");
   const int64_t M = logits.size(0), V = logits.size(1);
-  TORCH_CHECK(V % (dcode(logits) == 1 ? 8 : 4) == 0, "ce_bwd: V_local must be a multiple of the vector width");
   TORCH_CHECK(lse.scalar_type() == torch::kFloat32 && lse.numel() == M && gscale.scalar_type() == torch::kFloat32 &&
                   gscale.numel() == M && lse.is_contiguous() && gscale.is_contiguous(),
               "ce_bwd: lse/gscale fp32 [M]");
@@ -609,6 +619,60 @@ torch::Tensor grad_sumsq(torch::Tensor desc, torch::Tensor chunks) {
   return partial.sum();
 }
 
+// ------------------------------------------------------------- xGMI collectives (comm/) --
+void* xgmi_ptr(int64_t h) {
+  TORCH_CHECK(h != 0, "xgmi: null communicator");
+  return reinterpret_cast<void*>(h);
+}
+
+py::tuple xgmi_create(int64_t rank, int64_t world, int64_t cap_bytes) {
+  std::string hb((size_t)dpfs_xgmi_handle_bytes(), '\0');
+  void* h = dpfs_xgmi_create((int)rank, (int)world, cap_bytes, &hb[0]);
+  TORCH_CHECK(h != nullptr, "xgmi_create failed: ", dpfs_xgmi_last_error());
+  return py::make_tuple(reinterpret_cast<int64_t>(h), py::bytes(hb));
+}
+
+void xgmi_open(int64_t h, py::bytes all_handles) {
+  std::string s = all_handles;
+  TORCH_CHECK(s.size() % dpfs_xgmi_handle_bytes() == 0, "xgmi_open: handle blob size");
+  TORCH_CHECK(dpfs_xgmi_open(xgmi_ptr(h), s.data()) == 0, "xgmi_open failed: ", dpfs_xgmi_last_error());
+}
+
+// op 0 all-reduce (out may be x), 1 reduce-scatter (out = x.numel()/W elements),
+// 2 all-gather (out = W * x.numel() elements); launched on the current stream.
+void xgmi_run(int64_t h, int64_t op, torch::Tensor x, torch::Tensor out, int64_t world, double timeout_s) {
+  TORCH_CHECK(op >= 0 && op <= 2, "xgmi_run: op");
+  check_cuda(x, "x");
+  check_cuda(out, "out");
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous(), "xgmi_run: contiguous tensors");
+  TORCH_CHECK(x.scalar_type() == out.scalar_type(), "xgmi_run: dtype mismatch");
+  const int dt = dcode(x);
+  const int64_t vec = dt == 1 ? 8 : 4;
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "xgmi_run: 16-byte aligned buffers");
+  const int64_t n = x.numel();
+  TORCH_CHECK(n > 0 && n % vec == 0, "xgmi_run: numel must be a positive multiple of ", vec);
+  int64_t total, part;
+  if (op == 0) {
+    TORCH_CHECK(out.numel() == n, "xgmi all_reduce: out numel");
+    total = n;
+    part = ((n + world * vec - 1) / (world * vec)) * vec;
+  } else if (op == 1) {
+    TORCH_CHECK(n % (world * vec) == 0 && out.numel() * world == n, "xgmi reduce_scatter: sizes");
+    total = n;
+    part = n / world;
+  } else {
+    TORCH_CHECK(out.numel() == n * world, "xgmi all_gather: out numel");
+    total = n * world;
+    part = n;
+  }
+  const at::DeviceGuard g(x.device());
+  TORCH_CHECK(dpfs_xgmi_run(xgmi_ptr(h), (int)op, dt, x.data_ptr(), out.data_ptr(), total, part, timeout_s,
+                            stream()) == 0,
+              "xgmi_run failed: ", dpfs_xgmi_last_error());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -652,4 +716,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"), py::arg("step"), py::arg("grad_scale") = 1.0,
         py::arg("dscale") = py::none());
   m.def("grad_sumsq", &grad_sumsq);
+  m.def("xgmi_create", &xgmi_create, "allocate IPC buffers: -> (handle, ipc handle bytes)");
+  m.def("xgmi_open", &xgmi_open, "map every peer's buffers (rank-ordered concatenated handle bytes)");
+  m.def("xgmi_run", &xgmi_run, py::arg("h"), py::arg("op"), py::arg("x"), py::arg("out"), py::arg("world"),
+        py::arg("timeout_s") = 120.0);
+  m.def("xgmi_set_blocks", [](int64_t h, int b) { dpfs_xgmi_set_blocks(xgmi_ptr(h), b); });
+  m.def("xgmi_capacity", [](int64_t h) { return dpfs_xgmi_capacity(xgmi_ptr(h)); });
+  m.def("xgmi_error", [](int64_t h) { return dpfs_xgmi_error(xgmi_ptr(h)); });
+  m.def("xgmi_clear_error", [](int64_t h) { dpfs_xgmi_clear_error(xgmi_ptr(h)); });
+  m.def("xgmi_destroy", [](int64_t h) { dpfs_xgmi_destroy(xgmi_ptr(h)); });
 }

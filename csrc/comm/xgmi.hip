@@ -1,0 +1,385 @@
+// Intra-node tensor-parallel collectives over xGMI peer memory (MI355X, gfx950).
+//
+// An 8 x MI355X node is a fully connected xGMI mesh: every GPU has one ~153 GB/s link to each of
+// its 7 peers.  A ring collective (RCCL's default algorithm for large messages) drives one
+// outgoing link per step; the kernels here instead read from all peers at once, so a TP group
+// of W ranks keeps all W-1 links busy:
+//
+//   all-reduce  (two-shot)  copy-in | barrier | rank r sums slice r of every peer's buffer in
+//                           fixed rank order (fp32) -> own slice + tmp | barrier | gather the
+//                           other W-1 reduced slices from the peers' tmp
+//   reduce-scatter          the first two phases of the all-reduce
+//   all-gather              copy-in | barrier | read every peer's buffer
+//
+// Each call runs as ONE kernel on the caller's (side) stream.  Per rank there is one IPC data
+// allocation [in | tmp] and one uncached signal allocation; handles are exchanged over the
+// c10d store by the Python side (parallel/xgmi.py).  Workgroup b of every rank owns the same
+// vector range in every phase, so the barriers are per workgroup: b signals its peers' b and
+// waits for their b (no grid-wide barrier, no residency assumption).  Flags are monotonic
+// epochs (one per call, identical on every rank because every rank issues the same call
+// sequence), compared wrap-safe, never reset.
+//
+// Memory ordering across GPUs: every byte a peer will read is stored write-through
+// (sc0 sc1 buffer stores) and drained (s_waitcnt vmcnt(0)) before a system-scope release and
+// the flag store; every remote byte is loaded with sc0 sc1 (system-coherent) buffer loads, so
+// neither side depends on L2 state.  Flags are system-scope atomics in uncached memory.
+//
+// Why the phases are safe without an end barrier: rank r overwrites its `in` region only in
+// the copy-in of call k+1, i.e. after its kernel k finished, i.e. after every one of its
+// workgroups passed the second barrier of call k, which every peer workgroup signals only after
+// its phase-1 reads of `in` completed.  `tmp` is rewritten in phase 1 of call k+1, after the
+// start barrier of k+1, which a peer workgroup signals only once that peer's kernel k (and its
+// phase-2 reads of tmp) completed (same stream).
+//
+// Every wait is bounded (s_memrealtime, 100 MHz): on timeout the kernel records an error in a
+// host-mapped word and exits, so a broken peer can never hang the GPU.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <cstdio>
+
+namespace {
+
+constexpr int kMaxRanks = 8;
+constexpr int kMaxBlocks = 1024;
+constexpr int kThreads = 256;
+constexpr long long kSigBytes = 2LL * kMaxBlocks * kMaxRanks * sizeof(uint32_t);  // [phase][block][src]
+constexpr int kAuxSys = 1 | 16;  // sc0 | sc1: system-coherent (write-through stores, L2-bypassing loads)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+struct Peers {
+  char* data[kMaxRanks];     // [in | tmp] of every rank (own included)
+  uint32_t* sig[kMaxRanks];  // signal arrays of every rank
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ u32x4 ld_sys(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAuxSys);
+}
+__device__ __forceinline__ void st_sys(__amdgpu_buffer_rsrc_t r, unsigned off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxSys);
+}
+
+// 16-byte vector <-> fp32 lanes
+template <typename T> struct V16;
+template <> struct V16<__bf16> {
+  static constexpr int N = 8;
+  __device__ static void unpack(u32x4 v, float (&f)[8]) {
+    bf16x8 b = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = (float)b[i];
+  }
+  __device__ static u32x4 pack(const float (&f)[8]) {
+    bf16x8 b;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b[i] = (__bf16)f[i];
+    return __builtin_bit_cast(u32x4, b);
+  }
+};
+template <> struct V16<float> {
+  static constexpr int N = 4;
+  __device__ static void unpack(u32x4 v, float (&f)[4]) {
+    f32x4 b = __builtin_bit_cast(f32x4, v);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i] = b[i];
+  }
+  __device__ static u32x4 pack(const float (&f)[4]) {
+    f32x4 b;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b[i] = f[i];
+    return __builtin_bit_cast(u32x4, b);
+  }
+};
+
+__device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Signal every peer's workgroup `blockIdx.x` (phase p), then wait for all of them.  Lanes
+// 0..W-1 of wave 0 each handle one peer.  Returns false on timeout (error recorded).
+__device__ __forceinline__ void barrier(const Peers& P, int rank, int W, int phase, uint32_t epoch,
+                                        unsigned long long deadline, int* err) {
+  drain();           // every wave: its write-through stores have left
+  __syncthreads();   // ... for all waves of the workgroup
+  const int t = threadIdx.x;
+  if (t < W && t != rank) {
+    // No L2 write-back is needed (the payload went out write-through and every wave drained
+    // it above); the workgroup-scope fences only pin the compiler's ordering.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    uint32_t* f = P.sig[t] + ((size_t)phase * kMaxBlocks + blockIdx.x) * kMaxRanks + rank;
+    __hip_atomic_store(f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t* mine = P.sig[rank] + ((size_t)phase * kMaxBlocks + blockIdx.x) * kMaxRanks + t;
+    while ((int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() > deadline) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    // Remote bytes are read with system-coherent (sc0 sc1) loads, so no cache invalidation is
+    // needed here (a system acquire would drop the L2 under the GEMMs running beside us).
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  __syncthreads();
+}
+
+// op: 0 all-reduce (x[n] -> out[n], out may alias x), 1 reduce-scatter (x[n] -> out[part]),
+//     2 all-gather (x[part] -> out[W*part]).
+// n = total elements of the full tensor; part = per-rank slice length (multiple of N).
+template <typename T>
+__global__ __launch_bounds__(kThreads) void xgmi_coll_k(Peers P, int op, int rank, int W, const T* x, T* out,
+                                                       long long n, long long part, long long in_off,
+                                                       long long tmp_off, long long cap, uint32_t epoch,
+                                                       unsigned long long timeout_ticks, int* err) {
+  constexpr int N = V16<T>::N;
+  const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + timeout_ticks;
+  const long long nvec = part / N;                       // vectors per slice
+  const long long vpb = (nvec + gridDim.x - 1) / gridDim.x;
+  const long long v0 = (long long)blockIdx.x * vpb;
+  const long long v1 = v0 + vpb < nvec ? v0 + vpb : nvec;
+  char* mine = P.data[rank];
+  const __amdgpu_buffer_rsrc_t r_in = rsrc(mine + in_off, cap);
+  const __amdgpu_buffer_rsrc_t r_tmp = rsrc(mine + tmp_off, cap);
+  const u32x4* xv = reinterpret_cast<const u32x4*>(x);
+  u32x4* ov = reinterpret_cast<u32x4*>(out);
+
+  // ---- phase 0: copy-in of what the peers will read
+  if (op == 2) {
+    for (long long v = v0 + threadIdx.x; v < v1; v += kThreads) st_sys(r_in, (unsigned)(v * 16), xv[v]);
+  } else {
+    for (int s = 0; s < W; ++s) {
+      if (s == rank) continue;
+      const long long base = s * part;  // elements
+      for (long long v = v0 + threadIdx.x; v < v1; v += kThreads) {
+        const long long e = base + v * N;
+        if (e < n) st_sys(r_in, (unsigned)(e * sizeof(T)), xv[e / N]);
+      }
+    }
+  }
+  barrier(P, rank, W, 0, epoch, deadline, err);
+
+  // ---- phase 1
+  if (op == 2) {
+    for (int s = 0; s < W; ++s) {
+      if (s == rank) {
+        for (long long v = v0 + threadIdx.x; v < v1; v += kThreads) ov[(s * part) / N + v] = xv[v];
+      } else {
+        const __amdgpu_buffer_rsrc_t rp = rsrc(P.data[s] + in_off, cap);
+        for (long long v = v0 + threadIdx.x; v < v1; v += kThreads)
+          ov[(s * part) / N + v] = ld_sys(rp, (unsigned)(v * 16));
+      }
+    }
+  } else {
+    __amdgpu_buffer_rsrc_t rp[kMaxRanks];
+#pragma unroll
+    for (int s = 0; s < kMaxRanks; ++s) rp[s] = rsrc(P.data[s < W ? s : 0] + in_off, cap);
+    const long long base = rank * part;
+    for (long long v = v0 + threadIdx.x; v < v1; v += kThreads) {
+      const long long e = base + v * N;
+      if (e >= n) break;
+      u32x4 raw[kMaxRanks];
+#pragma unroll
+      for (int s = 0; s < kMaxRanks; ++s)   // issue every load before the first add
+        if (s < W && s != rank) raw[s] = ld_sys(rp[s], (unsigned)(e * sizeof(T)));
+      const u32x4 self = xv[e / N];
+#pragma unroll
+      for (int s = 0; s < kMaxRanks; ++s)
+        if (s == rank) raw[s] = self;
+      float acc[N], f[N];
+      V16<T>::unpack(raw[0], acc);
+#pragma unroll
+      for (int s = 1; s < kMaxRanks; ++s) {
+        if (s < W) {
+          V16<T>::unpack(raw[s], f);
+#pragma unroll
+          for (int i = 0; i < N; ++i) acc[i] += f[i];
+        }
+      }
+      const u32x4 r = V16<T>::pack(acc);
+      if (op == 0) {
+        st_sys(r_tmp, (unsigned)(v * 16), r);
+        ov[e / N] = r;
+      } else {
+        ov[v] = r;
+      }
+    }
+  }
+  barrier(P, rank, W, 1, epoch, deadline, err);
+
+  // ---- phase 2 (all-reduce): the other ranks' reduced slices
+  if (op == 0) {
+    for (int s = 0; s < W; ++s) {
+      if (s == rank) continue;
+      const __amdgpu_buffer_rsrc_t rp = rsrc(P.data[s] + tmp_off, cap);
+      const long long base = s * part;
+      for (long long v = v0 + threadIdx.x; v < v1; v += kThreads) {
+        const long long e = base + v * N;
+        if (e < n) ov[e / N] = ld_sys(rp, (unsigned)(v * 16));
+      }
+    }
+  }
+}
+
+struct Comm {
+  int rank = 0, world = 1;
+  long long cap = 0;          // bytes of each of in / tmp
+  char* data = nullptr;       // own [in | tmp]
+  uint32_t* sig = nullptr;    // own signals (uncached)
+  Peers peers{};
+  bool opened[kMaxRanks] = {};
+  uint32_t epoch = 0;
+  int* err_host = nullptr;
+  int* err_dev = nullptr;
+  int blocks = 256;
+};
+
+thread_local char g_msg[512];
+
+bool ok(hipError_t e, const char* what) {
+  if (e == hipSuccess) return true;
+  snprintf(g_msg, sizeof(g_msg), "%s: %s", what, hipGetErrorString(e));
+  return false;
+}
+
+}  // namespace
+
+extern "C" void dpfs_xgmi_destroy(void* h);
+
+extern "C" const char* dpfs_xgmi_last_error() { return g_msg; }
+
+extern "C" long long dpfs_xgmi_handle_bytes() { return 2 * (long long)sizeof(hipIpcMemHandle_t); }
+
+// Allocate this rank's buffers; writes [data handle | signal handle] to handles_out.
+extern "C" void* dpfs_xgmi_create(int rank, int world, long long cap_bytes, void* handles_out) {
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world) {
+    snprintf(g_msg, sizeof(g_msg), "xgmi: world %d / rank %d out of range (max %d ranks)", world, rank, kMaxRanks);
+    return nullptr;
+  }
+  if (cap_bytes <= 0 || cap_bytes >= (1LL << 31) || cap_bytes % 4096) {
+    snprintf(g_msg, sizeof(g_msg), "xgmi: capacity %lld must be a positive multiple of 4096 below 2 GiB", cap_bytes);
+    return nullptr;
+  }
+  Comm* c = new Comm();
+  c->rank = rank;
+  c->world = world;
+  c->cap = cap_bytes;
+  if (!ok(hipMalloc((void**)&c->data, 2 * cap_bytes), "hipMalloc(data)")) {
+    delete c;
+    return nullptr;
+  }
+  // Signals: uncached device memory when it can be IPC-exported, plain device memory otherwise
+  // (every signal access is a system-scope atomic either way).
+  hipIpcMemHandle_t hs;
+  if (hipExtMallocWithFlags((void**)&c->sig, kSigBytes, hipDeviceMallocUncached) != hipSuccess ||
+      hipIpcGetMemHandle(&hs, c->sig) != hipSuccess) {
+    (void)hipGetLastError();
+    if (c->sig) (void)hipFree(c->sig);
+    c->sig = nullptr;
+    if (!ok(hipMalloc((void**)&c->sig, kSigBytes), "hipMalloc(sig)") ||
+        !ok(hipIpcGetMemHandle(&hs, c->sig), "hipIpcGetMemHandle(sig)")) {
+      dpfs_xgmi_destroy(c);
+      return nullptr;
+    }
+  }
+  if (!ok(hipMemset(c->sig, 0, kSigBytes), "hipMemset(sig)") ||
+      !ok(hipHostMalloc((void**)&c->err_host, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent),
+          "hipHostMalloc(err)") ||
+      !ok(hipHostGetDevicePointer((void**)&c->err_dev, c->err_host, 0), "hipHostGetDevicePointer(err)")) {
+    dpfs_xgmi_destroy(c);
+    return nullptr;
+  }
+  *c->err_host = 0;
+  hipIpcMemHandle_t hd;
+  if (!ok(hipIpcGetMemHandle(&hd, c->data), "hipIpcGetMemHandle(data)")) {
+    dpfs_xgmi_destroy(c);
+    return nullptr;
+  }
+  memcpy(handles_out, &hd, sizeof(hd));
+  memcpy((char*)handles_out + sizeof(hd), &hs, sizeof(hs));
+  c->peers.data[rank] = c->data;
+  c->peers.sig[rank] = c->sig;
+  if (!ok(hipDeviceSynchronize(), "hipDeviceSynchronize")) {
+    dpfs_xgmi_destroy(c);
+    return nullptr;
+  }
+  return c;
+}
+
+// handles: world x [data handle | signal handle], in rank order.
+extern "C" int dpfs_xgmi_open(void* h, const void* handles) {
+  Comm* c = (Comm*)h;
+  const long long hb = dpfs_xgmi_handle_bytes();
+  for (int r = 0; r < c->world; ++r) {
+    if (r == c->rank) continue;
+    hipIpcMemHandle_t hd, hs;
+    memcpy(&hd, (const char*)handles + r * hb, sizeof(hd));
+    memcpy(&hs, (const char*)handles + r * hb + sizeof(hd), sizeof(hs));
+    void *pd = nullptr, *ps = nullptr;
+    if (!ok(hipIpcOpenMemHandle(&pd, hd, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(data)")) return -1;
+    if (!ok(hipIpcOpenMemHandle(&ps, hs, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(sig)")) return -1;
+    c->peers.data[r] = (char*)pd;
+    c->peers.sig[r] = (uint32_t*)ps;
+    c->opened[r] = true;
+  }
+  return 0;
+}
+
+extern "C" void dpfs_xgmi_set_blocks(void* h, int blocks) {
+  Comm* c = (Comm*)h;
+  c->blocks = blocks < 1 ? 1 : (blocks > kMaxBlocks ? kMaxBlocks : blocks);
+}
+
+extern "C" long long dpfs_xgmi_capacity(void* h) { return ((Comm*)h)->cap; }
+
+// Host-visible error word (1 = a barrier timed out).  Reading it does not synchronise.
+extern "C" int dpfs_xgmi_error(void* h) { return __atomic_load_n(((Comm*)h)->err_host, __ATOMIC_RELAXED); }
+
+extern "C" void dpfs_xgmi_clear_error(void* h) { __atomic_store_n(((Comm*)h)->err_host, 0, __ATOMIC_RELAXED); }
+
+// One collective on `stream`.  dtype 1 = bf16, 0 = fp32.  Element counts as in xgmi_coll_k;
+// the caller guarantees n*elt <= cap (op 0/1) / W*part*elt <= ... (op 2: part*elt <= cap) and
+// 16-byte alignment of x and out.
+extern "C" int dpfs_xgmi_run(void* h, int op, int dtype, const void* x, void* out, long long n, long long part,
+                             double timeout_s, hipStream_t stream) {
+  Comm* c = (Comm*)h;
+  const int elt = dtype == 1 ? 2 : 4;
+  const int N = 16 / elt;
+  if (part % N || (op == 2 ? part * elt > c->cap : ((n + N - 1) / N) * N * elt > c->cap) || n <= 0) {
+    snprintf(g_msg, sizeof(g_msg), "xgmi_run: bad sizes n=%lld part=%lld (cap %lld B)", n, part, c->cap);
+    return -1;
+  }
+  const long long nvec = part / N;
+  int grid = (int)((nvec + kThreads - 1) / kThreads);
+  if (grid > c->blocks) grid = c->blocks;
+  if (grid < 1) grid = 1;
+  c->epoch += 1;
+  if (c->epoch == 0) c->epoch = 1;
+  const unsigned long long ticks = (unsigned long long)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
+  if (dtype == 1)
+    hipLaunchKernelGGL(xgmi_coll_k<__bf16>, dim3(grid), dim3(kThreads), 0, stream, c->peers, op, c->rank, c->world,
+                       (const __bf16*)x, (__bf16*)out, n, part, 0LL, c->cap, c->cap, c->epoch, ticks, c->err_dev);
+  else
+    hipLaunchKernelGGL(xgmi_coll_k<float>, dim3(grid), dim3(kThreads), 0, stream, c->peers, op, c->rank, c->world,
+                       (const float*)x, (float*)out, n, part, 0LL, c->cap, c->cap, c->epoch, ticks, c->err_dev);
+  return ok(hipGetLastError(), "xgmi_coll_k launch") ? 0 : -1;
+}
+
+extern "C" void dpfs_xgmi_destroy(void* h) {
+  Comm* c = (Comm*)h;
+  if (!c) return;
+  (void)hipDeviceSynchronize();
+  for (int r = 0; r < c->world; ++r) {
+    if (!c->opened[r]) continue;
+    (void)hipIpcCloseMemHandle(c->peers.data[r]);
+    (void)hipIpcCloseMemHandle(c->peers.sig[r]);
+  }
+  if (c->data) (void)hipFree(c->data);
+  if (c->sig) (void)hipFree(c->sig);
+  if (c->err_host) (void)hipHostFree(c->err_host);
+  delete c;
+}

@@ -68,7 +68,8 @@ __global__ __launch_bounds__(256) void ce_stats_k(const T* __restrict__ logits, 
   const int row = blockIdx.x;
   const T* x = logits + (long long)row * V;
   MaxSum acc = {-INFINITY, 0.f};
-  const int nvec = vvalid / N;  // full vectors inside the valid range
+  // full vectors inside the valid range (rows are 16-B aligned only when V % N == 0)
+  const int nvec = V % N == 0 ? vvalid / N : 0;
   for (int c = threadIdx.x; c < nvec; c += blockDim.x) {
     float v[N];
     load_vec<T>(x + c * N, v);
@@ -99,13 +100,33 @@ __global__ __launch_bounds__(256) void ce_stats_k(const T* __restrict__ logits, 
   }
 }
 
+// N-wide access: the 16-byte vector when N == Vec<T>::N, element-wise otherwise (rows whose
+// width is not a multiple of the vector, e.g. an uneven vocab shard, are not 16-B aligned).
+template <typename T, int N>
+__device__ __forceinline__ void load_n(const T* p, float (&out)[N]) {
+  if constexpr (N == Vec<T>::N) {
+    load_vec<T>(p, out);
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = to_f(p[i]);
+  }
+}
+template <typename T, int N>
+__device__ __forceinline__ void store_n(T* p, const float (&in)[N]) {
+  if constexpr (N == Vec<T>::N) {
+    store_vec<T>(p, in);
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) p[i] = from_f<T>(in[i]);
+  }
+}
+
 // out[row, c] = (exp(x - lse[row]) - [c == target]) * g[row]; 0 for c >= vvalid.  out may
 // alias logits (in place).
-template <typename T>
+template <typename T, int N>
 __global__ __launch_bounds__(256) void ce_bwd_k(const T* logits, const int64_t* __restrict__ tgt,
                                                 const float* __restrict__ lse, const float* __restrict__ gscale,
                                                 T* out, int M, int V, long long vstart, int vvalid) {
-  constexpr int N = Vec<T>::N;
   const long long per_row = V / N;
   const long long total = (long long)M * per_row;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
@@ -114,7 +135,7 @@ __global__ __launch_bounds__(256) void ce_bwd_k(const T* logits, const int64_t* 
     const float l = lse[r], g = gscale[r];
     const long long loc = tgt[r] - vstart;
     float v[N];
-    load_vec<T>(logits + r * V + c, v);
+    load_n<T, N>(logits + r * V + c, v);
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       const int col = c + j;
@@ -122,20 +143,19 @@ __global__ __launch_bounds__(256) void ce_bwd_k(const T* logits, const int64_t* 
       if (col == loc && col < vvalid) p -= 1.f;
       v[j] = p * g;
     }
-    store_vec<T>(out + r * V + c, v);
+    store_n<T, N>(out + r * V + c, v);
   }
 }
 
 // CE backward fused with the lm_head bias gradient (column sums of dlogits): 2-D blocks of
 // 32 column vectors x 8 row lanes over a row chunk; fp32 partials [chunk][V], reduced in a
 // fixed order (deterministic).  Saves one full re-read of the [M, V_local] logits.
-template <typename T>
+template <typename T, int N>
 __global__ __launch_bounds__(256) void ce_bwd_colsum_k(const T* logits, const int64_t* __restrict__ tgt,
                                                        const float* __restrict__ lse,
                                                        const float* __restrict__ gscale, T* out,
                                                        float* __restrict__ partial, int M, int V, long long vstart,
                                                        int vvalid, int rows_per_chunk) {
-  constexpr int N = Vec<T>::N;
   __shared__ float red[8][32 * N];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int c = (blockIdx.x * 32 + tx) * N;
@@ -149,7 +169,7 @@ __global__ __launch_bounds__(256) void ce_bwd_colsum_k(const T* logits, const in
       const float l = lse[r], g = gscale[r];
       const long long loc = tgt[r] - vstart;
       float v[N];
-      load_vec<T>(logits + (long long)r * V + c, v);
+      load_n<T, N>(logits + (long long)r * V + c, v);
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         const int col = c + j;
@@ -158,7 +178,7 @@ __global__ __launch_bounds__(256) void ce_bwd_colsum_k(const T* logits, const in
         v[j] = p * g;
         acc[j] += v[j];
       }
-      store_vec<T>(out + (long long)r * V + c, v);
+      store_n<T, N>(out + (long long)r * V + c, v);
     }
   }
 #pragma unroll
@@ -189,25 +209,39 @@ using namespace dpfs;
 extern "C" int dpfs_colsum_plan(int M, int cblocks, int target_blocks, int* rpc);
 extern "C" void dpfs_colsum_rows_small(const float* part, float* out, int rows, int N, hipStream_t s);
 
+// Vector width of the CE backward: 16 B when every row is 16-B aligned, else element-wise.
+static inline int ce_vec(int dtype, int V) {
+  const int w = dtype == kBF16 ? 8 : 4;
+  return V % w == 0 ? w : 1;
+}
+
 extern "C" long long dpfs_ce_bwd_dbias_ws(int dtype, int M, int V) {
   int rpc;
-  const int chunks = dpfs_colsum_plan(M, (V / (dtype == kBF16 ? 8 : 4) + 31) / 32, 2048, &rpc);
+  const int chunks = dpfs_colsum_plan(M, (V / ce_vec(dtype, V) + 31) / 32, 2048, &rpc);
   return chunks > 1 ? (long long)chunks * V : 0;
 }
 
 extern "C" void dpfs_ce_bwd_dbias(int dtype, const void* logits, const int64_t* tgt, const float* lse,
                                   const float* gscale, void* out, float* dbias, float* ws, int M, int V,
                                   long long vstart, int vvalid, hipStream_t s) {
-  const int cblocks = (V / (dtype == kBF16 ? 8 : 4) + 31) / 32;
+  const int vec = ce_vec(dtype, V);
+  const int cblocks = (V / vec + 31) / 32;
   int rpc;
   const int chunks = dpfs_colsum_plan(M, cblocks, 2048, &rpc);
   float* part = chunks > 1 ? ws : dbias;
-  if (dtype == kBF16)
-    ce_bwd_colsum_k<bf16><<<dim3(cblocks, chunks), 256, 0, s>>>((const bf16*)logits, tgt, lse, gscale, (bf16*)out,
-                                                                part, M, V, vstart, vvalid, rpc);
+  const dim3 grid(cblocks, chunks);
+  if (dtype == kBF16 && vec == 8)
+    ce_bwd_colsum_k<bf16, 8><<<grid, 256, 0, s>>>((const bf16*)logits, tgt, lse, gscale, (bf16*)out, part, M, V,
+                                                  vstart, vvalid, rpc);
+  else if (dtype == kBF16)
+    ce_bwd_colsum_k<bf16, 1><<<grid, 256, 0, s>>>((const bf16*)logits, tgt, lse, gscale, (bf16*)out, part, M, V,
+                                                  vstart, vvalid, rpc);
+  else if (vec == 4)
+    ce_bwd_colsum_k<float, 4><<<grid, 256, 0, s>>>((const float*)logits, tgt, lse, gscale, (float*)out, part, M, V,
+                                                   vstart, vvalid, rpc);
   else
-    ce_bwd_colsum_k<float><<<dim3(cblocks, chunks), 256, 0, s>>>((const float*)logits, tgt, lse, gscale,
-                                                                 (float*)out, part, M, V, vstart, vvalid, rpc);
+    ce_bwd_colsum_k<float, 1><<<grid, 256, 0, s>>>((const float*)logits, tgt, lse, gscale, (float*)out, part, M, V,
+                                                   vstart, vvalid, rpc);
   if (chunks > 1) dpfs_colsum_rows_small(ws, dbias, chunks, V, s);
 }
 
@@ -241,10 +275,16 @@ extern "C" void dpfs_ce_stats(int dtype, const void* logits, const int64_t* tgt,
 
 extern "C" void dpfs_ce_bwd(int dtype, const void* logits, const int64_t* tgt, const float* lse, const float* gscale,
                             void* out, int M, int V, long long vstart, int vvalid, hipStream_t s) {
-  const int vec = dtype == kBF16 ? 8 : 4;
+  const int vec = ce_vec(dtype, V);
   const int grid = cap_grid2((long long)M * V / vec, 256);
-  if (dtype == kBF16)
-    ce_bwd_k<bf16><<<grid, 256, 0, s>>>((const bf16*)logits, tgt, lse, gscale, (bf16*)out, M, V, vstart, vvalid);
+  if (dtype == kBF16 && vec == 8)
+    ce_bwd_k<bf16, 8><<<grid, 256, 0, s>>>((const bf16*)logits, tgt, lse, gscale, (bf16*)out, M, V, vstart, vvalid);
+  else if (dtype == kBF16)
+    ce_bwd_k<bf16, 1><<<grid, 256, 0, s>>>((const bf16*)logits, tgt, lse, gscale, (bf16*)out, M, V, vstart, vvalid);
+  else if (vec == 4)
+    ce_bwd_k<float, 4><<<grid, 256, 0, s>>>((const float*)logits, tgt, lse, gscale, (float*)out, M, V, vstart,
+                                            vvalid);
   else
-    ce_bwd_k<float><<<grid, 256, 0, s>>>((const float*)logits, tgt, lse, gscale, (float*)out, M, V, vstart, vvalid);
+    ce_bwd_k<float, 1><<<grid, 256, 0, s>>>((const float*)logits, tgt, lse, gscale, (float*)out, M, V, vstart,
+                                            vvalid);
 }

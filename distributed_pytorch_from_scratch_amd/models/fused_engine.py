@@ -43,13 +43,15 @@ import torch.distributed as dist
 from ..ops import gemm_select as GS
 from ..ops.dispatch import K, shadow
 from ..parallel import process_manager as pm
+from ..parallel import tp_comm
 
 
 def _ar(t: torch.Tensor):
+    """Async TP all-reduce (RCCL or the xGMI peer-memory kernels: ``parallel/tp_comm.py``)."""
     p = pm.pgm
     if p is None or p.tp_size == 1:
         return None
-    return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=p.tp_group, async_op=True)
+    return tp_comm.all_reduce(t, async_op=True)
 
 
 def _wait(h):
@@ -193,9 +195,9 @@ class DecoderTrainFn(torch.autograd.Function):
         def tn(key_dict, key, dy, x):
             acc = key_dict.get(key)
             if acc is None:
-                key_dict[key] = k.gemm_tn(dy, x)
+                key_dict[key] = GS.gemm_tn(k, dy, x)
             else:
-                k.gemm_tn(dy, x, acc, True)
+                GS.gemm_tn(k, dy, x, acc, True)
 
         def bias_acc(key_dict, key, dy, present):
             if present is None:
@@ -300,6 +302,7 @@ class DecoderTrainFn(torch.autograd.Function):
             g["emb"] = _addg(g["emb"], dwe)
         dp_reduce(gl[0])
         dp_reduce(g, ("emb",))
+        tp_comm.check()   # an xGMI barrier that timed out raises here (host-mapped flag, no sync)
         if dp_pending:
             model._dpfs_dp_reduced = True   # DataParallelGradSync hooks skip this step
         for h, flat, d, keys in dp_pending:

@@ -55,15 +55,23 @@ def _pick(key: Tuple, ours: Callable, blas: Callable) -> str:
     return c
 
 
+def _aligned(*dims: int) -> bool:
+    """Our MFMA kernels stage 16-byte rows: every K / N (and TN's M) must be a multiple of 8.
+    Uneven vocab shards (e.g. 1000 over 2 ranks at vocab_pad_to=1) go to hipBLASLt."""
+    return all(d % 8 == 0 for d in dims)
+
+
 def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None) -> torch.Tensor:
     """y[M,N] = x[M,K] w[N,K]^T (+ bias fp32[N]) in x.dtype."""
     m = mode()
-    if k is reference or m == "ours" or not x.is_cuda:
+    if k is reference or not x.is_cuda or (m == "ours" and _aligned(x.shape[1], w.shape[0])):
         return k.gemm_nt(x, w, bias)
     bb = shadow(bias, x.dtype) if bias is not None else None
 
     def blas():
         return F.linear(x, w, bb)
+    if not _aligned(x.shape[1], w.shape[0]):
+        return blas()
 
     def ours():
         return k.gemm_nt(x, w, bias)
@@ -76,11 +84,13 @@ def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None) -> torch.Tensor:
 def gemm_nn(k, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """c[M,N] = a[M,K] b[K,N] in a.dtype."""
     m = mode()
-    if k is reference or m == "ours" or not a.is_cuda:
+    if k is reference or not a.is_cuda or (m == "ours" and _aligned(a.shape[1], b.shape[1])):
         return k.gemm_nn(a, b)
 
     def blas():
         return torch.matmul(a, b)
+    if not _aligned(a.shape[1], b.shape[1]):
+        return blas()
 
     def ours():
         return k.gemm_nn(a, b)
@@ -88,3 +98,16 @@ def gemm_nn(k, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
         return blas()
     key = ("nn", a.shape[0], b.shape[1], a.shape[1], a.device.index)
     return blas() if _pick(key, ours, blas) == "blas" else ours()
+
+
+def gemm_tn(k, a: torch.Tensor, b: torch.Tensor, out=None, accumulate: bool = False) -> torch.Tensor:
+    """fp32 c[M,N] (+)= a[K,M]^T b[K,N] (weight gradients).  Always our split-K kernel, except
+    for rows our kernel cannot stage (M or N not a multiple of 8: uneven vocab shards)."""
+    if k is reference or not a.is_cuda or _aligned(a.shape[1], b.shape[1]):
+        return k.gemm_tn(a, b, out, accumulate) if out is not None else k.gemm_tn(a, b)
+    c = torch.matmul(a.t(), b).float()
+    if out is None:
+        return c
+    if accumulate:
+        return out.add_(c)
+    return out.copy_(c)

@@ -1,0 +1,137 @@
+"""Tensor-parallel collectives over xGMI peer memory (``csrc/comm/xgmi.hip``).
+
+On an 8 x MI355X node every GPU has a direct xGMI link to each of its 7 peers.  RCCL (the
+``nccl`` backend of ``torch.distributed``) is used for bootstrap, DP gradients and as the
+fallback; the TP activation/gradient collectives of the training engine can instead run on
+:class:`XgmiComm`, whose kernels read from all peers at once (two-shot all-reduce,
+reduce-scatter, all-gather; see the kernel file for the protocol and its memory ordering).
+
+Bootstrap: every rank allocates one IPC data buffer
+``[in | tmp]`` and one signal buffer, the IPC handles are all-gathered over the TP group (the
+c10d store / RCCL carries the bytes), and every rank maps its peers' buffers.  Calls are
+issued on a dedicated HIP side stream with event hand-off to and from the caller's stream, so
+they overlap compute exactly like an ``async_op=True`` RCCL call.
+
+Reference parity: the reference's TP collectives are synchronous NCCL calls on the default
+stream (``models/comm_ops.py:26,39,59,74``); this is the MI355X-native replacement of the
+in-node transport, with identical semantics (sum / concatenate over the TP group).
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _ext
+
+_ALL_REDUCE, _REDUCE_SCATTER, _ALL_GATHER = 0, 1, 2
+
+
+class _Work:
+    """``async_op`` handle: ``wait()`` makes the caller's current stream wait for the call."""
+
+    __slots__ = ("event",)
+
+    def __init__(self, event: torch.cuda.Event):
+        self.event = event
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.event)
+        return True
+
+    def is_completed(self) -> bool:
+        return self.event.query()
+
+
+class XgmiComm:
+    """Peer-memory collectives for one TP group (every rank of the group on this node)."""
+
+    def __init__(self, group=None, cap_bytes: Optional[int] = None, timeout_s: float = 120.0,
+                 blocks: Optional[int] = None):
+        C = _ext.require()
+        self.C = C
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        assert 1 < self.world <= 8, "xGMI collectives: 2..8 ranks of one node"
+        cap = cap_bytes or int(os.environ.get("DPFS_XGMI_CAP_MB", "256")) * (1 << 20)
+        self.cap = cap
+        self.timeout_s = timeout_s
+        self.h, handle = C.xgmi_create(self.rank, self.world, cap)
+        handles: List[Optional[bytes]] = [None] * self.world
+        dist.all_gather_object(handles, handle, group=group)
+        C.xgmi_open(self.h, b"".join(handles))
+        blocks = blocks or int(os.environ.get("DPFS_XGMI_BLOCKS", "256"))
+        C.xgmi_set_blocks(self.h, blocks)
+        self.stream = torch.cuda.Stream()
+        dist.barrier(group=group)
+
+    # ------------------------------------------------------------------------ core ----
+    def _launch(self, op: int, x: torch.Tensor, out: torch.Tensor, timeout_s: Optional[float] = None):
+        cur = torch.cuda.current_stream()
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            self.C.xgmi_run(self.h, op, x, out, self.world, timeout_s or self.timeout_s)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        x.record_stream(self.stream)
+        if out.data_ptr() != x.data_ptr():
+            out.record_stream(self.stream)
+        return _Work(ev)
+
+    def _max_elems(self, t: torch.Tensor) -> int:
+        vec = 16 // t.element_size()
+        per = self.cap // t.element_size()
+        return (per // (self.world * vec)) * (self.world * vec)
+
+    def all_reduce(self, t: torch.Tensor, async_op: bool = True, timeout_s: Optional[float] = None):
+        """In-place SUM over the group (bf16/fp32, fp32 accumulation in rank order, so every
+        rank receives bitwise-identical values)."""
+        assert t.is_contiguous()
+        flat = t.view(-1)
+        step = self._max_elems(t)
+        work = None
+        for o in range(0, flat.numel(), step):
+            piece = flat[o: o + step]
+            work = self._launch(_ALL_REDUCE, piece, piece, timeout_s)
+        if not async_op:
+            work.wait()
+            return None
+        return work
+
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = True):
+        """out = (sum over ranks of inp)[rank-th of W equal slices] (same contract as
+        ``dist.reduce_scatter_tensor``)."""
+        assert inp.numel() == out.numel() * self.world and inp.numel() * inp.element_size() <= self.cap
+        work = self._launch(_REDUCE_SCATTER, inp.contiguous(), out)
+        if not async_op:
+            work.wait()
+            return None
+        return work
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = True):
+        """out = concat over ranks of inp (same contract as ``dist.all_gather_into_tensor``)."""
+        assert out.numel() == inp.numel() * self.world and inp.numel() * inp.element_size() <= self.cap
+        work = self._launch(_ALL_GATHER, inp.contiguous(), out)
+        if not async_op:
+            work.wait()
+            return None
+        return work
+
+    # --------------------------------------------------------------------- health ----
+    def error(self) -> int:
+        """Non-zero once any barrier of any call timed out (host-mapped word, no sync)."""
+        return int(self.C.xgmi_error(self.h))
+
+    def check(self):
+        if self.error():
+            raise RuntimeError(f"xGMI collective timed out on TP rank {self.rank} (a peer never arrived)")
+
+    def close(self):
+        if self.h:
+            torch.cuda.synchronize()
+            dist.barrier(group=self.group)
+            self.C.xgmi_destroy(self.h)
+            self.h = 0

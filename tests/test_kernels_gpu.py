@@ -164,7 +164,8 @@ def test_embedding(C):
         assert _rel(C.embedding_bwd(d, ids, V, st), R.embedding_bwd(d.float(), ids, V, st)) < 1e-3
 
 
-@pytest.mark.parametrize("V,valid,start", [(6288, 6288, 0), (6288, 6241, 6288 * 7), (1024, 1000, 0)])
+@pytest.mark.parametrize("V,valid,start", [(6288, 6288, 0), (6288, 6241, 6288 * 7), (1024, 1000, 0),
+                                           (500, 500, 500)])
 def test_cross_entropy_kernels(C, V, valid, start):
     torch.manual_seed(9)
     M = 257
@@ -316,7 +317,8 @@ def test_swiglu_bwd_fused_bias_grad(C, M, F):
     assert torch.equal(dgu, C.swiglu_bwd(dh, gu))
 
 
-@pytest.mark.parametrize("M,V,valid,start", [(2048, 6288, 6241, 6288 * 7), (100, 50304, 50257, 0)])
+@pytest.mark.parametrize("M,V,valid,start", [(2048, 6288, 6241, 6288 * 7), (100, 50304, 50257, 0),
+                                             (300, 500, 500, 500), (65, 37, 30, 0)])   # unaligned rows
 def test_ce_bwd_fused_bias_grad(C, M, V, valid, start):
     torch.manual_seed(16)
     logits = torch.randn(M, V, device=DEV).bfloat16()

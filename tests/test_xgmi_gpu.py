@@ -1,0 +1,93 @@
+"""xGMI peer-memory collectives (csrc/comm/xgmi.hip) on one MI355X with several ranks.
+
+The ranks are processes sharing one GPU: the IPC mapping, the per-workgroup epoch barriers,
+the two-shot all-reduce, reduce-scatter, all-gather, chunking past the buffer capacity and the
+engine's use of them are the same code paths as across the 8 GPUs of a node (only the link
+speed differs).  Bootstrap goes over gloo (RCCL refuses two ranks on one device).  Expected
+values are computed in fp32 on the host from the same rank-seeded inputs.
+"""
+import os
+
+import pytest
+import torch
+
+from dist_helpers import run_distributed
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(rank, n, dtype, seed=0):
+    g = torch.Generator().manual_seed(1000 * seed + rank)
+    return torch.randn(n, generator=g).to(dtype)
+
+
+def _collectives(rank, world, cases, cap_mb):
+    torch.cuda.set_device(0)
+    from distributed_pytorch_from_scratch_amd.parallel import process_manager as pm
+    from distributed_pytorch_from_scratch_amd.parallel.xgmi import XgmiComm
+    comm = XgmiComm(pm.pgm.tp_group, cap_bytes=cap_mb << 20, timeout_s=30.0)
+    out = {}
+    for i, (op, n, dt) in enumerate(cases):
+        dtype = getattr(torch, dt)
+        x = _inputs(rank, n, dtype, seed=i).cuda()
+        if op == "ar":
+            y = x.clone()
+            comm.all_reduce(y, async_op=True).wait()
+            y2 = x.clone()                      # back-to-back calls reuse the buffers
+            comm.all_reduce(y2, async_op=False)
+            res = (y.cpu(), y2.cpu())
+        elif op == "rs":
+            y = torch.empty(n // world, dtype=dtype, device="cuda")
+            comm.reduce_scatter(y, x, async_op=False)
+            res = (y.cpu(),)
+        else:
+            y = torch.empty(n * world, dtype=dtype, device="cuda")
+            comm.all_gather(y, x, async_op=False)
+            res = (y.cpu(),)
+        out[i] = res
+    torch.cuda.synchronize()
+    assert comm.error() == 0
+    comm.close()
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_collectives_match_fp32_sums(world):
+    cases = [("ar", 8 * 1000, "bfloat16"), ("ar", 4096 * 768 + 8, "bfloat16"), ("ar", 12288, "float32"),
+             ("ar", 3 * (1 << 20), "bfloat16"),          # > 4 MiB capacity: chunked
+             ("rs", world * 8 * 517, "bfloat16"), ("ag", 8 * 301, "bfloat16"), ("ag", 4 * 77, "float32")]
+    res = run_distributed(_collectives, world, cases, 4, tp_size=world)
+    for i, (op, n, dt) in enumerate(cases):
+        dtype = getattr(torch, dt)
+        xs = [_inputs(r, n, dtype, seed=i) for r in range(world)]
+        total = torch.stack([x.float() for x in xs]).sum(0)
+        for r in range(world):
+            got = res[r][i]
+            if op == "ar":
+                for y in got:
+                    assert torch.allclose(y.float(), total, atol=2e-2, rtol=1e-2), (op, n, r)
+                # fp32 sum in rank order, rounded once: identical on every rank
+                assert torch.equal(got[0], res[0][i][0]) and torch.equal(got[0], got[1])
+            elif op == "rs":
+                sl = total.view(world, -1)[r]
+                assert torch.allclose(got[0].float(), sl, atol=2e-2, rtol=1e-2), (op, n, r)
+            else:
+                assert torch.equal(got[0], torch.cat(xs)), (op, n, r)
+
+
+def _engine(rank, world, heads):
+    from test_multiproc_gpu import _train
+    return _train(rank, world, world, 1, heads)
+
+
+def test_engine_over_xgmi_follows_rccl_path(monkeypatch):
+    """The fused engine with its TP all-reduces on the xGMI kernels tracks the single-rank
+    trajectory (same check as test_multiproc_gpu)."""
+    from test_multiproc_gpu import _ref
+    ref = _ref(12)
+    monkeypatch.setenv("DPFS_TP_COMM", "xgmi")
+    res = run_distributed(_engine, 2, 12, tp_size=2)
+    for r, losses in res.items():
+        for a, b in zip(losses, ref):
+            assert abs(a - b) < 2e-2 * max(1.0, abs(b)), (r, losses, ref)
+    assert len({tuple(v) for v in res.values()}) == 1

@@ -60,8 +60,9 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> str:
 
     os.makedirs(OBJ, exist_ok=True)
     hipcc = _hipcc()
-    headers = glob.glob(os.path.join(CSRC, "kernels", "*.h"))
-    kernels = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    headers = glob.glob(os.path.join(CSRC, "kernels", "*.h")) + glob.glob(os.path.join(CSRC, "comm", "*.h"))
+    kernels = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))) + \
+        sorted(glob.glob(os.path.join(CSRC, "comm", "*.hip")))
     hip_flags = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
                  "-munsafe-fp-atomics", "-Wno-unused-result"]
     jobs_list = []
