@@ -47,7 +47,9 @@ def parse():
     ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--batch-per-gpu", type=int, default=32)
     ap.add_argument("--global-batch", type=int, default=None, help="override (strong scaling)")
-    ap.add_argument("--sp", action="store_true", help="Megatron sequence parallelism")
+    ap.add_argument("--sp", choices=["auto", "on", "off"], default="auto",
+                    help="Megatron sequence parallelism; auto = time both during the warmup steps "
+                         "(TP > 1, warmup >= 4) and keep the faster, else on for TP >= 4")
     ap.add_argument("--impl", choices=["ours", "reference"], default="ours")
     ap.add_argument("--layers", type=int, default=None, help="debug only: not a valid headline number")
     ap.add_argument("--seed", type=int, default=0)
@@ -60,6 +62,7 @@ def main():
     from distributed_pytorch_from_scratch_amd.ops.optim import FusedAdam
     from distributed_pytorch_from_scratch_amd.engine import TrainStep
     from distributed_pytorch_from_scratch_amd.utils.dist import init_dist_env, set_seed
+    from distributed_pytorch_from_scratch_amd.parallel import tp_comm
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world == 1 and a.gpus > 1:
@@ -71,7 +74,9 @@ def main():
     rank = dist.get_rank()
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
 
-    overrides = dict(sequence_parallel=a.sp)
+    # SP is a property of the step, not of the weights: build with the SP attributes and
+    # switch the engine per step (TrainStep.sp / args.sequence_parallel).
+    overrides = dict(sequence_parallel=world > 1 and a.sp != "off")
     if a.layers:
         overrides["num_layers"] = a.layers
     args = get_preset(a.model, **overrides)
@@ -116,8 +121,41 @@ def main():
             opt.step()
             return loss.detach()
 
-    for i in range(a.warmup):
-        loss = run(i)
+    def set_sp(on: bool):
+        if a.impl == "ours":
+            model.args.sequence_parallel = on
+            step.sp = on
+
+    sp_trial = {}
+    if a.impl == "ours" and world > 1 and a.sp == "auto" and a.warmup >= 4:
+        # The warmup steps double as the SP on/off trial: half each, the first step of each
+        # half untimed (first-call GEMM selection / transport choice), max over ranks.
+        half = a.warmup // 2
+        i = 0
+        for on in (False, True):
+            set_sp(on)
+            for j in range(half):
+                if j == 1:
+                    if dev.type == "cuda":
+                        torch.cuda.synchronize()
+                    dist.barrier()
+                    t0 = time.perf_counter()
+                loss = run(i)
+                i += 1
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+            dt_ = torch.tensor([(time.perf_counter() - t0) / (half - 1)], dtype=torch.float64, device=dev)
+            dist.all_reduce(dt_, op=dist.ReduceOp.MAX)
+            sp_trial[on] = float(dt_.item())
+        set_sp(sp_trial[True] < sp_trial[False])
+        for _ in range(a.warmup - 2 * half):
+            loss = run(i)
+            i += 1
+    else:
+        set_sp(world > 1 and (a.sp == "on" or (a.sp == "auto" and world >= 4)))
+        for i in range(a.warmup):
+            loss = run(i)
+    sp_used = bool(a.impl == "ours" and model.args.sequence_parallel)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dist.barrier()
@@ -161,9 +199,11 @@ def main():
             "model": a.model + (f"(L={a.layers})" if a.layers else ""),
             "global_batch": gb,
             "seq_len": T,
-            "parallelism": f"tp{world}" + ("+sp" if a.sp else ""),
+            "parallelism": f"tp{world}" + ("+sp" if sp_used else ""),
             "impl": a.impl,
             "params_matmul": args.matmul_params(),
+            "tp_comm": tp_comm.info(),
+            "sp_trial_ms": {("sp" if k else "nosp"): round(1000 * v, 2) for k, v in sp_trial.items()} or None,
         },
         "tflops_per_gpu": round(value * mflops / world / 1e12, 2),
         "mfu_vs_2.5pf_dense_bf16": round(value * mflops / world / 2.5e15, 4),

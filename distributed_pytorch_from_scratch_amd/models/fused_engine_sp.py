@@ -1,0 +1,267 @@
+"""Explicit-schedule training step with Megatron sequence parallelism (``--sp``).
+
+Same math and kernels as :mod:`.fused_engine`, but the residual stream between the
+tensor-parallel blocks is sharded over the TP group by token rows (rank r holds rows
+``[r*M/n, (r+1)*M/n)`` of every chunk):
+
+* forward, per block: ``RS`` (reduce-scatter) of the row-parallel output replaces the
+  all-reduce; bias + residual + RMSNorm run on the local rows only; an ``AG`` (all-gather) of
+  the normed rows feeds the next column-parallel GEMM;
+* backward, mirrored: the column-parallel input-gradient is reduce-scattered, the norm
+  backward runs on the local rows, and the residual gradient is all-gathered for the
+  row-parallel dgrad / wgrad.
+
+The bytes on the wire equal the all-reduce version (RS + AG = one all-reduce), but every
+per-token elementwise op (norms, residual adds) does 1/n of the work.  At TP = 8 on the
+GPT-2-small bench shape that removes ~19 ms/step of replicated norm work (24 add+RMSNorm
+forwards at 537 us and 24 norm backwards at 368 us for 262k rows, profiles/).  The gradients
+of the replicated parameters (norm scales, row-parallel biases) come out as per-rank partial
+sums over the local rows, exactly like the modular SP layers; ``TrainStep`` sums them over
+the TP group (``allreduce_sequence_parallel_grads``), so they end bitwise identical on every
+rank.
+
+Chunks (ping-pong) and the per-phase interleaving work as in the all-reduce engine: each
+collective is launched async and waited by the next phase of the same chunk, after the other
+chunk's phase has been enqueued.  Reference parity: the reference has no sequence
+parallelism; the modular layers' SP path (``parallel/comm_ops.py``
+``ScatterSeq`` / ``GatherSeq``) computes the same function.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.distributed as dist
+
+from ..ops import gemm_select as GS
+from ..ops.dispatch import K, shadow
+from ..parallel import process_manager as pm
+from ..parallel import tp_comm
+from .fused_engine import _Layer, _addg, _split, _wait
+
+
+def _rs(full: torch.Tensor, n: int):
+    """Reduce-scatter rows of ``full`` -> (local rows, work)."""
+    out = full.new_empty((full.size(0) // n,) + tuple(full.shape[1:]))
+    return out, tp_comm.reduce_scatter(out, full, async_op=True)
+
+
+def _ag(part: torch.Tensor, n: int):
+    """All-gather rows of ``part`` -> (full rows, work)."""
+    out = part.new_empty((part.size(0) * n,) + tuple(part.shape[1:]))
+    return out, tp_comm.all_gather(out, part, async_op=True)
+
+
+class DecoderTrainFnSP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, model, ids, pos, tgt, chunks: int, ignore_index: int, *params):
+        dev = ids.device
+        dt = model.act_dtype(dev)
+        k = K(model.embedding.weight)
+        p = pm.pgm
+        n = p.tp_size
+        B, T = ids.shape
+        C = max(1, min(chunks, B))
+        bounds = [(B * i) // C for i in range(C + 1)]
+        layers = [_Layer(l) for l in model.layers]
+        tab = model.rope_table(dev)
+        emb, head = model.embedding, model.lm_head
+        vst = head.odim_start
+        vvalid = max(0, min(model.vocab_size - vst, head.odim_partition))
+        W = lambda w: shadow(w, dt) if w is not None else None
+        st = []
+        for c in range(C):
+            b0, b1 = bounds[c], bounds[c + 1]
+            assert ((b1 - b0) * T) % n == 0, "sequence parallelism: chunk rows must divide by tp_size"
+            ids_c = ids[b0:b1].reshape(-1).contiguous()
+            x_s, h = _rs(k.embedding_fwd(ids_c, emb.weight, emb.vocab_st_idx, dt), n)
+            st.append(dict(B=b1 - b0, ids=ids_c, pos=pos[b0:b1].reshape(-1).contiguous(),
+                           tgt=tgt[b0:b1].reshape(-1).contiguous(), x=x_s, h=h, pend=None, pend_bias=None,
+                           layers=[]))
+        for L in layers:
+            for s in st:    # P1: (bias + residual +) norm1 on my rows -> all-gather
+                _wait(s["h"])
+                if s["pend"] is not None:
+                    s["x"], h1s, r1 = k.add_rmsnorm_fwd(s["pend"], s["pend_bias"], s["x"], L.s1, L.eps1)
+                else:
+                    h1s, r1 = k.rmsnorm_fwd(s["x"], L.s1, L.eps1)
+                h1, s["h"] = _ag(h1s, n)
+                s["layers"].append(dict(x=s["x"], r1=r1, h1=h1))
+            for s in st:    # P2: QKV (+RoPE), attention, Wo -> reduce-scatter
+                _wait(s["h"])
+                a = s["layers"][-1]
+                qkv = k.gemm_nt(a["h1"], W(L.wqkv), L.bqkv, s["pos"], tab, 2 * L.h, L.hd)
+                q, kk, v = _split(qkv, s["B"], T, L.h, L.hd)
+                o, lse = k.attn_fwd(q, kk, v, 1.0 / math.sqrt(L.hd), True)
+                pout = GS.gemm_nt(k, o.view(qkv.size(0), L.h * L.hd), W(L.wo), None)
+                a.update(qkv=qkv, o=o, lse=lse)
+                (s["pend"], s["h"]), s["pend_bias"] = _rs(pout, n), L.bo
+            for s in st:    # P3: bias + residual + norm2 on my rows -> all-gather
+                _wait(s["h"])
+                a = s["layers"][-1]
+                x2, h2s, r2 = k.add_rmsnorm_fwd(s["pend"], s["pend_bias"], s["x"], L.s2, L.eps2)
+                h2, s["h"] = _ag(h2s, n)
+                a.update(x2=x2, r2=r2, h2=h2)
+                s["x"] = x2
+            for s in st:    # P4: gate|up, SwiGLU, down -> reduce-scatter
+                _wait(s["h"])
+                a = s["layers"][-1]
+                gu = GS.gemm_nt(k, a["h2"], W(L.wgu), L.bgu)
+                sw = k.swiglu_fwd(gu)
+                qout = GS.gemm_nt(k, sw, W(L.wd), None)
+                a.update(gu=gu, sw=sw)
+                (s["pend"], s["h"]), s["pend_bias"] = _rs(qout, n), L.bd
+        for s in st:        # final norm on my rows -> all-gather
+            _wait(s["h"])
+            xf, hfs, rf = k.add_rmsnorm_fwd(s["pend"], s["pend_bias"], s["x"], model.norm.scale, model.norm.eps)
+            hf, s["h"] = _ag(hfs, n)
+            s.update(xf=xf, rf=rf, hf=hf)
+            del s["pend"]
+        losses_sum = torch.zeros((), device=dev, dtype=torch.float32)
+        n_valid_total = torch.zeros((), device=dev, dtype=torch.float32)
+        for s in st:        # lm_head shard + vocab-parallel CE statistics
+            _wait(s["h"])
+            logits = GS.gemm_nt(k, s["hf"], W(head.weight), head.bias)
+            stats = k.ce_fwd_stats(logits, s["tgt"], vst, vvalid)
+            allst = stats.new_empty((n * stats.size(0), 3))
+            dist.all_gather_into_tensor(allst, stats, group=p.tp_group)
+            allst = allst.view(n, -1, 3)
+            mx = allst[..., 0].amax(0)
+            lse = mx + torch.log((allst[..., 1] * torch.exp(allst[..., 0] - mx)).sum(0))
+            tl = allst[..., 2].sum(0)
+            valid = s["tgt"] != ignore_index
+            losses_sum = losses_sum + torch.where(valid, lse - tl, torch.zeros_like(lse)).sum()
+            n_valid_total = n_valid_total + valid.sum()
+            s.update(logits=logits, ce_lse=lse, valid=valid, h=None)
+        n_valid_total = n_valid_total.clamp_min(1.0)
+        ctx.model, ctx.st, ctx.layers, ctx.meta = model, st, layers, (T, dt, vst, vvalid, n)
+        ctx.n_valid, ctx.tab = n_valid_total, tab
+        return losses_sum / n_valid_total
+
+    @staticmethod
+    def backward(ctx, gloss):
+        model, st, layers = ctx.model, ctx.st, ctx.layers
+        T, dt, vst, vvalid, n = ctx.meta
+        k = K(model.embedding.weight)
+        head = model.lm_head
+        W = lambda w: shadow(w, dt) if w is not None else None
+        tab = ctx.tab
+        gscale_all = gloss.float() / ctx.n_valid
+        nL = len(layers)
+        g = {"emb": None, "nf": None, "lm_w": None, "lm_b": None}
+        gl = [dict() for _ in range(nL)]
+
+        def tn(d, key, dy, x):
+            if d.get(key) is None:
+                d[key] = GS.gemm_tn(k, dy, x)
+            else:
+                GS.gemm_tn(k, dy, x, d[key], True)
+
+        pg = pm.pgm
+        dp = pg.dp_size
+        dp_pending = []
+
+        def dp_reduce(d: dict, keys=None):
+            if dp <= 1:
+                return
+            keys = [key for key in (keys or sorted(d)) if d.get(key) is not None]
+            if keys:
+                flat = torch.cat([d[key].reshape(-1) for key in keys])
+                dp_pending.append((dist.all_reduce(flat, group=pg.dp_group, async_op=True), flat, d, keys))
+
+        for s in st:    # CE backward in place, lm_head dgrad -> reduce-scatter, lm_head wgrad
+            gs = s["valid"].float() * gscale_all
+            dl = s["logits"]
+            db = dl.new_empty(dl.size(1), dtype=torch.float32) if head.bias is not None else None
+            k.ce_bwd(dl, s["tgt"], s["ce_lse"], gs, vst, vvalid, dl, db)
+            s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dl, W(head.weight)), n)
+            tn(g, "lm_w", dl, s["hf"])
+            if db is not None:
+                g["lm_b"] = _addg(g["lm_b"], db)
+            del s["logits"], s["hf"]
+        for s in st:    # final norm backward on my rows -> all-gather the residual grad
+            _wait(s["h"])
+            s["g"], dsf = k.rmsnorm_bwd(s["dpend"], s["xf"], model.norm.scale, s["rf"])
+            g["nf"] = _addg(g["nf"], dsf)
+            s["gfull"], s["h"] = _ag(s["g"], n)
+            del s["xf"], s["rf"], s["dpend"]
+        dp_reduce(g, ("lm_w", "lm_b"))
+        for li in range(nL - 1, -1, -1):
+            L, G = layers[li], gl[li]
+            for s in st:    # B4: down / SwiGLU / gate|up grads -> reduce-scatter
+                _wait(s["h"])
+                a, gq = s["layers"][li], s["gfull"]
+                if L.bd is not None:   # partial over my rows (summed over TP by TrainStep)
+                    G["bd"] = _addg(G.get("bd"), k.bias_grad(s["g"]))
+                ds = GS.gemm_nn(k, gq, W(L.wd))
+                tn(G, "wd", gq, a["sw"])
+                dbgu = ds.new_empty(a["gu"].size(1), dtype=torch.float32) if L.bgu is not None else None
+                dgu = k.swiglu_bwd(ds, a["gu"], dbgu)
+                s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dgu, W(L.wgu)), n)
+                tn(G, "wgu", dgu, a["h2"])
+                if dbgu is not None:
+                    G["bgu"] = _addg(G.get("bgu"), dbgu)
+                del a["sw"], a["gu"], a["h2"], s["gfull"]
+            for s in st:    # B3: norm2 backward (+ residual grad) on my rows -> all-gather
+                _wait(s["h"])
+                a = s["layers"][li]
+                s["g"], ds2 = k.rmsnorm_bwd(s["dpend"], a["x2"], L.s2, a["r2"], s["g"])
+                G["s2"] = _addg(G.get("s2"), ds2)
+                s["gfull"], s["h"] = _ag(s["g"], n)
+                del a["x2"], a["r2"], s["dpend"]
+            for s in st:    # B2: Wo / attention / QKV grads -> reduce-scatter
+                _wait(s["h"])
+                a, g2 = s["layers"][li], s["gfull"]
+                if L.bo is not None:
+                    G["bo"] = _addg(G.get("bo"), k.bias_grad(s["g"]))
+                do = GS.gemm_nn(k, g2, W(L.wo))
+                tn(G, "wo", g2, a["o"].view(g2.size(0), -1))
+                Bc = s["B"]
+                q, kk, v = _split(a["qkv"], Bc, T, L.h, L.hd)
+                dqkv = torch.empty_like(a["qkv"])
+                dq, dk, dv = _split(dqkv, Bc, T, L.h, L.hd)
+                k.attn_bwd(do.view(Bc, T, L.h, L.hd), q, kk, v, a["o"], a["lse"], 1.0 / math.sqrt(L.hd), True,
+                           dq, dk, dv, s["pos"], tab)
+                s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dqkv, W(L.wqkv)), n)
+                tn(G, "wqkv", dqkv, a["h1"])
+                if L.bqkv is not None:
+                    G["bqkv"] = _addg(G.get("bqkv"), k.bias_grad(dqkv))
+                for key in ("qkv", "o", "lse", "h1"):
+                    a.pop(key, None)
+                del s["gfull"]
+            for s in st:    # B1: norm1 backward (+ residual grad) on my rows -> all-gather
+                _wait(s["h"])
+                a = s["layers"][li]
+                s["g"], ds1 = k.rmsnorm_bwd(s["dpend"], a["x"], L.s1, a["r1"], s["g"])
+                G["s1"] = _addg(G.get("s1"), ds1)
+                s["gfull"], s["h"] = _ag(s["g"], n)
+                del a["x"], a["r1"], s["dpend"]
+            dp_reduce(G)
+        for s in st:    # embedding backward over all rows of the chunk (vocab-sharded table)
+            _wait(s["h"])
+            dwe = k.embedding_bwd(s["gfull"], s["ids"], model.embedding.weight.size(0),
+                                  model.embedding.vocab_st_idx)
+            g["emb"] = _addg(g["emb"], dwe)
+            del s["gfull"]
+        dp_reduce(g, ("emb", "nf"))
+        tp_comm.check()
+        if dp_pending:
+            model._dpfs_dp_reduced = True
+        for h, flat, d, keys in dp_pending:
+            h.wait()
+            flat /= dp
+            off = 0
+            for key in keys:
+                num = d[key].numel()
+                d[key] = flat[off:off + num].view_as(d[key])
+                off += num
+        ctx.st = None
+        grads = [g["emb"]]
+        for li, L in enumerate(layers):
+            G = gl[li]
+            grads += [G["s1"], G["wqkv"], G.get("bqkv") if L.bqkv is not None else None,
+                      G["wo"], G.get("bo") if L.bo is not None else None, G["s2"], G["wgu"],
+                      G.get("bgu") if L.bgu is not None else None, G["wd"],
+                      G.get("bd") if L.bd is not None else None]
+        grads += [g["nf"], g["lm_w"], g["lm_b"] if head.bias is not None else None]
+        return (None, None, None, None, None, None) + tuple(grads)

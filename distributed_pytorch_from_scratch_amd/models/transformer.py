@@ -239,7 +239,9 @@ class Transformer(nn.Module):
         return logits[..., : self.vocab_size].reshape(B, T, self.vocab_size)
 
     def fused_supported(self) -> bool:
-        return (not self.args.sequence_parallel) and self.args.norm == "rmsnorm" and self.use_fused_engine
+        """The explicit-schedule engines cover RMSNorm blocks, with (``fused_engine_sp``) or
+        without (``fused_engine``) sequence parallelism; LayerNorm models use the modular path."""
+        return self.args.norm == "rmsnorm" and self.use_fused_engine
 
     def overlap_chunks(self) -> int:
         p = pm.pgm
@@ -257,8 +259,12 @@ class Transformer(nn.Module):
         if self.fused_supported():
             from .fused_engine import DecoderTrainFn, collect_params
             assert input_ids.size(1) <= self.args.maxlen
-            return DecoderTrainFn.apply(self, input_ids, position_ids, target_ids.reshape(input_ids.shape),
-                                        self.overlap_chunks(), ignore_index, *collect_params(self))
+            p = pm.pgm
+            fn = DecoderTrainFn
+            if self.args.sequence_parallel and p is not None and p.tp_size > 1:
+                from .fused_engine_sp import DecoderTrainFnSP as fn
+            return fn.apply(self, input_ids, position_ids, target_ids.reshape(input_ids.shape),
+                            self.overlap_chunks(), ignore_index, *collect_params(self))
         h, B, T = self._trunk(input_ids, position_ids)
         logits = self._lm_head_local(h)
         st = self.lm_head.odim_start

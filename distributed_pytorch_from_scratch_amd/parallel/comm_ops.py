@@ -35,6 +35,7 @@ import torch
 import torch.distributed as dist
 
 from . import process_manager as pm
+from . import tp_comm
 
 
 def _tp():
@@ -86,7 +87,7 @@ def all_reduce_(x: torch.Tensor, async_op: bool = False):
     n, _, group = _tp()
     if n == 1:
         return None
-    return dist.all_reduce(x, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+    return tp_comm.all_reduce(x, async_op=async_op)
 
 
 class Split(torch.autograd.Function):
@@ -153,7 +154,7 @@ def reduce_scatter_rows(x: torch.Tensor) -> torch.Tensor:
     x = x.contiguous()
     assert x.size(0) % n == 0, f"rows {x.size(0)} not divisible by tp_size {n}"
     out = x.new_empty((x.size(0) // n,) + tuple(x.shape[1:]))
-    dist.reduce_scatter_tensor(out, x, op=dist.ReduceOp.SUM, group=group)
+    tp_comm.reduce_scatter(out, x, async_op=False)
     return out
 
 
@@ -163,7 +164,7 @@ def all_gather_rows(x: torch.Tensor, async_op: bool = False):
         return (x, None) if async_op else x
     x = x.contiguous()
     out = x.new_empty((x.size(0) * n,) + tuple(x.shape[1:]))
-    h = dist.all_gather_into_tensor(out, x, group=group, async_op=async_op)
+    h = tp_comm.all_gather(out, x, async_op=async_op)
     return (out, h) if async_op else out
 
 

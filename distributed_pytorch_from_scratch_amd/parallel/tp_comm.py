@@ -94,6 +94,8 @@ def _decide(t: torch.Tensor, p) -> Optional[object]:
 
 
 def _comm(t: torch.Tensor, p):
+    if t.dtype not in (torch.bfloat16, torch.float32) or not t.is_cuda:
+        return None
     key = id(p.tp_group)
     if key not in _decisions:
         _decisions[key] = _decide(t, p)
@@ -117,7 +119,11 @@ def all_reduce(t: torch.Tensor, async_op: bool = True):
 
 
 def reduce_scatter(out: torch.Tensor, inp: torch.Tensor, async_op: bool = True):
+    """out = rank-th of tp_size equal row blocks of SUM(inp) over the TP group."""
     p = pm.pgm
+    if p is None or p.tp_size == 1:
+        out.copy_(inp.view_as(out))
+        return None
     c = _comm(inp, p)
     if c is None or inp.numel() * inp.element_size() > c.cap or inp.numel() % (8 * p.tp_size):
         return dist.reduce_scatter_tensor(out, inp, group=p.tp_group, async_op=async_op)
@@ -125,7 +131,11 @@ def reduce_scatter(out: torch.Tensor, inp: torch.Tensor, async_op: bool = True):
 
 
 def all_gather(out: torch.Tensor, inp: torch.Tensor, async_op: bool = True):
+    """out = concatenation (rank order, dim 0) of inp over the TP group."""
     p = pm.pgm
+    if p is None or p.tp_size == 1:
+        out.copy_(inp.view_as(out))
+        return None
     c = _comm(inp, p)
     if c is None or inp.numel() * inp.element_size() > c.cap or inp.numel() % 8:
         return dist.all_gather_into_tensor(out, inp, group=p.tp_group, async_op=async_op)

@@ -23,10 +23,11 @@ def _json_lines(out):
     return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
 
 
-@pytest.mark.parametrize("world", [1, 2])
-def test_bench_prints_one_json_line(world):
+@pytest.mark.parametrize("world,warmup", [(1, 1), (2, 1), (2, 4)])
+def test_bench_prints_one_json_line(world, warmup):
+    """warmup >= 4 at TP > 1 runs the SP on/off trial inside the warmup steps."""
     from dist_helpers import _free_port
-    args = ["--gpus", str(world), "--model", "plumbing", "--steps", "2", "--warmup", "1", "--seq-len", "64",
+    args = ["--gpus", str(world), "--model", "plumbing", "--steps", "2", "--warmup", str(warmup), "--seq-len", "64",
             "--batch-per-gpu", "2"]
     if world == 1:
         cmd = [sys.executable, "bench.py"] + args
@@ -39,6 +40,8 @@ def test_bench_prints_one_json_line(world):
     assert len(lines) == 1, r.stdout
     d = lines[0]
     assert REQUIRED <= d.keys()
-    assert d["n_gpus"] == world and d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "weak"
-    assert d["config"]["parallelism"] == f"tp{world}" and d["config"]["global_batch"] == 2 * world
+    assert d["n_gpus"] == world and d["steps"] == 2 and d["warmup"] == warmup and d["scaling"] == "weak"
+    assert d["config"]["parallelism"] in (f"tp{world}", f"tp{world}+sp") and d["config"]["global_batch"] == 2 * world
+    if warmup >= 4:
+        assert set(d["config"]["sp_trial_ms"]) == {"sp", "nosp"}
     assert d["value"] > 0 and d["higher_is_better"] is True

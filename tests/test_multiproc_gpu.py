@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 STEPS = 3
 
 
-def _train(rank, world, tp, dp, heads, dev="cuda"):
+def _train(rank, world, tp, dp, heads, dev="cuda", sp=False):
     import torch.distributed as dist
     if dev == "cuda":
         torch.cuda.set_device(0)
@@ -25,7 +25,8 @@ def _train(rank, world, tp, dp, heads, dev="cuda"):
     from distributed_pytorch_from_scratch_amd.engine import TrainStep
     from distributed_pytorch_from_scratch_amd.parallel import process_manager as pm
     from distributed_pytorch_from_scratch_amd.utils.dist import set_seed
-    args = get_preset("gpt2-small", num_layers=2, num_heads=heads, vocab_size=1000, vocab_pad_to=1)
+    args = get_preset("gpt2-small", num_layers=2, num_heads=heads, vocab_size=1000, vocab_pad_to=1,
+                      sequence_parallel=sp)
     m = Transformer.from_args(args).to(dev)
     set_seed(0)
     m.reset_parameters()
@@ -55,10 +56,11 @@ def _ref(heads):
     return run_distributed(_train, 1, 1, 1, heads, tp_size=1)[0]
 
 
-@pytest.mark.parametrize("world,tp,dp,heads", [(2, 2, 1, 12), (4, 4, 1, 6), (4, 2, 2, 12)])
-def test_multirank_engine_follows_single_rank(world, tp, dp, heads):
+@pytest.mark.parametrize("world,tp,dp,heads,sp", [(2, 2, 1, 12, False), (4, 4, 1, 6, False), (4, 2, 2, 12, False),
+                                                 (2, 2, 1, 12, True), (4, 2, 2, 12, True)])
+def test_multirank_engine_follows_single_rank(world, tp, dp, heads, sp):
     ref = _ref(heads)
-    res = run_distributed(_train, world, tp, dp, heads, tp_size=tp)
+    res = run_distributed(_train, world, tp, dp, heads, "cuda", sp, tp_size=tp)
     for r, losses in res.items():
         for a, b in zip(losses, ref):
             assert abs(a - b) < 2e-2 * max(1.0, abs(b)), (r, losses, ref)

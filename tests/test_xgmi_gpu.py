@@ -75,18 +75,21 @@ def test_xgmi_collectives_match_fp32_sums(world):
                 assert torch.equal(got[0], torch.cat(xs)), (op, n, r)
 
 
-def _engine(rank, world, heads):
+def _engine(rank, world, heads, sp):
     from test_multiproc_gpu import _train
-    return _train(rank, world, world, 1, heads)
+    return _train(rank, world, world, 1, heads, "cuda", sp)
 
 
-def test_engine_over_xgmi_follows_rccl_path(monkeypatch):
-    """The fused engine with its TP all-reduces on the xGMI kernels tracks the single-rank
-    trajectory (same check as test_multiproc_gpu)."""
+@pytest.mark.parametrize("world,sp", [(2, False), (2, True), (4, True)])
+def test_engine_over_xgmi_follows_single_rank(monkeypatch, world, sp):
+    """The fused engines with their TP collectives on the xGMI kernels (all-reduce; or
+    reduce-scatter / all-gather under sequence parallelism) track the single-rank trajectory
+    (same check as test_multiproc_gpu)."""
     from test_multiproc_gpu import _ref
-    ref = _ref(12)
+    heads = 12
+    ref = _ref(heads)
     monkeypatch.setenv("DPFS_TP_COMM", "xgmi")
-    res = run_distributed(_engine, 2, 12, tp_size=2)
+    res = run_distributed(_engine, world, heads, sp, tp_size=world)
     for r, losses in res.items():
         for a, b in zip(losses, ref):
             assert abs(a - b) < 2e-2 * max(1.0, abs(b)), (r, losses, ref)
