@@ -75,19 +75,26 @@ def _decide(t: torch.Tensor, p) -> Optional[object]:
     err = (y.float() - ref).abs().max().item()
     tol = 1e-2 * max(1.0, ref.abs().max().item())
     good = comm.error() == 0 and err <= tol
-    stats = torch.tensor([0.0 if good else 1.0, 0.0, 0.0], device=t.device)
+    grids = (128, 256, 512)
+    stats = torch.zeros(2 + len(grids), device=t.device)
+    stats[0] = 0.0 if good else 1.0
     if good and m == "auto" and backend == "nccl":
         a = t.detach().clone()
-        stats[1] = _time_ms(lambda: comm.all_reduce(a, async_op=False))
-        stats[2] = _time_ms(lambda: dist.all_reduce(a, group=g))
+        for i, nb in enumerate(grids):     # workgroups per call: link-latency hiding vs CUs taken
+            comm.set_blocks(nb)
+            stats[2 + i] = _time_ms(lambda: comm.all_reduce(a, async_op=False))
+        stats[1] = _time_ms(lambda: dist.all_reduce(a, group=g))
         comm.check()
     dist.all_reduce(stats, op=dist.ReduceOp.MAX, group=g)
-    bad, t_x, t_r = stats.tolist()
+    bad, t_r = stats[0].item(), stats[1].item()
+    best = 1 if bad or m != "auto" or backend != "nccl" else int(torch.argmin(stats[2:]).item())
+    t_x = stats[2 + best].item()
+    comm.set_blocks(grids[best])
     use = bad == 0 and (m == "xgmi" or t_x < 0.97 * t_r)
     if m == "xgmi" and bad:
         raise RuntimeError(f"xGMI all-reduce failed validation (max err {err:.3g}, timeout flag {comm.error()})")
     _info[id(g)] = dict(transport="xgmi" if use else "rccl", xgmi_ms=round(t_x, 3), rccl_ms=round(t_r, 3),
-                        bytes=t.numel() * t.element_size(), valid=not bad)
+                        xgmi_blocks=grids[best], bytes=t.numel() * t.element_size(), valid=not bad)
     if p.global_rank == 0 and os.environ.get("DPFS_QUIET", "0") != "1":
         print(f"[dpfs] TP collectives: {_info[id(g)]}", file=sys.stderr, flush=True)
     return comm if use else None

@@ -120,6 +120,10 @@ class XgmiComm:
             return None
         return work
 
+    def set_blocks(self, blocks: int):
+        """Workgroups per collective launch (must be equal on every rank of the group)."""
+        self.C.xgmi_set_blocks(self.h, int(blocks))
+
     # --------------------------------------------------------------------- health ----
     def error(self) -> int:
         """Non-zero once any barrier of any call timed out (host-mapped word, no sync)."""
