@@ -121,40 +121,45 @@ def main():
             opt.step()
             return loss.detach()
 
-    def set_sp(on: bool):
+    def set_cfg(cfg):
         if a.impl == "ours":
+            on, chunks = cfg
             model.args.sequence_parallel = on
             step.sp = on
+            model.chunks = chunks
 
-    sp_trial = {}
-    if a.impl == "ours" and world > 1 and a.sp == "auto" and a.warmup >= 4:
-        # The warmup steps double as the SP on/off trial: half each, the first step of each
-        # half untimed (first-call GEMM selection / transport choice), max over ranks.
-        half = a.warmup // 2
-        i = 0
-        for on in (False, True):
-            set_sp(on)
-            for j in range(half):
-                if j == 1:
-                    if dev.type == "cuda":
-                        torch.cuda.synchronize()
-                    dist.barrier()
-                    t0 = time.perf_counter()
-                loss = run(i)
-                i += 1
-            if dev.type == "cuda":
-                torch.cuda.synchronize()
-            dt_ = torch.tensor([(time.perf_counter() - t0) / (half - 1)], dtype=torch.float64, device=dev)
-            dist.all_reduce(dt_, op=dist.ReduceOp.MAX)
-            sp_trial[on] = float(dt_.item())
-        set_sp(sp_trial[True] < sp_trial[False])
-        for _ in range(a.warmup - 2 * half):
-            loss = run(i)
-            i += 1
+    # Engine configurations (SP on/off, ping-pong chunks), most likely first.  At TP > 1 the
+    # warmup steps double as a trial of as many as fit (2 steps each, the first untimed:
+    # first-call GEMM selection / transport choice); every rank takes the config with the
+    # lowest max-over-ranks step time.  Without a trial: SP from TP 4 up, 2 chunks.
+    default = (world >= 4 and a.sp != "off" or a.sp == "on", 2)
+    cands = [default]
+    if a.sp == "auto":
+        cands += [(not default[0], 2), (True, 4), (False, 4)]
     else:
-        set_sp(world > 1 and (a.sp == "on" or (a.sp == "auto" and world >= 4)))
-        for i in range(a.warmup):
-            loss = run(i)
+        cands += [(a.sp == "on", 4)]
+    cands = list(dict.fromkeys(cands))
+    ntrial = min(len(cands), a.warmup // 2) if a.impl == "ours" and world > 1 else 0
+    trial = {}
+    i = 0
+    for cfg in cands[:ntrial] if ntrial >= 2 else []:
+        set_cfg(cfg)
+        loss = run(i)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        loss = run(i + 1)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        dt_ = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(dt_, op=dist.ReduceOp.MAX)
+        trial[cfg] = float(dt_.item())
+        i += 2
+    set_cfg(min(trial, key=trial.get) if trial else default)
+    for _ in range(a.warmup - i):
+        loss = run(i)
+        i += 1
     sp_used = bool(a.impl == "ours" and model.args.sequence_parallel)
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -203,7 +208,9 @@ def main():
             "impl": a.impl,
             "params_matmul": args.matmul_params(),
             "tp_comm": tp_comm.info(),
-            "sp_trial_ms": {("sp" if k else "nosp"): round(1000 * v, 2) for k, v in sp_trial.items()} or None,
+            "chunks": model.overlap_chunks() if a.impl == "ours" else None,
+            "engine_trial_ms": {f"{'sp' if k[0] else 'nosp'}/c{k[1]}": round(1000 * v, 2)
+                                for k, v in trial.items()} or None,
         },
         "tflops_per_gpu": round(value * mflops / world / 1e12, 2),
         "mfu_vs_2.5pf_dense_bf16": round(value * mflops / world / 2.5e15, 4),

@@ -43,5 +43,5 @@ def test_bench_prints_one_json_line(world, warmup):
     assert d["n_gpus"] == world and d["steps"] == 2 and d["warmup"] == warmup and d["scaling"] == "weak"
     assert d["config"]["parallelism"] in (f"tp{world}", f"tp{world}+sp") and d["config"]["global_batch"] == 2 * world
     if warmup >= 4:
-        assert set(d["config"]["sp_trial_ms"]) == {"sp", "nosp"}
+        assert set(d["config"]["engine_trial_ms"]) == {"nosp/c2", "sp/c2"}
     assert d["value"] > 0 and d["higher_is_better"] is True
