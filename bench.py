@@ -132,7 +132,7 @@ def main():
     # warmup steps double as a trial of as many as fit (2 steps each, the first untimed:
     # first-call GEMM selection / transport choice); every rank takes the config with the
     # lowest max-over-ranks step time.  Without a trial: SP from TP 4 up, 2 chunks.
-    default = (world >= 4 and a.sp != "off" or a.sp == "on", 2)
+    default = (world >= 4 and a.sp != "off" or a.sp == "on", 2 if world > 1 else 1)
     cands = [default]
     if a.sp == "auto":
         cands += [(not default[0], 2), (True, 4), (False, 4)]

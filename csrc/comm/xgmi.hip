@@ -43,7 +43,7 @@ namespace {
 
 constexpr int kMaxRanks = 8;
 constexpr int kMaxBlocks = 1024;
-constexpr int kThreads = 256;
+constexpr int kThreads = 1024;
 constexpr long long kSigBytes = 2LL * kMaxBlocks * kMaxRanks * sizeof(uint32_t);  // [phase][block][src]
 constexpr int kAuxSys = 1 | 16;  // sc0 | sc1: system-coherent (write-through stores, L2-bypassing loads)
 
@@ -148,16 +148,31 @@ __global__ __launch_bounds__(kThreads) void xgmi_coll_k(Peers P, int op, int ran
   const u32x4* xv = reinterpret_cast<const u32x4*>(x);
   u32x4* ov = reinterpret_cast<u32x4*>(out);
 
+  // Every loop below issues all of its loads (one per peer) before its first store, so a
+  // thread keeps W-1 remote 16-byte reads in flight: with few workgroups (the collective must
+  // leave most CUs to the GEMMs running beside it) that is what covers the link latency.
+  __amdgpu_buffer_rsrc_t rin[kMaxRanks], rtmp[kMaxRanks];
+#pragma unroll
+  for (int s = 0; s < kMaxRanks; ++s) {
+    rin[s] = rsrc(P.data[s < W ? s : 0] + in_off, cap);
+    rtmp[s] = rsrc(P.data[s < W ? s : 0] + tmp_off, cap);
+  }
+
   // ---- phase 0: copy-in of what the peers will read
   if (op == 2) {
     for (long long v = v0 + threadIdx.x; v < v1; v += kThreads) st_sys(r_in, (unsigned)(v * 16), xv[v]);
   } else {
-    for (int s = 0; s < W; ++s) {
-      if (s == rank) continue;
-      const long long base = s * part;  // elements
-      for (long long v = v0 + threadIdx.x; v < v1; v += kThreads) {
-        const long long e = base + v * N;
-        if (e < n) st_sys(r_in, (unsigned)(e * sizeof(T)), xv[e / N]);
+    for (long long v = v0 + threadIdx.x; v < v1; v += kThreads) {
+      u32x4 c[kMaxRanks];
+#pragma unroll
+      for (int s = 0; s < kMaxRanks; ++s) {
+        const long long e = s * part + v * N;
+        if (s < W && s != rank && e < n) c[s] = xv[e / N];
+      }
+#pragma unroll
+      for (int s = 0; s < kMaxRanks; ++s) {
+        const long long e = s * part + v * N;
+        if (s < W && s != rank && e < n) st_sys(r_in, (unsigned)(e * sizeof(T)), c[s]);
       }
     }
   }
@@ -165,19 +180,17 @@ __global__ __launch_bounds__(kThreads) void xgmi_coll_k(Peers P, int op, int ran
 
   // ---- phase 1
   if (op == 2) {
-    for (int s = 0; s < W; ++s) {
-      if (s == rank) {
-        for (long long v = v0 + threadIdx.x; v < v1; v += kThreads) ov[(s * part) / N + v] = xv[v];
-      } else {
-        const __amdgpu_buffer_rsrc_t rp = rsrc(P.data[s] + in_off, cap);
-        for (long long v = v0 + threadIdx.x; v < v1; v += kThreads)
-          ov[(s * part) / N + v] = ld_sys(rp, (unsigned)(v * 16));
-      }
+    for (long long v = v0 + threadIdx.x; v < v1; v += kThreads) {
+      u32x4 c[kMaxRanks];
+#pragma unroll
+      for (int s = 0; s < kMaxRanks; ++s)
+        if (s < W) c[s] = (s == rank) ? xv[v] : ld_sys(rin[s], (unsigned)(v * 16));
+#pragma unroll
+      for (int s = 0; s < kMaxRanks; ++s)
+        if (s < W) ov[(s * part) / N + v] = c[s];
     }
   } else {
-    __amdgpu_buffer_rsrc_t rp[kMaxRanks];
-#pragma unroll
-    for (int s = 0; s < kMaxRanks; ++s) rp[s] = rsrc(P.data[s < W ? s : 0] + in_off, cap);
+    const __amdgpu_buffer_rsrc_t* rp = rin;
     const long long base = rank * part;
     for (long long v = v0 + threadIdx.x; v < v1; v += kThreads) {
       const long long e = base + v * N;
@@ -213,13 +226,15 @@ __global__ __launch_bounds__(kThreads) void xgmi_coll_k(Peers P, int op, int ran
 
   // ---- phase 2 (all-reduce): the other ranks' reduced slices
   if (op == 0) {
-    for (int s = 0; s < W; ++s) {
-      if (s == rank) continue;
-      const __amdgpu_buffer_rsrc_t rp = rsrc(P.data[s] + tmp_off, cap);
-      const long long base = s * part;
-      for (long long v = v0 + threadIdx.x; v < v1; v += kThreads) {
-        const long long e = base + v * N;
-        if (e < n) ov[e / N] = ld_sys(rp, (unsigned)(v * 16));
+    for (long long v = v0 + threadIdx.x; v < v1; v += kThreads) {
+      u32x4 c[kMaxRanks];
+#pragma unroll
+      for (int s = 0; s < kMaxRanks; ++s)
+        if (s < W && s != rank && s * part + v * N < n) c[s] = ld_sys(rtmp[s], (unsigned)(v * 16));
+#pragma unroll
+      for (int s = 0; s < kMaxRanks; ++s) {
+        const long long e = s * part + v * N;
+        if (s < W && s != rank && e < n) ov[e / N] = c[s];
       }
     }
   }
@@ -235,7 +250,7 @@ struct Comm {
   uint32_t epoch = 0;
   int* err_host = nullptr;
   int* err_dev = nullptr;
-  int blocks = 256;
+  int blocks = 32;
 };
 
 thread_local char g_msg[512];

@@ -63,7 +63,7 @@ class XgmiComm:
         handles: List[Optional[bytes]] = [None] * self.world
         dist.all_gather_object(handles, handle, group=group)
         C.xgmi_open(self.h, b"".join(handles))
-        blocks = blocks or int(os.environ.get("DPFS_XGMI_BLOCKS", "256"))
+        blocks = blocks or int(os.environ.get("DPFS_XGMI_BLOCKS", "32"))
         C.xgmi_set_blocks(self.h, blocks)
         self.stream = torch.cuda.Stream()
         dist.barrier(group=group)

@@ -77,7 +77,9 @@ def init_dist_env(args: Optional[Namespace] = None, rank: Optional[int] = None, 
         os.environ["RANK"] = str(rank)
         os.environ["LOCAL_RANK"] = str(rank)
         os.environ["WORLD_SIZE"] = str(world_size)
-    backend = backend or default_backend()
+    # DPFS_BACKEND=gloo: several ranks on one GPU (rehearsal of a multi-GPU launch on a
+    # single device; the TP collectives can still run on the xGMI kernels, DPFS_TP_COMM=xgmi).
+    backend = backend or os.environ.get("DPFS_BACKEND") or default_backend()
     kw = {}
     if backend == "nccl":
         torch.cuda.set_device(local_rank)

@@ -93,7 +93,7 @@ def main():
     ap.add_argument("--local", type=int, default=0, help="N ranks on one GPU (gloo bootstrap)")
     ap.add_argument("--sizes", type=int, nargs="+", default=[8, 50, 100, 200])
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--blocks", type=int, nargs="+", default=[128, 256, 512])
+    ap.add_argument("--blocks", type=int, nargs="+", default=[8, 16, 32, 64])
     a = ap.parse_args()
     if a.local:
         import torch.multiprocessing as mp
