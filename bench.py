@@ -131,8 +131,10 @@ def main():
     # Engine configurations (SP on/off, ping-pong chunks), most likely first.  At TP > 1 the
     # warmup steps double as a trial of as many as fit (2 steps each, the first untimed:
     # first-call GEMM selection / transport choice); every rank takes the config with the
-    # lowest max-over-ranks step time.  Without a trial: SP from TP 4 up, 2 chunks.
-    default = (world >= 4 and a.sp != "off" or a.sp == "on", 2 if world > 1 else 1)
+    # lowest max-over-ranks step time.  Without a trial: SP at any TP > 1 and 2 chunks (the
+    # compute-only per-rank step on one MI355X, tools/tp_sim.py: TP 2 / 4 / 8 = 50.0 / 55.1 /
+    # 73.8 ms without SP, 45.8 / 47.9 / 59.9 ms with it; 4 chunks cost 5-9 ms more).
+    default = (world > 1 and a.sp != "off", 2 if world > 1 else 1)
     cands = [default]
     if a.sp == "auto":
         cands += [(not default[0], 2), (True, 4), (False, 4)]

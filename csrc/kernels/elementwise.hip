@@ -159,6 +159,52 @@ __global__ __launch_bounds__(256) void colsum_stage_k(const T* __restrict__ x, f
   }
 }
 
+// Stage 2 of every column sum: out[N] = sum over R rows of fp32 partials[R, N].  R is a few
+// hundred and N small (768 at GPT-2 width), so the stage-1 shape (32 column vectors per block)
+// gave only N/128 blocks of long serial row walks; here a block is 4 column vectors x 64 row
+// lanes (N/16 blocks, R/64 rows per lane), reduced through LDS in a fixed order.
+template <bool VEC>   // VEC: N % 4 == 0, rows 16-B aligned
+__global__ __launch_bounds__(256) void colsum_rows_k(const float* __restrict__ part, float* __restrict__ out, int R,
+                                                     int N_) {
+  __shared__ float red[64][16];
+  const int cv = threadIdx.x & 3, rl = threadIdx.x >> 2;
+  const int c0 = (blockIdx.x * 4 + cv) * 4;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c0 < N_) {
+    for (int r = rl; r < R; r += 64) {
+      const float* p = part + (long long)r * N_ + c0;
+      if constexpr (VEC) {
+        float v[4];
+        load_vec<float>(p, v);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] += v[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (c0 + j < N_) acc[j] += p[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) red[rl][cv * 4 + j] = acc[j];
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    const int col = blockIdx.x * 16 + threadIdx.x;
+    if (col < N_) {
+      float s = 0.f;
+      for (int k = 0; k < 64; ++k) s += red[k][threadIdx.x];
+      out[col] = s;
+    }
+  }
+}
+
+static inline void colsum_rows(const float* part, float* out, int R, int N_, hipStream_t s) {
+  if (N_ % 4 == 0)
+    colsum_rows_k<true><<<dim3((N_ + 15) / 16), 256, 0, s>>>(part, out, R, N_);
+  else
+    colsum_rows_k<false><<<dim3((N_ + 15) / 16), 256, 0, s>>>(part, out, R, N_);
+}
+
 // Row-chunk plan shared by the fused "elementwise + column-sum" kernels: ~2048 blocks of
 // (32 column vectors x 8 row lanes); returns the chunk count, *rpc = rows per chunk.
 static int colsum_plan(int M, int cblocks, int target_blocks, int* rpc) {
@@ -239,8 +285,7 @@ static void colsum_launch(const T* x, float* out, float* ws, int M, int N_, hipS
     return;
   }
   colsum_stage_k<T><<<dim3(cblocks, chunks), 256, 0, s>>>(x, ws, M, N_, rpc);
-  const int cb2 = (N_ / 4 + 31) / 32;
-  colsum_stage_k<float><<<dim3(cb2, 1), 256, 0, s>>>(ws, out, chunks, N_, chunks);
+  colsum_rows(ws, out, chunks, N_, s);
 }
 
 }  // namespace dpfs
@@ -283,16 +328,12 @@ extern "C" void dpfs_swiglu_bwd_dbias(int dtype, const void* dh, const void* gu,
   else
     swiglu_bwd_colsum_k<float><<<dim3(cblocks, chunks), 256, 0, s>>>((const float*)dh, (const float*)gu, (float*)dgu,
                                                                      part, M, F, rpc);
-  if (chunks > 1) {
-    const int cb2 = (2 * F / 4 + 31) / 32;
-    colsum_stage_k<float><<<dim3(cb2, 1), 256, 0, s>>>(ws, dbias, chunks, 2 * F, chunks);
-  }
+  if (chunks > 1) colsum_rows(ws, dbias, chunks, 2 * F, s);
 }
 
 // Stage 2 of a fused column sum: out[N] = sum over `rows` rows of part[rows, N] (fixed order).
 extern "C" void dpfs_colsum_rows_small(const float* part, float* out, int rows, int N, hipStream_t s) {
-  const int cb2 = (N / 4 + 31) / 32;
-  colsum_stage_k<float><<<dim3(cb2, 1), 256, 0, s>>>(part, out, rows, N, rows);
+  colsum_rows(part, out, rows, N, s);
 }
 
 extern "C" int dpfs_colsum_plan(int M, int cblocks, int target_blocks, int* rpc) {

@@ -1,0 +1,90 @@
+"""Per-rank compute time of a TP = N training step, measured on ONE GPU.
+
+Builds the model exactly as TP rank ``--rank`` of an N-way group would (head / ffn / vocab
+shards, per-rank batch = ``batch_per_gpu * N`` for the weak-scaling bench) and runs the fused
+engine with every TP collective replaced by a no-op.  The result is the compute-only step
+time of that rank: the floor a perfectly overlapped N-GPU step can reach, and how much of it
+the replicated work (norms / residuals without SP) costs.  Numerics are meaningless (partial
+sums are never combined); only timing is reported.
+
+    python tools/tp_sim.py --tp 8 [--rank 0] [--steps 5]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+class SimPGM:
+    def __init__(self, tp, rank):
+        self.tp_size, self.tp_rank = tp, rank
+        self.dp_size, self.dp_rank = 1, 0
+        self.global_rank, self.world_size = 0, 1      # world 1: init broadcasts are skipped
+        self.tp_group = self.dp_group = None
+        self.tp_ranks, self.dp_ranks = list(range(tp)), [0]
+        self.tp_src_rank = 0
+        self.backend = "gloo"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tp", type=int, default=8)
+    ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--model", default="gpt2-small")
+    ap.add_argument("--seq-len", type=int, default=1024)
+    ap.add_argument("--batch-per-gpu", type=int, default=32)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--configs", default="nosp:2,sp:2,sp:4,nosp:4")
+    a = ap.parse_args()
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29581")
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    from distributed_pytorch_from_scratch_amd.parallel import process_manager as pm, tp_comm
+    from distributed_pytorch_from_scratch_amd.models import fused_engine_sp  # noqa: F401
+    pm.pgm = SimPGM(a.tp, a.rank)
+    tp_comm.all_reduce = lambda t, async_op=True: None
+    tp_comm.reduce_scatter = lambda out, inp, async_op=True: None
+    tp_comm.all_gather = lambda out, inp, async_op=True: None
+    n = a.tp
+    dist.all_gather_into_tensor = lambda out, inp, group=None, async_op=False: out.view(n, -1).copy_(
+        inp.reshape(1, -1).expand(n, -1))
+    dist.all_reduce = lambda t, *args, **kw: None
+    from distributed_pytorch_from_scratch_amd.models import get_preset, Transformer
+    from distributed_pytorch_from_scratch_amd.ops.optim import FusedAdam
+    from distributed_pytorch_from_scratch_amd.engine import TrainStep
+    dev = torch.device("cuda", 0)
+    args = get_preset(a.model, sequence_parallel=True)
+    model = Transformer.from_args(args).to(dev)
+    model.reset_parameters()
+    opt = FusedAdam(model.parameters(), lr=3e-4)
+    step = TrainStep(model, opt)
+    B, T = a.batch_per_gpu * n, a.seq_len
+    ids = torch.randint(0, args.vocab_size, (B, T + 1), device=dev)
+    pos = torch.arange(T, device=dev).unsqueeze(0).expand(B, T).contiguous()
+    res = {}
+    for cfg in a.configs.split(","):
+        sp, c = cfg.split(":")
+        model.args.sequence_parallel = step.sp = sp == "sp"
+        model.chunks = int(c)
+        for _ in range(2):
+            step(ids[:, :-1], pos, ids[:, 1:])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step(ids[:, :-1], pos, ids[:, 1:])
+        torch.cuda.synchronize()
+        res[cfg] = round(1000 * (time.perf_counter() - t0) / a.steps, 2)
+        print(json.dumps({"tp": n, "rank": a.rank, "config": cfg, "ms_per_step": res[cfg],
+                          "tokens": B * T}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
