@@ -66,6 +66,12 @@ void dpfs_attn_fwd(const void*, const void*, const void*, void*, float*, int, in
 void dpfs_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, float*, void*, void*,
                    void*, int, int, int, int, long long, long long, long long, long long, long long, long long,
                    long long, long long, float, int, const int64_t*, const float*, hipStream_t);
+// kernels/decode.hip
+int dpfs_decode_nsplit(int);
+void dpfs_attn_decode(const void*, long long, const void*, const void*, const int*, void*, long long, float*, int, int,
+                      int, int, float, hipStream_t);
+void dpfs_kv_append(const void*, const void*, long long, void*, void*, const int*, int, int, int, int, hipStream_t);
+void dpfs_step_advance(int*, int64_t*, int, hipStream_t);
 // comm/xgmi.hip
 const char* dpfs_xgmi_last_error();
 long long dpfs_xgmi_handle_bytes();
@@ -619,6 +625,64 @@ torch::Tensor grad_sumsq(torch::Tensor desc, torch::Tensor chunks) {
   return partial.sum();
 }
 
+// ----------------------------------------------------------------------------- decode --
+void check_cache(const torch::Tensor& c, const char* name) {
+  check_cuda(c, name);
+  TORCH_CHECK(c.dim() == 4 && c.is_contiguous() && c.scalar_type() == torch::kBFloat16, name,
+              " must be a contiguous bf16 (B, T_max, H, hd) cache");
+}
+
+void check_len(const torch::Tensor& len) {
+  check_cuda(len, "len");
+  TORCH_CHECK(len.scalar_type() == torch::kInt32 && len.numel() == 1, "len must be a device int32 scalar");
+}
+
+// o[B, H*hd] = softmax(q k^T * scale) v over keys [0, *len] of the cache (one query per
+// sequence and head).  q: [B, >= H*hd] rows (e.g. the q part of the packed qkv row).
+torch::Tensor attn_decode(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor len, double scale) {
+  check_rowmajor(q, "q");
+  check_cache(kc, "k_cache");
+  check_cache(vc, "v_cache");
+  check_len(len);
+  TORCH_CHECK(kc.sizes() == vc.sizes(), "k / v cache shapes differ");
+  const int64_t B = kc.size(0), Tmax = kc.size(1), H = kc.size(2), hd = kc.size(3);
+  TORCH_CHECK(hd == 64 || hd == 128, "attn_decode: head_dim 64 or 128");
+  TORCH_CHECK(q.size(0) == B && q.size(1) >= H * hd && q.stride(0) % 8 == 0 && q.scalar_type() == torch::kBFloat16,
+              "attn_decode: q rows");
+  const at::DeviceGuard g(q.device());
+  auto o = torch::empty({B, H * hd}, q.options());
+  const int ns = dpfs_decode_nsplit((int)Tmax);
+  auto part = torch::empty({B * H * ns * (hd + 2)}, q.options().dtype(torch::kFloat32));
+  dpfs_attn_decode(q.data_ptr(), q.stride(0), kc.data_ptr(), vc.data_ptr(), len.data_ptr<int>(), o.data_ptr(), H * hd,
+                   part.data_ptr<float>(), (int)B, (int)H, (int)hd, (int)Tmax, (float)scale, stream());
+  return o;
+}
+
+// Write the k / v parts of the packed qkv rows [B, 3*H*hd] into the caches at row *len.
+void kv_append(torch::Tensor qkv, torch::Tensor kc, torch::Tensor vc, torch::Tensor len) {
+  check_rowmajor(qkv, "qkv");
+  check_cache(kc, "k_cache");
+  check_cache(vc, "v_cache");
+  check_len(len);
+  const int64_t B = kc.size(0), Tmax = kc.size(1), H = kc.size(2), hd = kc.size(3);
+  TORCH_CHECK(qkv.size(0) == B && qkv.size(1) == 3 * H * hd && qkv.stride(0) % 8 == 0 &&
+                  qkv.scalar_type() == torch::kBFloat16,
+              "kv_append: qkv must be [B, 3*H*hd] bf16");
+  const at::DeviceGuard g(qkv.device());
+  const char* p = static_cast<const char*>(qkv.data_ptr());
+  dpfs_kv_append(p + H * hd * 2, p + 2 * H * hd * 2, qkv.stride(0), kc.data_ptr(), vc.data_ptr(), len.data_ptr<int>(),
+                 (int)B, (int)H, (int)hd, (int)Tmax, stream());
+}
+
+// *len += 1 and pos[:] = *len on the device (end of a decode step; graph-replayable).
+void step_advance(torch::Tensor len, torch::Tensor pos) {
+  check_len(len);
+  check_cuda(pos, "pos");
+  TORCH_CHECK(pos.scalar_type() == torch::kInt64 && pos.is_contiguous(), "pos must be contiguous int64");
+  const at::DeviceGuard g(len.device());
+  dpfs_step_advance(len.data_ptr<int>(), pos.data_ptr<int64_t>(), (int)pos.numel(), stream());
+}
+
 // ------------------------------------------------------------- xGMI collectives (comm/) --
 void* xgmi_ptr(int64_t h) {
   TORCH_CHECK(h != 0, "xgmi: null communicator");
@@ -716,6 +780,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"), py::arg("step"), py::arg("grad_scale") = 1.0,
         py::arg("dscale") = py::none());
   m.def("grad_sumsq", &grad_sumsq);
+  m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("len"),
+        py::arg("scale"));
+  m.def("kv_append", &kv_append, py::arg("qkv"), py::arg("k_cache"), py::arg("v_cache"), py::arg("len"));
+  m.def("step_advance", &step_advance, py::arg("len"), py::arg("pos"));
   m.def("xgmi_create", &xgmi_create, "allocate IPC buffers: -> (handle, ipc handle bytes)");
   m.def("xgmi_open", &xgmi_open, "map every peer's buffers (rank-ordered concatenated handle bytes)");
   m.def("xgmi_run", &xgmi_run, py::arg("h"), py::arg("op"), py::arg("x"), py::arg("out"), py::arg("world"),

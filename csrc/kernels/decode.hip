@@ -1,0 +1,219 @@
+// Single-token decode attention over a KV cache (gfx950), for KV-cached greedy generation.
+//
+// The reference decodes by re-running the whole prefix for every token (test.py:144-150).
+// generation.py keeps per-layer (B, T_max, H_local, hd) key / value caches instead; every
+// decode step appends one key/value row per sequence and attends one query row per
+// (sequence, head) against all cached keys.  That is a memory-bound GEMV-shaped problem
+// (a few MB of cache per layer, no MFMA-sized tiles), so the kernels here are VALU/LDS
+// split-K ("flash-decoding"):
+//
+//   attn_decode_split_k  grid (T_max/256 splits, B*H): one workgroup scores 256 keys, 4 waves
+//                        x 64 keys, lane-per-key dot products (q held in registers), wave
+//                        softmax, then P.V with lanes = 8 key groups x 8 dim groups (16-byte V
+//                        loads) and an xor-shuffle reduction; the 4 waves merge through LDS
+//                        into one (max, sum, o[hd]) fp32 partial per split.
+//   attn_decode_combine_k one wave per (b, h) merges the partials of the live splits.
+//
+// The current length is read from DEVICE memory (len_ptr), never from a kernel argument, and
+// the grid covers T_max: the whole decode step can be captured once in a HIP graph and
+// replayed for every token (splits past the length exit at once).  kv_append_k writes the
+// new token's (RoPE-rotated) key / value rows at row *len_ptr; step_advance_k bumps the
+// length and the position ids on the device at the end of the step.
+#include "common.h"
+
+namespace dpfs {
+
+constexpr int kSplit = 256;   // keys per workgroup
+
+template <int HD>
+__global__ __launch_bounds__(256) void attn_decode_split_k(const bf16* __restrict__ q, long long ldq,
+                                                          const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+                                                          const int* __restrict__ len_ptr, int H, int Tmax,
+                                                          float scale, float* __restrict__ part) {
+  constexpr int NV = HD / 8;               // 16-byte vectors per row
+  const int split = blockIdx.x, bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int L = min(*len_ptr + 1, Tmax);  // cached keys + the token being decoded
+  const int k0 = split * kSplit;
+  float* out = part + ((long long)bh * gridDim.x + split) * (HD + 2);
+  if (k0 >= L) return;                     // the combine kernel never reads this split
+  const int wave = threadIdx.x >> 6, l = lane_id();
+  __shared__ float p_lds[4][64];
+  __shared__ float o_lds[4][HD];
+  __shared__ float ml_lds[4][2];
+
+  // q in registers (every lane holds the full row for its own key's dot product)
+  float qf[HD];
+  const bf16* qrow = q + (long long)b * ldq + (long long)h * HD;
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    float v[8];
+    load_vec<bf16>(qrow + 8 * c, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[8 * c + j] = v[j] * scale;
+  }
+  // scores: lane-per-key
+  const int key = k0 + wave * 64 + l;
+  float s = -INFINITY;
+  if (key < L) {
+    const bf16* krow = kc + (((long long)b * Tmax + key) * H + h) * HD;
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      float v[8];
+      load_vec<bf16>(krow + 8 * c, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc = fmaf(qf[8 * c + j], v[j], acc);
+    }
+    s = acc;
+  }
+  const float m = wave_max(s);
+  float p = (key < L && m != -INFINITY) ? __expf(s - m) : 0.f;
+  const float lsum = wave_sum(p);
+  p_lds[wave][l] = p;
+  __syncthreads();
+  // P.V: lane = (key group kg = l >> 3, dim group dg = l & 7); each lane walks 8 keys
+  const int kg = l >> 3, dg = l & 7;
+  constexpr int DPL = HD / 8;              // dims per lane (8 at hd 64, 16 at hd 128)
+  float o[DPL];
+#pragma unroll
+  for (int j = 0; j < DPL; ++j) o[j] = 0.f;
+  const int kw0 = k0 + wave * 64;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int kk = kg + 8 * i;             // key within the wave's 64
+    const float pk = p_lds[wave][kk];
+    if (kw0 + kk < L) {
+      const bf16* vrow = vc + (((long long)b * Tmax + kw0 + kk) * H + h) * HD + dg * DPL;
+#pragma unroll
+      for (int c = 0; c < DPL / 8; ++c) {
+        float v[8];
+        load_vec<bf16>(vrow + 8 * c, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[8 * c + j] = fmaf(pk, v[j], o[8 * c + j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < DPL; ++j) {          // sum over the 8 key groups (lanes l ^ 8, 16, 32)
+    float v = o[j];
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    o[j] = v;
+  }
+  if (kg == 0) {
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) o_lds[wave][dg * DPL + j] = o[j];
+  }
+  if (l == 0) {
+    ml_lds[wave][0] = m;
+    ml_lds[wave][1] = lsum;
+  }
+  __syncthreads();
+  // merge the 4 waves (fixed order) into this split's partial
+  if (threadIdx.x < HD) {
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, ml_lds[w][0]);
+    float acc = 0.f, ls = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float mw = ml_lds[w][0];
+      const float f = mw == -INFINITY ? 0.f : __expf(mw - M);
+      acc += f * o_lds[w][threadIdx.x];
+      ls += f * ml_lds[w][1];
+    }
+    out[2 + threadIdx.x] = acc;
+    if (threadIdx.x == 0) {
+      out[0] = M;
+      out[1] = ls;
+    }
+  }
+}
+
+template <int HD>
+__global__ __launch_bounds__(64) void attn_decode_combine_k(const float* __restrict__ part, int nsplit,
+                                                           const int* __restrict__ len_ptr, bf16* __restrict__ o,
+                                                           long long ldo, int H) {
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int L = min(*len_ptr + 1, nsplit * kSplit);
+  const int live = (L + kSplit - 1) / kSplit;
+  const float* p = part + (long long)bh * nsplit * (HD + 2);
+  float M = -INFINITY;
+  for (int s = 0; s < live; ++s) M = fmaxf(M, p[s * (HD + 2)]);
+  constexpr int DPL = HD / 64;
+  float acc[DPL];
+#pragma unroll
+  for (int j = 0; j < DPL; ++j) acc[j] = 0.f;
+  float ls = 0.f;
+  for (int s = 0; s < live; ++s) {
+    const float* ps = p + s * (HD + 2);
+    const float f = __expf(ps[0] - M);
+    ls += f * ps[1];
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) acc[j] += f * ps[2 + threadIdx.x + 64 * j];
+  }
+  const float inv = 1.f / ls;
+  bf16* orow = o + (long long)b * ldo + (long long)h * HD;
+#pragma unroll
+  for (int j = 0; j < DPL; ++j) orow[threadIdx.x + 64 * j] = (bf16)(acc[j] * inv);
+}
+
+// cache[b, *len, h, :] = src rows (k and v parts of the packed qkv row of sequence b)
+__global__ __launch_bounds__(256) void kv_append_k(const bf16* __restrict__ ksrc, const bf16* __restrict__ vsrc,
+                                                  long long ld, bf16* __restrict__ kc, bf16* __restrict__ vc,
+                                                  const int* __restrict__ len_ptr, int B, int H, int HD, int Tmax) {
+  const int t = *len_ptr;
+  if (t < 0 || t >= Tmax) return;          // full cache: nothing to append (never out of bounds)
+  const int nv = H * HD / 8;               // 16-byte vectors per token row
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 2 * B * nv; i += gridDim.x * blockDim.x) {
+    const int isv = i >= B * nv;
+    const int j = isv ? i - B * nv : i;
+    const int b = j / nv, c = j % nv;
+    const bf16* src = (isv ? vsrc : ksrc) + (long long)b * ld + 8 * c;
+    bf16* dst = (isv ? vc : kc) + ((long long)b * Tmax + t) * H * HD + 8 * c;
+    *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(src);
+  }
+}
+
+// *len += 1; pos[b] = *len (the next token's position) for every sequence.
+__global__ void step_advance_k(int* __restrict__ len_ptr, int64_t* __restrict__ pos, int B) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const int t = *len_ptr + 1;
+    *len_ptr = t;
+    for (int b = 0; b < B; ++b) pos[b] = t;
+  }
+}
+
+}  // namespace dpfs
+
+using namespace dpfs;
+
+extern "C" int dpfs_decode_nsplit(int Tmax) { return (Tmax + kSplit - 1) / kSplit; }
+
+extern "C" void dpfs_attn_decode(const void* q, long long ldq, const void* kc, const void* vc, const int* len_ptr,
+                                 void* o, long long ldo, float* part, int B, int H, int HD, int Tmax, float scale,
+                                 hipStream_t s) {
+  const int ns = dpfs_decode_nsplit(Tmax);
+  const dim3 grid(ns, B * H);
+  if (HD == 64) {
+    attn_decode_split_k<64><<<grid, 256, 0, s>>>((const bf16*)q, ldq, (const bf16*)kc, (const bf16*)vc, len_ptr, H,
+                                                  Tmax, scale, part);
+    attn_decode_combine_k<64><<<B * H, 64, 0, s>>>(part, ns, len_ptr, (bf16*)o, ldo, H);
+  } else {
+    attn_decode_split_k<128><<<grid, 256, 0, s>>>((const bf16*)q, ldq, (const bf16*)kc, (const bf16*)vc, len_ptr, H,
+                                                   Tmax, scale, part);
+    attn_decode_combine_k<128><<<B * H, 64, 0, s>>>(part, ns, len_ptr, (bf16*)o, ldo, H);
+  }
+}
+
+extern "C" void dpfs_kv_append(const void* ksrc, const void* vsrc, long long ld, void* kc, void* vc,
+                               const int* len_ptr, int B, int H, int HD, int Tmax, hipStream_t s) {
+  const int n = 2 * B * H * HD / 8;
+  kv_append_k<<<(n + 255) / 256, 256, 0, s>>>((const bf16*)ksrc, (const bf16*)vsrc, ld, (bf16*)kc, (bf16*)vc,
+                                              len_ptr, B, H, HD, Tmax);
+}
+
+extern "C" void dpfs_step_advance(int* len_ptr, int64_t* pos, int B, hipStream_t s) {
+  step_advance_k<<<1, 64, 0, s>>>(len_ptr, pos, B);
+}

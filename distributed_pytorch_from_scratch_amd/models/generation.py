@@ -2,10 +2,19 @@
 
 The reference decodes greedily by re-running the whole prefix every token (``test.py:144-150``:
 O(T²·L) work per token, no cache). This module keeps each layer's post-RoPE keys and values
-for the local head shard. It prefills the prompt with the causal flash-attention kernel, then
-decodes one token per step: one query row against the cached keys. TP works as in training:
-heads are sharded, the row-parallel projections all-reduce, and the vocab-sharded logits are
-all-gathered before the argmax. Every rank therefore picks the same token.
+for the local head shard:
+
+* prefill: the prompt goes through the causal flash-attention kernel and fills cache rows
+  ``[0, T0)``;
+* decode: one token per sequence per step.  The step is written against DEVICE state only —
+  the cache length ``cache.len_t`` (int32) and the position ids ``pos`` live on the GPU, the
+  new key/value rows are appended at ``len_t`` (``kv_append``), the single-query split-K
+  attention kernel (``attn_decode``, csrc/kernels/decode.hip) reads ``len_t`` itself, and
+  ``step_advance`` bumps ``len_t`` / ``pos`` at the end — so at TP = 1 the whole step (about
+  20 kernels per layer) is captured once in a HIP graph and replayed per token, instead of being
+  re-launched from Python.  With TP > 1 the same step runs eagerly (the row-parallel outputs
+  are all-reduced and the vocab-sharded logits all-gathered, so every rank picks the same
+  token).  ``DPFS_DECODE_GRAPH=0`` forces the eager step.
 
 ``generate(model, prompt, ...)`` returns the prompt followed by the generated ids.
 ``logits_step`` exposes the last-position logits (tests compare it against the full recompute).
@@ -13,12 +22,16 @@ all-gathered before the argmax. Every rank therefore picks the same token.
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional
 
 import torch
 
-from ..ops.dispatch import K
+from ..ops import gemm_select as GS
+from ..ops.dispatch import K, shadow
 from ..parallel import comm_ops
+from ..parallel import process_manager as pm
+from ..parallel import tp_comm
 
 
 class KVCache:
@@ -27,11 +40,16 @@ class KVCache:
     def __init__(self, n_layers: int, B: int, t_max: int, h_local: int, hd: int, dtype, device):
         self.k = [torch.empty(B, t_max, h_local, hd, dtype=dtype, device=device) for _ in range(n_layers)]
         self.v = [torch.empty(B, t_max, h_local, hd, dtype=dtype, device=device) for _ in range(n_layers)]
-        self.len = 0
+        self.len = 0                      # host view (prefill / multi-token steps)
+        self.len_t = torch.zeros(1, dtype=torch.int32, device=device)   # device view (decode steps)
         self.t_max = t_max
+
+    def sync_device_len(self):
+        self.len_t.fill_(self.len)
 
 
 def _attention_step(layer, x2d, positions, tab, cache: KVCache, li: int, B: int, T: int):
+    """Multi-token step (prefill, or T > 1 continuation) with host-side cache bookkeeping."""
     attn = layer.attn
     h, hd = attn.num_local_heads, attn.head_dim
     qkv = attn.wqkv(x2d)                                     # (B*T, 3*h*hd)
@@ -48,14 +66,13 @@ def _attention_step(layer, x2d, positions, tab, cache: KVCache, li: int, B: int,
         # prefill: causal flash attention over the prompt
         o, _ = k_.attn_fwd(q, kk, v, scale, True)
     else:
-        # decode: T new queries (T == 1 in greedy decode) against every cached key
+        # T new queries against every cached key (continuation chunk)
         keys = cache.k[li][:, : t0 + T].float()             # (B, S, h, hd)
         vals = cache.v[li][:, : t0 + T].float()
         s = torch.einsum("bthd,bshd->bhts", q.float(), keys) * scale
-        if T > 1:
-            S = t0 + T
-            mask = torch.ones(T, S, dtype=torch.bool, device=s.device).triu(S - T + 1)
-            s = s.masked_fill(mask, float("-inf"))
+        S = t0 + T
+        mask = torch.ones(T, S, dtype=torch.bool, device=s.device).triu(S - T + 1)
+        s = s.masked_fill(mask, float("-inf"))
         p = torch.softmax(s, dim=-1)
         o = torch.einsum("bhts,bshd->bthd", p, vals).to(q.dtype)
     return attn.wo(o.reshape(B * T, h * hd))
@@ -68,6 +85,12 @@ def logits_step(model, ids: torch.Tensor, cache: KVCache) -> torch.Tensor:
     dev = ids.device
     dt = model.act_dtype(dev)
     assert cache.len + T <= cache.t_max <= model.args.maxlen
+    if T == 1 and cache.len > 0:
+        cache.sync_device_len()
+        pos = torch.full((B,), cache.len, dtype=torch.int64, device=dev)
+        _, logits = decode_step(model, ids, pos, cache)
+        cache.len += 1
+        return logits
     model.embedding.out_dtype = dt
     x = model.embedding(ids).reshape(B * T, -1).to(dt)
     positions = torch.arange(cache.len, cache.len + T, device=dev).repeat(B)
@@ -80,6 +103,109 @@ def logits_step(model, ids: torch.Tensor, cache: KVCache) -> torch.Tensor:
     logits = model._lm_head_local(h)
     logits = comm_ops.Gather.apply(logits, model.lm_head.sizes)
     return logits[..., : model.vocab_size].float()
+
+
+def decode_step(model, ids: torch.Tensor, pos: torch.Tensor, cache: KVCache):
+    """One token per sequence (``ids`` (B, 1), ``pos`` (B,) int64 = cache.len_t) against the
+    cache; advances ``cache.len_t`` and ``pos`` on the device.  Returns (next ids (B,),
+    logits (B, vocab) fp32).  Touches no host state: graph-capturable."""
+    from .fused_engine import _Layer
+    if model.args.norm != "rmsnorm":
+        return _decode_step_modules(model, ids, pos, cache)
+    B = ids.size(0)
+    dev = ids.device
+    dt = model.act_dtype(dev)
+    k = K(model.embedding.weight)
+    W = lambda w: shadow(w, dt) if w is not None else None
+    model.embedding.out_dtype = dt
+    x = model.embedding(ids).reshape(B, -1).to(dt)
+    tab = model.rope_table(dev)
+    pend = pend_bias = None
+    # Per layer: [bias + residual +] RMSNorm (one kernel), QKV GEMM, RoPE, append k/v at len,
+    # split-K decode attention, Wo GEMM, bias + residual + RMSNorm, gate|up
+    # GEMM, SwiGLU, down GEMM (its bias + residual fold into the next layer's norm).
+    for li, layer in enumerate(model.layers):
+        L = _Layer(layer)
+        if pend is None:
+            h1, _ = k.rmsnorm_fwd(x, L.s1, L.eps1)
+        else:
+            x, h1, _ = k.add_rmsnorm_fwd(pend, pend_bias, x, L.s1, L.eps1)
+        qkv = GS.gemm_nt(k, h1, W(L.wqkv), L.bqkv)   # few rows: the library GEMV-class kernels win
+        k.rope_(qkv, pos, tab, 2 * L.h, L.hd, False)
+        k.kv_append(qkv, cache.k[li], cache.v[li], cache.len_t)
+        o = k.attn_decode(qkv, cache.k[li], cache.v[li], cache.len_t, 1.0 / math.sqrt(L.hd))
+        pout = GS.gemm_nt(k, o, W(L.wo), None)
+        tp_comm.all_reduce(pout, async_op=False)
+        x, h2, _ = k.add_rmsnorm_fwd(pout, L.bo, x, L.s2, L.eps2)
+        sw = k.swiglu_fwd(GS.gemm_nt(k, h2, W(L.wgu), L.bgu))
+        pend, pend_bias = GS.gemm_nt(k, sw, W(L.wd), None), L.bd
+        tp_comm.all_reduce(pend, async_op=False)
+    _, hfin, _ = k.add_rmsnorm_fwd(pend, pend_bias, x, model.norm.scale, model.norm.eps)
+    logits = GS.gemm_nt(k, hfin, W(model.lm_head.weight), model.lm_head.bias)
+    logits = comm_ops.Gather.apply(logits, model.lm_head.sizes)[..., : model.vocab_size].float()
+    nxt = logits.argmax(-1)
+    K(pos).step_advance(cache.len_t, pos)
+    return nxt, logits
+
+
+def _decode_step_modules(model, ids: torch.Tensor, pos: torch.Tensor, cache: KVCache):
+    """decode_step through the nn.Module layers (any norm type, e.g. the LayerNorm variant)."""
+    B = ids.size(0)
+    dev = ids.device
+    dt = model.act_dtype(dev)
+    model.embedding.out_dtype = dt
+    x = model.embedding(ids).reshape(B, -1).to(dt)
+    tab = model.rope_table(dev)
+    for li, layer in enumerate(model.layers):
+        attn = layer.attn
+        h, hd = attn.num_local_heads, attn.head_dim
+        qkv = attn.wqkv(layer.norm1(x))                      # (B, 3*h*hd)
+        k_ = K(qkv)
+        k_.rope_(qkv, pos, tab, 2 * h, hd, False)
+        k_.kv_append(qkv, cache.k[li], cache.v[li], cache.len_t)
+        x = x + attn.wo(k_.attn_decode(qkv, cache.k[li], cache.v[li], cache.len_t, 1.0 / math.sqrt(hd)))
+        x = x + layer.ffn(layer.norm2(x))
+    logits = model._lm_head_local(model.norm(x))
+    logits = comm_ops.Gather.apply(logits, model.lm_head.sizes)[..., : model.vocab_size].float()
+    nxt = logits.argmax(-1)
+    K(pos).step_advance(cache.len_t, pos)
+    return nxt, logits
+
+
+class DecodeGraph:
+    """One decode step captured as a HIP graph (static ids / pos / output buffers)."""
+
+    def __init__(self, model, cache: KVCache, B: int):
+        dev = cache.len_t.device
+        self.cache = cache
+        self.ids = torch.zeros(B, 1, dtype=torch.int64, device=dev)
+        self.pos = torch.zeros(B, dtype=torch.int64, device=dev)
+        saved = cache.len_t.clone()
+        # Warm-up off the capture (first-call GEMM choices, allocator pools).  It appends a row
+        # at len_t, which the first real step rewrites before anything reads it.
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self.pos.copy_(cache.len_t.long().expand(B))
+            decode_step(model, self.ids, self.pos, cache)
+        torch.cuda.current_stream().wait_stream(s)
+        cache.len_t.copy_(saved)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out, self.logits = decode_step(model, self.ids, self.pos, cache)
+        cache.len_t.copy_(saved)
+
+    def step(self, ids: torch.Tensor) -> torch.Tensor:
+        """Feed ids (B,) at the cache's device length; returns the next ids (B,) (device)."""
+        self.ids.copy_(ids.view(-1, 1))
+        self.graph.replay()
+        return self.out
+
+
+def _use_graph(dev) -> bool:
+    p = pm.pgm
+    return (dev.type == "cuda" and os.environ.get("DPFS_DECODE_GRAPH", "1") != "0"
+            and (p is None or p.tp_size == 1))
 
 
 @torch.inference_mode()
@@ -98,10 +224,12 @@ def generate(model, prompt: torch.Tensor, max_new_tokens: int, eos_id: Optional[
     done = [False] * B
     if max_new_tokens <= 0 or T0 >= t_max:
         return out
-    logits = logits_step(model, prompt, cache)
+    nxt = logits_step(model, prompt, cache).argmax(-1)
+    cache.sync_device_len()
+    pos = torch.full((B,), cache.len, dtype=torch.int64, device=dev)
+    graph = None
     n_gen = 0
     while True:
-        nxt = logits.argmax(-1)
         n_gen += 1
         for b, t in enumerate(nxt.tolist()):
             if not done[b]:
@@ -109,4 +237,11 @@ def generate(model, prompt: torch.Tensor, max_new_tokens: int, eos_id: Optional[
                 done[b] = eos_id is not None and int(t) == eos_id
         if all(done) or n_gen >= max_new_tokens or cache.len >= t_max:
             return out
-        logits = logits_step(model, nxt.view(B, 1), cache)
+        if graph is None and _use_graph(dev):
+            graph = DecodeGraph(model, cache, B)
+        if graph is not None:
+            graph.pos.fill_(cache.len)
+            nxt = graph.step(nxt)
+        else:
+            nxt, _ = decode_step(model, nxt.view(B, 1), pos, cache)
+        cache.len += 1

@@ -55,6 +55,12 @@ def _pick(key: Tuple, ours: Callable, blas: Callable) -> str:
     return c
 
 
+# Below this many rows (decode steps, tiny batches) our 256-row tiles are mostly padding and
+# the library's GEMV-class kernels win; timing cannot tell them apart there (a launch-bound
+# loop measures the host launch cost, which favours the thinner pybind path).
+_MIN_ROWS = 256
+
+
 def _aligned(*dims: int) -> bool:
     """Our MFMA kernels stage 16-byte rows: every K / N (and TN's M) must be a multiple of 8.
     Uneven vocab shards (e.g. 1000 over 2 ranks at vocab_pad_to=1) go to hipBLASLt."""
@@ -70,7 +76,7 @@ def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None) -> torch.Tensor:
 
     def blas():
         return F.linear(x, w, bb)
-    if not _aligned(x.shape[1], w.shape[0]):
+    if not _aligned(x.shape[1], w.shape[0]) or x.shape[0] < _MIN_ROWS:
         return blas()
 
     def ours():
@@ -89,7 +95,7 @@ def gemm_nn(k, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 
     def blas():
         return torch.matmul(a, b)
-    if not _aligned(a.shape[1], b.shape[1]):
+    if not _aligned(a.shape[1], b.shape[1]) or a.shape[0] < _MIN_ROWS:
         return blas()
 
     def ours():

@@ -188,6 +188,32 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float,
     return o.to(q.dtype), lse
 
 
+def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, len: torch.Tensor,
+                scale: float) -> torch.Tensor:
+    """One query row per (sequence, head) against cache rows [0, len]: q [B, >= H*hd] rows,
+    caches (B, T_max, H, hd), len a 1-element int tensor.  Returns o [B, H*hd] in q.dtype."""
+    B, _, H, hd = k_cache.shape
+    L = int(len.reshape(-1)[0]) + 1
+    qf = q[:, : H * hd].float().view(B, H, 1, hd)
+    kf = k_cache[:, :L].float().transpose(1, 2)          # B H L hd
+    vf = v_cache[:, :L].float().transpose(1, 2)
+    p = torch.softmax((qf @ kf.transpose(-1, -2)) * scale, dim=-1)
+    return (p @ vf).reshape(B, H * hd).to(q.dtype)
+
+
+def kv_append(qkv: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, len: torch.Tensor) -> None:
+    """cache[:, len] = the k / v parts of the packed qkv rows [B, 3*H*hd]."""
+    B, _, H, hd = k_cache.shape
+    t = int(len.reshape(-1)[0])
+    k_cache[:, t] = qkv[:, H * hd: 2 * H * hd].view(B, H, hd).to(k_cache.dtype)
+    v_cache[:, t] = qkv[:, 2 * H * hd: 3 * H * hd].view(B, H, hd).to(v_cache.dtype)
+
+
+def step_advance(len: torch.Tensor, pos: torch.Tensor) -> None:
+    len += 1
+    pos.fill_(int(len.reshape(-1)[0]))
+
+
 def _rot_bthd(x: torch.Tensor, positions: torch.Tensor, table: torch.Tensor, inverse: bool) -> torch.Tensor:
     """Rotate-half RoPE of an fp32 (B, T, H, hd) tensor; ``positions`` is flat [B*T]."""
     B, T, H, hd = x.shape

@@ -317,6 +317,29 @@ def test_swiglu_bwd_fused_bias_grad(C, M, F):
     assert torch.equal(dgu, C.swiglu_bwd(dh, gu))
 
 
+@pytest.mark.parametrize("hd", [64, 128])
+@pytest.mark.parametrize("L", [0, 255, 256, 699])
+def test_decode_attention_and_kv_append(C, hd, L):
+    """Split-K single-query attention over a KV cache (csrc/kernels/decode.hip) against the
+    fp32 oracle, across split boundaries; kv_append writes row *len; step_advance."""
+    torch.manual_seed(21)
+    B, H, Tmax = 3, 5, 700
+    kc = torch.randn(B, Tmax, H, hd, device=DEV).bfloat16()
+    vc = torch.randn(B, Tmax, H, hd, device=DEV).bfloat16()
+    qkv = torch.randn(B, 3 * H * hd, device=DEV).bfloat16()
+    ln = torch.tensor([L], dtype=torch.int32, device=DEV)
+    kr, vr = kc.clone(), vc.clone()
+    C.kv_append(qkv, kc, vc, ln)
+    R.kv_append(qkv, kr, vr, ln)
+    assert torch.equal(kc, kr) and torch.equal(vc, vr)
+    o = C.attn_decode(qkv, kc, vc, ln, 1 / math.sqrt(hd))
+    ref = R.attn_decode(qkv.float(), kc.float(), vc.float(), ln.cpu(), 1 / math.sqrt(hd))
+    assert _rel(o, ref) < 1e-2
+    pos = torch.zeros(B, dtype=torch.int64, device=DEV)
+    C.step_advance(ln, pos)
+    assert ln.item() == L + 1 and pos.tolist() == [L + 1] * B
+
+
 @pytest.mark.parametrize("M,V,valid,start", [(2048, 6288, 6241, 6288 * 7), (100, 50304, 50257, 0),
                                              (300, 500, 500, 500), (65, 37, 30, 0)])   # unaligned rows
 def test_ce_bwd_fused_bias_grad(C, M, V, valid, start):

@@ -175,6 +175,24 @@ def test_kv_cache_generation_on_gpu(dist1):
     assert len(out) == 2 and all(len(o) == 120 for o in out)
 
 
+def test_decode_graph_matches_eager_decode(dist1, monkeypatch):
+    """The HIP-graph-replayed decode step produces exactly the eager step's tokens (same
+    kernels, device-side length / positions), across a split boundary of the decode kernel."""
+    from distributed_pytorch_from_scratch_amd.models import get_preset, Transformer
+    from distributed_pytorch_from_scratch_amd.models.generation import generate
+    args = get_preset("gpt2-small", num_layers=2)
+    m = Transformer.from_args(args).cuda()
+    m.reset_parameters()
+    m.eval()
+    prompt = torch.randint(0, args.vocab_size, (3, 240), device="cuda")
+    monkeypatch.setenv("DPFS_DECODE_GRAPH", "0")
+    eager = generate(m, prompt, max_new_tokens=40)
+    monkeypatch.setenv("DPFS_DECODE_GRAPH", "1")
+    graph = generate(m, prompt, max_new_tokens=40)
+    assert eager == graph
+    assert all(len(o) == 280 for o in graph)
+
+
 def test_kernel_debug_modes_run_clean_and_catch_nan(dist1, monkeypatch):
     """DPFS_SYNC_DEBUG / DPFS_NAN_CHECK: a clean step raises nothing; a NaN weight is
     reported against the first kernel op that produces non-finite values."""
