@@ -75,13 +75,14 @@ void dpfs_step_advance(int*, int64_t*, int, hipStream_t);
 // comm/xgmi.hip
 const char* dpfs_xgmi_last_error();
 long long dpfs_xgmi_handle_bytes();
-void* dpfs_xgmi_create(int, int, long long, void*);
+void* dpfs_xgmi_create(int, int, long long, int, void*);
+void* dpfs_xgmi_slot(void*, int);
 int dpfs_xgmi_open(void*, const void*);
 void dpfs_xgmi_set_blocks(void*, int);
 long long dpfs_xgmi_capacity(void*);
 int dpfs_xgmi_error(void*);
 void dpfs_xgmi_clear_error(void*);
-int dpfs_xgmi_run(void*, int, int, const void*, void*, long long, long long, double, hipStream_t);
+int dpfs_xgmi_run(void*, int, int, const void*, void*, long long, long long, double, int, hipStream_t);
 void dpfs_xgmi_destroy(void*);
 }
 
@@ -118,9 +119,20 @@ const float* opt_f32(const c10::optional<torch::Tensor>& t, int64_t n, const cha
 torch::Tensor rope_(torch::Tensor qkv, torch::Tensor positions, torch::Tensor table, int64_t n_rot_heads,
                     int64_t head_dim, bool inverse);
 
+// Output buffer: `out` when given (contiguous [M, N] of a's dtype, e.g. a staging slot of the
+// xGMI collectives), else a fresh tensor.
+torch::Tensor gemm_out(const c10::optional<torch::Tensor>& out, const torch::Tensor& a, int64_t M, int64_t N) {
+  if (!out.has_value() || !out->defined()) return torch::empty({M, N}, a.options());
+  check_cuda(*out, "out");
+  TORCH_CHECK(out->is_contiguous() && out->dim() == 2 && out->size(0) == M && out->size(1) == N &&
+                  out->scalar_type() == a.scalar_type(),
+              "gemm: out must be a contiguous [M, N] tensor of the operand dtype");
+  return *out;
+}
+
 torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> bias,
                       c10::optional<torch::Tensor> rope_pos, c10::optional<torch::Tensor> rope_tab,
-                      int64_t rope_heads, int64_t rope_hd) {
+                      int64_t rope_heads, int64_t rope_hd, c10::optional<torch::Tensor> out) {
   check_rowmajor(a, "a");
   check_rowmajor(b, "b");
   TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "gemm_nt: bf16 operands");
@@ -129,10 +141,9 @@ torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
   TORCH_CHECK(K % 8 == 0, "gemm_nt: K must be a multiple of 8, got ", K);
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm_nt: row strides must be multiples of 8");
   const at::DeviceGuard g(a.device());
-  auto c = torch::empty({M, N}, a.options());
+  auto c = gemm_out(out, a, M, N);
   if (M == 0 || N == 0) return c;
   if (K == 0) return c.zero_();
-  TORCH_CHECK(N % 2 == 0 || true, "");
   TORCH_CHECK(N % 4 == 0, "gemm_nt: N must be a multiple of 4, got ", N);
   const long long wsn = dpfs_gemm_bf16_ws((int)M, (int)N, (int)K);
   torch::Tensor ws;
@@ -157,7 +168,7 @@ torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
   return c;
 }
 
-torch::Tensor gemm_nn(torch::Tensor a, torch::Tensor b) {
+torch::Tensor gemm_nn(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> out) {
   check_rowmajor(a, "a");
   check_rowmajor(b, "b");
   TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "gemm_nn: bf16 operands");
@@ -166,7 +177,7 @@ torch::Tensor gemm_nn(torch::Tensor a, torch::Tensor b) {
   TORCH_CHECK(K % 8 == 0 && N % 8 == 0, "gemm_nn: K and N must be multiples of 8, got ", K, " ", N);
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm_nn: row strides must be multiples of 8");
   const at::DeviceGuard g(a.device());
-  auto c = torch::empty({M, N}, a.options());
+  auto c = gemm_out(out, a, M, N);
   if (M == 0 || N == 0) return c;
   if (K == 0) return c.zero_();
   const long long wsn = dpfs_gemm_bf16_ws((int)M, (int)N, (int)K);
@@ -689,9 +700,9 @@ void* xgmi_ptr(int64_t h) {
   return reinterpret_cast<void*>(h);
 }
 
-py::tuple xgmi_create(int64_t rank, int64_t world, int64_t cap_bytes) {
+py::tuple xgmi_create(int64_t rank, int64_t world, int64_t cap_bytes, int64_t nslots) {
   std::string hb((size_t)dpfs_xgmi_handle_bytes(), '\0');
-  void* h = dpfs_xgmi_create((int)rank, (int)world, cap_bytes, &hb[0]);
+  void* h = dpfs_xgmi_create((int)rank, (int)world, cap_bytes, (int)nslots, &hb[0]);
   TORCH_CHECK(h != nullptr, "xgmi_create failed: ", dpfs_xgmi_last_error());
   return py::make_tuple(reinterpret_cast<int64_t>(h), py::bytes(hb));
 }
@@ -704,7 +715,16 @@ void xgmi_open(int64_t h, py::bytes all_handles) {
 
 // op 0 all-reduce (out may be x), 1 reduce-scatter (out = x.numel()/W elements),
 // 2 all-gather (out = W * x.numel() elements); launched on the current stream.
-void xgmi_run(int64_t h, int64_t op, torch::Tensor x, torch::Tensor out, int64_t world, double timeout_s) {
+// A staging slot as a non-owning uint8 tensor of `cap` bytes on `device` (the communicator
+// owns the memory; the Python side keeps the communicator alive as long as the views).
+torch::Tensor xgmi_slot_tensor(int64_t h, int64_t slot, int64_t cap, torch::Device device) {
+  void* p = dpfs_xgmi_slot(xgmi_ptr(h), (int)slot);
+  TORCH_CHECK(p != nullptr, "xgmi: no staging slot ", slot);
+  return torch::from_blob(p, {cap}, torch::TensorOptions().dtype(torch::kUInt8).device(device));
+}
+
+void xgmi_run(int64_t h, int64_t op, torch::Tensor x, torch::Tensor out, int64_t world, double timeout_s,
+              int64_t slot) {
   TORCH_CHECK(op >= 0 && op <= 2, "xgmi_run: op");
   check_cuda(x, "x");
   check_cuda(out, "out");
@@ -733,7 +753,7 @@ void xgmi_run(int64_t h, int64_t op, torch::Tensor x, torch::Tensor out, int64_t
   }
   const at::DeviceGuard g(x.device());
   TORCH_CHECK(dpfs_xgmi_run(xgmi_ptr(h), (int)op, dt, x.data_ptr(), out.data_ptr(), total, part, timeout_s,
-                            stream()) == 0,
+                            (int)slot, stream()) == 0,
               "xgmi_run failed: ", dpfs_xgmi_last_error());
 }
 
@@ -743,8 +763,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels of distributed_pytorch_from_scratch_amd";
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("bias") = py::none(),
         py::arg("rope_pos") = py::none(), py::arg("rope_tab") = py::none(), py::arg("rope_heads") = 0,
-        py::arg("rope_hd") = 0);
-  m.def("gemm_nn", &gemm_nn);
+        py::arg("rope_hd") = 0, py::arg("out") = py::none());
+  m.def("gemm_nn", &gemm_nn, py::arg("a"), py::arg("b"), py::arg("out") = py::none());
   m.def("gemm_force", [](int cfg, int splits) { dpfs_gemm_force(cfg, splits); },
         "force the v2 tile config (-1 auto, 0 = 256x256, 1 = 256x128) and K-splits (0 auto)");
   m.def("gemm_v2_sched", [](int v) { dpfs_gemm_v2_sched(v); }, "v2 256x256 schedule (-1 per-layout default, 0..4 see gemm2_k SCHED)");
@@ -787,7 +807,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xgmi_create", &xgmi_create, "allocate IPC buffers: -> (handle, ipc handle bytes)");
   m.def("xgmi_open", &xgmi_open, "map every peer's buffers (rank-ordered concatenated handle bytes)");
   m.def("xgmi_run", &xgmi_run, py::arg("h"), py::arg("op"), py::arg("x"), py::arg("out"), py::arg("world"),
-        py::arg("timeout_s") = 120.0);
+        py::arg("timeout_s") = 120.0, py::arg("slot") = -1);
+  m.def("xgmi_slot_tensor", &xgmi_slot_tensor, py::arg("h"), py::arg("slot"), py::arg("cap"), py::arg("device"));
   m.def("xgmi_set_blocks", [](int64_t h, int b) { dpfs_xgmi_set_blocks(xgmi_ptr(h), b); });
   m.def("xgmi_capacity", [](int64_t h) { return dpfs_xgmi_capacity(xgmi_ptr(h)); });
   m.def("xgmi_error", [](int64_t h) { return dpfs_xgmi_error(xgmi_ptr(h)); });

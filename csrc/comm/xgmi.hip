@@ -158,8 +158,18 @@ __global__ __launch_bounds__(kThreads) void xgmi_coll_k(Peers P, int op, int ran
     rtmp[s] = rsrc(P.data[s < W ? s : 0] + tmp_off, cap);
   }
 
-  // ---- phase 0: copy-in of what the peers will read
-  if (op == 2) {
+  // ---- phase 0: copy-in of what the peers will read.  Staged (op & 8): the producer GEMM
+  // wrote x straight into this rank's slot (x == slot base), so nothing is copied; its plain
+  // stores may still sit dirty in the XCD L2s, hence a system-scope release (L2 write-back)
+  // by one lane of every workgroup before the start barrier (grids >= 8 reach every XCD).
+  const bool staged = (op & 8) != 0;
+  op &= 7;
+  if (staged) {
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  } else if (op == 2) {
     for (long long v = v0 + threadIdx.x; v < v1; v += kThreads) st_sys(r_in, (unsigned)(v * 16), xv[v]);
   } else {
     for (long long v = v0 + threadIdx.x; v < v1; v += kThreads) {
@@ -242,8 +252,9 @@ __global__ __launch_bounds__(kThreads) void xgmi_coll_k(Peers P, int op, int ran
 
 struct Comm {
   int rank = 0, world = 1;
-  long long cap = 0;          // bytes of each of in / tmp
-  char* data = nullptr;       // own [in | tmp]
+  long long cap = 0;          // bytes of each region
+  int nslots = 0;             // staging slots (producer GEMMs write here: no copy-in)
+  char* data = nullptr;       // own [slot 0 .. slot S-1 | stage | tmp], cap bytes each
   uint32_t* sig = nullptr;    // own signals (uncached)
   Peers peers{};
   bool opened[kMaxRanks] = {};
@@ -269,8 +280,11 @@ extern "C" const char* dpfs_xgmi_last_error() { return g_msg; }
 
 extern "C" long long dpfs_xgmi_handle_bytes() { return 2 * (long long)sizeof(hipIpcMemHandle_t); }
 
+static long long stage_off(const Comm* c) { return (long long)c->nslots * c->cap; }
+static long long tmp_off(const Comm* c) { return (long long)(c->nslots + 1) * c->cap; }
+
 // Allocate this rank's buffers; writes [data handle | signal handle] to handles_out.
-extern "C" void* dpfs_xgmi_create(int rank, int world, long long cap_bytes, void* handles_out) {
+extern "C" void* dpfs_xgmi_create(int rank, int world, long long cap_bytes, int nslots, void* handles_out) {
   if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world) {
     snprintf(g_msg, sizeof(g_msg), "xgmi: world %d / rank %d out of range (max %d ranks)", world, rank, kMaxRanks);
     return nullptr;
@@ -279,11 +293,16 @@ extern "C" void* dpfs_xgmi_create(int rank, int world, long long cap_bytes, void
     snprintf(g_msg, sizeof(g_msg), "xgmi: capacity %lld must be a positive multiple of 4096 below 2 GiB", cap_bytes);
     return nullptr;
   }
+  if (nslots < 0 || nslots > 16) {
+    snprintf(g_msg, sizeof(g_msg), "xgmi: %d staging slots (0..16)", nslots);
+    return nullptr;
+  }
   Comm* c = new Comm();
   c->rank = rank;
   c->world = world;
   c->cap = cap_bytes;
-  if (!ok(hipMalloc((void**)&c->data, 2 * cap_bytes), "hipMalloc(data)")) {
+  c->nslots = nslots;
+  if (!ok(hipMalloc((void**)&c->data, (nslots + 2) * cap_bytes), "hipMalloc(data)")) {
     delete c;
     return nullptr;
   }
@@ -351,6 +370,12 @@ extern "C" void dpfs_xgmi_set_blocks(void* h, int blocks) {
 
 extern "C" long long dpfs_xgmi_capacity(void* h) { return ((Comm*)h)->cap; }
 
+// Device address of staging slot `slot` (cap bytes), or null.
+extern "C" void* dpfs_xgmi_slot(void* h, int slot) {
+  Comm* c = (Comm*)h;
+  return (slot >= 0 && slot < c->nslots) ? c->data + (long long)slot * c->cap : nullptr;
+}
+
 // Host-visible error word (1 = a barrier timed out).  Reading it does not synchronise.
 extern "C" int dpfs_xgmi_error(void* h) { return __atomic_load_n(((Comm*)h)->err_host, __ATOMIC_RELAXED); }
 
@@ -360,8 +385,17 @@ extern "C" void dpfs_xgmi_clear_error(void* h) { __atomic_store_n(((Comm*)h)->er
 // the caller guarantees n*elt <= cap (op 0/1) / W*part*elt <= ... (op 2: part*elt <= cap) and
 // 16-byte alignment of x and out.
 extern "C" int dpfs_xgmi_run(void* h, int op, int dtype, const void* x, void* out, long long n, long long part,
-                             double timeout_s, hipStream_t stream) {
+                             double timeout_s, int slot, hipStream_t stream) {
   Comm* c = (Comm*)h;
+  long long in_off = stage_off(c);
+  if (slot >= 0) {   // staged input: x must be the slot itself (reduce-scatter / all-reduce)
+    if (slot >= c->nslots || x != c->data + (long long)slot * c->cap || op == 2) {
+      snprintf(g_msg, sizeof(g_msg), "xgmi_run: staged input must start at slot %d (all-reduce / reduce-scatter)",
+               slot);
+      return -1;
+    }
+    in_off = (long long)slot * c->cap;
+  }
   const int elt = dtype == 1 ? 2 : 4;
   const int N = 16 / elt;
   if (part % N || (op == 2 ? part * elt > c->cap : ((n + N - 1) / N) * N * elt > c->cap) || n <= 0) {
@@ -375,12 +409,15 @@ extern "C" int dpfs_xgmi_run(void* h, int op, int dtype, const void* x, void* ou
   c->epoch += 1;
   if (c->epoch == 0) c->epoch = 1;
   const unsigned long long ticks = (unsigned long long)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
+  const int kop = op | (slot >= 0 ? 8 : 0);
   if (dtype == 1)
-    hipLaunchKernelGGL(xgmi_coll_k<__bf16>, dim3(grid), dim3(kThreads), 0, stream, c->peers, op, c->rank, c->world,
-                       (const __bf16*)x, (__bf16*)out, n, part, 0LL, c->cap, c->cap, c->epoch, ticks, c->err_dev);
+    hipLaunchKernelGGL(xgmi_coll_k<__bf16>, dim3(grid), dim3(kThreads), 0, stream, c->peers, kop, c->rank, c->world,
+                       (const __bf16*)x, (__bf16*)out, n, part, in_off, tmp_off(c), c->cap, c->epoch, ticks,
+                       c->err_dev);
   else
-    hipLaunchKernelGGL(xgmi_coll_k<float>, dim3(grid), dim3(kThreads), 0, stream, c->peers, op, c->rank, c->world,
-                       (const float*)x, (float*)out, n, part, 0LL, c->cap, c->cap, c->epoch, ticks, c->err_dev);
+    hipLaunchKernelGGL(xgmi_coll_k<float>, dim3(grid), dim3(kThreads), 0, stream, c->peers, kop, c->rank, c->world,
+                       (const float*)x, (float*)out, n, part, in_off, tmp_off(c), c->cap, c->epoch, ticks,
+                       c->err_dev);
   return ok(hipGetLastError(), "xgmi_coll_k launch") ? 0 : -1;
 }
 

@@ -54,6 +54,13 @@ def _ar(t: torch.Tensor):
     return tp_comm.all_reduce(t, async_op=True)
 
 
+def _slot(ci: int, rows: int, cols: int, dt):
+    """Staging buffer (xGMI communicator slot of chunk ``ci``) for a GEMM output that is
+    all-reduced in place next (no copy-in); None -> the GEMM allocates.  The reduced tensor
+    stays in the slot until the chunk's next staged GEMM, which comes after its consumers."""
+    return tp_comm.staging(ci, (rows, cols), dt)
+
+
 def _wait(h):
     if h is not None:
         h.wait()
@@ -122,7 +129,7 @@ class DecoderTrainFn(torch.autograd.Function):
                            pend_bias=None, layers=[]))
         for li, L in enumerate(layers):
             # seg1: (wait + residual), norm1, QKV, RoPE, attention, Wo -> async all-reduce
-            for s in st:
+            for ci, s in enumerate(st):
                 _wait(s["h"])
                 if s["pend"] is not None:   # residual epilogue of the previous layer fused into norm1
                     s["x"], h1, r1 = k.add_rmsnorm_fwd(s["pend"], s["pend_bias"], s["x"], L.s1, L.eps1)
@@ -135,16 +142,16 @@ class DecoderTrainFn(torch.autograd.Function):
                 q, kk, v = _split(qkv, Bc, T, L.h, L.hd)
                 o, lse = k.attn_fwd(q, kk, v, 1.0 / math.sqrt(L.hd), True)
                 o2 = o.view(Mc, L.h * L.hd)
-                pout = GS.gemm_nt(k, o2, W(L.wo), None)
+                pout = GS.gemm_nt(k, o2, W(L.wo), None, out=_slot(ci, Mc, d, dt))
                 s["layers"].append(dict(x=x, r1=r1, h1=h1, qkv=qkv, o=o, lse=lse))
                 s["pend"], s["pend_bias"], s["h"] = pout, L.bo, _ar(pout)
             # seg2: wait + bias + residual, norm2, gate|up, SwiGLU, down -> async all-reduce
-            for s in st:
+            for ci, s in enumerate(st):
                 _wait(s["h"])
                 x2, h2, r2 = k.add_rmsnorm_fwd(s["pend"], s["pend_bias"], s["x"], L.s2, L.eps2)
                 gu = GS.gemm_nt(k, h2, W(L.wgu), L.bgu)
                 sw = k.swiglu_fwd(gu)
-                qout = GS.gemm_nt(k, sw, W(L.wd), None)
+                qout = GS.gemm_nt(k, sw, W(L.wd), None, out=_slot(ci, sw.size(0), d, dt))
                 s["layers"][-1].update(x2=x2, r2=r2, h2=h2, gu=gu, sw=sw)
                 s["x"] = x2
                 s["pend"], s["pend_bias"], s["h"] = qout, L.bd, _ar(qout)
@@ -222,12 +229,12 @@ class DecoderTrainFn(torch.autograd.Function):
             dp_pending.append((dist.all_reduce(flat, group=pg.dp_group, async_op=True), flat, d, keys))
 
         # ---- head: CE backward in place over the logits, lm_head dgrad -> async AR
-        for s in st:
+        for ci, s in enumerate(st):
             gs = s["valid"].float() * gscale_all
             dl = s["logits"]
             db = dl.new_empty(dl.size(1), dtype=torch.float32) if head.bias is not None else None
             k.ce_bwd(dl, s["tgt"], s["ce_lse"], gs, vst, vvalid, dl, db)    # + lm_head bias grad
-            dh = GS.gemm_nn(k, dl, W(head.weight))
+            dh = GS.gemm_nn(k, dl, W(head.weight), out=_slot(ci, dl.size(0), d, dt))
             s["bh"] = _ar(dh)
             s["dpend"] = dh
             tn(g, "lm_w", dl, s["hf"])
@@ -251,7 +258,7 @@ class DecoderTrainFn(torch.autograd.Function):
         for li in range(nL - 1, -1, -1):
             L, G = layers[li], gl[li]
             # b2: down / SwiGLU / gate|up grads -> AR(dh2)
-            for s in st:
+            for ci, s in enumerate(st):
                 if s["dpend"] is not None:     # finish the upper layer: wait, norm1 bwd, residual
                     _finish_norm1(k, s, layers[li + 1], gl[li + 1], li + 1, (G, L.bd))
                 a = s["layers"][li]
@@ -262,7 +269,7 @@ class DecoderTrainFn(torch.autograd.Function):
                 tn(G, "wd", gq, a["sw"])
                 dbgu = ds.new_empty(a["gu"].size(1), dtype=torch.float32) if L.bgu is not None else None
                 dgu = k.swiglu_bwd(ds, a["gu"], dbgu)     # + gate|up bias grad in the same pass
-                dh2 = GS.gemm_nn(k, dgu, W(L.wgu))
+                dh2 = GS.gemm_nn(k, dgu, W(L.wgu), out=_slot(ci, dgu.size(0), d, dt))
                 s["bh"], s["dpend"] = _ar(dh2), dh2
                 tn(G, "wgu", dgu, a["h2"])
                 if dbgu is not None:
@@ -271,7 +278,7 @@ class DecoderTrainFn(torch.autograd.Function):
             if li + 1 < nL:
                 dp_reduce(gl[li + 1])           # layer li+1 is complete (its norm1 grad just landed)
             # b1: wait, norm2 bwd, Wo / attention / QKV grads -> AR(dh)
-            for s in st:
+            for ci, s in enumerate(st):
                 a = s["layers"][li]
                 _wait(s["bh"])
                 dbo = None
@@ -289,7 +296,7 @@ class DecoderTrainFn(torch.autograd.Function):
                 dq, dk, dv = _split(dqkv, Bc, T, L.h, L.hd)
                 k.attn_bwd(do.view(Bc, T, L.h, L.hd), q, kk, v, a["o"], a["lse"], 1.0 / math.sqrt(L.hd), True,
                            dq, dk, dv, s["pos"], tab)   # inverse RoPE fused into the dq/dk stores
-                dh = GS.gemm_nn(k, dqkv, W(L.wqkv))
+                dh = GS.gemm_nn(k, dqkv, W(L.wqkv), out=_slot(ci, dqkv.size(0), d, dt))
                 s["bh"], s["dpend"] = _ar(dh), dh
                 tn(G, "wqkv", dqkv, a["h1"])
                 bias_acc(G, "bqkv", dqkv, L.bqkv)

@@ -46,6 +46,12 @@ def _rs(full: torch.Tensor, n: int):
     return out, tp_comm.reduce_scatter(out, full, async_op=True)
 
 
+def _slot(ci: int, rows: int, cols: int, dt):
+    """Staging buffer (xGMI communicator slot of chunk ``ci``) for a GEMM output that feeds a
+    reduce-scatter, so the collective reads it in place; None -> the GEMM allocates."""
+    return tp_comm.staging(ci, (rows, cols), dt)
+
+
 def _ag(part: torch.Tensor, n: int):
     """All-gather rows of ``part`` -> (full rows, work)."""
     out = part.new_empty((part.size(0) * n,) + tuple(part.shape[1:]))
@@ -66,6 +72,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
         layers = [_Layer(l) for l in model.layers]
         tab = model.rope_table(dev)
         emb, head = model.embedding, model.lm_head
+        d = model.args.attn_dim
         vst = head.odim_start
         vvalid = max(0, min(model.vocab_size - vst, head.odim_partition))
         W = lambda w: shadow(w, dt) if w is not None else None
@@ -87,13 +94,14 @@ class DecoderTrainFnSP(torch.autograd.Function):
                     h1s, r1 = k.rmsnorm_fwd(s["x"], L.s1, L.eps1)
                 h1, s["h"] = _ag(h1s, n)
                 s["layers"].append(dict(x=s["x"], r1=r1, h1=h1))
-            for s in st:    # P2: QKV (+RoPE), attention, Wo -> reduce-scatter
+            for ci, s in enumerate(st):    # P2: QKV (+RoPE), attention, Wo -> reduce-scatter
                 _wait(s["h"])
                 a = s["layers"][-1]
                 qkv = k.gemm_nt(a["h1"], W(L.wqkv), L.bqkv, s["pos"], tab, 2 * L.h, L.hd)
                 q, kk, v = _split(qkv, s["B"], T, L.h, L.hd)
                 o, lse = k.attn_fwd(q, kk, v, 1.0 / math.sqrt(L.hd), True)
-                pout = GS.gemm_nt(k, o.view(qkv.size(0), L.h * L.hd), W(L.wo), None)
+                pout = GS.gemm_nt(k, o.view(qkv.size(0), L.h * L.hd), W(L.wo), None,
+                                  out=_slot(ci, qkv.size(0), d, dt))
                 a.update(qkv=qkv, o=o, lse=lse)
                 (s["pend"], s["h"]), s["pend_bias"] = _rs(pout, n), L.bo
             for s in st:    # P3: bias + residual + norm2 on my rows -> all-gather
@@ -103,12 +111,12 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 h2, s["h"] = _ag(h2s, n)
                 a.update(x2=x2, r2=r2, h2=h2)
                 s["x"] = x2
-            for s in st:    # P4: gate|up, SwiGLU, down -> reduce-scatter
+            for ci, s in enumerate(st):    # P4: gate|up, SwiGLU, down -> reduce-scatter
                 _wait(s["h"])
                 a = s["layers"][-1]
                 gu = GS.gemm_nt(k, a["h2"], W(L.wgu), L.bgu)
                 sw = k.swiglu_fwd(gu)
-                qout = GS.gemm_nt(k, sw, W(L.wd), None)
+                qout = GS.gemm_nt(k, sw, W(L.wd), None, out=_slot(ci, sw.size(0), d, dt))
                 a.update(gu=gu, sw=sw)
                 (s["pend"], s["h"]), s["pend_bias"] = _rs(qout, n), L.bd
         for s in st:        # final norm on my rows -> all-gather
@@ -169,12 +177,13 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 flat = torch.cat([d[key].reshape(-1) for key in keys])
                 dp_pending.append((dist.all_reduce(flat, group=pg.dp_group, async_op=True), flat, d, keys))
 
-        for s in st:    # CE backward in place, lm_head dgrad -> reduce-scatter, lm_head wgrad
+        d = model.args.attn_dim
+        for ci, s in enumerate(st):    # CE backward in place, lm_head dgrad -> reduce-scatter, lm_head wgrad
             gs = s["valid"].float() * gscale_all
             dl = s["logits"]
             db = dl.new_empty(dl.size(1), dtype=torch.float32) if head.bias is not None else None
             k.ce_bwd(dl, s["tgt"], s["ce_lse"], gs, vst, vvalid, dl, db)
-            s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dl, W(head.weight)), n)
+            s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dl, W(head.weight), out=_slot(ci, dl.size(0), d, dt)), n)
             tn(g, "lm_w", dl, s["hf"])
             if db is not None:
                 g["lm_b"] = _addg(g["lm_b"], db)
@@ -188,7 +197,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
         dp_reduce(g, ("lm_w", "lm_b"))
         for li in range(nL - 1, -1, -1):
             L, G = layers[li], gl[li]
-            for s in st:    # B4: down / SwiGLU / gate|up grads -> reduce-scatter
+            for ci, s in enumerate(st):    # B4: down / SwiGLU / gate|up grads -> reduce-scatter
                 _wait(s["h"])
                 a, gq = s["layers"][li], s["gfull"]
                 if L.bd is not None:   # partial over my rows (summed over TP by TrainStep)
@@ -197,7 +206,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 tn(G, "wd", gq, a["sw"])
                 dbgu = ds.new_empty(a["gu"].size(1), dtype=torch.float32) if L.bgu is not None else None
                 dgu = k.swiglu_bwd(ds, a["gu"], dbgu)
-                s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dgu, W(L.wgu)), n)
+                s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dgu, W(L.wgu), out=_slot(ci, dgu.size(0), d, dt)), n)
                 tn(G, "wgu", dgu, a["h2"])
                 if dbgu is not None:
                     G["bgu"] = _addg(G.get("bgu"), dbgu)
@@ -209,7 +218,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 G["s2"] = _addg(G.get("s2"), ds2)
                 s["gfull"], s["h"] = _ag(s["g"], n)
                 del a["x2"], a["r2"], s["dpend"]
-            for s in st:    # B2: Wo / attention / QKV grads -> reduce-scatter
+            for ci, s in enumerate(st):    # B2: Wo / attention / QKV grads -> reduce-scatter
                 _wait(s["h"])
                 a, g2 = s["layers"][li], s["gfull"]
                 if L.bo is not None:
@@ -222,7 +231,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 dq, dk, dv = _split(dqkv, Bc, T, L.h, L.hd)
                 k.attn_bwd(do.view(Bc, T, L.h, L.hd), q, kk, v, a["o"], a["lse"], 1.0 / math.sqrt(L.hd), True,
                            dq, dk, dv, s["pos"], tab)
-                s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dqkv, W(L.wqkv)), n)
+                s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dqkv, W(L.wqkv), out=_slot(ci, dqkv.size(0), d, dt)), n)
                 tn(G, "wqkv", dqkv, a["h1"])
                 if L.bqkv is not None:
                     G["bqkv"] = _addg(G.get("bqkv"), k.bias_grad(dqkv))

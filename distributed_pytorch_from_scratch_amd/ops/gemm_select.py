@@ -67,39 +67,44 @@ def _aligned(*dims: int) -> bool:
     return all(d % 8 == 0 for d in dims)
 
 
-def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None) -> torch.Tensor:
-    """y[M,N] = x[M,K] w[N,K]^T (+ bias fp32[N]) in x.dtype."""
+def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, out=None) -> torch.Tensor:
+    """y[M,N] = x[M,K] w[N,K]^T (+ bias fp32[N]) in x.dtype (into ``out`` when given: e.g. a
+    staging slot of the xGMI collectives, so the collective needs no copy-in)."""
     m = mode()
     if k is reference or not x.is_cuda or (m == "ours" and _aligned(x.shape[1], w.shape[0])):
-        return k.gemm_nt(x, w, bias)
+        return k.gemm_nt(x, w, bias, out=out)
     bb = shadow(bias, x.dtype) if bias is not None else None
 
     def blas():
-        return F.linear(x, w, bb)
+        if out is None:
+            return F.linear(x, w, bb)
+        if bb is None:
+            return torch.mm(x, w.t(), out=out)
+        return torch.addmm(bb, x, w.t(), out=out)
     if not _aligned(x.shape[1], w.shape[0]) or x.shape[0] < _MIN_ROWS:
         return blas()
 
     def ours():
-        return k.gemm_nt(x, w, bias)
+        return k.gemm_nt(x, w, bias, out=out)
     if m == "blas":
         return blas()
     key = ("nt", x.shape[0], w.shape[0], x.shape[1], bias is not None, x.device.index)
     return blas() if _pick(key, ours, blas) == "blas" else ours()
 
 
-def gemm_nn(k, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """c[M,N] = a[M,K] b[K,N] in a.dtype."""
+def gemm_nn(k, a: torch.Tensor, b: torch.Tensor, out=None) -> torch.Tensor:
+    """c[M,N] = a[M,K] b[K,N] in a.dtype (into ``out`` when given)."""
     m = mode()
     if k is reference or not a.is_cuda or (m == "ours" and _aligned(a.shape[1], b.shape[1])):
-        return k.gemm_nn(a, b)
+        return k.gemm_nn(a, b, out=out)
 
     def blas():
-        return torch.matmul(a, b)
+        return torch.matmul(a, b) if out is None else torch.matmul(a, b, out=out)
     if not _aligned(a.shape[1], b.shape[1]) or a.shape[0] < _MIN_ROWS:
         return blas()
 
     def ours():
-        return k.gemm_nn(a, b)
+        return k.gemm_nn(a, b, out=out)
     if m == "blas":
         return blas()
     key = ("nn", a.shape[0], b.shape[1], a.shape[1], a.device.index)

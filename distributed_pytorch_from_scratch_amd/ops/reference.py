@@ -28,7 +28,7 @@ import torch.nn.functional as F
 # ------------------------------------------------------------------------------- GEMM ----
 
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None, rope_pos=None, rope_tab=None,
-            rope_heads: int = 0, rope_hd: int = 0) -> torch.Tensor:
+            rope_heads: int = 0, rope_hd: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """c[M,N] = a[M,K] @ b[N,K]^T (+ bias[N]); output dtype = a.dtype.  With ``rope_pos`` the first
     ``rope_heads`` heads of each row are then rotated (the GPU kernel fuses this into its
     epilogue)."""
@@ -38,12 +38,13 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = Non
     c = c.to(a.dtype)
     if rope_pos is not None and rope_heads > 0:
         rope_(c, rope_pos, rope_tab, rope_heads, rope_hd, False)
-    return c
+    return out.copy_(c) if out is not None else c
 
 
-def gemm_nn(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """c[M,N] = a[M,K] @ b[K,N]; output dtype = a.dtype."""
-    return (a.float() @ b.float()).to(a.dtype)
+def gemm_nn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """c[M,N] = a[M,K] @ b[K,N]; output dtype = a.dtype (written into ``out`` when given)."""
+    c = (a.float() @ b.float()).to(a.dtype)
+    return out.copy_(c) if out is not None else c
 
 
 def gemm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,

@@ -156,6 +156,21 @@ def all_gather(out: torch.Tensor, inp: torch.Tensor, async_op: bool = True):
     return c.all_gather(out, inp, async_op=async_op)
 
 
+def staging(slot: int, shape, dtype: torch.dtype) -> Optional[torch.Tensor]:
+    """Output buffer for a GEMM whose result feeds the next TP all-reduce / reduce-scatter:
+    a view of the xGMI communicator's staging slot ``slot`` (then the collective skips its
+    copy-in), or None when the group runs on RCCL, has not chosen yet, or it does not fit.
+    Use one slot per in-flight chunk; a slot may be rewritten once the collective that read
+    it has been waited."""
+    p = pm.pgm
+    if p is None or p.tp_size == 1 or os.environ.get("DPFS_XGMI_STAGING", "1") == "0":
+        return None
+    c = _decisions.get(id(p.tp_group))
+    if c is None:
+        return None
+    return c.staging(slot, shape, dtype)
+
+
 def check():
     """Raise if any xGMI call of this process timed out (cheap: one host-mapped word)."""
     p = pm.pgm

@@ -49,7 +49,7 @@ class XgmiComm:
     """Peer-memory collectives for one TP group (every rank of the group on this node)."""
 
     def __init__(self, group=None, cap_bytes: Optional[int] = None, timeout_s: float = 120.0,
-                 blocks: Optional[int] = None):
+                 blocks: Optional[int] = None, nslots: Optional[int] = None):
         C = _ext.require()
         self.C = C
         self.group = group
@@ -59,26 +59,53 @@ class XgmiComm:
         cap = cap_bytes or int(os.environ.get("DPFS_XGMI_CAP_MB", "256")) * (1 << 20)
         self.cap = cap
         self.timeout_s = timeout_s
-        self.h, handle = C.xgmi_create(self.rank, self.world, cap)
+        self.nslots = int(os.environ.get("DPFS_XGMI_SLOTS", "4")) if nslots is None else nslots
+        self.h, handle = C.xgmi_create(self.rank, self.world, cap, self.nslots)
         handles: List[Optional[bytes]] = [None] * self.world
         dist.all_gather_object(handles, handle, group=group)
         C.xgmi_open(self.h, b"".join(handles))
         blocks = blocks or int(os.environ.get("DPFS_XGMI_BLOCKS", "32"))
         C.xgmi_set_blocks(self.h, blocks)
         self.stream = torch.cuda.Stream()
+        dev = torch.device("cuda", torch.cuda.current_device())
+        # Staging slots: producer GEMMs write their output straight into one (``staging``), so
+        # the reduce-scatter / all-reduce of it skips the copy-in.
+        self._slots = [C.xgmi_slot_tensor(self.h, i, cap, dev) for i in range(self.nslots)]
         dist.barrier(group=group)
 
     # ------------------------------------------------------------------------ core ----
-    def _launch(self, op: int, x: torch.Tensor, out: torch.Tensor, timeout_s: Optional[float] = None):
+    def staging(self, slot: int, shape, dtype: torch.dtype) -> Optional[torch.Tensor]:
+        """A tensor of ``shape`` / ``dtype`` living in staging slot ``slot`` (None if it does
+        not fit).  The caller owns the slot until the collective it feeds has been waited,
+        and keeps one slot per in-flight chunk."""
+        if not 0 <= slot < self.nslots:
+            return None
+        numel = 1
+        for d in shape:
+            numel *= d
+        nbytes = numel * torch.empty((), dtype=dtype).element_size()
+        if nbytes > self.cap or nbytes % 16:
+            return None
+        return self._slots[slot][:nbytes].view(dtype).view(*shape)
+
+    def _slot_of(self, t: torch.Tensor) -> int:
+        p = t.data_ptr()
+        for i, sl in enumerate(self._slots):
+            if sl.data_ptr() == p:
+                return i
+        return -1
+
+    def _launch(self, op: int, x: torch.Tensor, out: torch.Tensor, timeout_s: Optional[float] = None,
+                slot: int = -1):
         cur = torch.cuda.current_stream()
         self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):
-            self.C.xgmi_run(self.h, op, x, out, self.world, timeout_s or self.timeout_s)
+            self.C.xgmi_run(self.h, op, x, out, self.world, timeout_s or self.timeout_s, slot)
             ev = torch.cuda.Event()
             ev.record(self.stream)
-        x.record_stream(self.stream)
-        if out.data_ptr() != x.data_ptr():
-            out.record_stream(self.stream)
+        for t in (x, out):   # caching-allocator memory only (slots are the communicator's)
+            if self._slot_of(t) < 0 and (t is x or t.data_ptr() != x.data_ptr()):
+                t.record_stream(self.stream)
         return _Work(ev)
 
     def _max_elems(self, t: torch.Tensor) -> int:
@@ -90,6 +117,13 @@ class XgmiComm:
         """In-place SUM over the group (bf16/fp32, fp32 accumulation in rank order, so every
         rank receives bitwise-identical values)."""
         assert t.is_contiguous()
+        slot = self._slot_of(t)
+        if slot >= 0:                      # produced in a staging slot: no copy-in
+            work = self._launch(_ALL_REDUCE, t.view(-1), t.view(-1), timeout_s, slot)
+            if not async_op:
+                work.wait()
+                return None
+            return work
         flat = t.view(-1)
         step = self._max_elems(t)
         work = None
@@ -105,7 +139,8 @@ class XgmiComm:
         """out = (sum over ranks of inp)[rank-th of W equal slices] (same contract as
         ``dist.reduce_scatter_tensor``)."""
         assert inp.numel() == out.numel() * self.world and inp.numel() * inp.element_size() <= self.cap
-        work = self._launch(_REDUCE_SCATTER, inp.contiguous(), out)
+        inp = inp.contiguous()
+        work = self._launch(_REDUCE_SCATTER, inp, out, slot=self._slot_of(inp))
         if not async_op:
             work.wait()
             return None

@@ -35,11 +35,20 @@ def _collectives(rank, world, cases, cap_mb):
             comm.all_reduce(y, async_op=True).wait()
             y2 = x.clone()                      # back-to-back calls reuse the buffers
             comm.all_reduce(y2, async_op=False)
-            res = (y.cpu(), y2.cpu())
+            st = comm.staging(i % comm.nslots, (n,), dtype)   # produced in a staging slot
+            if st is not None:
+                st.copy_(x)
+                comm.all_reduce(st, async_op=False)
+                st = st.cpu()
+            res = (y.cpu(), y2.cpu()) + ((st,) if st is not None else ())
         elif op == "rs":
             y = torch.empty(n // world, dtype=dtype, device="cuda")
             comm.reduce_scatter(y, x, async_op=False)
-            res = (y.cpu(),)
+            st = comm.staging(1, (n,), dtype)
+            st.copy_(x)
+            y2 = torch.empty_like(y)
+            comm.reduce_scatter(y2, st, async_op=False)
+            res = (y.cpu(), y2.cpu())
         else:
             y = torch.empty(n * world, dtype=dtype, device="cuda")
             comm.all_gather(y, x, async_op=False)
@@ -71,6 +80,7 @@ def test_xgmi_collectives_match_fp32_sums(world):
             elif op == "rs":
                 sl = total.view(world, -1)[r]
                 assert torch.allclose(got[0].float(), sl, atol=2e-2, rtol=1e-2), (op, n, r)
+                assert torch.equal(got[0], got[1])   # staged input: same result, no copy-in
             else:
                 assert torch.equal(got[0], torch.cat(xs)), (op, n, r)
 
