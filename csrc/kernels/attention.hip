@@ -502,9 +502,13 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd2_k(
 // (accumulator tile d + DT/2), so the transpose rotation is applied in registers.
 //   dx1 = dy1 c + dy2 s ;  dx2 = dy2 c - dy1 s
 // ========================================================================= bwd: dK, dV ==
-// Block: 4 waves x 16 keys = 64 keys of one (b,h); query tiles of 64 (Q and dO staged in
-// LDS, double buffered; lse/delta staged alongside).
-template <int HD>
+// Block: 4 waves x 16*KW keys of one (b,h); query tiles of 64 (Q and dO staged in LDS,
+// double buffered; lse/delta staged alongside).  KW = key tiles per wave: every Q / dO
+// fragment read from LDS (row reads for S / dP, transposed reads for dV / dK) feeds KW key
+// tiles, so KW = 2 halves the LDS traffic per MFMA (the KW = 1 kernel issues ~32 KiB of LDS
+// reads per 32 MFMAs per wave: at 8 waves per CU the LDS port, not the MFMA pipe, set its
+// pace) and the global Q / dO tile loads are shared by 128 keys.
+template <int HD, int KW = 1>
 __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                           const bf16* __restrict__ V, const bf16* __restrict__ dO,
                                                           const float* __restrict__ LSE,
@@ -513,28 +517,27 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv_k(const 
                                                           long long ldk, long long ldv, long long lddo,
                                                           long long lddk, long long lddv, float scale, int causal,
                                                           const int64_t* __restrict__ rpos, const float* __restrict__ rtab) {
-  constexpr int BKV = 64, BQ = 64, KT = HD / 32, DT = HD / 16;
+  constexpr int BKV = 64 * KW, BQ = 64, KT = HD / 32, DT = HD / 16;
   constexpr int TILE = BQ * HD * 2;
   __shared__ __attribute__((aligned(16))) char smem[2 * (2 * TILE + 2 * BQ * 4)];
   constexpr int BUF = 2 * TILE + 2 * BQ * 4;
-  const int nkb = (T + BKV - 1) / BKV;
   const int kb = blockIdx.x;  // light-to-heavy is fine: causal work per block = T - k0
   const int bh = blockIdx.y, b = bh / H, h = bh % H;
   const int k0 = kb * BKV;
   const int wave = threadIdx.x >> 6, l = lane_id(), g = l >> 4;
-  const int wk0 = k0 + wave * 16;  // this wave's 16 keys
+  const int wk0 = k0 + wave * 16 * KW;  // this wave's 16*KW keys
   const float c2 = scale * kLog2e;
-  (void)nkb;
 
   const bf16* qbase = Q + (long long)b * T * ldq + (long long)h * HD;
   const bf16* dobase = dO + (long long)b * T * lddo + (long long)h * HD;
   const float* lse_b = LSE + ((long long)b * H + h) * T;
   const float* del_b = DELTA + ((long long)b * H + h) * T;
 
-  // K^T and V^T B-operands in registers: lane holds K[wk0 + (l&15)][32kk + 8g + j].
-  bf16x8 kf[KT], vf[KT];
-  {
-    const int ki = wk0 + (l & 15);
+  // K^T and V^T B-operands in registers: lane holds K[wk0 + 16kt + (l&15)][32kk + 8g + j].
+  bf16x8 kf[KW][KT], vf[KW][KT];
+#pragma unroll
+  for (int kt = 0; kt < KW; ++kt) {
+    const int ki = wk0 + 16 * kt + (l & 15);
 #pragma unroll
     for (int kk = 0; kk < KT; ++kk) {
       bf16x8 a = {}, c = {};
@@ -542,16 +545,18 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv_k(const 
         a = *reinterpret_cast<const bf16x8*>(K + ((long long)b * T + ki) * ldk + (long long)h * HD + 32 * kk + 8 * g);
         c = *reinterpret_cast<const bf16x8*>(V + ((long long)b * T + ki) * ldv + (long long)h * HD + 32 * kk + 8 * g);
       }
-      kf[kk] = a;
-      vf[kk] = c;
+      kf[kt][kk] = a;
+      vf[kt][kk] = c;
     }
   }
-  f32x4 dk[DT], dv[DT];
+  f32x4 dk[KW][DT], dv[KW][DT];
 #pragma unroll
-  for (int d = 0; d < DT; ++d) {
-    dk[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    dv[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  }
+  for (int kt = 0; kt < KW; ++kt)
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+      dk[kt][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      dv[kt][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
 
   const int qstart = causal ? (k0 / BQ) * BQ : 0;
   const int nq = (T - qstart + BQ - 1) / BQ;
@@ -589,44 +594,64 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv_k(const 
     }
     const bool wave_active = !causal || (qq0 + BQ - 1 >= wk0);
     if (wave_active) {
-      // S[q][k] and dP[q][k] for 4 query tiles of 16.
-      f32x4 s[4], dp[4];
+      // S[q][k] and dP[q][k] for 4 query tiles of 16 x KW key tiles.
+      f32x4 s[KW][4], dp[KW][4];
 #pragma unroll
       for (int qt = 0; qt < 4; ++qt) {
-        s[qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        dp[qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kt = 0; kt < KW; ++kt) {
+          s[kt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+          dp[kt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
 #pragma unroll
         for (int kk = 0; kk < KT; ++kk) {
-          s[qt] = MFMA(row_frag<HD>(lq, 16 * qt, 32 * kk), kf[kk], s[qt]);
-          dp[qt] = MFMA(row_frag<HD>(ldo_, 16 * qt, 32 * kk), vf[kk], dp[qt]);
+          const bf16x8 qa = row_frag<HD>(lq, 16 * qt, 32 * kk);
+          const bf16x8 da = row_frag<HD>(ldo_, 16 * qt, 32 * kk);
+#pragma unroll
+          for (int kt = 0; kt < KW; ++kt) {
+            s[kt][qt] = MFMA(qa, kf[kt][kk], s[kt][qt]);
+            dp[kt][qt] = MFMA(da, vf[kt][kk], dp[kt][qt]);
+          }
         }
       }
-      const int ki = wk0 + (l & 15);
-      const bool need_mask = (causal && wk0 + 15 > qq0) || (qq0 + BQ > T) || (wk0 + 16 > T);
+      const bool need_mask = (causal && wk0 + 16 * KW - 1 > qq0) || (qq0 + BQ > T) || (wk0 + 16 * KW > T);
 #pragma unroll
       for (int qt = 0; qt < 4; ++qt) {
         const f32x4 lsv = *reinterpret_cast<const f32x4*>(ls + 16 * qt + 4 * g);
         const f32x4 dsv = *reinterpret_cast<const f32x4*>(ds + 16 * qt + 4 * g);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float p = __builtin_amdgcn_exp2f(fmaf(s[qt][j], c2, -lsv[j]));
-          if (need_mask) {
-            const int qi = qq0 + 16 * qt + 4 * g + j;
-            if (qi >= T || ki >= T || (causal && ki > qi)) p = 0.f;
+        for (int kt = 0; kt < KW; ++kt) {
+          const int ki = wk0 + 16 * kt + (l & 15);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float p = __builtin_amdgcn_exp2f(fmaf(s[kt][qt][j], c2, -lsv[j]));
+            if (need_mask) {
+              const int qi = qq0 + 16 * qt + 4 * g + j;
+              if (qi >= T || ki >= T || (causal && ki > qi)) p = 0.f;
+            }
+            s[kt][qt][j] = p;
+            dp[kt][qt][j] = p * (dp[kt][qt][j] - dsv[j]);
           }
-          s[qt][j] = p;
-          dp[qt][j] = p * (dp[qt][j] - dsv[j]);
         }
       }
       // dV[k][d] += P^T dO ;  dK[k][d] += dS^T Q
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 pa = pack_pt(s[2 * ks], s[2 * ks + 1]);
-        const bf16x8 da = pack_pt(dp[2 * ks], dp[2 * ks + 1]);
+        bf16x8 pa[KW], sa[KW];
+#pragma unroll
+        for (int kt = 0; kt < KW; ++kt) {
+          pa[kt] = pack_pt(s[kt][2 * ks], s[kt][2 * ks + 1]);
+          sa[kt] = pack_pt(dp[kt][2 * ks], dp[kt][2 * ks + 1]);
+        }
 #pragma unroll
         for (int d = 0; d < DT; ++d) {
-          dv[d] = MFMA(pa, tr_frag<HD>(ldo_, 32 * ks, 16 * d), dv[d]);
-          dk[d] = MFMA(da, tr_frag<HD>(lq, 32 * ks, 16 * d), dk[d]);
+          const bf16x8 dob = tr_frag<HD>(ldo_, 32 * ks, 16 * d);
+          const bf16x8 qb = tr_frag<HD>(lq, 32 * ks, 16 * d);
+#pragma unroll
+          for (int kt = 0; kt < KW; ++kt) {
+            dv[kt][d] = MFMA(pa[kt], dob, dv[kt][d]);
+            dk[kt][d] = MFMA(sa[kt], qb, dk[kt][d]);
+          }
         }
       }
     }
@@ -638,36 +663,39 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv_k(const 
     }
     __syncthreads();
   }
-  // Write dK (scaled), dV: C layout col = d (l&15), rows = keys 4g + j.
+  // Write dK (scaled), dV: C layout col = d (l&15), rows = keys 16kt + 4g + j.
 #pragma unroll
-  for (int d = 0; d < DT; ++d)
+  for (int kt = 0; kt < KW; ++kt) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dk[d][j] *= scale;
-  if (rpos) {
+    for (int d = 0; d < DT; ++d)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int ki = wk0 + 4 * g + j;
-      if (ki < T) {
-        const float* tr = rtab + rpos[(long long)b * T + ki] * HD;
+      for (int j = 0; j < 4; ++j) dk[kt][d][j] *= scale;
+    if (rpos) {
 #pragma unroll
-        for (int d = 0; d < DT / 2; ++d) {
-          const float c = tr[16 * d + (l & 15)], sn = tr[HD / 2 + 16 * d + (l & 15)];
-          const float x1 = dk[d][j], x2 = dk[d + DT / 2][j];
-          dk[d][j] = x1 * c + x2 * sn;
-          dk[d + DT / 2][j] = x2 * c - x1 * sn;
+      for (int j = 0; j < 4; ++j) {
+        const int ki = wk0 + 16 * kt + 4 * g + j;
+        if (ki < T) {
+          const float* tr = rtab + rpos[(long long)b * T + ki] * HD;
+#pragma unroll
+          for (int d = 0; d < DT / 2; ++d) {
+            const float c = tr[16 * d + (l & 15)], sn = tr[HD / 2 + 16 * d + (l & 15)];
+            const float x1 = dk[kt][d][j], x2 = dk[kt][d + DT / 2][j];
+            dk[kt][d][j] = x1 * c + x2 * sn;
+            dk[kt][d + DT / 2][j] = x2 * c - x1 * sn;
+          }
         }
       }
     }
-  }
 #pragma unroll
-  for (int d = 0; d < DT; ++d) {
+    for (int d = 0; d < DT; ++d) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int ki = wk0 + 4 * g + j;
-      if (ki < T) {
-        const long long col = (long long)h * HD + 16 * d + (l & 15);
-        dK[((long long)b * T + ki) * lddk + col] = (bf16)dk[d][j];
-        dV[((long long)b * T + ki) * lddv + col] = (bf16)dv[d][j];
+      for (int j = 0; j < 4; ++j) {
+        const int ki = wk0 + 16 * kt + 4 * g + j;
+        if (ki < T) {
+          const long long col = (long long)h * HD + 16 * d + (l & 15);
+          dK[((long long)b * T + ki) * lddk + col] = (bf16)dk[kt][d][j];
+          dV[((long long)b * T + ki) * lddv + col] = (bf16)dv[kt][d][j];
+        }
       }
     }
   }
@@ -1064,7 +1092,8 @@ extern "C" int dpfs_attn_supported_hd(int hd) { return hd == 32 || hd == 64 || h
 
 static int g_attn_impl = 1;  // 1 = register-staged (default, fastest measured), 2 / 3 = LDS-DMA ring with 8 / 4 waves
 extern "C" void dpfs_attn_set_impl(int v) { g_attn_impl = v; }
-static int g_attn_bwd_impl = 2;  // dK/dV kernel: 2 = LDS-DMA ring (default), 1 = register-staged
+static int g_attn_bwd_impl = 2;  // dK/dV kernel: 2 = LDS-DMA ring (default), 1 = register-staged,
+                                 // 3 = register-staged with 32 keys per wave (hd <= 64)
 extern "C" void dpfs_attn_set_bwd_impl(int v) { g_attn_bwd_impl = v; }
 
 extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int T, int H,
@@ -1100,6 +1129,18 @@ extern "C" void dpfs_attn_bwd(const void* dout, const void* q, const void* k, co
                                                              (const bf16*)dout, (const bf16*)o, lse, delta, (bf16*)dq,
                                                              T, H, ldq, ldk, ldv, lddo, ldo, lddq, scale, causal,
                                                              rope_pos, rope_tab));
+  if (g_attn_bwd_impl == 3 && hd <= 64) {
+    dim3 gk2((T + 127) / 128, B * H);
+    if (hd == 64)
+      attn_bwd_dkdv_k<64, 2><<<gk2, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,
+                                                 lse, delta, (bf16*)dk, (bf16*)dv, T, H, ldq, ldk, ldv, lddo, lddk,
+                                                 lddv, scale, causal, rope_pos, rope_tab);
+    else
+      attn_bwd_dkdv_k<32, 2><<<gk2, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,
+                                                 lse, delta, (bf16*)dk, (bf16*)dv, T, H, ldq, ldk, ldv, lddo, lddk,
+                                                 lddv, scale, causal, rope_pos, rope_tab);
+    return;
+  }
   dim3 gk((T + 63) / 64, B * H);
   if (g_attn_bwd_impl == 2) {
     DPFS_HD_DISPATCH(hd, attn_bwd_dkdv2_k<HD_><<<gk, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,

@@ -196,6 +196,16 @@ def test_attention(C, B, T, H, hd, impl):
         C.attn_set_bwd_impl(2)
 
 
+@pytest.mark.parametrize("B,T,H,hd", [(2, 256, 4, 64), (1, 300, 2, 64), (1, 1000, 2, 64), (2, 200, 3, 32)])
+def test_attention_bwd_dkdv_32_keys_per_wave(C, B, T, H, hd):
+    """dK/dV kernel variant with two key tiles per wave (impl 3, hd <= 64)."""
+    C.attn_set_bwd_impl(3)
+    try:
+        _check_attention(C, B, T, H, hd)
+    finally:
+        C.attn_set_bwd_impl(2)
+
+
 def _check_attention(C, B, T, H, hd):
     torch.manual_seed(10)
     qkv = torch.randn(B * T, 3 * H * hd, device=DEV).bfloat16()
