@@ -43,6 +43,11 @@ class ModelArgs:
     norm_eps: float = 1e-5
     vocab_pad_to: int = 128
     sequence_parallel: bool = False
+    # When the heads do not divide over the TP ranks (12 heads at TP 8: 2 on ranks 0-3, 1 on
+    # ranks 4-7), give the lighter ranks a larger vocabulary shard so every rank carries the
+    # same work (vocab_partition).  Off, or with an even head split, the reference's vocab
+    # ranges are used (equal shards, remainder on the last rank: layers.py:120-132).
+    vocab_balance: bool = True
 
     @property
     def head_dim(self) -> int:
@@ -69,6 +74,37 @@ class ModelArgs:
         """Training FLOPs/token: 6 * matmul params + causal attention (fwd+bwd)."""
         attn = 12 * self.num_layers * self.attn_dim * seq_len / 2  # causal -> half of T^2
         return 6 * self.matmul_params() + attn
+
+
+def vocab_partition(args: "ModelArgs", head_sizes, granule: int = 64):
+    """Per-rank vocab shard sizes for a TP group whose ranks hold ``head_sizes`` heads.
+
+    Each rank's step work ~ heads_r * W_head + vocab_r * W_col with, per token and layer,
+    W_head = 24 d hd (QKV + Wo GEMMs, fwd + bwd) + 21 T hd (causal attention fwd + bwd, counted
+    at 1/3 of GEMM efficiency) and W_col = 6 d / L (lm_head GEMMs).  Ranks with fewer heads get
+    (h_max - h_r) * W_head / W_col extra columns; shards are multiples of ``granule`` (the
+    last rank takes the remainder).  Even head splits keep the reference ranges."""
+    n = len(head_sizes)
+    V = args.padded_vocab_size
+    per = V // n
+    ref = [per] * (n - 1) + [V - per * (n - 1)]
+    if n == 1 or not args.vocab_balance or len(set(head_sizes)) == 1 or V < 4 * granule * n:
+        return ref
+    d, hd, L = args.attn_dim, args.head_dim, args.num_layers
+    T = min(args.maxlen, 2048)
+    cols_per_head = L * (24 * d * hd + 21 * T * hd) / (6 * d)
+    hmax = max(head_sizes)
+    extra = [(hmax - h) * cols_per_head for h in head_sizes]
+    base = (V - sum(extra)) / n
+    if base < granule:                       # vocab too small to balance fully: scale down
+        f = (V - granule * n) / max(1.0, sum(extra))
+        extra = [e * f for e in extra]
+        base = (V - sum(extra)) / n
+    sizes = [max(granule, int(round((base + e) / granule)) * granule) for e in extra[:-1]]
+    last = V - sum(sizes)
+    if last < granule // 2:
+        return ref
+    return sizes + [last]
 
 
 # Backwards-compatible alias with the reference's (misspelt) name.

@@ -39,7 +39,7 @@ from ..parallel.cross_entropy import IGNORE_INDEX, vocab_parallel_cross_entropy
 from ..parallel.layers import (ColumnParallelLinear, FusedColumnParallelLinear, LayerNorm,
                                ParallelVocabularyEmbedding, RMSNorm, RowParallelLinear,
                                attach_fused, partition_sizes)
-from .config import ModelArgs
+from .config import ModelArgs, vocab_partition
 
 
 def _tp():
@@ -141,13 +141,14 @@ class Transformer(nn.Module):
         self.vocab_size = args.vocab_size
         self.padded_vocab_size = args.padded_vocab_size
         sp = args.sequence_parallel
+        # Vocab shards (embedding rows = lm_head rows): the reference ranges, or balanced
+        # against an uneven head split (config.vocab_partition).
+        head_sizes = [w // args.head_dim for w in partition_sizes(args.attn_dim, n, args.head_dim)]
+        vsizes = vocab_partition(args, head_sizes)
         self.embedding = ParallelVocabularyEmbedding(self.padded_vocab_size, args.attn_dim,
-                                                     sequence_parallel=sp)
+                                                     sequence_parallel=sp, sizes=vsizes)
         self.layers = nn.ModuleList([DecoderLayer(args) for _ in range(args.num_layers)])
         self.norm = _make_norm(args, sp)
-        # lm_head vocab shards = the embedding's [st, ed) ranges (last rank takes the remainder).
-        per = self.padded_vocab_size // n
-        vsizes = [per] * (n - 1) + [self.padded_vocab_size - per * (n - 1)]
         self.lm_head = ColumnParallelLinear(args.attn_dim, self.padded_vocab_size, add_bias=args.bias,
                                             gather_output=False, sizes=vsizes, sequence_parallel=sp)
         self.compute_dtype: Optional[torch.dtype] = None

@@ -273,13 +273,19 @@ class ParallelVocabularyEmbedding(nn.Module):
     """Vocab-sharded embedding: masked local lookup + all-reduce(SUM) over the TP group."""
 
     def __init__(self, vocab_size: int, hdim: int, out_dtype: Optional[torch.dtype] = None,
-                 sequence_parallel: bool = False):
+                 sequence_parallel: bool = False, sizes: Optional[Sequence[int]] = None):
         super().__init__()
         self.vocab_size = vocab_size
         self.hdim = hdim
         self.out_dtype = out_dtype
         self.sequence_parallel = sequence_parallel
-        self.vocab_st_idx, self.vocab_ed_idx = self._get_vocab_range(vocab_size)
+        if sizes is None:
+            self.vocab_st_idx, self.vocab_ed_idx = self._get_vocab_range(vocab_size)
+        else:   # explicit per-rank shard sizes (e.g. models.config.vocab_partition)
+            n, r = _tp_size_rank()
+            assert len(sizes) == n and sum(sizes) == vocab_size
+            self.vocab_st_idx = sum(sizes[:r])
+            self.vocab_ed_idx = self.vocab_st_idx + sizes[r]
         self.weight = nn.Parameter(torch.empty(self.vocab_ed_idx - self.vocab_st_idx, hdim))
 
     def _get_vocab_range(self, vocab_size: int) -> Tuple[int, int]:

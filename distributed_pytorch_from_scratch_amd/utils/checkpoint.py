@@ -116,9 +116,12 @@ def merge_tp(shards: Sequence[Dict[str, torch.Tensor]]) -> Dict[str, torch.Tenso
     return out
 
 
-def split_tp(full: Dict[str, torch.Tensor], n: int, head_dim: Optional[int] = None) -> List[Dict[str, torch.Tensor]]:
+def split_tp(full: Dict[str, torch.Tensor], n: int, head_dim: Optional[int] = None,
+             vocab_sizes: Optional[Sequence[int]] = None) -> List[Dict[str, torch.Tensor]]:
     """Split a TP=1 state dict into ``n`` shards using the framework's partition rules
-    (heads whole when ``head_dim`` is given; vocab remainder on the last rank)."""
+    (heads whole when ``head_dim`` is given; vocab shards = ``vocab_sizes`` — e.g.
+    ``models.config.vocab_partition`` for a model built with an uneven head split — or the
+    reference ranges, remainder on the last rank)."""
     from ..parallel.layers import partition_sizes
     outs = [dict() for _ in range(n)]
     for k, v in full.items():
@@ -129,8 +132,11 @@ def split_tp(full: Dict[str, torch.Tensor], n: int, head_dim: Optional[int] = No
             continue
         total = v.size(d)
         if k.startswith("embedding") or k.startswith("lm_head"):
-            per = total // n
-            sizes = [per] * (n - 1) + [total - per * (n - 1)]
+            if vocab_sizes is not None:
+                sizes = list(vocab_sizes)
+            else:
+                per = total // n
+                sizes = [per] * (n - 1) + [total - per * (n - 1)]
         elif head_dim and (".attn." in k):
             sizes = partition_sizes(total, n, head_dim)
         else:

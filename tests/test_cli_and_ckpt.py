@@ -103,6 +103,38 @@ def test_tp_merge_split_roundtrip():
             assert torch.equal(split[r][k], sd4[r][k]), (r, k)
 
 
+def _get_sd_balanced(rank, world):
+    from distributed_pytorch_from_scratch_amd.models import Transformer, ModelArgs
+    from distributed_pytorch_from_scratch_amd.utils.dist import set_seed
+    m = Transformer.from_args(ModelArgs(attn_dim=48, ffn_dim=64, num_heads=6, num_layers=1, vocab_size=2000,
+                                        maxlen=16, vocab_pad_to=1))
+    set_seed(0)
+    m.reset_parameters()
+    return {k: v.clone() for k, v in m.state_dict().items()}
+
+
+def test_balanced_vocab_shards_merge_split():
+    """6 heads over 4 ranks (2, 2, 1, 1): the one-head ranks get larger vocab shards
+    (config.vocab_partition); merge / split with those sizes round-trips exactly."""
+    from dist_helpers import run_distributed
+    from distributed_pytorch_from_scratch_amd.models import ModelArgs
+    from distributed_pytorch_from_scratch_amd.models.config import vocab_partition
+    from distributed_pytorch_from_scratch_amd.utils import checkpoint as ck
+    args = ModelArgs(attn_dim=48, ffn_dim=64, num_heads=6, num_layers=1, vocab_size=2000, maxlen=16, vocab_pad_to=1)
+    vs = vocab_partition(args, [2, 2, 1, 1])
+    assert sum(vs) == 2000 and vs[0] < vs[2] and len(set(vs[:2])) == 1
+    sd1 = run_distributed(_get_sd_balanced, 1)[0]
+    sd4 = run_distributed(_get_sd_balanced, 4)
+    assert [sd4[r]["embedding.weight"].size(0) for r in range(4)] == vs
+    merged = ck.merge_tp([sd4[r] for r in range(4)])
+    for k in sd1:
+        assert torch.equal(merged[k], sd1[k]), k
+    split = ck.split_tp(sd1, 4, head_dim=8, vocab_sizes=vs)
+    for r in range(4):
+        for k in sd1:
+            assert torch.equal(split[r][k], sd4[r][k]), (r, k)
+
+
 def test_data_pipeline(tmp_path):
     pytest.importorskip("tokenizers")
     raw = tmp_path / "raw.txt"
