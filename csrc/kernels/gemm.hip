@@ -703,14 +703,39 @@ static int tn_v2_splits(int M, int N, int K) {
   return best;
 }
 
-static bool tn_use_v1(int M, int N, int K) {
-  if (g_gemm_impl == 1) return true;
-  if (g_force_cfg >= 0 || g_force_splits > 0) return false;
-  const double waste = (double)tiles2(M, N, 256, 256) * 65536.0 / ((double)M * N);
-  return waste > 1.3;
+// Small outputs (fewer than 256 tiles of 256x256: every TP-sharded wgrad at TP 4-8, e.g.
+// 384 x 768 or 768 x 128 at TP 8) cannot fill the chip without a K-split, and power-of-2
+// splits leave ragged rounds (6 tiles x 64 = 384 blocks = 1.5 rounds).  Search every split
+// 1..64 and both tile shapes with the makespan model (256x128 K-step ~1.5 us); measured on
+// the TP 8 shapes (tools/tn_split_sweep.py): 384x768 0.182 -> 0.140 ms (6 tiles x 42 splits),
+// 768x128 0.081 -> 0.069 ms (256x128 tiles, 64 splits).
+static int tn_small_plan(int M, int N, int K, int* cfg) {
+  double best_t = 1e300;
+  int best_s = 1;
+  *cfg = 0;
+  for (int c = 0; c < 2; ++c) {
+    const long long tiles = c == 0 ? tiles2(M, N, 256, 256) : tiles2(M, N, 256, 128);
+    const double step = c == 0 ? 1.95 : 1.5;
+    for (int S = 1; S <= 64; ++S) {
+      if (S > 1 && K / S < 512) break;
+      const long long kps = ((K + S - 1) / S + 63) / 64;
+      const long long rounds = (tiles * S + 255) / 256;
+      const double t = (double)rounds * kps * step + (S > 1 ? (double)S * M * N * 8.0 / 4.0e6 : 0.0);
+      if (t < best_t * 0.97) {
+        best_t = t;
+        best_s = S;
+        *cfg = c;
+      }
+    }
+  }
+  return best_s;
 }
 
-extern "C" int dpfs_gemm_tn_splits(int M, int N, int K) {
+static bool tn_use_v1(int M, int N, int K) { return g_gemm_impl == 1; }
+
+// (tile config, K-splits) of a TN GEMM.
+static int tn_plan(int M, int N, int K, int* cfg) {
+  *cfg = g_force_cfg >= 0 ? g_force_cfg : 0;
   if (tn_use_v1(M, N, K)) {
     const int tiles = tiles_of(M, N);
     int s = 1;
@@ -718,7 +743,13 @@ extern "C" int dpfs_gemm_tn_splits(int M, int N, int K) {
     return s;
   }
   if (g_force_splits > 0) return g_force_splits;
+  if (g_force_cfg < 0 && tiles2(M, N, 256, 256) < 256) return tn_small_plan(M, N, K, cfg);
   return tn_v2_splits(M, N, K);
+}
+
+extern "C" int dpfs_gemm_tn_splits(int M, int N, int K) {
+  int cfg;
+  return tn_plan(M, N, K, &cfg);
 }
 
 // Floats of slab workspace dpfs_gemm_tn needs (0: none).
@@ -731,7 +762,8 @@ extern "C" long long dpfs_gemm_tn_ws(int M, int N, int K, int accumulate) {
 extern "C" void dpfs_gemm_tn(const void* A, const void* B, float* C, float* ws, int M, int N, int K, int lda, int ldb,
                              int accumulate, hipStream_t s) {
   const long long n = (long long)M * N;
-  const int S = dpfs_gemm_tn_splits(M, N, K);
+  int cfg;
+  const int S = tn_plan(M, N, K, &cfg);
   int kps = (K + S - 1) / S;
   kps = ((kps + BKK - 1) / BKK) * BKK;
   const bool direct = (S == 1 && !accumulate);
@@ -741,7 +773,7 @@ extern "C" void dpfs_gemm_tn(const void* A, const void* B, float* C, float* ws, 
                                                                    N, K, lda, ldb, N, direct ? K : kps,
                                                                    direct ? 0 : n);
   } else {
-    launch2<false, false, 1>(g_force_cfg >= 0 ? g_force_cfg : 0, A, B, dst, nullptr, M, N, K, lda, ldb, N, S, direct ? K : kps,
+    launch2<false, false, 1>(cfg, A, B, dst, nullptr, M, N, K, lda, ldb, N, S, direct ? K : kps,
                              direct ? 0 : n, span_bytes(K, lda, M), span_bytes(K, ldb, N), s);
   }
   if (direct) return;
