@@ -57,6 +57,17 @@ def run(rank, world, sizes_mb, reps, blocks_list):
                     else:
                         comm.all_gather(x, part, async_op=False)
                 cands.append((f"xgmi/{nb}", f))
+            st = comm.staging(0, (n,), torch.bfloat16) if op != "all_gather" else None
+            if st is not None:          # producer wrote into a staging slot: no copy-in
+                st.copy_(x)
+
+                def fs(nb=blocks_list[-1]):
+                    comm.set_blocks(nb)
+                    if op == "all_reduce":
+                        comm.all_reduce(st, async_op=False)
+                    else:
+                        comm.reduce_scatter(part, st, async_op=False)
+                cands.append((f"staged/{blocks_list[-1]}", fs))
             if nccl:
                 def r():
                     if op == "all_reduce":
