@@ -40,17 +40,22 @@ class ProcessGroupManager:
         self.dp_rank, self.tp_rank = [int(v) for v in (self.grid == self.global_rank).nonzero()[0]]
         self.backend = dist.get_backend()
 
-        # Every rank must take part in every new_group call, in the same order.
+        # Every rank must take part in every new_group call, in the same order.  RCCL groups get
+        # high-priority HIP streams (their collectives sit on the overlapped critical path).
+        kw = {}
+        if self.backend == "nccl":
+            kw["pg_options"] = dist.ProcessGroupNCCL.Options()
+            kw["pg_options"].is_high_priority_stream = True
         self.tp_group = None
         self.dp_group = None
         for d in range(dp_size):
             ranks = self.grid[d].tolist()
-            g = dist.new_group(ranks) if tp_size < self.world_size else dist.group.WORLD
+            g = dist.new_group(ranks, **kw) if tp_size < self.world_size else dist.group.WORLD
             if d == self.dp_rank:
                 self.tp_group = g
         for t in range(tp_size):
             ranks = self.grid[:, t].tolist()
-            g = dist.new_group(ranks) if dp_size < self.world_size else dist.group.WORLD
+            g = dist.new_group(ranks, **kw) if dp_size < self.world_size else dist.group.WORLD
             if t == self.tp_rank:
                 self.dp_group = g
         self.tp_ranks = self.grid[self.dp_rank].tolist()

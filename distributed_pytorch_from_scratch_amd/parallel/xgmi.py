@@ -66,7 +66,9 @@ class XgmiComm:
         C.xgmi_open(self.h, b"".join(handles))
         blocks = blocks or int(os.environ.get("DPFS_XGMI_BLOCKS", "32"))
         C.xgmi_set_blocks(self.h, blocks)
-        self.stream = torch.cuda.Stream()
+        # High-priority side stream: a collective that overlaps compute is the critical path
+        # of the other chunk, so its (narrow) kernel should win the CU arbitration.
+        self.stream = torch.cuda.Stream(priority=-1)
         dev = torch.device("cuda", torch.cuda.current_device())
         # Staging slots: producer GEMMs write their output straight into one (``staging``), so
         # the reduce-scatter / all-reduce of it skips the copy-in.

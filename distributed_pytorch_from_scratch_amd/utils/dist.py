@@ -84,6 +84,11 @@ def init_dist_env(args: Optional[Namespace] = None, rank: Optional[int] = None, 
     if backend == "nccl":
         torch.cuda.set_device(local_rank)
         kw["device_id"] = torch.device("cuda", local_rank)
+        # RCCL collectives on a high-priority HIP stream: they overlap the other ping-pong
+        # chunk's compute and are on its critical path.
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        kw["pg_options"] = opts
     if not dist.is_initialized():
         dist.init_process_group(backend=backend, init_method="env://", world_size=world_size,
                                 rank=rank, timeout=datetime.timedelta(seconds=timeout_s), **kw)
