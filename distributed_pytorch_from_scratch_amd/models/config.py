@@ -48,6 +48,10 @@ class ModelArgs:
     # same work (vocab_partition).  Off, or with an even head split, the reference's vocab
     # ranges are used (equal shards, remainder on the last rank: layers.py:120-132).
     vocab_balance: bool = True
+    # Activation recompute in the explicit-schedule engines: keep only each layer's input and
+    # re-run the layer forward (collectives included) in backward.  ~16x less activation
+    # memory per layer at GPT-2 width for ~1/3 more compute (long-sequence / large configs).
+    recompute: bool = False
 
     @property
     def head_dim(self) -> int:

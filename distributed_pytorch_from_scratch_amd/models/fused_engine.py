@@ -117,6 +117,7 @@ class DecoderTrainFn(torch.autograd.Function):
         vst = head.odim_start
         vvalid = max(0, min(model.vocab_size - vst, head.odim_partition))
         d = model.args.attn_dim
+        recompute = bool(getattr(model.args, "recompute", False))
 
         W = lambda w: shadow(w, dt) if w is not None else None  # bf16 compute copies
         st = []  # per-chunk saved state
@@ -155,6 +156,8 @@ class DecoderTrainFn(torch.autograd.Function):
                 s["layers"][-1].update(x2=x2, r2=r2, h2=h2, gu=gu, sw=sw)
                 s["x"] = x2
                 s["pend"], s["pend_bias"], s["h"] = qout, L.bd, _ar(qout)
+                if recompute:          # keep only the layer input; the rest is rebuilt in backward
+                    s["layers"][-1] = {"x": s["layers"][-1]["x"]}
         # head: residual, final norm, lm_head shard, vocab-parallel CE statistics
         losses_sum = torch.zeros((), device=dev, dtype=torch.float32)
         n_valid_total = torch.zeros((), device=dev, dtype=torch.float32)
@@ -183,6 +186,7 @@ class DecoderTrainFn(torch.autograd.Function):
         ctx.n_valid = n_valid_total
         ctx.tab = tab
         ctx.nparams = len(params)
+        ctx.recompute = recompute
         return loss
 
     @staticmethod
@@ -254,9 +258,31 @@ class DecoderTrainFn(torch.autograd.Function):
             s["dpend"] = None
             del s["xf"], s["hf"]
         dp_reduce(g, ("nf", "lm_w", "lm_b"))
+
+        def rebuild(L, li):
+            """Activation recompute: re-run layer li's forward from its saved input up to the
+            SwiGLU output.  The Wo all-reduce runs unstaged: each chunk's staging slot still
+            holds the pending norm1 input-grad of layer li+1."""
+            for s in st:
+                a = s["layers"][li]
+                a["h1"], a["r1"] = k.rmsnorm_fwd(a["x"], L.s1, L.eps1)
+                a["qkv"] = k.gemm_nt(a["h1"], W(L.wqkv), L.bqkv, s["pos"], tab, 2 * L.h, L.hd)
+                q, kk, v = _split(a["qkv"], s["B"], T, L.h, L.hd)
+                a["o"], a["lse"] = k.attn_fwd(q, kk, v, 1.0 / math.sqrt(L.hd), True)
+                pout = GS.gemm_nt(k, a["o"].view(a["qkv"].size(0), L.h * L.hd), W(L.wo), None)
+                a["pout"], a["hh"] = pout, _ar(pout)
+            for s in st:
+                a = s["layers"][li]
+                _wait(a.pop("hh"))
+                a["x2"], a["h2"], a["r2"] = k.add_rmsnorm_fwd(a.pop("pout"), L.bo, a["x"], L.s2, L.eps2)
+                a["gu"] = GS.gemm_nt(k, a["h2"], W(L.wgu), L.bgu)
+                a["sw"] = k.swiglu_fwd(a["gu"])
+
         # ---- layers, reversed
         for li in range(nL - 1, -1, -1):
             L, G = layers[li], gl[li]
+            if ctx.recompute:
+                rebuild(L, li)
             # b2: down / SwiGLU / gate|up grads -> AR(dh2)
             for ci, s in enumerate(st):
                 if s["dpend"] is not None:     # finish the upper layer: wait, norm1 bwd, residual

@@ -73,6 +73,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
         tab = model.rope_table(dev)
         emb, head = model.embedding, model.lm_head
         d = model.args.attn_dim
+        recompute = bool(getattr(model.args, "recompute", False))
         vst = head.odim_start
         vvalid = max(0, min(model.vocab_size - vst, head.odim_partition))
         W = lambda w: shadow(w, dt) if w is not None else None
@@ -119,6 +120,8 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 qout = GS.gemm_nt(k, sw, W(L.wd), None, out=_slot(ci, sw.size(0), d, dt))
                 a.update(gu=gu, sw=sw)
                 (s["pend"], s["h"]), s["pend_bias"] = _rs(qout, n), L.bd
+                if recompute:          # keep only the layer input; the rest is rebuilt in backward
+                    s["layers"][-1] = {"x": a["x"]}
         for s in st:        # final norm on my rows -> all-gather
             _wait(s["h"])
             xf, hfs, rf = k.add_rmsnorm_fwd(s["pend"], s["pend_bias"], s["x"], model.norm.scale, model.norm.eps)
@@ -143,6 +146,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
             s.update(logits=logits, ce_lse=lse, valid=valid, h=None)
         n_valid_total = n_valid_total.clamp_min(1.0)
         ctx.model, ctx.st, ctx.layers, ctx.meta = model, st, layers, (T, dt, vst, vvalid, n)
+        ctx.recompute = recompute
         ctx.n_valid, ctx.tab = n_valid_total, tab
         return losses_sum / n_valid_total
 
@@ -195,8 +199,38 @@ class DecoderTrainFnSP(torch.autograd.Function):
             s["gfull"], s["h"] = _ag(s["g"], n)
             del s["xf"], s["rf"], s["dpend"]
         dp_reduce(g, ("lm_w", "lm_b"))
+
+        def rebuild(L, li):
+            """Activation recompute: re-run layer li's forward (with its collectives) from the
+            saved layer input, up to the SwiGLU output (the down projection is not needed)."""
+            for s in st:
+                a = s["layers"][li]
+                h1s, a["r1"] = k.rmsnorm_fwd(a["x"], L.s1, L.eps1)
+                a["h1"], a["hh"] = _ag(h1s, n)
+            for ci, s in enumerate(st):
+                a = s["layers"][li]
+                _wait(a.pop("hh"))
+                a["qkv"] = k.gemm_nt(a["h1"], W(L.wqkv), L.bqkv, s["pos"], tab, 2 * L.h, L.hd)
+                q, kk, v = _split(a["qkv"], s["B"], T, L.h, L.hd)
+                a["o"], a["lse"] = k.attn_fwd(q, kk, v, 1.0 / math.sqrt(L.hd), True)
+                pout = GS.gemm_nt(k, a["o"].view(a["qkv"].size(0), L.h * L.hd), W(L.wo), None,
+                                  out=_slot(ci, a["qkv"].size(0), d, dt))
+                a["pend"], a["hh"] = _rs(pout, n)
+            for s in st:
+                a = s["layers"][li]
+                _wait(a.pop("hh"))
+                a["x2"], h2s, a["r2"] = k.add_rmsnorm_fwd(a.pop("pend"), L.bo, a["x"], L.s2, L.eps2)
+                a["h2"], a["hh"] = _ag(h2s, n)
+            for s in st:
+                a = s["layers"][li]
+                _wait(a.pop("hh"))
+                a["gu"] = GS.gemm_nt(k, a["h2"], W(L.wgu), L.bgu)
+                a["sw"] = k.swiglu_fwd(a["gu"])
+
         for li in range(nL - 1, -1, -1):
             L, G = layers[li], gl[li]
+            if ctx.recompute:
+                rebuild(L, li)
             for ci, s in enumerate(st):    # B4: down / SwiGLU / gate|up grads -> reduce-scatter
                 _wait(s["h"])
                 a, gq = s["layers"][li], s["gfull"]

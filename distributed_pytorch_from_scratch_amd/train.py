@@ -48,6 +48,7 @@ def get_train_args(argv=None) -> Namespace:
     g.add_argument("--tp_size", type=int, default=2)
     g.add_argument("--dp_size", type=int, default=1)
     g.add_argument("--sp", action="store_true", help="Megatron sequence parallelism")
+    g.add_argument("--recompute", action="store_true", help="activation recompute (layer inputs only)")
     g.add_argument("--master_addr", type=str, default="127.0.0.1")
     g.add_argument("--master_port", type=str, default="25555")
     g = p.add_argument_group("training")
@@ -94,7 +95,8 @@ def train(rank, args: Namespace):
     log0 = (lambda *a_: print(*a_, flush=True)) if grank == 0 else (lambda *a_: None)
     log0(f"{'Enable' if compute_dtype == torch.bfloat16 else 'Disable'} bf16 training  [{p}]")
 
-    margs = replace(get_preset(args.model), sequence_parallel=args.sp)
+    margs = replace(get_preset(args.model), sequence_parallel=args.sp,
+                    recompute=getattr(args, "recompute", False))
     model = Transformer.from_args(margs).to(dev)
     model.set_compute_dtype(compute_dtype)
     model.reset_parameters()

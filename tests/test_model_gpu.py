@@ -109,14 +109,16 @@ def test_fused_engine_matches_modular_path_and_chunks(dist1):
     tgt = torch.randint(0, args.vocab_size, (4, 128), device="cuda")
     pos = torch.arange(128, device="cuda").repeat(4, 1)
     res = {}
-    for mode in ("modular", "c1", "c2"):
+    for mode in ("modular", "c1", "c2", "c2rc"):
         m.zero_grad(set_to_none=True)
         m.use_fused_engine = mode != "modular"
-        m.chunks = 2 if mode == "c2" else 1
+        m.chunks = 2 if mode.startswith("c2") else 1
+        m.args.recompute = mode == "c2rc"     # activation recompute: same grads
         loss = m.loss(ids, pos, tgt)
         loss.backward()
         res[mode] = (loss.item(), {n: p.grad.clone() for n, p in m.named_parameters()})
-    for mode in ("c1", "c2"):
+    m.args.recompute = False
+    for mode in ("c1", "c2", "c2rc"):
         assert abs(res[mode][0] - res["modular"][0]) < 1e-3
         for n, g in res["modular"][1].items():
             rel = ((res[mode][1][n] - g).norm() / (g.norm() + 1e-12)).item()

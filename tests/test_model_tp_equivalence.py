@@ -106,6 +106,17 @@ def test_sequence_parallel_matches(world, fused):
             assert torch.equal(res[r][1][key], res[0][1][key]), key
 
 
+@pytest.mark.parametrize("world,sp", [(1, False), (2, False), (2, True)])
+def test_activation_recompute_matches(world, sp):
+    """ModelArgs.recompute: the engines keep only each layer's input and re-run the layer
+    forward (collectives included) in backward -- same trajectory as the vanilla model."""
+    cfg = dict(CFG, recompute=True)
+    van, _ = _train_vanilla(CFG, 3)
+    res = run_distributed(_train_parallel, world, cfg, 3, sp, True, True)
+    for r in range(world):
+        assert torch.allclose(torch.tensor(res[r][0]), torch.tensor(van), atol=2e-5), (res[r][0], van)
+
+
 def test_state_dict_layout_is_reference_layout():
     cfg = dict(CFG)
     res = run_distributed(_train_parallel, 2, cfg, 1, False, True)

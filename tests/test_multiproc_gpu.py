@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 STEPS = 3
 
 
-def _train(rank, world, tp, dp, heads, dev="cuda", sp=False):
+def _train(rank, world, tp, dp, heads, dev="cuda", sp=False, recompute=False):
     import torch.distributed as dist
     if dev == "cuda":
         torch.cuda.set_device(0)
@@ -26,7 +26,7 @@ def _train(rank, world, tp, dp, heads, dev="cuda", sp=False):
     from distributed_pytorch_from_scratch_amd.parallel import process_manager as pm
     from distributed_pytorch_from_scratch_amd.utils.dist import set_seed
     args = get_preset("gpt2-small", num_layers=2, num_heads=heads, vocab_size=1000, vocab_pad_to=1,
-                      sequence_parallel=sp)
+                      sequence_parallel=sp, recompute=recompute)
     m = Transformer.from_args(args).to(dev)
     set_seed(0)
     m.reset_parameters()

@@ -85,21 +85,23 @@ def test_xgmi_collectives_match_fp32_sums(world):
                 assert torch.equal(got[0], torch.cat(xs)), (op, n, r)
 
 
-def _engine(rank, world, heads, sp):
+def _engine(rank, world, heads, sp, recompute=False):
     from test_multiproc_gpu import _train
-    return _train(rank, world, world, 1, heads, "cuda", sp)
+    return _train(rank, world, world, 1, heads, "cuda", sp, recompute)
 
 
-@pytest.mark.parametrize("world,sp", [(2, False), (2, True), (4, True)])
-def test_engine_over_xgmi_follows_single_rank(monkeypatch, world, sp):
+@pytest.mark.parametrize("world,sp,rc", [(2, False, False), (2, True, False), (4, True, False),
+                                         (2, False, True), (2, True, True)])
+def test_engine_over_xgmi_follows_single_rank(monkeypatch, world, sp, rc):
     """The fused engines with their TP collectives on the xGMI kernels (all-reduce; or
     reduce-scatter / all-gather under sequence parallelism) track the single-rank trajectory
-    (same check as test_multiproc_gpu)."""
+    (same check as test_multiproc_gpu); ``rc``: with activation recompute, whose rebuilt
+    forward issues its own collectives between the backward's (staging-slot reuse)."""
     from test_multiproc_gpu import _ref
     heads = 12
     ref = _ref(heads)
     monkeypatch.setenv("DPFS_TP_COMM", "xgmi")
-    res = run_distributed(_engine, world, heads, sp, tp_size=world)
+    res = run_distributed(_engine, world, heads, sp, rc, tp_size=world)
     for r, losses in res.items():
         for a, b in zip(losses, ref):
             assert abs(a - b) < 2e-2 * max(1.0, abs(b)), (r, losses, ref)

@@ -71,9 +71,11 @@ def main():
     pos = torch.arange(T, device=dev).unsqueeze(0).expand(B, T).contiguous()
     res = {}
     for cfg in a.configs.split(","):
-        sp, c = cfg.split(":")
+        sp, c, *rest = cfg.split(":")       # sp:2 or sp:2:rc (activation recompute)
         model.args.sequence_parallel = step.sp = sp == "sp"
+        model.args.recompute = "rc" in rest
         model.chunks = int(c)
+        torch.cuda.reset_peak_memory_stats()
         for _ in range(2):
             step(ids[:, :-1], pos, ids[:, 1:])
         torch.cuda.synchronize()
@@ -83,7 +85,8 @@ def main():
         torch.cuda.synchronize()
         res[cfg] = round(1000 * (time.perf_counter() - t0) / a.steps, 2)
         print(json.dumps({"tp": n, "rank": a.rank, "config": cfg, "ms_per_step": res[cfg],
-                          "tokens": B * T}), flush=True)
+                          "tokens": B * T,
+                          "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2)}), flush=True)
 
 
 if __name__ == "__main__":
