@@ -58,7 +58,7 @@ def _slot(ci: int, rows: int, cols: int, dt):
     """Staging buffer (xGMI communicator slot of chunk ``ci``) for a GEMM output that is
     all-reduced in place next (no copy-in); None -> the GEMM allocates.  The reduced tensor
     stays in the slot until the chunk's next staged GEMM, which comes after its consumers."""
-    return tp_comm.staging(ci, (rows, cols), dt)
+    return tp_comm.staging(ci, (rows, cols), dt, "all_reduce")
 
 
 def _wait(h):

@@ -49,7 +49,7 @@ def _rs(full: torch.Tensor, n: int):
 def _slot(ci: int, rows: int, cols: int, dt):
     """Staging buffer (xGMI communicator slot of chunk ``ci``) for a GEMM output that feeds a
     reduce-scatter, so the collective reads it in place; None -> the GEMM allocates."""
-    return tp_comm.staging(ci, (rows, cols), dt)
+    return tp_comm.staging(ci, (rows, cols), dt, "reduce_scatter")
 
 
 def _ag(part: torch.Tensor, n: int):

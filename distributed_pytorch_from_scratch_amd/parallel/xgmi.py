@@ -27,6 +27,7 @@ import torch.distributed as dist
 from ..ops import _ext
 
 _ALL_REDUCE, _REDUCE_SCATTER, _ALL_GATHER = 0, 1, 2
+_NAMES = ("all_reduce", "reduce_scatter", "all_gather")
 
 
 class _Work:
@@ -66,6 +67,9 @@ class XgmiComm:
         C.xgmi_open(self.h, b"".join(handles))
         blocks = blocks or int(os.environ.get("DPFS_XGMI_BLOCKS", "32"))
         C.xgmi_set_blocks(self.h, blocks)
+        self._blocks = blocks
+        # per-op grid width (tp_comm picks one per op); None = the communicator default
+        self.op_blocks = {"all_reduce": None, "reduce_scatter": None, "all_gather": None}
         # High-priority side stream: a collective that overlaps compute is the critical path
         # of the other chunk, so its (narrow) kernel should win the CU arbitration.
         self.stream = torch.cuda.Stream(priority=-1)
@@ -99,6 +103,9 @@ class XgmiComm:
 
     def _launch(self, op: int, x: torch.Tensor, out: torch.Tensor, timeout_s: Optional[float] = None,
                 slot: int = -1):
+        nb = self.op_blocks[_NAMES[op]]
+        if nb is not None and nb != self._blocks:   # same call sequence on every rank
+            self.set_blocks(nb)
         cur = torch.cuda.current_stream()
         self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):
@@ -137,21 +144,23 @@ class XgmiComm:
             return None
         return work
 
-    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = True):
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = True,
+                       timeout_s: Optional[float] = None):
         """out = (sum over ranks of inp)[rank-th of W equal slices] (same contract as
         ``dist.reduce_scatter_tensor``)."""
         assert inp.numel() == out.numel() * self.world and inp.numel() * inp.element_size() <= self.cap
         inp = inp.contiguous()
-        work = self._launch(_REDUCE_SCATTER, inp, out, slot=self._slot_of(inp))
+        work = self._launch(_REDUCE_SCATTER, inp, out, timeout_s, slot=self._slot_of(inp))
         if not async_op:
             work.wait()
             return None
         return work
 
-    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = True):
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = True,
+                   timeout_s: Optional[float] = None):
         """out = concat over ranks of inp (same contract as ``dist.all_gather_into_tensor``)."""
         assert out.numel() == inp.numel() * self.world and inp.numel() * inp.element_size() <= self.cap
-        work = self._launch(_ALL_GATHER, inp.contiguous(), out)
+        work = self._launch(_ALL_GATHER, inp.contiguous(), out, timeout_s)
         if not async_op:
             work.wait()
             return None
@@ -160,6 +169,7 @@ class XgmiComm:
     def set_blocks(self, blocks: int):
         """Workgroups per collective launch (must be equal on every rank of the group)."""
         self.C.xgmi_set_blocks(self.h, int(blocks))
+        self._blocks = int(blocks)
 
     # --------------------------------------------------------------------- health ----
     def error(self) -> int:
