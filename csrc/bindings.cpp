@@ -487,7 +487,7 @@ void attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tenso
     rp = rope_pos->data_ptr<int64_t>();
     rt = rope_tab->data_ptr<float>();
   }
-  auto delta = torch::empty({B, H, T}, lse.options());
+  auto delta = torch::empty({2, B, H, T}, lse.options());   // -delta | -lse/scale
   dpfs_attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
                 delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), (int)B, (int)T, (int)H, (int)hd,
                 vdo.ld, vq.ld, vk.ld, vv.ld, vo.ld, vdq.ld, vdk.ld, vdv.ld, (float)scale, causal ? 1 : 0, rp, rt, stream());

@@ -630,7 +630,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv_k(const 
               if (qi >= T || ki >= T || (causal && ki > qi)) p = 0.f;
             }
             s[kt][qt][j] = p;
-            dp[kt][qt][j] = p * (dp[kt][qt][j] - dsv[j]);
+            dp[kt][qt][j] = p * (dp[kt][qt][j] + dsv[j]);   // DELTA holds -delta
           }
         }
       }
@@ -745,6 +745,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv2_k(
     const float* __restrict__ LSE, const float* __restrict__ DELTA, bf16* __restrict__ dK, bf16* __restrict__ dV,
     int T, int H, long long ldq, long long ldk, long long ldv, long long lddo, long long lddk, long long lddv,
     float scale, int causal, const int64_t* __restrict__ rpos, const float* __restrict__ rtab) {
+  // LSE here = -lse/scale and DELTA = -delta per query row (written by attn_bwd_dq_k).
   constexpr int BKV = 64, BQ = 64, KT = HD / 32, DT = HD / 16;
   constexpr int TILE = BQ * HD * 2;
   constexpr int BUF = 2 * TILE + 1024;        // Q, dO, lse, delta, dummy slot (1 KiB aligned stages)
@@ -811,11 +812,14 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv2_k(
     if (t + 2 < nq) qdo_dma<HD>(rq, rdo, rl, rd, smem + nb * BUF, qq0 + 2 * BQ, T, ldq, lddo);
     const bool wave_active = !causal || (qq0 + BQ - 1 >= wk0);
     if (!wave_active) continue;
+    // Row constants as the initial accumulators (rows = queries 16qt + 4g + j): S' = QK^T -
+    // lse/scale and dP' = dO V^T - delta, so p = exp2(c2 S') and dS = p dP' need no per-element
+    // subtraction (the dQ kernel wrote -lse/scale and -delta).
     f32x4 s[4], dp[4];
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
-      s[qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      dp[qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      s[qt] = *reinterpret_cast<const f32x4*>(ls + 16 * qt + 4 * g);
+      dp[qt] = *reinterpret_cast<const f32x4*>(ds + 16 * qt + 4 * g);
 #pragma unroll
       for (int kk = 0; kk < KT; ++kk) {
         s[qt] = MFMA(row_frag<HD>(lq, 16 * qt, 32 * kk), kf[kk], s[qt]);
@@ -837,17 +841,15 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv2_k(
     const bool need_mask = (causal && wk0 + 15 > qq0) || (qq0 + BQ > T) || (wk0 + 16 > T);
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
-      const f32x4 lsv = *reinterpret_cast<const f32x4*>(ls + 16 * qt + 4 * g);
-      const f32x4 dsv = *reinterpret_cast<const f32x4*>(ds + 16 * qt + 4 * g);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float p = __builtin_amdgcn_exp2f(fmaf(s[qt][j], c2, -lsv[j] * kLog2e));
+        float p = __builtin_amdgcn_exp2f(s[qt][j] * c2);
         if (need_mask) {
           const int qi = qq0 + 16 * qt + 4 * g + j;
           if (qi >= T || ki >= T || (causal && ki > qi)) p = 0.f;
         }
         s[qt][j] = p;
-        dp[qt][j] = p * (dp[qt][j] - dsv[j]);
+        dp[qt][j] = p * dp[qt][j];
       }
     }
     bf16x8 pa[2], da[2];
@@ -916,7 +918,8 @@ template <int HD>
 __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                         const bf16* __restrict__ V, const bf16* __restrict__ dO,
                                                         const bf16* __restrict__ Og, const float* __restrict__ LSE,
-                                                        float* __restrict__ DELTA_OUT, bf16* __restrict__ dQ, int T,
+                                                        float* __restrict__ DELTA_OUT, float* __restrict__ LSN_OUT,
+                                                        bf16* __restrict__ dQ, int T,
                                                         int H, long long ldq, long long ldk, long long ldv,
                                                         long long lddo, long long ldo, long long lddq, float scale,
                                                         int causal, const int64_t* __restrict__ rpos,
@@ -950,7 +953,8 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
       qf[c][kk] = a;
       dof[c][kk] = d;
     }
-    lse2[c] = qi < T ? LSE[((long long)b * H + h) * T + qi] * kLog2e : 0.f;
+    lse2[c] = qi < T ? -LSE[((long long)b * H + h) * T + qi] / scale : 0.f;   // S' = S - lse/scale
+    if (g == 0 && qi < T) LSN_OUT[((long long)b * H + h) * T + qi] = lse2[c];
     // delta = rowsum(dO * O), fused here (written for the dK/dV kernel that runs next).
     float dsum = 0.f;
     if (qi < T) {
@@ -964,8 +968,8 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
     }
     dsum += __shfl_xor(dsum, 16, 64);
     dsum += __shfl_xor(dsum, 32, 64);
-    del[c] = dsum;
-    if (g == 0 && qi < T) DELTA_OUT[((long long)b * H + h) * T + qi] = dsum;
+    del[c] = -dsum;                                                             // dP' = dP - delta
+    if (g == 0 && qi < T) DELTA_OUT[((long long)b * H + h) * T + qi] = -dsum;
   }
   f32x4 dq[2][DT];
 #pragma unroll
@@ -999,9 +1003,9 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          s[i][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
-          dp[i][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int c = 0; c < 2; ++c) {   // row constants as initial accumulators (cols = queries)
+          s[i][c] = (f32x4){lse2[c], lse2[c], lse2[c], lse2[c]};
+          dp[i][c] = (f32x4){del[c], del[c], del[c], del[c]};
         }
 #pragma unroll
         for (int kk = 0; kk < KT; ++kk) {
@@ -1022,12 +1026,12 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            float p = __builtin_amdgcn_exp2f(fmaf(s[i][c][j], c2, -lse2[c]));
+            float p = __builtin_amdgcn_exp2f(s[i][c][j] * c2);
             if (need_mask) {
               const int ki = kv0 + 16 * i + 4 * g + j;
               if (ki >= T || (causal && ki > qi)) p = 0.f;
             }
-            s[i][c][j] = p * (dp[i][c][j] - del[c]);  // dS^T
+            s[i][c][j] = p * dp[i][c][j];  // dS^T
           }
       }
       // dQ^T[d][q] += K^T[d][k] dS^T[k][q]
@@ -1118,7 +1122,7 @@ extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void*
                                                             lse, T, H, ldq, ldk, ldv, ldo, scale, causal));
 }
 
-// delta: workspace [B, H, T] fp32.
+// delta: workspace [2][B, H, T] fp32: -delta (rowsum(dO*O)) and -lse/scale, written by the dQ kernel.
 extern "C" void dpfs_attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o,
                               const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int T, int H,
                               int hd, long long lddo, long long ldq, long long ldk, long long ldv, long long ldo,
@@ -1126,7 +1130,8 @@ extern "C" void dpfs_attn_bwd(const void* dout, const void* q, const void* k, co
                               const int64_t* rope_pos, const float* rope_tab, hipStream_t s) {
   dim3 gq((T + 127) / 128, B * H);
   DPFS_HD_DISPATCH(hd, attn_bwd_dq_k<HD_><<<gq, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
-                                                             (const bf16*)dout, (const bf16*)o, lse, delta, (bf16*)dq,
+                                                             (const bf16*)dout, (const bf16*)o, lse, delta,
+                                                             delta + (long long)B * H * T, (bf16*)dq,
                                                              T, H, ldq, ldk, ldv, lddo, ldo, lddq, scale, causal,
                                                              rope_pos, rope_tab));
   if (g_attn_bwd_impl == 3 && hd <= 64) {
@@ -1144,7 +1149,8 @@ extern "C" void dpfs_attn_bwd(const void* dout, const void* q, const void* k, co
   dim3 gk((T + 63) / 64, B * H);
   if (g_attn_bwd_impl == 2) {
     DPFS_HD_DISPATCH(hd, attn_bwd_dkdv2_k<HD_><<<gk, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
-                                                                  (const bf16*)dout, lse, delta, (bf16*)dk,
+                                                                  (const bf16*)dout, delta + (long long)B * H * T,
+                                                                  delta, (bf16*)dk,
                                                                   (bf16*)dv, T, H, ldq, ldk, ldv, lddo, lddk, lddv,
                                                                   scale, causal, rope_pos, rope_tab));
     return;
