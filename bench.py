@@ -220,6 +220,10 @@ def main():
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
+        if os.environ.get("DPFS_SHOW_GEMM") == "1":     # per-shape ours/hipBLASLt choices (ms)
+            from distributed_pytorch_from_scratch_amd.ops import gemm_select
+            for key, v in sorted(gemm_select.choices(with_times=True).items(), key=str):
+                print(f"[gemm] {key} -> {v}", file=sys.stderr, flush=True)
         if os.environ.get("DPFS_BENCH_VERBOSE"):
             from distributed_pytorch_from_scratch_amd.ops import gemm_select
             for key, c in sorted(gemm_select.choices().items(), key=str):

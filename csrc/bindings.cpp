@@ -84,6 +84,19 @@ int dpfs_xgmi_error(void*);
 void dpfs_xgmi_clear_error(void*);
 int dpfs_xgmi_run(void*, int, int, const void*, void*, long long, long long, double, int, hipStream_t);
 void dpfs_xgmi_destroy(void*);
+// comm/rccl_comm.hip
+const char* dpfs_rccl_last_error();
+int dpfs_rccl_id_bytes();
+int dpfs_rccl_unique_id(void*);
+int dpfs_rccl_init(const void*, int, int, void**);
+int dpfs_rccl_destroy(void*);
+int dpfs_rccl_async_error(void*);
+int dpfs_rccl_all_reduce(void*, const void*, void*, size_t, int, int, hipStream_t);
+int dpfs_rccl_reduce_scatter(void*, const void*, void*, size_t, int, int, hipStream_t);
+int dpfs_rccl_all_gather(void*, const void*, void*, size_t, int, hipStream_t);
+int dpfs_rccl_broadcast(void*, const void*, void*, size_t, int, int, hipStream_t);
+int dpfs_rccl_group_start();
+int dpfs_rccl_group_end();
 }
 
 namespace {
@@ -757,6 +770,84 @@ void xgmi_run(int64_t h, int64_t op, torch::Tensor x, torch::Tensor out, int64_t
               "xgmi_run failed: ", dpfs_xgmi_last_error());
 }
 
+// ------------------------------------------------------- native RCCL communicator (comm/) --
+void* rccl_ptr(int64_t h) {
+  TORCH_CHECK(h != 0, "rccl: null communicator");
+  return reinterpret_cast<void*>(h);
+}
+
+int rccl_dtype(const torch::Tensor& t) {   // ncclDataType_t values (rccl.h)
+  switch (t.scalar_type()) {
+    case torch::kBFloat16: return 9;
+    case torch::kFloat32: return 7;
+    case torch::kFloat16: return 6;
+    case torch::kFloat64: return 8;
+    case torch::kInt64: return 4;
+    case torch::kInt32: return 2;
+    case torch::kUInt8: return 1;
+    default: TORCH_CHECK(false, "rccl: unsupported dtype ", t.scalar_type());
+  }
+  return -1;
+}
+
+void rccl_check(int rc, const char* what) { TORCH_CHECK(rc == 0, what, " failed: ", dpfs_rccl_last_error()); }
+
+py::bytes rccl_unique_id() {
+  std::string b((size_t)dpfs_rccl_id_bytes(), '\0');
+  rccl_check(dpfs_rccl_unique_id(&b[0]), "ncclGetUniqueId");
+  return py::bytes(b);
+}
+
+int64_t rccl_init(py::bytes id, int64_t nranks, int64_t rank) {
+  std::string b = id;
+  TORCH_CHECK((int)b.size() == dpfs_rccl_id_bytes(), "rccl_init: unique id size");
+  void* c = nullptr;
+  {
+    py::gil_scoped_release nogil;   // blocks until every rank has joined
+    rccl_check(dpfs_rccl_init(b.data(), (int)nranks, (int)rank, &c), "ncclCommInitRank");
+  }
+  return reinterpret_cast<int64_t>(c);
+}
+
+// Collectives on the CURRENT HIP stream (the Python side selects its side stream).
+void rccl_all_reduce(int64_t h, torch::Tensor x, torch::Tensor out, int64_t op) {
+  check_cuda(x, "x");
+  check_cuda(out, "out");
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && x.numel() == out.numel() &&
+                  x.scalar_type() == out.scalar_type(), "rccl all_reduce: contiguous, same size and dtype");
+  const at::DeviceGuard g(x.device());
+  rccl_check(dpfs_rccl_all_reduce(rccl_ptr(h), x.data_ptr(), out.data_ptr(), (size_t)x.numel(), rccl_dtype(x),
+                                  (int)op, stream()), "ncclAllReduce");
+}
+
+void rccl_reduce_scatter(int64_t h, torch::Tensor out, torch::Tensor x, int64_t world, int64_t op) {
+  check_cuda(x, "x");
+  check_cuda(out, "out");
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && out.numel() * world == x.numel() &&
+                  x.scalar_type() == out.scalar_type(), "rccl reduce_scatter: out = in / world elements");
+  const at::DeviceGuard g(x.device());
+  rccl_check(dpfs_rccl_reduce_scatter(rccl_ptr(h), x.data_ptr(), out.data_ptr(), (size_t)out.numel(), rccl_dtype(x),
+                                      (int)op, stream()), "ncclReduceScatter");
+}
+
+void rccl_all_gather(int64_t h, torch::Tensor out, torch::Tensor x, int64_t world) {
+  check_cuda(x, "x");
+  check_cuda(out, "out");
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && x.numel() * world == out.numel() &&
+                  x.scalar_type() == out.scalar_type(), "rccl all_gather: out = world x in elements");
+  const at::DeviceGuard g(x.device());
+  rccl_check(dpfs_rccl_all_gather(rccl_ptr(h), x.data_ptr(), out.data_ptr(), (size_t)x.numel(), rccl_dtype(x),
+                                  stream()), "ncclAllGather");
+}
+
+void rccl_broadcast(int64_t h, torch::Tensor t, int64_t root) {
+  check_cuda(t, "t");
+  TORCH_CHECK(t.is_contiguous(), "rccl broadcast: contiguous tensor");
+  const at::DeviceGuard g(t.device());
+  rccl_check(dpfs_rccl_broadcast(rccl_ptr(h), t.data_ptr(), t.data_ptr(), (size_t)t.numel(), rccl_dtype(t),
+                                 (int)root, stream()), "ncclBroadcast");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -814,4 +905,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xgmi_error", [](int64_t h) { return dpfs_xgmi_error(xgmi_ptr(h)); });
   m.def("xgmi_clear_error", [](int64_t h) { dpfs_xgmi_clear_error(xgmi_ptr(h)); });
   m.def("xgmi_destroy", [](int64_t h) { dpfs_xgmi_destroy(xgmi_ptr(h)); });
+  m.def("rccl_unique_id", &rccl_unique_id, "ncclGetUniqueId -> bytes");
+  m.def("rccl_init", &rccl_init, py::arg("id"), py::arg("nranks"), py::arg("rank"),
+        "ncclCommInitRank on the current device -> communicator handle");
+  m.def("rccl_all_reduce", &rccl_all_reduce, py::arg("h"), py::arg("x"), py::arg("out"), py::arg("op") = 0);
+  m.def("rccl_reduce_scatter", &rccl_reduce_scatter, py::arg("h"), py::arg("out"), py::arg("x"), py::arg("world"),
+        py::arg("op") = 0);
+  m.def("rccl_all_gather", &rccl_all_gather, py::arg("h"), py::arg("out"), py::arg("x"), py::arg("world"));
+  m.def("rccl_broadcast", &rccl_broadcast, py::arg("h"), py::arg("t"), py::arg("root"));
+  m.def("rccl_group_start", []() { TORCH_CHECK(dpfs_rccl_group_start() == 0, "ncclGroupStart"); });
+  m.def("rccl_group_end", []() { rccl_check(dpfs_rccl_group_end(), "ncclGroupEnd"); });
+  m.def("rccl_async_error", [](int64_t h) {
+    return dpfs_rccl_async_error(rccl_ptr(h)) == 0 ? std::string() : std::string(dpfs_rccl_last_error());
+  });
+  m.def("rccl_destroy", [](int64_t h) { rccl_check(dpfs_rccl_destroy(rccl_ptr(h)), "ncclCommDestroy"); });
 }

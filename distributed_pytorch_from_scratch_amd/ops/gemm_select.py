@@ -23,13 +23,16 @@ from . import reference
 from .dispatch import shadow
 
 _choice: Dict[Tuple, str] = {}
+_times: Dict[Tuple, Tuple[float, float]] = {}   # key -> (ours ms, hipBLASLt ms) at selection
 
 
 def mode() -> str:
     return os.environ.get("DPFS_GEMM_BACKEND", "auto")
 
 
-def choices() -> Dict[Tuple, str]:
+def choices(with_times: bool = False) -> Dict[Tuple, object]:
+    if with_times:
+        return {k: (c,) + tuple(round(t, 4) for t in _times.get(k, ())) for k, c in _choice.items()}
     return dict(_choice)
 
 
@@ -52,6 +55,7 @@ def _pick(key: Tuple, ours: Callable, blas: Callable) -> str:
         t_b = min(_ms(blas), _ms(blas))
         c = "blas" if t_b < 0.97 * t_o else "ours"
         _choice[key] = c
+        _times[key] = (t_o, t_b)
     return c
 
 

@@ -1,18 +1,22 @@
-"""Transport of the tensor-parallel collectives: RCCL or xGMI peer memory.
+"""Transport of the tensor-parallel collectives: RCCL (two ways) or xGMI peer memory.
 
-``DPFS_TP_COMM`` = ``auto`` (default) | ``rccl`` | ``xgmi``.
+``DPFS_TP_COMM`` = ``auto`` (default) | ``rccl`` | ``native`` | ``xgmi``.
 
-* ``rccl``: ``torch.distributed`` on the TP group (``nccl`` backend = RCCL on ROCm).
+* ``rccl``: ``torch.distributed`` on the TP group (ProcessGroupNCCL; ``nccl`` = RCCL on ROCm).
+* ``native``: :class:`~.rccl.RcclComm`, the RCCL C API on our own side stream.
 * ``xgmi``: :class:`~.xgmi.XgmiComm` (hand-written peer-memory kernels, all links at once).
 * ``auto``: on the first TP collective of the process, every TP rank builds the xGMI
   communicator and, for each of all-reduce, reduce-scatter and all-gather separately, checks
-  its result against RCCL on a rank-dependent tensor of the live message size and times both
-  (xGMI at several grid widths); an op goes to xGMI only if it was correct on every rank and
-  faster (max over ranks).  Every rank reaches the same decisions (they are computed from
-  all-reduced numbers), so the call sequence stays identical across the group.
+  its results against an fp32 ProcessGroupNCCL sum on a rank-dependent tensor of the live
+  message size and times both (xGMI at several grid widths).  An op leaves ProcessGroupNCCL
+  only if xGMI was correct on every rank and at least 3 % faster (max over ranks).  Every
+  rank reaches the same decisions (they are computed from all-reduced numbers), so the call
+  sequence stays identical across the group.  (``native`` runs the same RCCL kernels as
+  ProcessGroupNCCL, so ``auto`` does not open a second RCCL communicator: two communicators
+  with kernels in flight at once are only safe while the GPU can hold both.)
 
 Only the TP group's activation / activation-gradient collectives go through here; DP gradient
-buckets, the CE statistics gather and init broadcasts stay on RCCL.
+buckets, the CE statistics gather and init broadcasts stay on ProcessGroupNCCL.
 """
 from __future__ import annotations
 
@@ -26,13 +30,15 @@ import torch.distributed as dist
 
 from . import process_manager as pm
 
+_OPS = ("all_reduce", "reduce_scatter", "all_gather")
+_GRIDS = (8, 16, 32, 64)
 _decisions: Dict[int, Optional["_Choice"]] = {}   # id(tp_group) -> per-op transport (None = RCCL)
 _info: Dict[int, dict] = {}
 
 
 def mode() -> str:
     m = os.environ.get("DPFS_TP_COMM", "auto")
-    assert m in ("auto", "rccl", "xgmi"), f"DPFS_TP_COMM={m!r}: expected auto | rccl | xgmi"
+    assert m in ("auto", "rccl", "native", "xgmi"), f"DPFS_TP_COMM={m!r}: expected auto | rccl | native | xgmi"
     return m
 
 
@@ -46,33 +52,58 @@ def _time_ms(fn, reps: int = 5) -> float:
     return 1000 * (time.perf_counter() - t0) / reps
 
 
-_OPS = ("all_reduce", "reduce_scatter", "all_gather")
-_GRIDS = (8, 16, 32, 64)
-
-
 class _Choice:
-    """The group's communicator and which ops run on it (the rest stay on RCCL)."""
+    """The group's communicators and which transport each op uses ("rccl" = ProcessGroupNCCL)."""
 
-    def __init__(self, comm, use: Dict[str, bool]):
-        self.comm, self.use = comm, use
+    def __init__(self, xgmi, native, use: Dict[str, str]):
+        self.xgmi, self.native, self.use = xgmi, native, use
+
+    def comm(self, op: str):
+        u = self.use[op]
+        return self.xgmi if u == "xgmi" else self.native if u == "native" else None
 
 
-def _xgmi_op(comm, op: str, x: torch.Tensor, part: torch.Tensor, gathered: torch.Tensor, timeout_s=None):
+def _run_op(comm, op: str, x, part, gathered, timeout_s=None):
+    """One blocking collective on ``comm`` (XgmiComm / RcclComm) or, for comm = (None, group),
+    on ProcessGroupNCCL."""
+    if isinstance(comm, tuple):
+        g = comm[1]
+        if op == "all_reduce":
+            dist.all_reduce(x, group=g)
+        elif op == "reduce_scatter":
+            dist.reduce_scatter_tensor(part, x, group=g)
+        else:
+            dist.all_gather_into_tensor(gathered, part, group=g)
+        return
+    kw = {} if timeout_s is None else {"timeout_s": timeout_s}
     if op == "all_reduce":
-        comm.all_reduce(x, async_op=False, timeout_s=timeout_s)
+        comm.all_reduce(x, async_op=False, **kw)
     elif op == "reduce_scatter":
-        comm.reduce_scatter(part, x, async_op=False, timeout_s=timeout_s)
+        comm.reduce_scatter(part, x, async_op=False, **kw)
     else:
-        comm.all_gather(gathered, part, async_op=False, timeout_s=timeout_s)
+        comm.all_gather(gathered, part, async_op=False, **kw)
 
 
-def _rccl_op(op: str, g, x, part, gathered):
-    if op == "all_reduce":
-        dist.all_reduce(x, group=g)
-    elif op == "reduce_scatter":
-        dist.reduce_scatter_tensor(part, x, group=g)
-    else:
-        dist.all_gather_into_tensor(gathered, part, group=g)
+def _build(kind: str, g, forced: bool):
+    """Communicator of ``kind`` on every rank of g, or None on every rank if any rank failed."""
+    ok = torch.ones(1, device="cuda")
+    comm, why = None, ""
+    try:
+        if kind == "xgmi":
+            from .xgmi import XgmiComm
+            comm = XgmiComm(g)
+        else:
+            from .rccl import RcclComm
+            comm = RcclComm(g)
+    except Exception as e:   # IPC / RCCL unavailable: the whole group does without it
+        ok.zero_()
+        why = f"setup failed: {e}"
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=g)
+    if ok.item() == 0:
+        if forced:
+            raise RuntimeError(f"DPFS_TP_COMM={kind} but the communicator could not be built ({why})")
+        return None
+    return comm
 
 
 def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
@@ -80,24 +111,18 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
     backend = dist.get_backend(p.tp_group)
     if m == "rccl" or not t.is_cuda or (m == "auto" and backend != "nccl"):
         return None
-    from .xgmi import XgmiComm
     g = p.tp_group
     W, r = p.tp_size, p.tp_rank
-    ok = torch.ones(1, device=t.device)
-    comm, why = None, ""
-    try:
-        comm = XgmiComm(g)
-    except Exception as e:   # IPC unavailable etc.: the whole group falls back together
-        ok.zero_()
-        why = f"setup failed: {e}"
-    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=g)
-    if ok.item() == 0:
-        if m == "xgmi":
-            raise RuntimeError(f"DPFS_TP_COMM=xgmi but the xGMI communicator could not be built ({why})")
+    kinds = [m] if m != "auto" else ["xgmi"]
+    comms = {k: _build(k, g, forced=m != "auto") for k in kinds}
+    comms = {k: c for k, c in comms.items() if c is not None}
+    if not comms:
         return None
     # Correctness of every op on a rank-dependent tensor of the live size, against fp32 sums
-    # (RCCL / gloo all-reduce only: the all-gather oracle is a zero-padded sum, exact).
-    n = min(t.numel(), comm._max_elems(t))
+    # (ProcessGroup all-reduce only: the all-gather oracle is a zero-padded sum, exact).
+    n = t.numel()
+    if "xgmi" in comms:
+        n = min(n, comms["xgmi"]._max_elems(t))
     n = max(8 * W, n - n % (8 * W))
     gen = torch.Generator(device=t.device).manual_seed(4321 + r)
     x = torch.randn(n, generator=gen, device=t.device).to(t.dtype)
@@ -108,51 +133,80 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
     pad[r] = mine.float()
     dist.all_reduce(pad, group=g)
     tol = 1e-2 * max(1.0, ref.abs().max().item())
-    y, part, gathered = x.clone(), torch.empty_like(mine), torch.empty_like(x)
-    _xgmi_op(comm, "all_reduce", y, None, None, 30.0)
-    _xgmi_op(comm, "reduce_scatter", x, part, None, 30.0)
-    _xgmi_op(comm, "all_gather", None, mine, gathered, 30.0)
-    torch.cuda.synchronize()
-    errs = [(y.float() - ref).abs().max().item(), (part.float() - ref.view(W, -1)[r]).abs().max().item(),
-            (gathered.float() - pad.view(-1)).abs().max().item()]
-    good = [comm.error() == 0 and errs[0] <= tol, comm.error() == 0 and errs[1] <= tol,
-            comm.error() == 0 and errs[2] == 0.0]
-    # Workgroups per call (1024 threads each): every CU that holds one cannot also hold a
-    # 2-wave-per-SIMD GEMM block (~250 VGPRs per wave), so a collective must stay narrow to
-    # overlap compute (as RCCL's few channels do).  Per op, take the narrowest grid within
-    # 10 % of the fastest one measured in isolation.
+    kl = sorted(comms)
+    bad = torch.zeros(len(kl), 3, device=t.device)
+    errs = {}
+    for a, k in enumerate(kl):
+        c = comms[k]
+        y, part, gathered = x.clone(), torch.empty_like(mine), torch.empty_like(x)
+        to = 30.0 if k == "xgmi" else None
+        _run_op(c, "all_reduce", y, None, None, to)
+        _run_op(c, "reduce_scatter", x, part, None, to)
+        _run_op(c, "all_gather", None, mine, gathered, to)
+        torch.cuda.synchronize()
+        e = [(y.float() - ref).abs().max().item(), (part.float() - ref.view(W, -1)[r]).abs().max().item(),
+             (gathered.float() - pad.view(-1)).abs().max().item()]
+        timed_out = k == "xgmi" and c.error() != 0
+        errs[k] = e
+        for i in range(3):
+            good = not timed_out and (e[i] <= tol if i < 2 else e[i] == 0.0)
+            bad[a, i] = 0.0 if good else 1.0
+    dist.all_reduce(bad, op=dist.ReduceOp.MAX, group=g)
+    if m != "auto" and bad.sum().item() > 0:
+        raise RuntimeError(f"DPFS_TP_COMM={m}: collectives failed validation (max errors {errs[m]})")
+    # Timing (ProcessGroupNCCL backend only).  xGMI workgroups per call (1024 threads each):
+    # every CU that holds one cannot also hold a 2-wave-per-SIMD GEMM block, so per op take
+    # the narrowest grid within 10 % of the fastest one measured in isolation.
     G = len(_GRIDS)
-    stats = torch.zeros(3 + 3 + 3 * G, device=t.device)   # bad[3], rccl_ms[3], xgmi_ms[3][G]
-    for i in range(3):
-        stats[i] = 0.0 if good[i] else 1.0
-    timed = all(good) and m == "auto" and backend == "nccl"
+    cols = ["rccl"] + [k for k in kl if k != "xgmi"] + ([f"xgmi/{nb}" for nb in _GRIDS] if "xgmi" in comms else [])
+    times = torch.zeros(3, len(cols), device=t.device)
+    timed = m == "auto" and backend == "nccl"
     if timed:
-        a, ap, ag = t.detach().reshape(-1)[:n].clone(), torch.empty_like(mine), torch.empty_like(x)
+        a_, ap, ag = t.detach().reshape(-1)[:n].clone(), torch.empty_like(mine), torch.empty_like(x)
         for i, op in enumerate(_OPS):
-            for j, nb in enumerate(_GRIDS):
-                comm.set_blocks(nb)
-                stats[6 + i * G + j] = _time_ms(lambda: _xgmi_op(comm, op, a, ap, ag))
-            stats[3 + i] = _time_ms(lambda: _rccl_op(op, g, a, ap, ag))
-        comm.check()
-    dist.all_reduce(stats, op=dist.ReduceOp.MAX, group=g)
+            for j, col in enumerate(cols):
+                kind = col.split("/")[0]
+                if kind != "rccl" and bad[kl.index(kind), i] > 0:
+                    continue
+                if col == "rccl":
+                    c = (None, g)
+                else:
+                    c = comms[kind]
+                    if kind == "xgmi":
+                        c.set_blocks(int(col.split("/")[1]))
+                times[i, j] = _time_ms(lambda c=c, op=op: _run_op(c, op, a_, ap, ag))
+        if "xgmi" in comms:
+            comms["xgmi"].check()
+    dist.all_reduce(times, op=dist.ReduceOp.MAX, group=g)
     use, info = {}, dict(bytes=n * x.element_size())
     for i, op in enumerate(_OPS):
-        bad, t_r = stats[i].item() > 0, stats[3 + i].item()
-        times = stats[6 + i * G: 6 + (i + 1) * G].tolist()
-        best = min(j for j, tt in enumerate(times) if tt <= 1.1 * min(times)) if timed and not bad \
-            else _GRIDS.index(32)
-        t_x = times[best]
-        comm.op_blocks[op] = _GRIDS[best]
-        if m == "xgmi" and bad:
-            raise RuntimeError(f"xGMI {op} failed validation (max err {errs[i]:.3g}, timeout flag {comm.error()})")
-        use[op] = not bad and (m == "xgmi" or t_x < 0.97 * t_r)
-        info[op] = dict(transport="xgmi" if use[op] else "rccl", xgmi_ms=round(t_x, 3), rccl_ms=round(t_r, 3),
-                        xgmi_blocks=_GRIDS[best], valid=not bad)
-    info["transport"] = "/".join(f"{op}:{'xgmi' if use[op] else 'rccl'}" for op in _OPS)
+        row = times[i].tolist()
+        ok = {k: bad[a, i].item() == 0 for a, k in enumerate(kl)}
+        cand = {"rccl": row[0]}
+        if "native" in comms and ok["native"]:
+            cand["native"] = row[cols.index("native")]
+        if "xgmi" in comms:
+            xt = row[len(cols) - G:]
+            jx = min(j for j, tt in enumerate(xt) if tt <= 1.1 * min(xt)) if timed else _GRIDS.index(32)
+            comms["xgmi"].op_blocks[op] = _GRIDS[jx]
+            if ok["xgmi"]:
+                cand["xgmi"] = xt[jx]
+        if m != "auto":
+            choice = m
+        else:
+            fastest = min(cand, key=cand.get)
+            choice = fastest if fastest != "rccl" and cand[fastest] < 0.97 * cand["rccl"] else "rccl"
+        use[op] = choice
+        info[op] = dict(transport=choice, **{f"{k}_ms": round(v, 3) for k, v in cand.items()})
+        if "xgmi" in comms:
+            info[op]["xgmi_blocks"] = comms["xgmi"].op_blocks[op]
+    info["transport"] = "/".join(f"{op}:{use[op]}" for op in _OPS)
     _info[id(g)] = info
     if p.global_rank == 0 and os.environ.get("DPFS_QUIET", "0") != "1":
         print(f"[dpfs] TP collectives: {info}", file=sys.stderr, flush=True)
-    return _Choice(comm, use) if any(use.values()) else None
+    if all(u == "rccl" for u in use.values()):
+        return None
+    return _Choice(comms.get("xgmi"), comms.get("native"), use)
 
 
 def _comm(t: torch.Tensor, p, op: str):
@@ -162,12 +216,19 @@ def _comm(t: torch.Tensor, p, op: str):
     if key not in _decisions:
         _decisions[key] = _decide(t, p)
     ch = _decisions[key]
-    return ch.comm if ch is not None and ch.use[op] else None
+    return None if ch is None else ch.comm(op)
 
 
 def info() -> Optional[dict]:
     p = pm.pgm
     return None if p is None else _info.get(id(p.tp_group))
+
+
+def _fits(c, t: torch.Tensor, mult: int) -> bool:
+    """xGMI takes messages up to its buffer capacity, in 16-byte vectors; RCCL takes any."""
+    if not hasattr(c, "cap"):
+        return True
+    return t.numel() * t.element_size() <= c.cap and t.numel() % mult == 0
 
 
 def all_reduce(t: torch.Tensor, async_op: bool = True):
@@ -188,7 +249,7 @@ def reduce_scatter(out: torch.Tensor, inp: torch.Tensor, async_op: bool = True):
         out.copy_(inp.view_as(out))
         return None
     c = _comm(inp, p, "reduce_scatter")
-    if c is None or inp.numel() * inp.element_size() > c.cap or inp.numel() % (8 * p.tp_size):
+    if c is None or not _fits(c, inp, 8 * p.tp_size):
         return dist.reduce_scatter_tensor(out, inp, group=p.tp_group, async_op=async_op)
     return c.reduce_scatter(out, inp, async_op=async_op)
 
@@ -200,7 +261,7 @@ def all_gather(out: torch.Tensor, inp: torch.Tensor, async_op: bool = True):
         out.copy_(inp.view_as(out))
         return None
     c = _comm(inp, p, "all_gather")
-    if c is None or inp.numel() * inp.element_size() > c.cap or inp.numel() % 8:
+    if c is None or not _fits(c, inp, 8):
         return dist.all_gather_into_tensor(out, inp, group=p.tp_group, async_op=async_op)
     return c.all_gather(out, inp, async_op=async_op)
 
@@ -208,23 +269,27 @@ def all_gather(out: torch.Tensor, inp: torch.Tensor, async_op: bool = True):
 def staging(slot: int, shape, dtype: torch.dtype, op: str = "all_reduce") -> Optional[torch.Tensor]:
     """Output buffer for a GEMM whose result feeds the next TP all-reduce / reduce-scatter:
     a view of the xGMI communicator's staging slot ``slot`` (then the collective skips its
-    copy-in), or None when ``op`` runs on RCCL, the group has not chosen yet, or it does not fit.
-    Use one slot per in-flight chunk; a slot may be rewritten once the collective that read
-    it has been waited."""
+    copy-in), or None when ``op`` does not run on xGMI, the group has not chosen yet, or it
+    does not fit.  Use one slot per in-flight chunk; a slot may be rewritten once the
+    collective that read it has been waited."""
     p = pm.pgm
     if p is None or p.tp_size == 1 or os.environ.get("DPFS_XGMI_STAGING", "1") == "0":
         return None
     ch = _decisions.get(id(p.tp_group))
-    if ch is None or not ch.use[op]:
+    if ch is None or ch.use[op] != "xgmi":
         return None
-    return ch.comm.staging(slot, shape, dtype)
+    return ch.xgmi.staging(slot, shape, dtype)
 
 
 def check():
-    """Raise if any xGMI call of this process timed out (cheap: one host-mapped word)."""
+    """Raise if any xGMI call of this process timed out (one host-mapped word) or the native
+    RCCL communicator reported an asynchronous error."""
     p = pm.pgm
     if p is None:
         return
     ch = _decisions.get(id(p.tp_group))
     if ch is not None:
-        ch.comm.check()
+        if ch.xgmi is not None:
+            ch.xgmi.check()
+        if ch.native is not None:
+            ch.native.check()

@@ -216,3 +216,23 @@ def test_kernel_debug_modes_run_clean_and_catch_nan(dist1, monkeypatch):
     monkeypatch.delenv("DPFS_SYNC_DEBUG")
     monkeypatch.delenv("DPFS_NAN_CHECK")
     assert not isinstance(_ext.require(), _ext._DebugProxy)
+
+
+def test_native_rccl_communicator(dist1):
+    """parallel/rccl.py: the RCCL C API from our extension (ncclCommInitRank from a unique id
+    broadcast over the store) on a side stream; one rank, so sums are identities."""
+    from distributed_pytorch_from_scratch_amd.parallel.rccl import RcclComm
+    c = RcclComm()
+    x = torch.randn(4096, device="cuda").bfloat16()
+    y = x.clone()
+    c.all_reduce(y).wait()
+    part, gat = torch.empty_like(x), torch.empty_like(x)
+    c.reduce_scatter(part, x).wait()
+    c.all_gather(gat, part, async_op=False)
+    z = torch.randn(1000, device="cuda")
+    z0 = z.clone()
+    c.broadcast(z, 0).wait()
+    torch.cuda.synchronize()
+    assert torch.equal(y, x) and torch.equal(part, x) and torch.equal(gat, x) and torch.equal(z, z0)
+    assert c.error() is None
+    c.close()

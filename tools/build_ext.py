@@ -98,7 +98,7 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> str:
         tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
         link = ["g++", "-shared", "-o", out] + objs + [
             "-L" + tlib, "-Wl,-rpath," + tlib, "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python",
-            "-lc10_hip", "-ltorch_hip", "-lamdhip64"]
+            "-lc10_hip", "-ltorch_hip", "-lamdhip64", "-lrccl"]   # torch's own librccl.so (same instance)
         _run(link)
         if verbose:
             print("[build_ext] linked", out, flush=True)
