@@ -84,6 +84,7 @@ int dpfs_xgmi_error(void*);
 void dpfs_xgmi_clear_error(void*);
 int dpfs_xgmi_run(void*, int, int, const void*, void*, long long, long long, double, int, hipStream_t);
 void dpfs_xgmi_destroy(void*);
+void dpfs_adam_patch_grads(void*, const long long*, int, hipStream_t);
 // comm/rccl_comm.hip
 const char* dpfs_rccl_last_error();
 int dpfs_rccl_id_bytes();
@@ -621,9 +622,28 @@ std::vector<torch::Tensor> adam_build(std::vector<torch::Tensor> params, std::ve
     }
   }
   auto dev = params.empty() ? torch::Device(torch::kCUDA) : params[0].device();
-  auto d = torch::from_blob(desc.data(), {(int64_t)desc.size()}, torch::kInt64).to(dev);
-  auto c = torch::from_blob(chunks.data(), {(int64_t)chunks.size()}, torch::kInt32).to(dev);
+  // Pinned staging + async copies: a pageable H2D copy would block the host until the GPU
+  // has drained every queued kernel (the whole backward), idling the GPU while the host then
+  // enqueues the optimizer and the next step.  The caching host allocator keeps the pinned
+  // blocks alive until their copies have run.
+  auto d = torch::from_blob(desc.data(), {(int64_t)desc.size()}, torch::kInt64).pin_memory().to(dev, true);
+  auto c = torch::from_blob(chunks.data(), {(int64_t)chunks.size()}, torch::kInt32).pin_memory().to(dev, true);
   return {d, c};
+}
+
+// Rewrite the gradient pointers of a descriptor table built by adam_build (same params,
+// same order; only the gradient tensors changed) without a host -> device copy.
+void adam_patch_grads(torch::Tensor desc, std::vector<torch::Tensor> grads) {
+  TORCH_CHECK(desc.is_cuda() && desc.scalar_type() == torch::kInt64 && desc.numel() == (int64_t)grads.size() * 6,
+              "adam_patch_grads: descriptor table / grad list mismatch");
+  std::vector<long long> ptrs(grads.size());
+  for (size_t i = 0; i < grads.size(); ++i) {
+    TORCH_CHECK(grads[i].is_cuda() && grads[i].scalar_type() == torch::kFloat32 && grads[i].is_contiguous(),
+                "adam_patch_grads: grads must be contiguous fp32 on the device");
+    ptrs[i] = (long long)grads[i].data_ptr();
+  }
+  const at::DeviceGuard g(desc.device());
+  dpfs_adam_patch_grads(desc.data_ptr(), ptrs.data(), (int)ptrs.size(), stream());
 }
 
 void adam_step(torch::Tensor desc, torch::Tensor chunks, double lr, double b1, double b2, double eps, double wd,
@@ -891,6 +911,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"), py::arg("step"), py::arg("grad_scale") = 1.0,
         py::arg("dscale") = py::none());
   m.def("grad_sumsq", &grad_sumsq);
+  m.def("adam_patch_grads", &adam_patch_grads, py::arg("desc"), py::arg("grads"));
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("len"),
         py::arg("scale"));
   m.def("kv_append", &kv_append, py::arg("qkv"), py::arg("k_cache"), py::arg("v_cache"), py::arg("len"));

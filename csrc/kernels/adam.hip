@@ -90,6 +90,29 @@ __global__ __launch_bounds__(256) void sumsq_k(const AdamTensor* __restrict__ ts
 
 using namespace dpfs;
 
+// Gradient pointers of the descriptor table, rewritten in place from kernel arguments (up to
+// kPatch per launch): the training engine hands back fresh gradient tensors every step, and
+// an H2D copy of a rebuilt table would stall the stream on a host round trip.
+namespace dpfs {
+constexpr int kPatch = 256;
+struct GradPtrs {
+  long long v[kPatch];
+};
+__global__ __launch_bounds__(256) void adam_patch_grads_k(AdamTensor* __restrict__ ts, GradPtrs p, int i0, int n) {
+  const int i = threadIdx.x;
+  if (i < n) ts[i0 + i].g = reinterpret_cast<const float*>(p.v[i]);
+}
+}  // namespace dpfs
+
+extern "C" void dpfs_adam_patch_grads(void* desc, const long long* ptrs, int n, hipStream_t s) {
+  for (int i0 = 0; i0 < n; i0 += kPatch) {
+    GradPtrs p;
+    const int m = n - i0 < kPatch ? n - i0 : kPatch;
+    for (int i = 0; i < m; ++i) p.v[i] = ptrs[i0 + i];
+    adam_patch_grads_k<<<1, 256, 0, s>>>(reinterpret_cast<AdamTensor*>(desc), p, i0, m);
+  }
+}
+
 extern "C" int dpfs_adam_chunk() { return kAdamChunk; }
 extern "C" int dpfs_adam_desc_bytes() { return (int)sizeof(AdamTensor); }
 

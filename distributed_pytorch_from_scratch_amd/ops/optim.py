@@ -6,8 +6,9 @@ same per-parameter ``step``/``exp_avg``/``exp_avg_sq`` entries.
 
 On the GPU one ``adam_k`` launch (``csrc/kernels/adam.hip``) updates every parameter of a
 group and refreshes the bf16 compute shadows the GEMMs read (``ops.dispatch.shadow``), so
-there is no per-step cast kernel.  The device descriptor table is rebuilt only when a
-gradient buffer moves (the caching allocator usually hands back the same blocks).
+there is no per-step cast kernel.  The device descriptor table is built once (rebuilt only if a
+parameter or shadow moves); fresh gradient tensors are patched in by a one-block kernel whose
+pointers travel as kernel arguments, so a step never waits on a host -> device copy.
 On CPU the same math runs through ``ops.reference.adam_step``.
 
 Optional ``max_grad_norm`` clips by the global L2 norm (sum over TP-sharded params across the
@@ -88,16 +89,22 @@ class FusedAdam(torch.optim.Optimizer):
                 # epilogue reads one (a hipBLASLt bias, ops.gemm_select).
                 shadows = [self._shadow_for(p) if (p.dim() >= 2 or peek_shadow(p) is not None) else None
                            for p in params]
-                key = tuple((p.data_ptr(), p.grad.data_ptr(), s.data_ptr() if s is not None else 0)
+                key = tuple((p.data_ptr(), s.data_ptr() if s is not None else 0, p.numel())
                             for p, s in zip(params, shadows))
+                grads = [p.grad if p.grad.is_contiguous() else p.grad.contiguous() for p in params]
+                gkey = tuple(g.data_ptr() for g in grads)
                 tab = self._tables.get(gi)
                 if tab is None or tab[0] != key:
-                    grads = [p.grad if p.grad.is_contiguous() else p.grad.contiguous() for p in params]
                     desc, chunks = C.adam_build([p.data for p in params], grads,
                                                 [self.state[p]["exp_avg"] for p in params],
                                                 [self.state[p]["exp_avg_sq"] for p in params], shadows)
-                    tab = (key, desc, chunks, grads)
+                    tab = [key, desc, chunks, grads, gkey]
                     self._tables[gi] = tab
+                elif tab[4] != gkey:
+                    # The engine hands back fresh gradient tensors each step: rewrite only the
+                    # table's gradient pointers on the device (no host round trip).
+                    C.adam_patch_grads(tab[1], grads)
+                    tab[3], tab[4] = grads, gkey
                 C.adam_step(tab[1], tab[2], lr, b1, b2, eps, wd, step, 1.0, coef)
                 # Shadows written by the kernel are current for the (unchanged) versions.
                 for p, s in zip(params, shadows):

@@ -29,11 +29,9 @@ def _flat_allreduce(tensors: List[torch.Tensor], group, average_by: int = 1) -> 
     dist.all_reduce(flat, group=group)
     if average_by > 1:
         flat /= average_by
-    off = 0
-    for t in tensors:
-        n = t.numel()
-        t.copy_(flat[off:off + n].view_as(t))
-        off += n
+    # one multi-tensor copy back (per-tensor copy_ calls cost a launch + stream hand-off each)
+    parts = flat.split([t.numel() for t in tensors])
+    torch._foreach_copy_(tensors, [q.view_as(t) for q, t in zip(parts, tensors)])
 
 
 def allreduce_sequence_parallel_grads(model: torch.nn.Module) -> None:

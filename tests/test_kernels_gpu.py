@@ -429,3 +429,25 @@ def test_rmsnorm_bwd_fused_output_colsum(C):
     dx2, dw2 = C.rmsnorm_bwd(dy, x, w, rstd, dres)
     assert torch.equal(dx, dx2) and torch.equal(dw, dw2)
     assert _rel(db, dx.float().sum(0)) < 5e-3   # db sums the fp32 values before the bf16 store
+
+
+def test_fused_adam_fresh_grad_tensors_each_step(C):
+    """FusedAdam with new gradient tensors every step (what the training engine returns):
+    the table's gradient pointers are patched on the device; trajectory = torch.optim.Adam."""
+    from distributed_pytorch_from_scratch_amd.ops.optim import FusedAdam
+    torch.manual_seed(12)
+    shapes = [(300, 64), (16384 * 2 + 7,), (4096,)]
+    ps = [torch.nn.Parameter(torch.randn(*s, device=DEV)) for s in shapes]
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    opt = FusedAdam(ps, lr=1e-3, betas=(0.9, 0.95), weight_decay=0.01)
+    topt = torch.optim.Adam(ref, lr=1e-3, betas=(0.9, 0.95), weight_decay=0.01)
+    keep = []
+    for step in range(4):
+        gs = [torch.randn_like(p) for p in ps]
+        keep.append(gs)                       # distinct live tensors -> distinct pointers
+        for p, r, g in zip(ps, ref, gs):
+            p.grad, r.grad = g, g.clone()
+        opt.step()
+        topt.step()
+    for p, r in zip(ps, ref):
+        assert (p.detach() - r.detach()).abs().max().item() < 1e-5

@@ -41,6 +41,10 @@ def main():
     ap.add_argument("--batch-per-gpu", type=int, default=32)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--configs", default="nosp:2,sp:2,sp:4,nosp:4")
+    ap.add_argument("--cprofile", action="store_true", help="host-side profile of one step per config")
+    ap.add_argument("--head-start-ms", type=float, default=0.0,
+                    help="queue a GPU sleep of this length before each timed step and subtract it: "
+                         "with the host that far ahead, launch latency cannot starve the GPU")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -79,13 +83,46 @@ def main():
         for _ in range(2):
             step(ids[:, :-1], pos, ids[:, 1:])
         torch.cuda.synchronize()
+        sleep_cycles, sleep_ms = 0, 0.0
+        if a.head_start_ms > 0:          # calibrate torch.cuda._sleep (clock cycles -> ms)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            torch.cuda._sleep(10_000_000)
+            e1.record()
+            e1.synchronize()
+            sleep_cycles = int(10_000_000 * a.head_start_ms / e0.elapsed_time(e1))
+        ev = []
         t0 = time.perf_counter()
         for _ in range(a.steps):
-            step(ids[:, :-1], pos, ids[:, 1:])
+            if sleep_cycles:
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda._sleep(sleep_cycles)
+                e0.record()
+                step(ids[:, :-1], pos, ids[:, 1:])
+                e1.record()
+                ev.append((e0, e1))
+            else:
+                step(ids[:, :-1], pos, ids[:, 1:])
         torch.cuda.synchronize()
         res[cfg] = round(1000 * (time.perf_counter() - t0) / a.steps, 2)
+        if ev:                           # GPU time of the step alone (sleep excluded)
+            res[cfg] = round(sum(x.elapsed_time(y) for x, y in ev) / len(ev), 2)
+        # host enqueue time of one step (returns before the GPU finishes unless the host blocks)
+        t1 = time.perf_counter()
+        if a.cprofile:
+            import cProfile
+            import pstats
+            pr = cProfile.Profile()
+            pr.enable()
+        step(ids[:, :-1], pos, ids[:, 1:])
+        host_ms = round(1000 * (time.perf_counter() - t1), 2)
+        if a.cprofile:
+            pr.disable()
+            pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(25)
+        torch.cuda.synchronize()
         print(json.dumps({"tp": n, "rank": a.rank, "config": cfg, "ms_per_step": res[cfg],
-                          "tokens": B * T,
+                          "tokens": B * T, "host_ms": host_ms,
                           "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2)}), flush=True)
 
 
