@@ -229,17 +229,19 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd_k(const b
       // The causal / tail mask is evaluated only on tiles that need it (wave-uniform), the
       // 1/sqrt(hd)*log2(e) scale is folded into the exp2 argument with one FMA, and every
       // visited tile has >= 1 valid key per query (key kv0 <= wq0), so no -inf guards.
-      const bool need_mask = (causal && kv0 + BKV - 1 > wq0) || (kv0 + BKV > T);
+      const bool need_mask = __builtin_amdgcn_readfirstlane(
+          (int)((causal && kv0 + BKV - 1 > wq0) || (kv0 + BKV > T)));
 #pragma unroll
       for (int c = 0; c < QC; ++c) {
         const int qi = wq0 + 16 * c + (l & 15);
-        if (need_mask) {
+        if (need_mask) {   // wave-uniform; branch-free selects
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const int ki = kv0 + 16 * i + 4 * g + j;
-              if (ki >= T || (causal && ki > qi)) s[i][c][j] = -INFINITY;
+              const bool z = (ki >= T) | (causal & (ki > qi));
+              s[i][c][j] = z ? -INFINITY : s[i][c][j];
             }
         }
         float mx = s[0][c][0];
@@ -739,6 +741,55 @@ __device__ __forceinline__ void qdo_dma(__amdgpu_buffer_rsrc_t rq, __amdgpu_buff
                                            4, soff, 0, 0, 0);
 }
 
+// qdo_dma with the per-lane part of every DMA offset computed once per kernel: per tile only
+// the wave-uniform q0 * ld term and the tail-row test remain (the generic form re-derived
+// the swizzled chunk / row split of every piece for every tile: ~50 VALU + ~60 SALU a tile).
+template <int HD>
+struct QdoPlan {
+  static constexpr int TILE = 64 * HD * 2;
+  static constexpr int PW = 2 * TILE / 1024 / 4;   // 1 KiB pieces per wave
+  unsigned base[PW];                               // (r * ld + ch * 8) * 2
+  int r[PW];                                       // row within the tile
+  __device__ void init(long long ldq, long long lddo) {
+    constexpr int CPR = HD / 8;
+    constexpr int P = 2 * TILE / 1024;
+    const int l = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int j = wave + 4 * i;
+      const bool isdo = i >= P / 8;             // (waves < 4: piece j < P/2 <=> i < P/8)
+      const int jj = isdo ? j - P / 2 : j;
+      const int pos = jj * 64 + l;
+      const int rr = pos / CPR, cp = pos % CPR;
+      const int ch = ((sw_off<HD>(rr, cp) - rr * HD * 2) >> 4);
+      r[i] = rr;
+      base[i] = (unsigned)(((long long)rr * (isdo ? lddo : ldq) + ch * 8) * 2);
+    }
+  }
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rq, __amdgpu_buffer_rsrc_t rdo,
+                                        __amdgpu_buffer_rsrc_t rl, __amdgpu_buffer_rsrc_t rd, char* stage, int q0,
+                                        int T, long long ldq, long long lddo) const {
+    constexpr int P = 2 * TILE / 1024;
+    const int l = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const unsigned qoff = (unsigned)((long long)q0 * ldq * 2), dooff = (unsigned)((long long)q0 * lddo * 2);
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int j = wave + 4 * i;
+      const bool isdo = i >= P / 8;             // compile-time per unrolled i
+      const int jj = isdo ? j - P / 2 : j;
+      const unsigned off = q0 + r[i] < T ? base[i] + (isdo ? dooff : qoff) : kOOB;
+      dma16(isdo ? rdo : rq, stage + (isdo ? TILE : 0) + jj * 1024, off);
+    }
+    char* st = stage + 2 * TILE;
+    const unsigned soff = (wave < 2 && q0 + l < T) ? (unsigned)((q0 + l) * 4) : kOOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wave == 1 ? rd : rl,
+                                             (__attribute__((address_space(3))) void*)(st + (wave < 2 ? wave : 2) * 256),
+                                             4, soff, 0, 0, 0);
+  }
+};
+
 template <int HD>
 __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv2_k(
     const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V, const bf16* __restrict__ dO,
@@ -772,8 +823,10 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv2_k(
 
   const int qstart = causal ? (k0 / BQ) * BQ : 0;
   const int nq = (T - qstart + BQ - 1) / BQ;
-  if (nq > 0) qdo_dma<HD>(rq, rdo, rl, rd, smem, qstart, T, ldq, lddo);
-  if (nq > 1) qdo_dma<HD>(rq, rdo, rl, rd, smem + BUF, qstart + BQ, T, ldq, lddo);
+  QdoPlan<HD> plan;
+  plan.init(ldq, lddo);
+  if (nq > 0) plan.issue(rq, rdo, rl, rd, smem, qstart, T, ldq, lddo);
+  if (nq > 1) plan.issue(rq, rdo, rl, rd, smem + BUF, qstart + BQ, T, ldq, lddo);
 
   bf16x8 kf[KT], vf[KT];
   {
@@ -809,7 +862,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv2_k(
     if (nb >= NST) nb -= NST;
     cur = (cur + 1 == NST) ? 0 : cur + 1;
     const int qq0 = qstart + t * BQ;
-    if (t + 2 < nq) qdo_dma<HD>(rq, rdo, rl, rd, smem + nb * BUF, qq0 + 2 * BQ, T, ldq, lddo);
+    if (t + 2 < nq) plan.issue(rq, rdo, rl, rd, smem + nb * BUF, qq0 + 2 * BQ, T, ldq, lddo);
     const bool wave_active = !causal || (qq0 + BQ - 1 >= wk0);
     if (!wave_active) continue;
     // Row constants as the initial accumulators (rows = queries 16qt + 4g + j): S' = QK^T -
@@ -838,20 +891,28 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv2_k(
 #pragma unroll
       for (int d = 0; d < DT; ++d) tr_frag_asm<HD>(ldo_, 32 * ks, 16 * d, th[2 * (ks * DT + d)], th[2 * (ks * DT + d) + 1]);
     const int ki = wk0 + (l & 15);
-    const bool need_mask = (causal && wk0 + 15 > qq0) || (qq0 + BQ > T) || (wk0 + 16 > T);
+    // The mask test is wave-uniform (readfirstlane) and only diagonal / tail tiles run the
+    // per-element selects: branch-free v_cndmask there, nothing on the other tiles.
+    const bool need_mask = __builtin_amdgcn_readfirstlane(
+        (int)((causal && wk0 + 15 > qq0) || (qq0 + BQ > T) || (wk0 + 16 > T)));
 #pragma unroll
-    for (int qt = 0; qt < 4; ++qt) {
+    for (int qt = 0; qt < 4; ++qt)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float p = __builtin_amdgcn_exp2f(s[qt][j] * c2);
-        if (need_mask) {
+      for (int j = 0; j < 4; ++j) s[qt][j] = __builtin_amdgcn_exp2f(s[qt][j] * c2);
+    if (need_mask) {
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
           const int qi = qq0 + 16 * qt + 4 * g + j;
-          if (qi >= T || ki >= T || (causal && ki > qi)) p = 0.f;
+          const bool z = (qi >= T) | (ki >= T) | (causal & (ki > qi));
+          s[qt][j] = z ? 0.f : s[qt][j];
         }
-        s[qt][j] = p;
-        dp[qt][j] = p * dp[qt][j];
-      }
     }
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dp[qt][j] *= s[qt][j];
     bf16x8 pa[2], da[2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -1018,22 +1079,34 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
           }
         }
       }
-      const bool need_mask = (causal && kv0 + BKV - 1 > wq0) || (kv0 + BKV > T);
+      const bool need_mask = __builtin_amdgcn_readfirstlane(
+          (int)((causal && kv0 + BKV - 1 > wq0) || (kv0 + BKV > T)));
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int qi = wq0 + 16 * c + (l & 15);
+      for (int c = 0; c < 2; ++c)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            float p = __builtin_amdgcn_exp2f(s[i][c][j] * c2);
-            if (need_mask) {
+          for (int j = 0; j < 4; ++j) s[i][c][j] = __builtin_amdgcn_exp2f(s[i][c][j] * c2);
+      if (need_mask) {   // wave-uniform: diagonal / tail tiles only, branch-free selects
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int qi = wq0 + 16 * c + (l & 15);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
               const int ki = kv0 + 16 * i + 4 * g + j;
-              if (ki >= T || (causal && ki > qi)) p = 0.f;
+              const bool z = (ki >= T) | (causal & (ki > qi));
+              s[i][c][j] = z ? 0.f : s[i][c][j];
             }
-            s[i][c][j] = p * dp[i][c][j];  // dS^T
-          }
+        }
       }
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s[i][c][j] *= dp[i][c][j];  // dS^T
       // dQ^T[d][q] += K^T[d][k] dS^T[k][q]
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
