@@ -1062,23 +1062,33 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
     if (wave_active) {
       f32x4 s[4][2], dp[4][2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int c = 0; c < 2; ++c) {   // row constants as initial accumulators (cols = queries)
           s[i][c] = (f32x4){lse2[c], lse2[c], lse2[c], lse2[c]};
           dp[i][c] = (f32x4){del[c], del[c], del[c], del[c]};
         }
+      // k-slices outermost: 16 independent MFMAs separate each accumulator's dependent pair
+      // (with the slice innermost the compiler padded the chains with ~80 s_nop per tile).
 #pragma unroll
-        for (int kk = 0; kk < KT; ++kk) {
-          const bf16x8 kr = row_frag<HD>(lk, 16 * i, 32 * kk);
-          const bf16x8 vr = row_frag<HD>(lv, 16 * i, 32 * kk);
+      for (int kk = 0; kk < KT; ++kk) {
+        bf16x8 kr[4], vr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          kr[i] = row_frag<HD>(lk, 16 * i, 32 * kk);
+          vr[i] = row_frag<HD>(lv, 16 * i, 32 * kk);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int c = 0; c < 2; ++c) {
-            s[i][c] = MFMA(kr, qf[c][kk], s[i][c]);
-            dp[i][c] = MFMA(vr, dof[c][kk], dp[i][c]);
+            s[i][c] = MFMA(kr[i], qf[c][kk], s[i][c]);
+            dp[i][c] = MFMA(vr[i], dof[c][kk], dp[i][c]);
           }
-        }
       }
+      // All 32 S / dP MFMAs issue before the softmax reads their results (interleaved, the
+      // scheduler padded each early read with s_nop for the MFMA latency).
+      __builtin_amdgcn_sched_barrier(0);
       const bool need_mask = __builtin_amdgcn_readfirstlane(
           (int)((causal && kv0 + BKV - 1 > wq0) || (kv0 + BKV > T)));
 #pragma unroll
