@@ -113,6 +113,23 @@ __device__ __forceinline__ bf16x8 pack_pt(const f32x4& a, const f32x4& b) {
 
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
+// Max / sum over the four 16-lane groups of a wave (lanes l, l^16, l^32, l^48) with the
+// CDNA4 half-exchange permlanes (VALU) instead of ds_bpermute round trips through the LDS
+// unit: v_permlane16_swap with vdst = src = x leaves {x from my group, x from group ^1} in
+// the two results, v_permlane32_swap likewise for group ^2.
+__device__ __forceinline__ float group4_max(float x) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float group4_sum(float x) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 // Global -> registers -> swizzled LDS tile of R rows x HD (rows >= nvalid are zero).
 template <int HD, int R, int NT = 256>
 struct Stage {
@@ -249,8 +266,7 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd_k(const b
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) mx = fmaxf(mx, s[i][c][j]);
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        mx = group4_max(mx);
         const float mnew = fmaxf(m[c], mx * c2);
         const float alpha = __builtin_amdgcn_exp2f(m[c] - mnew);
         m[c] = mnew;
@@ -292,9 +308,7 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd_k(const b
   // Epilogue: O[q][d] = O^T[d][q] / l ; lse = (m + log2 l) * ln2.
 #pragma unroll
   for (int c = 0; c < QC; ++c) {
-    float ls = lsum[c];
-    ls += __shfl_xor(ls, 16, 64);
-    ls += __shfl_xor(ls, 32, 64);
+    const float ls = group4_sum(lsum[c]);
     const int qi = wq0 + 16 * c + (l & 15);
     if (qi < T) {
       const float inv = 1.f / ls;
@@ -1027,8 +1041,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
         for (int j = 0; j < 8; ++j) dsum += (float)dof[c][kk][j] * (float)ov[j];
       }
     }
-    dsum += __shfl_xor(dsum, 16, 64);
-    dsum += __shfl_xor(dsum, 32, 64);
+    dsum = group4_sum(dsum);
     del[c] = -dsum;                                                             // dP' = dP - delta
     if (g == 0 && qi < T) DELTA_OUT[((long long)b * H + h) * T + qi] = -dsum;
   }
