@@ -267,21 +267,32 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd_k(const b
 #pragma unroll
           for (int j = 0; j < 4; ++j) mx = fmaxf(mx, s[i][c][j]);
         mx = group4_max(mx);
-        const float mnew = fmaxf(m[c], mx * c2);
-        const float alpha = __builtin_amdgcn_exp2f(m[c] - mnew);
-        m[c] = mnew;
+        // Deferred rescale: the running max m moves only when this tile's max exceeds it by
+        // more than kDefer (log2 units).  Otherwise p = exp2(s c2 - m) <= 2^kDefer, exact in
+        // fp32 and representable in bf16, and the final 1/l normalisation (and lse = m +
+        // log2 l) is unchanged; the alpha exp and the O / l rescale run only on the (wave-
+        // uniform) tiles where some column's max grew that much — rarely after the first.
+        constexpr float kDefer = 8.f;
+        const bool grow = mx * c2 > m[c] + kDefer;
+        if (__builtin_amdgcn_ballot_w64(grow) != 0) {
+          const float mnew = grow ? mx * c2 : m[c];
+          const float alpha = __builtin_amdgcn_exp2f(m[c] - mnew);
+          m[c] = mnew;
+          lsum[c] *= alpha;
+#pragma unroll
+          for (int d = 0; d < DT; ++d) o[c][d] *= alpha;
+        }
+        const float mc = m[c];
         float ps = 0.f;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float pv = __builtin_amdgcn_exp2f(fmaf(s[i][c][j], c2, -mnew));
+            const float pv = __builtin_amdgcn_exp2f(fmaf(s[i][c][j], c2, -mc));
             s[i][c][j] = pv;
             ps += pv;
           }
-        lsum[c] = lsum[c] * alpha + ps;
-#pragma unroll
-        for (int d = 0; d < DT; ++d) o[c][d] *= alpha;
+        lsum[c] += ps;
       }
       // O^T[d][q] += V^T[d][k] P^T[k][q]
 #pragma unroll
