@@ -171,8 +171,11 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd_k(const b
   constexpr int TILE = BKV * HD * 2;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
   const int nqb = (T + BQ - 1) / BQ;
-  const int qb = nqb - 1 - blockIdx.x;  // heaviest first
-  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  // XCD-aware order: the blocks of one (b, h) -- which share its K / V -- run on one XCD
+  // (one L2); within a head the heaviest query blocks still go first.
+  const int xl = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+  const int qb = nqb - 1 - xl % gridDim.x;  // heaviest first
+  const int bh = xl / gridDim.x, b = bh / H, h = bh % H;
   const int q0 = qb * BQ;
   const int wave = threadIdx.x >> 6, l = lane_id(), g = l >> 4;
   const int wq0 = q0 + wave * QW;
@@ -828,8 +831,11 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv2_k(
   constexpr int NST = 3;
   constexpr int PWV = 2 * TILE / 1024 / 4 + 1;  // DMA instructions per wave per tile
   __shared__ __attribute__((aligned(1024))) char smem[NST * BUF];
-  const int kb = blockIdx.x;
-  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  // XCD-aware order: the key blocks of one (b, h) -- which all stream its Q / dO -- run on one
+  // XCD (one L2).
+  const int xl = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+  const int kb = xl % gridDim.x;
+  const int bh = xl / gridDim.x, b = bh / H, h = bh % H;
   const int k0 = kb * BKV;
   const int wave = threadIdx.x >> 6, l = lane_id(), g = l >> 4;
   const int wk0 = k0 + wave * 16;
@@ -1014,8 +1020,11 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
   constexpr int TILE = BKV * HD * 2;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
   const int nqb = (T + BQ - 1) / BQ;
-  const int qb = nqb - 1 - blockIdx.x;
-  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  // XCD-aware order: the blocks of one (b, h) -- which share its K / V -- run on one XCD
+  // (one L2); within a head the heaviest query blocks still go first.
+  const int xl = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+  const int qb = nqb - 1 - xl % gridDim.x;  // heaviest first
+  const int bh = xl / gridDim.x, b = bh / H, h = bh % H;
   const int q0 = qb * BQ;
   const int wave = threadIdx.x >> 6, l = lane_id(), g = l >> 4;
   const int wq0 = q0 + wave * 32;
