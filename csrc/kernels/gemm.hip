@@ -341,10 +341,16 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 2 : 1) void gemm2_k(const bf16
   const int tiles_n = (N + BN_ - 1) / BN_;
   const int tiles_m = (M + BM_ - 1) / BM_;
   const int nwg = tiles_m * tiles_n;
-  const int wg = xcd_remap(blockIdx.x, nwg);
+  // XCD-aware over the whole (tile, split) grid: the hardware deals linear block ids to the 8
+  // XCDs round-robin, so remap the LINEAR id (a split-K grid's tile count is rarely a multiple
+  // of 8); every XCD then holds a contiguous run of (split, tile) pairs: the tiles of one
+  // K-split, which stream the same K-slab of both operands, share that XCD's L2.
+  const int lin = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, nwg * gridDim.y);
+  const int split = lin / nwg;
+  const int wg = lin - split * nwg;
   const int tm = wg / tiles_n, tn = wg % tiles_n;
   const int m0 = tm * BM_, n0 = tn * BN_;
-  const int kbeg = blockIdx.y * k_per_split;
+  const int kbeg = split * k_per_split;
   const int kend = min(K, kbeg + k_per_split);
   const int nk = kend > kbeg ? (kend - kbeg + 63) / 64 : 0;
 
@@ -494,7 +500,7 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 2 : 1) void gemm2_k(const bf16
         bf16x4 o = {(bf16)v[j][0], (bf16)v[j][1], (bf16)v[j][2], (bf16)v[j][3]};
         *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(C) + (long long)m * ldc + n) = o;
       } else {
-        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + blockIdx.y * slab_stride + (long long)m * ldc + n) = v[j];
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + split * slab_stride + (long long)m * ldc + n) = v[j];
       }
     }
   }
