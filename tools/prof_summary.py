@@ -33,7 +33,12 @@ def load(path: str):
     else:
         with open(path) as f:
             for rec in csv.DictReader(f):
-                r = rows[_short(rec["Name"])]
+                if "Kernel_Name" in rec:          # *kernel_trace.csv: one row per dispatch
+                    r = rows[_short(rec["Kernel_Name"])]
+                    r[0] += (int(rec["End_Timestamp"]) - int(rec["Start_Timestamp"])) / 1e6
+                    r[1] += 1
+                    continue
+                r = rows[_short(rec["Name"])]      # *kernel_stats.csv: one row per kernel
                 r[0] += float(rec["TotalDurationNs"]) / 1e6
                 r[1] += int(rec["Calls"])
     return rows
