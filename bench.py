@@ -183,7 +183,8 @@ def main():
 
     tokens = gb * T * a.steps
     value = tokens / elapsed
-    base = REFERENCE_TOKENS_PER_S_TP1
+    # The reference-formulation baseline was measured on GPT-2 small only; other shapes get null.
+    base = REFERENCE_TOKENS_PER_S_TP1 if (a.model == "gpt2-small" and not a.layers) else None
     vs = None
     if base:
         # Reference measured at TP=1; for N>1 compare against ideal linear scaling of it.
