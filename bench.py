@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--impl", choices=["ours", "reference"], default="ours")
     ap.add_argument("--layers", type=int, default=None, help="debug only: not a valid headline number")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--recompute", action="store_true", help="activation recompute (layer inputs only)")
     return ap.parse_args()
 
 
@@ -79,6 +80,8 @@ def main():
     overrides = dict(sequence_parallel=world > 1 and a.sp != "off")
     if a.layers:
         overrides["num_layers"] = a.layers
+    if a.recompute:
+        overrides["recompute"] = True
     args = get_preset(a.model, **overrides)
     T = a.seq_len
     assert T <= args.maxlen
@@ -209,6 +212,7 @@ def main():
             "seq_len": T,
             "parallelism": f"tp{world}" + ("+sp" if sp_used else ""),
             "impl": a.impl,
+            "recompute": bool(a.recompute),
             "params_matmul": args.matmul_params(),
             "tp_comm": tp_comm.info(),
             "chunks": model.overlap_chunks() if a.impl == "ours" else None,

@@ -45,3 +45,15 @@ def test_bench_prints_one_json_line(world, warmup):
     if warmup >= 4:
         assert set(d["config"]["engine_trial_ms"]) == {"nosp/c2", "sp/c2"}
     assert d["value"] > 0 and d["higher_is_better"] is True
+
+
+def test_bench_recompute_flag_and_baseline_scope():
+    """--recompute reaches the model and is reported; vs_baseline is null off the GPT-2 small config."""
+    cmd = [sys.executable, "bench.py", "--model", "plumbing", "--recompute", "--steps", "2", "--warmup", "1",
+           "--seq-len", "64", "--batch-per-gpu", "2"]
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    (d,) = _json_lines(r.stdout)
+    assert d["config"]["recompute"] is True
+    assert d["vs_baseline"] is None
+    assert d["value"] > 0
