@@ -9,10 +9,12 @@ sides, elapsed = MAX over ranks, rank 0 prints ONE JSON line.
 Config (BASELINE.json metric "tokens/sec (whole node), GPT-2-small TP at 1/2/4/8 MI355X"):
 GPT-2 small shape in the reference block (d=768, 12 layers, 12 heads, SwiGLU ffn 2048,
 vocab 50257 padded to 50304, untied head; 123.6M matmul params), seq_len 1024, bf16 compute
-with fp32 master weights + Adam, random init, synthetic uniform token data.  Tensor
-parallel degree = N (12 heads over 8 ranks: 2 heads on ranks 0-3, 1 on ranks 4-7).  Weak
-scaling: the global batch is ``--batch-per-gpu x N`` sequences (every rank does the same
-FLOPs per step for every N).
+with fp32 master weights + Adam, random init, synthetic uniform token data.  Layout: TP
+degree ``--tp`` (default ``auto`` = the model's BASELINE.json TP degree: 2 for GPT-2 small,
+capped at N) with data parallelism over the remaining GPUs (``tp2dp4`` at N = 8); ``--tp N``
+gives pure TP (12 heads over 8 ranks: 2 heads on ranks 0-3, 1 on ranks 4-7).  Weak scaling:
+the global batch is ``--batch-per-gpu x N`` sequences (every rank does the same FLOPs per
+step for every N and layout).
 
 ``--impl reference`` times the reference's eager formulation (nn.Linear/autocast, materialised
 causal softmax, full-logit CE, torch.optim.Adam; tests/vanilla_model.py) on one GPU — the
@@ -50,11 +52,28 @@ def parse():
     ap.add_argument("--sp", choices=["auto", "on", "off"], default="auto",
                     help="Megatron sequence parallelism; auto = time both during the warmup steps "
                          "(TP > 1, warmup >= 4) and keep the faster, else on for TP >= 4")
+    ap.add_argument("--tp", default="auto",
+                    help="tensor-parallel degree (DP over the rest of the GPUs); auto = the BASELINE.json "
+                         "config's TP degree for the model (gpt2-small 2, gpt2-large 4, 7B/13B 8), capped at N")
     ap.add_argument("--impl", choices=["ours", "reference"], default="ours")
     ap.add_argument("--layers", type=int, default=None, help="debug only: not a valid headline number")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--recompute", action="store_true", help="activation recompute (layer inputs only)")
     return ap.parse_args()
+
+
+# TP degree of each model's BASELINE.json config (GPT-2 small TP=2, GPT-2 large TP=4, 7B / 13B
+# TP=8).  GPT-2 small at d=768 is xGMI-link-bound beyond TP 2 under weak scaling (README
+# "Known limits"), so `auto` scales it out by data parallelism over TP=2 groups.
+BASELINE_TP = {"gpt2-small": 2, "gpt2-large": 4, "llama2-7b": 8, "llama-13b": 8}
+
+
+def resolve_tp(tp: str, model: str, world: int) -> int:
+    t = BASELINE_TP.get(model, world) if tp == "auto" else int(tp)
+    t = max(1, min(t, world))
+    while world % t:
+        t -= 1
+    return t
 
 
 def main():
@@ -71,13 +90,14 @@ def main():
     assert world == a.gpus, f"WORLD_SIZE={world} but --gpus {a.gpus}"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
-    p = init_dist_env(rank=None, tp_size=world)
+    tp = resolve_tp(a.tp, a.model, world)
+    p = init_dist_env(rank=None, tp_size=tp, dp_size=world // tp)
     rank = dist.get_rank()
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
 
     # SP is a property of the step, not of the weights: build with the SP attributes and
     # switch the engine per step (TrainStep.sp / args.sequence_parallel).
-    overrides = dict(sequence_parallel=world > 1 and a.sp != "off")
+    overrides = dict(sequence_parallel=tp > 1 and a.sp != "off")
     if a.layers:
         overrides["num_layers"] = a.layers
     if a.recompute:
@@ -86,13 +106,16 @@ def main():
     T = a.seq_len
     assert T <= args.maxlen
     gb = a.global_batch or a.batch_per_gpu * world
+    assert gb % p.dp_size == 0, f"global batch {gb} not divisible by DP {p.dp_size}"
+    lb = gb // p.dp_size          # sequences per TP group (= per DP replica) per step
     V = args.vocab_size
 
     set_seed(a.seed)
-    g = torch.Generator(device=dev).manual_seed(1234)  # same synthetic data on every TP rank
+    # same synthetic data on every rank of a TP group, a different stream per DP replica
+    g = torch.Generator(device=dev).manual_seed(1234 + 7919 * p.dp_rank)
     n_pool = 4
-    pool = [torch.randint(0, V, (gb, T + 1), device=dev, generator=g) for _ in range(n_pool)]
-    pos = torch.arange(T, device=dev).unsqueeze(0).expand(gb, T).contiguous()
+    pool = [torch.randint(0, V, (lb, T + 1), device=dev, generator=g) for _ in range(n_pool)]
+    pos = torch.arange(T, device=dev).unsqueeze(0).expand(lb, T).contiguous()
 
     if a.impl == "ours":
         model = Transformer.from_args(args).to(dev)
@@ -137,14 +160,14 @@ def main():
     # lowest max-over-ranks step time.  Without a trial: SP at any TP > 1 and 2 chunks (the
     # compute-only per-rank step on one MI355X, tools/tp_sim.py: TP 2 / 4 / 8 = 50.0 / 55.1 /
     # 73.8 ms without SP, 45.8 / 47.9 / 59.9 ms with it; 4 chunks cost 5-9 ms more).
-    default = (world > 1 and a.sp != "off", 2 if world > 1 else 1)
+    default = (tp > 1 and a.sp != "off", 2 if tp > 1 else 1)
     cands = [default]
     if a.sp == "auto":
         cands += [(not default[0], 2), (True, 4), (False, 4)]
     else:
         cands += [(a.sp == "on", 4)]
     cands = list(dict.fromkeys(cands))
-    ntrial = min(len(cands), a.warmup // 2) if a.impl == "ours" and world > 1 else 0
+    ntrial = min(len(cands), a.warmup // 2) if a.impl == "ours" and tp > 1 else 0
     trial = {}
     i = 0
     for cfg in cands[:ntrial] if ntrial >= 2 else []:
@@ -210,7 +233,7 @@ def main():
             "model": a.model + (f"(L={a.layers})" if a.layers else ""),
             "global_batch": gb,
             "seq_len": T,
-            "parallelism": f"tp{world}" + ("+sp" if sp_used else ""),
+            "parallelism": f"tp{tp}" + (f"dp{p.dp_size}" if p.dp_size > 1 else "") + ("+sp" if sp_used else ""),
             "impl": a.impl,
             "recompute": bool(a.recompute),
             "params_matmul": args.matmul_params(),

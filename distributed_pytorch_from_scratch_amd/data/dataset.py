@@ -23,7 +23,7 @@ from functools import partial
 from typing import Dict, List, Optional
 
 import torch
-from torch.utils.data import DataLoader, Dataset
+from torch.utils.data import DataLoader, Dataset, Sampler
 
 from ..constants import BOS_TOKEN, EOS_TOKEN, UNK_TOKEN, IGNORE_INDEX
 
@@ -91,12 +91,61 @@ def collate_fn(batch: List[List[int]], bos: int, eos: int, ignore_idx: int) -> D
     return {"input_ids": input_ids, "target_ids": target_ids, "position_ids": position_ids}
 
 
+class ResumableSampler(Sampler):
+    """Epoch-indexed sample order that can start mid-epoch (extension: the reference restarts
+    its DataLoader from scratch, so it cannot resume a run at the batch it stopped at).
+
+    Epoch ``e`` visits ``randperm(n)`` drawn from a generator seeded ``seed + e`` (or
+    ``arange(n)`` without shuffling), so any epoch's order is reproducible without replaying
+    the earlier ones; ``set_epoch(e, skip)`` makes the next iteration start ``skip`` samples in.
+    """
+
+    def __init__(self, n: int, shuffle: bool, seed: int):
+        self.n, self.shuffle, self.seed = n, shuffle, seed
+        self.epoch, self.skip = 0, 0
+
+    def set_epoch(self, epoch: int, skip: int = 0) -> None:
+        self.epoch, self.skip = epoch, skip
+
+    def __len__(self) -> int:
+        return self.n - self.skip
+
+    def __iter__(self):
+        if self.shuffle:
+            g = torch.Generator().manual_seed(self.seed + self.epoch)
+            order = torch.randperm(self.n, generator=g)
+        else:
+            order = torch.arange(self.n)
+        skip, self.skip = self.skip, 0
+        self.epoch += 1
+        return iter(order[skip:].tolist())
+
+
 def _loader(ds, batch_size, ignore_idx, shuffle, seed, num_workers=0, drop_last=False):
+    sampler = ResumableSampler(len(ds), shuffle, seed)
+    # The generator only feeds DataLoader's per-iteration base seed, keeping the global RNG
+    # untouched by data loading.
     g = torch.Generator()
     g.manual_seed(seed)
-    return DataLoader(ds, batch_size=batch_size, shuffle=shuffle, generator=g,
+    return DataLoader(ds, batch_size=batch_size, sampler=sampler, generator=g,
                       collate_fn=partial(collate_fn, bos=ds.bos, eos=ds.eos, ignore_idx=ignore_idx),
                       num_workers=num_workers, pin_memory=torch.cuda.is_available(), drop_last=drop_last)
+
+
+def resume_position(loader: DataLoader, step: int):
+    """(epoch, batches into that epoch) after ``step`` optimizer steps with one batch per step."""
+    n = loader.sampler.n
+    per_epoch = n // loader.batch_size if loader.drop_last else -(-n // loader.batch_size)
+    per_epoch = max(1, per_epoch)
+    return step // per_epoch, step % per_epoch
+
+
+def seek(loader: DataLoader, step: int) -> int:
+    """Position ``loader`` so its next iteration yields the batch of optimizer step ``step + 1``;
+    returns the epoch that iteration belongs to."""
+    epoch, k = resume_position(loader, step)
+    loader.sampler.set_epoch(epoch, k * loader.batch_size)
+    return epoch
 
 
 def get_dataloader(data_path: str, batch_size: int, ignore_idx: int = IGNORE_INDEX, split: str = "train",

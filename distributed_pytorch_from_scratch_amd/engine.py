@@ -74,10 +74,13 @@ class TrainStep:
         self.optimizer.zero_grad(set_to_none=True)
         with roctx("bwd"):
             loss.backward()
-            if self.sp:
-                allreduce_sequence_parallel_grads(self.model)
+            # DP first: finish() copies the DP-averaged buckets (packed during backward, before
+            # any TP sum) back into .grad; the SP sum over TP must act on those copied-back grads.
+            # The two sums commute, so this order gives sum_tp(mean_dp(g)).
             if self.dp is not None:
                 self.dp.finish()
+            if self.sp:
+                allreduce_sequence_parallel_grads(self.model)
         e2 = self._event()
         with roctx("opt"):
             self.optimizer.step()

@@ -37,6 +37,10 @@ class FusedAdam(torch.optim.Optimizer):
         self._replicated = set(id(p) for p in (replicated_params or []))
         self._tables = {}
 
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._tables = {}   # the cached device tables point at the replaced moment buffers
+
     def _shadow_for(self, p):
         from .dispatch import peek_shadow
         s = peek_shadow(p)
@@ -89,7 +93,10 @@ class FusedAdam(torch.optim.Optimizer):
                 # epilogue reads one (a hipBLASLt bias, ops.gemm_select).
                 shadows = [self._shadow_for(p) if (p.dim() >= 2 or peek_shadow(p) is not None) else None
                            for p in params]
-                key = tuple((p.data_ptr(), s.data_ptr() if s is not None else 0, p.numel())
+                # Every pointer the device table holds is part of the key: load_state_dict()
+                # swaps in new moment tensors, which must force a rebuild.
+                key = tuple((p.data_ptr(), s.data_ptr() if s is not None else 0, p.numel(),
+                             self.state[p]["exp_avg"].data_ptr(), self.state[p]["exp_avg_sq"].data_ptr())
                             for p, s in zip(params, shadows))
                 grads = [p.grad if p.grad.is_contiguous() else p.grad.contiguous() for p in params]
                 gkey = tuple(g.data_ptr() for g in grads)

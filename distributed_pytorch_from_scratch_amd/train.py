@@ -27,7 +27,7 @@ import torch
 import torch.distributed as dist
 
 from .constants import IGNORE_INDEX
-from .data.dataset import get_dataloader, get_synthetic_dataloader
+from .data.dataset import get_dataloader, get_synthetic_dataloader, resume_position, seek
 from .engine import TrainStep
 from .models import Transformer, get_preset
 from .ops.optim import FusedAdam
@@ -141,17 +141,20 @@ def train(rank, args: Namespace):
                 for _ in range(min(start_step, args.max_steps - 1)):
                     sched.step()
             log0(f"resumed from {path} at step {start_step}")
+    # Continue the data stream where the saved run stopped (same epoch order, next batch).
+    start_epoch = seek(loader, start_step)
+    # the epoch holding the last step's batch, plus one
+    max_epoch = max(start_epoch, resume_position(loader, max(0, args.max_steps - 1))[0]) + 1
 
     tag = "vanilla" if args.use_vallina_impl else f"TP-{p.tp_rank}"
     n = start_step
     accum = torch.zeros((), device=dev, dtype=torch.float64)
     accum_host = 0.0
     t_last, n_last = time.time(), n
-    max_epoch = math.ceil(max(1, args.max_steps - n) / max(1, len(loader)))
     flops_tok = margs.flops_per_token(seq_len)
     dist.barrier()
     done = False
-    for epoch in range(max_epoch):
+    for epoch in range(start_epoch, max_epoch):
         for batch in loader:
             ids = batch["input_ids"].to(dev, non_blocking=True)
             tgt = batch["target_ids"].to(dev, non_blocking=True)

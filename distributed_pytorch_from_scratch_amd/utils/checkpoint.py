@@ -83,7 +83,9 @@ def load_resume(path: str, optimizer=None, scheduler=None) -> Optional[dict]:
     side = path + ".optim"
     if not os.path.exists(side):
         return None
-    st = torch.load(side, map_location="cpu", weights_only=False)  # our own file (optimizer state)
+    # Everything in the sidecar is plain data (state dicts, ByteTensor RNG states, ints, dicts),
+    # so the weights-only unpickler loads it; nothing in the file can execute code.
+    st = torch.load(side, map_location="cpu", weights_only=True)
     if optimizer is not None:
         optimizer.load_state_dict(st["optimizer"])
     if scheduler is not None and st.get("scheduler") is not None:

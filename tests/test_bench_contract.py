@@ -57,3 +57,26 @@ def test_bench_recompute_flag_and_baseline_scope():
     assert d["config"]["recompute"] is True
     assert d["vs_baseline"] is None
     assert d["value"] > 0
+
+
+def test_bench_tp_dp_layout():
+    """--tp 2 on 4 ranks: TP pairs {0,1}, {2,3} with DP over them (the `auto` layout for
+    GPT-2 small at N = 4 / 8); every replica gets its own data, the global batch stays 2 x N."""
+    from dist_helpers import _free_port
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+           "--gpus", "4", "--tp", "2", "--model", "plumbing", "--steps", "2", "--warmup", "1", "--seq-len", "64",
+           "--batch-per-gpu", "2"]
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    (d,) = _json_lines(r.stdout)
+    assert d["config"]["parallelism"] in ("tp2dp2", "tp2dp2+sp") and d["config"]["global_batch"] == 8
+    assert d["n_gpus"] == 4 and d["value"] > 0
+
+
+def test_resolve_tp():
+    sys.path.insert(0, ROOT)
+    from bench import resolve_tp
+    assert [resolve_tp("auto", "gpt2-small", n) for n in (1, 2, 4, 8)] == [1, 2, 2, 2]
+    assert [resolve_tp("auto", "llama2-7b", n) for n in (1, 2, 4, 8)] == [1, 2, 4, 8]
+    assert resolve_tp("8", "gpt2-small", 8) == 8 and resolve_tp("3", "gpt2-small", 8) == 2

@@ -170,3 +170,75 @@ def test_reference_tokenizer_fixture_if_present():
     assert [tok.token_to_id(t) for t in ("<BOS>", "<EOS>", "<UNK>")] == [0, 1, 2]
     s = "Nice to meet you, it's"
     assert tok.decode(tok.encode(s).ids).strip() == s
+
+
+def test_resume_reproduces_uninterrupted_run(tmp_path):
+    """Stop at step 4 and resume to step 8 == train 8 steps straight: weights, optimizer,
+    schedule, RNG and the data stream (same epoch order, next batch) all continue exactly."""
+    data = tmp_path / "tokens.json"
+    _token_json(data, V=1024, n=10)          # 5 batches per epoch at -b 2: the run crosses epochs
+    a, b = tmp_path / "a", tmp_path / "b"
+    common = ["train.py", "--tp_size", "2", "--data_path", str(data), "--model", "plumbing", "-b", "2",
+              "--max_steps", "8", "--warmup_steps", "2", "--log_interval", "100", "--device", "cpu"]
+    r = _run(common + ["--save_interval", "4", "--save_dir", str(a), "--master_port", _port()])
+    assert r.returncode == 0, r.stdout + r.stderr
+    os.makedirs(b)
+    for f in glob.glob(str(a / "*_iter-4_*")):
+        import shutil
+        shutil.copy(f, b / os.path.basename(f))
+    r = _run(common + ["--save_interval", "8", "--save_dir", str(b), "--resume", "latest",
+                       "--master_port", _port()])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "resumed from" in r.stdout
+    for rank in (0, 1):
+        fa = glob.glob(str(a / f"tprank-{rank}_iter-8_*.pth"))[0]
+        fb = glob.glob(str(b / f"tprank-{rank}_iter-8_*.pth"))[0]
+        sa, sb = torch.load(fa, weights_only=True), torch.load(fb, weights_only=True)
+        for k in sa:
+            assert torch.equal(sa[k], sb[k]), (rank, k)
+
+
+def test_resumable_sampler_seek():
+    from distributed_pytorch_from_scratch_amd.data.dataset import SyntheticTokenDataset, _loader, seek
+
+    class _Idx(SyntheticTokenDataset):
+        def __getitem__(self, i):
+            return [i + 3]
+
+    def stream(loader, n):
+        out = []
+        while len(out) < n:
+            for bt in loader:
+                out.append(bt["input_ids"][:, 1].tolist())
+                if len(out) == n:
+                    break
+        return out
+
+    ds = _Idx(vocab_size=64, seq_len=4, num_samples=10)
+    full = stream(_loader(ds, 3, -1, shuffle=True, seed=5), 9)      # 4 batches/epoch (last short)
+    for k in (0, 2, 4, 6):
+        ld = _loader(ds, 3, -1, shuffle=True, seed=5)
+        seek(ld, k)
+        assert stream(ld, 9 - k) == full[k:], k
+    assert sorted(sum(full[:4], [])) == list(range(3, 13))         # one epoch = a permutation
+
+
+def test_sidecar_loads_weights_only(tmp_path):
+    """The resume sidecar (optimizer + OneCycleLR + RNG) is plain data: weights_only loads it."""
+    from distributed_pytorch_from_scratch_amd.ops.optim import FusedAdam
+    from distributed_pytorch_from_scratch_amd.utils import checkpoint as ck
+    m = torch.nn.Linear(4, 3)
+    opt = FusedAdam(m.parameters(), lr=1e-3)
+    sched = torch.optim.lr_scheduler.OneCycleLR(opt, 1e-3, total_steps=10, pct_start=0.2)
+    m(torch.randn(2, 4)).sum().backward()
+    opt.step()
+    sched.step()
+    path = ck.save_checkpoint(m, str(tmp_path), 0, 1, 1.0, opt, sched)
+    side = torch.load(path + ".optim", weights_only=True)
+    assert side["step"] == 1
+    opt2 = FusedAdam(torch.nn.Linear(4, 3).parameters(), lr=1e-3)
+    sched2 = torch.optim.lr_scheduler.OneCycleLR(opt2, 1e-3, total_steps=10, pct_start=0.2)
+    st = ck.load_resume(path, opt2, sched2)
+    assert st["step"] == 1 and sched2.state_dict()["last_epoch"] == 1
+    s1, s2 = opt.state_dict()["state"], opt2.state_dict()["state"]
+    assert all(torch.equal(s1[i]["exp_avg"], s2[i]["exp_avg"]) for i in s1)

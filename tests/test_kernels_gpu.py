@@ -451,3 +451,31 @@ def test_fused_adam_fresh_grad_tensors_each_step(C):
         topt.step()
     for p, r in zip(ps, ref):
         assert (p.detach() - r.detach()).abs().max().item() < 1e-5
+
+
+def test_fused_adam_load_state_dict_after_first_step(C):
+    """load_state_dict() after the device table exists swaps in new moment tensors: the next
+    step must read the loaded moments (not the freed ones the cached table pointed at)."""
+    from distributed_pytorch_from_scratch_amd.ops.optim import FusedAdam
+    torch.manual_seed(13)
+    shapes = [(257, 96), (5000,)]
+    ps = [torch.nn.Parameter(torch.randn(*s, device=DEV)) for s in shapes]
+    donor = [torch.nn.Parameter(torch.randn(*s, device=DEV)) for s in shapes]
+    opt = FusedAdam(ps, lr=1e-3)
+    dopt = FusedAdam(donor, lr=1e-3)
+    for _ in range(3):                         # build opt's table; give the donor other moments
+        for p, q in zip(ps, donor):
+            p.grad, q.grad = torch.randn_like(p), 5 * torch.randn_like(q)
+        opt.step()
+        dopt.step()
+    opt.load_state_dict(dopt.state_dict())
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    topt = torch.optim.Adam(ref, lr=1e-3)
+    topt.load_state_dict(dopt.state_dict())
+    gs = [torch.randn_like(p) for p in ps]
+    for p, r, g in zip(ps, ref, gs):
+        p.grad, r.grad = g, g.clone()
+    opt.step()
+    topt.step()
+    for p, r in zip(ps, ref):
+        assert (p.detach() - r.detach()).abs().max().item() < 1e-5
