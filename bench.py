@@ -78,6 +78,9 @@ def resolve_tp(tp: str, model: str, world: int) -> int:
 
 def main():
     a = parse()
+    if os.environ.get("DPFS_STACK_DUMP_S"):   # hang diagnosis: every rank prints its Python stacks
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["DPFS_STACK_DUMP_S"]), repeat=True)
     from distributed_pytorch_from_scratch_amd.models import get_preset, Transformer
     from distributed_pytorch_from_scratch_amd.ops.optim import FusedAdam
     from distributed_pytorch_from_scratch_amd.engine import TrainStep

@@ -137,7 +137,7 @@ class DecoderTrainFn(torch.autograd.Function):
                 else:
                     h1, r1 = k.rmsnorm_fwd(s["x"], L.s1, L.eps1)
                 x = s["x"]
-                qkv = k.gemm_nt(h1, W(L.wqkv), L.bqkv, s["pos"], tab, 2 * L.h, L.hd)  # RoPE in the epilogue
+                qkv = GS.gemm_nt_rope(k, h1, W(L.wqkv), L.bqkv, s["pos"], tab, 2 * L.h, L.hd)  # RoPE in the epilogue
                 Mc = x.size(0)
                 Bc = s["B"]
                 q, kk, v = _split(qkv, Bc, T, L.h, L.hd)
@@ -266,7 +266,7 @@ class DecoderTrainFn(torch.autograd.Function):
             for s in st:
                 a = s["layers"][li]
                 a["h1"], a["r1"] = k.rmsnorm_fwd(a["x"], L.s1, L.eps1)
-                a["qkv"] = k.gemm_nt(a["h1"], W(L.wqkv), L.bqkv, s["pos"], tab, 2 * L.h, L.hd)
+                a["qkv"] = GS.gemm_nt_rope(k, a["h1"], W(L.wqkv), L.bqkv, s["pos"], tab, 2 * L.h, L.hd)
                 q, kk, v = _split(a["qkv"], s["B"], T, L.h, L.hd)
                 a["o"], a["lse"] = k.attn_fwd(q, kk, v, 1.0 / math.sqrt(L.hd), True)
                 pout = GS.gemm_nt(k, a["o"].view(a["qkv"].size(0), L.h * L.hd), W(L.wo), None)

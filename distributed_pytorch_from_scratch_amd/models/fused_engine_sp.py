@@ -98,7 +98,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
             for ci, s in enumerate(st):    # P2: QKV (+RoPE), attention, Wo -> reduce-scatter
                 _wait(s["h"])
                 a = s["layers"][-1]
-                qkv = k.gemm_nt(a["h1"], W(L.wqkv), L.bqkv, s["pos"], tab, 2 * L.h, L.hd)
+                qkv = GS.gemm_nt_rope(k, a["h1"], W(L.wqkv), L.bqkv, s["pos"], tab, 2 * L.h, L.hd)
                 q, kk, v = _split(qkv, s["B"], T, L.h, L.hd)
                 o, lse = k.attn_fwd(q, kk, v, 1.0 / math.sqrt(L.hd), True)
                 pout = GS.gemm_nt(k, o.view(qkv.size(0), L.h * L.hd), W(L.wo), None,
@@ -210,7 +210,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
             for ci, s in enumerate(st):
                 a = s["layers"][li]
                 _wait(a.pop("hh"))
-                a["qkv"] = k.gemm_nt(a["h1"], W(L.wqkv), L.bqkv, s["pos"], tab, 2 * L.h, L.hd)
+                a["qkv"] = GS.gemm_nt_rope(k, a["h1"], W(L.wqkv), L.bqkv, s["pos"], tab, 2 * L.h, L.hd)
                 q, kk, v = _split(a["qkv"], s["B"], T, L.h, L.hd)
                 a["o"], a["lse"] = k.attn_fwd(q, kk, v, 1.0 / math.sqrt(L.hd), True)
                 pout = GS.gemm_nt(k, a["o"].view(a["qkv"].size(0), L.h * L.hd), W(L.wo), None,

@@ -115,14 +115,87 @@ def gemm_nn(k, a: torch.Tensor, b: torch.Tensor, out=None) -> torch.Tensor:
     return blas() if _pick(key, ours, blas) == "blas" else ours()
 
 
-def gemm_tn(k, a: torch.Tensor, b: torch.Tensor, out=None, accumulate: bool = False) -> torch.Tensor:
-    """fp32 c[M,N] (+)= a[K,M]^T b[K,N] (weight gradients).  Always our split-K kernel, except
-    for rows our kernel cannot stage (M or N not a multiple of 8: uneven vocab shards)."""
-    if k is reference or not a.is_cuda or _aligned(a.shape[1], b.shape[1]):
-        return k.gemm_tn(a, b, out, accumulate) if out is not None else k.gemm_tn(a, b)
-    c = torch.matmul(a.t(), b).float()
+def gemm_nt_rope(k, x: torch.Tensor, w: torch.Tensor, bias, pos, tab, rot_heads: int, hd: int) -> torch.Tensor:
+    """Packed QKV projection with rotate-half RoPE on the first ``rot_heads`` heads: our NT
+    kernel with the rotation in its epilogue, or hipBLASLt followed by the in-place RoPE
+    kernel (timed per shape like every plain GEMM)."""
+    m = mode()
+    if k is reference or not x.is_cuda or m == "ours" or not _aligned(x.shape[1], w.shape[0]) \
+            or x.shape[0] < _MIN_ROWS:
+        return k.gemm_nt(x, w, bias, pos, tab, rot_heads, hd)
+    bb = shadow(bias, x.dtype) if bias is not None else None
+
+    def blas():
+        y = F.linear(x, w, bb)
+        k.rope_(y, pos, tab, rot_heads, hd)
+        return y
+
+    def ours():
+        return k.gemm_nt(x, w, bias, pos, tab, rot_heads, hd)
+    if m == "blas":
+        return blas()
+    key = ("nt_rope", x.shape[0], w.shape[0], x.shape[1], hd, x.device.index)
+    return blas() if _pick(key, ours, blas) == "blas" else ours()
+
+
+_TN_BLAS = {}   # device index -> whether hipBLASLt's bf16 x bf16 -> fp32 mm works on this build
+
+
+def _blas_tn(a: torch.Tensor, b: torch.Tensor, out, accumulate: bool) -> torch.Tensor:
+    """hipBLASLt fp32-output wgrad: c[M,N] (+)= a[K,M]^T b[K,N] via aten mm/addmm(out_dtype)."""
+    at = a.t()
     if out is None:
-        return c
+        return torch.mm(at, b, out_dtype=torch.float32)
     if accumulate:
-        return out.add_(c)
-    return out.copy_(c)
+        return torch.addmm(out, at, b, out_dtype=torch.float32, out=out)
+    return torch.mm(at, b, out_dtype=torch.float32, out=out)
+
+
+def _tn_blas_ok(a, b) -> bool:
+    dev = a.device.index
+    ok = _TN_BLAS.get(dev)
+    if ok is None:
+        try:   # functional probe on a small problem against an fp32 matmul (incl. accumulate)
+            g = torch.Generator(device=a.device).manual_seed(0)
+            pa = torch.randn(96, 32, device=a.device, generator=g).to(a.dtype)
+            pb = torch.randn(96, 40, device=a.device, generator=g).to(a.dtype)
+            ref = pa.float().t() @ pb.float()
+            c = _blas_tn(pa, pb, None, False)
+            c2 = _blas_tn(pa, pb, c.clone(), True)
+            ok = c.dtype == torch.float32 and bool(torch.allclose(c, ref, atol=1e-2, rtol=1e-3)) and \
+                bool(torch.allclose(c2, 2 * ref, atol=2e-2, rtol=1e-3))
+        except Exception:   # this torch / ROCm build has no bf16 -> fp32 mm: ours only
+            ok = False
+        _TN_BLAS[dev] = ok
+    return ok
+
+
+def gemm_tn(k, a: torch.Tensor, b: torch.Tensor, out=None, accumulate: bool = False) -> torch.Tensor:
+    """fp32 c[M,N] (+)= a[K,M]^T b[K,N] (weight gradients): our split-K kernel or hipBLASLt
+    with fp32 output, timed per (shape, accumulate) on a scratch output (an accumulating
+    candidate must not be timed into the live gradient)."""
+    if k is reference or not a.is_cuda:
+        return k.gemm_tn(a, b, out, accumulate) if out is not None else k.gemm_tn(a, b)
+    if not _aligned(a.shape[1], b.shape[1]):
+        c = torch.matmul(a.t(), b).float()
+        if out is None:
+            return c
+        if accumulate:
+            return out.add_(c)
+        return out.copy_(c)
+
+    def run(kind, dst, acc):
+        if kind == "blas":
+            return _blas_tn(a, b, dst, acc)
+        return k.gemm_tn(a, b, dst, acc) if dst is not None else k.gemm_tn(a, b)
+    m = mode()
+    if m == "ours" or a.shape[0] < _MIN_ROWS or not _tn_blas_ok(a, b):
+        return run("ours", out, accumulate)
+    if m == "blas":
+        return run("blas", out, accumulate)
+    key = ("tn", a.shape[1], b.shape[1], a.shape[0], bool(accumulate), a.device.index)
+    c = _choice.get(key)
+    if c is None:
+        scratch = torch.zeros(a.shape[1], b.shape[1], device=a.device, dtype=torch.float32)
+        c = _pick(key, lambda: run("ours", scratch, accumulate), lambda: run("blas", scratch, accumulate))
+    return run(c, out, accumulate)

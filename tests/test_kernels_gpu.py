@@ -468,10 +468,13 @@ def test_fused_adam_load_state_dict_after_first_step(C):
             p.grad, q.grad = torch.randn_like(p), 5 * torch.randn_like(q)
         opt.step()
         dopt.step()
-    opt.load_state_dict(dopt.state_dict())
+    import copy
+    # deep copies: load_state_dict keeps same-device tensors by reference, and the two
+    # optimisers must not share (and double-update) one set of moments
+    opt.load_state_dict(copy.deepcopy(dopt.state_dict()))
     ref = [torch.nn.Parameter(p.detach().clone()) for p in ps]
     topt = torch.optim.Adam(ref, lr=1e-3)
-    topt.load_state_dict(dopt.state_dict())
+    topt.load_state_dict(copy.deepcopy(dopt.state_dict()))
     gs = [torch.randn_like(p) for p in ps]
     for p, r, g in zip(ps, ref, gs):
         p.grad, r.grad = g, g.clone()
@@ -479,3 +482,34 @@ def test_fused_adam_load_state_dict_after_first_step(C):
     topt.step()
     for p, r in zip(ps, ref):
         assert (p.detach() - r.detach()).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("backend", ["blas", "auto"])
+def test_gemm_select_tn_and_qkv_rope_paths(C, backend, monkeypatch):
+    """gemm_select's hipBLASLt candidates for the fp32 wgrad (incl. accumulate into a live
+    gradient) and for the RoPE'd QKV projection match the fp32 oracle; `auto` times both on a
+    scratch output, so the live accumulator is updated exactly once."""
+    from distributed_pytorch_from_scratch_amd.ops import gemm_select as GS
+    monkeypatch.setenv("DPFS_GEMM_BACKEND", backend)
+    GS._choice.clear()
+    torch.manual_seed(21)
+    K_, M_, N_ = 1024, 384, 256
+    a = torch.randn(K_, M_, device=DEV).bfloat16()
+    b = torch.randn(K_, N_, device=DEV).bfloat16()
+    ref = a.float().t() @ b.float()
+    c = GS.gemm_tn(C, a, b)
+    assert c.dtype == torch.float32 and _rel(c, ref) < 1e-3
+    acc = ref.clone()
+    GS.gemm_tn(C, a, b, acc, True)
+    assert _rel(acc, 2 * ref) < 1e-3
+    # QKV + RoPE (2 rotated heads of 64 = q|k, then v)
+    Mx, Kx, H, hd = 512, 256, 2, 64
+    x = torch.randn(Mx, Kx, device=DEV).bfloat16()
+    w = torch.randn(3 * H * hd, Kx, device=DEV).bfloat16() * 0.05
+    bias = torch.randn(3 * H * hd, device=DEV) * 0.1
+    pos = torch.arange(Mx, device=DEV) % 128
+    tab = R.rope_table(256, hd, 10000.0, device=DEV)
+    y = GS.gemm_nt_rope(C, x, w, bias, pos, tab, 2 * H, hd)
+    yr = R.gemm_nt(x.float(), w.float(), bias, pos, tab, 2 * H, hd)
+    assert _rel(y, yr) < 1e-2
+    GS._choice.clear()
