@@ -879,7 +879,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_force", [](int cfg, int splits) { dpfs_gemm_force(cfg, splits); },
         "force the v2 tile config (-1 auto, 0 = 256x256, 1 = 256x128) and K-splits (0 auto)");
   m.def("gemm_v2_sched", [](int v) { dpfs_gemm_v2_sched(v); }, "v2 256x256 schedule (-1 per-layout default, 0..4 see gemm2_k SCHED)");
-  m.def("gemm_set_impl", [](int v) { dpfs_gemm_set_impl(v); }, "1 = v1 (128x128 register-staged), 2 = v2 (LDS-DMA, default)");
+  m.def("gemm_set_impl", [](int v) { dpfs_gemm_set_impl(v); }, "1 = v1 (128x128 register-staged), 2 = v2 (LDS-DMA, one tile per workgroup), 3 = v3 (persistent v2, default)");
   m.def("gemm_tn", &gemm_tn, py::arg("a"), py::arg("b"), py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("bias_grad", &bias_grad);
   m.def("add_bias_", &add_bias_);

@@ -30,6 +30,8 @@
 //    (deterministic, no float atomics).
 #include "common.h"
 
+#include <algorithm>
+
 namespace dpfs {
 
 constexpr int BM = 128, BN = 128, BKK = 64;
@@ -506,6 +508,211 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 2 : 1) void gemm2_k(const bf16
   }
 }
 
+// ============================================================= GEMM v3 (persistent) ====
+// gemm2_k's 256-wide tile, made persistent: one workgroup per CU walks the (split, tile)
+// items i = r, r + G, r + 2G, ... (r = XCD-remapped block id, G = grid), so the per-tile
+// fixed cost the one-tile-per-workgroup kernel pays on short-K shapes (K = 768: ~40 % of its
+// time on MI355X) overlaps the neighbouring tiles' MFMA work:
+//  * the LAST K-step of an item issues the LDS-DMA of the NEXT item's first K-tile (the
+//    stage the K-loop would have filled next), so the next item's operands are in flight
+//    while this item's MFMAs drain and its epilogue stores issue — no pipeline restart;
+//  * epilogue stores are buffer stores with out-of-range lanes dropped by the descriptor
+//    bound (no per-lane branches): every wave issues exactly TM*TN stores, so the next
+//    item's first wait is a counted `vmcnt(TM*TN)` that retires the prefetched tile without
+//    waiting for the stores to drain;
+//  * item order: grouped (GROUP_M tile rows, then the next tile column), and the XCD remap
+//    makes the items running concurrently on one XCD a contiguous run = a GROUP_M x (32 /
+//    GROUP_M) block of tiles sharing A rows and B columns in that XCD's L2.
+// NSTAGE = 2 (two 64-deep K stages, 128 KiB LDS at 256x256), SCHED as gemm2_k (2 or 4).
+template <int BM_, int BN_, int WAVES_M, bool AK, bool BKM, int OUT, int SCHED>
+__global__ __launch_bounds__(512, 1) void gemmp_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                  void* __restrict__ C, const float* __restrict__ bias, int M, int N,
+                                                  int K, int lda, int ldb, int ldc, int k_per_split, int splits,
+                                                  long long slab_stride, unsigned a_bytes, unsigned b_bytes,
+                                                  unsigned c_bytes, RopeArgs rope, int group_m) {
+  constexpr int NWV = 8;
+  constexpr int WAVES_N = NWV / WAVES_M;
+  constexpr int WM = BM_ / WAVES_M, WN = BN_ / WAVES_N;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int A_BYTES = BM_ * 128, B_BYTES = BN_ * 128, STAGE = A_BYTES + B_BYTES;
+  constexpr int PA = BM_ / 8 / NWV, PB = BN_ / 8 / NWV;
+  constexpr int PIECES = PA + PB;
+  constexpr int STORES = TM * TN;
+  static_assert(STORES < 64 && PIECES < 64, "vmcnt range");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int tiles_n = (N + BN_ - 1) / BN_;
+  const int tiles_m = (M + BM_ - 1) / BM_;
+  const int nwg = tiles_m * tiles_n;
+  const int total = nwg * splits;
+  const int G = gridDim.x;
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int l = lane_id();
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (int)b_bytes, 0x00020000);
+
+  auto decode = [&](int lin, int& m0, int& n0, int& kb, int& ke, int& split) {
+    split = lin / nwg;
+    const int wg = lin - split * nwg;
+    const int per_group = group_m * tiles_n;
+    const int gid = wg / per_group;
+    const int first_m = gid * group_m;
+    const int gsz = min(tiles_m - first_m, group_m);
+    const int r = wg - gid * per_group;
+    m0 = (first_m + r % gsz) * BM_;
+    n0 = (r / gsz) * BN_;
+    kb = split * k_per_split;
+    ke = min(K, kb + k_per_split);
+  };
+
+  int it = xcd_remap(blockIdx.x, G);
+  if (it >= total) return;
+  int m0, n0, kb, ke, split;
+  decode(it, m0, n0, kb, ke, split);
+  issue_tile<AK, BM_, NWV>(ra, smem, m0, kb, lda, ke);
+  issue_tile<BKM, BN_, NWV>(rb, smem + A_BYTES, n0, kb, ldb, ke);
+  int cur = 0;
+  bool first = true;
+  for (; it < total; it += G) {
+    const bool has_next = it + G < total;
+    int m0n = 0, n0n = 0, kbn = 0, ken = 0, splitn = 0;
+    if (has_next) decode(it + G, m0n, n0n, kbn, ken, splitn);
+    const int nk = max(1, (ke - kb + 63) / 64);   // an empty K-split runs one all-zero step
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    for (int t = 0; t < nk; ++t) {
+      // The tile of step t is the youngest DMA batch but for the previous item's epilogue
+      // stores (issued after it) at t == 0.
+      if (t == 0 && !first) wait_vmcnt<STORES>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();  // tile t landed for all waves; the other stage is free
+      const bool in_item = t + 1 < nk;
+      const bool more = in_item || has_next;
+      const int pm0 = in_item ? m0 : m0n, pn0 = in_item ? n0 : n0n;
+      const int pk = in_item ? kb + (t + 1) * 64 : kbn, pke = in_item ? ke : ken;
+      char* nst = smem + (cur ^ 1) * STAGE;
+      const char* la = smem + cur * STAGE;
+      const char* lb = la + A_BYTES;
+      auto piece = [&](int q) {
+        if (q < PA) issue_piece<AK, BM_, NWV>(ra, nst, pm0, pk, lda, pke, q);
+        else issue_piece<BKM, BN_, NWV>(rb, nst + A_BYTES, pn0, pk, ldb, pke, q - PA);
+      };
+      if constexpr (SCHED == 4) {
+        bf16x8 fa[2][TM], fb[2][TN];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) fb[s][j] = frag2<BKM, BN_>(lb, wn * WN + 16 * j, 32 * s);
+#pragma unroll
+          for (int i = 0; i < TM; ++i) fa[s][i] = frag2<AK, BM_>(la, wm * WM + 16 * i, 32 * s);
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[s][j], fa[s][i], acc[i][j], 0, 0, 0);
+            if (s == 0 && more) {
+#pragma unroll
+              for (int q = 0; q < PIECES; ++q)
+                if ((q * TM) / PIECES == i) piece(q);
+            }
+          }
+          __builtin_amdgcn_s_setprio(0);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 fa[TM], fb[TN];
+#pragma unroll
+          for (int i = 0; i < TM; ++i) fa[i] = frag2<AK, BM_>(la, wm * WM + 16 * i, 32 * s);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) fb[j] = frag2<BKM, BN_>(lb, wn * WN + 16 * j, 32 * s);
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+            if (s == 0 && more) {
+#pragma unroll
+              for (int q = 0; q < PIECES; ++q)
+                if ((q * TM) / PIECES == i) piece(q);
+            }
+          }
+          __builtin_amdgcn_s_setprio(0);
+        }
+      }
+      cur ^= 1;
+    }
+
+    // Epilogue (as gemm2_k): lane holds C[m = .. + (l&15)][n = .. + 4g + r]; every wave issues
+    // exactly TM*TN buffer stores, out-of-range lanes get an offset past num_records.
+    const int g = l >> 4;
+    const int wcol0 = n0 + wn * WN;
+    char* cbase = reinterpret_cast<char*>(C) + (OUT == 1 ? (long long)split * slab_stride * 4 : 0);
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)cbase, (short)0, (int)c_bytes, 0x00020000);
+    const bool do_rope = (OUT == 0) && (WN % 64 == 0) && rope.cols > 0 && wcol0 < rope.cols;
+    f32x4 bv[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = wcol0 + 16 * j + 4 * g;
+      bv[j] = (OUT == 0 && bias && n < N) ? *reinterpret_cast<const f32x4*>(bias + n) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm * WM + 16 * i + (l & 15);
+      f32x4 v[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) v[j] = acc[i][j] + bv[j];
+      if constexpr (OUT == 0 && WN % 64 == 0) {
+        if (do_rope && m < M) {
+          const float* tr = rope.tab + rope.pos[m] * 64;
+#pragma unroll
+          for (int hg = 0; hg < WN / 64; ++hg) {
+            if (wcol0 + 64 * hg >= rope.cols) break;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const f32x4 cs = *reinterpret_cast<const f32x4*>(tr + 16 * j + 4 * g);
+              const f32x4 sn = *reinterpret_cast<const f32x4*>(tr + 32 + 16 * j + 4 * g);
+              const f32x4 x1 = v[4 * hg + j], x2 = v[4 * hg + j + 2];
+              v[4 * hg + j] = x1 * cs - x2 * sn;
+              v[4 * hg + j + 2] = x2 * cs + x1 * sn;
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = wcol0 + 16 * j + 4 * g;
+        const bool ok = m < M && n < N;
+        if (OUT == 0) {
+          const unsigned off = ok ? (unsigned)(((long long)m * ldc + n) * 2) : kOOB;
+          bf16x4 o = {(bf16)v[j][0], (bf16)v[j][1], (bf16)v[j][2], (bf16)v[j][3]};
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), rc, off, 0, 0);
+        } else {
+          const unsigned off = ok ? (unsigned)(((long long)m * ldc + n) * 4) : kOOB;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[j]), rc, off, 0, 0);
+        }
+      }
+    }
+    first = false;
+    m0 = m0n;
+    n0 = n0n;
+    kb = kbn;
+    ke = ken;
+    split = splitn;
+  }
+}
+
 // bf16 out[m*ldc + n] = sum_s slab[s][m*N + n] (+ bias[n]), fixed order; N % 4 == 0.
 __global__ __launch_bounds__(256) void splitk_reduce_bf16_k(const float* __restrict__ slabs, bf16* __restrict__ out,
                                                             const float* __restrict__ bias, int M, int N, int ldc,
@@ -581,6 +788,50 @@ static void launch2(int cfg, const void* A, const void* B, void* C, const float*
   }
 }
 
+// Persistent v3 launch (gemmp_k): grid = min(items, CUs) (one 512-thread workgroup per CU:
+// 128 KiB LDS), NSTAGE 2 for both tile shapes.  Returns false when an operand / output span
+// does not fit the 32-bit buffer descriptors (then the caller runs v2).
+static int g_group_m = 4;
+extern "C" void dpfs_gemm_group_m(int g) { g_group_m = g > 0 ? g : 4; }
+static int cu_count() {
+  static int n[16] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 16) dev = 0;
+  if (n[dev] == 0) {
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+    n[dev] = c;
+  }
+  return n[dev];
+}
+template <bool AK, bool BKM, int OUT>
+static bool launchp(int cfg, const void* A, const void* B, void* C, const float* bias, int M, int N, int K, int lda,
+                    int ldb, int ldc, int splits, int kps, long long slab, unsigned ab, unsigned bb, hipStream_t s,
+                    RopeArgs rope = RopeArgs{nullptr, nullptr, 0}) {
+  const long long cspan = M > 0 ? ((long long)(M - 1) * ldc + N) * (OUT == 1 ? 4 : 2) : 0;
+  if (cspan >= (1ll << 32) - 16) return false;
+  const int bm = 256, bn = cfg == 0 ? 256 : 128;
+  const long long items = (long long)tiles2(M, N, bm, bn) * splits;
+  if (items <= 0 || items >= (1ll << 31)) return false;
+  const int grid = (int)std::min<long long>(items, cu_count());
+  const int sched = v2_sched<AK, BKM>() == 4 ? 4 : 2;
+  const unsigned cb = (unsigned)cspan;
+#define DPFS_GEMMP(BN_, WM_, SC_)                                                                                    \
+  gemmp_k<256, BN_, WM_, AK, BKM, OUT, SC_><<<grid, 512, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K,  \
+                                                                lda, ldb, ldc, kps, splits, slab, ab, bb, cb, rope, \
+                                                                g_group_m)
+  if (cfg == 0) {
+    if (sched == 4) DPFS_GEMMP(256, 2, 4);
+    else DPFS_GEMMP(256, 2, 2);
+  } else {
+    if (sched == 4) DPFS_GEMMP(128, 4, 4);
+    else DPFS_GEMMP(128, 4, 2);
+  }
+#undef DPFS_GEMMP
+  return true;
+}
+
 static int g_force_cfg = -1;     // -1 auto, 0 = 256x256, 1 = 256x128 (tuning / A-B runs)
 static int g_force_splits = 0;   // 0 auto
 extern "C" void dpfs_gemm_force(int cfg, int splits) {
@@ -612,7 +863,7 @@ static int bf16_splits(int M, int N, int K) {
   return v2_splits(M, N, K, pick_cfg(M, N, 1));
 }
 
-static int g_gemm_impl = 2;  // 2 = v2 (default), 1 = v1
+static int g_gemm_impl = 3;  // 3 = v3 persistent (default), 2 = v2 one tile per workgroup, 1 = v1
 extern "C" void dpfs_gemm_set_impl(int v) { g_gemm_impl = v; }
 
 static thread_local float* g_ws = nullptr;  // split-K workspace for bf16 outputs (set by host)
@@ -639,14 +890,19 @@ static void bf16_gemm(const void* A, const void* B, void* C, const float* bias, 
   if (S > 1 && g_ws && g_ws_floats >= (long long)S * M * N) {
     int kps = (K + S - 1) / S;
     kps = ((kps + BKK - 1) / BKK) * BKK;
-    launch2<true, BKM, 1>(pick_cfg(M, N, S), A, B, g_ws, nullptr, M, N, K, lda, ldb, N, S, kps, (long long)M * N, ab,
-                          bb, s);
+    if (g_gemm_impl != 3 || !launchp<true, BKM, 1>(pick_cfg(M, N, S), A, B, g_ws, nullptr, M, N, K, lda, ldb, N, S,
+                                                    kps, (long long)M * N, ab, bb, s))
+      launch2<true, BKM, 1>(pick_cfg(M, N, S), A, B, g_ws, nullptr, M, N, K, lda, ldb, N, S, kps, (long long)M * N, ab,
+                            bb, s);
     long long g = ((long long)M * N / 4 + 255) / 256;
     if (g > 4096) g = 4096;
     splitk_reduce_bf16_k<<<(int)g, 256, 0, s>>>(g_ws, (bf16*)C, bias, M, N, ldc, S);
     if (rope.cols > 0) dpfs_rope_after_gemm(C, rope, M, ldc, s);
     return;
   }
+  if (g_gemm_impl == 3 && launchp<true, BKM, 0>(pick_cfg(M, N, 1), A, B, C, bias, M, N, K, lda, ldb, ldc, 1, K, 0, ab,
+                                                bb, s, rope))
+    return;
   launch2<true, BKM, 0>(pick_cfg(M, N, 1), A, B, C, bias, M, N, K, lda, ldb, ldc, 1, K, 0, ab, bb, s, rope);
 }
 
@@ -778,7 +1034,9 @@ extern "C" void dpfs_gemm_tn(const void* A, const void* B, float* C, float* ws, 
     gemm_k<false, false, 1><<<dim3(tiles_of(M, N), S), 256, 0, s>>>((const bf16*)A, (const bf16*)B, dst, nullptr, M,
                                                                    N, K, lda, ldb, N, direct ? K : kps,
                                                                    direct ? 0 : n);
-  } else {
+  } else if (g_gemm_impl != 3 ||
+             !launchp<false, false, 1>(cfg, A, B, dst, nullptr, M, N, K, lda, ldb, N, S, direct ? K : kps,
+                                       direct ? 0 : n, span_bytes(K, lda, M), span_bytes(K, ldb, N), s)) {
     launch2<false, false, 1>(cfg, A, B, dst, nullptr, M, N, K, lda, ldb, N, S, direct ? K : kps,
                              direct ? 0 : n, span_bytes(K, lda, M), span_bytes(K, ldb, N), s);
   }

@@ -369,10 +369,13 @@ def test_ce_bwd_fused_bias_grad(C, M, V, valid, start):
 
 @pytest.mark.parametrize("impl,cfg,splits,sched", [(2, -1, 0, -1), (2, 0, 1, 0), (2, 0, 1, 1), (2, 0, 1, 2),
                                                   (2, 0, 1, 3), (2, 0, 1, 4), (2, 1, 1, -1), (2, 0, 3, -1),
-                                                  (2, 1, 2, -1), (2, 0, 7, 4), (1, -1, 0, -1)])
+                                                  (2, 1, 2, -1), (2, 0, 7, 4), (1, -1, 0, -1),
+                                                  (3, -1, 0, -1), (3, 0, 1, 2), (3, 0, 1, 4), (3, 1, 1, -1),
+                                                  (3, 0, 3, -1), (3, 1, 2, -1), (3, 0, 7, 4), (3, 1, 5, 2)])
 def test_gemm_plans(C, impl, cfg, splits, sched):
-    """Every GEMM variant (tile configs, K-splits, DMA schedules, v1) on ragged shapes, all
-    three layouts, TN with and without accumulate."""
+    """Every GEMM variant (v3 persistent / v2 / v1, tile configs, K-splits incl. empty
+    trailing splits, DMA schedules) on ragged shapes, all three layouts, TN with and without
+    accumulate."""
     torch.manual_seed(17)
     M, N, K = 8200, 2104, 712
     a = torch.randn(M, K, device=DEV).bfloat16()
@@ -393,7 +396,7 @@ def test_gemm_plans(C, impl, cfg, splits, sched):
         C.gemm_tn(at, bn, acc, True)
         assert _rel(acc, want) < 1e-2
     finally:
-        C.gemm_set_impl(2)
+        C.gemm_set_impl(3)
         C.gemm_force(-1, 0)
         C.gemm_v2_sched(-1)
 

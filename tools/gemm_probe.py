@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--sched", type=int, nargs="+", default=[-1])
     ap.add_argument("--cfg", type=int, nargs="+", default=[-1])
+    ap.add_argument("--blas", action="store_true", help="also time hipBLASLt (torch) on the same layout")
+    ap.add_argument("--check", action="store_true", help="relative error of each implementation vs fp32 torch")
     a = ap.parse_args()
     C = _ext.require()
     M, N, K = a.M, a.N, a.K
@@ -29,10 +31,16 @@ def main():
     w = torch.randn(N, K, device="cuda").bfloat16()
     dy = torch.randn(M, N, device="cuda").bfloat16()
     fn = {"nt": lambda: C.gemm_nt(x, w, None), "nn": lambda: C.gemm_nn(dy, w), "tn": lambda: C.gemm_tn(dy, x)}[a.layout]
-    for impl, sched, cfg in [(i, sc, cf) for i in a.impl for sc in (a.sched if i == 2 else [0]) for cf in a.cfg]:
+    ref = {"nt": lambda: x.float() @ w.float().t(), "nn": lambda: dy.float() @ w.float(),
+           "tn": lambda: dy.float().t() @ x.float()}[a.layout]() if a.check else None
+    for impl, sched, cfg in [(i, sc, cf) for i in a.impl for sc in (a.sched if i >= 2 else [0]) for cf in a.cfg]:
         C.gemm_set_impl(impl)
         C.gemm_v2_sched(sched)
         C.gemm_force(cfg, 0)
+        if ref is not None:
+            out = fn().float()
+            err = ((out - ref).norm() / ref.norm()).item()
+            print(f"impl {impl} sched {sched} cfg {cfg} {a.layout} {M}x{N}x{K}: rel err {err:.2e}", flush=True)
         for _ in range(a.iters):
             fn()
         torch.cuda.synchronize()
@@ -44,9 +52,23 @@ def main():
         torch.cuda.synchronize()
         ms = s.elapsed_time(e) / a.iters
         print(f"impl {impl} sched {sched} cfg {cfg} {a.layout} {M}x{N}x{K}: {ms:.4f} ms {2.0 * M * N * K / ms / 1e9:.1f} TF", flush=True)
-    C.gemm_set_impl(2)
+    C.gemm_set_impl(3)
     C.gemm_v2_sched(-1)
     C.gemm_force(-1, 0)
+    if a.blas:
+        bfn = {"nt": lambda: torch.nn.functional.linear(x, w), "nn": lambda: torch.matmul(dy, w),
+               "tn": lambda: torch.mm(dy.t(), x, out_dtype=torch.float32)}[a.layout]
+        for _ in range(a.iters):
+            bfn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.iters):
+            bfn()
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / a.iters
+        print(f"hipBLASLt {a.layout} {M}x{N}x{K}: {ms:.4f} ms {2.0 * M * N * K / ms / 1e9:.1f} TF", flush=True)
 
 
 if __name__ == "__main__":

@@ -45,7 +45,7 @@ def main():
                     def g():
                         C.gemm_set_impl(impl); C.gemm_force(cfg, sp)
                         fn()
-                        C.gemm_set_impl(2); C.gemm_force(-1, 0)
+                        C.gemm_set_impl(3); C.gemm_force(-1, 0)
                     return g
                 variants["v1"] = mk(1, -1, 0)
                 variants["auto"] = mk(2, -1, 0)
