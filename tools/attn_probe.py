@@ -44,6 +44,14 @@ def main():
             else:
                 C.attn_fwd(q, k, v, scale, True)
         return g
+    if not a.bwd:   # forward outputs of every implementation against impl 1
+        C.attn_set_impl(1)
+        o1, l1 = C.attn_fwd(q, k, v, scale, True)
+        for impl in a.impl:
+            C.attn_set_impl(impl)
+            oi, li = C.attn_fwd(q, k, v, scale, True)
+            print(f"impl {impl} vs 1: max|dO| {(oi.float() - o1.float()).abs().max().item():.3e} "
+                  f"max|dLSE| {(li - l1).abs().max().item():.3e}", flush=True)
     res = timeit({impl: mk(impl) for impl in a.impl}, iters=a.iters, rounds=5)  # interleaved, median
     for impl, ms in res.items():
         print(f"impl {impl} {'bwd' if a.bwd else 'fwd'}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF", flush=True)
