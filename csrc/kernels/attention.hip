@@ -378,8 +378,10 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd2_k(
   constexpr int PW = 2 * TILE / 1024 / NW;
   __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
   const int nqb = (T + BQ - 1) / BQ;
-  const int qb = nqb - 1 - blockIdx.x;  // heaviest first
-  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  // XCD-aware order (as attn_fwd_k): the blocks of one (b, h) run on one XCD; heaviest first.
+  const int xl = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+  const int qb = nqb - 1 - xl % gridDim.x;
+  const int bh = xl / gridDim.x, b = bh / H, h = bh % H;
   const int q0 = qb * BQ;
   const int wave = threadIdx.x >> 6, l = lane_id(), g = l >> 4;
   const int wq0 = q0 + wave * 32;
@@ -455,7 +457,8 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd2_k(
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int d = 0; d < DT; ++d) tr_frag_asm<HD>(lv, 32 * ks, 16 * d, vh[2 * (ks * DT + d)], vh[2 * (ks * DT + d) + 1]);
-    const bool need_mask = (causal && kv0 + BKV - 1 > wq0) || (kv0 + BKV > T);
+    const bool need_mask = __builtin_amdgcn_readfirstlane(
+        (int)((causal && kv0 + BKV - 1 > wq0) || (kv0 + BKV > T)));
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int qi = wq0 + 16 * c + (l & 15);
@@ -465,7 +468,8 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd2_k(
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int ki = kv0 + 16 * i + 4 * g + j;
-            if (ki >= T || (causal && ki > qi)) s[i][c][j] = -INFINITY;
+            const bool z = (ki >= T) | (causal & (ki > qi));
+            s[i][c][j] = z ? -INFINITY : s[i][c][j];
           }
       }
       float mx = s[0][c][0];
@@ -473,23 +477,29 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd2_k(
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) mx = fmaxf(mx, s[i][c][j]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m[c], mx * c2);
-      const float alpha = __builtin_amdgcn_exp2f(m[c] - mnew);
-      m[c] = mnew;
+      mx = group4_max(mx);
+      // deferred rescale (as attn_fwd_k): m moves only when the tile max exceeds it by > 2^8
+      constexpr float kDefer = 8.f;
+      const bool grow = mx * c2 > m[c] + kDefer;
+      if (__builtin_amdgcn_ballot_w64(grow) != 0) {
+        const float mnew = grow ? mx * c2 : m[c];
+        const float alpha = __builtin_amdgcn_exp2f(m[c] - mnew);
+        m[c] = mnew;
+        lsum[c] *= alpha;
+#pragma unroll
+        for (int d = 0; d < DT; ++d) o[c][d] *= alpha;
+      }
+      const float mc = m[c];
       float ps = 0.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float pv = __builtin_amdgcn_exp2f(fmaf(s[i][c][j], c2, -mnew));
+          const float pv = __builtin_amdgcn_exp2f(fmaf(s[i][c][j], c2, -mc));
           s[i][c][j] = pv;
           ps += pv;
         }
-      lsum[c] = lsum[c] * alpha + ps;
-#pragma unroll
-      for (int d = 0; d < DT; ++d) o[c][d] *= alpha;
+      lsum[c] += ps;
     }
 #pragma unroll
     for (int w = 0; w < (NVH + 15) / 16; ++w) tr_wait8(*reinterpret_cast<s16x4(*)[16]>(&vh[16 * w]));
@@ -509,9 +519,7 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd2_k(
 
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
-    float ls = lsum[c];
-    ls += __shfl_xor(ls, 16, 64);
-    ls += __shfl_xor(ls, 32, 64);
+    const float ls = group4_sum(lsum[c]);
     const int qi = wq0 + 16 * c + (l & 15);
     if (qi < T) {
       const float inv = 1.f / ls;
