@@ -1,10 +1,15 @@
 """Transport of the tensor-parallel collectives: RCCL (two ways) or xGMI peer memory.
 
-``DPFS_TP_COMM`` = ``auto`` (default) | ``rccl`` | ``native`` | ``xgmi``.
+``DPFS_TP_COMM`` = ``auto`` (default) | ``rccl`` | ``native`` | ``xgmi`` | ``relay``.
 
 * ``rccl``: ``torch.distributed`` on the TP group (ProcessGroupNCCL; ``nccl`` = RCCL on ROCm).
 * ``native``: :class:`~.rccl.RcclComm`, the RCCL C API on our own side stream.
 * ``xgmi``: :class:`~.xgmi.XgmiComm` (hand-written peer-memory kernels, all links at once).
+* ``relay``: :class:`~.relay.RelayComm` (TP = 2 with other pairs on the node: each pair's
+  exchange split over the direct link and two-hop paths through every other GPU, RCCL
+  point-to-point on the WORLD group).  Every rank of the WORLD takes part in each relayed
+  collective, so when it is a candidate the validation / timing results are reduced over the
+  WORLD and every TP group reaches the same decision.
 * ``auto``: on the first TP collective of the process, every TP rank builds the xGMI
   communicator and, for each of all-reduce, reduce-scatter and all-gather separately, checks
   its results against an fp32 ProcessGroupNCCL sum on a rank-dependent tensor of the live
@@ -38,7 +43,8 @@ _info: Dict[int, dict] = {}
 
 def mode() -> str:
     m = os.environ.get("DPFS_TP_COMM", "auto")
-    assert m in ("auto", "rccl", "native", "xgmi"), f"DPFS_TP_COMM={m!r}: expected auto | rccl | native | xgmi"
+    assert m in ("auto", "rccl", "native", "xgmi", "relay"), \
+        f"DPFS_TP_COMM={m!r}: expected auto | rccl | native | xgmi | relay"
     return m
 
 
@@ -58,9 +64,11 @@ class _Choice:
     def __init__(self, xgmi, native, use: Dict[str, str]):
         self.xgmi, self.native, self.use = xgmi, native, use
 
+    relay = None
+
     def comm(self, op: str):
         u = self.use[op]
-        return self.xgmi if u == "xgmi" else self.native if u == "native" else None
+        return {"xgmi": self.xgmi, "native": self.native, "relay": self.relay}.get(u)
 
 
 def _run_op(comm, op: str, x, part, gathered, timeout_s=None):
@@ -106,16 +114,29 @@ def _build(kind: str, g, forced: bool):
     return comm
 
 
+def _relay_possible(p) -> bool:
+    W = dist.get_world_size()
+    return p.tp_size == 2 and W >= 4 and W % 2 == 0
+
+
 def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
     m = mode()
     backend = dist.get_backend(p.tp_group)
-    if m == "rccl" or not t.is_cuda or (m == "auto" and backend != "nccl"):
+    if m == "rccl" or (m != "relay" and not t.is_cuda) or (m == "auto" and backend != "nccl"):
         return None
     g = p.tp_group
     W, r = p.tp_size, p.tp_rank
     kinds = [m] if m != "auto" else ["xgmi"]
-    comms = {k: _build(k, g, forced=m != "auto") for k in kinds}
+    relay_cand = (m == "relay" or m == "auto") and _relay_possible(p)
+    if m == "relay" and not relay_cand:
+        raise RuntimeError("DPFS_TP_COMM=relay needs TP = 2 and at least two TP pairs")
+    comms = {k: _build(k, g, forced=m != "auto") for k in kinds if k != "relay"}
     comms = {k: c for k, c in comms.items() if c is not None}
+    if relay_cand:
+        from .relay import RelayComm
+        comms["relay"] = RelayComm(p)
+    # relayed ops involve every rank of the WORLD: reduce every decision input over it
+    red_group = None if relay_cand else g
     if not comms:
         return None
     # Correctness of every op on a rank-dependent tensor of the live size, against fp32 sums
@@ -126,7 +147,7 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
     n = max(8 * W, n - n % (8 * W))
     gen = torch.Generator(device=t.device).manual_seed(4321 + r)
     x = torch.randn(n, generator=gen, device=t.device).to(t.dtype)
-    ref = x.float()
+    ref = x.float().clone()      # (an fp32 x must not be summed in place: it is the test input)
     dist.all_reduce(ref, group=g)
     mine = x.view(W, -1)[r]
     pad = torch.zeros(W, n // W, device=t.device)
@@ -143,7 +164,8 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
         _run_op(c, "all_reduce", y, None, None, to)
         _run_op(c, "reduce_scatter", x, part, None, to)
         _run_op(c, "all_gather", None, mine, gathered, to)
-        torch.cuda.synchronize()
+        if t.is_cuda:
+            torch.cuda.synchronize()
         e = [(y.float() - ref).abs().max().item(), (part.float() - ref.view(W, -1)[r]).abs().max().item(),
              (gathered.float() - pad.view(-1)).abs().max().item()]
         timed_out = k == "xgmi" and c.error() != 0
@@ -151,7 +173,7 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
         for i in range(3):
             good = not timed_out and (e[i] <= tol if i < 2 else e[i] == 0.0)
             bad[a, i] = 0.0 if good else 1.0
-    dist.all_reduce(bad, op=dist.ReduceOp.MAX, group=g)
+    dist.all_reduce(bad, op=dist.ReduceOp.MAX, group=red_group)
     if m != "auto" and bad.sum().item() > 0:
         raise RuntimeError(f"DPFS_TP_COMM={m}: collectives failed validation (max errors {errs[m]})")
     # Timing (ProcessGroupNCCL backend only).  xGMI workgroups per call (1024 threads each):
@@ -177,14 +199,15 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
                 times[i, j] = _time_ms(lambda c=c, op=op: _run_op(c, op, a_, ap, ag))
         if "xgmi" in comms:
             comms["xgmi"].check()
-    dist.all_reduce(times, op=dist.ReduceOp.MAX, group=g)
+    dist.all_reduce(times, op=dist.ReduceOp.MAX, group=red_group)
     use, info = {}, dict(bytes=n * x.element_size())
     for i, op in enumerate(_OPS):
         row = times[i].tolist()
         ok = {k: bad[a, i].item() == 0 for a, k in enumerate(kl)}
         cand = {"rccl": row[0]}
-        if "native" in comms and ok["native"]:
-            cand["native"] = row[cols.index("native")]
+        for k in ("native", "relay"):
+            if k in comms and ok[k]:
+                cand[k] = row[cols.index(k)]
         if "xgmi" in comms:
             xt = row[len(cols) - G:]
             jx = min(j for j, tt in enumerate(xt) if tt <= 1.1 * min(xt)) if timed else _GRIDS.index(32)
@@ -206,11 +229,13 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
         print(f"[dpfs] TP collectives: {info}", file=sys.stderr, flush=True)
     if all(u == "rccl" for u in use.values()):
         return None
-    return _Choice(comms.get("xgmi"), comms.get("native"), use)
+    ch = _Choice(comms.get("xgmi"), comms.get("native"), use)
+    ch.relay = comms.get("relay")
+    return ch
 
 
 def _comm(t: torch.Tensor, p, op: str):
-    if t.dtype not in (torch.bfloat16, torch.float32) or not t.is_cuda:
+    if t.dtype not in (torch.bfloat16, torch.float32) or (not t.is_cuda and mode() != "relay"):
         return None
     key = id(p.tp_group)
     if key not in _decisions:

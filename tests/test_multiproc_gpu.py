@@ -16,7 +16,10 @@ pytestmark = pytest.mark.gpu
 STEPS = 3
 
 
-def _train(rank, world, tp, dp, heads, dev="cuda", sp=False, recompute=False):
+def _train(rank, world, tp, dp, heads, dev="cuda", sp=False, recompute=False, transport=None):
+    import os
+    if transport:
+        os.environ["DPFS_TP_COMM"] = transport
     import torch.distributed as dist
     if dev == "cuda":
         torch.cuda.set_device(0)
@@ -66,4 +69,16 @@ def test_multirank_engine_follows_single_rank(world, tp, dp, heads, sp):
             assert abs(a - b) < 2e-2 * max(1.0, abs(b)), (r, losses, ref)
     # training moves the loss, identically on every rank
     assert ref[-1] < ref[0]
+    assert len({tuple(v) for v in res.values()}) == 1
+
+
+@pytest.mark.parametrize("sp", [True, False])
+def test_relay_transport_engine_follows_single_rank(sp):
+    """DP 2 x TP 2 on the GPU kernels with the TP collectives relayed through the other pair
+    (parallel/relay.py; gloo point-to-point here, fenced, RCCL on a real node)."""
+    ref = _ref(12)
+    res = run_distributed(_train, 4, 2, 2, 12, "cuda", sp, False, "relay", tp_size=2)
+    for r, losses in res.items():
+        for a, b in zip(losses, ref):
+            assert abs(a - b) < 2e-2 * max(1.0, abs(b)), (r, losses, ref)
     assert len({tuple(v) for v in res.values()}) == 1
