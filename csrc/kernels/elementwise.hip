@@ -94,6 +94,50 @@ __global__ __launch_bounds__(256) void rope_k(T* __restrict__ qkv, const int64_t
   }
 }
 
+// Same rotation, one 16-byte vector of each half per thread (8 bf16 / 4 fp32 frequency
+// pairs) and 32-bit index math: the pass is a pure HBM stream (read + write the q / k
+// columns once), where the scalar form above issued 2-byte accesses with 64-bit divisions.
+// Needs (hd / 2) % N == 0 and total = M * n_heads * hd / (2 N) < 2^31 (host checks).
+template <typename T>
+__global__ __launch_bounds__(256) void rope_vec_k(T* __restrict__ qkv, const int64_t* __restrict__ pos,
+                                                  const float* __restrict__ table, int M, int ld, int n_heads,
+                                                  int hd, float sign) {
+  constexpr int N = Vec<T>::N;
+  const int h2 = hd / 2;
+  const int qn = h2 / N;                 // threads per head
+  const int per_row = n_heads * qn;
+  const int total = M * per_row;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int row = i / per_row;
+    const int rem = i - row * per_row;
+    const int head = rem / qn;
+    const int f0 = (rem - head * qn) * N;
+    const float* tr = table + pos[row] * (long long)hd;
+    T* base = qkv + (long long)row * ld + head * hd;
+    float x1[N], x2[N], c[N], sn[N];
+    load_vec<T>(base + f0, x1);
+    load_vec<T>(base + h2 + f0, x2);
+#pragma unroll
+    for (int j = 0; j < N; j += 4) {
+      const f32x4 cv = *reinterpret_cast<const f32x4*>(tr + f0 + j);
+      const f32x4 sv = *reinterpret_cast<const f32x4*>(tr + h2 + f0 + j);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        c[j + u] = cv[u];
+        sn[j + u] = sign * sv[u];
+      }
+    }
+    float o1[N], o2[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      o1[j] = x1[j] * c[j] - x2[j] * sn[j];
+      o2[j] = x2[j] * c[j] + x1[j] * sn[j];
+    }
+    store_vec<T>(base + f0, o1);
+    store_vec<T>(base + h2 + f0, o2);
+  }
+}
+
 // ------------------------------------------------------------------- bias / residual --
 // out = (residual ? residual : 0) + y + bias  (bias may be null; out may alias y).
 template <typename T>
@@ -358,6 +402,16 @@ extern "C" void dpfs_rope(int dtype, void* qkv, const int64_t* pos, const float*
                           int hd, int inverse, hipStream_t s) {
   const long long work = (long long)M * n_heads * (hd / 8);
   const float sign = inverse ? -1.f : 1.f;
+  const int vn = dtype == kBF16 ? 8 : 4;
+  const long long vwork = (long long)M * n_heads * (hd / 2 / vn);
+  if ((hd / 2) % vn == 0 && vwork < (1ll << 31) && ld % vn == 0) {
+    const int grid = (int)std::min<long long>((vwork + 255) / 256, 8192);
+    if (dtype == kBF16)
+      rope_vec_k<bf16><<<grid, 256, 0, s>>>((bf16*)qkv, pos, table, M, ld, n_heads, hd, sign);
+    else
+      rope_vec_k<float><<<grid, 256, 0, s>>>((float*)qkv, pos, table, M, ld, n_heads, hd, sign);
+    return;
+  }
   if (dtype == kBF16)
     rope_k<bf16><<<cap_grid(work, 256), 256, 0, s>>>((bf16*)qkv, pos, table, M, ld, n_heads, hd, sign);
   else

@@ -121,20 +121,25 @@ def test_swiglu(C):
     assert _rel(C.swiglu_bwd(dh, gu), R.swiglu_bwd(dh.float(), gu.float())) < 1e-2
 
 
-@pytest.mark.parametrize("hd", [32, 64, 128])
-def test_rope(C, hd):
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("hd", [16, 32, 48, 64, 128])
+def test_rope(C, hd, dtype):
+    """Vectorised kernel (hd/2 a multiple of the 16-byte vector) and the scalar fallback
+    (bf16 hd 48), both against the fp32 reference; the inverse rotation restores the input."""
     torch.manual_seed(6)
-    M, H = 96, 3
-    qkv = torch.randn(M, 3 * H * hd, device=DEV).bfloat16()
+    M, H = 1000, 3
+    qkv = torch.randn(M, 3 * H * hd, device=DEV).to(dtype)
     pos = torch.randint(0, 200, (M,), device=DEV)
     tab = R.rope_table(256, hd, 10000.0).to(DEV)
     a = qkv.clone()
     C.rope_(a, pos, tab, 2 * H, hd, False)
     b = qkv.float().clone()
     R.rope_(b, pos, tab, 2 * H, hd, False)
-    assert _rel(a, b) < 1e-2
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
+    assert _rel(a, b) < tol
+    assert torch.equal(a[:, 2 * H * hd:], qkv[:, 2 * H * hd:])     # v heads untouched
     C.rope_(a, pos, tab, 2 * H, hd, True)  # inverse restores
-    assert _rel(a, qkv) < 1e-2
+    assert _rel(a, qkv) < tol
 
 
 def test_bias_grad_and_residual(C):
