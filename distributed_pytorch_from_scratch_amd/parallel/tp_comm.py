@@ -145,6 +145,10 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
     if "xgmi" in comms:
         n = min(n, comms["xgmi"]._max_elems(t))
     n = max(8 * W, n - n % (8 * W))
+    if relay_cand:   # relayed exchanges pair every rank with every other: one size for the WORLD
+        nt = torch.tensor([n], dtype=torch.int64, device=t.device)
+        dist.all_reduce(nt, op=dist.ReduceOp.MIN)
+        n = int(nt.item())
     gen = torch.Generator(device=t.device).manual_seed(4321 + r)
     x = torch.randn(n, generator=gen, device=t.device).to(t.dtype)
     ref = x.float().clone()      # (an fp32 x must not be summed in place: it is the test input)
