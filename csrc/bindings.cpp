@@ -72,6 +72,11 @@ void dpfs_attn_decode(const void*, long long, const void*, const void*, const in
                       int, int, float, hipStream_t);
 void dpfs_kv_append(const void*, const void*, long long, void*, void*, const int*, int, int, int, int, hipStream_t);
 void dpfs_step_advance(int*, int64_t*, int, hipStream_t);
+int dpfs_gemv16_ok(int, int, int, long long, long long);
+void dpfs_gemv16(const void*, long long, const void*, long long, const float*, void*, long long, int, int, int, int,
+                 hipStream_t);
+void dpfs_rope_append(void*, long long, const int64_t*, const float*, void*, void*, const int*, int, int, int, int,
+                      hipStream_t);
 // comm/xgmi.hip
 const char* dpfs_xgmi_last_error();
 long long dpfs_xgmi_handle_bytes();
@@ -718,6 +723,49 @@ void kv_append(torch::Tensor qkv, torch::Tensor kc, torch::Tensor vc, torch::Ten
                  (int)B, (int)H, (int)hd, (int)Tmax, stream());
 }
 
+// y[M, N] = x[M, K] w[N, K]^T (+ bias) for M <= 16 (decode-step projections); with swiglu,
+// x is the packed [M, 2K] gate|up output and the operand is silu(gate) * up.
+bool gemv_nt_ok(torch::Tensor x, torch::Tensor w, bool swiglu) {
+  if (!x.is_cuda() || x.dim() != 2 || w.dim() != 2 || x.scalar_type() != torch::kBFloat16 ||
+      w.scalar_type() != torch::kBFloat16 || x.stride(1) != 1 || w.stride(1) != 1)
+    return false;
+  const int64_t K = w.size(1);
+  if (x.size(1) != (swiglu ? 2 * K : K)) return false;
+  return dpfs_gemv16_ok((int)x.size(0), (int)w.size(0), (int)K, x.stride(0), w.stride(0)) != 0;
+}
+
+torch::Tensor gemv_nt(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, bool swiglu) {
+  TORCH_CHECK(gemv_nt_ok(x, w, swiglu), "gemv_nt: needs bf16 row-major x [M <= 16, K or 2K], w [N, K], K % 32 == 0");
+  const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
+  const at::DeviceGuard g(x.device());
+  auto y = torch::empty({M, N}, x.options());
+  dpfs_gemv16(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), opt_f32(bias, N, "bias"), y.data_ptr(), N, (int)M,
+              (int)N, (int)K, swiglu ? 1 : 0, stream());
+  return y;
+}
+
+// rope_ on the q and k heads of the packed qkv rows + kv_append of the rotated k and v rows
+// at *len, one kernel (decode step).
+void rope_append(torch::Tensor qkv, torch::Tensor pos, torch::Tensor table, torch::Tensor kc, torch::Tensor vc,
+                 torch::Tensor len) {
+  check_rowmajor(qkv, "qkv");
+  check_cache(kc, "k_cache");
+  check_cache(vc, "v_cache");
+  check_len(len);
+  const int64_t B = kc.size(0), Tmax = kc.size(1), H = kc.size(2), hd = kc.size(3);
+  TORCH_CHECK(qkv.size(0) == B && qkv.size(1) == 3 * H * hd && qkv.stride(0) % 8 == 0 &&
+                  qkv.scalar_type() == torch::kBFloat16 && hd % 16 == 0,
+              "rope_append: qkv must be [B, 3*H*hd] bf16, hd % 16 == 0");
+  TORCH_CHECK(pos.is_cuda() && pos.scalar_type() == torch::kInt64 && pos.is_contiguous() && pos.numel() == B,
+              "rope_append: pos must be contiguous int64 [B]");
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == torch::kFloat32 && table.is_contiguous() &&
+                  table.size(1) == hd,
+              "rope_append: table must be fp32 [maxlen, hd]");
+  const at::DeviceGuard g(qkv.device());
+  dpfs_rope_append(qkv.data_ptr(), qkv.stride(0), pos.data_ptr<int64_t>(), table.data_ptr<float>(), kc.data_ptr(),
+                   vc.data_ptr(), len.data_ptr<int>(), (int)B, (int)H, (int)hd, (int)Tmax, stream());
+}
+
 // *len += 1 and pos[:] = *len on the device (end of a decode step; graph-replayable).
 void step_advance(torch::Tensor len, torch::Tensor pos) {
   check_len(len);
@@ -916,6 +964,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("scale"));
   m.def("kv_append", &kv_append, py::arg("qkv"), py::arg("k_cache"), py::arg("v_cache"), py::arg("len"));
   m.def("step_advance", &step_advance, py::arg("len"), py::arg("pos"));
+  m.def("gemv_nt_ok", &gemv_nt_ok, py::arg("x"), py::arg("w"), py::arg("swiglu") = false);
+  m.def("gemv_nt", &gemv_nt, py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("swiglu") = false);
+  m.def("rope_append", &rope_append, py::arg("qkv"), py::arg("pos"), py::arg("table"), py::arg("k_cache"),
+        py::arg("v_cache"), py::arg("len"));
   m.def("xgmi_create", &xgmi_create, "allocate IPC buffers: -> (handle, ipc handle bytes)");
   m.def("xgmi_open", &xgmi_open, "map every peer's buffers (rank-ordered concatenated handle bytes)");
   m.def("xgmi_run", &xgmi_run, py::arg("h"), py::arg("op"), py::arg("x"), py::arg("out"), py::arg("world"),

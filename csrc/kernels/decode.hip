@@ -176,6 +176,122 @@ __global__ __launch_bounds__(256) void kv_append_k(const bf16* __restrict__ ksrc
   }
 }
 
+// -------------------------------------------------------------- small-M projections --
+// y[M, N] (+ bias) = A[M, K] W[N, K]^T for M <= 16 rows (the decode step's projections: one
+// row per sequence).  hipBLASLt's tiles for these shapes move ~0.5 TB/s of W (7 us for the
+// 3.5 MB GPT-2 QKV weight); here each wave is one v_mfma_f32_16x16x32_bf16 chain: the M rows
+// are its A tile (rows >= M read as zeros), 16 rows of W its B tile (4 lanes x 16 B per row
+// segment), and the KS waves of a workgroup split K and merge in LDS in a fixed order.  W is
+// streamed once with all of a wave's loads issued ahead of its MFMAs; A (a few KB) stays in
+// L2.  SW: A = silu(g) * u of a packed [M, 2K] gate|up input -- the SwiGLU fused into the down
+// projection's operand load (same fp32 formula and bf16 rounding as swiglu_fwd_k).
+__device__ __forceinline__ float silu_dec(float g) { return g / (1.f + __expf(-g)); }
+
+template <int KS, bool SW>
+__global__ __launch_bounds__(64 * KS) void gemv16_k(const bf16* __restrict__ A, long long lda,
+                                                    const bf16* __restrict__ W, long long ldw,
+                                                    const float* __restrict__ bias, bf16* __restrict__ Y,
+                                                    long long ldy, int M, int N, int K) {
+  constexpr int CH = 8;                      // MFMA k-steps per batch of loads
+  __shared__ f32x4 red[KS][64];
+  const int wave = threadIdx.x >> 6, l = lane_id(), g = l >> 4, i = l & 15;
+  const int n0 = blockIdx.x * 16;
+  const int nk = K / 32;
+  const int per = (nk + KS - 1) / KS;
+  const int c0 = wave * per, c1 = min(nk, c0 + per);
+  const bf16* wp = W + (long long)min(n0 + i, N - 1) * ldw + 8 * g;
+  const bool mv = i < M;
+  const bf16* ap = A + (long long)(mv ? i : 0) * lda + 8 * g;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int cb = c0; cb < c1; cb += CH) {
+    bf16x8 b[CH], a[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const int c = cb + u;
+      if (c < c1) {
+        b[u] = *reinterpret_cast<const bf16x8*>(wp + 32 * c);
+        if (SW) {
+          const bf16x8 gv = *reinterpret_cast<const bf16x8*>(ap + 32 * c);
+          const bf16x8 uv = *reinterpret_cast<const bf16x8*>(ap + K + 32 * c);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) a[u][j] = (bf16)(silu_dec((float)gv[j]) * (float)uv[j]);
+        } else {
+          a[u] = *reinterpret_cast<const bf16x8*>(ap + 32 * c);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      if (cb + u < c1) {
+        const bf16x8 z = {};
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mv ? a[u] : z, b[u], acc, 0, 0, 0);
+      }
+    }
+  }
+  red[wave][l] = acc;
+  __syncthreads();
+  if (wave == 0) {
+#pragma unroll
+    for (int w = 1; w < KS; ++w) acc += red[w][l];
+    const int n = n0 + i;                    // D[row = 4g + j][col = lane & 15]
+    if (n < N) {
+      const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = 4 * g + j;
+        if (m < M) Y[(long long)m * ldy + n] = (bf16)(acc[j] + bv);
+      }
+    }
+  }
+}
+
+// RoPE of the q and k heads of the packed qkv rows (in place) fused with the cache append of
+// the rotated k row and the v row at row *len: one launch instead of rope_k + kv_append_k.
+// Same arithmetic and rounding as rope_vec_k (sign +1).  8 frequency pairs per thread.
+__global__ __launch_bounds__(256) void rope_append_k(bf16* __restrict__ qkv, long long ld,
+                                                     const int64_t* __restrict__ pos,
+                                                     const float* __restrict__ tab, bf16* __restrict__ kc,
+                                                     bf16* __restrict__ vc, const int* __restrict__ len_ptr,
+                                                     int B, int H, int HD, int Tmax) {
+  const int t = *len_ptr;
+  const bool app = t >= 0 && t < Tmax;     // full cache: rotate, append nothing
+  const int h2 = HD / 2, q8 = h2 / 8;
+  const int rot_per_b = 2 * H * q8;
+  const int nrot = B * rot_per_b;
+  const int vpr = H * HD / 8;              // 16-byte v vectors per sequence
+  const int total = nrot + B * vpr;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    if (i < nrot) {
+      const int b = i / rot_per_b, r = i - b * rot_per_b;
+      const int head = r / q8, f0 = (r - head * q8) * 8;
+      bf16* base = qkv + (long long)b * ld + head * HD;
+      const float* tr = tab + pos[b] * (long long)HD;
+      const bf16x8 xa = *reinterpret_cast<const bf16x8*>(base + f0);
+      const bf16x8 xb = *reinterpret_cast<const bf16x8*>(base + h2 + f0);
+      bf16x8 oa, ob;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float c = tr[f0 + j], sn = tr[h2 + f0 + j];
+        const float x1 = (float)xa[j], x2 = (float)xb[j];
+        oa[j] = (bf16)(x1 * c - x2 * sn);
+        ob[j] = (bf16)(x2 * c + x1 * sn);
+      }
+      *reinterpret_cast<bf16x8*>(base + f0) = oa;
+      *reinterpret_cast<bf16x8*>(base + h2 + f0) = ob;
+      if (head >= H && app) {
+        bf16* dst = kc + (((long long)b * Tmax + t) * H + (head - H)) * HD;
+        *reinterpret_cast<bf16x8*>(dst + f0) = oa;
+        *reinterpret_cast<bf16x8*>(dst + h2 + f0) = ob;
+      }
+    } else if (app) {
+      const int j = i - nrot, b = j / vpr, c = j - b * vpr;
+      const bf16* src = qkv + (long long)b * ld + 2 * H * HD + 8 * c;
+      bf16* dst = vc + ((long long)b * Tmax + t) * H * HD + 8 * c;
+      *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(src);
+    }
+  }
+}
+
 // *len += 1; pos[b] = *len (the next token's position) for every sequence.
 __global__ void step_advance_k(int* __restrict__ len_ptr, int64_t* __restrict__ pos, int B) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
@@ -216,4 +332,30 @@ extern "C" void dpfs_kv_append(const void* ksrc, const void* vsrc, long long ld,
 
 extern "C" void dpfs_step_advance(int* len_ptr, int64_t* pos, int B, hipStream_t s) {
   step_advance_k<<<1, 64, 0, s>>>(len_ptr, pos, B);
+}
+
+extern "C" int dpfs_gemv16_ok(int M, int N, int K, long long lda, long long ldw) {
+  return M >= 1 && M <= 16 && N >= 1 && K % 32 == 0 && K > 0 && lda % 8 == 0 && ldw % 8 == 0;
+}
+
+extern "C" void dpfs_gemv16(const void* A, long long lda, const void* W, long long ldw, const float* bias, void* Y,
+                            long long ldy, int M, int N, int K, int swiglu, hipStream_t s) {
+  const int nb = (N + 15) / 16;
+  // K split over 8 waves while that still leaves >= 2 MFMA k-steps per wave and the grid is
+  // small; 4 waves for wide N (the lm_head: thousands of workgroups already)
+  const bool ks8 = nb <= 512 && K / 32 >= 16;
+  if (ks8) {
+    if (swiglu) gemv16_k<8, true><<<nb, 512, 0, s>>>((const bf16*)A, lda, (const bf16*)W, ldw, bias, (bf16*)Y, ldy, M, N, K);
+    else gemv16_k<8, false><<<nb, 512, 0, s>>>((const bf16*)A, lda, (const bf16*)W, ldw, bias, (bf16*)Y, ldy, M, N, K);
+  } else {
+    if (swiglu) gemv16_k<4, true><<<nb, 256, 0, s>>>((const bf16*)A, lda, (const bf16*)W, ldw, bias, (bf16*)Y, ldy, M, N, K);
+    else gemv16_k<4, false><<<nb, 256, 0, s>>>((const bf16*)A, lda, (const bf16*)W, ldw, bias, (bf16*)Y, ldy, M, N, K);
+  }
+}
+
+extern "C" void dpfs_rope_append(void* qkv, long long ld, const int64_t* pos, const float* tab, void* kc, void* vc,
+                                 const int* len_ptr, int B, int H, int HD, int Tmax, hipStream_t s) {
+  const int total = B * 2 * H * (HD / 16) + B * H * HD / 8;
+  const int grid = (total + 255) / 256;
+  rope_append_k<<<grid, 256, 0, s>>>((bf16*)qkv, ld, pos, tab, (bf16*)kc, (bf16*)vc, len_ptr, B, H, HD, Tmax);
 }

@@ -121,27 +121,36 @@ def decode_step(model, ids: torch.Tensor, pos: torch.Tensor, cache: KVCache):
     x = model.embedding(ids).reshape(B, -1).to(dt)
     tab = model.rope_table(dev)
     pend = pend_bias = None
-    # Per layer: [bias + residual +] RMSNorm (one kernel), QKV GEMM, RoPE, append k/v at len,
-    # split-K decode attention, Wo GEMM, bias + residual + RMSNorm, gate|up
-    # GEMM, SwiGLU, down GEMM (its bias + residual fold into the next layer's norm).
+    small = B <= 16 and os.environ.get("DPFS_DECODE_GEMV", "1") != "0"
+
+    def proj(a, w, bias=None, swiglu=False):
+        if small:   # MFMA GEMV-class kernel, SwiGLU fused into the down projection's operand
+            return GS.small_nt(k, a, w, bias, swiglu)
+        return GS.gemm_nt(k, k.swiglu_fwd(a) if swiglu else a, w, bias)
+    # Per layer: [bias + residual +] RMSNorm (one kernel), QKV projection, RoPE + append of
+    # k/v at len (one kernel), split-K decode attention, Wo projection, bias + residual +
+    # RMSNorm, gate|up projection, SwiGLU + down projection (its bias + residual fold into the
+    # next layer's norm).
     for li, layer in enumerate(model.layers):
         L = _Layer(layer)
         if pend is None:
             h1, _ = k.rmsnorm_fwd(x, L.s1, L.eps1)
         else:
             x, h1, _ = k.add_rmsnorm_fwd(pend, pend_bias, x, L.s1, L.eps1)
-        qkv = GS.gemm_nt(k, h1, W(L.wqkv), L.bqkv)   # few rows: the library GEMV-class kernels win
-        k.rope_(qkv, pos, tab, 2 * L.h, L.hd, False)
-        k.kv_append(qkv, cache.k[li], cache.v[li], cache.len_t)
+        qkv = proj(h1, W(L.wqkv), L.bqkv)
+        if L.hd % 16 == 0:
+            k.rope_append(qkv, pos, tab, cache.k[li], cache.v[li], cache.len_t)
+        else:
+            k.rope_(qkv, pos, tab, 2 * L.h, L.hd, False)
+            k.kv_append(qkv, cache.k[li], cache.v[li], cache.len_t)
         o = k.attn_decode(qkv, cache.k[li], cache.v[li], cache.len_t, 1.0 / math.sqrt(L.hd))
-        pout = GS.gemm_nt(k, o, W(L.wo), None)
+        pout = proj(o, W(L.wo))
         tp_comm.all_reduce(pout, async_op=False)
         x, h2, _ = k.add_rmsnorm_fwd(pout, L.bo, x, L.s2, L.eps2)
-        sw = k.swiglu_fwd(GS.gemm_nt(k, h2, W(L.wgu), L.bgu))
-        pend, pend_bias = GS.gemm_nt(k, sw, W(L.wd), None), L.bd
+        pend, pend_bias = proj(proj(h2, W(L.wgu), L.bgu), W(L.wd), swiglu=True), L.bd
         tp_comm.all_reduce(pend, async_op=False)
     _, hfin, _ = k.add_rmsnorm_fwd(pend, pend_bias, x, model.norm.scale, model.norm.eps)
-    logits = GS.gemm_nt(k, hfin, W(model.lm_head.weight), model.lm_head.bias)
+    logits = proj(hfin, W(model.lm_head.weight), model.lm_head.bias)
     logits = comm_ops.Gather.apply(logits, model.lm_head.sizes)[..., : model.vocab_size].float()
     nxt = logits.argmax(-1)
     K(pos).step_advance(cache.len_t, pos)

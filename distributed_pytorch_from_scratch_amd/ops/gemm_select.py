@@ -96,6 +96,19 @@ def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, out=None) -> torch.T
     return blas() if _pick(key, ours, blas) == "blas" else ours()
 
 
+def small_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, swiglu: bool = False) -> torch.Tensor:
+    """Decode-step projection, M <= 16 rows: y = a w^T (+ bias), a = x or, with ``swiglu``,
+    silu(gate) * up of the packed x = [gate | up].  The MFMA GEMV-class kernel (gemv16_k,
+    csrc/kernels/decode.hip; SwiGLU fused into its operand load) wherever it applies, else
+    hipBLASLt after a separate SwiGLU pass.  Not timed per shape: at these sizes a host-timed
+    loop measures launch cost (see _MIN_ROWS); the kernel times are in profiles/."""
+    if k is reference or not x.is_cuda:
+        return k.gemv_nt(x, w, bias, swiglu)
+    if mode() != "blas" and k.gemv_nt_ok(x, w, swiglu):
+        return k.gemv_nt(x, w, bias, swiglu)
+    return gemm_nt(k, k.swiglu_fwd(x) if swiglu else x, w, bias)
+
+
 def gemm_nn(k, a: torch.Tensor, b: torch.Tensor, out=None) -> torch.Tensor:
     """c[M,N] = a[M,K] b[K,N] in a.dtype (into ``out`` when given)."""
     m = mode()

@@ -210,6 +210,34 @@ def kv_append(qkv: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, l
     v_cache[:, t] = qkv[:, 2 * H * hd: 3 * H * hd].view(B, H, hd).to(v_cache.dtype)
 
 
+def gemv_nt_ok(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> bool:
+    return True
+
+
+def gemv_nt(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
+            swiglu: bool = False) -> torch.Tensor:
+    """y = a w^T (+ bias) in x.dtype, a = x, or with ``swiglu`` a = silu(g) * u of the packed
+    x = [g | u] rounded to x.dtype (the GPU kernel's fused operand; swiglu_fwd's rounding)."""
+    if swiglu:
+        K = w.size(1)
+        g, u = x[:, :K].float(), x[:, K:].float()
+        a = (g / (1.0 + torch.exp(-g)) * u).to(x.dtype)
+    else:
+        a = x
+    y = a.float() @ w.float().t()
+    if bias is not None:
+        y = y + bias.float()
+    return y.to(x.dtype)
+
+
+def rope_append(qkv: torch.Tensor, pos: torch.Tensor, table: torch.Tensor, k_cache: torch.Tensor,
+                v_cache: torch.Tensor, len: torch.Tensor) -> None:
+    """rope_ on the q and k heads of the packed rows, then kv_append (one GPU kernel)."""
+    H, hd = k_cache.size(2), k_cache.size(3)
+    rope_(qkv, pos, table, 2 * H, hd, False)
+    kv_append(qkv, k_cache, v_cache, len)
+
+
 def step_advance(len: torch.Tensor, pos: torch.Tensor) -> None:
     len += 1
     pos.fill_(int(len.reshape(-1)[0]))

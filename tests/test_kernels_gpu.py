@@ -355,6 +355,48 @@ def test_decode_attention_and_kv_append(C, hd, L):
     assert ln.item() == L + 1 and pos.tolist() == [L + 1] * B
 
 
+@pytest.mark.parametrize("M", [1, 3, 8, 16])
+@pytest.mark.parametrize("N,K", [(2304, 768), (768, 2048), (50304, 768), (100, 64), (37, 4096)])
+@pytest.mark.parametrize("swiglu", [False, True])
+def test_gemv_small_m(C, M, N, K, swiglu):
+    """Decode-step projection kernel (gemv16_k, M <= 16 rows as an MFMA A tile, K split over
+    waves) against the fp32 oracle, with and without bias and with the fused SwiGLU operand
+    (the same bf16 operand as swiglu_fwd: compared exactly through a plain call)."""
+    torch.manual_seed(23 + M)
+    x = torch.randn(M, 2 * K if swiglu else K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    bias = torch.randn(N, device=DEV)
+    assert C.gemv_nt_ok(x, w, swiglu)
+    for b in (None, bias):
+        y = C.gemv_nt(x, w, b, swiglu)
+        ref = R.gemv_nt(x, w, b, swiglu)    # fp32 product of the same bf16 operand
+        assert y.shape == (M, N) and y.dtype == torch.bfloat16
+        assert _rel(y, ref) < 1e-2, (b is None, _rel(y, ref))
+    if swiglu:
+        assert torch.equal(C.gemv_nt(C.swiglu_fwd(x), w, bias), C.gemv_nt(x, w, bias, True))
+    assert not C.gemv_nt_ok(torch.randn(17, K, device=DEV).bfloat16(), w)   # > 16 rows: caller falls back
+
+
+@pytest.mark.parametrize("hd", [64, 128])
+@pytest.mark.parametrize("L", [0, 699, 700])   # 700 = full cache: rotate, append nothing
+def test_rope_append_matches_rope_then_append(C, hd, L):
+    torch.manual_seed(24)
+    B, H, Tmax = 3, 5, 700
+    kc = torch.randn(B, Tmax, H, hd, device=DEV).bfloat16()
+    vc = torch.randn(B, Tmax, H, hd, device=DEV).bfloat16()
+    qkv = torch.randn(B, 3 * H * hd, device=DEV).bfloat16()
+    pos = torch.randint(0, 900, (B,), device=DEV)
+    tab = R.rope_table(1024, hd, 10000.0).to(DEV)
+    ln = torch.tensor([L], dtype=torch.int32, device=DEV)
+    a, ka, va = qkv.clone(), kc.clone(), vc.clone()
+    C.rope_append(a, pos, tab, ka, va, ln)
+    b, kb, vb = qkv.clone(), kc.clone(), vc.clone()
+    C.rope_(b, pos, tab, 2 * H, hd, False)
+    if L < Tmax:
+        C.kv_append(b, kb, vb, ln)
+    assert torch.equal(a, b) and torch.equal(ka, kb) and torch.equal(va, vb)
+
+
 @pytest.mark.parametrize("M,V,valid,start", [(2048, 6288, 6241, 6288 * 7), (100, 50304, 50257, 0),
                                              (300, 500, 500, 500), (65, 37, 30, 0)])   # unaligned rows
 def test_ce_bwd_fused_bias_grad(C, M, V, valid, start):
