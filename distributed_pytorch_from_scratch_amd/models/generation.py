@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import math
 import os
+import weakref
 from typing import List, Optional
 
 import torch
@@ -182,13 +183,18 @@ def _decode_step_modules(model, ids: torch.Tensor, pos: torch.Tensor, cache: KVC
 
 
 class DecodeGraph:
-    """One decode step captured as a HIP graph (static ids / pos / output buffers)."""
+    """``nsteps`` decode steps captured as one HIP graph (static ids / pos / output buffers):
+    step s writes its next ids into ``outs[s]`` and feeds them to step s + 1 on the device, so
+    the host reads the tokens back (and checks EOS) once per replay instead of once per token
+    (that round trip, ~90 us, was idle GPU time in every step)."""
 
-    def __init__(self, model, cache: KVCache, B: int):
+    def __init__(self, model, cache: KVCache, B: int, nsteps: int = 1):
         dev = cache.len_t.device
         self.cache = cache
+        self.nsteps = nsteps
         self.ids = torch.zeros(B, 1, dtype=torch.int64, device=dev)
         self.pos = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.outs = torch.zeros(nsteps, B, dtype=torch.int64, device=dev)
         saved = cache.len_t.clone()
         # Warm-up off the capture (first-call GEMM choices, allocator pools).  It appends a row
         # at len_t, which the first real step rewrites before anything reads it.
@@ -201,20 +207,50 @@ class DecodeGraph:
         cache.len_t.copy_(saved)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.out, self.logits = decode_step(model, self.ids, self.pos, cache)
+            for i in range(nsteps):
+                nxt, self.logits = decode_step(model, self.ids, self.pos, cache)
+                self.outs[i].copy_(nxt)
+                if i + 1 < nsteps:
+                    self.ids.copy_(nxt.view(-1, 1))
+        self.out = self.outs[nsteps - 1]
         cache.len_t.copy_(saved)
 
     def step(self, ids: torch.Tensor) -> torch.Tensor:
-        """Feed ids (B,) at the cache's device length; returns the next ids (B,) (device)."""
+        """Feed ids (B,) at the cache's device length; returns the next ids of every captured
+        step (nsteps, B) (device); the cache advances by nsteps rows."""
         self.ids.copy_(ids.view(-1, 1))
         self.graph.replay()
-        return self.out
+        return self.outs
 
 
 def _use_graph(dev) -> bool:
     p = pm.pgm
     return (dev.type == "cuda" and os.environ.get("DPFS_DECODE_GRAPH", "1") != "0"
             and (p is None or p.tp_size == 1))
+
+
+_SESSIONS = {}   # (id(model), B, t_max, device) -> KV cache + captured decode graphs
+
+
+def _session(model, B: int, t_max: int, dev):
+    """The KV cache and decode graphs for this (model, batch, length): reused by the next
+    generate() call of the same shape, so serving pays the graph capture once.  Reused only
+    while it is the same live model object and no parameter changed since the capture (the
+    graphs hold the bf16 weight copies of that version); otherwise rebuilt."""
+    attn0 = model.layers[0].attn
+    key = (id(model), B, t_max, str(dev))
+    vers = tuple(p._version for p in model.parameters())
+    ent = _SESSIONS.get(key)
+    if ent is not None and ent["model"]() is model and ent["vers"] == vers:
+        ent["cache"].len = 0
+        return ent["cache"], ent["graphs"]
+    cache = KVCache(len(model.layers), B, t_max, attn0.num_local_heads, attn0.head_dim, model.act_dtype(dev), dev)
+    graphs = {}
+    if _use_graph(dev):
+        for k in [k for k, e in _SESSIONS.items() if e["model"]() is None or k[0] == id(model)]:
+            del _SESSIONS[k]          # dead models, and other shapes of this one
+        _SESSIONS[key] = {"model": weakref.ref(model), "vers": vers, "cache": cache, "graphs": graphs}
+    return cache, graphs
 
 
 @torch.inference_mode()
@@ -226,9 +262,7 @@ def generate(model, prompt: torch.Tensor, max_new_tokens: int, eos_id: Optional[
     B, T0 = prompt.shape
     dev = prompt.device
     t_max = min(model.args.maxlen, max_len or model.args.maxlen, T0 + max_new_tokens)
-    attn0 = model.layers[0].attn
-    cache = KVCache(len(model.layers), B, t_max, attn0.num_local_heads, attn0.head_dim,
-                    model.act_dtype(dev), dev)
+    cache, graphs = _session(model, B, t_max, dev)
     out = [list(map(int, row)) for row in prompt.tolist()]
     done = [False] * B
     if max_new_tokens <= 0 or T0 >= t_max:
@@ -236,21 +270,38 @@ def generate(model, prompt: torch.Tensor, max_new_tokens: int, eos_id: Optional[
     nxt = logits_step(model, prompt, cache).argmax(-1)
     cache.sync_device_len()
     pos = torch.full((B,), cache.len, dtype=torch.int64, device=dev)
-    graph = None
+    chunk = max(1, int(os.environ.get("DPFS_DECODE_GRAPH_STEPS", "8")))
     n_gen = 0
-    while True:
+
+    def emit(row) -> bool:
+        """Append one step's ids; True when generation is finished."""
+        nonlocal n_gen
         n_gen += 1
-        for b, t in enumerate(nxt.tolist()):
+        for b, t in enumerate(row):
             if not done[b]:
                 out[b].append(int(t))
                 done[b] = eos_id is not None and int(t) == eos_id
-        if all(done) or n_gen >= max_new_tokens or cache.len >= t_max:
-            return out
-        if graph is None and _use_graph(dev):
-            graph = DecodeGraph(model, cache, B)
-        if graph is not None:
-            graph.pos.fill_(cache.len)
-            nxt = graph.step(nxt)
+        return all(done) or n_gen >= max_new_tokens or cache.len >= t_max
+
+    if emit(nxt.tolist()):
+        return out
+    while True:
+        if _use_graph(dev):
+            # S steps per replay while S more tokens are wanted and the cache has room for them
+            S = chunk if (max_new_tokens - n_gen >= chunk and cache.len + chunk <= t_max) else 1
+            g = graphs.get(S)
+            if g is None:
+                g = graphs[S] = DecodeGraph(model, cache, B, S)
+            g.pos.fill_(cache.len)
+            outs = g.step(nxt)
+            rows = outs.tolist()
+            nxt = g.out
+            for row in rows:
+                cache.len += 1
+                if emit(row):
+                    return out
         else:
             nxt, _ = decode_step(model, nxt.view(B, 1), pos, cache)
-        cache.len += 1
+            cache.len += 1
+            if emit(nxt.tolist()):
+                return out

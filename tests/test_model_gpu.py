@@ -195,6 +195,34 @@ def test_decode_graph_matches_eager_decode(dist1, monkeypatch):
     assert all(len(o) == 280 for o in graph)
 
 
+def test_decode_session_reuse_and_weight_change(dist1, monkeypatch):
+    """A second generate() of the same shape reuses the KV cache and the captured multi-step
+    decode graphs (same tokens as the eager step); after a weight update the graphs are
+    rebuilt, so the graph path still follows the eager path."""
+    from distributed_pytorch_from_scratch_amd.models import get_preset, Transformer
+    from distributed_pytorch_from_scratch_amd.models import generation as G
+    args = get_preset("gpt2-small", num_layers=2)
+    m = Transformer.from_args(args).cuda()
+    m.reset_parameters()
+    m.eval()
+    prompt = torch.randint(0, args.vocab_size, (2, 50), device="cuda")
+    monkeypatch.setenv("DPFS_DECODE_GRAPH", "1")
+    a = G.generate(m, prompt, max_new_tokens=21)          # 1 + 8-step chunks + single steps
+    sess = dict(G._SESSIONS)
+    b = G.generate(m, prompt, max_new_tokens=21)
+    assert a == b and all(len(o) == 71 for o in a)
+    assert len(sess) == 1 and all(G._SESSIONS[k]["graphs"] is v["graphs"] for k, v in sess.items())
+    monkeypatch.setenv("DPFS_DECODE_GRAPH", "0")
+    assert G.generate(m, prompt, max_new_tokens=21) == a
+    with torch.no_grad():
+        m.lm_head.weight.mul_(-1.0)                       # version bump: the captured graphs are stale
+    e = G.generate(m, prompt, max_new_tokens=21)
+    monkeypatch.setenv("DPFS_DECODE_GRAPH", "1")
+    g = G.generate(m, prompt, max_new_tokens=21)
+    assert g == e
+    assert all(G._SESSIONS[k]["graphs"] is not v["graphs"] for k, v in sess.items())
+
+
 def test_kernel_debug_modes_run_clean_and_catch_nan(dist1, monkeypatch):
     """DPFS_SYNC_DEBUG / DPFS_NAN_CHECK: a clean step raises nothing; a NaN weight is
     reported against the first kernel op that produces non-finite values."""

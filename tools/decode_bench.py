@@ -41,7 +41,8 @@ def main():
         prompt = torch.randint(0, args.vocab_size, (B, a.prompt), device="cuda")
         for mode in ("graph", "eager"):
             os.environ["DPFS_DECODE_GRAPH"] = "1" if mode == "graph" else "0"
-            generate(m, prompt, max_new_tokens=8)               # warm-up (GEMM choices, pools)
+            generate(m, prompt, max_new_tokens=a.new)           # warm-up: GEMM choices, graph capture
+                                                                #   (reused by the same-shape call)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             generate(m, prompt, max_new_tokens=a.new)
