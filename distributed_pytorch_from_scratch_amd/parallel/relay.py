@@ -126,9 +126,8 @@ class RelayComm:
             for j, k in enumerate(self.relays):
                 ops.append(P(dist.irecv, recv[d + j * q: d + (j + 1) * q], k))
             works = dist.batch_isend_irecv(ops)
-        if relay_buf is not None and relay_buf.is_cuda:
-            relay_buf.record_stream(side)
-        return works + ([_Fence()] if fence else [])
+        # relay_buf is read by the second hop: it lives until the caller's wait on the handle
+        return works + [_Hold(relay_buf)] + ([_Fence()] if fence else [])
 
     # ----------------------------------------------------------------- collectives ----
     def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = True):
@@ -181,6 +180,17 @@ class RelayComm:
             h.wait()
             return None
         return h
+
+
+class _Hold:
+    """Keeps a tensor an in-flight transfer reads alive until the handle is waited."""
+
+    def __init__(self, t):
+        self.t = t
+
+    def wait(self):
+        self.t = None
+        return True
 
 
 class _Fence:
