@@ -731,6 +731,8 @@ bool gemv_nt_ok(torch::Tensor x, torch::Tensor w, bool swiglu) {
     return false;
   const int64_t K = w.size(1);
   if (x.size(1) != (swiglu ? 2 * K : K)) return false;
+  if (reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 || reinterpret_cast<uintptr_t>(w.data_ptr()) % 16)
+    return false;   // 16-byte operand loads
   return dpfs_gemv16_ok((int)x.size(0), (int)w.size(0), (int)K, x.stride(0), w.stride(0)) != 0;
 }
 

@@ -236,7 +236,9 @@ def _session(model, B: int, t_max: int, dev):
     """The KV cache and decode graphs for this (model, batch, length): reused by the next
     generate() call of the same shape, so serving pays the graph capture once.  Reused only
     while it is the same live model object and no parameter changed since the capture (the
-    graphs hold the bf16 weight copies of that version); otherwise rebuilt."""
+    graphs hold the bf16 weight copies of that version); otherwise rebuilt.  One kept shape
+    per model, and only caches up to DPFS_DECODE_SESSION_MAX_GB (default 16) are kept;
+    ``clear_sessions()`` frees them."""
     attn0 = model.layers[0].attn
     key = (id(model), B, t_max, str(dev))
     vers = tuple(p._version for p in model.parameters())
@@ -246,11 +248,18 @@ def _session(model, B: int, t_max: int, dev):
         return ent["cache"], ent["graphs"]
     cache = KVCache(len(model.layers), B, t_max, attn0.num_local_heads, attn0.head_dim, model.act_dtype(dev), dev)
     graphs = {}
-    if _use_graph(dev):
+    kv_bytes = sum(t.numel() * t.element_size() for t in cache.k + cache.v)
+    keep_gb = float(os.environ.get("DPFS_DECODE_SESSION_MAX_GB", "16"))
+    if _use_graph(dev) and kv_bytes <= keep_gb * 2 ** 30:
         for k in [k for k, e in _SESSIONS.items() if e["model"]() is None or k[0] == id(model)]:
             del _SESSIONS[k]          # dead models, and other shapes of this one
         _SESSIONS[key] = {"model": weakref.ref(model), "vers": vers, "cache": cache, "graphs": graphs}
     return cache, graphs
+
+
+def clear_sessions():
+    """Drop every kept KV cache and decode graph (frees their device memory)."""
+    _SESSIONS.clear()
 
 
 @torch.inference_mode()
