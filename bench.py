@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--layers", type=int, default=None, help="debug only: not a valid headline number")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--recompute", action="store_true", help="activation recompute (layer inputs only)")
+    ap.add_argument("--fp8", action="store_true",
+                    help="fp8 (e4m3 / e5m2) forward and data-gradient GEMMs (ops/fp8.py); NOT the bf16 headline")
     return ap.parse_args()
 
 
@@ -105,6 +107,8 @@ def main():
         overrides["num_layers"] = a.layers
     if a.recompute:
         overrides["recompute"] = True
+    if a.fp8:
+        overrides["fp8"] = True
     args = get_preset(a.model, **overrides)
     T = a.seq_len
     assert T <= args.maxlen
@@ -230,7 +234,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if a.global_batch else "weak",
         "vs_baseline": round(vs, 4) if vs else None,
-        "dtype": "bf16" if dev.type == "cuda" else "fp32",
+        "dtype": ("fp8-e4m3/e5m2 GEMMs + bf16" if a.fp8 else "bf16") if dev.type == "cuda" else "fp32",
         "data": "synthetic (uniform random token ids), random-init weights",
         "config": {
             "model": a.model + (f"(L={a.layers})" if a.layers else ""),
@@ -239,6 +243,7 @@ def main():
             "parallelism": f"tp{tp}" + (f"dp{p.dp_size}" if p.dp_size > 1 else "") + ("+sp" if sp_used else ""),
             "impl": a.impl,
             "recompute": bool(a.recompute),
+            "fp8": bool(a.fp8),
             "params_matmul": args.matmul_params(),
             "tp_comm": tp_comm.info(),
             "chunks": model.overlap_chunks() if a.impl == "ours" else None,

@@ -72,6 +72,8 @@ void dpfs_attn_decode(const void*, long long, const void*, const void*, const in
                       int, int, float, hipStream_t);
 void dpfs_kv_append(const void*, const void*, long long, void*, void*, const int*, int, int, int, int, hipStream_t);
 void dpfs_step_advance(int*, int64_t*, int, hipStream_t);
+void dpfs_fp8_quant(const void*, long long, int, void*, float*, float*, hipStream_t);
+int dpfs_fp8_work_floats();
 int dpfs_gemv16_ok(int, int, int, long long, long long);
 void dpfs_gemv16(const void*, long long, const void*, long long, const float*, void*, long long, int, int, int, int,
                  hipStream_t);
@@ -768,6 +770,27 @@ void rope_append(torch::Tensor qkv, torch::Tensor pos, torch::Tensor table, torc
                    vc.data_ptr(), len.data_ptr<int>(), (int)B, (int)H, (int)hd, (int)Tmax, stream());
 }
 
+// Per-tensor fp8 quantisation with current scaling: (q, inv) with q = sat(x * FMAX / amax)
+// in float8_e4m3fn (fmt 0) or float8_e5m2 (fmt 1), inv = amax / FMAX as an fp32 0-d tensor
+// (the scale torch._scaled_mm multiplies back).  No host synchronisation.
+std::vector<torch::Tensor> fp8_quant(torch::Tensor x, int64_t fmt) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && x.is_contiguous() && x.numel() % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "fp8_quant: x must be contiguous bf16 with numel % 8 == 0");
+  TORCH_CHECK(fmt == 0 || fmt == 1, "fp8_quant: fmt 0 (e4m3) or 1 (e5m2)");
+  const at::DeviceGuard g(x.device());
+  auto q = torch::empty(x.sizes(), x.options().dtype(fmt == 0 ? at::kFloat8_e4m3fn : at::kFloat8_e5m2));
+  auto inv = torch::empty({}, x.options().dtype(torch::kFloat32));
+  auto work = torch::empty({dpfs_fp8_work_floats()}, x.options().dtype(torch::kFloat32));
+  if (x.numel())
+    dpfs_fp8_quant(x.data_ptr(), x.numel(), (int)fmt, q.data_ptr(), inv.data_ptr<float>(), work.data_ptr<float>(),
+                   stream());
+  else
+    inv.fill_(1.0);
+  return {q, inv};
+}
+
 // *len += 1 and pos[:] = *len on the device (end of a decode step; graph-replayable).
 void step_advance(torch::Tensor len, torch::Tensor pos) {
   check_len(len);
@@ -966,6 +989,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("scale"));
   m.def("kv_append", &kv_append, py::arg("qkv"), py::arg("k_cache"), py::arg("v_cache"), py::arg("len"));
   m.def("step_advance", &step_advance, py::arg("len"), py::arg("pos"));
+  m.def("fp8_quant", &fp8_quant, py::arg("x"), py::arg("fmt") = 0);
   m.def("gemv_nt_ok", &gemv_nt_ok, py::arg("x"), py::arg("w"), py::arg("swiglu") = false);
   m.def("gemv_nt", &gemv_nt, py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("swiglu") = false);
   m.def("rope_append", &rope_append, py::arg("qkv"), py::arg("pos"), py::arg("table"), py::arg("k_cache"),

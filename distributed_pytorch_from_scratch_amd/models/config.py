@@ -52,6 +52,10 @@ class ModelArgs:
     # re-run the layer forward (collectives included) in backward.  ~16x less activation
     # memory per layer at GPT-2 width for ~1/3 more compute (long-sequence / large configs).
     recompute: bool = False
+    # fp8 GEMMs in the explicit-schedule engines (ops/fp8.py): forward and data-gradient
+    # projections with per-tensor e4m3 / e5m2 operands on hipBLASLt's fp8 kernels; weight
+    # gradients, attention, norms and the optimizer stay bf16 / fp32.  Off by default.
+    fp8: bool = False
 
     @property
     def head_dim(self) -> int:

@@ -40,6 +40,7 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
+from ..ops import fp8 as F8
 from ..ops import gemm_select as GS
 from ..ops.dispatch import K, shadow
 from ..parallel import process_manager as pm
@@ -120,6 +121,11 @@ class DecoderTrainFn(torch.autograd.Function):
         recompute = bool(getattr(model.args, "recompute", False))
 
         W = lambda w: shadow(w, dt) if w is not None else None  # bf16 compute copies
+        # fp8 step: one e4m3 copy (+ transposed copy) of every projection weight, looked up by
+        # ops.gemm_select for the forward and the data-gradient GEMMs of this step
+        f8map = F8.prepare([W(w) for L in layers for w in (L.wqkv, L.wo, L.wgu, L.wd)] + [W(model.lm_head.weight)]) \
+            if getattr(model.args, "fp8", False) else None
+        F8.activate(f8map)
         st = []  # per-chunk saved state
         for c in range(C):
             b0, b1 = bounds[c], bounds[c + 1]
@@ -187,6 +193,8 @@ class DecoderTrainFn(torch.autograd.Function):
         ctx.tab = tab
         ctx.nparams = len(params)
         ctx.recompute = recompute
+        ctx.f8map = f8map
+        F8.activate(None)
         return loss
 
     @staticmethod
@@ -196,6 +204,7 @@ class DecoderTrainFn(torch.autograd.Function):
         k = K(model.embedding.weight)
         head = model.lm_head
         W = lambda w: shadow(w, dt) if w is not None else None
+        F8.activate(ctx.f8map)
         tab = ctx.tab
         gscale_all = (gloss.float() / ctx.n_valid)
         nL = len(layers)
@@ -355,6 +364,7 @@ class DecoderTrainFn(torch.autograd.Function):
                       G.get("bgu") if L.bgu is not None else None, G.get("wd"),
                       G.get("bd") if L.bd is not None else None]
         grads += [g["nf"], g["lm_w"], g["lm_b"] if head.bias is not None else None]
+        F8.activate(None)
         return (None, None, None, None, None, None) + tuple(grads)
 
 

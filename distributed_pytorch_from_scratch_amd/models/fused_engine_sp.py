@@ -33,6 +33,7 @@ import math
 import torch
 import torch.distributed as dist
 
+from ..ops import fp8 as F8
 from ..ops import gemm_select as GS
 from ..ops.dispatch import K, shadow
 from ..parallel import process_manager as pm
@@ -77,6 +78,11 @@ class DecoderTrainFnSP(torch.autograd.Function):
         vst = head.odim_start
         vvalid = max(0, min(model.vocab_size - vst, head.odim_partition))
         W = lambda w: shadow(w, dt) if w is not None else None
+        # fp8 step: one e4m3 copy (+ transposed copy) of every projection weight, looked up by
+        # ops.gemm_select for the forward and the data-gradient GEMMs of this step
+        f8map = F8.prepare([W(w) for L in layers for w in (L.wqkv, L.wo, L.wgu, L.wd)] + [W(model.lm_head.weight)]) \
+            if getattr(model.args, "fp8", False) else None
+        F8.activate(f8map)
         st = []
         for c in range(C):
             b0, b1 = bounds[c], bounds[c + 1]
@@ -148,6 +154,8 @@ class DecoderTrainFnSP(torch.autograd.Function):
         ctx.model, ctx.st, ctx.layers, ctx.meta = model, st, layers, (T, dt, vst, vvalid, n)
         ctx.recompute = recompute
         ctx.n_valid, ctx.tab = n_valid_total, tab
+        ctx.f8map = f8map
+        F8.activate(None)
         return losses_sum / n_valid_total
 
     @staticmethod
@@ -157,6 +165,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
         k = K(model.embedding.weight)
         head = model.lm_head
         W = lambda w: shadow(w, dt) if w is not None else None
+        F8.activate(ctx.f8map)
         tab = ctx.tab
         gscale_all = gloss.float() / ctx.n_valid
         nL = len(layers)
@@ -307,4 +316,5 @@ class DecoderTrainFnSP(torch.autograd.Function):
                       G.get("bgu") if L.bgu is not None else None, G["wd"],
                       G.get("bd") if L.bd is not None else None]
         grads += [g["nf"], g["lm_w"], g["lm_b"] if head.bias is not None else None]
+        F8.activate(None)
         return (None, None, None, None, None, None) + tuple(grads)

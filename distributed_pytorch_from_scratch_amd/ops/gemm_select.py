@@ -19,6 +19,7 @@ from typing import Callable, Dict, Tuple
 import torch
 import torch.nn.functional as F
 
+from . import fp8 as F8
 from . import reference
 from .dispatch import shadow
 
@@ -74,6 +75,9 @@ def _aligned(*dims: int) -> bool:
 def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, out=None) -> torch.Tensor:
     """y[M,N] = x[M,K] w[N,K]^T (+ bias fp32[N]) in x.dtype (into ``out`` when given: e.g. a
     staging slot of the xGMI collectives, so the collective needs no copy-in)."""
+    fw = F8.lookup(w)
+    if fw is not None:          # fp8 step (ModelArgs.fp8): e4m3 operands, hipBLASLt fp8 GEMM
+        return F8.nt(x, fw, bias, out=out)
     m = mode()
     if k is reference or not x.is_cuda or (m == "ours" and _aligned(x.shape[1], w.shape[0])):
         return k.gemm_nt(x, w, bias, out=out)
@@ -111,6 +115,9 @@ def small_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, swiglu: bool = Fals
 
 def gemm_nn(k, a: torch.Tensor, b: torch.Tensor, out=None) -> torch.Tensor:
     """c[M,N] = a[M,K] b[K,N] in a.dtype (into ``out`` when given)."""
+    fw = F8.lookup(b, dgrad=True)
+    if fw is not None:          # fp8 step: e5m2 gradient x e4m3 weight
+        return F8.nn(a, fw, out=out)
     m = mode()
     if k is reference or not a.is_cuda or (m == "ours" and _aligned(a.shape[1], b.shape[1])):
         return k.gemm_nn(a, b, out=out)
@@ -132,6 +139,11 @@ def gemm_nt_rope(k, x: torch.Tensor, w: torch.Tensor, bias, pos, tab, rot_heads:
     """Packed QKV projection with rotate-half RoPE on the first ``rot_heads`` heads: our NT
     kernel with the rotation in its epilogue, or hipBLASLt followed by the in-place RoPE
     kernel (timed per shape like every plain GEMM)."""
+    fw = F8.lookup(w)
+    if fw is not None:          # fp8 step: fp8 GEMM, then the RoPE pass
+        y = F8.nt(x, fw, bias)
+        k.rope_(y, pos, tab, rot_heads, hd, False)
+        return y
     m = mode()
     if k is reference or not x.is_cuda or m == "ours" or not _aligned(x.shape[1], w.shape[0]) \
             or x.shape[0] < _MIN_ROWS:

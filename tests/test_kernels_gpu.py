@@ -397,6 +397,45 @@ def test_rope_append_matches_rope_then_append(C, hd, L):
     assert torch.equal(a, b) and torch.equal(ka, kb) and torch.equal(va, vb)
 
 
+@pytest.mark.parametrize("fmt", [0, 1])
+@pytest.mark.parametrize("n", [8, 4096, 3 * 1024 * 1024 + 8, 25 * 1024 * 1024])
+def test_fp8_quantize_matches_oracle(C, fmt, n):
+    """fp8 current-scaling quantisation (csrc/kernels/fp8.hip): same bytes and scale as the
+    PyTorch oracle (ops/fp8.py: the same fp32 operations), including a non-multiple grid."""
+    from distributed_pytorch_from_scratch_amd.ops import fp8 as F8
+    torch.manual_seed(26)
+    x = (torch.randn(n, device=DEV) * 3).bfloat16()
+    q, inv = C.fp8_quant(x, fmt)
+    qr, invr = F8.quantize_ref(x, fmt)
+    assert q.dtype == qr.dtype and inv.shape == ()
+    assert torch.equal(inv, invr)
+    assert torch.equal(q.view(torch.uint8), qr.view(torch.uint8))
+
+
+def test_fp8_gemms_against_oracle(C):
+    """fp8 forward (e4m3 x e4m3 + bias) and data-gradient (e5m2 x e4m3) GEMMs: close to the
+    bf16 product (quantisation error only) and equal to the fp32 product of the quantised
+    operands up to the GEMM's accumulation."""
+    from distributed_pytorch_from_scratch_amd.ops import fp8 as F8
+    torch.manual_seed(27)
+    M, N, K = 4096, 2304, 768
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device=DEV)
+    fw = F8.Fp8Weight(w)
+    y = F8.nt(x, fw, b)
+    ref = x.float() @ w.float().t() + b
+    assert y.dtype == torch.bfloat16 and _rel(y, ref) < 6e-2
+    x8, sx = F8.quantize(x, 0)
+    refq = (x8.float() * sx) @ (fw.w8.float() * fw.s).t() + b
+    assert _rel(y, refq) < 1e-2
+    dy = torch.randn(M, N, device=DEV).bfloat16()
+    fw.wt8 = fw.w8.t().contiguous()
+    dx = F8.nn(dy, fw)
+    refd = dy.float() @ w.float()
+    assert dx.shape == (M, K) and _rel(dx, refd) < 1e-1
+
+
 @pytest.mark.parametrize("M,V,valid,start", [(2048, 6288, 6241, 6288 * 7), (100, 50304, 50257, 0),
                                              (300, 500, 500, 500), (65, 37, 30, 0)])   # unaligned rows
 def test_ce_bwd_fused_bias_grad(C, M, V, valid, start):

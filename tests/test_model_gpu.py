@@ -223,6 +223,29 @@ def test_decode_session_reuse_and_weight_change(dist1, monkeypatch):
     assert all(G._SESSIONS[k]["graphs"] is not v["graphs"] for k, v in sess.items())
 
 
+def test_fp8_training_tracks_bf16(dist1, monkeypatch):
+    """ModelArgs.fp8: forward and data-gradient projections on fp8 GEMMs (threshold lowered so
+    every projection of a small model takes the fp8 path); the loss follows the bf16 run."""
+    from distributed_pytorch_from_scratch_amd.models import ModelArgs, Transformer
+    from distributed_pytorch_from_scratch_amd.engine import TrainStep
+    from distributed_pytorch_from_scratch_amd.utils.dist import set_seed
+    monkeypatch.setenv("DPFS_FP8_MIN_DIM", "128")
+    losses = {}
+    for f8 in (False, True):
+        m = Transformer.from_args(ModelArgs(attn_dim=256, ffn_dim=512, num_heads=4, num_layers=2, vocab_size=1024,
+                                            maxlen=256, fp8=f8)).cuda()
+        set_seed(0)
+        m.reset_parameters()
+        st = TrainStep(m, torch.optim.Adam(m.parameters(), lr=1e-3))
+        g = torch.Generator(device="cuda").manual_seed(5)
+        ids = torch.randint(0, 1024, (8, 256), device="cuda", generator=g)
+        pos = torch.arange(256, device="cuda").repeat(8, 1)
+        losses[f8] = [float(st(ids, pos, ids.roll(-1, 1))) for _ in range(6)]
+    for a, b in zip(losses[True], losses[False]):
+        assert abs(a - b) < 2e-2 * abs(b), losses
+    assert losses[True][-1] < losses[True][0] - 0.05
+
+
 def test_kernel_debug_modes_run_clean_and_catch_nan(dist1, monkeypatch):
     """DPFS_SYNC_DEBUG / DPFS_NAN_CHECK: a clean step raises nothing; a NaN weight is
     reported against the first kernel op that produces non-finite values."""
