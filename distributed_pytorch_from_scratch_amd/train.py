@@ -61,6 +61,8 @@ def get_train_args(argv=None) -> Namespace:
     g.add_argument("--reserv_last_n_ckpts", type=int, default=-1)
     g.add_argument("--batch_size", "-b", type=int, default=32)
     g.add_argument("--bf16", action="store_true", help="bf16 compute (always on for the GPU kernels)")
+    g.add_argument("--fp8", action="store_true",
+                   help="fp8 (e4m3 / e5m2) GEMMs for the large projections (ops/fp8.py); bf16 elsewhere")
     g.add_argument("--max_grad_norm", type=float, default=None)
     g.add_argument("--resume", type=str, default=None, help="checkpoint path, or 'latest'")
     g = p.add_argument_group("model")
@@ -96,7 +98,7 @@ def train(rank, args: Namespace):
     log0(f"{'Enable' if compute_dtype == torch.bfloat16 else 'Disable'} bf16 training  [{p}]")
 
     margs = replace(get_preset(args.model), sequence_parallel=args.sp,
-                    recompute=getattr(args, "recompute", False))
+                    recompute=getattr(args, "recompute", False), fp8=getattr(args, "fp8", False))
     model = Transformer.from_args(margs).to(dev)
     model.set_compute_dtype(compute_dtype)
     model.reset_parameters()
