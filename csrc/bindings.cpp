@@ -92,6 +92,12 @@ void dpfs_xgmi_clear_error(void*);
 int dpfs_xgmi_run(void*, int, int, const void*, void*, long long, long long, double, int, hipStream_t);
 void dpfs_xgmi_destroy(void*);
 void dpfs_adam_patch_grads(void*, const long long*, int, hipStream_t);
+// blas/blaslt.hip
+const char* dpfs_lt_last_error();
+int dpfs_lt_algos(int, long long, long long, long long, int);
+long long dpfs_lt_workspace(int, long long, long long, long long, int, int);
+int dpfs_lt_run(int, long long, long long, long long, const float*, int, const void*, const void*, void*, float, void*,
+                long long, hipStream_t);
 // comm/rccl_comm.hip
 const char* dpfs_rccl_last_error();
 int dpfs_rccl_id_bytes();
@@ -941,6 +947,56 @@ void rccl_broadcast(int64_t h, torch::Tensor t, int64_t root) {
                                  (int)root, stream()), "ncclBroadcast");
 }
 
+// ---- hipBLASLt, driven directly (blas/blaslt.hip) ----
+// layout 0 NT: out[M,N] bf16 = a[M,K] b[N,K]^T (+ bias fp32[N]);  1 NN: out = a[M,K] b[K,N];
+// 2 TN: out[M,N] fp32 (+)= a[K,M]^T b[K,N].  Operands contiguous bf16.
+int64_t lt_algos(int64_t layout, int64_t M, int64_t N, int64_t K, bool bias) {
+  return dpfs_lt_algos((int)layout, M, N, K, bias ? 1 : 0);
+}
+
+void lt_run(int64_t layout, torch::Tensor a, torch::Tensor b, torch::Tensor out, c10::optional<torch::Tensor> bias,
+            int64_t algo, bool accumulate) {
+  TORCH_CHECK(layout >= 0 && layout <= 2, "lt_run: layout 0 (NT), 1 (NN) or 2 (TN)");
+  for (const torch::Tensor* t : {&a, &b, &out}) {
+    check_cuda(*t, "lt_run operand");
+    TORCH_CHECK(t->dim() == 2 && t->is_contiguous(), "lt_run: 2-D contiguous operands");
+  }
+  TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "lt_run: bf16 operands");
+  int64_t M, N, K;
+  if (layout == 0) {
+    M = a.size(0), K = a.size(1), N = b.size(0);
+    TORCH_CHECK(b.size(1) == K, "lt_run NT: a [M,K], b [N,K]");
+  } else if (layout == 1) {
+    M = a.size(0), K = a.size(1), N = b.size(1);
+    TORCH_CHECK(b.size(0) == K, "lt_run NN: a [M,K], b [K,N]");
+  } else {
+    K = a.size(0), M = a.size(1), N = b.size(1);
+    TORCH_CHECK(b.size(0) == K, "lt_run TN: a [K,M], b [K,N]");
+  }
+  TORCH_CHECK(out.size(0) == M && out.size(1) == N, "lt_run: out must be [M, N]");
+  TORCH_CHECK(out.scalar_type() == (layout == 2 ? torch::kFloat32 : torch::kBFloat16),
+              "lt_run: out fp32 for TN, bf16 otherwise");
+  TORCH_CHECK(!accumulate || layout == 2, "lt_run: accumulate is TN only");
+  const float* bp = nullptr;
+  if (bias.has_value()) {
+    TORCH_CHECK(layout == 0, "lt_run: bias is NT only");
+    check_cuda(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->is_contiguous() && bias->numel() == N,
+                "lt_run: bias fp32 [N] contiguous");
+    bp = bias->data_ptr<float>();
+  }
+  TORCH_CHECK(a.device() == b.device() && a.device() == out.device(), "lt_run: operands on one device");
+  const at::DeviceGuard g(a.device());
+  const int n = dpfs_lt_algos((int)layout, M, N, K, bp ? 1 : 0);
+  TORCH_CHECK(algo >= 0 && algo < n, "lt_run: algorithm ", algo, " of ", n, " (", dpfs_lt_last_error(), ")");
+  const long long wsb = dpfs_lt_workspace((int)layout, M, N, K, bp ? 1 : 0, (int)algo);
+  torch::Tensor ws;
+  if (wsb > 0) ws = torch::empty({wsb}, a.options().dtype(torch::kUInt8));
+  const int st = dpfs_lt_run((int)layout, M, N, K, bp, (int)algo, a.data_ptr(), b.data_ptr(), out.data_ptr(),
+                             accumulate ? 1.f : 0.f, wsb > 0 ? ws.data_ptr() : nullptr, wsb > 0 ? wsb : 0, stream());
+  TORCH_CHECK(st == 0, "hipBLASLt: ", dpfs_lt_last_error());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -989,6 +1045,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("scale"));
   m.def("kv_append", &kv_append, py::arg("qkv"), py::arg("k_cache"), py::arg("v_cache"), py::arg("len"));
   m.def("step_advance", &step_advance, py::arg("len"), py::arg("pos"));
+  m.def("lt_algos", &lt_algos, py::arg("layout"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("bias") = false,
+        "hipBLASLt heuristic algorithms for a problem (0 NT, 1 NN, 2 TN)");
+  m.def("lt_run", &lt_run, py::arg("layout"), py::arg("a"), py::arg("b"), py::arg("out"), py::arg("bias") = py::none(),
+        py::arg("algo") = 0, py::arg("accumulate") = false);
   m.def("fp8_quant", &fp8_quant, py::arg("x"), py::arg("fmt") = 0);
   m.def("gemv_nt_ok", &gemv_nt_ok, py::arg("x"), py::arg("w"), py::arg("swiglu") = false);
   m.def("gemv_nt", &gemv_nt, py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("swiglu") = false);

@@ -1,20 +1,30 @@
 """Per-shape choice between our MFMA GEMM kernels and hipBLASLt for *plain* GEMMs.
 
 Our kernels (``csrc/kernels/gemm.hip``) carry every GEMM with a fused epilogue: RoPE in the QKV
-projection, the fp32 split-K weight-gradient GEMMs that accumulate in place. For the remaining
-plain bf16 GEMMs (the forward projections with at most a bias, and the NN data-gradient GEMMs),
-the first call on a new (layout, M, N, K, bias) shape times both implementations on the live
-operands. Every later call uses the faster one. hipBLASLt is reached through ``torch.nn.functional.linear`` /
-``torch.matmul``, with a bias epilogue where there is a bias. The measured per-shape winners are
-in ``choices()`` and in ``profiles/``.
+projection, the fp32 split-K weight-gradient GEMMs that accumulate in place. For the plain
+bf16 GEMMs (the forward projections with at most a bias, the NN data-gradient GEMMs) and the
+fp32-output weight-gradient GEMMs, the first call on a new (layout, M, N, K, bias) shape times
+the candidates on the live operands and every later call uses the fastest:
 
-``DPFS_GEMM_BACKEND`` = ``auto`` (default) | ``ours`` | ``blas`` pins the choice (tests pin
-``ours`` to exercise the HIP kernels).
+* ``ours``  -- our kernel;
+* ``blas``  -- hipBLASLt through ``torch.nn.functional.linear`` / ``torch.matmul`` /
+  ``torch.mm(out_dtype=fp32)`` (the library heuristic's first algorithm);
+* ``ltN``   -- hipBLASLt driven directly (``csrc/blas/blaslt.hip``) with algorithm N of its
+  heuristic list: every algorithm gets one quick timing, the two fastest enter the final
+  round.  On MI355X this finds 8-22 % faster algorithms for the weight-gradient GEMMs and the
+  QKV projection (``tools/blaslt_probe.cpp``, profiles/r2_blaslt_probe.txt).
+
+A library candidate must beat ``ours`` by 3 % to be chosen.  The measured per-shape winners
+are in ``choices()`` and in ``profiles/``.
+
+``DPFS_GEMM_BACKEND`` = ``auto`` (default) | ``ours`` | ``blas`` | ``lt`` pins the choice (tests
+pin ``ours`` to exercise the HIP kernels, ``lt`` runs hipBLASLt's first algorithm through our
+binding).  ``DPFS_GEMM_LT=0`` leaves the direct hipBLASLt candidates out of ``auto``.
 """
 from __future__ import annotations
 
 import os
-from typing import Callable, Dict, Tuple
+from typing import Callable, Dict, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -24,7 +34,7 @@ from . import reference
 from .dispatch import shadow
 
 _choice: Dict[Tuple, str] = {}
-_times: Dict[Tuple, Tuple[float, float]] = {}   # key -> (ours ms, hipBLASLt ms) at selection
+_times: Dict[Tuple, Dict[str, float]] = {}   # key -> {candidate: ms} at selection
 
 
 def mode() -> str:
@@ -33,7 +43,7 @@ def mode() -> str:
 
 def choices(with_times: bool = False) -> Dict[Tuple, object]:
     if with_times:
-        return {k: (c,) + tuple(round(t, 4) for t in _times.get(k, ())) for k, c in _choice.items()}
+        return {k: (c, {n: round(t, 4) for n, t in _times.get(k, {}).items()}) for k, c in _choice.items()}
     return dict(_choice)
 
 
@@ -48,16 +58,43 @@ def _ms(fn: Callable[[], torch.Tensor], reps: int = 3) -> float:
     return s.elapsed_time(e) / reps
 
 
-def _pick(key: Tuple, ours: Callable, blas: Callable) -> str:
+_LT_FINALISTS = 2
+
+
+def _lt_count(k, layout: int, M: int, N: int, K: int, bias: bool) -> int:
+    """Algorithms hipBLASLt offers for this problem through our binding (0: none / disabled)."""
+    if os.environ.get("DPFS_GEMM_LT", "1") == "0" or not hasattr(k, "lt_algos"):
+        return 0
+    return int(k.lt_algos(layout, M, N, K, bias))
+
+
+def _pick(key: Tuple, cands: Dict[str, Callable], lt_count: Callable[[], int] = lambda: 0,
+          lt_mk: Optional[Callable[[int], Callable]] = None) -> str:
     c = _choice.get(key)
     if c is None:
-        # two interleaved rounds, best of each: robust to a collective running alongside
-        t_o = min(_ms(ours), _ms(ours))
-        t_b = min(_ms(blas), _ms(blas))
-        c = "blas" if t_b < 0.97 * t_o else "ours"
+        cands = dict(cands)
+        n = lt_count() if lt_mk is not None else 0
+        if n > 0:
+            quick = []
+            for i in range(n):
+                try:
+                    quick.append((_ms(lt_mk(i), reps=2), i))
+                except RuntimeError:      # an algorithm the library rejects at run time
+                    continue
+            for _, i in sorted(quick)[:_LT_FINALISTS]:
+                cands[f"lt{i}"] = lt_mk(i)
+        # two rounds per candidate, best of each: robust to a collective running alongside
+        times = {name: min(_ms(fn), _ms(fn)) for name, fn in cands.items()}
+        c = min(times, key=times.get)
+        if c != "ours" and "ours" in times and times[c] >= 0.97 * times["ours"]:
+            c = "ours"
         _choice[key] = c
-        _times[key] = (t_o, t_b)
+        _times[key] = times
     return c
+
+
+def _lt_index(c: str) -> int:
+    return int(c[2:])
 
 
 # Below this many rows (decode steps, tiny batches) our 256-row tiles are mostly padding and
@@ -70,6 +107,14 @@ def _aligned(*dims: int) -> bool:
     """Our MFMA kernels stage 16-byte rows: every K / N (and TN's M) must be a multiple of 8.
     Uneven vocab shards (e.g. 1000 over 2 ranks at vocab_pad_to=1) go to hipBLASLt."""
     return all(d % 8 == 0 for d in dims)
+
+
+def _lt_operands_ok(*ts) -> bool:
+    return all(t is None or (t.is_contiguous() and t.dtype == torch.bfloat16) for t in ts)
+
+
+def _lt_bias_ok(bias) -> bool:
+    return bias is None or (bias.dtype == torch.float32 and bias.is_contiguous())
 
 
 def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, out=None) -> torch.Tensor:
@@ -91,13 +136,28 @@ def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, out=None) -> torch.T
         return torch.addmm(bb, x, w.t(), out=out)
     if not _aligned(x.shape[1], w.shape[0]) or x.shape[0] < _MIN_ROWS:
         return blas()
+    M, N, K = x.shape[0], w.shape[0], x.shape[1]
+    lt_ok = _lt_operands_ok(x, w, out) and _lt_bias_ok(bias)
+
+    def lt(i):
+        def run():
+            y = out if out is not None else torch.empty(M, N, device=x.device, dtype=x.dtype)
+            k.lt_run(0, x, w, y, bias, i)
+            return y
+        return run
 
     def ours():
         return k.gemm_nt(x, w, bias, out=out)
     if m == "blas":
         return blas()
-    key = ("nt", x.shape[0], w.shape[0], x.shape[1], bias is not None, x.device.index)
-    return blas() if _pick(key, ours, blas) == "blas" else ours()
+    if m == "lt":
+        return lt(0)() if lt_ok and _lt_count(k, 0, M, N, K, bias is not None) else blas()
+    key = ("nt", M, N, K, bias is not None, x.device.index)
+    c = _pick(key, {"ours": ours, "blas": blas}, lambda: _lt_count(k, 0, M, N, K, bias is not None),
+              lt if lt_ok else None)
+    if c == "ours" or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
+        return ours()
+    return blas() if c == "blas" else lt(_lt_index(c))()
 
 
 def small_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, swiglu: bool = False) -> torch.Tensor:
@@ -126,19 +186,33 @@ def gemm_nn(k, a: torch.Tensor, b: torch.Tensor, out=None) -> torch.Tensor:
         return torch.matmul(a, b) if out is None else torch.matmul(a, b, out=out)
     if not _aligned(a.shape[1], b.shape[1]) or a.shape[0] < _MIN_ROWS:
         return blas()
+    M, N, K = a.shape[0], b.shape[1], a.shape[1]
+    lt_ok = _lt_operands_ok(a, b, out)
+
+    def lt(i):
+        def run():
+            y = out if out is not None else torch.empty(M, N, device=a.device, dtype=a.dtype)
+            k.lt_run(1, a, b, y, None, i)
+            return y
+        return run
 
     def ours():
         return k.gemm_nn(a, b, out=out)
     if m == "blas":
         return blas()
-    key = ("nn", a.shape[0], b.shape[1], a.shape[1], a.device.index)
-    return blas() if _pick(key, ours, blas) == "blas" else ours()
+    if m == "lt":
+        return lt(0)() if lt_ok and _lt_count(k, 1, M, N, K, False) else blas()
+    key = ("nn", M, N, K, a.device.index)
+    c = _pick(key, {"ours": ours, "blas": blas}, lambda: _lt_count(k, 1, M, N, K, False), lt if lt_ok else None)
+    if c == "ours" or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
+        return ours()
+    return blas() if c == "blas" else lt(_lt_index(c))()
 
 
 def gemm_nt_rope(k, x: torch.Tensor, w: torch.Tensor, bias, pos, tab, rot_heads: int, hd: int) -> torch.Tensor:
     """Packed QKV projection with rotate-half RoPE on the first ``rot_heads`` heads: our NT
-    kernel with the rotation in its epilogue, or hipBLASLt followed by the in-place RoPE
-    kernel (timed per shape like every plain GEMM)."""
+    kernel with the rotation in its epilogue, or hipBLASLt (through torch or directly)
+    followed by the in-place RoPE kernel (timed per shape like every plain GEMM)."""
     fw = F8.lookup(w)
     if fw is not None:          # fp8 step: fp8 GEMM, then the RoPE pass
         y = F8.nt(x, fw, bias)
@@ -149,18 +223,34 @@ def gemm_nt_rope(k, x: torch.Tensor, w: torch.Tensor, bias, pos, tab, rot_heads:
             or x.shape[0] < _MIN_ROWS:
         return k.gemm_nt(x, w, bias, pos, tab, rot_heads, hd)
     bb = shadow(bias, x.dtype) if bias is not None else None
+    M, N, K = x.shape[0], w.shape[0], x.shape[1]
+    lt_ok = _lt_operands_ok(x, w) and _lt_bias_ok(bias)
 
     def blas():
         y = F.linear(x, w, bb)
         k.rope_(y, pos, tab, rot_heads, hd)
         return y
 
+    def lt(i):
+        def run():
+            y = torch.empty(M, N, device=x.device, dtype=x.dtype)
+            k.lt_run(0, x, w, y, bias, i)
+            k.rope_(y, pos, tab, rot_heads, hd)
+            return y
+        return run
+
     def ours():
         return k.gemm_nt(x, w, bias, pos, tab, rot_heads, hd)
     if m == "blas":
         return blas()
-    key = ("nt_rope", x.shape[0], w.shape[0], x.shape[1], hd, x.device.index)
-    return blas() if _pick(key, ours, blas) == "blas" else ours()
+    if m == "lt":
+        return lt(0)() if lt_ok and _lt_count(k, 0, M, N, K, bias is not None) else blas()
+    key = ("nt_rope", M, N, K, hd, x.device.index)
+    c = _pick(key, {"ours": ours, "blas": blas}, lambda: _lt_count(k, 0, M, N, K, bias is not None),
+              lt if lt_ok else None)
+    if c == "ours" or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
+        return ours()
+    return blas() if c == "blas" else lt(_lt_index(c))()
 
 
 _TN_BLAS = {}   # device index -> whether hipBLASLt's bf16 x bf16 -> fp32 mm works on this build
@@ -196,9 +286,10 @@ def _tn_blas_ok(a, b) -> bool:
 
 
 def gemm_tn(k, a: torch.Tensor, b: torch.Tensor, out=None, accumulate: bool = False) -> torch.Tensor:
-    """fp32 c[M,N] (+)= a[K,M]^T b[K,N] (weight gradients): our split-K kernel or hipBLASLt
-    with fp32 output, timed per (shape, accumulate) on a scratch output (an accumulating
-    candidate must not be timed into the live gradient)."""
+    """fp32 c[M,N] (+)= a[K,M]^T b[K,N] (weight gradients): our split-K kernel, hipBLASLt through
+    torch (fp32 output) or hipBLASLt directly (accumulating in place, beta = 1), timed per
+    (shape, accumulate) on a scratch output (an accumulating candidate must not be timed into
+    the live gradient)."""
     if k is reference or not a.is_cuda:
         return k.gemm_tn(a, b, out, accumulate) if out is not None else k.gemm_tn(a, b)
     if not _aligned(a.shape[1], b.shape[1]):
@@ -208,19 +299,36 @@ def gemm_tn(k, a: torch.Tensor, b: torch.Tensor, out=None, accumulate: bool = Fa
         if accumulate:
             return out.add_(c)
         return out.copy_(c)
+    M, N, K = a.shape[1], b.shape[1], a.shape[0]
+    lt_ok = _lt_operands_ok(a, b) and (out is None or out.is_contiguous())
 
     def run(kind, dst, acc):
         if kind == "blas":
             return _blas_tn(a, b, dst, acc)
+        if kind.startswith("lt"):
+            if dst is None:
+                dst, acc = torch.empty(M, N, device=a.device, dtype=torch.float32), False
+            k.lt_run(2, a, b, dst, None, _lt_index(kind), acc)
+            return dst
         return k.gemm_tn(a, b, dst, acc) if dst is not None else k.gemm_tn(a, b)
     m = mode()
-    if m == "ours" or a.shape[0] < _MIN_ROWS or not _tn_blas_ok(a, b):
+    if m == "ours" or a.shape[0] < _MIN_ROWS:
         return run("ours", out, accumulate)
-    if m == "blas":
+    blas_ok = _tn_blas_ok(a, b)
+    if m == "blas" and blas_ok:
         return run("blas", out, accumulate)
-    key = ("tn", a.shape[1], b.shape[1], a.shape[0], bool(accumulate), a.device.index)
+    if m == "lt":
+        ok = lt_ok and _lt_count(k, 2, M, N, K, False) > 0
+        return run("lt0" if ok else "ours", out, accumulate)
+    key = ("tn", M, N, K, bool(accumulate), a.device.index)
     c = _choice.get(key)
     if c is None:
-        scratch = torch.zeros(a.shape[1], b.shape[1], device=a.device, dtype=torch.float32)
-        c = _pick(key, lambda: run("ours", scratch, accumulate), lambda: run("blas", scratch, accumulate))
+        scratch = torch.zeros(M, N, device=a.device, dtype=torch.float32)
+        cands = {"ours": lambda: run("ours", scratch, accumulate)}
+        if blas_ok:
+            cands["blas"] = lambda: run("blas", scratch, accumulate)
+        c = _pick(key, cands, lambda: _lt_count(k, 2, M, N, K, False),
+                  (lambda i: (lambda: run(f"lt{i}", scratch, accumulate))) if lt_ok else None)
+    if c.startswith("lt") and not lt_ok:
+        c = "ours"
     return run(c, out, accumulate)

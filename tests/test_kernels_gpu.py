@@ -573,7 +573,7 @@ def test_fused_adam_load_state_dict_after_first_step(C):
         assert (p.detach() - r.detach()).abs().max().item() < 1e-5
 
 
-@pytest.mark.parametrize("backend", ["blas", "auto"])
+@pytest.mark.parametrize("backend", ["blas", "lt", "auto"])
 def test_gemm_select_tn_and_qkv_rope_paths(C, backend, monkeypatch):
     """gemm_select's hipBLASLt candidates for the fp32 wgrad (incl. accumulate into a live
     gradient) and for the RoPE'd QKV projection match the fp32 oracle; `auto` times both on a
@@ -602,3 +602,37 @@ def test_gemm_select_tn_and_qkv_rope_paths(C, backend, monkeypatch):
     yr = R.gemm_nt(x.float(), w.float(), bias, pos, tab, 2 * H, hd)
     assert _rel(y, yr) < 1e-2
     GS._choice.clear()
+
+
+@pytest.mark.parametrize("layout", [0, 1, 2])
+def test_blaslt_direct_every_algorithm(C, layout):
+    """hipBLASLt driven through our binding (csrc/blas/blaslt.hip): every heuristic algorithm
+    of NT (+ fp32 bias epilogue), NN and TN (fp32 out, overwrite and beta = 1 accumulate) on
+    row-major PyTorch operands matches the fp32 oracle."""
+    torch.manual_seed(31 + layout)
+    M, N, K = 512, 384, 640
+    bias = None
+    if layout == 0:
+        a = torch.randn(M, K, device=DEV).bfloat16()
+        b = torch.randn(N, K, device=DEV).bfloat16()
+        bias = torch.randn(N, device=DEV)
+        ref = a.float() @ b.float().t() + bias
+    elif layout == 1:
+        a = torch.randn(M, K, device=DEV).bfloat16()
+        b = torch.randn(K, N, device=DEV).bfloat16()
+        ref = a.float() @ b.float()
+    else:
+        a = torch.randn(K, M, device=DEV).bfloat16()
+        b = torch.randn(K, N, device=DEV).bfloat16()
+        ref = a.float().t() @ b.float()
+    n = C.lt_algos(layout, M, N, K, bias is not None)
+    assert n > 0, "hipBLASLt offered no algorithm"
+    for i in range(n):
+        out = torch.empty(M, N, device=DEV, dtype=torch.float32 if layout == 2 else torch.bfloat16)
+        C.lt_run(layout, a, b, out, bias, i)
+        assert _rel(out, ref) < (1e-3 if layout == 2 else 1e-2), f"algorithm {i}"
+        if layout == 2:
+            C.lt_run(layout, a, b, out, None, i, True)
+            assert _rel(out, 2 * ref) < 1e-3, f"algorithm {i} (accumulate)"
+    with pytest.raises(RuntimeError):
+        C.lt_run(layout, a, b, torch.empty(M + 1, N, device=DEV), bias, 0)

@@ -2,11 +2,11 @@
 
 Two-stage native build, no hipify, no JIT cache:
 
-1. every ``csrc/kernels/*.hip`` -> ``hipcc --offload-arch=gfx950 -O3 -c`` (pure HIP, no torch
-   headers, so each kernel file compiles in seconds; parallel; mtime-cached);
+1. every ``csrc/{kernels,comm,blas}/*.hip`` -> ``hipcc --offload-arch=gfx950 -O3 -c`` (pure HIP,
+   no torch headers, so each file compiles in seconds; parallel; mtime-cached);
 2. ``csrc/bindings.cpp`` -> ``g++`` against the PyTorch headers (host code only);
-3. link with the ROCm runtime that PyTorch itself ships (``torch/lib/libamdhip64.so``), so
-   the process has exactly one HIP runtime.
+3. link with the ROCm runtime, RCCL and hipBLASLt that PyTorch itself ships (``torch/lib``), so
+   the process has exactly one instance of each.
 
 Usage: ``python tools/build_ext.py [--jobs N] [--force]`` (also called by ``setup.py`` and
 ``__graft_entry__.build()``).
@@ -62,7 +62,8 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> str:
     hipcc = _hipcc()
     headers = glob.glob(os.path.join(CSRC, "kernels", "*.h")) + glob.glob(os.path.join(CSRC, "comm", "*.h"))
     kernels = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))) + \
-        sorted(glob.glob(os.path.join(CSRC, "comm", "*.hip")))
+        sorted(glob.glob(os.path.join(CSRC, "comm", "*.hip"))) + \
+        sorted(glob.glob(os.path.join(CSRC, "blas", "*.hip")))
     hip_flags = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
                  "-munsafe-fp-atomics", "-Wno-unused-result"]
     jobs_list = []
@@ -98,7 +99,8 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> str:
         tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
         link = ["g++", "-shared", "-o", out] + objs + [
             "-L" + tlib, "-Wl,-rpath," + tlib, "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python",
-            "-lc10_hip", "-ltorch_hip", "-lamdhip64", "-lrccl"]   # torch's own librccl.so (same instance)
+            "-lc10_hip", "-ltorch_hip", "-lamdhip64", "-lrccl",   # torch's own librccl.so (same instance)
+            "-lhipblaslt"]                                       # and torch's own libhipblaslt.so
         _run(link)
         if verbose:
             print("[build_ext] linked", out, flush=True)
