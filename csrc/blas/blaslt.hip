@@ -2,11 +2,11 @@
 // instance), for the plain GEMMs where its heuristic's FIRST algorithm -- the one
 // torch.nn.functional.linear / torch.matmul / mm(out_dtype=fp32) run -- is not its fastest.
 //
-// tools/blaslt_probe.cpp on MI355X (GPT-2 small step shapes, 64 heuristic algorithms each):
-// the weight-gradient GEMMs (bf16 x bf16 -> fp32, accumulating in place with beta = 1) and the
-// QKV projection have algorithms 4-22 % faster than heuristic #0 and than our split-K TN kernel.
-// The plan (descriptors + the heuristic's algorithm list) is built once per shape; which
-// algorithm runs is chosen by ops/gemm_select.py, by timing on the live operands.
+// tools/blaslt_probe.cpp / tools/lt_probe.py on MI355X (GPT-2 small step shapes, 64 heuristic
+// algorithms each): for several projections an algorithm further down the list beats heuristic
+// #0 by 4-17 % (profiles/r2_blaslt_probe.txt).  The plan (descriptors + the heuristic's
+// algorithm list) is built once per shape; which algorithm runs is chosen by
+// ops/gemm_select.py, by timing on the live operands against our kernels and torch's path.
 //
 // Row-major PyTorch tensors are handed to the column-major library as their transposes:
 //   0 NT  y[M,N]  = x[M,K] w[N,K]^T (+ bias[N] fp32)  ->  D^T[N,M] = op_T(w) x^T

@@ -11,8 +11,9 @@ the candidates on the live operands and every later call uses the fastest:
   ``torch.mm(out_dtype=fp32)`` (the library heuristic's first algorithm);
 * ``ltN``   -- hipBLASLt driven directly (``csrc/blas/blaslt.hip``) with algorithm N of its
   heuristic list: every algorithm gets one quick timing, the two fastest enter the final
-  round.  On MI355X this finds 8-22 % faster algorithms for the weight-gradient GEMMs and the
-  QKV projection (``tools/blaslt_probe.cpp``, profiles/r2_blaslt_probe.txt).
+  round.  In the GPT-2-small step it wins the small projections by 4-10 % over torch's
+  algorithm (Wo / down forward, Wo / QKV data gradient); our split-K kernel keeps every
+  weight-gradient GEMM (profiles/r2_blaslt_probe.txt).
 
 A library candidate must beat ``ours`` by 3 % to be chosen.  The measured per-shape winners
 are in ``choices()`` and in ``profiles/``.
