@@ -4,7 +4,10 @@
 
 Groups dispatches by kernel name (template arguments shortened), prints total / per-step time,
 call counts and share of GPU time.  ``--steps`` divides totals by the number of training steps
-the profiled run executed (warmup + timed) to give ms/step per kernel.
+the profiled run executed (warmup + timed) to give ms/step per kernel.  ``--after adam_k
+--skip 5`` (rocpd database only) keeps the dispatches that start after the 5th dispatch whose
+name contains ``adam_k`` -- i.e. the timed steps of ``bench.py --warmup 5`` -- and also
+reports the first-to-last dispatch span.
 """
 from __future__ import annotations
 
@@ -22,14 +25,28 @@ def _short(name: str, width: int = 90) -> str:
     return name if len(name) <= width else name[: width - 3] + "..."
 
 
-def load(path: str):
+def load(path: str, after: str = None, skip: int = 0, span=None):
     rows = defaultdict(lambda: [0.0, 0])
     if path.endswith(".db"):
         con = sqlite3.connect(path)
-        for name, dur in con.execute("select name, duration from kernels"):
+        recs = list(con.execute("select name, start, end from kernels order by start"))
+        t0 = None
+        if after:
+            marks = [st for name, st, _ in recs if after in name]
+            if len(marks) < skip:
+                raise SystemExit(f"only {len(marks)} dispatches match {after!r} (need {skip})")
+            t0 = marks[skip - 1] if skip > 0 else None
+        first = last = None
+        for name, st, en in recs:
+            if t0 is not None and st <= t0:
+                continue
+            first = st if first is None else first
+            last = en if last is None else max(last, en)
             r = rows[_short(name)]
-            r[0] += dur / 1e6
+            r[0] += (en - st) / 1e6
             r[1] += 1
+        if span is not None and first is not None:
+            span.append((last - first) / 1e6)
     else:
         with open(path) as f:
             for rec in csv.DictReader(f):
@@ -50,11 +67,16 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--csv", default=None)
+    ap.add_argument("--after", default=None, help="keep dispatches after the --skip'th one containing this")
+    ap.add_argument("--skip", type=int, default=0)
     a = ap.parse_args(argv)
-    rows = load(a.path)
+    span = []
+    rows = load(a.path, a.after, a.skip, span)
     tot = sum(v[0] for v in rows.values())
     items = sorted(rows.items(), key=lambda kv: -kv[1][0])
     print(f"total GPU kernel time {tot:.2f} ms over {a.steps} step(s) = {tot / a.steps:.2f} ms/step")
+    if span:
+        print(f"first-to-last dispatch {span[0]:.2f} ms = {span[0] / a.steps:.2f} ms/step")
     print(f"{'ms/step':>9} {'calls/step':>10} {'us/call':>9} {'share':>6}  kernel")
     for name, (ms, n) in items[: a.top]:
         print(f"{ms / a.steps:9.3f} {n / a.steps:10.1f} {1e3 * ms / max(1, n):9.1f} {100 * ms / tot:5.1f}%  {name}")
