@@ -38,7 +38,7 @@ from ..ops import gemm_select as GS
 from ..ops.dispatch import K, shadow
 from ..parallel import process_manager as pm
 from ..parallel import tp_comm
-from .fused_engine import _Layer, _addg, _split, _wait
+from .fused_engine import _Layer, _addg, _defer_begin, _defer_end, _defer_flush, _split, _wait
 
 
 def _rs(full: torch.Tensor, n: int):
@@ -166,6 +166,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
         head = model.lm_head
         W = lambda w: shadow(w, dt) if w is not None else None
         F8.activate(ctx.f8map)
+        _defer_begin()
         tab = ctx.tab
         gscale_all = gloss.float() / ctx.n_valid
         nL = len(layers)
@@ -185,6 +186,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
         def dp_reduce(d: dict, keys=None):
             if dp <= 1:
                 return
+            _defer_flush()
             keys = [key for key in (keys or sorted(d)) if d.get(key) is not None]
             if keys:
                 flat = torch.cat([d[key].reshape(-1) for key in keys])
@@ -201,9 +203,19 @@ class DecoderTrainFnSP(torch.autograd.Function):
             if db is not None:
                 g["lm_b"] = _addg(g["lm_b"], db)
             del s["logits"], s["hf"]
+        def norm_bwd(dy, x, w, r, dres, bias_below, below_key):
+            """RMSNorm backward on my rows (+ residual grad); the bias grad of the projection
+            whose output feeds this residual (column sums of the result) from the same pass."""
+            db = dy.new_empty(dy.size(1), dtype=torch.float32) if bias_below is not None else None
+            out, ds = k.rmsnorm_bwd(dy, x, w, r, dres, db)
+            if db is not None:
+                below_key[0][below_key[1]] = _addg(below_key[0].get(below_key[1]), db)
+            return out, ds
+
         for s in st:    # final norm backward on my rows -> all-gather the residual grad
             _wait(s["h"])
-            s["g"], dsf = k.rmsnorm_bwd(s["dpend"], s["xf"], model.norm.scale, s["rf"])
+            s["g"], dsf = norm_bwd(s["dpend"], s["xf"], model.norm.scale, s["rf"], None,
+                                   layers[-1].bd, (gl[nL - 1], "bd"))
             g["nf"] = _addg(g["nf"], dsf)
             s["gfull"], s["h"] = _ag(s["g"], n)
             del s["xf"], s["rf"], s["dpend"]
@@ -243,8 +255,8 @@ class DecoderTrainFnSP(torch.autograd.Function):
             for ci, s in enumerate(st):    # B4: down / SwiGLU / gate|up grads -> reduce-scatter
                 _wait(s["h"])
                 a, gq = s["layers"][li], s["gfull"]
-                if L.bd is not None:   # partial over my rows (summed over TP by TrainStep)
-                    G["bd"] = _addg(G.get("bd"), k.bias_grad(s["g"]))
+                # (bd's grad, partial over my rows and summed over TP by TrainStep, came out of
+                # the norm backward above this layer)
                 ds = GS.gemm_nn(k, gq, W(L.wd))
                 tn(G, "wd", gq, a["sw"])
                 dbgu = ds.new_empty(a["gu"].size(1), dtype=torch.float32) if L.bgu is not None else None
@@ -257,15 +269,13 @@ class DecoderTrainFnSP(torch.autograd.Function):
             for s in st:    # B3: norm2 backward (+ residual grad) on my rows -> all-gather
                 _wait(s["h"])
                 a = s["layers"][li]
-                s["g"], ds2 = k.rmsnorm_bwd(s["dpend"], a["x2"], L.s2, a["r2"], s["g"])
+                s["g"], ds2 = norm_bwd(s["dpend"], a["x2"], L.s2, a["r2"], s["g"], L.bo, (G, "bo"))
                 G["s2"] = _addg(G.get("s2"), ds2)
                 s["gfull"], s["h"] = _ag(s["g"], n)
                 del a["x2"], a["r2"], s["dpend"]
             for ci, s in enumerate(st):    # B2: Wo / attention / QKV grads -> reduce-scatter
                 _wait(s["h"])
                 a, g2 = s["layers"][li], s["gfull"]
-                if L.bo is not None:
-                    G["bo"] = _addg(G.get("bo"), k.bias_grad(s["g"]))
                 do = GS.gemm_nn(k, g2, W(L.wo))
                 tn(G, "wo", g2, a["o"].view(g2.size(0), -1))
                 Bc = s["B"]
@@ -284,7 +294,8 @@ class DecoderTrainFnSP(torch.autograd.Function):
             for s in st:    # B1: norm1 backward (+ residual grad) on my rows -> all-gather
                 _wait(s["h"])
                 a = s["layers"][li]
-                s["g"], ds1 = k.rmsnorm_bwd(s["dpend"], a["x"], L.s1, a["r1"], s["g"])
+                s["g"], ds1 = norm_bwd(s["dpend"], a["x"], L.s1, a["r1"], s["g"],
+                                       layers[li - 1].bd if li > 0 else None, (gl[li - 1], "bd"))
                 G["s1"] = _addg(G.get("s1"), ds1)
                 s["gfull"], s["h"] = _ag(s["g"], n)
                 del a["x"], a["r1"], s["dpend"]
@@ -296,6 +307,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
             g["emb"] = _addg(g["emb"], dwe)
             del s["gfull"]
         dp_reduce(g, ("emb", "nf"))
+        _defer_end()
         tp_comm.check()
         if dp_pending:
             model._dpfs_dp_reduced = True
