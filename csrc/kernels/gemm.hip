@@ -730,233 +730,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_bf16_k(const float* __restr
   }
 }
 
-// ======================================================= GEMM v6 (8-phase ping-pong) ====
-// 256x256x64 tile, 8 waves (2 per SIMD) in two groups staggered by one barrier, after the
-// CDNA guide's 256^2 8-phase structure (cdna_hip_programming.md §5 "The 256^2 8-phase
-// template"); written for this repo's three layouts and epilogues.  What v3 lacked (PMC in
-// profiles/r2_gemm_v4_experiment.txt: one 64-deep K tile in flight, vmcnt(0) per K-step):
-//  * LDS = 8 half-tile slots of 16 KiB (128 rows/cols x 64 k): half-tile h = 4t + j of K-tile
-//    t is j = 0 A rows 0-127, 1 B cols 0-127, 2 B cols 128-255, 3 A rows 128-255 (the order
-//    the phases first read them), slot h & 7;
-//  * wave w: group wr = w / 4 (rows wr*64 of each A half), wc = w % 4 (cols wc*32 of each B
-//    half).  Its 128x64 output is four 64x32 quadrants (qm, qn), one per phase, in the order
-//    (0,0) (0,1) (1,1) (1,0): phase 0 reads A0 + B0, 1 reads B1, 2 reads A1, 3 reads nothing
-//    (B0 kept in registers); 16 MFMAs per phase;
-//  * phase q issues half-tile q + 6 (one 2-piece LDS-DMA per wave) into the slot freed >= 2
-//    phases earlier, then a COUNTED vmcnt (never 0 in the loop) retires exactly the
-//    half-tiles phase q + 1 reads: 4-5 half-tiles (64-80 KiB) stay in flight;
-//  * per phase: [ds_reads, DMA issue, vmcnt] barrier [lgkmcnt(0), setprio 1, 16 MFMA]
-//    barrier; group 1 starts one barrier late, so on every SIMD one wave multiplies while
-//    the other reads / issues (ping-pong).  RAW: a half-tile read at phase q + 1 was waited
-//    for by group 0 in phase q's load section and by group 1 in its (one slot later) load
-//    section, both before the barrier preceding the read.  WAR: a slot is re-filled >= 2
-//    phases after its last ds_read, whose lgkmcnt(0) precedes a barrier both groups pass.
-//  * K tails and half-tiles past the last K-tile are issued with out-of-range offsets
-//    (zeros, no HBM traffic) so every phase's vmcnt count is the same constant.
-template <bool AK, bool BKM, int OUT>
-__global__ __launch_bounds__(512, 1) void gemm8_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                  void* __restrict__ C, const float* __restrict__ bias, int M, int N,
-                                                  int K, int lda, int ldb, int ldc, int k_per_split, int splits,
-                                                  long long slab_stride, unsigned a_bytes, unsigned b_bytes,
-                                                  unsigned c_bytes, int group_m) {
-  constexpr int HT = 16384;
-  constexpr int STORES = 32;  // epilogue buffer stores per wave (2 x 2 quadrants x 4 x 2)
-  __shared__ __attribute__((aligned(1024))) char smem[8 * HT];
-
-  const int tiles_n = (N + 255) / 256;
-  const int tiles_m = (M + 255) / 256;
-  const int nwg = tiles_m * tiles_n;
-  const int total = nwg * splits;
-  const int G = gridDim.x;
-  const int nk = max(1, (k_per_split + 63) / 64);  // K-tiles per item (uniform; tails read zeros)
-
-  auto decode = [&](int lin, int& m0, int& n0, int& kb, int& ke, int& split) {
-    split = lin / nwg;
-    const int wg = lin - split * nwg;
-    const int per_group = group_m * tiles_n;
-    const int gid = wg / per_group;
-    const int first_m = gid * group_m;
-    const int gsz = min(tiles_m - first_m, group_m);
-    const int r = wg - gid * per_group;
-    m0 = (first_m + r % gsz) * 256;
-    n0 = (r / gsz) * 256;
-    kb = split * k_per_split;
-    ke = min(K, kb + k_per_split);
-  };
-
-  int it = xcd_remap(blockIdx.x, G);
-  if (it >= total) return;
-  const int wave = threadIdx.x >> 6;
-  const int wr = wave >> 2, wc = wave & 3;
-  const int l = lane_id();
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)a_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (int)b_bytes, 0x00020000);
-
-  int m0, n0, kb, ke, split;
-  decode(it, m0, n0, kb, ke, split);
-  int m0n = 0, n0n = 0, kbn = 0, ken = 0, splitn = 0;
-  bool has_next = it + G < total;
-  if (has_next) decode(it + G, m0n, n0n, kbn, ken, splitn);
-
-  // Half-tile h of the stream, counted from the current item's first K-tile; h >= 4 nk
-  // belongs to the next item (nk >= 3: at most one item ahead).  The stream is continuous
-  // across items: `hbase` = stream index of the current item's first half-tile, slot =
-  // (hbase + h) & 7.
-  int hbase = 0;
-  auto issue_half = [&](int h) {
-    const int j = h & 3;
-    char* dst = smem + ((hbase + h) & 7) * HT;
-    int t = h >> 2, mm = m0, nn = n0, kk = kb, ee = ke;
-    if (t >= nk) {
-      t -= nk;
-      mm = m0n; nn = n0n; kk = kbn;
-      ee = has_next ? ken : 0;  // no next item: every offset out of range (zeros)
-    }
-    const int k0 = kk + t * 64;  // >= ee past the item's last K-tile: out of range
-    if (j == 0 || j == 3) {
-      const int r0 = mm + (j == 3 ? 128 : 0);
-      issue_piece<AK, 128, 8>(ra, dst, r0, k0, lda, ee, 0);
-      issue_piece<AK, 128, 8>(ra, dst, r0, k0, lda, ee, 1);
-    } else {
-      const int r0 = nn + (j == 2 ? 128 : 0);
-      issue_piece<BKM, 128, 8>(rb, dst, r0, k0, ldb, ee, 0);
-      issue_piece<BKM, 128, 8>(rb, dst, r0, k0, ldb, ee, 1);
-    }
-  };
-
-  f32x4 acc[2][2][4][2];
-  bf16x8 fa[2][4], fb0[2][2], fb1[2][2];
-
-  auto mfma_quad = [&](int qm, int qn, const bf16x8 (&fbq)[2][2]) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[qm][qn][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fbq[s][j], fa[s][i], acc[qm][qn][i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  auto sync = [&]() {
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-
-  // Prologue: half-tiles 0..5 in flight; 0 and 1 (phase 0's operands) landed.
-#pragma unroll
-  for (int h = 0; h < 6; ++h) issue_half(h);
-  wait_vmcnt<8>();
-  __builtin_amdgcn_s_barrier();
-  if (wr == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind
-
-  bool first = true;
-  const int g = l >> 4;
-  for (;;) {
-#pragma unroll
-    for (int a0 = 0; a0 < 2; ++a0)
-#pragma unroll
-      for (int a1 = 0; a1 < 2; ++a1)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[a0][a1][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-    for (int t = 0; t < nk; ++t) {
-      // The previous item's epilogue stores were issued after the DMAs the first K-tile's
-      // waits retire: count them as outstanding (in-order vmcnt) instead of draining them.
-      const bool after_stores = (t == 0 && !first);
-      const char* base = smem + ((hbase + 4 * t) & 4) * HT;
-      const int h = 4 * t;
-      // phase 0: quadrant (0, 0) <- A0, B0
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) fb0[s][j] = frag2<BKM, 128>(base + 1 * HT, wc * 32 + 16 * j, 32 * s);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[s][i] = frag2<AK, 128>(base, wr * 64 + 16 * i, 32 * s);
-      }
-      issue_half(h + 6);
-      if (after_stores) wait_vmcnt<8 + STORES>(); else wait_vmcnt<8>();
-      sync();
-      mfma_quad(0, 0, fb0);
-      sync();
-      // phase 1: quadrant (0, 1) <- A0 (registers), B1
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) fb1[s][j] = frag2<BKM, 128>(base + 2 * HT, wc * 32 + 16 * j, 32 * s);
-      issue_half(h + 7);
-      if (after_stores) wait_vmcnt<8 + STORES>(); else wait_vmcnt<8>();
-      sync();
-      mfma_quad(0, 1, fb1);
-      sync();
-      // phase 2: quadrant (1, 1) <- A1, B1 (registers)
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[s][i] = frag2<AK, 128>(base + 3 * HT, wr * 64 + 16 * i, 32 * s);
-      issue_half(h + 8);
-      if (after_stores) wait_vmcnt<10 + STORES>(); else wait_vmcnt<10>();
-      sync();
-      mfma_quad(1, 1, fb1);
-      sync();
-      // phase 3: quadrant (1, 0) <- A1, B0 (registers)
-      issue_half(h + 9);
-      if (after_stores) wait_vmcnt<8 + STORES>(); else wait_vmcnt<8>();
-      sync();
-      mfma_quad(1, 0, fb0);
-      sync();
-    }
-
-    // Epilogue: lane holds C[m = .. + (l&15)][n = .. + 4g + r]; every wave issues exactly
-    // STORES buffer stores, out-of-range lanes get an offset past num_records (dropped).
-    char* cbase = reinterpret_cast<char*>(C) + (OUT == 1 ? (long long)split * slab_stride * 4 : 0);
-    const __amdgpu_buffer_rsrc_t rc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)cbase, (short)0, (int)c_bytes, 0x00020000);
-#pragma unroll
-    for (int qn = 0; qn < 2; ++qn) {
-      f32x4 bv[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int n = n0 + qn * 128 + wc * 32 + 16 * j + 4 * g;
-        bv[j] = (OUT == 0 && bias && n < N) ? *reinterpret_cast<const f32x4*>(bias + n) : (f32x4){0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int qm = 0; qm < 2; ++qm)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = m0 + qm * 128 + wr * 64 + 16 * i + (l & 15);
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int n = n0 + qn * 128 + wc * 32 + 16 * j + 4 * g;
-            const bool ok = m < M && n < N;
-            const f32x4 v = acc[qm][qn][i][j] + bv[j];
-            if (OUT == 0) {
-              const unsigned off = ok ? (unsigned)(((long long)m * ldc + n) * 2) : kOOB;
-              bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), rc, off, 0, 0);
-            } else {
-              const unsigned off = ok ? (unsigned)(((long long)m * ldc + n) * 4) : kOOB;
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rc, off, 0, 0);
-            }
-          }
-        }
-    }
-    if (!has_next) break;
-    first = false;
-    hbase += 4 * nk;
-    it += G;
-    m0 = m0n; n0 = n0n; kb = kbn; ke = ken; split = splitn;
-    has_next = it + G < total;
-    if (has_next) decode(it + G, m0n, n0n, kbn, ken, splitn);
-  }
-  if (wr == 0) __builtin_amdgcn_s_barrier();  // match group 1's extra barrier
-  wait_vmcnt<0>();                            // drain the trailing (out-of-range) DMAs
-}
-
 }  // namespace dpfs
 
 using namespace dpfs;
@@ -1059,24 +832,6 @@ static bool launchp(int cfg, const void* A, const void* B, void* C, const float*
   return true;
 }
 
-// v6 launch (gemm8_k, 256x256 tiles, persistent): grid = min(items, CUs).  Returns false
-// where it does not apply (the caller then runs v3): other tile shapes, fewer than 3 K-tiles
-// per item (the half-tile stream runs up to 2.25 K-tiles ahead, at most one item), or
-// spans past the 32-bit buffer descriptors.
-template <bool AK, bool BKM, int OUT>
-static bool launch8(int cfg, const void* A, const void* B, void* C, const float* bias, int M, int N, int K, int lda,
-                    int ldb, int ldc, int splits, int kps, long long slab, unsigned ab, unsigned bb, hipStream_t s) {
-  if (cfg != 0 || (kps + 63) / 64 < 3) return false;
-  const long long cspan = M > 0 ? ((long long)(M - 1) * ldc + N) * (OUT == 1 ? 4 : 2) : 0;
-  if (cspan >= (1ll << 32) - 16) return false;
-  const long long items = (long long)tiles2(M, N, 256, 256) * splits;
-  if (items <= 0 || items >= (1ll << 31)) return false;
-  const int grid = (int)std::min<long long>(items, cu_count());
-  gemm8_k<AK, BKM, OUT><<<grid, 512, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, kps,
-                                             splits, slab, ab, bb, (unsigned)cspan, g_group_m);
-  return true;
-}
-
 static int g_force_cfg = -1;     // -1 auto, 0 = 256x256, 1 = 256x128 (tuning / A-B runs)
 static int g_force_splits = 0;   // 0 auto
 extern "C" void dpfs_gemm_force(int cfg, int splits) {
@@ -1108,7 +863,7 @@ static int bf16_splits(int M, int N, int K) {
   return v2_splits(M, N, K, pick_cfg(M, N, 1));
 }
 
-static int g_gemm_impl = 3;  // 4 = v6 8-phase (256x256 tiles, else v3), 3 = v3 persistent (default), 2 = v2, 1 = v1
+static int g_gemm_impl = 3;  // 3 = v3 persistent (default), 2 = v2 one tile per workgroup, 1 = v1
 extern "C" void dpfs_gemm_set_impl(int v) { g_gemm_impl = v; }
 
 static thread_local float* g_ws = nullptr;  // split-K workspace for bf16 outputs (set by host)
@@ -1135,11 +890,8 @@ static void bf16_gemm(const void* A, const void* B, void* C, const float* bias, 
   if (S > 1 && g_ws && g_ws_floats >= (long long)S * M * N) {
     int kps = (K + S - 1) / S;
     kps = ((kps + BKK - 1) / BKK) * BKK;
-    const int cfg = pick_cfg(M, N, S);
-    if (!(g_gemm_impl == 4 && launch8<true, BKM, 1>(cfg, A, B, g_ws, nullptr, M, N, K, lda, ldb, N, S, kps,
-                                                    (long long)M * N, ab, bb, s)) &&
-        (g_gemm_impl < 3 || !launchp<true, BKM, 1>(cfg, A, B, g_ws, nullptr, M, N, K, lda, ldb, N, S, kps,
-                                                   (long long)M * N, ab, bb, s)))
+    if (g_gemm_impl != 3 || !launchp<true, BKM, 1>(pick_cfg(M, N, S), A, B, g_ws, nullptr, M, N, K, lda, ldb, N, S,
+                                                    kps, (long long)M * N, ab, bb, s))
       launch2<true, BKM, 1>(pick_cfg(M, N, S), A, B, g_ws, nullptr, M, N, K, lda, ldb, N, S, kps, (long long)M * N, ab,
                             bb, s);
     long long g = ((long long)M * N / 4 + 255) / 256;
@@ -1148,10 +900,7 @@ static void bf16_gemm(const void* A, const void* B, void* C, const float* bias, 
     if (rope.cols > 0) dpfs_rope_after_gemm(C, rope, M, ldc, s);
     return;
   }
-  if (g_gemm_impl == 4 && rope.cols == 0 &&
-      launch8<true, BKM, 0>(pick_cfg(M, N, 1), A, B, C, bias, M, N, K, lda, ldb, ldc, 1, K, 0, ab, bb, s))
-    return;
-  if (g_gemm_impl >= 3 && launchp<true, BKM, 0>(pick_cfg(M, N, 1), A, B, C, bias, M, N, K, lda, ldb, ldc, 1, K, 0, ab,
+  if (g_gemm_impl == 3 && launchp<true, BKM, 0>(pick_cfg(M, N, 1), A, B, C, bias, M, N, K, lda, ldb, ldc, 1, K, 0, ab,
                                                 bb, s, rope))
     return;
   launch2<true, BKM, 0>(pick_cfg(M, N, 1), A, B, C, bias, M, N, K, lda, ldb, ldc, 1, K, 0, ab, bb, s, rope);
@@ -1285,12 +1034,9 @@ extern "C" void dpfs_gemm_tn(const void* A, const void* B, float* C, float* ws, 
     gemm_k<false, false, 1><<<dim3(tiles_of(M, N), S), 256, 0, s>>>((const bf16*)A, (const bf16*)B, dst, nullptr, M,
                                                                    N, K, lda, ldb, N, direct ? K : kps,
                                                                    direct ? 0 : n);
-  } else if (!(g_gemm_impl == 4 &&
-               launch8<false, false, 1>(cfg, A, B, dst, nullptr, M, N, K, lda, ldb, N, S, direct ? K : kps,
-                                        direct ? 0 : n, span_bytes(K, lda, M), span_bytes(K, ldb, N), s)) &&
-             (g_gemm_impl < 3 ||
-              !launchp<false, false, 1>(cfg, A, B, dst, nullptr, M, N, K, lda, ldb, N, S, direct ? K : kps,
-                                        direct ? 0 : n, span_bytes(K, lda, M), span_bytes(K, ldb, N), s))) {
+  } else if (g_gemm_impl != 3 ||
+             !launchp<false, false, 1>(cfg, A, B, dst, nullptr, M, N, K, lda, ldb, N, S, direct ? K : kps,
+                                       direct ? 0 : n, span_bytes(K, lda, M), span_bytes(K, ldb, N), s)) {
     launch2<false, false, 1>(cfg, A, B, dst, nullptr, M, N, K, lda, ldb, N, S, direct ? K : kps,
                              direct ? 0 : n, span_bytes(K, lda, M), span_bytes(K, ldb, N), s);
   }
