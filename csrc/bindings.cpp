@@ -27,6 +27,9 @@ void dpfs_gemm_v2_sched(int);
 void dpfs_gemm_set_workspace(float*, long long);
 long long dpfs_gemm_bf16_ws(int, int, int);
 void dpfs_gemm_tn(const void*, const void*, float*, float*, int, int, int, int, int, int, hipStream_t);
+int dpfs_gemm_tn2(const void*, const void*, const void*, const void*, float*, float*, int, int, int, int, int, int, int,
+                  int, int, hipStream_t);
+long long dpfs_gemm_tn2_ws(int, int, int, int);
 void dpfs_rmsnorm_fwd(int, const void*, const float*, void*, float*, int, int, float, hipStream_t);
 void dpfs_layernorm_fwd(int, const void*, const float*, const float*, void*, float*, float*, int, int, float,
                         hipStream_t);
@@ -246,6 +249,40 @@ torch::Tensor gemm_tn(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
   if (wsn > 0) ws = torch::empty({(int64_t)wsn}, c.options());
   dpfs_gemm_tn(a.data_ptr(), b.data_ptr(), c.data_ptr<float>(), ws.defined() ? ws.data_ptr<float>() : nullptr, (int)M,
                (int)N, (int)K, (int)a.stride(0), (int)b.stride(0), accumulate ? 1 : 0, stream());
+  return c;
+}
+
+// c[M,N] fp32 (+)= a0[K0,M]^T b0[K0,N] + a1[K1,M]^T b1[K1,N] in one split-K launch; None
+// (nothing written) when the K-split plan does not fit the two buffers.
+c10::optional<torch::Tensor> gemm_tn2(torch::Tensor a0, torch::Tensor b0, torch::Tensor a1, torch::Tensor b1,
+                                      c10::optional<torch::Tensor> out, bool accumulate) {
+  for (auto* t : {&a0, &b0, &a1, &b1}) {
+    check_rowmajor(*t, "gemm_tn2 operand");
+    TORCH_CHECK(t->scalar_type() == torch::kBFloat16 && t->stride(0) % 8 == 0, "gemm_tn2: bf16, row stride % 8");
+  }
+  const int64_t K0 = a0.size(0), K1 = a1.size(0), M = a0.size(1), N = b0.size(1);
+  TORCH_CHECK(b0.size(0) == K0 && b1.size(0) == K1 && a1.size(1) == M && b1.size(1) == N, "gemm_tn2: shape mismatch");
+  TORCH_CHECK(M % 8 == 0 && N % 8 == 0, "gemm_tn2: M and N must be multiples of 8");
+  TORCH_CHECK(a1.device() == a0.device() && b0.device() == a0.device() && b1.device() == a0.device(),
+              "gemm_tn2: one device");
+  const at::DeviceGuard g(a0.device());
+  torch::Tensor c;
+  if (out.has_value() && out->defined()) {
+    c = *out;
+    TORCH_CHECK(c.scalar_type() == torch::kFloat32 && c.is_contiguous() && c.size(0) == M && c.size(1) == N,
+                "gemm_tn2: out must be contiguous fp32 [M,N]");
+  } else {
+    c = torch::empty({M, N}, a0.options().dtype(torch::kFloat32));
+    accumulate = false;
+  }
+  if (M == 0 || N == 0 || K0 == 0 || K1 == 0) return c10::nullopt;
+  const long long wsn = dpfs_gemm_tn2_ws((int)M, (int)N, (int)K0, (int)K1);
+  if (wsn <= 0) return c10::nullopt;
+  auto ws = torch::empty({wsn}, c.options());
+  const int ok = dpfs_gemm_tn2(a0.data_ptr(), b0.data_ptr(), a1.data_ptr(), b1.data_ptr(), c.data_ptr<float>(),
+                               ws.data_ptr<float>(), (int)M, (int)N, (int)K0, (int)K1, (int)a0.stride(0),
+                               (int)b0.stride(0), (int)a1.stride(0), (int)b1.stride(0), accumulate ? 1 : 0, stream());
+  if (!ok) return c10::nullopt;
   return c;
 }
 
@@ -1009,6 +1046,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "force the v2 tile config (-1 auto, 0 = 256x256, 1 = 256x128) and K-splits (0 auto)");
   m.def("gemm_v2_sched", [](int v) { dpfs_gemm_v2_sched(v); }, "v2 256x256 schedule (-1 per-layout default, 0..4 see gemm2_k SCHED)");
   m.def("gemm_set_impl", [](int v) { dpfs_gemm_set_impl(v); }, "1 = v1 (128x128 register-staged), 2 = v2 (LDS-DMA, one tile per workgroup), 3 = v3 (persistent v2, default)");
+  m.def("gemm_tn2", &gemm_tn2, "fp32 c (+)= a0^T b0 + a1^T b1 (reduction dim over two buffers), one split-K launch; None if the plan does not fit",
+        py::arg("a0"), py::arg("b0"), py::arg("a1"), py::arg("b1"), py::arg("out") = py::none(),
+        py::arg("accumulate") = false);
   m.def("gemm_tn", &gemm_tn, py::arg("a"), py::arg("b"), py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("bias_grad", &bias_grad);
   m.def("add_bias_", &add_bias_);

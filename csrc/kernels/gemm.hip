@@ -508,6 +508,18 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 2 : 1) void gemm2_k(const bf16
   }
 }
 
+// Second operand pair of a TN GEMM whose reduction dim is split over two buffers (the two
+// ping-pong chunks' activations of a chunked training step): k < k_switch reads (A, B),
+// k >= k_switch reads (A2, B2) at k - k_switch.  K-splits never straddle k_switch (the
+// launcher checks it), so each work item reads one pair.  k_switch = INT_MAX: one pair.
+struct Dual {
+  const bf16* A2;
+  const bf16* B2;
+  int k_switch, lda2, ldb2;
+  unsigned a2_bytes, b2_bytes;
+};
+constexpr Dual kNoDual = {nullptr, nullptr, 0x7fffffff, 0, 0, 0u, 0u};
+
 // ============================================================= GEMM v3 (persistent) ====
 // gemm2_k's 256-wide tile, made persistent: one workgroup per CU walks the (split, tile)
 // items i = r, r + G, r + 2G, ... (r = XCD-remapped block id, G = grid), so the per-tile
@@ -529,7 +541,7 @@ __global__ __launch_bounds__(512, 1) void gemmp_k(const bf16* __restrict__ A, co
                                                   void* __restrict__ C, const float* __restrict__ bias, int M, int N,
                                                   int K, int lda, int ldb, int ldc, int k_per_split, int splits,
                                                   long long slab_stride, unsigned a_bytes, unsigned b_bytes,
-                                                  unsigned c_bytes, RopeArgs rope, int group_m) {
+                                                  unsigned c_bytes, RopeArgs rope, int group_m, Dual dual) {
   constexpr int NWV = 8;
   constexpr int WAVES_N = NWV / WAVES_M;
   constexpr int WM = BM_ / WAVES_M, WN = BN_ / WAVES_N;
@@ -551,8 +563,14 @@ __global__ __launch_bounds__(512, 1) void gemmp_k(const bf16* __restrict__ A, co
   const int l = lane_id();
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (int)b_bytes, 0x00020000);
+  const bool dual_on = dual.A2 != nullptr;
+  const __amdgpu_buffer_rsrc_t ra2 =
+      dual_on ? __builtin_amdgcn_make_buffer_rsrc((void*)dual.A2, (short)0, (int)dual.a2_bytes, 0x00020000) : ra;
+  const __amdgpu_buffer_rsrc_t rb2 =
+      dual_on ? __builtin_amdgcn_make_buffer_rsrc((void*)dual.B2, (short)0, (int)dual.b2_bytes, 0x00020000) : rb;
+  const int lda2 = dual_on ? dual.lda2 : lda, ldb2 = dual_on ? dual.ldb2 : ldb;
 
-  auto decode = [&](int lin, int& m0, int& n0, int& kb, int& ke, int& split) {
+  auto decode = [&](int lin, int& m0, int& n0, int& kb, int& ke, int& split, int& sel) {
     split = lin / nwg;
     const int wg = lin - split * nwg;
     const int per_group = group_m * tiles_n;
@@ -564,20 +582,26 @@ __global__ __launch_bounds__(512, 1) void gemmp_k(const bf16* __restrict__ A, co
     n0 = (r / gsz) * BN_;
     kb = split * k_per_split;
     ke = min(K, kb + k_per_split);
+    sel = 0;
+    if (kb >= dual.k_switch) {
+      sel = 1;
+      kb -= dual.k_switch;
+      ke -= dual.k_switch;
+    }
   };
 
   int it = xcd_remap(blockIdx.x, G);
   if (it >= total) return;
-  int m0, n0, kb, ke, split;
-  decode(it, m0, n0, kb, ke, split);
-  issue_tile<AK, BM_, NWV>(ra, smem, m0, kb, lda, ke);
-  issue_tile<BKM, BN_, NWV>(rb, smem + A_BYTES, n0, kb, ldb, ke);
+  int m0, n0, kb, ke, split, sel;
+  decode(it, m0, n0, kb, ke, split, sel);
+  issue_tile<AK, BM_, NWV>(sel ? ra2 : ra, smem, m0, kb, sel ? lda2 : lda, ke);
+  issue_tile<BKM, BN_, NWV>(sel ? rb2 : rb, smem + A_BYTES, n0, kb, sel ? ldb2 : ldb, ke);
   int cur = 0;
   bool first = true;
   for (; it < total; it += G) {
     const bool has_next = it + G < total;
-    int m0n = 0, n0n = 0, kbn = 0, ken = 0, splitn = 0;
-    if (has_next) decode(it + G, m0n, n0n, kbn, ken, splitn);
+    int m0n = 0, n0n = 0, kbn = 0, ken = 0, splitn = 0, seln = 0;
+    if (has_next) decode(it + G, m0n, n0n, kbn, ken, splitn, seln);
     const int nk = max(1, (ke - kb + 63) / 64);   // an empty K-split runs one all-zero step
 
     f32x4 acc[TM][TN];
@@ -596,12 +620,13 @@ __global__ __launch_bounds__(512, 1) void gemmp_k(const bf16* __restrict__ A, co
       const bool more = in_item || has_next;
       const int pm0 = in_item ? m0 : m0n, pn0 = in_item ? n0 : n0n;
       const int pk = in_item ? kb + (t + 1) * 64 : kbn, pke = in_item ? ke : ken;
+      const int psel = in_item ? sel : seln;
       char* nst = smem + (cur ^ 1) * STAGE;
       const char* la = smem + cur * STAGE;
       const char* lb = la + A_BYTES;
       auto piece = [&](int q) {
-        if (q < PA) issue_piece<AK, BM_, NWV>(ra, nst, pm0, pk, lda, pke, q);
-        else issue_piece<BKM, BN_, NWV>(rb, nst + A_BYTES, pn0, pk, ldb, pke, q - PA);
+        if (q < PA) issue_piece<AK, BM_, NWV>(psel ? ra2 : ra, nst, pm0, pk, psel ? lda2 : lda, pke, q);
+        else issue_piece<BKM, BN_, NWV>(psel ? rb2 : rb, nst + A_BYTES, pn0, pk, psel ? ldb2 : ldb, pke, q - PA);
       };
       if constexpr (SCHED == 4) {
         bf16x8 fa[2][TM], fb[2][TN];
@@ -710,6 +735,7 @@ __global__ __launch_bounds__(512, 1) void gemmp_k(const bf16* __restrict__ A, co
     kb = kbn;
     ke = ken;
     split = splitn;
+    sel = seln;
   }
 }
 
@@ -808,7 +834,7 @@ static int cu_count() {
 template <bool AK, bool BKM, int OUT>
 static bool launchp(int cfg, const void* A, const void* B, void* C, const float* bias, int M, int N, int K, int lda,
                     int ldb, int ldc, int splits, int kps, long long slab, unsigned ab, unsigned bb, hipStream_t s,
-                    RopeArgs rope = RopeArgs{nullptr, nullptr, 0}) {
+                    RopeArgs rope = RopeArgs{nullptr, nullptr, 0}, Dual dual = kNoDual) {
   const long long cspan = M > 0 ? ((long long)(M - 1) * ldc + N) * (OUT == 1 ? 4 : 2) : 0;
   if (cspan >= (1ll << 32) - 16) return false;
   const int bm = 256, bn = cfg == 0 ? 256 : 128;
@@ -820,7 +846,7 @@ static bool launchp(int cfg, const void* A, const void* B, void* C, const float*
 #define DPFS_GEMMP(BN_, WM_, SC_)                                                                                    \
   gemmp_k<256, BN_, WM_, AK, BKM, OUT, SC_><<<grid, 512, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K,  \
                                                                 lda, ldb, ldc, kps, splits, slab, ab, bb, cb, rope, \
-                                                                g_group_m)
+                                                                g_group_m, dual)
   if (cfg == 0) {
     if (sched == 4) DPFS_GEMMP(256, 2, 4);
     else DPFS_GEMMP(256, 2, 2);
@@ -1044,4 +1070,63 @@ extern "C" void dpfs_gemm_tn(const void* A, const void* B, float* C, float* ws, 
   long long g = (n / 4 + 255) / 256;
   if (g > 4096) g = 4096;
   splitk_reduce_k<<<(int)g, 256, 0, s>>>(ws, C, n, S, accumulate);
+}
+
+// TN with the reduction dim split over two buffer pairs (a chunked step's two ping-pong
+// chunks): C[M,N] fp32 (+)= A0[K0,M]^T B0[K0,N] + A1[K1,M]^T B1[K1,N] as ONE persistent
+// split-K launch and ONE slab reduction, planned as dpfs_gemm_tn over K0 + K1 (so the same
+// tile / split counts as one tall GEMM; two separate calls pay two reductions and two
+// under-filled grids).  ws: dpfs_gemm_tn2_ws floats.  Returns 0 (nothing launched) when no
+// K-split length divides K0 (a split must not straddle the two buffers).
+static int tn2_plan(int M, int N, int K0, int K1, int* cfg_out, int* kps_out) {
+  if (g_gemm_impl != 3 || K0 <= 0 || K1 <= 0) return 0;
+  const int K = K0 + K1;
+  int cfg;
+  (void)tn_plan(M, N, K, &cfg);
+  // K-split length: a divisor K0 / j (multiple of 64) so no split straddles the buffers,
+  // chosen with the makespan model of tn_small_plan over the whole K0 + K1.
+  const long long tiles = cfg == 0 ? tiles2(M, N, 256, 256) : tiles2(M, N, 256, 128);
+  const double step = cfg == 0 ? 1.95 : 1.5;
+  int kps = 0, S = 0;
+  double best = 1e300;
+  for (int j = 1; j <= 64; ++j) {
+    if (K0 % j) continue;
+    const int kp = K0 / j;
+    if (kp % BKK || kp < 512) continue;
+    const int Sj = (K + kp - 1) / kp;
+    if (Sj < 2 || Sj > 64) continue;
+    const double t = (double)((tiles * Sj + 255) / 256) * (kp / 64) * step + (double)Sj * M * N * 8.0 / 4.0e6;
+    if (t < best * 0.97) {
+      best = t;
+      kps = kp;
+      S = Sj;
+    }
+  }
+  *cfg_out = cfg;
+  *kps_out = kps;
+  return S;
+}
+
+extern "C" long long dpfs_gemm_tn2_ws(int M, int N, int K0, int K1) {
+  int cfg, kps;
+  const int S = tn2_plan(M, N, K0, K1, &cfg, &kps);
+  return (long long)S * M * N;
+}
+
+extern "C" int dpfs_gemm_tn2(const void* A0, const void* B0, const void* A1, const void* B1, float* C, float* ws,
+                             int M, int N, int K0, int K1, int lda0, int ldb0, int lda1, int ldb1, int accumulate,
+                             hipStream_t s) {
+  int cfg, kps;
+  const int S = tn2_plan(M, N, K0, K1, &cfg, &kps);
+  if (S == 0) return 0;
+  const int K = K0 + K1;
+  const long long n = (long long)M * N;
+  const Dual d = {(const bf16*)A1, (const bf16*)B1, K0, lda1, ldb1, span_bytes(K1, lda1, M), span_bytes(K1, ldb1, N)};
+  if (!launchp<false, false, 1>(cfg, A0, B0, ws, nullptr, M, N, K, lda0, ldb0, N, S, kps, n, span_bytes(K0, lda0, M),
+                                span_bytes(K0, ldb0, N), s, RopeArgs{nullptr, nullptr, 0}, d))
+    return 0;
+  long long g = (n / 4 + 255) / 256;
+  if (g > 4096) g = 4096;
+  splitk_reduce_k<<<(int)g, 256, 0, s>>>(ws, C, n, S, accumulate);
+  return 1;
 }

@@ -262,6 +262,24 @@ class DecoderTrainFn(torch.autograd.Function):
             else:
                 GS.gemm_tn(k, dy, x, acc, True)
 
+        def tn_chunks(key_dict, key, pairs):
+            """Weight gradient summed over the chunks ((dy, x) per chunk), issued after the
+            last chunk's data-gradient GEMM of the phase: chunks go two at a time through
+            GS.gemm_tn_pair (one split-K launch over both chunks' rows, one reduction)."""
+            i = 0
+            while i < len(pairs):
+                if i + 1 < len(pairs):
+                    (a0, b0), (a1, b1) = pairs[i], pairs[i + 1]
+                    if key_dict.get(key) is None:
+                        key_dict[key] = GS.gemm_tn_pair(k, a0, b0, a1, b1)
+                    else:
+                        GS.gemm_tn_pair(k, a0, b0, a1, b1, key_dict[key], True)
+                    i += 2
+                else:
+                    tn(key_dict, key, *pairs[i])
+                    i += 1
+            pairs.clear()
+
         def bias_acc(key_dict, key, dy, present):
             if present is None:
                 return
@@ -337,6 +355,7 @@ class DecoderTrainFn(torch.autograd.Function):
             if ctx.recompute:
                 rebuild(L, li)
             # b2: down / SwiGLU / gate|up grads -> AR(dh2)
+            wd_p, wgu_p = [], []
             for ci, s in enumerate(st):
                 if s["dpend"] is not None:     # finish the upper layer: wait, norm1 bwd, residual
                     _finish_norm1(k, s, layers[li + 1], gl[li + 1], li + 1, (G, L.bd))
@@ -345,18 +364,21 @@ class DecoderTrainFn(torch.autograd.Function):
                 if not s.pop("bd_done", False):
                     bias_acc(G, "bd", gq, L.bd)
                 ds = GS.gemm_nn(k, gq, W(L.wd))
-                tn(G, "wd", gq, a["sw"])
+                wd_p.append((gq, a["sw"]))
                 dbgu = ds.new_empty(a["gu"].size(1), dtype=torch.float32) if L.bgu is not None else None
                 dgu = k.swiglu_bwd(ds, a["gu"], dbgu)     # + gate|up bias grad in the same pass
                 dh2 = GS.gemm_nn(k, dgu, W(L.wgu), out=_slot(ci, dgu.size(0), d, dt))
                 s["bh"], s["dpend"] = _ar(dh2), dh2
-                tn(G, "wgu", dgu, a["h2"])
+                wgu_p.append((dgu, a["h2"]))
                 if dbgu is not None:
                     G["bgu"] = _addg(G.get("bgu"), dbgu)
                 del a["sw"], a["gu"]
+            tn_chunks(G, "wd", wd_p)        # under the chunks' all-reduces
+            tn_chunks(G, "wgu", wgu_p)
             if li + 1 < nL:
                 dp_reduce(gl[li + 1])           # layer li+1 is complete (its norm1 grad just landed)
             # b1: wait, norm2 bwd, Wo / attention / QKV grads -> AR(dh)
+            wo_p, wqkv_p = [], []
             for ci, s in enumerate(st):
                 a = s["layers"][li]
                 _wait(s["bh"])
@@ -368,7 +390,7 @@ class DecoderTrainFn(torch.autograd.Function):
                 if dbo is not None:
                     G["bo"] = _addg(G.get("bo"), dbo)
                 do = GS.gemm_nn(k, g2, W(L.wo))
-                tn(G, "wo", g2, a["o"].view(g2.size(0), -1))
+                wo_p.append((g2, a["o"].view(g2.size(0), -1)))
                 Bc = s["B"]
                 q, kk, v = _split(a["qkv"], Bc, T, L.h, L.hd)
                 dqkv = torch.empty_like(a["qkv"])
@@ -377,11 +399,13 @@ class DecoderTrainFn(torch.autograd.Function):
                            dq, dk, dv, s["pos"], tab)   # inverse RoPE fused into the dq/dk stores
                 dh = GS.gemm_nn(k, dqkv, W(L.wqkv), out=_slot(ci, dqkv.size(0), d, dt))
                 s["bh"], s["dpend"] = _ar(dh), dh
-                tn(G, "wqkv", dqkv, a["h1"])
+                wqkv_p.append((dqkv, a["h1"]))
                 bias_acc(G, "bqkv", dqkv, L.bqkv)
                 s["g"] = g2
                 for key in ("x2", "r2", "h2", "qkv", "o", "lse"):
                     a.pop(key, None)
+            tn_chunks(G, "wo", wo_p)
+            tn_chunks(G, "wqkv", wqkv_p)
         for s in st:
             _finish_norm1(k, s, layers[0], gl[0], 0)
             dwe = k.embedding_bwd(s["g"], s["ids"], model.embedding.weight.size(0), model.embedding.vocab_st_idx)

@@ -179,6 +179,24 @@ class DecoderTrainFnSP(torch.autograd.Function):
             else:
                 GS.gemm_tn(k, dy, x, d[key], True)
 
+        def tn_chunks(d, key, pairs):
+            """Weight gradient summed over the chunks ((dy, x) per chunk), issued after the
+            last chunk's data-gradient GEMM of the phase: chunks go two at a time through
+            GS.gemm_tn_pair (one split-K launch over both chunks' rows, one reduction)."""
+            i = 0
+            while i < len(pairs):
+                if i + 1 < len(pairs):
+                    (a0, b0), (a1, b1) = pairs[i], pairs[i + 1]
+                    if d.get(key) is None:
+                        d[key] = GS.gemm_tn_pair(k, a0, b0, a1, b1)
+                    else:
+                        GS.gemm_tn_pair(k, a0, b0, a1, b1, d[key], True)
+                    i += 2
+                else:
+                    tn(d, key, *pairs[i])
+                    i += 1
+            pairs.clear()
+
         pg = pm.pgm
         dp = pg.dp_size
         dp_pending = []
@@ -252,20 +270,23 @@ class DecoderTrainFnSP(torch.autograd.Function):
             L, G = layers[li], gl[li]
             if ctx.recompute:
                 rebuild(L, li)
+            wd_p, wgu_p = [], []
             for ci, s in enumerate(st):    # B4: down / SwiGLU / gate|up grads -> reduce-scatter
                 _wait(s["h"])
                 a, gq = s["layers"][li], s["gfull"]
                 # (bd's grad, partial over my rows and summed over TP by TrainStep, came out of
                 # the norm backward above this layer)
                 ds = GS.gemm_nn(k, gq, W(L.wd))
-                tn(G, "wd", gq, a["sw"])
+                wd_p.append((gq, a["sw"]))
                 dbgu = ds.new_empty(a["gu"].size(1), dtype=torch.float32) if L.bgu is not None else None
                 dgu = k.swiglu_bwd(ds, a["gu"], dbgu)
                 s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dgu, W(L.wgu), out=_slot(ci, dgu.size(0), d, dt)), n)
-                tn(G, "wgu", dgu, a["h2"])
+                wgu_p.append((dgu, a["h2"]))
                 if dbgu is not None:
                     G["bgu"] = _addg(G.get("bgu"), dbgu)
                 del a["sw"], a["gu"], a["h2"], s["gfull"]
+            tn_chunks(G, "wd", wd_p)       # under the chunks' reduce-scatters
+            tn_chunks(G, "wgu", wgu_p)
             for s in st:    # B3: norm2 backward (+ residual grad) on my rows -> all-gather
                 _wait(s["h"])
                 a = s["layers"][li]
@@ -273,11 +294,12 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 G["s2"] = _addg(G.get("s2"), ds2)
                 s["gfull"], s["h"] = _ag(s["g"], n)
                 del a["x2"], a["r2"], s["dpend"]
+            wo_p, wqkv_p = [], []
             for ci, s in enumerate(st):    # B2: Wo / attention / QKV grads -> reduce-scatter
                 _wait(s["h"])
                 a, g2 = s["layers"][li], s["gfull"]
                 do = GS.gemm_nn(k, g2, W(L.wo))
-                tn(G, "wo", g2, a["o"].view(g2.size(0), -1))
+                wo_p.append((g2, a["o"].view(g2.size(0), -1)))
                 Bc = s["B"]
                 q, kk, v = _split(a["qkv"], Bc, T, L.h, L.hd)
                 dqkv = torch.empty_like(a["qkv"])
@@ -285,12 +307,14 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 k.attn_bwd(do.view(Bc, T, L.h, L.hd), q, kk, v, a["o"], a["lse"], 1.0 / math.sqrt(L.hd), True,
                            dq, dk, dv, s["pos"], tab)
                 s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dqkv, W(L.wqkv), out=_slot(ci, dqkv.size(0), d, dt)), n)
-                tn(G, "wqkv", dqkv, a["h1"])
+                wqkv_p.append((dqkv, a["h1"]))
                 if L.bqkv is not None:
                     G["bqkv"] = _addg(G.get("bqkv"), k.bias_grad(dqkv))
                 for key in ("qkv", "o", "lse", "h1"):
                     a.pop(key, None)
                 del s["gfull"]
+            tn_chunks(G, "wo", wo_p)
+            tn_chunks(G, "wqkv", wqkv_p)
             for s in st:    # B1: norm1 backward (+ residual grad) on my rows -> all-gather
                 _wait(s["h"])
                 a = s["layers"][li]

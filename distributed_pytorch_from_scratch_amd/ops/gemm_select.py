@@ -333,3 +333,36 @@ def gemm_tn(k, a: torch.Tensor, b: torch.Tensor, out=None, accumulate: bool = Fa
     if c.startswith("lt") and not lt_ok:
         c = "ours"
     return run(c, out, accumulate)
+
+
+def gemm_tn_pair(k, a0: torch.Tensor, b0: torch.Tensor, a1: torch.Tensor, b1: torch.Tensor, out=None,
+                 accumulate: bool = False) -> torch.Tensor:
+    """fp32 c (+)= a0^T b0 + a1^T b1 -- a weight gradient over the two ping-pong chunks of a
+    chunked step.  Candidates, timed per shape like the others: ``pair`` = ONE split-K launch
+    whose K-splits read either chunk's buffers and ONE slab reduction (``gemm_tn2``: the plan
+    of a single tall GEMM), ``split`` = two :func:`gemm_tn` calls (two under-filled grids,
+    two reductions).  ``DPFS_TN_PAIR=0`` always splits (A/B runs)."""
+    def split(dst, acc):
+        c = gemm_tn(k, a0, b0, dst, acc)
+        return gemm_tn(k, a1, b1, c, True)
+
+    if k is reference or not a0.is_cuda or not hasattr(k, "gemm_tn2") or mode() not in ("auto", "ours") \
+            or os.environ.get("DPFS_TN_PAIR", "1") == "0":
+        return split(out, accumulate)
+    M, N = a0.shape[1], b0.shape[1]
+    if not _aligned(M, N) or min(a0.shape[0], a1.shape[0]) < _MIN_ROWS:
+        return split(out, accumulate)
+    key = ("tn2", M, N, a0.shape[0], a1.shape[0], bool(accumulate), a0.device.index)
+    c = _choice.get(key)
+    if c is None:
+        scratch = torch.zeros(M, N, device=a0.device, dtype=torch.float32)
+        if k.gemm_tn2(a0, b0, a1, b1, scratch, accumulate) is None:    # the K-split plan does not fit
+            c = _choice[key] = "split"
+        else:
+            c = _pick(key, {"split": lambda: split(scratch, accumulate),
+                            "pair": lambda: k.gemm_tn2(a0, b0, a1, b1, scratch, accumulate)})
+    if c == "pair":
+        r = k.gemm_tn2(a0, b0, a1, b1, out, accumulate)
+        if r is not None:
+            return r
+    return split(out, accumulate)

@@ -60,6 +60,14 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None
     return out
 
 
+def gemm_tn2(a0: torch.Tensor, b0: torch.Tensor, a1: torch.Tensor, b1: torch.Tensor,
+             out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+    """c[M,N] (fp32) = a0^T b0 + a1^T b1: a TN GEMM whose reduction dim is split over two
+    buffers (+= into ``out`` if ``accumulate``)."""
+    c = gemm_tn(a0, b0, out, accumulate)
+    return gemm_tn(a1, b1, c, True)
+
+
 def add_bias_(y: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
     """y[M,N] += bias[N] in place (fp32 add, rounded to y.dtype); returns y."""
     y.copy_((y.float() + bias.float()).to(y.dtype))

@@ -453,6 +453,22 @@ def test_ce_bwd_fused_bias_grad(C, M, V, valid, start):
     assert _rel(out, rout) < 1e-2 and _rel(db, rdb) < 1e-3
 
 
+@pytest.mark.parametrize("M,N,K0,K1", [(768, 768, 8192, 8192), (1000, 776, 4096, 2048), (2304, 768, 32768, 32768)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_gemm_tn2_two_buffer_reduction(C, M, N, K0, K1, accumulate):
+    """One split-K launch over a reduction dim split across two buffers (the chunked engines'
+    weight gradients) == a0^T b0 + a1^T b1 in fp32 (the split length divides K0)."""
+    torch.manual_seed(25)
+    a0, a1 = torch.randn(K0, M, device=DEV).bfloat16(), torch.randn(K1, M, device=DEV).bfloat16()
+    b0, b1 = torch.randn(K0, N, device=DEV).bfloat16(), torch.randn(K1, N, device=DEV).bfloat16()
+    ref = a0.float().t() @ b0.float() + a1.float().t() @ b1.float()
+    out = torch.randn(M, N, device=DEV)
+    want = out + ref if accumulate else ref
+    r = C.gemm_tn2(a0, b0, a1, b1, out, accumulate)
+    assert r is not None and r.data_ptr() == out.data_ptr()
+    assert _rel(out, want) < 1e-5
+
+
 @pytest.mark.parametrize("impl,cfg,splits,sched", [(2, -1, 0, -1), (2, 0, 1, 0), (2, 0, 1, 1), (2, 0, 1, 2),
                                                   (2, 0, 1, 3), (2, 0, 1, 4), (2, 1, 1, -1), (2, 0, 3, -1),
                                                   (2, 1, 2, -1), (2, 0, 7, 4), (1, -1, 0, -1),
