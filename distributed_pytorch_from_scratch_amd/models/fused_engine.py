@@ -304,6 +304,7 @@ class DecoderTrainFn(torch.autograd.Function):
             dp_pending.append((dist.all_reduce(flat, group=pg.dp_group, async_op=True), flat, d, keys))
 
         # ---- head: CE backward in place over the logits, lm_head dgrad -> async AR
+        lm_p = []
         for ci, s in enumerate(st):
             gs = s["valid"].float() * gscale_all
             dl = s["logits"]
@@ -312,10 +313,11 @@ class DecoderTrainFn(torch.autograd.Function):
             dh = GS.gemm_nn(k, dl, W(head.weight), out=_slot(ci, dl.size(0), d, dt))
             s["bh"] = _ar(dh)
             s["dpend"] = dh
-            tn(g, "lm_w", dl, s["hf"])
+            lm_p.append((dl, s["hf"]))
             if db is not None:
                 g["lm_b"] = _addg(g["lm_b"], db)
             del s["logits"]
+        tn_chunks(g, "lm_w", lm_p)
         for s in st:
             _wait(s["bh"])
             Lt = layers[-1]

@@ -211,16 +211,18 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 dp_pending.append((dist.all_reduce(flat, group=pg.dp_group, async_op=True), flat, d, keys))
 
         d = model.args.attn_dim
+        lm_p = []
         for ci, s in enumerate(st):    # CE backward in place, lm_head dgrad -> reduce-scatter, lm_head wgrad
             gs = s["valid"].float() * gscale_all
             dl = s["logits"]
             db = dl.new_empty(dl.size(1), dtype=torch.float32) if head.bias is not None else None
             k.ce_bwd(dl, s["tgt"], s["ce_lse"], gs, vst, vvalid, dl, db)
             s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dl, W(head.weight), out=_slot(ci, dl.size(0), d, dt)), n)
-            tn(g, "lm_w", dl, s["hf"])
+            lm_p.append((dl, s["hf"]))
             if db is not None:
                 g["lm_b"] = _addg(g["lm_b"], db)
             del s["logits"], s["hf"]
+        tn_chunks(g, "lm_w", lm_p)
         def norm_bwd(dy, x, w, r, dres, bias_below, below_key):
             """RMSNorm backward on my rows (+ residual grad); the bias grad of the projection
             whose output feeds this residual (column sums of the result) from the same pass."""
