@@ -152,3 +152,31 @@ def _load_roundtrip(rank, world):
 def test_state_dict_roundtrip():
     res = run_distributed(_load_roundtrip, 2)
     assert res[0] == 0.0 and res[1] == 0.0
+
+
+def _grads_chunked(rank, world, cfg, sp, chunks):
+    from distributed_pytorch_from_scratch_amd.models import Transformer, ModelArgs
+    from distributed_pytorch_from_scratch_amd.utils.dist import set_seed
+    m = Transformer.from_args(ModelArgs(**cfg, vocab_pad_to=1, sequence_parallel=sp))
+    set_seed(0)
+    m.reset_parameters()
+    m.chunks = chunks
+    ids, pos, tgt = _batch(cfg["vocab_size"], 4, 16, seed=7)
+    loss = m.loss(ids, pos, tgt)
+    loss.backward()
+    if sp:
+        from distributed_pytorch_from_scratch_amd.parallel.grad_sync import allreduce_sequence_parallel_grads
+        allreduce_sequence_parallel_grads(m)
+    return loss.item(), {n: p.grad.clone() for n, p in m.named_parameters()}
+
+
+@pytest.mark.parametrize("sp", [False, True])
+def test_chunk_counts_give_same_grads(sp):
+    """The chunked engines sum each weight gradient over the ping-pong chunks two at a time
+    (ops.gemm_select.gemm_tn_pair) plus a leftover single chunk: 1, 2, 3 and 4 chunks of a
+    4-sequence batch give the same loss and gradients at TP 2."""
+    res = {c: run_distributed(_grads_chunked, 2, CFG, sp, c)[0] for c in (1, 2, 3, 4)}
+    for c in (2, 3, 4):
+        assert abs(res[c][0] - res[1][0]) < 1e-5
+        for n, g in res[1][1].items():
+            assert torch.allclose(res[c][1][n], g, atol=1e-5, rtol=1e-4), (c, n)
