@@ -207,9 +207,10 @@ __global__ __launch_bounds__(256) void colsum_stage_k(const T* __restrict__ x, f
 // hundred and N small (768 at GPT-2 width), so the stage-1 shape (32 column vectors per block)
 // gave only N/128 blocks of long serial row walks; here a block is 4 column vectors x 64 row
 // lanes (N/16 blocks, R/64 rows per lane), reduced through LDS in a fixed order.
+// Columns >= split go to out2[col - split] (two column sums reduced by one launch).
 template <bool VEC>   // VEC: N % 4 == 0, rows 16-B aligned
 __global__ __launch_bounds__(256) void colsum_rows_k(const float* __restrict__ part, float* __restrict__ out, int R,
-                                                     int N_) {
+                                                     int N_, float* __restrict__ out2, int split) {
   __shared__ float red[64][16];
   const int cv = threadIdx.x & 3, rl = threadIdx.x >> 2;
   const int c0 = (blockIdx.x * 4 + cv) * 4;
@@ -237,16 +238,19 @@ __global__ __launch_bounds__(256) void colsum_rows_k(const float* __restrict__ p
     if (col < N_) {
       float s = 0.f;
       for (int k = 0; k < 64; ++k) s += red[k][threadIdx.x];
-      out[col] = s;
+      if (col < split) out[col] = s;
+      else out2[col - split] = s;
     }
   }
 }
 
-static inline void colsum_rows(const float* part, float* out, int R, int N_, hipStream_t s) {
+static inline void colsum_rows(const float* part, float* out, int R, int N_, hipStream_t s, float* out2 = nullptr,
+                               int split = -1) {
+  if (split < 0) split = N_;
   if (N_ % 4 == 0)
-    colsum_rows_k<true><<<dim3((N_ + 15) / 16), 256, 0, s>>>(part, out, R, N_);
+    colsum_rows_k<true><<<dim3((N_ + 15) / 16), 256, 0, s>>>(part, out, R, N_, out2, split);
   else
-    colsum_rows_k<false><<<dim3((N_ + 15) / 16), 256, 0, s>>>(part, out, R, N_);
+    colsum_rows_k<false><<<dim3((N_ + 15) / 16), 256, 0, s>>>(part, out, R, N_, out2, split);
 }
 
 // Row-chunk plan shared by the fused "elementwise + column-sum" kernels: ~2048 blocks of
@@ -438,4 +442,20 @@ extern "C" void dpfs_bias_grad(int dtype, const void* dy, float* out, float* ws,
 
 extern "C" void dpfs_colsum_f32(const float* x, float* out, float* ws, int M, int N, hipStream_t s) {
   colsum_launch<float>(x, out, ws, M, N, s);
+}
+
+// Column sums of an fp32 [M, N] whose columns [0, split) go to out and [split, N) to out2:
+// two reductions stored side by side in one partial row (the norm backward's weight and
+// bias partials) in two launches instead of four.  ws: dpfs_colsum_ws(M, N) floats.
+extern "C" void dpfs_colsum_f32_split(const float* x, float* out, float* out2, int split, float* ws, int M, int N,
+                                      hipStream_t s) {
+  const int cblocks = (N / 4 + 31) / 32;
+  int chunks = 1024 / cblocks;
+  const int max_chunks = (M + 63) / 64;
+  if (chunks > max_chunks) chunks = max_chunks;
+  if (chunks < 1) chunks = 1;
+  const int rpc = (M + chunks - 1) / chunks;
+  chunks = (M + rpc - 1) / rpc;
+  colsum_stage_k<float><<<dim3(cblocks, chunks), 256, 0, s>>>(x, ws, M, N, rpc);
+  colsum_rows(ws, out, chunks, N, s, out2, split);
 }

@@ -171,7 +171,8 @@ __global__ __launch_bounds__(256) void layernorm_fwd_k(const T* __restrict__ x, 
 }
 
 // -------------------------------------------------------------------------- backward --
-// MODE 0 = RMSNorm, 1 = LayerNorm.  partial_w / partial_b: [gridDim.x, D] fp32.
+// MODE 0 = RMSNorm, 1 = LayerNorm, 2 = RMSNorm + column sums of dx.  partial_w: [gridDim.x, D]
+// fp32 (MODE 0) or [gridDim.x, 2D] (weight sums then bias / dx sums per row); partial_b unused.
 template <typename T, int VPL, int MODE>
 __global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, const T* __restrict__ x,
                                                   const float* __restrict__ w, const float* __restrict__ mean_in,
@@ -261,9 +262,12 @@ __global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, cons
     }
     __syncthreads();
   }
+  // Partial row of this block: [D] weight sums, followed for MODE != 0 by the [D] bias sums
+  // (one [G, 2D] matrix, reduced by a single two-output column sum).
+  const size_t rs = MODE != 0 ? 2 * (size_t)D : (size_t)D;
   for (int col = threadIdx.x; col < D; col += blockDim.x) {
-    partial_w[(size_t)blockIdx.x * D + col] = red[col];
-    if (MODE != 0) partial_b[(size_t)blockIdx.x * D + col] = red[D + col];
+    partial_w[(size_t)blockIdx.x * rs + col] = red[col];
+    if (MODE != 0) partial_w[(size_t)blockIdx.x * rs + D + col] = red[D + col];
   }
 }
 
@@ -296,13 +300,16 @@ int norm_bwd_grid(int M) {
 using namespace dpfs;
 
 extern "C" void dpfs_colsum_f32(const float* x, float* out, float* ws, int M, int N, hipStream_t s);
+extern "C" void dpfs_colsum_f32_split(const float* x, float* out, float* out2, int split, float* ws, int M, int N,
+                                      hipStream_t s);
 extern "C" long long dpfs_colsum_ws(int M, int N);
 
 extern "C" int dpfs_norm_bwd_grid(int M) { return norm_bwd_grid(M); }
 // Total fp32 workspace of dpfs_norm_bwd: block partials (x2 for LayerNorm) + stage-2 partials.
 extern "C" long long dpfs_norm_bwd_ws(int mode, int M, int D) {
   const int G = norm_bwd_grid(M);
-  return (long long)G * D * (mode != 0 ? 2 : 1) + dpfs_colsum_ws(G, D);
+  const int cols = D * (mode != 0 ? 2 : 1);
+  return (long long)G * cols + dpfs_colsum_ws(G, cols);
 }
 
 extern "C" void dpfs_rmsnorm_fwd(int dtype, const void* x, const float* w, void* y, float* rstd, int M, int D,
@@ -342,7 +349,8 @@ extern "C" void dpfs_layernorm_fwd(int dtype, const void* x, const float* w, con
 }
 
 // mode 0 = rms, 1 = layernorm, 2 = rms + column sums of dx (the bias grad of the layer whose
-// output grad dx is) into db.  partial_w/partial_b: [dpfs_norm_bwd_grid(M), D] workspace.
+// output grad dx is) into db.  partial_w: dpfs_norm_bwd_ws floats ([G, D] or [G, 2D] block
+// partials, then the column-sum workspace); partial_b is not used (kept for the ABI).
 extern "C" void dpfs_norm_bwd(int mode, int dtype, const void* dy, const void* x, const float* w, const float* mean,
                               const float* rstd, const void* dres, void* dx, float* dw, float* db, float* partial_w,
                               float* partial_b, int M, int D, hipStream_t s) {
@@ -360,6 +368,6 @@ extern "C" void dpfs_norm_bwd(int mode, int dtype, const void* dy, const void* x
   // Stage 2 (fixed-order 2-D column reduction over the G block partials).  The workspace
   // for its own partials lives after the G*D block partials (dpfs_norm_bwd_ws).
   float* ws2 = partial_w + (size_t)G * D * (mode != 0 ? 2 : 1);
-  dpfs_colsum_f32(partial_w, dw, ws2, G, D, s);
-  if (mode != 0) dpfs_colsum_f32(partial_b, db, ws2, G, D, s);
+  if (mode != 0) dpfs_colsum_f32_split(partial_w, dw, db, D, ws2, G, 2 * D, s);
+  else dpfs_colsum_f32(partial_w, dw, ws2, G, D, s);
 }
