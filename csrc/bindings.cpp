@@ -66,9 +66,10 @@ void dpfs_attn_set_impl(int);
 void dpfs_attn_set_bwd_impl(int);
 void dpfs_attn_fwd(const void*, const void*, const void*, void*, float*, int, int, int, int, long long, long long,
                    long long, long long, float, int, hipStream_t);
-void dpfs_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, float*, void*, void*,
+int dpfs_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, float*, void*, void*,
                    void*, int, int, int, int, long long, long long, long long, long long, long long, long long,
-                   long long, long long, float, int, const int64_t*, const float*, hipStream_t);
+                   long long, long long, float, int, const int64_t*, const float*, hipStream_t, float*, float*);
+long long dpfs_attn_bias_ws(int, int, int, int);
 // kernels/decode.hip
 int dpfs_decode_nsplit(int);
 void dpfs_attn_decode(const void*, long long, const void*, const void*, const int*, void*, long long, float*, int, int,
@@ -527,9 +528,13 @@ std::vector<torch::Tensor> attn_fwd(torch::Tensor q, torch::Tensor k, torch::Ten
   return {o, lse};
 }
 
-void attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Tensor o,
+// With dbias (fp32 [3 * H * hd], the packed QKV projection's bias layout) the q / k / v bias
+// gradient (column sums of the stored dq / dk / dv) comes out of the same kernels; returns
+// whether it did (false: another dK/dV variant is selected, dbias untouched).
+bool attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Tensor o,
               torch::Tensor lse, double scale, bool causal, torch::Tensor dq, torch::Tensor dk, torch::Tensor dv,
-              c10::optional<torch::Tensor> rope_pos, c10::optional<torch::Tensor> rope_tab) {
+              c10::optional<torch::Tensor> rope_pos, c10::optional<torch::Tensor> rope_tab,
+              c10::optional<torch::Tensor> dbias) {
   const int64_t B = q.size(0), T = q.size(1), H = q.size(2), hd = q.size(3);
   TORCH_CHECK(dpfs_attn_supported_hd((int)hd), "attn: head_dim not supported");
   auto vq = check_bthd(q, "q", B, T, H, hd), vk = check_bthd(k, "k", B, T, H, hd), vv = check_bthd(v, "v", B, T, H, hd);
@@ -539,7 +544,17 @@ void attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tenso
   TORCH_CHECK(lse.is_cuda() && lse.scalar_type() == torch::kFloat32 && lse.is_contiguous() && lse.numel() == B * H * T,
               "attn_bwd: lse must be contiguous fp32 (B, H, T)");
   const at::DeviceGuard g(q.device());
-  if (B * T * H == 0) return;
+  float* db = nullptr;
+  if (dbias.has_value() && dbias->defined()) {
+    TORCH_CHECK(dbias->is_cuda() && dbias->scalar_type() == torch::kFloat32 && dbias->is_contiguous() &&
+                    dbias->numel() == 3 * H * hd,
+                "attn_bwd: dbias must be contiguous fp32 [3 * H * hd]");
+    db = dbias->data_ptr<float>();
+  }
+  if (B * T * H == 0) {
+    if (db) dbias->zero_();
+    return db != nullptr;
+  }
   const int64_t* rp = nullptr;
   const float* rt = nullptr;
   if (rope_pos.has_value() && rope_pos->defined()) {
@@ -552,9 +567,12 @@ void attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tenso
     rt = rope_tab->data_ptr<float>();
   }
   auto delta = torch::empty({2, B, H, T}, lse.options());   // -delta | -lse/scale
-  dpfs_attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
-                delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), (int)B, (int)T, (int)H, (int)hd,
-                vdo.ld, vq.ld, vk.ld, vv.ld, vo.ld, vdq.ld, vdk.ld, vdv.ld, (float)scale, causal ? 1 : 0, rp, rt, stream());
+  torch::Tensor bws;
+  if (db) bws = torch::empty({dpfs_attn_bias_ws((int)B, (int)T, (int)H, (int)hd)}, lse.options());
+  return dpfs_attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
+                       delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), (int)B, (int)T, (int)H,
+                       (int)hd, vdo.ld, vq.ld, vk.ld, vv.ld, vo.ld, vdq.ld, vdk.ld, vdv.ld, (float)scale, causal ? 1 : 0,
+                       rp, rt, stream(), db, db ? bws.data_ptr<float>() : nullptr) != 0;
 }
 
 // ------------------------------------------------------------------- embedding / CE --
@@ -1069,7 +1087,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_set_bwd_impl", [](int v) { dpfs_attn_set_bwd_impl(v); }, "dK/dV kernel: 2 = LDS-DMA ring (default), 1 = register-staged");
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("scale"), py::arg("causal"), py::arg("dq"), py::arg("dk"), py::arg("dv"),
-        py::arg("rope_pos") = py::none(), py::arg("rope_tab") = py::none());
+        py::arg("rope_pos") = py::none(), py::arg("rope_tab") = py::none(), py::arg("dbias") = py::none());
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("ce_fwd_stats", &ce_fwd_stats);

@@ -831,8 +831,11 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv2_k(
     const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V, const bf16* __restrict__ dO,
     const float* __restrict__ LSE, const float* __restrict__ DELTA, bf16* __restrict__ dK, bf16* __restrict__ dV,
     int T, int H, long long ldq, long long ldk, long long ldv, long long lddo, long long lddk, long long lddv,
-    float scale, int causal, const int64_t* __restrict__ rpos, const float* __restrict__ rtab) {
+    float scale, int causal, const int64_t* __restrict__ rpos, const float* __restrict__ rtab,
+    float* __restrict__ BPK, float* __restrict__ BPV) {
   // LSE here = -lse/scale and DELTA = -delta per query row (written by attn_bwd_dq_k).
+  // BPK / BPV (optional): each wave's column sums of its stored dK / dV rows, row
+  // ((h * B + b) * nkb + kb) * 4 + wave of a [H * B * nkb * 4, HD] partial (k / v bias grad).
   constexpr int BKV = 64, BQ = 64, KT = HD / 32, DT = HD / 16;
   constexpr int TILE = BQ * HD * 2;
   constexpr int BUF = 2 * TILE + 1024;        // Q, dO, lse, delta, dummy slot (1 KiB aligned stages)
@@ -1010,6 +1013,35 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv2_k(
       }
     }
   }
+  if (BPK) {
+    // Column sums over the wave's 16 keys (4 in-lane, then the 4 lane groups).
+    float sk[DT], sv[DT];
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+      sk[d] = 0.f;
+      sv[d] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (wk0 + 4 * g + j < T) {
+          sk[d] += dk[d][j];
+          sv[d] += dv[d][j];
+        }
+      }
+      sk[d] += __shfl_xor(sk[d], 16, 64);
+      sv[d] += __shfl_xor(sv[d], 16, 64);
+      sk[d] += __shfl_xor(sk[d], 32, 64);
+      sv[d] += __shfl_xor(sv[d], 32, 64);
+    }
+    // One partial row per wave (no block barrier: a wave that finishes early leaves).
+    if (l < 16) {
+      const long long row = (((long long)h * (gridDim.y / H) + b) * gridDim.x + kb) * 4 + wave;
+#pragma unroll
+      for (int d = 0; d < DT; ++d) {
+        BPK[row * HD + 16 * d + l] = sk[d];
+        BPV[row * HD + 16 * d + l] = sv[d];
+      }
+    }
+  }
 }
 
 // ============================================================================ bwd: dQ ==
@@ -1023,7 +1055,9 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
                                                         int H, long long ldq, long long ldk, long long ldv,
                                                         long long lddo, long long ldo, long long lddq, float scale,
                                                         int causal, const int64_t* __restrict__ rpos,
-                                                        const float* __restrict__ rtab) {
+                                                        const float* __restrict__ rtab, float* __restrict__ BPQ) {
+  // BPQ (optional): each wave's column sums of its stored dQ rows, row ((h * B + b) * nqb +
+  // qb) * 4 + wave of a [H * B * nqb * 4, HD] partial (the q bias gradient).
   constexpr int BQ = 128, BKV = 64, KT = HD / 32, DT = HD / 16;
   constexpr int TILE = BKV * HD * 2;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
@@ -1203,6 +1237,54 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
       }
     }
   }
+  if (BPQ) {
+    // Column sums over the wave's 32 queries (2 in-lane, then the 16 lanes of a group).
+    f32x4 sq[DT];
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+      sq[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        if (wq0 + 16 * c + (l & 15) < T) sq[d] += dq[c][d];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sq[d][r] += __shfl_xor(sq[d][r], o, 64);
+    }
+    // One partial row per wave (no block barrier: a wave that finishes early leaves).
+    if ((l & 15) == 0) {
+      float* dst = BPQ + ((((long long)h * (gridDim.y / H) + b) * gridDim.x + qb) * 4 + wave) * HD + 4 * g;
+#pragma unroll
+      for (int d = 0; d < DT; ++d) *reinterpret_cast<f32x4*>(dst + 16 * d) = sq[d];
+    }
+  }
+}
+
+// Bias gradient of the packed QKV projection from the attention backward's per-wave column
+// sums: out[seg * H * HD + h * HD + col] = sum over the R rows of head h's partial (seg 0 = q
+// with Rq rows, 1 / 2 = k / v with Rk rows).  One 1024-thread block per (seg, head, 16-column
+// group): 16 columns x 64 row lanes, then the lanes in a fixed order (deterministic).
+template <int HD>
+__global__ __launch_bounds__(1024) void attn_bias_grad_k(const float* __restrict__ PQ, const float* __restrict__ PK,
+                                                         const float* __restrict__ PV, float* __restrict__ out, int H,
+                                                         int Rq, int Rk) {
+  constexpr int CG = HD / 16;
+  __shared__ float red[64][16];
+  const int cgi = blockIdx.x % CG, sh = blockIdx.x / CG, seg = sh / H, h = sh % H;
+  const float* P = seg == 0 ? PQ : (seg == 1 ? PK : PV);
+  const int R = seg == 0 ? Rq : Rk;
+  const int c = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const float* base = P + (long long)h * R * HD + cgi * 16 + c;
+  float s = 0.f;
+#pragma unroll 8
+  for (int r = rl; r < R; r += 64) s += base[(long long)r * HD];
+  red[rl][c] = s;
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    float t = 0.f;
+    for (int k = 0; k < 64; ++k) t += red[k][threadIdx.x];
+    out[(long long)seg * H * HD + (long long)h * HD + cgi * 16 + threadIdx.x] = t;
+  }
 }
 
 }  // namespace dpfs
@@ -1247,17 +1329,25 @@ extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void*
 }
 
 // delta: workspace [2][B, H, T] fp32: -delta (rowsum(dO*O)) and -lse/scale, written by the dQ kernel.
-extern "C" void dpfs_attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o,
+extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o,
                               const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int T, int H,
                               int hd, long long lddo, long long ldq, long long ldk, long long ldv, long long ldo,
                               long long lddq, long long lddk, long long lddv, float scale, int causal,
-                              const int64_t* rope_pos, const float* rope_tab, hipStream_t s) {
-  dim3 gq((T + 127) / 128, B * H);
+                              const int64_t* rope_pos, const float* rope_tab, hipStream_t s, float* dbias,
+                              float* bws) {
+  // The QKV bias gradient rides on the default kernel pair (dQ + LDS-DMA dK/dV); with another
+  // dK/dV variant the caller computes it with a separate column sum.
+  const bool bias = dbias != nullptr && bws != nullptr && g_attn_bwd_impl == 2;
+  const int nqb = (T + 127) / 128, nkb = (T + 63) / 64;
+  float* pq = bias ? bws : nullptr;
+  float* pk = bias ? bws + (long long)H * B * nqb * 4 * hd : nullptr;
+  float* pv = bias ? pk + (long long)H * B * nkb * 4 * hd : nullptr;
+  dim3 gq(nqb, B * H);
   DPFS_HD_DISPATCH(hd, attn_bwd_dq_k<HD_><<<gq, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
                                                              (const bf16*)dout, (const bf16*)o, lse, delta,
                                                              delta + (long long)B * H * T, (bf16*)dq,
                                                              T, H, ldq, ldk, ldv, lddo, ldo, lddq, scale, causal,
-                                                             rope_pos, rope_tab));
+                                                             rope_pos, rope_tab, pq));
   if (g_attn_bwd_impl == 3 && hd <= 64) {
     dim3 gk2((T + 127) / 128, B * H);
     if (hd == 64)
@@ -1268,7 +1358,7 @@ extern "C" void dpfs_attn_bwd(const void* dout, const void* q, const void* k, co
       attn_bwd_dkdv_k<32, 2><<<gk2, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,
                                                  lse, delta, (bf16*)dk, (bf16*)dv, T, H, ldq, ldk, ldv, lddo, lddk,
                                                  lddv, scale, causal, rope_pos, rope_tab);
-    return;
+    return 0;
   }
   dim3 gk((T + 63) / 64, B * H);
   if (g_attn_bwd_impl == 2) {
@@ -1276,11 +1366,24 @@ extern "C" void dpfs_attn_bwd(const void* dout, const void* q, const void* k, co
                                                                   (const bf16*)dout, delta + (long long)B * H * T,
                                                                   delta, (bf16*)dk,
                                                                   (bf16*)dv, T, H, ldq, ldk, ldv, lddo, lddk, lddv,
-                                                                  scale, causal, rope_pos, rope_tab));
-    return;
+                                                                  scale, causal, rope_pos, rope_tab, pk, pv));
+    if (bias) {
+      DPFS_HD_DISPATCH(hd, attn_bias_grad_k<HD_><<<3 * H * (HD_ / 16), 1024, 0, s>>>(pq, pk, pv, dbias, H,
+                                                                                       B * nqb * 4, B * nkb * 4));
+      return 1;
+    }
+    return 0;
   }
   DPFS_HD_DISPATCH(hd, attn_bwd_dkdv_k<HD_><<<gk, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
                                                                (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv, T,
                                                                H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal,
                                                                rope_pos, rope_tab));
+  return 0;
+}
+
+// Floats of the bias-gradient partials dpfs_attn_bwd needs (one q row per dQ wave, one k and
+// one v row per dK/dV wave, HD columns each).
+extern "C" long long dpfs_attn_bias_ws(int B, int T, int H, int hd) {
+  const long long nqb = (T + 127) / 128, nkb = (T + 63) / 64;
+  return (long long)H * B * (nqb + 2 * nkb) * 4 * hd;
 }

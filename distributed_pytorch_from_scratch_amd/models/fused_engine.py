@@ -35,6 +35,7 @@ presets).  ``ModelArgs.sequence_parallel`` / LayerNorm models use the modular au
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional
 
 import torch
@@ -397,12 +398,16 @@ class DecoderTrainFn(torch.autograd.Function):
                 q, kk, v = _split(a["qkv"], Bc, T, L.h, L.hd)
                 dqkv = torch.empty_like(a["qkv"])
                 dq, dk, dv = _split(dqkv, Bc, T, L.h, L.hd)
-                k.attn_bwd(do.view(Bc, T, L.h, L.hd), q, kk, v, a["o"], a["lse"], 1.0 / math.sqrt(L.hd), True,
-                           dq, dk, dv, s["pos"], tab)   # inverse RoPE fused into the dq/dk stores
+                dbq = dqkv.new_empty(dqkv.size(1), dtype=torch.float32) \
+                    if L.bqkv is not None and _QKV_BIAS_IN_ATTN else None
+                # inverse RoPE fused into the dq/dk stores, the QKV bias grad into their epilogues
+                bq_fused = k.attn_bwd(do.view(Bc, T, L.h, L.hd), q, kk, v, a["o"], a["lse"], 1.0 / math.sqrt(L.hd),
+                                      True, dq, dk, dv, s["pos"], tab, dbias=dbq)
                 dh = GS.gemm_nn(k, dqkv, W(L.wqkv), out=_slot(ci, dqkv.size(0), d, dt))
                 s["bh"], s["dpend"] = _ar(dh), dh
                 wqkv_p.append((dqkv, a["h1"]))
-                bias_acc(G, "bqkv", dqkv, L.bqkv)
+                if L.bqkv is not None:
+                    G["bqkv"] = _addg(G.get("bqkv"), dbq if bq_fused else k.bias_grad(dqkv))
                 s["g"] = g2
                 for key in ("x2", "r2", "h2", "qkv", "o", "lse"):
                     a.pop(key, None)
@@ -457,6 +462,11 @@ def _finish_norm1(k, s, L, G, li, below=None):
     s["dpend"] = None
     for key in ("x", "r1", "h1"):
         a.pop(key, None)
+
+
+# The QKV bias gradient from the attention backward's epilogues (default) or a separate column
+# sum over d(QKV) (DPFS_QKV_BIAS_IN_ATTN=0, A/B runs).
+_QKV_BIAS_IN_ATTN = os.environ.get("DPFS_QKV_BIAS_IN_ATTN", "1") != "0"
 
 
 def _split(qkv, B, T, h, hd):

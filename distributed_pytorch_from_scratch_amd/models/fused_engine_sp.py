@@ -38,7 +38,7 @@ from ..ops import gemm_select as GS
 from ..ops.dispatch import K, shadow
 from ..parallel import process_manager as pm
 from ..parallel import tp_comm
-from .fused_engine import _Layer, _addg, _defer_begin, _defer_end, _defer_flush, _split, _wait
+from .fused_engine import _QKV_BIAS_IN_ATTN, _Layer, _addg, _defer_begin, _defer_end, _defer_flush, _split, _wait
 
 
 def _rs(full: torch.Tensor, n: int):
@@ -306,12 +306,14 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 q, kk, v = _split(a["qkv"], Bc, T, L.h, L.hd)
                 dqkv = torch.empty_like(a["qkv"])
                 dq, dk, dv = _split(dqkv, Bc, T, L.h, L.hd)
-                k.attn_bwd(do.view(Bc, T, L.h, L.hd), q, kk, v, a["o"], a["lse"], 1.0 / math.sqrt(L.hd), True,
-                           dq, dk, dv, s["pos"], tab)
+                dbq = dqkv.new_empty(dqkv.size(1), dtype=torch.float32) \
+                    if L.bqkv is not None and _QKV_BIAS_IN_ATTN else None
+                bq_fused = k.attn_bwd(do.view(Bc, T, L.h, L.hd), q, kk, v, a["o"], a["lse"], 1.0 / math.sqrt(L.hd),
+                                      True, dq, dk, dv, s["pos"], tab, dbias=dbq)
                 s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dqkv, W(L.wqkv), out=_slot(ci, dqkv.size(0), d, dt)), n)
                 wqkv_p.append((dqkv, a["h1"]))
                 if L.bqkv is not None:
-                    G["bqkv"] = _addg(G.get("bqkv"), k.bias_grad(dqkv))
+                    G["bqkv"] = _addg(G.get("bqkv"), dbq if bq_fused else k.bias_grad(dqkv))
                 for key in ("qkv", "o", "lse", "h1"):
                     a.pop(key, None)
                 del s["gfull"]

@@ -264,9 +264,11 @@ def _rot_bthd(x: torch.Tensor, positions: torch.Tensor, table: torch.Tensor, inv
 
 
 def attn_bwd(do, q, k, v, o, lse, scale: float, causal: bool, dq_out, dk_out, dv_out, rope_pos=None,
-             rope_tab=None):
+             rope_tab=None, dbias=None):
     """Writes dq/dk/dv into the given (B, T, H, hd) views (packed dqkv buffer).  With
-    ``rope_pos`` the inverse RoPE is applied to dq and dk (fused into the stores on the GPU)."""
+    ``rope_pos`` the inverse RoPE is applied to dq and dk (fused into the stores on the GPU).
+    With ``dbias`` (fp32 [3 * H * hd]) also the packed QKV bias gradient: the column sums of
+    dq | dk | dv over all tokens.  Returns whether ``dbias`` was written."""
     qf, kf, vf, dof, of = (t.float().transpose(1, 2) for t in (q, k, v, do, o))
     s = (qf @ kf.transpose(-1, -2)) * scale
     if causal:
@@ -287,6 +289,10 @@ def attn_bwd(do, q, k, v, o, lse, scale: float, causal: bool, dq_out, dk_out, dv
     dq_out.copy_(dq)
     dk_out.copy_(dk)
     dv_out.copy_(dv.transpose(1, 2))
+    if dbias is None:
+        return False
+    dbias.copy_(torch.cat([t.float().sum((0, 1)).reshape(-1) for t in (dq, dk, dv.transpose(1, 2))]))
+    return True
 
 
 # ------------------------------------------------------------------------- SwiGLU ----

@@ -306,6 +306,32 @@ def test_attention_bwd_fused_inverse_rope(C, hd):
     assert _rel(d, r) < 3e-2
 
 
+@pytest.mark.parametrize("hd,T", [(64, 192), (128, 130), (32, 1024)])
+def test_attention_bwd_fused_qkv_bias_grad(C, hd, T):
+    """dbias = column sums of the stored dq | dk | dv (inverse RoPE applied), from the attention
+    backward's epilogues; ragged T masks the rows past the sequence."""
+    torch.manual_seed(26)
+    B, H = 2, 3
+    qkv = torch.randn(B * T, 3 * H * hd, device=DEV).bfloat16()
+    q, k, v = (qkv[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+    o, lse = C.attn_fwd(q, k, v, hd ** -0.5, True)
+    do = torch.randn_like(o)
+    pos = torch.randint(0, 2048, (B * T,), device=DEV)
+    tab = R.rope_table(2048, hd, 10000.0).to(DEV)
+    d = torch.empty_like(qkv)
+    dq, dk, dv = (d[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+    db = torch.full((3 * H * hd,), float("nan"), device=DEV)
+    assert C.attn_bwd(do, q, k, v, o, lse, hd ** -0.5, True, dq, dk, dv, pos, tab, dbias=db)
+    want = d.float().sum(0)
+    assert _rel(db, want) < 5e-3
+    r = torch.empty(B * T, 3 * H * hd, device=DEV)
+    rq, rk, rv = (r[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+    rdb = torch.empty(3 * H * hd, device=DEV)
+    R.attn_bwd(do.float(), q.float(), k.float(), v.float(), o.float(), lse, hd ** -0.5, True, rq, rk, rv,
+               pos, tab, dbias=rdb)
+    assert _rel(db, rdb) < 3e-2
+
+
 def test_rmsnorm_bwd_fused_residual_grad(C):
     torch.manual_seed(14)
     M, D = 513, 768
