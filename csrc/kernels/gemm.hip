@@ -968,7 +968,7 @@ extern "C" void dpfs_gemm_nn(const void* A, const void* B, void* C, int M, int N
 }
 
 // TN (wgrad) plan.  Outputs are small (weight shards) and K = tokens is long, so the K-split
-// count S sets the grid.  v2 256x256: S (power of 2, K/S >= 512) minimising a makespan model
+// count S sets the grid.  v2 256x256: S (K/S >= 512) minimising a makespan model
 // calibrated on MI355X sweeps (profiles/r1_gemm_tn_sweep.log, within ~10 % on every TP1-8
 // GPT-2 wgrad shape):  ceil(tiles*S / 256 CUs) * ceil(K/S / 64) * 1.95 us   (one 256x256x64
 // K-step per CU)  +  S*M*N*8 B / 4 TB/s  (fp32 slabs written + reduced).  The 128x128 v1
@@ -978,7 +978,9 @@ static int tn_v2_splits(int M, int N, int K) {
   const long long tiles = tiles2(M, N, 256, 256);
   int best = 1;
   double best_t = 1e300;
-  for (int S = 1; S <= 64; S *= 2) {
+  // Every split count, not only powers of 2: the lm_head wgrad (591 tiles = 2.3 rounds of 256
+  // CUs) runs best at S = 3 (7 full rounds): 2.44 vs 2.58 ms at S = 2 (tools/tn_lmhead_probe.py).
+  for (int S = 1; S <= 64; ++S) {
     if (S > 1 && K / S < 512) break;
     const long long kps = ((K + S - 1) / S + 63) / 64;
     const long long rounds = (tiles * S + 255) / 256;
