@@ -1,7 +1,7 @@
 """Loader for the in-tree native extension ``distributed_pytorch_from_scratch_amd._C``.
 
 The extension holds every hand-written HIP/CDNA4 kernel (``csrc/kernels/*.hip``, built for
-gfx950 by ``setup.py build_ext --inplace`` / ``__graft_entry__.build()``).  There is exactly
+gfx950 by ``python tools/build_ext.py`` / ``__graft_entry__.build()``).  There is exactly
 one compute path per device:
 
 * ``cuda`` (HIP) tensors -> ``_C`` kernels.  If the extension is missing or fails to load,
@@ -46,7 +46,7 @@ def require():
     if _C is None:
         raise RuntimeError(
             "distributed_pytorch_from_scratch_amd._C (HIP kernels for gfx950) is not built or "
-            f"failed to load: {_ERR!r}. Run `python setup.py build_ext --inplace` "
+            f"failed to load: {_ERR!r}. Run `python tools/build_ext.py` "
             "(or __graft_entry__.build()).")
     if debug_sync() or nan_check():
         if _PROXY is None:

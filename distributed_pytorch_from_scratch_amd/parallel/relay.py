@@ -26,6 +26,13 @@ sorted relay list; x's partner expects unit j from the relay at position j of IT
 the same set (every rank but the two of the pair) in the same order.  Because every rank of the WORLD takes part in every relayed collective,
 ``parallel/tp_comm.py`` only selects this transport by a WORLD-wide decision (validated against
 the RCCL sum and timed against RCCL / xGMI on every rank), never per group.
+
+Message sizes: a relay receives a unit from every other pair, so every pair must cut its payload
+with the SAME unit size.  Two pairs of a ``tp2dpN`` layout hold different batches, and real-data
+batches are padded per batch, so their payloads can differ.  Unless the caller declared fixed
+shapes (``tp_comm.set_fixed_shapes``: synthetic data / fixed-length batches, the only case
+``auto`` offers this transport for), every exchange first agrees on the WORLD-wide maximum
+payload (one tiny all-reduce) and pads to it; the receiver keeps its own pair's prefix.
 """
 from __future__ import annotations
 
@@ -75,6 +82,9 @@ class RelayComm:
         # gloo moves CUDA tensors by their raw device pointers from host threads, outside any
         # stream order (single-GPU multi-rank rehearsals only): fence it with device syncs
         self._host_fence = dist.get_backend() == "gloo"
+        # payload sizes are WORLD-uniform (set by tp_comm from set_fixed_shapes); otherwise
+        # every exchange agrees on the WORLD maximum first and pads to it
+        self.fixed_shapes = False
 
     # ---------------------------------------------------------------- exchange core ----
     def _split(self, n: int):
@@ -82,7 +92,26 @@ class RelayComm:
         q = (n // (self.R + 2)) // 8 * 8
         return n - self.R * q, q
 
+    def _world_max(self, n: int) -> int:
+        t = torch.tensor([n], dtype=torch.int64,
+                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return int(t.item())
+
     def _exchange(self, payload: torch.Tensor, recv: torch.Tensor) -> List:
+        """recv <- the partner's payload (same numel: the two ranks of a pair always agree).
+        Pads to the WORLD-wide maximum payload first unless shapes are declared fixed."""
+        n = payload.numel()
+        N = n if self.fixed_shapes else self._world_max(n)
+        if N == n:
+            return self._exchange_n(payload, recv)
+        pay_p = payload.new_zeros(N)
+        pay_p[:n].copy_(payload)
+        recv_p = recv.new_empty(N)
+        works = self._exchange_n(pay_p, recv_p)
+        return works + [_CopyBack(recv, recv_p[:n], keep=pay_p)]
+
+    def _exchange_n(self, payload: torch.Tensor, recv: torch.Tensor) -> List:
         """recv <- the partner's payload (same numel), direct units + relayed units.
         Returns the works of the second hop (or of the only hop when nothing is relayed).
 
@@ -165,7 +194,16 @@ class RelayComm:
         ordered on the side stream (the caller's stream only waits on the returned handle)."""
         flat = t.view(-1)
         if flat.numel() % 2:
-            raise ValueError("relayed all-reduce needs an even element count")
+            # odd count: sum a zero-padded copy (every rank pads the same way, so the call
+            # sequence stays WORLD-uniform; no per-rank fallback to another transport)
+            padded = flat.new_zeros(flat.numel() + 1)
+            padded[:-1].copy_(flat)
+            h = self.all_reduce(padded, async_op=True)
+            cb = _RelayWork([h, _CopyBack(flat, padded[:-1])])
+            if not async_op:
+                cb.wait()
+                return None
+            return cb
         if flat.is_cuda:
             if self._side is None:
                 self._side = torch.cuda.Stream(priority=-1)
@@ -180,6 +218,20 @@ class RelayComm:
             h.wait()
             return None
         return h
+
+
+class _CopyBack:
+    """Completion step of a padded exchange: the pair's own prefix of the padded receive
+    buffer goes to the caller's tensor (after every hop has been waited)."""
+
+    def __init__(self, dst, src, keep=None):
+        self.dst, self.src, self.keep = dst, src, keep
+
+    def wait(self):
+        if self.src is not None:
+            self.dst.view(-1).copy_(self.src)
+        self.src = self.keep = None
+        return True
 
 
 class _Hold:

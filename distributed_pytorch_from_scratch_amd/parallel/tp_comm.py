@@ -114,6 +114,18 @@ def _build(kind: str, g, forced: bool):
     return comm
 
 
+_fixed_shapes = False
+
+
+def set_fixed_shapes(v: bool = True):
+    """Declare that every rank of the WORLD passes the same message sizes to every TP
+    collective (synthetic data / fixed-length batches: bench.py, ``train.py --synthetic``).
+    Only then does ``auto`` consider the relayed transport, whose exchanges pair every rank
+    with every other (parallel/relay.py pads to a WORLD-agreed size otherwise)."""
+    global _fixed_shapes
+    _fixed_shapes = bool(v)
+
+
 def _relay_possible(p) -> bool:
     W = dist.get_world_size()
     return p.tp_size == 2 and W >= 4 and W % 2 == 0
@@ -127,14 +139,21 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
     g = p.tp_group
     W, r = p.tp_size, p.tp_rank
     kinds = [m] if m != "auto" else ["xgmi"]
-    relay_cand = (m == "relay" or m == "auto") and _relay_possible(p)
-    if m == "relay" and not relay_cand:
+    relay_cand = (m == "relay" or (m == "auto" and _fixed_shapes)) and _relay_possible(p)
+    if m == "relay" and not _relay_possible(p):
         raise RuntimeError("DPFS_TP_COMM=relay needs TP = 2 and at least two TP pairs")
     comms = {k: _build(k, g, forced=m != "auto") for k in kinds if k != "relay"}
     comms = {k: c for k, c in comms.items() if c is not None}
     if relay_cand:
+        # every decision input below is reduced over the WORLD, so every pair must hold the
+        # same candidate set: drop xGMI everywhere unless every pair built it
+        have = torch.tensor([1.0 if "xgmi" in comms else 0.0], device=t.device)
+        dist.all_reduce(have, op=dist.ReduceOp.MIN)
+        if have.item() == 0.0:
+            comms.pop("xgmi", None)
         from .relay import RelayComm
         comms["relay"] = RelayComm(p)
+        comms["relay"].fixed_shapes = _fixed_shapes
     # relayed ops involve every rank of the WORLD: reduce every decision input over it
     red_group = None if relay_cand else g
     if not comms:

@@ -75,6 +75,9 @@ def get_train_args(argv=None) -> Namespace:
     g.add_argument("--random_seed", type=int, default=0)
     g.add_argument("--use_vallina_impl", action="store_true", help="only changes the log tag (reference)")
     g.add_argument("--fault_inject_step", type=int, default=-1)
+    g.add_argument("--heartbeat_stale_s", type=float, default=300.0,
+                   help="abort the job when a rank's heartbeat is older than this (must be < the "
+                        "600 s RCCL timeout so a hung rank is reported instead of waited out); 0 = off")
     g.add_argument("--device", type=str, default=None, help="cuda|cpu (default: cuda if available)")
     a = p.parse_args(argv)
     if a.data_path is None and not a.synthetic:
@@ -101,6 +104,11 @@ def train(rank, args: Namespace):
                     recompute=getattr(args, "recompute", False), fp8=getattr(args, "fp8", False))
     model = Transformer.from_args(margs).to(dev)
     model.set_compute_dtype(compute_dtype)
+    if margs.fp8 and not (model.fused_supported() and use_cuda):
+        # fp8 GEMMs live in the explicit-schedule engines (RMSNorm models on the GPU); say so
+        # instead of logging an fp8 run that trains in bf16
+        raise SystemExit(f"--fp8 needs the fused engine on the GPU (RMSNorm model, CUDA); "
+                         f"model norm={margs.norm!r}, device={dev.type}")
     model.reset_parameters()
     model.train()
     nparam = model.num_parameters(global_count=True)
@@ -124,7 +132,9 @@ def train(rank, args: Namespace):
                                                 pct_start=min(0.99, args.warmup_steps / max(1, args.max_steps)))
     step_fn = TrainStep(model, opt, sched)
     writer = SummaryWriter(os.path.join(args.save_dir, f"tprank-{p.tp_rank}")) if p.dp_rank == 0 else None
-    hb = Heartbeat(interval_s=30.0)
+    hb_stale = getattr(args, "heartbeat_stale_s", 300.0)
+    hb = Heartbeat(interval_s=min(30.0, max(1.0, hb_stale / 10)), stale_s=hb_stale,
+                   abort_on_stale=hb_stale > 0) if hb_stale > 0 else Heartbeat(interval_s=30.0)
 
     start_step = 0
     if args.resume:

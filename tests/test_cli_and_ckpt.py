@@ -242,3 +242,41 @@ def test_sidecar_loads_weights_only(tmp_path):
     assert st["step"] == 1 and sched2.state_dict()["last_epoch"] == 1
     s1, s2 = opt.state_dict()["state"], opt2.state_dict()["state"]
     assert all(torch.equal(s1[i]["exp_avg"], s2[i]["exp_avg"]) for i in s1)
+
+
+_HB_SCRIPT = r'''
+import os, sys, time
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+def run(rank):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=sys.argv[1])
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    sys.path.insert(0, sys.argv[2])
+    from distributed_pytorch_from_scratch_amd.utils.fault import Heartbeat
+    hb = Heartbeat(interval_s=0.3, stale_s=2.0, abort_on_stale=True)
+    hb.beat(1)
+    if rank == 1:
+        time.sleep(30)          # hung rank: no more heartbeats
+    else:
+        for s in range(200):    # healthy rank keeps beating; the watcher must abort the job
+            time.sleep(0.1)
+            hb.beat(s + 2)
+    os._exit(0)
+
+if __name__ == "__main__":
+    mp.spawn(run, nprocs=2, join=True)
+'''
+
+
+def test_heartbeat_aborts_on_stale_rank(tmp_path):
+    """A rank that stops beating is detected by rank 0's watcher, which aborts the job (exit
+    17) long before the RCCL timeout instead of only printing a warning."""
+    import time
+    script = tmp_path / "hb.py"
+    script.write_text(_HB_SCRIPT)
+    t0 = time.time()
+    r = _run([str(script), _port(), ROOT], timeout=120)
+    assert r.returncode != 0, r.stdout + r.stderr
+    assert "stale ranks" in (r.stdout + r.stderr)
+    assert time.time() - t0 < 25

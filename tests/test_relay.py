@@ -89,3 +89,45 @@ def test_relay_training_step_matches(sp):
     got = run_distributed(_train, 4, "relay", sp, tp_size=2)
     for r in range(4):
         assert all(abs(a - b) < 1e-5 for a, b in zip(got[r], ref[r])), (r, got[r], ref[r])
+
+
+def _ragged(rank, world, base_sizes):
+    """Every TP pair passes a DIFFERENT message size in the same collective (real-data batches
+    padded per batch on each DP rank): the relay must agree on one unit size over the WORLD."""
+    os.environ["DPFS_TP_COMM"] = "relay"
+    import torch.distributed as dist
+    from distributed_pytorch_from_scratch_amd.parallel import process_manager as pm, tp_comm
+    p = pm.get_pgm()
+    errs = []
+    for base in base_sizes:
+        n = base + 24 * p.dp_rank                 # pair-dependent, even
+        g = torch.Generator().manual_seed(7 * n + rank)
+        x = torch.randn(n, generator=g)
+        ref = x.clone()
+        dist.all_reduce(ref, group=p.tp_group)
+        out = torch.empty(n // 2)
+        h = tp_comm.reduce_scatter(out, x, async_op=True)
+        if h is not None:
+            h.wait()
+        errs.append((out - ref.view(2, -1)[p.tp_rank]).abs().max().item())
+        full = torch.empty(n)
+        h = tp_comm.all_gather(full, out, async_op=True)
+        if h is not None:
+            h.wait()
+        errs.append((full - ref).abs().max().item())
+        for odd in (n + 1, n + 3):                # odd all-reduce counts (zero-padded inside)
+            y = torch.randn(odd, generator=g)
+            r2 = y.clone()
+            dist.all_reduce(r2, group=p.tp_group)
+            h = tp_comm.all_reduce(y, async_op=True)
+            if h is not None:
+                h.wait()
+            errs.append((y - r2).abs().max().item())
+    return max(errs)
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_relay_ragged_sizes_across_pairs(world):
+    res = run_distributed(_ragged, world, [48, 1000, 20_000], tp_size=2)
+    for r, err in res.items():
+        assert err < 1e-5, (r, err)

@@ -8,7 +8,7 @@ Two-stage native build, no hipify, no JIT cache:
 3. link with the ROCm runtime, RCCL and hipBLASLt that PyTorch itself ships (``torch/lib``), so
    the process has exactly one instance of each.
 
-Usage: ``python tools/build_ext.py [--jobs N] [--force]`` (also called by ``setup.py`` and
+Usage: ``python tools/build_ext.py [--jobs N] [--force]`` (also called by
 ``__graft_entry__.build()``).
 """
 from __future__ import annotations
