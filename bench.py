@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--layers", type=int, default=None, help="debug only: not a valid headline number")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--recompute", action="store_true", help="activation recompute (layer inputs only)")
+    ap.add_argument("--no-pure-tp", dest="pure_tp", action="store_false",
+                    help="at N > 1 with a TP x DP headline layout, skip the extra pure-TP (tp = N) measurement")
     ap.add_argument("--fp8", action="store_true",
                     help="fp8 (e4m3 / e5m2) forward and data-gradient GEMMs (ops/fp8.py); NOT the bf16 headline")
     return ap.parse_args()
@@ -78,27 +80,18 @@ def resolve_tp(tp: str, model: str, world: int) -> int:
     return t
 
 
-def main():
-    a = parse()
-    if os.environ.get("DPFS_STACK_DUMP_S"):   # hang diagnosis: every rank prints its Python stacks
-        import faulthandler
-        faulthandler.dump_traceback_later(float(os.environ["DPFS_STACK_DUMP_S"]), repeat=True)
+def measure(a, tp: int, world: int, dev, first: bool):
+    """Build the model on a (dp = world / tp) x tp grid, run the warmup (with the engine trial
+    at TP > 1) and EXACTLY ``a.steps`` timed steps bracketed by barrier + synchronize on both
+    sides.  Returns the layout's numbers (elapsed = max over ranks)."""
     from distributed_pytorch_from_scratch_amd.models import get_preset, Transformer
     from distributed_pytorch_from_scratch_amd.ops.optim import FusedAdam
     from distributed_pytorch_from_scratch_amd.engine import TrainStep
     from distributed_pytorch_from_scratch_amd.utils.dist import init_dist_env, set_seed
-    from distributed_pytorch_from_scratch_amd.parallel import tp_comm
+    from distributed_pytorch_from_scratch_amd.parallel import process_manager as pm, tp_comm
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world == 1 and a.gpus > 1:
-        raise SystemExit("for --gpus > 1 launch with torch.distributed.run --nproc-per-node N")
-    assert world == a.gpus, f"WORLD_SIZE={world} but --gpus {a.gpus}"
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29511")
-    tp = resolve_tp(a.tp, a.model, world)
-    p = init_dist_env(rank=None, tp_size=tp, dp_size=world // tp)
-    rank = dist.get_rank()
-    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    p = init_dist_env(rank=None, tp_size=tp, dp_size=world // tp) if first else pm.init_pgm(tp, world // tp)
+    tp_comm.set_fixed_shapes(True)   # synthetic fixed-shape batches on every rank
 
     # SP is a property of the step, not of the weights: build with the SP attributes and
     # switch the engine per step (TrainStep.sp / args.sequence_parallel).
@@ -161,6 +154,10 @@ def main():
             step.sp = on
             model.chunks = chunks
 
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+
     # Engine configurations (SP on/off, ping-pong chunks), most likely first.  At TP > 1 the
     # warmup steps double as a trial of as many as fit (2 steps each, the first untimed:
     # first-call GEMM selection / transport choice); every rank takes the config with the
@@ -170,9 +167,9 @@ def main():
     default = (tp > 1 and a.sp != "off", 2 if tp > 1 else 1)
     cands = [default]
     if a.sp == "auto":
-        cands += [(not default[0], 2), (True, 4), (False, 4)]
+        cands += [(default[0], 1), (not default[0], 2), (not default[0], 1), (True, 4), (False, 4)]
     else:
-        cands += [(a.sp == "on", 4)]
+        cands += [(a.sp == "on", 4), (a.sp == "on", 1)]
     cands = list(dict.fromkeys(cands))
     ntrial = min(len(cands), a.warmup // 2) if a.impl == "ours" and tp > 1 else 0
     trial = {}
@@ -180,13 +177,11 @@ def main():
     for cfg in cands[:ntrial] if ntrial >= 2 else []:
         set_cfg(cfg)
         loss = run(i)
-        if dev.type == "cuda":
-            torch.cuda.synchronize()
+        sync()
         dist.barrier()
         t0 = time.perf_counter()
         loss = run(i + 1)
-        if dev.type == "cuda":
-            torch.cuda.synchronize()
+        sync()
         dt_ = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
         dist.all_reduce(dt_, op=dist.ReduceOp.MAX)
         trial[cfg] = float(dt_.item())
@@ -196,26 +191,60 @@ def main():
         loss = run(i)
         i += 1
     sp_used = bool(a.impl == "ours" and model.args.sequence_parallel)
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
+    sync()
     dist.barrier()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(a.steps):
         loss = run(a.warmup + i)
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
+    sync()
     dist.barrier()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
+    sync()
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
-    final_loss = float(loss.float().item())
+    res = dict(
+        value=gb * T * a.steps / elapsed, elapsed=elapsed, gb=gb, T=T, args=args,
+        parallelism=f"tp{tp}" + (f"dp{p.dp_size}" if p.dp_size > 1 else "") + ("+sp" if sp_used else ""),
+        final_loss=float(loss.float().item()), tp_comm=tp_comm.info(),
+        chunks=model.overlap_chunks() if a.impl == "ours" else None,
+        trial={f"{'sp' if k[0] else 'nosp'}/c{k[1]}": round(1000 * v, 2) for k, v in trial.items()} or None)
+    del model, opt, pool
+    if a.impl == "ours":
+        del step
+    if dev.type == "cuda":
+        torch.cuda.empty_cache()
+    return res
 
-    tokens = gb * T * a.steps
-    value = tokens / elapsed
+
+def main():
+    a = parse()
+    if os.environ.get("DPFS_STACK_DUMP_S"):   # hang diagnosis: every rank prints its Python stacks
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["DPFS_STACK_DUMP_S"]), repeat=True)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and a.gpus > 1:
+        raise SystemExit("for --gpus > 1 launch with torch.distributed.run --nproc-per-node N")
+    assert world == a.gpus, f"WORLD_SIZE={world} but --gpus {a.gpus}"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29511")
+    tp = resolve_tp(a.tp, a.model, world)
+    if torch.cuda.is_available():
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+
+    head = measure(a, tp, world, dev, first=True)
+    rank = dist.get_rank()
+    # The reference trains with tp_size == world_size (process_manager.py:13-15, recipe.sh TP 1 /
+    # 2 / 4): at N > 1 the pure-TP layout is measured as well and reported next to the headline
+    # layout (same contract: W warmup + K timed steps, max over ranks), each with its label.
+    layouts = [head]
+    if world > 1 and tp != world and a.pure_tp:
+        layouts.append(measure(a, world, world, dev, first=False))
+
+    args, T, gb = head["args"], head["T"], head["gb"]
+    value, elapsed = head["value"], head["elapsed"]
     # The reference-formulation baseline was measured on GPT-2 small only; other shapes get null.
     base = REFERENCE_TOKENS_PER_S_TP1 if (a.model == "gpt2-small" and not a.layers) else None
     vs = None
@@ -240,20 +269,27 @@ def main():
             "model": a.model + (f"(L={a.layers})" if a.layers else ""),
             "global_batch": gb,
             "seq_len": T,
-            "parallelism": f"tp{tp}" + (f"dp{p.dp_size}" if p.dp_size > 1 else "") + ("+sp" if sp_used else ""),
+            "parallelism": head["parallelism"],
             "impl": a.impl,
             "recompute": bool(a.recompute),
             "fp8": bool(a.fp8),
             "params_matmul": args.matmul_params(),
-            "tp_comm": tp_comm.info(),
-            "chunks": model.overlap_chunks() if a.impl == "ours" else None,
-            "engine_trial_ms": {f"{'sp' if k[0] else 'nosp'}/c{k[1]}": round(1000 * v, 2)
-                                for k, v in trial.items()} or None,
+            "tp_comm": head["tp_comm"],
+            "chunks": head["chunks"],
+            "engine_trial_ms": head["trial"],
         },
         "tflops_per_gpu": round(value * mflops / world / 1e12, 2),
         "mfu_vs_2.5pf_dense_bf16": round(value * mflops / world / 2.5e15, 4),
-        "final_loss": round(final_loss, 4),
+        "final_loss": round(head["final_loss"], 4),
     }
+    if world > 1:
+        out["layouts"] = [{"parallelism": L["parallelism"], "value": round(L["value"], 1),
+                           "ms_per_step": round(1000 * L["elapsed"] / a.steps, 3),
+                           "vs_baseline": round(L["value"] / (base * world), 4) if base else None,
+                           "tp_comm": L["tp_comm"], "chunks": L["chunks"], "engine_trial_ms": L["trial"]}
+                          for L in layouts]
+        pure = [L for L in out["layouts"] if L["parallelism"].split("+")[0] == f"tp{world}"]
+        out["tp_pure"] = pure[0] if pure else None
     if rank == 0:
         print(json.dumps(out), flush=True)
         if os.environ.get("DPFS_SHOW_GEMM") == "1":     # per-shape ours/hipBLASLt choices (ms)

@@ -117,6 +117,8 @@ def train(rank, args: Namespace):
 
     seq_len = args.seq_len or margs.maxlen
     if args.synthetic:
+        from .parallel import tp_comm
+        tp_comm.set_fixed_shapes(True)   # every rank's batches have the same shape
         loader = get_synthetic_dataloader(margs.vocab_size, seq_len, args.batch_size,
                                           seed=args.random_seed + 17 * p.dp_rank)
     else:

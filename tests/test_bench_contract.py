@@ -43,7 +43,10 @@ def test_bench_prints_one_json_line(world, warmup):
     assert d["n_gpus"] == world and d["steps"] == 2 and d["warmup"] == warmup and d["scaling"] == "weak"
     assert d["config"]["parallelism"] in (f"tp{world}", f"tp{world}+sp") and d["config"]["global_batch"] == 2 * world
     if warmup >= 4:
-        assert set(d["config"]["engine_trial_ms"]) == {"nosp/c2", "sp/c2"}
+        assert set(d["config"]["engine_trial_ms"]) == {"sp/c2", "sp/c1"}
+    if world > 1:   # pure TP is the headline here (plumbing: TP = N): one layout, labelled
+        assert [L["parallelism"].split("+")[0] for L in d["layouts"]] == [f"tp{world}"]
+        assert d["tp_pure"]["value"] == d["value"]
     assert d["value"] > 0 and d["higher_is_better"] is True
 
 
@@ -72,6 +75,11 @@ def test_bench_tp_dp_layout():
     (d,) = _json_lines(r.stdout)
     assert d["config"]["parallelism"] in ("tp2dp2", "tp2dp2+sp") and d["config"]["global_batch"] == 8
     assert d["n_gpus"] == 4 and d["value"] > 0
+    # the pure-TP layout (the reference's tp_size == world_size) is measured and labelled too
+    labels = [L["parallelism"].split("+")[0] for L in d["layouts"]]
+    assert labels == ["tp2dp2", "tp4"], labels
+    assert d["tp_pure"]["parallelism"].startswith("tp4") and d["tp_pure"]["value"] > 0
+    assert d["tp_pure"]["ms_per_step"] > 0
 
 
 def test_resolve_tp():
