@@ -21,7 +21,11 @@ long long dpfs_gemm_tn_ws(int, int, int, int);
 void dpfs_gemm_set_impl(int);
 int dpfs_gemm_rope_fusable(int, int, int, int);
 void dpfs_gemm_nt_rope(const void*, const void*, void*, const float*, int, int, int, int, int, int, const int64_t*,
-                       const float*, int, hipStream_t);
+                       const float*, int, int, hipStream_t);
+void dpfs_gemm_v4_mask(int);
+void dpfs_gemm4_sched(int);
+void dpfs_gemm4_ablate(int);
+int dpfs_gemm_v4_get_mask();
 void dpfs_gemm_force(int, int);
 void dpfs_gemm_v2_sched(int);
 void dpfs_gemm_set_workspace(float*, long long);
@@ -189,7 +193,7 @@ torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
                 "gemm_nt: rope_tab must be fp32 [maxlen, hd]");
     dpfs_gemm_nt_rope(a.data_ptr(), b.data_ptr(), c.data_ptr(), opt_f32(bias, N, "bias"), (int)M, (int)N, (int)K,
                       (int)a.stride(0), (int)b.stride(0), (int)N, rope_pos->data_ptr<int64_t>(),
-                      rope_tab->data_ptr<float>(), (int)(rope_heads * rope_hd), stream());
+                      rope_tab->data_ptr<float>(), (int)(rope_heads * rope_hd), (int)rope_hd, stream());
   } else {
     dpfs_gemm_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), opt_f32(bias, N, "bias"), (int)M, (int)N, (int)K,
                  (int)a.stride(0), (int)b.stride(0), (int)N, stream());
@@ -1062,6 +1066,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nn", &gemm_nn, py::arg("a"), py::arg("b"), py::arg("out") = py::none());
   m.def("gemm_force", [](int cfg, int splits) { dpfs_gemm_force(cfg, splits); },
         "force the v2 tile config (-1 auto, 0 = 256x256, 1 = 256x128) and K-splits (0 auto)");
+  m.def("gemm_v4_mask", [](int v) { dpfs_gemm_v4_mask(v); },
+        "layouts on the v4 kernel (one wave per SIMD, 128x128 per wave): bit 1 NT, 2 NN, 4 TN; 0 = all on v3");
+  m.def("gemm_v4_get_mask", []() { return dpfs_gemm_v4_get_mask(); });
+  m.def("gemm4_ablate", [](int v) { dpfs_gemm4_ablate(v); }, "timing-only: 1 = drop stores, 2 = zero operands");
+  m.def("gemm4_sched", [](int v) { dpfs_gemm4_sched(v); },
+        "v4 main-loop schedule: 0 compiler order, 1 = 8 chunks (DMA piece + 2 fragment reads + 8 MFMAs), "
+        "2 = MFMA pairs interleaved with single reads / DMA pieces (precomputed DMA offsets)");
   m.def("gemm_v2_sched", [](int v) { dpfs_gemm_v2_sched(v); }, "v2 256x256 schedule (-1 per-layout default, 0..4 see gemm2_k SCHED)");
   m.def("gemm_set_impl", [](int v) { dpfs_gemm_set_impl(v); }, "1 = v1 (128x128 register-staged), 2 = v2 (LDS-DMA, one tile per workgroup), 3 = v3 (persistent v2, default)");
   m.def("gemm_tn2", &gemm_tn2, "fp32 c (+)= a0^T b0 + a1^T b1 (reduction dim over two buffers), one split-K launch; None if the plan does not fit",

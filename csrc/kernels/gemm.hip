@@ -306,6 +306,7 @@ struct RopeArgs {
   const int64_t* pos;
   const float* tab;
   int cols;
+  int hd = 64;
 };
 
 template <int PIECES, int NSTAGE>
@@ -901,8 +902,21 @@ extern "C" void dpfs_gemm_set_workspace(float* ws, long long n) {
 extern "C" void dpfs_rope(int dtype, void* qkv, const int64_t* pos, const float* table, int M, int ld, int n_heads,
                           int hd, int inverse, hipStream_t s);
 static void dpfs_rope_after_gemm(void* C, RopeArgs r, int M, int ldc, hipStream_t s) {
-  dpfs_rope(1, C, r.pos, r.tab, M, ldc, r.cols / 64, 64, 0, s);
+  dpfs_rope(1, C, r.pos, r.tab, M, ldc, r.cols / r.hd, r.hd, 0, s);
 }
+
+// v4 (csrc/kernels/gemm4.hip: one wave per SIMD, 128 x 128 per wave).  Bit mask of the
+// layouts it carries: 1 = NT, 2 = NN, 4 = TN (fp32 split-K).  Where the launcher declines a
+// shape (32-bit spans, alignment) the v3 kernel runs.
+extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const void* B, void* C, const float* bias,
+                                  int M, int N, int K, int lda, int ldb, int ldc, int kps, int splits,
+                                  long long slab_stride, unsigned a_bytes, unsigned b_bytes, const int64_t* rope_pos,
+                                  const float* rope_tab, int rope_cols, int rope_hd, const void* A2, const void* B2,
+                                  int k_switch, int lda2, int ldb2, unsigned a2_bytes, unsigned b2_bytes,
+                                  hipStream_t s);
+static int g_v4_mask = 3;
+extern "C" void dpfs_gemm_v4_mask(int m) { g_v4_mask = m; }
+extern "C" int dpfs_gemm_v4_get_mask() { return g_v4_mask; }
 
 extern "C" long long dpfs_gemm_bf16_ws(int M, int N, int K) {
   const int S = bf16_splits(M, N, K);
@@ -913,17 +927,30 @@ template <bool BKM>
 static void bf16_gemm(const void* A, const void* B, void* C, const float* bias, int M, int N, int K, int lda, int ldb,
                       int ldc, unsigned ab, unsigned bb, hipStream_t s, RopeArgs rope = RopeArgs{nullptr, nullptr, 0}) {
   const int S = bf16_splits(M, N, K);
+  const bool v4 = g_gemm_impl >= 3 && (g_v4_mask & (BKM ? 1 : 2)) != 0;
+  const int lay = BKM ? 0 : 1;
   if (S > 1 && g_ws && g_ws_floats >= (long long)S * M * N) {
     int kps = (K + S - 1) / S;
     kps = ((kps + BKK - 1) / BKK) * BKK;
-    if (g_gemm_impl != 3 || !launchp<true, BKM, 1>(pick_cfg(M, N, S), A, B, g_ws, nullptr, M, N, K, lda, ldb, N, S,
-                                                    kps, (long long)M * N, ab, bb, s))
+    const bool done4 = v4 && dpfs_gemm4_launch(lay, 1, A, B, g_ws, nullptr, M, N, K, lda, ldb, N, kps, S,
+                                               (long long)M * N, ab, bb, nullptr, nullptr, 0, 64, nullptr, nullptr, 0,
+                                               0, 0, 0u, 0u, s);
+    if (!done4 && (g_gemm_impl != 3 || !launchp<true, BKM, 1>(pick_cfg(M, N, S), A, B, g_ws, nullptr, M, N, K, lda,
+                                                               ldb, N, S, kps, (long long)M * N, ab, bb, s)))
       launch2<true, BKM, 1>(pick_cfg(M, N, S), A, B, g_ws, nullptr, M, N, K, lda, ldb, N, S, kps, (long long)M * N, ab,
                             bb, s);
     long long g = ((long long)M * N / 4 + 255) / 256;
     if (g > 4096) g = 4096;
     splitk_reduce_bf16_k<<<(int)g, 256, 0, s>>>(g_ws, (bf16*)C, bias, M, N, ldc, S);
     if (rope.cols > 0) dpfs_rope_after_gemm(C, rope, M, ldc, s);
+    return;
+  }
+  if (v4 && dpfs_gemm4_launch(lay, 0, A, B, C, bias, M, N, K, lda, ldb, ldc, ((K + 31) / 32) * 32, 1, 0, ab, bb,
+                               rope.pos, rope.tab, rope.cols, rope.hd, nullptr, nullptr, 0, 0, 0, 0u, 0u, s))
+    return;
+  if (rope.cols > 0 && rope.hd != 64) {   // v3's epilogue rotates 64-wide heads only
+    bf16_gemm<BKM>(A, B, C, bias, M, N, K, lda, ldb, ldc, ab, bb, s);
+    dpfs_rope_after_gemm(C, rope, M, ldc, s);
     return;
   }
   if (g_gemm_impl == 3 && launchp<true, BKM, 0>(pick_cfg(M, N, 1), A, B, C, bias, M, N, K, lda, ldb, ldc, 1, K, 0, ab,
@@ -935,14 +962,16 @@ static void bf16_gemm(const void* A, const void* B, void* C, const float* bias, 
 // Whether dpfs_gemm_nt_rope fuses the rotation into the GEMM epilogue (hd 64; otherwise it
 // runs the separate RoPE kernel after the GEMM — same result).
 extern "C" int dpfs_gemm_rope_fusable(int M, int N, int K, int hd) {
-  return g_gemm_impl != 1 && hd == 64 && N % 64 == 0;
+  if (g_gemm_impl == 1) return 0;
+  if (hd == 64) return N % 64 == 0;
+  return hd == 128 && (g_v4_mask & 1) && N % 128 == 0;
 }
 
 extern "C" void dpfs_gemm_nt_rope(const void* A, const void* B, void* C, const float* bias, int M, int N, int K,
                                   int lda, int ldb, int ldc, const int64_t* pos, const float* tab, int rope_cols,
-                                  hipStream_t s) {
+                                  int rope_hd, hipStream_t s) {
   bf16_gemm<true>(A, B, C, bias, M, N, K, lda, ldb, ldc, span_bytes(M, lda, K), span_bytes(N, ldb, K), s,
-                  RopeArgs{pos, tab, rope_cols});
+                  RopeArgs{pos, tab, rope_cols, rope_hd});
 }
 
 // NT: C[M,N] bf16 = A[M,K] B[N,K]^T (+ bias)
@@ -1058,6 +1087,23 @@ extern "C" void dpfs_gemm_tn(const void* A, const void* B, float* C, float* ws, 
   kps = ((kps + BKK - 1) / BKK) * BKK;
   const bool direct = (S == 1 && !accumulate);
   float* dst = direct ? C : ws;
+  if ((g_v4_mask & 4) && g_gemm_impl >= 3) {
+    const int S4 = g_force_splits > 0 ? g_force_splits : tn_v2_splits(M, N, K);
+    if (S4 == S || (S4 < S)) {   // v4 plans with 256 x 256 tiles; its split count never needs more slabs
+      int kps4 = (K + S4 - 1) / S4;
+      kps4 = ((kps4 + BKK - 1) / BKK) * BKK;
+      const bool direct4 = (S4 == 1 && !accumulate);
+      if (dpfs_gemm4_launch(2, 1, A, B, direct4 ? C : ws, nullptr, M, N, K, lda, ldb, N, direct4 ? ((K + 31) / 32) * 32 : kps4,
+                            S4, direct4 ? 0 : n, span_bytes(K, lda, M), span_bytes(K, ldb, N), nullptr, nullptr, 0, 64,
+                            nullptr, nullptr, 0, 0, 0, 0u, 0u, s)) {
+        if (direct4) return;
+        long long g = (n / 4 + 255) / 256;
+        if (g > 4096) g = 4096;
+        splitk_reduce_k<<<(int)g, 256, 0, s>>>(ws, C, n, S4, accumulate);
+        return;
+      }
+    }
+  }
   if (tn_use_v1(M, N, K)) {
     gemm_k<false, false, 1><<<dim3(tiles_of(M, N), S), 256, 0, s>>>((const bf16*)A, (const bf16*)B, dst, nullptr, M,
                                                                    N, K, lda, ldb, N, direct ? K : kps,
@@ -1124,7 +1170,11 @@ extern "C" int dpfs_gemm_tn2(const void* A0, const void* B0, const void* A1, con
   const int K = K0 + K1;
   const long long n = (long long)M * N;
   const Dual d = {(const bf16*)A1, (const bf16*)B1, K0, lda1, ldb1, span_bytes(K1, lda1, M), span_bytes(K1, ldb1, N)};
-  if (!launchp<false, false, 1>(cfg, A0, B0, ws, nullptr, M, N, K, lda0, ldb0, N, S, kps, n, span_bytes(K0, lda0, M),
+  const bool done4 = (g_v4_mask & 4) &&
+                     dpfs_gemm4_launch(2, 1, A0, B0, ws, nullptr, M, N, K, lda0, ldb0, N, kps, S, n,
+                                       span_bytes(K0, lda0, M), span_bytes(K0, ldb0, N), nullptr, nullptr, 0, 64, A1,
+                                       B1, K0, lda1, ldb1, d.a2_bytes, d.b2_bytes, s);
+  if (!done4 && !launchp<false, false, 1>(cfg, A0, B0, ws, nullptr, M, N, K, lda0, ldb0, N, S, kps, n, span_bytes(K0, lda0, M),
                                 span_bytes(K0, ldb0, N), s, RopeArgs{nullptr, nullptr, 0}, d))
     return 0;
   long long g = (n / 4 + 255) / 256;

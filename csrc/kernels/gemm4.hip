@@ -1,0 +1,612 @@
+// bf16 MFMA GEMM v4 for gfx950 (MI355X): one wave per SIMD, 128 x 128 outputs per wave.
+//
+//   C[m][n] = sum_k A(m,k) B(k,n), fp32 accumulation in the accumulator (AGPR) file.
+//   Layouts as gemm.hip: NT forward (F.linear, reference models/layers.py:49,93), NN dgrad,
+//   TN wgrad (fp32 split-K slabs).
+//
+// Why a new main loop (the v3 kernel in gemm.hip runs 8 waves, 2 per SIMD, 128 x 64 each):
+//  * 128 x 128 per wave halves the LDS bytes read per MFMA (16 ds_read_b128 per 64
+//    v_mfma_f32_16x16x32_bf16 = 0.25, v3 0.375) and one wave per SIMD leaves each SIMD's
+//    matrix pipe to one instruction stream (no partner wave's MFMAs in the way).  The 256
+//    fp32 accumulators per lane live in AGPRs; operand fragments, addresses and the epilogue
+//    in the 256 arch VGPRs (512-register budget at one wave per SIMD, no spills).
+//  * The K loop walks 32-deep steps through a 4-slot LDS ring (32 KiB per slot: A and B
+//    256 x 32 bf16 each).  Step s multiplies fragments already in registers, reads the next
+//    step's fragments (one step of register prefetch, so no LDS latency is exposed at a
+//    step boundary) and issues the LDS-DMA of step s + 3: each DMA has two full steps
+//    (~2 x 64 MFMAs) to land.  One barrier per step; counted `s_waitcnt vmcnt` (never 0 in
+//    the loop).
+//  * Persistent: one 256-thread workgroup per CU walks (split, tile) items in grouped,
+//    XCD-contiguous order; the DMA stream continues across item boundaries, so the next
+//    item's first three steps are in flight while an item's epilogue runs.  Past the last
+//    item the producer issues out-of-range DMAs (zeros into dead slots) so every wait count
+//    stays static.
+//  * Epilogue: bias (+ RoPE for the QKV projection, head_dim 64 or 128: the rotation
+//    partner of column d is d + hd/2, the same lane's tile j + hd/32) in fp32, bf16 packed
+//    into a wave-private 8 KiB LDS staging area (XOR-swizzled, conflict-free ds_write_b64),
+//    read back by rows and written as 16-byte buffer stores covering whole 128-byte lines
+//    (the v3 epilogue's 8-byte stores touched 16 partial lines per instruction).
+//    Out-of-range rows / columns get an offset past the descriptor (dropped by hardware).
+//  * LDS images: K-contiguous operands [256 rows][64 B] with the 16-byte chunk of row r at
+//    slot c ^ h(r), h(r) = (-(r >> 2)) & 3: every ds_read_b128 lane group covers the 16 bank
+//    slots exactly once.  MN-contiguous operands [32 k][256] as gemm.hip (read with the
+//    ds_read_b64_tr_b16 hardware transpose).  The swizzle is applied on the DMA SOURCE
+//    address (LDS-DMA writes lane-linear 1 KiB pieces).
+#include "common.h"
+
+#include <algorithm>
+#include <type_traits>
+
+namespace dpfs {
+namespace g4 {
+
+constexpr int SLOT = 32768;          // one ring slot: A (16 KiB) + B (16 KiB)
+constexpr int RING = 4 * SLOT;       // 128 KiB
+constexpr int STG = 8192;            // epilogue staging per wave
+constexpr int LDS_TOTAL = RING + 4 * STG;   // 160 KiB
+
+__device__ __forceinline__ int kh(int r) { return (4 - ((r >> 2) & 3)) & 3; }
+__device__ __forceinline__ int mnh(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+
+
+struct Rope {
+  const int64_t* pos;
+  const float* tab;   // [maxlen][hd] = [cos(0..hd/2) | sin(0..hd/2)]
+  int cols;           // rotate output columns < cols (q and k heads)
+  int hd;             // 64 or 128
+};
+
+struct Dual {
+  const bf16* A2;
+  const bf16* B2;
+  int k_switch, lda2, ldb2;
+  unsigned a2_bytes, b2_bytes;
+};
+
+// One operand's half of a ring slot (16 KiB): 16 pieces of 1 KiB, 4 per wave.
+template <bool KMAJ>
+__device__ __forceinline__ void issue_half(__amdgpu_buffer_rsrc_t rs, char* dst, int r0, int k0, int ke, int ld,
+                                           int wave, int l) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = wave + 4 * i;
+    unsigned off;
+    if (KMAJ) {
+      const int row = 16 * j + (l >> 2);
+      const int c = (l & 3) ^ kh(row);
+      const int k = k0 + 8 * c;
+      off = (k < ke) ? (unsigned)(((long long)(r0 + row) * ld + k) * 2) : kOOB;
+    } else {
+      const int lin = j * 64 + l;
+      const int row = lin >> 5;
+      const int c = (lin & 31) ^ (mnh(row) << 1);
+      const int k = k0 + row;
+      off = (k < ke) ? (unsigned)(((long long)k * ld + r0 + 8 * c) * 2) : kOOB;
+    }
+    dma16(rs, dst + j * 1024, off);
+  }
+}
+
+// Piece i (< 4) of issue_half, for schedules that spread the pieces between MFMAs.
+template <bool KMAJ>
+__device__ __forceinline__ void issue_piece(__amdgpu_buffer_rsrc_t rs, char* dst, int r0, int k0, int ke, int ld,
+                                            int wave, int l, int i) {
+  const int j = wave + 4 * i;
+  unsigned off;
+  if (KMAJ) {
+    const int row = 16 * j + (l >> 2);
+    const int c = (l & 3) ^ kh(row);
+    const int k = k0 + 8 * c;
+    off = (k < ke) ? (unsigned)(((long long)(r0 + row) * ld + k) * 2) : kOOB;
+  } else {
+    const int lin = j * 64 + l;
+    const int row = lin >> 5;
+    const int c = (lin & 31) ^ (mnh(row) << 1);
+    const int k = k0 + row;
+    off = (k < ke) ? (unsigned)(((long long)k * ld + r0 + 8 * c) * 2) : kOOB;
+  }
+  dma16(rs, dst + j * 1024, off);
+}
+
+// Fragment of the 16x16x32 MFMA operand: lane l holds X[rb + (l&15)][8(l>>4) + e], e < 8.
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8 frag(const char* half, int rb, int l) {
+  if (KMAJ) {
+    const int row = rb + (l & 15);
+    const int c = l >> 4;
+    return *reinterpret_cast<const bf16x8*>(half + row * 64 + ((c ^ kh(row)) << 4));
+  } else {
+    const int i = l & 15, q = i >> 2, p = i & 3;
+    const int chunk = (rb + 4 * p) >> 3;
+    const int k_lo = 8 * (l >> 4) + q;
+    const int k_hi = k_lo + 4;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(half + k_lo * 512 + ((chunk ^ (mnh(k_lo) << 1)) << 4) + (p & 1) * 8));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(half + k_hi * 512 + ((chunk ^ (mnh(k_hi) << 1)) << 4) + (p & 1) * 8));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+// MN-major fragment halves through inline asm: hipcc puts `s_waitcnt vmcnt(0)` in front of
+// the ds_read_b64_tr_b16 builtin whenever an LDS-DMA is in flight (it cannot tell the DMA's
+// LDS destination from the read's), which would drain the ring at every read.  The asm form
+// is invisible to that bookkeeping; Opnd::pin retires the reads with one `s_waitcnt
+// lgkmcnt(0)` naming every destination "+v" before any use (guide §5.7 item 1, form (ii)).
+__device__ __forceinline__ s16x4 ds_tr16(const char* p) {
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"((unsigned)(size_t)((__attribute__((address_space(3))) const char*)p)));
+  return r;
+}
+
+template <bool KMAJ>
+struct Opnd;
+template <>
+struct Opnd<true> {
+  bf16x8 v[8];
+  __device__ __forceinline__ void load(int i, const char* half, int rb, int l) { v[i] = frag<true>(half, rb, l); }
+  __device__ __forceinline__ bf16x8 get(int i) const { return v[i]; }
+  __device__ __forceinline__ void pin() {}
+};
+template <>
+struct Opnd<false> {
+  s16x4 lo[8], hi[8];
+  __device__ __forceinline__ void load(int i, const char* half, int rb, int l) {
+    const int ii = l & 15, q = ii >> 2, p = ii & 3;
+    const int chunk = (rb + 4 * p) >> 3;
+    const int k_lo = 8 * (l >> 4) + q;
+    const int k_hi = k_lo + 4;
+    lo[i] = ds_tr16(half + k_lo * 512 + ((chunk ^ (mnh(k_lo) << 1)) << 4) + (p & 1) * 8);
+    hi[i] = ds_tr16(half + k_hi * 512 + ((chunk ^ (mnh(k_hi) << 1)) << 4) + (p & 1) * 8);
+  }
+  __device__ __forceinline__ bf16x8 get(int i) const {
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    s16x8 v = {lo[i][0], lo[i][1], lo[i][2], lo[i][3], hi[i][0], hi[i][1], hi[i][2], hi[i][3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+  __device__ __forceinline__ void pin() {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]), "+v"(lo[3]), "+v"(lo[4]), "+v"(lo[5]), "+v"(lo[6]),
+                   "+v"(lo[7]));
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(hi[0]), "+v"(hi[1]), "+v"(hi[2]), "+v"(hi[3]), "+v"(hi[4]), "+v"(hi[5]), "+v"(hi[6]),
+                   "+v"(hi[7]));
+  }
+};
+
+template <bool AK, bool BKM>
+struct Frags {
+  Opnd<AK> a;
+  Opnd<BKM> b;
+};
+
+template <bool AK, bool BKM>
+__device__ __forceinline__ void read_frags(Frags<AK, BKM>& f, const char* slot, int wm, int wn, int l) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f.a.load(i, slot, wm * 128 + 16 * i, l);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f.b.load(j, slot + 16384, wn * 128 + 16 * j, l);
+}
+
+template <bool ZERO, bool AK, bool BKM>
+__device__ __forceinline__ void mma(f32x4 (&acc)[8][8], const Frags<AK, BKM>& f) {
+  // (no s_setprio: one wave per SIMD has no partner to arbitrate against, and the builtin
+  // would fence the MFMAs off from the interleaved loads)
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.b.get(j), f.a.get(i), ZERO ? z : acc[i][j], 0, 0, 0);
+}
+
+// Work item -> tile origin and K range (grouped order as gemm.hip's gemmp_k).
+struct Item {
+  int m0, n0, kb, ke, split, sel;
+};
+
+__device__ __forceinline__ Item decode(int lin, int nwg, int tiles_m, int tiles_n, int group_m, int K, int kps,
+                                       int k_switch) {
+  Item it;
+  it.split = lin / nwg;
+  const int wg = lin - it.split * nwg;
+  const int per_group = group_m * tiles_n;
+  const int gid = wg / per_group;
+  const int first_m = gid * group_m;
+  const int gsz = min(tiles_m - first_m, group_m);
+  const int r = wg - gid * per_group;
+  it.m0 = (first_m + r % gsz) * 256;
+  it.n0 = (r / gsz) * 256;
+  it.kb = it.split * kps;
+  it.ke = min(K, it.kb + kps);
+  it.sel = 0;
+  if (it.kb >= k_switch) {
+    it.sel = 1;
+    it.kb -= k_switch;
+    it.ke -= k_switch;
+  }
+  return it;
+}
+
+__device__ __forceinline__ int nsteps(const Item& it) {
+  const int n = max(1, (it.ke - it.kb + 31) / 32);
+  return (n + 1) & ~1;
+}
+
+// Epilogue of one item.  OUT 0: bias (+ RoPE) in fp32, bf16 through the wave's LDS staging
+// area, 16-byte row stores; OUT 1: fp32 16-byte stores of each lane's 4 columns.
+// Exactly STORES (32 / 64) buffer stores per wave (out-of-range lanes get an offset past the
+// descriptor), which the next item's first wait counts.
+template <int OUT>
+__device__ __forceinline__ void epilogue(f32x4 (&acc)[8][8], const Item& ci, void* C, const float* bias,
+                                         const Rope& rope, int M, int N, int ldc, long long slab_stride,
+                                         unsigned c_bytes, char* stg, int wm, int wn, int l) {
+  const int g = l >> 4;
+  const int wcol0 = ci.n0 + wn * 128;
+  if constexpr (OUT == 0) {
+    f32x4 bv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = wcol0 + 16 * j + 4 * g;
+      bv[j] = (bias && n < N) ? *reinterpret_cast<const f32x4*>(bias + n) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    const bool do_rope = rope.cols > 0 && wcol0 < rope.cols;
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(C, (short)0, (int)c_bytes, 0x00020000);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        __builtin_amdgcn_sched_barrier(0);
+        const int i = 2 * r + ii;
+        f32x4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = acc[i][j] + bv[j];
+        if (do_rope) {
+          const int m = ci.m0 + wm * 128 + 16 * i + (l & 15);
+          const float* tr = rope.tab + (m < M ? rope.pos[m] : 0) * rope.hd;
+          const int half = rope.hd >> 1;
+          const int hj = half >> 4;   // tiles per half head: 2 (hd 64) or 4 (hd 128)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int jh = j % (2 * hj);
+            if (jh < hj && wcol0 + 16 * j < rope.cols) {
+              const f32x4 cs = *reinterpret_cast<const f32x4*>(tr + 16 * jh + 4 * g);
+              const f32x4 sn = *reinterpret_cast<const f32x4*>(tr + half + 16 * jh + 4 * g);
+              const f32x4 x1 = v[j], x2 = v[j + hj];
+              v[j] = x1 * cs - x2 * sn;
+              v[j + hj] = x2 * cs + x1 * sn;
+            }
+          }
+        }
+        const int row = 16 * ii + (l & 15);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          bf16x4 o = {(bf16)v[j][0], (bf16)v[j][1], (bf16)v[j][2], (bf16)v[j][3]};
+          const int u = (4 * j + g) ^ (row & 15);
+          *reinterpret_cast<u32x2*>(stg + row * 256 + u * 8) = __builtin_bit_cast(u32x2, o);
+        }
+      }
+      // read back whole rows: lane L -> row 4q + (L>>4), 16-byte chunk L&15
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int row = 4 * q + (l >> 4);
+        const int c = l & 15;
+        u32x4 w = *reinterpret_cast<const u32x4*>(stg + row * 256 + ((c ^ ((row >> 1) & 7)) << 4));
+        if (row & 1) w = (u32x4){w[2], w[3], w[0], w[1]};
+        const int m = ci.m0 + wm * 128 + 32 * r + row;
+        const int n = wcol0 + 8 * c;
+        const bool ok = m < M && n < N;
+        const unsigned off = ok ? (unsigned)(((long long)m * ldc + n) * 2) : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b128(w, rc, off, 0, 0);
+      }
+    }
+  } else {
+    char* cbase = reinterpret_cast<char*>(C) + (long long)ci.split * slab_stride * 4;
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)cbase, (short)0, (int)c_bytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = ci.m0 + wm * 128 + 16 * i + (l & 15);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int n = wcol0 + 16 * j + 4 * g;
+        const bool ok = m < M && n < N;
+        const unsigned off = ok ? (unsigned)(((long long)m * ldc + n) * 4) : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rc, off, 0, 0);
+      }
+    }
+  }
+}
+
+// OUT: 0 = bf16 C (+ fp32 bias[n], + RoPE); 1 = fp32 C / split-K slab.
+template <bool AK, bool BKM, int OUT, int SCHED>
+__global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                  void* __restrict__ C, const float* __restrict__ bias, int M, int N,
+                                                  int K, int lda, int ldb, int ldc, int kps, int splits,
+                                                  long long slab_stride, unsigned a_bytes, unsigned b_bytes,
+                                                  unsigned c_bytes, Rope rope, int group_m, Dual dual) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_TOTAL];
+  constexpr int STORES = OUT == 0 ? 32 : 64;   // store instructions per wave per item
+
+  const int tiles_n = (N + 255) / 256;
+  const int tiles_m = (M + 255) / 256;
+  const int nwg = tiles_m * tiles_n;
+  const int total = nwg * splits;
+  const int G = gridDim.x;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int l = lane_id();
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (int)b_bytes, 0x00020000);
+  const bool dual_on = dual.A2 != nullptr;
+  const __amdgpu_buffer_rsrc_t ra2 =
+      dual_on ? __builtin_amdgcn_make_buffer_rsrc((void*)dual.A2, (short)0, (int)dual.a2_bytes, 0x00020000) : ra;
+  const __amdgpu_buffer_rsrc_t rb2 =
+      dual_on ? __builtin_amdgcn_make_buffer_rsrc((void*)dual.B2, (short)0, (int)dual.b2_bytes, 0x00020000) : rb;
+  const int lda2 = dual_on ? dual.lda2 : lda, ldb2 = dual_on ? dual.ldb2 : ldb;
+
+  int it = xcd_remap(blockIdx.x, G);
+  if (it >= total) return;
+
+  // ---- producer cursor: the DMA stream runs 3 steps ahead of the consumer, across items.
+  // Every item takes an EVEN number of 32-deep steps (a trailing all-zero step when the K
+  // range is an odd number of steps) so the two fragment register sets alternate statically.
+  int p_it = it;
+  Item pi = decode(p_it, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
+  int p_t = 0, p_nk = nsteps(pi);
+  int p_slot = 0;
+  // DMA of the producer's current stage (no branches: kept in the step's scheduling region).
+  auto issue_stage = [&]() {
+    char* dst = smem + p_slot * SLOT;
+    const bool live = p_it < total;
+    const int ke = live ? pi.ke : 0;    // dead stream: every offset out of range -> zeros
+    const int k0 = pi.kb + 32 * p_t;
+    const bool s2 = pi.sel != 0;
+    issue_half<AK>(s2 ? ra2 : ra, dst, pi.m0, k0, ke, s2 ? lda2 : lda, wave, l);
+    issue_half<BKM>(s2 ? rb2 : rb, dst + 16384, pi.n0, k0, ke, s2 ? ldb2 : ldb, wave, l);
+    p_slot = (p_slot + 1) & 3;
+  };
+  // Per-item lane offsets of the wave's 8 DMA pieces (SCHED 2): a step then adds one
+  // uniform term per operand and checks the K bound against a lane constant.
+  unsigned pbase[8];
+  auto rebase = [&]() {
+    const bool s2 = pi.sel != 0;
+    const int la = s2 ? lda2 : lda, lb = s2 ? ldb2 : ldb;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const bool isA = q < 4;
+      const bool km = isA ? AK : BKM;
+      const int j = wave + 4 * (q & 3);
+      const int r0 = isA ? pi.m0 : pi.n0;
+      const int ld = isA ? la : lb;
+      if (km) {
+        const int row = 16 * j + (l >> 2);
+        const int c = (l & 3) ^ kh(row);
+        pbase[q] = (unsigned)(((long long)(r0 + row) * ld + 8 * c) * 2);
+      } else {
+        const int lin = j * 64 + l;
+        const int row = lin >> 5;
+        const int c = (lin & 31) ^ (mnh(row) << 1);
+        pbase[q] = (unsigned)(((long long)row * ld + r0 + 8 * c) * 2);
+      }
+    }
+  };
+  // lane constant compared with (ke - k0): the k offset of the lane's 16 bytes in the step
+  auto kpos = [&](int q) -> int {
+    const bool km = q < 4 ? AK : BKM;
+    const int j = wave + 4 * (q & 3);
+    if (km) {
+      const int row = 16 * j + (l >> 2);
+      return 8 * ((l & 3) ^ kh(row));
+    }
+    return (j * 64 + l) >> 5;
+  };
+  if constexpr (SCHED == 2) rebase();
+  auto advance = [&]() {
+    if (p_it < total && ++p_t == p_nk) {
+      p_it += G;
+      p_t = 0;
+      if (p_it < total) {
+        pi = decode(p_it, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
+        p_nk = nsteps(pi);
+        if constexpr (SCHED == 2) rebase();
+      }
+    }
+  };
+  auto produce = [&]() {
+    issue_stage();
+    advance();
+  };
+  produce();
+  produce();
+  produce();
+
+  Frags<AK, BKM> F0, F1;
+  f32x4 acc[8][8];
+  int c_slot = 0;
+  // fragments of the first step: stage 0 landed (two younger stages of 8 pieces in flight)
+  wait_vmcnt<16>();
+  __builtin_amdgcn_s_barrier();
+  read_frags<AK, BKM>(F0, smem, wm, wn, l);
+
+  // One consumer step on `cur`, prefetching the next step's fragments into `nxt`.
+  // Entry wait: stage s+1 landed for this wave (younger: stage s+2 = 8 pieces, plus the
+  // previous item's epilogue stores on an item's first step), then the step barrier.
+  auto step = [&](Frags<AK, BKM>& cur, Frags<AK, BKM>& nxt, bool first, auto zero) {
+    // `cur` was read a whole step ago: retire it here so the MFMAs below need no LDS wait
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+    cur.a.pin();
+    cur.b.pin();
+    if (first) wait_vmcnt<(8 + STORES < 63 ? 8 + STORES : 63)>();
+    else wait_vmcnt<8>();
+    __builtin_amdgcn_s_barrier();
+    c_slot = (c_slot + 1) & 3;
+    if constexpr (SCHED == 0) {
+      issue_stage();
+      read_frags<AK, BKM>(nxt, smem + c_slot * SLOT, wm, wn, l);
+      mma<decltype(zero)::value, AK, BKM>(acc, cur);
+    } else if constexpr (SCHED == 1) {
+      // 8 chunks in fixed program order: one DMA piece and the next step's A / B fragment
+      // q, then the 8 MFMAs of accumulator row q (row q's A fragment is dead after them)
+      char* dst = smem + p_slot * SLOT;
+      const bool live = p_it < total;
+      const int ke = live ? pi.ke : 0;
+      const int k0 = pi.kb + 32 * p_t;
+      const bool s2 = pi.sel != 0;
+      const char* src = smem + c_slot * SLOT;
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (q < 4) issue_piece<AK>(s2 ? ra2 : ra, dst, pi.m0, k0, ke, s2 ? lda2 : lda, wave, l, q);
+        else issue_piece<BKM>(s2 ? rb2 : rb, dst + 16384, pi.n0, k0, ke, s2 ? ldb2 : ldb, wave, l, q - 4);
+        nxt.a.load(q, src, wm * 128 + 16 * q, l);
+        nxt.b.load(q, src + 16384, wn * 128 + 16 * q, l);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[q][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.b.get(j), cur.a.get(q), decltype(zero)::value ? z : acc[q][j],
+                                                              0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      p_slot = (p_slot + 1) & 3;
+    } else {
+      // finer interleave: pairs of MFMAs with one fragment read or one DMA piece between
+      char* dst = smem + p_slot * SLOT;
+      const bool live = p_it < total;
+      const int krem = (live ? pi.ke : 0) - (pi.kb + 32 * p_t);   // valid k in this step
+      const int k0 = pi.kb + 32 * p_t;
+      const bool s2 = pi.sel != 0;
+      const unsigned addA = AK ? (unsigned)(k0 * 2) : (unsigned)((long long)k0 * (s2 ? lda2 : lda) * 2);
+      const unsigned addB = BKM ? (unsigned)(k0 * 2) : (unsigned)((long long)k0 * (s2 ? ldb2 : ldb) * 2);
+      const char* src = smem + c_slot * SLOT;
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      constexpr bool ZR = decltype(zero)::value;
+#define DPFS_G4_MM(j_) acc[q][j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.b.get(j_), cur.a.get(q), ZR ? z : acc[q][j_], 0, 0, 0)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        DPFS_G4_MM(0);
+        DPFS_G4_MM(1);
+        __builtin_amdgcn_sched_barrier(0);
+        nxt.a.load(q, src, wm * 128 + 16 * q, l);
+        __builtin_amdgcn_sched_barrier(0);
+        DPFS_G4_MM(2);
+        DPFS_G4_MM(3);
+        __builtin_amdgcn_sched_barrier(0);
+        nxt.b.load(q, src + 16384, wn * 128 + 16 * q, l);
+        __builtin_amdgcn_sched_barrier(0);
+        DPFS_G4_MM(4);
+        DPFS_G4_MM(5);
+        __builtin_amdgcn_sched_barrier(0);
+        {
+          const unsigned off = (kpos(q) < krem) ? pbase[q] + (q < 4 ? addA : addB) : kOOB;
+          dma16(q < 4 ? (s2 ? ra2 : ra) : (s2 ? rb2 : rb), dst + (q < 4 ? 0 : 16384) + (wave + 4 * (q & 3)) * 1024,
+                off);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        DPFS_G4_MM(6);
+        DPFS_G4_MM(7);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#undef DPFS_G4_MM
+      p_slot = (p_slot + 1) & 3;
+    }
+    advance();
+  };
+
+  for (bool first = true; it < total; it += G, first = false) {
+    const Item ci = decode(it, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
+    const int nk = nsteps(ci);
+    step(F0, F1, !first, std::true_type{});
+    step(F1, F0, false, std::false_type{});
+    for (int t = 2; t < nk; t += 2) {
+      step(F0, F1, false, std::false_type{});
+      step(F1, F0, false, std::false_type{});
+    }
+    epilogue<OUT>(acc, ci, C, bias, rope, M, N, ldc, slab_stride, c_bytes, smem + RING + wave * STG, wm, wn, l);
+  }
+  // no LDS-DMA may still be writing when the workgroup's LDS is released
+  wait_vmcnt<0>();
+}
+
+}  // namespace g4
+}  // namespace dpfs
+
+using namespace dpfs;
+using namespace dpfs::g4;
+
+static int g4_cu_count() {
+  static int n[16] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 16) dev = 0;
+  if (n[dev] == 0) {
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+    n[dev] = c;
+  }
+  return n[dev];
+}
+
+static int g_g4_group_m = 4;
+static int g_g4_sched = 2;
+// Timing-only ablations (tools/gemm4_probe.py --ablate): bit 1 = output descriptor with zero
+// records (every store dropped), bit 2 = operand descriptors with zero records (every DMA
+// returns zeros, no memory traffic).  The instruction stream is unchanged.
+static int g_g4_ablate = 0;
+extern "C" void dpfs_gemm4_ablate(int v) { g_g4_ablate = v; }
+extern "C" void dpfs_gemm4_sched(int v) { g_g4_sched = v; }
+extern "C" void dpfs_gemm4_group_m(int g) { g_g4_group_m = g > 0 ? g : 4; }
+
+// Launch v4.  layout: 0 = NT (A K-major, B K-major), 1 = NN (B MN-major), 2 = TN (both
+// MN-major, fp32 out).  Returns false (nothing launched) when a span does not fit the 32-bit
+// buffer descriptors or a contiguous dimension is not a multiple of 8.
+extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const void* B, void* C, const float* bias,
+                                  int M, int N, int K, int lda, int ldb, int ldc, int kps, int splits,
+                                  long long slab_stride, unsigned a_bytes, unsigned b_bytes, const int64_t* rope_pos,
+                                  const float* rope_tab, int rope_cols, int rope_hd, const void* A2, const void* B2,
+                                  int k_switch, int lda2, int ldb2, unsigned a2_bytes, unsigned b2_bytes,
+                                  hipStream_t s) {
+  if (M <= 0 || N <= 0 || (N % 8) || (K % 8)) return false;
+  if (layout == 2 && (M % 8)) return false;
+  if (rope_cols > 0 && rope_hd != 64 && rope_hd != 128) return false;
+  if (kps % 32) return false;
+  const long long cspan = ((long long)(M - 1) * ldc + N) * (out_f32 ? 4 : 2);
+  if (cspan >= (1ll << 32) - 16) return false;
+  const long long items = (long long)((M + 255) / 256) * ((N + 255) / 256) * splits;
+  if (items <= 0 || items >= (1ll << 31)) return false;
+  const int grid = (int)std::min<long long>(items, g4_cu_count());
+  const Rope rope = {rope_pos, rope_tab, rope_cols, rope_hd};
+  const Dual dual = {(const bf16*)A2, (const bf16*)B2, A2 ? k_switch : 0x7fffffff, lda2, ldb2, a2_bytes, b2_bytes};
+  const unsigned cb = (g_g4_ablate & 1) ? 0u : (unsigned)cspan;
+  if (g_g4_ablate & 2) {
+    a_bytes = b_bytes = a2_bytes = b2_bytes = 0u;
+  }
+#define DPFS_G4(AK_, BK_, OUT_)                                                                                   \
+  do {                                                                                                            \
+    if (g_g4_sched == 2)                                                                                          \
+      gemm4_k<AK_, BK_, OUT_, 2><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb,\
+                                                      ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb, rope,  \
+                                                      g_g4_group_m, dual);                                        \
+    else if (g_g4_sched == 1)                                                                                     \
+      gemm4_k<AK_, BK_, OUT_, 1><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb,\
+                                                      ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb, rope,  \
+                                                      g_g4_group_m, dual);                                        \
+    else                                                                                                          \
+      gemm4_k<AK_, BK_, OUT_, 0><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb,\
+                                                      ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb, rope,  \
+                                                      g_g4_group_m, dual);                                        \
+  } while (0)
+  if (layout == 0) {
+    if (out_f32) DPFS_G4(true, true, 1);
+    else DPFS_G4(true, true, 0);
+  } else if (layout == 1) {
+    if (out_f32) DPFS_G4(true, false, 1);
+    else DPFS_G4(true, false, 0);
+  } else {
+    if (!out_f32) return false;
+    DPFS_G4(false, false, 1);
+  }
+#undef DPFS_G4
+  return true;
+}

@@ -268,11 +268,13 @@ def test_adam_matches_torch(C):
         assert torch.equal(s, p.bfloat16())
 
 
-@pytest.mark.parametrize("M,N,K,heads", [(2048, 2304, 768, 24), (300, 1152, 768, 12), (4096, 576, 768, 6)])
-def test_gemm_nt_fused_rope(C, M, N, K, heads):
-    """QKV projection with the RoPE rotation in the GEMM epilogue (hd=64) vs GEMM + reference RoPE."""
+@pytest.mark.parametrize("M,N,K,heads,hd", [(2048, 2304, 768, 24, 64), (300, 1152, 768, 12, 64),
+                                            (4096, 576, 768, 6, 64), (1000, 3072, 1024, 16, 128),
+                                            (513, 1536, 512, 8, 128)])
+def test_gemm_nt_fused_rope(C, M, N, K, heads, hd):
+    """QKV projection with the RoPE rotation in the GEMM epilogue (hd 64 and 128) vs GEMM +
+    reference RoPE."""
     torch.manual_seed(12)
-    hd = 64
     a = torch.randn(M, K, device=DEV).bfloat16()
     b = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
     bias = torch.randn(N, device=DEV)
@@ -678,3 +680,67 @@ def test_blaslt_direct_every_algorithm(C, layout):
             assert _rel(out, 2 * ref) < 1e-3, f"algorithm {i} (accumulate)"
     with pytest.raises(RuntimeError):
         C.lt_run(layout, a, b, torch.empty(M + 1, N, device=DEV), bias, 0)
+
+
+@pytest.mark.parametrize("sched", [0, 1, 2])
+@pytest.mark.parametrize("M,N,K", [(8200, 2104, 712), (1000, 776, 2304), (257, 264, 96), (4096, 768, 768)])
+def test_gemm_v4_bitwise_equals_v3(C, M, N, K, sched):
+    """The v4 kernel (one wave per SIMD, 128x128 per wave, 32-deep LDS ring) accumulates every
+    output in the same k order as v3, so NT (+bias) and NN results are bit-identical."""
+    torch.manual_seed(26)
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    bt = torch.randn(N, K, device=DEV).bfloat16()
+    bn = torch.randn(K, N, device=DEV).bfloat16()
+    bias = torch.randn(N, device=DEV)
+    old = C.gemm_v4_get_mask()
+    try:
+        C.gemm_v4_mask(7)
+        C.gemm4_sched(sched)
+        nt4, nn4 = C.gemm_nt(a, bt, bias), C.gemm_nn(a, bn)
+        C.gemm_v4_mask(0)
+        nt3, nn3 = C.gemm_nt(a, bt, bias), C.gemm_nn(a, bn)
+    finally:
+        C.gemm_v4_mask(old)
+        C.gemm4_sched(2)
+    assert _rel(nt4, R.gemm_nt(a.float(), bt.float(), bias)) < 1e-2
+    assert torch.equal(nt4, nt3)
+    assert torch.equal(nn4, nn3)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (2304, 768, 4096), (96, 768, 1000), (776, 2104, 8192)])
+@pytest.mark.parametrize("splits", [0, 3])
+def test_gemm_v4_tn(C, M, N, K, splits):
+    """TN (fp32 weight gradient, split-K slabs) on the v4 kernel, with and without accumulate."""
+    torch.manual_seed(27)
+    a = torch.randn(K, M, device=DEV).bfloat16()
+    b = torch.randn(K, N, device=DEV).bfloat16()
+    old = C.gemm_v4_get_mask()
+    try:
+        C.gemm_v4_mask(7)
+        C.gemm_force(-1, splits)
+        out = C.gemm_tn(a, b)
+        ref = R.gemm_tn(a.float(), b.float())
+        assert _rel(out, ref) < 1e-5
+        acc = torch.randn(M, N, device=DEV)
+        want = acc + ref
+        C.gemm_tn(a, b, acc, True)
+        assert _rel(acc, want) < 1e-5
+    finally:
+        C.gemm_v4_mask(old)
+        C.gemm_force(-1, 0)
+
+
+def test_gemm_v4_split_k_bf16_long_k(C):
+    """bf16-output GEMM with a long K (the lm_head data gradient: N = d_model, K = vocab shard)
+    takes the split-K fp32 slab path on v4."""
+    torch.manual_seed(28)
+    M, N, K = 2048, 768, 50304
+    a = (torch.randn(M, K, device=DEV) / 16).bfloat16()
+    b = (torch.randn(K, N, device=DEV) / 16).bfloat16()
+    old = C.gemm_v4_get_mask()
+    try:
+        C.gemm_v4_mask(7)
+        out = C.gemm_nn(a, b)
+    finally:
+        C.gemm_v4_mask(old)
+    assert _rel(out, R.gemm_nn(a.float(), b.float())) < 1e-2

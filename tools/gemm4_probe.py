@@ -1,0 +1,117 @@
+"""GEMM v4 (csrc/kernels/gemm4.hip) vs v3 (gemm.hip gemmp_k) vs hipBLASLt on the GPT-2-small
+step shapes: correctness against fp32 torch, then interleaved timing rounds in one process
+(CDNA guide rule 24: variants x rounds, median and min reported).
+
+    python tools/gemm4_probe.py [--rounds 7] [--iters 10] [--layouts nt nn tn] [--check-only]
+"""
+import argparse
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_pytorch_from_scratch_amd.ops import _ext  # noqa: E402
+
+T = 32768
+SHAPES = {
+    # (M, N, K) of C[M,N] = A . B  (names: the GPT-2-small projection they serve)
+    "nt": [("qkv", T, 2304, 768), ("wo", T, 768, 768), ("gateup", T, 4096, 768), ("down", T, 768, 2048),
+           ("lmhead", T, 50304, 768)],
+    "nn": [("qkv", T, 768, 2304), ("wo", T, 768, 768), ("gateup", T, 768, 4096), ("down", T, 2048, 768),
+           ("lmhead", T, 768, 50304)],
+    "tn": [("qkv", 2304, 768, T), ("wo", 768, 768, T), ("gateup", 4096, 768, T), ("down", 768, 2048, T),
+           ("lmhead", 50304, 768, T)],
+}
+BIT = {"nt": 1, "nn": 2, "tn": 4}
+
+
+def operands(layout, M, N, K, gen):
+    r = lambda *s: torch.randn(*s, device="cuda", generator=gen).bfloat16()
+    if layout == "nt":
+        a, b = r(M, K), r(N, K)
+        return a, b, (lambda C: C.gemm_nt(a, b, None)), (lambda: torch.nn.functional.linear(a, b)), \
+            (lambda: a.float() @ b.float().t())
+    if layout == "nn":
+        a, b = r(M, K), r(K, N)
+        return a, b, (lambda C: C.gemm_nn(a, b)), (lambda: torch.matmul(a, b)), (lambda: a.float() @ b.float())
+    a, b = r(K, M), r(K, N)
+    return a, b, (lambda C: C.gemm_tn(a, b)), (lambda: torch.mm(a.t(), b, out_dtype=torch.float32)), \
+        (lambda: a.float().t() @ b.float())
+
+
+def timed(fn, iters):
+    fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--layouts", nargs="+", default=["nt", "nn", "tn"])
+    ap.add_argument("--shapes", nargs="+", default=None, help="subset of names (qkv wo gateup down lmhead)")
+    ap.add_argument("--check-only", action="store_true")
+    ap.add_argument("--scheds", type=int, nargs="+", default=[0, 1, 2])
+    ap.add_argument("--no-blas", action="store_true")
+    ap.add_argument("--ablate", type=int, nargs="*", default=[],
+                    help="extra v4 arms with timing-only ablations (1 no stores, 2 zero operands, 3 both)")
+    a = ap.parse_args()
+    C = _ext.require()
+    gen = torch.Generator(device="cuda").manual_seed(0)
+    for layout in a.layouts:
+        for name, M, N, K in SHAPES[layout]:
+            if a.shapes and name not in a.shapes:
+                continue
+            _, _, ours, blas, ref = operands(layout, M, N, K, gen)
+            want = ref() if M * N <= 50304 * 768 * 2 else None
+            res = {}
+            for tag, mask, sc in [(f"v4s{sc}", 7, sc) for sc in a.scheds] + [("v3", 0, 0)]:
+                C.gemm_v4_mask(mask)
+                C.gemm4_sched(sc)
+                if want is not None:
+                    out = ours(C).float()
+                    res[tag] = ((out - want).norm() / want.norm()).item()
+            C.gemm_v4_mask(3)
+            del want
+            flops = 2.0 * M * N * K
+            print(f"{layout} {name} {M}x{N}x{K}: rel err " + " ".join(f"{k} {v:.2e}" for k, v in res.items()),
+                  flush=True)
+            if a.check_only:
+                continue
+            arms = [f"v4s{sc}" for sc in a.scheds] + [f"abl{x}" for x in a.ablate] + ["v3"] + \
+                ([] if a.no_blas else ["blas"])
+            ts = {k: [] for k in arms}
+            for _ in range(a.rounds):
+                for k in arms:
+                    if k.startswith("v4s"):
+                        C.gemm_v4_mask(7)
+                        C.gemm4_sched(int(k[3:]))
+                        ts[k].append(timed(lambda: ours(C), a.iters))
+                    elif k.startswith("abl"):
+                        C.gemm_v4_mask(7)
+                        C.gemm4_sched(a.scheds[-1])
+                        C.gemm4_ablate(int(k[3:]))
+                        ts[k].append(timed(lambda: ours(C), a.iters))
+                        C.gemm4_ablate(0)
+                    elif k == "v3":
+                        C.gemm_v4_mask(0)
+                        ts[k].append(timed(lambda: ours(C), a.iters))
+                    else:
+                        ts[k].append(timed(blas, a.iters))
+            C.gemm_v4_mask(3)
+            C.gemm4_sched(a.scheds[-1])
+            line = "   ".join(f"{k} {statistics.median(v):.4f} ms (min {min(v):.4f}) "
+                               f"{flops / statistics.median(v) / 1e9:.0f} TF" for k, v in ts.items())
+            print(f"{layout} {name} {M}x{N}x{K}: {line}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -23,9 +23,15 @@ def main():
     ap.add_argument("--sched", type=int, nargs="+", default=[-1])
     ap.add_argument("--cfg", type=int, nargs="+", default=[-1])
     ap.add_argument("--blas", action="store_true", help="also time hipBLASLt (torch) on the same layout")
+    ap.add_argument("--v4", type=int, default=None, help="v4 layout mask (gemm_v4_mask) for impl 3")
+    ap.add_argument("--sched4", type=int, default=None, help="v4 schedule (gemm4_sched)")
     ap.add_argument("--check", action="store_true", help="relative error of each implementation vs fp32 torch")
     a = ap.parse_args()
     C = _ext.require()
+    if a.v4 is not None:
+        C.gemm_v4_mask(a.v4)
+    if a.sched4 is not None:
+        C.gemm4_sched(a.sched4)
     M, N, K = a.M, a.N, a.K
     x = torch.randn(M, K, device="cuda").bfloat16()
     w = torch.randn(N, K, device="cuda").bfloat16()
