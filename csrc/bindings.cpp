@@ -25,6 +25,7 @@ void dpfs_gemm_nt_rope(const void*, const void*, void*, const float*, int, int, 
 void dpfs_gemm_v4_mask(int);
 void dpfs_gemm4_sched(int);
 void dpfs_gemm4_ablate(int);
+void dpfs_gemm4_diag(void*);
 int dpfs_gemm_v4_get_mask();
 void dpfs_gemm_force(int, int);
 void dpfs_gemm_v2_sched(int);
@@ -1070,6 +1071,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "layouts on the v4 kernel (one wave per SIMD, 128x128 per wave): bit 1 NT, 2 NN, 4 TN; 0 = all on v3");
   m.def("gemm_v4_get_mask", []() { return dpfs_gemm_v4_get_mask(); });
   m.def("gemm4_ablate", [](int v) { dpfs_gemm4_ablate(v); }, "timing-only: 1 = drop stores, 2 = zero operands");
+  m.def("gemm4_diag", [](torch::Tensor t) { dpfs_gemm4_diag(t.defined() && t.numel() ? t.data_ptr() : nullptr); },
+        "int64 buffer [grid*4*4] for the DIAG build's per-wave cycle split (gemm4_ablate bit 16)");
   m.def("gemm4_sched", [](int v) { dpfs_gemm4_sched(v); },
         "v4 main-loop schedule: 0 compiler order, 1 = 8 chunks (DMA piece + 2 fragment reads + 8 MFMAs), "
         "2 = MFMA pairs interleaved with single reads / DMA pieces (precomputed DMA offsets)");

@@ -7,31 +7,32 @@
 // Why a new main loop (the v3 kernel in gemm.hip runs 8 waves, 2 per SIMD, 128 x 64 each):
 //  * 128 x 128 per wave halves the LDS bytes read per MFMA (16 ds_read_b128 per 64
 //    v_mfma_f32_16x16x32_bf16 = 0.25, v3 0.375) and one wave per SIMD leaves each SIMD's
-//    matrix pipe to one instruction stream (no partner wave's MFMAs in the way).  The 256
-//    fp32 accumulators per lane live in AGPRs; operand fragments, addresses and the epilogue
-//    in the 256 arch VGPRs (512-register budget at one wave per SIMD, no spills).
+//    matrix pipe to one instruction stream.  The 256 fp32 accumulators per lane are
+//    asm-owned AGPRs a[0:255] (gemm4_acc.inc, generated): hipcc never moves or spills them,
+//    and fragments, addresses and the epilogue get the 256 arch VGPRs.
 //  * The K loop walks 32-deep steps through a 4-slot LDS ring (32 KiB per slot: A and B
 //    256 x 32 bf16 each).  Step s multiplies fragments already in registers, reads the next
-//    step's fragments (one step of register prefetch, so no LDS latency is exposed at a
-//    step boundary) and issues the LDS-DMA of step s + 3: each DMA has two full steps
-//    (~2 x 64 MFMAs) to land.  One barrier per step; counted `s_waitcnt vmcnt` (never 0 in
-//    the loop).
+//    step's fragments in its first half (one step of register prefetch: no LDS latency at a
+//    step boundary) and issues the LDS-DMA of step s + 3 in its second half (two full steps
+//    for each DMA to land).  One barrier per step; counted `s_waitcnt vmcnt` (never 0 in
+//    the loop).  Fragment reads and DMA pieces sit between MFMA pairs in a fixed order
+//    (sched_barrier), the DMA offsets are per-item lane constants plus one uniform add.
 //  * Persistent: one 256-thread workgroup per CU walks (split, tile) items in grouped,
 //    XCD-contiguous order; the DMA stream continues across item boundaries, so the next
 //    item's first three steps are in flight while an item's epilogue runs.  Past the last
 //    item the producer issues out-of-range DMAs (zeros into dead slots) so every wait count
 //    stays static.
-//  * Epilogue: bias (+ RoPE for the QKV projection, head_dim 64 or 128: the rotation
-//    partner of column d is d + hd/2, the same lane's tile j + hd/32) in fp32, bf16 packed
-//    into a wave-private 8 KiB LDS staging area (XOR-swizzled, conflict-free ds_write_b64),
-//    read back by rows and written as 16-byte buffer stores covering whole 128-byte lines
-//    (the v3 epilogue's 8-byte stores touched 16 partial lines per instruction).
-//    Out-of-range rows / columns get an offset past the descriptor (dropped by hardware).
+//  * Epilogue: the wave's 128 bias values arrive in its own LDS area by LDS-DMA issued at the
+//    item's last step (a counted vmcnt, no ring drain); bias (+ RoPE for the QKV projection,
+//    head_dim 64 or 128: the rotation partner of column d is d + hd/2, the same lane's tile
+//    j + hd/32) in fp32, bf16; v_permlane16_swap pairs two 16-column tiles so each lane
+//    writes 8 consecutive columns with one 16-byte buffer store.  Out-of-range rows /
+//    columns get an offset past the descriptor (dropped by hardware).
 //  * LDS images: K-contiguous operands [256 rows][64 B] with the 16-byte chunk of row r at
 //    slot c ^ h(r), h(r) = (-(r >> 2)) & 3: every ds_read_b128 lane group covers the 16 bank
 //    slots exactly once.  MN-contiguous operands [32 k][256] as gemm.hip (read with the
-//    ds_read_b64_tr_b16 hardware transpose).  The swizzle is applied on the DMA SOURCE
-//    address (LDS-DMA writes lane-linear 1 KiB pieces).
+//    ds_read_b64_tr_b16 hardware transpose, through inline asm: see ds_tr16).  The swizzle
+//    is applied on the DMA SOURCE address (LDS-DMA writes lane-linear 1 KiB pieces).
 #include "common.h"
 
 #include <algorithm>
@@ -40,14 +41,23 @@
 namespace dpfs {
 namespace g4 {
 
+#include "gemm4_acc.inc"
+
 constexpr int SLOT = 32768;          // one ring slot: A (16 KiB) + B (16 KiB)
 constexpr int RING = 4 * SLOT;       // 128 KiB
-constexpr int STG = 8192;            // epilogue staging per wave
-constexpr int LDS_TOTAL = RING + 4 * STG;   // 160 KiB
+constexpr int BIAS_LDS = 4 * 512;    // per wave: its 128 fp32 bias values
+constexpr int LDS_TOTAL = RING + BIAS_LDS;
+
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
 
 __device__ __forceinline__ int kh(int r) { return (4 - ((r >> 2) & 3)) & 3; }
 __device__ __forceinline__ int mnh(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
-
 
 struct Rope {
   const int64_t* pos;
@@ -63,71 +73,11 @@ struct Dual {
   unsigned a2_bytes, b2_bytes;
 };
 
-// One operand's half of a ring slot (16 KiB): 16 pieces of 1 KiB, 4 per wave.
-template <bool KMAJ>
-__device__ __forceinline__ void issue_half(__amdgpu_buffer_rsrc_t rs, char* dst, int r0, int k0, int ke, int ld,
-                                           int wave, int l) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int j = wave + 4 * i;
-    unsigned off;
-    if (KMAJ) {
-      const int row = 16 * j + (l >> 2);
-      const int c = (l & 3) ^ kh(row);
-      const int k = k0 + 8 * c;
-      off = (k < ke) ? (unsigned)(((long long)(r0 + row) * ld + k) * 2) : kOOB;
-    } else {
-      const int lin = j * 64 + l;
-      const int row = lin >> 5;
-      const int c = (lin & 31) ^ (mnh(row) << 1);
-      const int k = k0 + row;
-      off = (k < ke) ? (unsigned)(((long long)k * ld + r0 + 8 * c) * 2) : kOOB;
-    }
-    dma16(rs, dst + j * 1024, off);
-  }
-}
-
-// Piece i (< 4) of issue_half, for schedules that spread the pieces between MFMAs.
-template <bool KMAJ>
-__device__ __forceinline__ void issue_piece(__amdgpu_buffer_rsrc_t rs, char* dst, int r0, int k0, int ke, int ld,
-                                            int wave, int l, int i) {
-  const int j = wave + 4 * i;
-  unsigned off;
-  if (KMAJ) {
-    const int row = 16 * j + (l >> 2);
-    const int c = (l & 3) ^ kh(row);
-    const int k = k0 + 8 * c;
-    off = (k < ke) ? (unsigned)(((long long)(r0 + row) * ld + k) * 2) : kOOB;
-  } else {
-    const int lin = j * 64 + l;
-    const int row = lin >> 5;
-    const int c = (lin & 31) ^ (mnh(row) << 1);
-    const int k = k0 + row;
-    off = (k < ke) ? (unsigned)(((long long)k * ld + r0 + 8 * c) * 2) : kOOB;
-  }
-  dma16(rs, dst + j * 1024, off);
-}
-
 // Fragment of the 16x16x32 MFMA operand: lane l holds X[rb + (l&15)][8(l>>4) + e], e < 8.
-template <bool KMAJ>
-__device__ __forceinline__ bf16x8 frag(const char* half, int rb, int l) {
-  if (KMAJ) {
-    const int row = rb + (l & 15);
-    const int c = l >> 4;
-    return *reinterpret_cast<const bf16x8*>(half + row * 64 + ((c ^ kh(row)) << 4));
-  } else {
-    const int i = l & 15, q = i >> 2, p = i & 3;
-    const int chunk = (rb + 4 * p) >> 3;
-    const int k_lo = 8 * (l >> 4) + q;
-    const int k_hi = k_lo + 4;
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4*)(half + k_lo * 512 + ((chunk ^ (mnh(k_lo) << 1)) << 4) + (p & 1) * 8));
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4*)(half + k_hi * 512 + ((chunk ^ (mnh(k_hi) << 1)) << 4) + (p & 1) * 8));
-    typedef short s16x8 __attribute__((ext_vector_type(8)));
-    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, v);
-  }
+__device__ __forceinline__ bf16x8 frag_k(const char* half, int rb, int l) {
+  const int row = rb + (l & 15);
+  const int c = l >> 4;
+  return *reinterpret_cast<const bf16x8*>(half + row * 64 + ((c ^ kh(row)) << 4));
 }
 
 // MN-major fragment halves through inline asm: hipcc puts `s_waitcnt vmcnt(0)` in front of
@@ -146,7 +96,7 @@ struct Opnd;
 template <>
 struct Opnd<true> {
   bf16x8 v[8];
-  __device__ __forceinline__ void load(int i, const char* half, int rb, int l) { v[i] = frag<true>(half, rb, l); }
+  __device__ __forceinline__ void load(int i, const char* half, int rb, int l) { v[i] = frag_k(half, rb, l); }
   __device__ __forceinline__ bf16x8 get(int i) const { return v[i]; }
   __device__ __forceinline__ void pin() {}
 };
@@ -190,18 +140,6 @@ __device__ __forceinline__ void read_frags(Frags<AK, BKM>& f, const char* slot, 
   for (int j = 0; j < 8; ++j) f.b.load(j, slot + 16384, wn * 128 + 16 * j, l);
 }
 
-template <bool ZERO, bool AK, bool BKM>
-__device__ __forceinline__ void mma(f32x4 (&acc)[8][8], const Frags<AK, BKM>& f) {
-  // (no s_setprio: one wave per SIMD has no partner to arbitrate against, and the builtin
-  // would fence the MFMAs off from the interleaved loads)
-  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.b.get(j), f.a.get(i), ZERO ? z : acc[i][j], 0, 0, 0);
-}
-
 // Work item -> tile origin and K range (grouped order as gemm.hip's gemmp_k).
 struct Item {
   int m0, n0, kb, ke, split, sel;
@@ -230,102 +168,97 @@ __device__ __forceinline__ Item decode(int lin, int nwg, int tiles_m, int tiles_
   return it;
 }
 
+// 32-deep steps of an item, rounded up to an even count (the two fragment register sets
+// alternate statically; a trailing step past the K range reads zeros).
 __device__ __forceinline__ int nsteps(const Item& it) {
   const int n = max(1, (it.ke - it.kb + 31) / 32);
   return (n + 1) & ~1;
 }
 
-// Epilogue of one item.  OUT 0: bias (+ RoPE) in fp32, bf16 through the wave's LDS staging
-// area, 16-byte row stores; OUT 1: fp32 16-byte stores of each lane's 4 columns.
-// Exactly STORES (32 / 64) buffer stores per wave (out-of-range lanes get an offset past the
-// descriptor), which the next item's first wait counts.
+// Epilogue of one item.  OUT 0: bias (+ RoPE) in fp32, bf16; v_permlane16_swap pairs two
+// 16-column tiles so each lane holds 8 consecutive columns and writes them with ONE 16-byte
+// buffer store (16 rows x 64 contiguous bytes per instruction; the two halves of a row's
+// 128-byte line are written by consecutive instructions).  OUT 1: fp32, each lane's 4 columns
+// per tile as one 16-byte store.  Exactly STORES (32 / 64) buffer stores per wave
+// (out-of-range lanes get an offset past the descriptor), which the next item's first wait
+// counts.
 template <int OUT>
-__device__ __forceinline__ void epilogue(f32x4 (&acc)[8][8], const Item& ci, void* C, const float* bias,
+__device__ __forceinline__ void epilogue(const char* bias_lds, bool has_bias, const Item& ci, void* C,
                                          const Rope& rope, int M, int N, int ldc, long long slab_stride,
-                                         unsigned c_bytes, char* stg, int wm, int wn, int l) {
+                                         unsigned c_bytes, int wm, int wn, int l) {
   const int g = l >> 4;
   const int wcol0 = ci.n0 + wn * 128;
+  acc_drain();
   if constexpr (OUT == 0) {
-    f32x4 bv[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int n = wcol0 + 16 * j + 4 * g;
-      bv[j] = (bias && n < N) ? *reinterpret_cast<const f32x4*>(bias + n) : (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
     const bool do_rope = rope.cols > 0 && wcol0 < rope.cols;
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(C, (short)0, (int)c_bytes, 0x00020000);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii) {
-        __builtin_amdgcn_sched_barrier(0);
-        const int i = 2 * r + ii;
-        f32x4 v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = acc[i][j] + bv[j];
-        if (do_rope) {
-          const int m = ci.m0 + wm * 128 + 16 * i + (l & 15);
-          const float* tr = rope.tab + (m < M ? rope.pos[m] : 0) * rope.hd;
-          const int half = rope.hd >> 1;
-          const int hj = half >> 4;   // tiles per half head: 2 (hd 64) or 4 (hd 128)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int jh = j % (2 * hj);
-            if (jh < hj && wcol0 + 16 * j < rope.cols) {
-              const f32x4 cs = *reinterpret_cast<const f32x4*>(tr + 16 * jh + 4 * g);
-              const f32x4 sn = *reinterpret_cast<const f32x4*>(tr + half + 16 * jh + 4 * g);
-              const f32x4 x1 = v[j], x2 = v[j + hj];
-              v[j] = x1 * cs - x2 * sn;
-              v[j + hj] = x2 * cs + x1 * sn;
-            }
-          }
-        }
-        const int row = 16 * ii + (l & 15);
+    const int colg = 16 * (g & 1) + 8 * (g >> 1);
+    static_for<0, 8>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      f32x4 v[8];
+      static_for<0, 8>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        v[j] = acc_read<i, j>();
+        if (has_bias) v[j] += *reinterpret_cast<const f32x4*>(bias_lds + 64 * j + 16 * g);
+      });
+      const int m = ci.m0 + wm * 128 + 16 * i + (l & 15);
+      if (do_rope) {
+        const float* tr = rope.tab + (m < M ? rope.pos[m] : 0) * rope.hd;
+        const int half = rope.hd >> 1;
+        const int hj = half >> 4;   // tiles per half head: 2 (hd 64) or 4 (hd 128)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          bf16x4 o = {(bf16)v[j][0], (bf16)v[j][1], (bf16)v[j][2], (bf16)v[j][3]};
-          const int u = (4 * j + g) ^ (row & 15);
-          *reinterpret_cast<u32x2*>(stg + row * 256 + u * 8) = __builtin_bit_cast(u32x2, o);
+          const int jh = j % (2 * hj);
+          if (jh < hj && wcol0 + 16 * j < rope.cols) {
+            const f32x4 cs = *reinterpret_cast<const f32x4*>(tr + 16 * jh + 4 * g);
+            const f32x4 sn = *reinterpret_cast<const f32x4*>(tr + half + 16 * jh + 4 * g);
+            const f32x4 x1 = v[j], x2 = v[j + hj];
+            v[j] = x1 * cs - x2 * sn;
+            v[j + hj] = x2 * cs + x1 * sn;
+          }
         }
       }
-      // read back whole rows: lane L -> row 4q + (L>>4), 16-byte chunk L&15
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int row = 4 * q + (l >> 4);
-        const int c = l & 15;
-        u32x4 w = *reinterpret_cast<const u32x4*>(stg + row * 256 + ((c ^ ((row >> 1) & 7)) << 4));
-        if (row & 1) w = (u32x4){w[2], w[3], w[0], w[1]};
-        const int m = ci.m0 + wm * 128 + 32 * r + row;
-        const int n = wcol0 + 8 * c;
+      for (int jp = 0; jp < 4; ++jp) {
+        const bf16x4 o0 = {(bf16)v[2 * jp][0], (bf16)v[2 * jp][1], (bf16)v[2 * jp][2], (bf16)v[2 * jp][3]};
+        const bf16x4 o1 = {(bf16)v[2 * jp + 1][0], (bf16)v[2 * jp + 1][1], (bf16)v[2 * jp + 1][2],
+                           (bf16)v[2 * jp + 1][3]};
+        const u32x2 d = __builtin_bit_cast(u32x2, o0), e = __builtin_bit_cast(u32x2, o1);
+        const auto sx = __builtin_amdgcn_permlane16_swap(d[0], e[0], false, false);
+        const auto sy = __builtin_amdgcn_permlane16_swap(d[1], e[1], false, false);
+        const u32x4 w = {sx[0], sy[0], sx[1], sy[1]};
+        const int n = wcol0 + 32 * jp + colg;
         const bool ok = m < M && n < N;
         const unsigned off = ok ? (unsigned)(((long long)m * ldc + n) * 2) : kOOB;
         __builtin_amdgcn_raw_buffer_store_b128(w, rc, off, 0, 0);
       }
-    }
+    });
   } else {
     char* cbase = reinterpret_cast<char*>(C) + (long long)ci.split * slab_stride * 4;
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)cbase, (short)0, (int)c_bytes, 0x00020000);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    static_for<0, 8>([&](auto I) {
+      constexpr int i = decltype(I)::value;
       const int m = ci.m0 + wm * 128 + 16 * i + (l & 15);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      static_for<0, 8>([&](auto J) {
+        constexpr int j = decltype(J)::value;
         const int n = wcol0 + 16 * j + 4 * g;
         const bool ok = m < M && n < N;
         const unsigned off = ok ? (unsigned)(((long long)m * ldc + n) * 4) : kOOB;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rc, off, 0, 0);
-      }
-    }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc_read<i, j>()), rc, off, 0, 0);
+      });
+    });
   }
 }
 
 // OUT: 0 = bf16 C (+ fp32 bias[n], + RoPE); 1 = fp32 C / split-K slab.
-template <bool AK, bool BKM, int OUT, int SCHED>
+// dbg (timing-only ablations, tools/gemm4_probe.py): 4 = no DMA wait, 8 = no step barrier.
+template <bool AK, bool BKM, int OUT, int DIAG = 0>
 __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                   void* __restrict__ C, const float* __restrict__ bias, int M, int N,
                                                   int K, int lda, int ldb, int ldc, int kps, int splits,
                                                   long long slab_stride, unsigned a_bytes, unsigned b_bytes,
-                                                  unsigned c_bytes, Rope rope, int group_m, Dual dual) {
+                                                  unsigned c_bytes, Rope rope, int group_m, Dual dual, int dbg,
+                                                  unsigned long long* diag) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_TOTAL];
   constexpr int STORES = OUT == 0 ? 32 : 64;   // store instructions per wave per item
 
@@ -345,30 +278,20 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   const __amdgpu_buffer_rsrc_t rb2 =
       dual_on ? __builtin_amdgcn_make_buffer_rsrc((void*)dual.B2, (short)0, (int)dual.b2_bytes, 0x00020000) : rb;
   const int lda2 = dual_on ? dual.lda2 : lda, ldb2 = dual_on ? dual.ldb2 : ldb;
+  const __amdgpu_buffer_rsrc_t rbias =
+      __builtin_amdgcn_make_buffer_rsrc((void*)bias, (short)0, bias ? N * 4 : 0, 0x00020000);
+  char* bias_lds = smem + RING + wave * 512;
 
   int it = xcd_remap(blockIdx.x, G);
   if (it >= total) return;
 
   // ---- producer cursor: the DMA stream runs 3 steps ahead of the consumer, across items.
-  // Every item takes an EVEN number of 32-deep steps (a trailing all-zero step when the K
-  // range is an odd number of steps) so the two fragment register sets alternate statically.
   int p_it = it;
   Item pi = decode(p_it, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
   int p_t = 0, p_nk = nsteps(pi);
   int p_slot = 0;
-  // DMA of the producer's current stage (no branches: kept in the step's scheduling region).
-  auto issue_stage = [&]() {
-    char* dst = smem + p_slot * SLOT;
-    const bool live = p_it < total;
-    const int ke = live ? pi.ke : 0;    // dead stream: every offset out of range -> zeros
-    const int k0 = pi.kb + 32 * p_t;
-    const bool s2 = pi.sel != 0;
-    issue_half<AK>(s2 ? ra2 : ra, dst, pi.m0, k0, ke, s2 ? lda2 : lda, wave, l);
-    issue_half<BKM>(s2 ? rb2 : rb, dst + 16384, pi.n0, k0, ke, s2 ? ldb2 : ldb, wave, l);
-    p_slot = (p_slot + 1) & 3;
-  };
-  // Per-item lane offsets of the wave's 8 DMA pieces (SCHED 2): a step then adds one
-  // uniform term per operand and checks the K bound against a lane constant.
+  // Per-item lane offsets of the wave's 8 DMA pieces (4 of A, 4 of B): a step adds one
+  // uniform term per operand and checks the K bound against a lane constant (kpos).
   unsigned pbase[8];
   auto rebase = [&]() {
     const bool s2 = pi.sel != 0;
@@ -392,7 +315,6 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
       }
     }
   };
-  // lane constant compared with (ke - k0): the k offset of the lane's 16 bytes in the step
   auto kpos = [&](int q) -> int {
     const bool km = q < 4 ? AK : BKM;
     const int j = wave + 4 * (q & 3);
@@ -402,128 +324,168 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
     }
     return (j * 64 + l) >> 5;
   };
-  if constexpr (SCHED == 2) rebase();
+  rebase();
+  // DMA piece q (< 8) of the producer's current stage
+  auto issue = [&](int q) {
+    const bool live = p_it < total;
+    const int krem = (live ? pi.ke : 0) - (pi.kb + 32 * p_t);   // valid k in this stage
+    const int k0 = pi.kb + 32 * p_t;
+    const bool s2 = pi.sel != 0;
+    const bool isA = q < 4;
+    const bool km = isA ? AK : BKM;
+    const unsigned add = km ? (unsigned)(k0 * 2)
+                            : (unsigned)((long long)k0 * (isA ? (s2 ? lda2 : lda) : (s2 ? ldb2 : ldb)) * 2);
+    const unsigned off = (kpos(q) < krem) ? pbase[q] + add : kOOB;
+    if constexpr (DIAG == 2) return;   // timing-only: no DMA issued (stale LDS, wrong results)
+    dma16(isA ? (s2 ? ra2 : ra) : (s2 ? rb2 : rb),
+          smem + p_slot * SLOT + (isA ? 0 : 16384) + (wave + 4 * (q & 3)) * 1024, off);
+  };
   auto advance = [&]() {
+    p_slot = (p_slot + 1) & 3;
     if (p_it < total && ++p_t == p_nk) {
       p_it += G;
       p_t = 0;
       if (p_it < total) {
         pi = decode(p_it, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
         p_nk = nsteps(pi);
-        if constexpr (SCHED == 2) rebase();
+        rebase();
       }
     }
   };
-  auto produce = [&]() {
-    issue_stage();
+#pragma unroll
+  for (int s0 = 0; s0 < 3; ++s0) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) issue(q);
     advance();
-  };
-  produce();
-  produce();
-  produce();
+  }
 
   Frags<AK, BKM> F0, F1;
-  f32x4 acc[8][8];
   int c_slot = 0;
+  // DIAG build only (timing diagnosis, never the production kernel): cycles spent in the
+  // step-entry waits + barrier, in the step bodies and in the epilogues, per wave.
+  unsigned long long t_wait = 0, t_body = 0, t_epi = 0, t_mark = 0;
+  auto stamp = [&]() -> unsigned long long {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+  };
   // fragments of the first step: stage 0 landed (two younger stages of 8 pieces in flight)
   wait_vmcnt<16>();
   __builtin_amdgcn_s_barrier();
   read_frags<AK, BKM>(F0, smem, wm, wn, l);
+  if constexpr (DIAG) t_mark = stamp();
 
   // One consumer step on `cur`, prefetching the next step's fragments into `nxt`.
   // Entry wait: stage s+1 landed for this wave (younger: stage s+2 = 8 pieces, plus the
   // previous item's epilogue stores on an item's first step), then the step barrier.
-  auto step = [&](Frags<AK, BKM>& cur, Frags<AK, BKM>& nxt, bool first, auto zero) {
+  auto step = [&](Frags<AK, BKM>& cur, Frags<AK, BKM>& nxt, bool first, auto zero, bool last, int bcol0) {
+    constexpr bool ZR = decltype(zero)::value;
+    if constexpr (DIAG) {
+      const unsigned long long t = stamp();
+      t_body += t - t_mark;
+      t_mark = t;
+    }
     // `cur` was read a whole step ago: retire it here so the MFMAs below need no LDS wait
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
     cur.a.pin();
     cur.b.pin();
-    if (first) wait_vmcnt<(8 + STORES < 63 ? 8 + STORES : 63)>();
+    if (dbg & 4) wait_vmcnt<63>();   // timing-only: no wait for the DMA (wrong results)
+    else if (first) wait_vmcnt<(8 + STORES < 63 ? 8 + STORES : 63)>();
     else wait_vmcnt<8>();
-    __builtin_amdgcn_s_barrier();
-    c_slot = (c_slot + 1) & 3;
-    if constexpr (SCHED == 0) {
-      issue_stage();
-      read_frags<AK, BKM>(nxt, smem + c_slot * SLOT, wm, wn, l);
-      mma<decltype(zero)::value, AK, BKM>(acc, cur);
-    } else if constexpr (SCHED == 1) {
-      // 8 chunks in fixed program order: one DMA piece and the next step's A / B fragment
-      // q, then the 8 MFMAs of accumulator row q (row q's A fragment is dead after them)
-      char* dst = smem + p_slot * SLOT;
-      const bool live = p_it < total;
-      const int ke = live ? pi.ke : 0;
-      const int k0 = pi.kb + 32 * p_t;
-      const bool s2 = pi.sel != 0;
-      const char* src = smem + c_slot * SLOT;
-      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        if (q < 4) issue_piece<AK>(s2 ? ra2 : ra, dst, pi.m0, k0, ke, s2 ? lda2 : lda, wave, l, q);
-        else issue_piece<BKM>(s2 ? rb2 : rb, dst + 16384, pi.n0, k0, ke, s2 ? ldb2 : ldb, wave, l, q - 4);
-        nxt.a.load(q, src, wm * 128 + 16 * q, l);
-        nxt.b.load(q, src + 16384, wn * 128 + 16 * q, l);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          acc[q][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.b.get(j), cur.a.get(q), decltype(zero)::value ? z : acc[q][j],
-                                                              0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      p_slot = (p_slot + 1) & 3;
-    } else {
-      // finer interleave: pairs of MFMAs with one fragment read or one DMA piece between
-      char* dst = smem + p_slot * SLOT;
-      const bool live = p_it < total;
-      const int krem = (live ? pi.ke : 0) - (pi.kb + 32 * p_t);   // valid k in this step
-      const int k0 = pi.kb + 32 * p_t;
-      const bool s2 = pi.sel != 0;
-      const unsigned addA = AK ? (unsigned)(k0 * 2) : (unsigned)((long long)k0 * (s2 ? lda2 : lda) * 2);
-      const unsigned addB = BKM ? (unsigned)(k0 * 2) : (unsigned)((long long)k0 * (s2 ? ldb2 : ldb) * 2);
-      const char* src = smem + c_slot * SLOT;
-      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      constexpr bool ZR = decltype(zero)::value;
-#define DPFS_G4_MM(j_) acc[q][j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.b.get(j_), cur.a.get(q), ZR ? z : acc[q][j_], 0, 0, 0)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        DPFS_G4_MM(0);
-        DPFS_G4_MM(1);
-        __builtin_amdgcn_sched_barrier(0);
-        nxt.a.load(q, src, wm * 128 + 16 * q, l);
-        __builtin_amdgcn_sched_barrier(0);
-        DPFS_G4_MM(2);
-        DPFS_G4_MM(3);
-        __builtin_amdgcn_sched_barrier(0);
-        nxt.b.load(q, src + 16384, wn * 128 + 16 * q, l);
-        __builtin_amdgcn_sched_barrier(0);
-        DPFS_G4_MM(4);
-        DPFS_G4_MM(5);
-        __builtin_amdgcn_sched_barrier(0);
-        {
-          const unsigned off = (kpos(q) < krem) ? pbase[q] + (q < 4 ? addA : addB) : kOOB;
-          dma16(q < 4 ? (s2 ? ra2 : ra) : (s2 ? rb2 : rb), dst + (q < 4 ? 0 : 16384) + (wave + 4 * (q & 3)) * 1024,
-                off);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        DPFS_G4_MM(6);
-        DPFS_G4_MM(7);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#undef DPFS_G4_MM
-      p_slot = (p_slot + 1) & 3;
+    if (!(dbg & 8)) __builtin_amdgcn_s_barrier();
+    if constexpr (DIAG) {
+      const unsigned long long t = stamp();
+      t_wait += t - t_mark;
+      t_mark = t;
     }
+    if (OUT == 0 && last && bias) {
+      // the epilogue's 128 bias values of this wave into its LDS area by two 256-byte LDS-DMA
+      // pieces, ahead of this step's 8 ring pieces (the epilogue waits vmcnt(8), no barrier:
+      // the wave reads only what it loaded)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int n = bcol0 + 64 * h + l;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rbias, (__attribute__((address_space(3))) void*)(bias_lds + 256 * h),
+                                                 4, n < N ? (unsigned)(n * 4) : kOOB, 0, 0, 0);
+      }
+    }
+    c_slot = (c_slot + 1) & 3;
+    const char* src = smem + c_slot * SLOT;
+    // every fragment read of the next step in the first half, the DMA pieces in the second
+    static_for<0, 8>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      if constexpr (q < 4) {
+        acc_mfma<q, 0, ZR>(cur.b.get(0), cur.a.get(q));
+        __builtin_amdgcn_sched_barrier(0);
+        nxt.a.load(2 * q, src, wm * 128 + 32 * q, l);
+        __builtin_amdgcn_sched_barrier(0);
+        acc_mfma<q, 1, ZR>(cur.b.get(1), cur.a.get(q));
+        acc_mfma<q, 2, ZR>(cur.b.get(2), cur.a.get(q));
+        __builtin_amdgcn_sched_barrier(0);
+        nxt.b.load(2 * q, src + 16384, wn * 128 + 32 * q, l);
+        __builtin_amdgcn_sched_barrier(0);
+        acc_mfma<q, 3, ZR>(cur.b.get(3), cur.a.get(q));
+        acc_mfma<q, 4, ZR>(cur.b.get(4), cur.a.get(q));
+        __builtin_amdgcn_sched_barrier(0);
+        nxt.a.load(2 * q + 1, src, wm * 128 + 32 * q + 16, l);
+        __builtin_amdgcn_sched_barrier(0);
+        acc_mfma<q, 5, ZR>(cur.b.get(5), cur.a.get(q));
+        acc_mfma<q, 6, ZR>(cur.b.get(6), cur.a.get(q));
+        __builtin_amdgcn_sched_barrier(0);
+        nxt.b.load(2 * q + 1, src + 16384, wn * 128 + 32 * q + 16, l);
+        __builtin_amdgcn_sched_barrier(0);
+        acc_mfma<q, 7, ZR>(cur.b.get(7), cur.a.get(q));
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        static_for<0, 2>([&](auto H) {
+          constexpr int h = decltype(H)::value;
+          acc_mfma<q, 4 * h, ZR>(cur.b.get(4 * h), cur.a.get(q));
+          acc_mfma<q, 4 * h + 1, ZR>(cur.b.get(4 * h + 1), cur.a.get(q));
+          __builtin_amdgcn_sched_barrier(0);
+          issue(2 * (q - 4) + h);
+          __builtin_amdgcn_sched_barrier(0);
+          acc_mfma<q, 4 * h + 2, ZR>(cur.b.get(4 * h + 2), cur.a.get(q));
+          acc_mfma<q, 4 * h + 3, ZR>(cur.b.get(4 * h + 3), cur.a.get(q));
+          __builtin_amdgcn_sched_barrier(0);
+        });
+      }
+    });
     advance();
   };
 
   for (bool first = true; it < total; it += G, first = false) {
     const Item ci = decode(it, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
     const int nk = nsteps(ci);
-    step(F0, F1, !first, std::true_type{});
-    step(F1, F0, false, std::false_type{});
+    const int bcol0 = ci.n0 + wn * 128;
+    step(F0, F1, !first, std::true_type{}, false, bcol0);
+    step(F1, F0, false, std::false_type{}, nk == 2, bcol0);
     for (int t = 2; t < nk; t += 2) {
-      step(F0, F1, false, std::false_type{});
-      step(F1, F0, false, std::false_type{});
+      step(F0, F1, false, std::false_type{}, false, bcol0);
+      step(F1, F0, false, std::false_type{}, t + 2 >= nk, bcol0);
     }
-    epilogue<OUT>(acc, ci, C, bias, rope, M, N, ldc, slab_stride, c_bytes, smem + RING + wave * STG, wm, wn, l);
+    if constexpr (DIAG) {
+      const unsigned long long t = stamp();
+      t_body += t - t_mark;
+      t_mark = t;
+    }
+    if (OUT == 0 && bias) wait_vmcnt<8>();   // this wave's bias DMA landed (8 younger ring pieces)
+    epilogue<OUT>(bias_lds, bias != nullptr, ci, C, rope, M, N, ldc, slab_stride, c_bytes, wm, wn, l);
+    if constexpr (DIAG) {
+      const unsigned long long t = stamp();
+      t_epi += t - t_mark;
+      t_mark = t;
+    }
+  }
+  if constexpr (DIAG) {
+    if (l == 0) {
+      unsigned long long* d = diag + (blockIdx.x * 4 + wave) * 4;
+      d[0] = t_wait;
+      d[1] = t_body;
+      d[2] = t_epi;
+      d[3] = 1;
+    }
   }
   // no LDS-DMA may still be writing when the workgroup's LDS is released
   wait_vmcnt<0>();
@@ -549,13 +511,14 @@ static int g4_cu_count() {
 }
 
 static int g_g4_group_m = 4;
-static int g_g4_sched = 2;
 // Timing-only ablations (tools/gemm4_probe.py --ablate): bit 1 = output descriptor with zero
 // records (every store dropped), bit 2 = operand descriptors with zero records (every DMA
-// returns zeros, no memory traffic).  The instruction stream is unchanged.
+// returns zeros, no memory traffic), 4 = no DMA wait, 8 = no step barrier (wrong results).
 static int g_g4_ablate = 0;
+static unsigned long long* g_g4_diag = nullptr;   // [grid][4 waves][wait, body, epilogue, valid]
 extern "C" void dpfs_gemm4_ablate(int v) { g_g4_ablate = v; }
-extern "C" void dpfs_gemm4_sched(int v) { g_g4_sched = v; }
+extern "C" void dpfs_gemm4_diag(void* p) { g_g4_diag = (unsigned long long*)p; }
+extern "C" void dpfs_gemm4_sched(int) {}   // one schedule since the asm-owned accumulators
 extern "C" void dpfs_gemm4_group_m(int g) { g_g4_group_m = g > 0 ? g : 4; }
 
 // Launch v4.  layout: 0 = NT (A K-major, B K-major), 1 = NN (B MN-major), 2 = TN (both
@@ -582,21 +545,22 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
   if (g_g4_ablate & 2) {
     a_bytes = b_bytes = a2_bytes = b2_bytes = 0u;
   }
-#define DPFS_G4(AK_, BK_, OUT_)                                                                                   \
-  do {                                                                                                            \
-    if (g_g4_sched == 2)                                                                                          \
-      gemm4_k<AK_, BK_, OUT_, 2><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb,\
-                                                      ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb, rope,  \
-                                                      g_g4_group_m, dual);                                        \
-    else if (g_g4_sched == 1)                                                                                     \
-      gemm4_k<AK_, BK_, OUT_, 1><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb,\
-                                                      ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb, rope,  \
-                                                      g_g4_group_m, dual);                                        \
-    else                                                                                                          \
-      gemm4_k<AK_, BK_, OUT_, 0><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb,\
-                                                      ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb, rope,  \
-                                                      g_g4_group_m, dual);                                        \
-  } while (0)
+#define DPFS_G4(AK_, BK_, OUT_)                                                                                  \
+  gemm4_k<AK_, BK_, OUT_><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, \
+                                               kps, splits, slab_stride, a_bytes, b_bytes, cb, rope,            \
+                                               g_g4_group_m, dual, g_g4_ablate & ~3, nullptr)
+  if ((g_g4_ablate & 32) && g_g4_diag && layout == 0 && !out_f32) {
+    gemm4_k<true, true, 0, 2><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb,
+                                                   ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb, rope,
+                                                   g_g4_group_m, dual, g_g4_ablate & ~51, g_g4_diag);
+    return true;
+  }
+  if ((g_g4_ablate & 16) && g_g4_diag && layout == 0 && !out_f32) {
+    gemm4_k<true, true, 0, 1><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb,
+                                                      ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb, rope,
+                                                      g_g4_group_m, dual, g_g4_ablate & ~19, g_g4_diag);
+    return true;
+  }
   if (layout == 0) {
     if (out_f32) DPFS_G4(true, true, 1);
     else DPFS_G4(true, true, 0);

@@ -87,8 +87,11 @@ def _pick(key: Tuple, cands: Dict[str, Callable], lt_count: Callable[[], int] = 
         # two rounds per candidate, best of each: robust to a collective running alongside
         times = {name: min(_ms(fn), _ms(fn)) for name, fn in cands.items()}
         c = min(times, key=times.get)
-        if c != "ours" and "ours" in times and times[c] >= 0.97 * times["ours"]:
-            c = "ours"
+        ours_t = {n: t for n, t in times.items() if n.startswith("ours")}
+        if not c.startswith("ours") and ours_t:
+            best = min(ours_t, key=ours_t.get)
+            if times[c] >= 0.97 * ours_t[best]:
+                c = best
         _choice[key] = c
         _times[key] = times
     return c
@@ -96,6 +99,33 @@ def _pick(key: Tuple, cands: Dict[str, Callable], lt_count: Callable[[], int] = 
 
 def _lt_index(c: str) -> int:
     return int(c[2:])
+
+
+_V4_BIT = {"nt": 1, "nn": 2, "tn": 4}
+
+
+def _ours_variants(k, layout: str, fn: Callable[[], torch.Tensor]) -> Dict[str, Callable]:
+    """Our candidates for one call: ``ours`` = the v4 kernel (one wave per SIMD, 128 x 128 per
+    wave, csrc/kernels/gemm4.hip), ``ours3`` = the v3 kernel (8 waves, gemm.hip).  Which of
+    the two wins depends on the shape (the epilogue / K-loop balance), so both are timed."""
+    if not hasattr(k, "gemm_v4_mask"):
+        return {"ours": fn}
+    bit = _V4_BIT[layout]
+
+    def with_mask(on: bool):
+        def run():
+            old = k.gemm_v4_get_mask()
+            k.gemm_v4_mask((old | bit) if on else (old & ~bit))
+            try:
+                return fn()
+            finally:
+                k.gemm_v4_mask(old)
+        return run
+    return {"ours": with_mask(True), "ours3": with_mask(False)}
+
+
+def _run_ours(k, layout: str, choice: str, fn: Callable[[], torch.Tensor]):
+    return _ours_variants(k, layout, fn).get(choice, fn)()
 
 
 # Below this many rows (decode steps, tiny batches) our 256-row tiles are mostly padding and
@@ -154,10 +184,10 @@ def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, out=None) -> torch.T
     if m == "lt":
         return lt(0)() if lt_ok and _lt_count(k, 0, M, N, K, bias is not None) else blas()
     key = ("nt", M, N, K, bias is not None, x.device.index)
-    c = _pick(key, {"ours": ours, "blas": blas}, lambda: _lt_count(k, 0, M, N, K, bias is not None),
-              lt if lt_ok else None)
-    if c == "ours" or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
-        return ours()
+    c = _pick(key, {**_ours_variants(k, "nt", ours), "blas": blas},
+              lambda: _lt_count(k, 0, M, N, K, bias is not None), lt if lt_ok else None)
+    if c.startswith("ours") or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
+        return _run_ours(k, "nt", c, ours)
     return blas() if c == "blas" else lt(_lt_index(c))()
 
 
@@ -204,9 +234,10 @@ def gemm_nn(k, a: torch.Tensor, b: torch.Tensor, out=None) -> torch.Tensor:
     if m == "lt":
         return lt(0)() if lt_ok and _lt_count(k, 1, M, N, K, False) else blas()
     key = ("nn", M, N, K, a.device.index)
-    c = _pick(key, {"ours": ours, "blas": blas}, lambda: _lt_count(k, 1, M, N, K, False), lt if lt_ok else None)
-    if c == "ours" or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
-        return ours()
+    c = _pick(key, {**_ours_variants(k, "nn", ours), "blas": blas}, lambda: _lt_count(k, 1, M, N, K, False),
+              lt if lt_ok else None)
+    if c.startswith("ours") or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
+        return _run_ours(k, "nn", c, ours)
     return blas() if c == "blas" else lt(_lt_index(c))()
 
 
@@ -247,10 +278,10 @@ def gemm_nt_rope(k, x: torch.Tensor, w: torch.Tensor, bias, pos, tab, rot_heads:
     if m == "lt":
         return lt(0)() if lt_ok and _lt_count(k, 0, M, N, K, bias is not None) else blas()
     key = ("nt_rope", M, N, K, hd, x.device.index)
-    c = _pick(key, {"ours": ours, "blas": blas}, lambda: _lt_count(k, 0, M, N, K, bias is not None),
-              lt if lt_ok else None)
-    if c == "ours" or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
-        return ours()
+    c = _pick(key, {**_ours_variants(k, "nt", ours), "blas": blas},
+              lambda: _lt_count(k, 0, M, N, K, bias is not None), lt if lt_ok else None)
+    if c.startswith("ours") or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
+        return _run_ours(k, "nt", c, ours)
     return blas() if c == "blas" else lt(_lt_index(c))()
 
 
@@ -311,6 +342,9 @@ def gemm_tn(k, a: torch.Tensor, b: torch.Tensor, out=None, accumulate: bool = Fa
                 dst, acc = torch.empty(M, N, device=a.device, dtype=torch.float32), False
             k.lt_run(2, a, b, dst, None, _lt_index(kind), acc)
             return dst
+        if kind == "ours3" or kind == "ours":
+            fn = (lambda: k.gemm_tn(a, b, dst, acc)) if dst is not None else (lambda: k.gemm_tn(a, b))
+            return _run_ours(k, "tn", kind, fn)
         return k.gemm_tn(a, b, dst, acc) if dst is not None else k.gemm_tn(a, b)
     m = mode()
     if m == "ours" or a.shape[0] < _MIN_ROWS:
@@ -326,6 +360,8 @@ def gemm_tn(k, a: torch.Tensor, b: torch.Tensor, out=None, accumulate: bool = Fa
     if c is None:
         scratch = torch.zeros(M, N, device=a.device, dtype=torch.float32)
         cands = {"ours": lambda: run("ours", scratch, accumulate)}
+        if hasattr(k, "gemm_v4_mask"):
+            cands["ours3"] = lambda: run("ours3", scratch, accumulate)
         if blas_ok:
             cands["blas"] = lambda: run("blas", scratch, accumulate)
         c = _pick(key, cands, lambda: _lt_count(k, 2, M, N, K, False),

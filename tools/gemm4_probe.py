@@ -61,8 +61,10 @@ def main():
     ap.add_argument("--check-only", action="store_true")
     ap.add_argument("--scheds", type=int, nargs="+", default=[0, 1, 2])
     ap.add_argument("--no-blas", action="store_true")
+    ap.add_argument("--diag", action="store_true",
+                    help="NT only: DIAG build's per-wave cycle split (step waits / bodies / epilogues), s_memtime")
     ap.add_argument("--ablate", type=int, nargs="*", default=[],
-                    help="extra v4 arms with timing-only ablations (1 no stores, 2 zero operands, 3 both)")
+                    help="extra v4 arms with timing-only ablations (bits: 1 no stores, 2 zero operands, 4 no DMA wait, 8 no step barrier)")
     a = ap.parse_args()
     C = _ext.require()
     gen = torch.Generator(device="cuda").manual_seed(0)
@@ -86,6 +88,25 @@ def main():
                   flush=True)
             if a.check_only:
                 continue
+            for dmode in ((16, 32) if a.diag and layout == "nt" else ()):
+                d = torch.zeros(256 * 4 * 4, dtype=torch.int64, device="cuda")
+                C.gemm4_diag(d)
+                C.gemm_v4_mask(7)
+                C.gemm4_ablate(dmode)
+                ours(C)
+                torch.cuda.synchronize()
+                C.gemm4_ablate(0)
+                C.gemm4_diag(torch.empty(0))
+                v = d.view(-1, 4).double()
+                v = v[v[:, 3] > 0]
+                tiles = ((M + 255) // 256) * ((N + 255) // 256)
+                per = tiles / (v.shape[0] / 4)
+                tot = v[:, :3].sum(1)
+                print(f"{layout} {name} DIAG{'' if dmode == 16 else '(no DMA issued)'} per wave (s_memtime ticks, mean over {v.shape[0]} waves, {per:.1f} tiles "
+                      f"per WG): wait {v[:, 0].mean():.0f}  body {v[:, 1].mean():.0f}  epilogue {v[:, 2].mean():.0f}  "
+                      f"-> per tile wait {v[:, 0].mean() / per:.0f} body {v[:, 1].mean() / per:.0f} "
+                      f"epi {v[:, 2].mean() / per:.0f}; shares wait {(v[:, 0] / tot).mean():.3f} "
+                      f"epi {(v[:, 2] / tot).mean():.3f}", flush=True)
             arms = [f"v4s{sc}" for sc in a.scheds] + [f"abl{x}" for x in a.ablate] + ["v3"] + \
                 ([] if a.no_blas else ["blas"])
             ts = {k: [] for k in arms}
