@@ -42,6 +42,12 @@ PROMPTS = [
 ]
 
 
+def _backend(use_cuda: bool) -> str:
+    """RCCL on GPUs; ``DPFS_BACKEND=gloo`` runs several ranks on one GPU (the TP collectives
+    then go through ``DPFS_TP_COMM``'s transports, e.g. the xGMI kernels)."""
+    return os.environ.get("DPFS_BACKEND") or ("nccl" if use_cuda else "gloo")
+
+
 def get_test_args(argv=None):
     p = ArgumentParser()
     g = p.add_argument_group("distributed")
@@ -111,7 +117,7 @@ def greedy_decode(model: Transformer, prompt_ids, bos: int, eos: int, max_len: i
 def test(rank, args):
     set_seed(args.random_seed)
     use_cuda = (args.device or ("cuda" if torch.cuda.is_available() else "cpu")) == "cuda"
-    p = init_dist_env(args, rank, world_size=args.tp_size, backend="nccl" if use_cuda else "gloo")
+    p = init_dist_env(args, rank, world_size=args.tp_size, backend=_backend(use_cuda))
     dev = torch.device("cuda", torch.cuda.current_device()) if use_cuda else torch.device("cpu")
     margs = get_preset(args.model)
     model = Transformer.from_args(margs).to(dev)

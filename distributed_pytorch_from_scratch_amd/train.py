@@ -42,6 +42,12 @@ from .utils.tb import SummaryWriter
 MI355X_BF16_PEAK = 2.5e15
 
 
+def _backend(use_cuda: bool) -> str:
+    """RCCL on GPUs; ``DPFS_BACKEND=gloo`` runs several ranks on one GPU (the TP collectives
+    then go through ``DPFS_TP_COMM``'s transports, e.g. the xGMI kernels)."""
+    return os.environ.get("DPFS_BACKEND") or ("nccl" if use_cuda else "gloo")
+
+
 def get_train_args(argv=None) -> Namespace:
     p = ArgumentParser()
     g = p.add_argument_group("distributed")
@@ -91,9 +97,9 @@ def train(rank, args: Namespace):
     use_cuda = (args.device or ("cuda" if torch.cuda.is_available() else "cpu")) == "cuda"
     if rank is None:
         p = init_dist_env(rank=None, tp_size=args.tp_size, dp_size=args.dp_size,
-                          backend="nccl" if use_cuda else "gloo")
+                          backend=_backend(use_cuda))
     else:
-        p = init_dist_env(args, rank, world_size=world, backend="nccl" if use_cuda else "gloo")
+        p = init_dist_env(args, rank, world_size=world, backend=_backend(use_cuda))
     grank = dist.get_rank()
     dev = torch.device("cuda", torch.cuda.current_device()) if use_cuda else torch.device("cpu")
     compute_dtype = torch.bfloat16 if (use_cuda or args.bf16) else torch.float32

@@ -89,6 +89,8 @@ def init_dist_env(args: Optional[Namespace] = None, rank: Optional[int] = None, 
         opts = dist.ProcessGroupNCCL.Options()
         opts.is_high_priority_stream = True
         kw["pg_options"] = opts
+    elif os.environ.get("DPFS_BACKEND") == "gloo" and torch.cuda.is_available():
+        torch.cuda.set_device(local_rank % torch.cuda.device_count())
     if not dist.is_initialized():
         dist.init_process_group(backend=backend, init_method="env://", world_size=world_size,
                                 rank=rank, timeout=datetime.timedelta(seconds=timeout_s), **kw)

@@ -33,8 +33,11 @@ def _models(args):
 
 
 @pytest.mark.parametrize("preset,T", [("plumbing", 128), ("gpt2-small", 256)])
-def test_gpu_loss_and_grads_match_cpu(dist1, preset, T):
+def test_gpu_loss_and_grads_match_cpu(dist1, monkeypatch, preset, T):
+    """Every GEMM on our kernels (gemm.hip / gemm4.hip, no hipBLASLt candidate): loss within
+    1 % and every parameter gradient within 2 % (relative L2) of the fp32 CPU oracle."""
     from distributed_pytorch_from_scratch_amd.models import get_preset
+    monkeypatch.setenv("DPFS_GEMM_BACKEND", "ours")
     args = get_preset(preset, num_layers=2)
     cpu, gpu = _models(args)
     g = torch.Generator().manual_seed(1)
@@ -46,12 +49,68 @@ def test_gpu_loss_and_grads_match_cpu(dist1, preset, T):
     lc.backward()
     lg = gpu.loss(ids.cuda(), pos.cuda(), tgt.cuda())
     lg.backward()
-    assert abs(lc.item() - lg.item()) < 2e-2 * max(1.0, abs(lc.item()))
+    assert abs(lc.item() - lg.item()) < 1e-2 * max(1.0, abs(lc.item()))
     gc = dict(cpu.named_parameters())
+    rels = {}
     for n, p in gpu.named_parameters():
         ref = gc[n].grad
-        rel = ((p.grad.cpu() - ref).norm() / (ref.norm() + 1e-12)).item()
-        assert rel < 6e-2, (n, rel)
+        rels[n] = ((p.grad.cpu() - ref).norm() / (ref.norm() + 1e-12)).item()
+    worst = max(rels, key=rels.get)
+    print(f"{preset}: loss cpu {lc.item():.5f} gpu {lg.item():.5f}; worst grad rel err {worst} {rels[worst]:.2e}")
+    assert rels[worst] < 2e-2, (worst, rels[worst])
+
+
+def test_bf16_loss_curve_tracks_vanilla_reference(dist1, monkeypatch):
+    """200 Adam steps of our engine (fused schedule, native kernels, every GEMM ours) against
+    the plain-PyTorch formulation of the reference model (tests/vanilla_model.py, materialised
+    softmax, nn.Linear) under bf16 autocast, same init and the same batches: the final losses
+    (mean of the last 20 steps) agree within 1 %.  Data: next token = current + r, r uniform in
+    {1..4}, so the loss floor is ln 4 and the curve has a long tail to compare."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from vanilla_model import VanillaTransformer
+    from distributed_pytorch_from_scratch_amd.models import ModelArgs, Transformer
+    from distributed_pytorch_from_scratch_amd.ops.optim import FusedAdam
+    from distributed_pytorch_from_scratch_amd.engine import TrainStep
+    from distributed_pytorch_from_scratch_amd.utils.dist import set_seed
+    monkeypatch.setenv("DPFS_GEMM_BACKEND", "ours")
+    cfg = dict(attn_dim=256, ffn_dim=512, num_heads=4, num_layers=2, vocab_size=1024, maxlen=256)
+    STEPS, B, T = 200, 8, 128
+    ours = Transformer.from_args(ModelArgs(**cfg, vocab_pad_to=1))
+    set_seed(0)
+    ours.reset_parameters()
+    van = VanillaTransformer(**cfg)
+    torch.manual_seed(0)
+    van.reset_parameters()
+    assert torch.equal(van.lm_head.weight, ours.lm_head.weight)     # same init (RNG replay)
+    ours, van = ours.cuda(), van.cuda()
+    van.cos, van.sin = van.cos.cuda(), van.sin.cuda()
+    step = TrainStep(ours, FusedAdam(ours.parameters(), lr=1e-3))
+    vopt = torch.optim.Adam(van.parameters(), lr=1e-3)
+    g = torch.Generator().manual_seed(3)
+    pos = torch.arange(T, device="cuda").repeat(B, 1)
+    lo, lv = [], []
+    for _ in range(STEPS):
+        start = torch.randint(0, 1024, (B, 1), generator=g)
+        seq = (start + torch.randint(1, 5, (B, T), generator=g).cumsum(1)) % 1024
+        ids, tgt = seq[:, :-1].cuda(), seq[:, 1:].cuda()
+        p = pos[:, :T - 1]
+        lo.append(step(ids, p, tgt))
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            logits = van(ids, p)
+        loss = torch.nn.functional.cross_entropy(logits.float().reshape(-1, 1024), tgt.reshape(-1))
+        vopt.zero_grad()
+        loss.backward()
+        vopt.step()
+        lv.append(loss.detach())
+    lo = [float(x) for x in lo]
+    lv = [float(x) for x in lv]
+    fo, fv = sum(lo[-20:]) / 20, sum(lv[-20:]) / 20
+    print(f"loss curve: ours {lo[0]:.4f} -> {fo:.4f}, vanilla {lv[0]:.4f} -> {fv:.4f}; "
+          f"max |diff| over steps {max(abs(a - b) for a, b in zip(lo, lv)):.4f}")
+    assert abs(lo[0] - lv[0]) < 1e-2 * lv[0]
+    assert fv < lv[0] - 2.0, "the reference formulation did not learn"
+    assert abs(fo - fv) < 1e-2 * fv, (fo, fv)
 
 
 def test_gpu_training_memorizes_batch(dist1):
