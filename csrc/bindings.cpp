@@ -763,7 +763,7 @@ torch::Tensor attn_decode(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, t
   check_len(len);
   TORCH_CHECK(kc.sizes() == vc.sizes(), "k / v cache shapes differ");
   const int64_t B = kc.size(0), Tmax = kc.size(1), H = kc.size(2), hd = kc.size(3);
-  TORCH_CHECK(hd == 64 || hd == 128, "attn_decode: head_dim 64 or 128");
+  TORCH_CHECK(hd == 32 || hd == 64 || hd == 128, "attn_decode: head_dim 32, 64 or 128");
   TORCH_CHECK(q.size(0) == B && q.size(1) >= H * hd && q.stride(0) % 8 == 0 && q.scalar_type() == torch::kBFloat16,
               "attn_decode: q rows");
   const at::DeviceGuard g(q.device());

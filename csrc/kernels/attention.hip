@@ -713,6 +713,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv_k(const 
       for (int j = 0; j < 4; ++j) {
         const int ki = wk0 + 16 * kt + 4 * g + j;
         if (ki < T) {
+          DPFS_KASSERT(rpos[(long long)b * T + ki] >= 0, "rope position at key %d", ki);
           const float* tr = rtab + rpos[(long long)b * T + ki] * HD;
 #pragma unroll
           for (int d = 0; d < DT / 2; ++d) {
@@ -990,6 +991,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv2_k(
     for (int j = 0; j < 4; ++j) {
       const int ki = wk0 + 4 * g + j;
       if (ki < T) {
+        DPFS_KASSERT(rpos[(long long)b * T + ki] >= 0, "rope position at key %d", ki);
         const float* tr = rtab + rpos[(long long)b * T + ki] * HD;
 #pragma unroll
         for (int d = 0; d < DT / 2; ++d) {
@@ -1220,6 +1222,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
 #pragma unroll
       for (int d = 0; d < DT; ++d) dq[c][d] *= scale;
       if (rpos) {
+        DPFS_KASSERT(rpos[(long long)b * T + qi] >= 0, "rope position at query %d", qi);
         const float* tr = rtab + rpos[(long long)b * T + qi] * HD;
 #pragma unroll
         for (int d = 0; d < DT / 2; ++d) {

@@ -13,6 +13,26 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Device-side bounds asserts of the DPFS_KERNEL_ASSERT=1 build (python tools/build_ext.py
+// --kernel-assert -> _C_kassert*.so, loaded when DPFS_KERNEL_ASSERT=1 is set at run time):
+// a failed check prints the file, line, condition and the offending values, then traps the
+// wave (the launch fails with a device exception at the next synchronisation).  In the
+// default build the macro is empty, so the hot kernels carry no extra instruction.
+#if defined(DPFS_KERNEL_ASSERT) && DPFS_KERNEL_ASSERT
+#define DPFS_KASSERT(cond, fmt, ...)                                                             \
+  do {                                                                                          \
+    if (!(cond)) {                                                                              \
+      printf("[dpfs kernel assert] %s:%d: %s (block %d, thread %d): " fmt "\n", __FILE__, __LINE__, \
+             #cond, (int)blockIdx.x, (int)threadIdx.x, ##__VA_ARGS__);                          \
+      __builtin_trap();                                                                         \
+    }                                                                                           \
+  } while (0)
+#else
+#define DPFS_KASSERT(cond, fmt, ...) \
+  do {                               \
+  } while (0)
+#endif
+
 namespace dpfs {
 
 typedef __bf16 bf16;

@@ -71,16 +71,19 @@ __global__ __launch_bounds__(256) void attn_decode_split_k(const bf16* __restric
   const float lsum = wave_sum(p);
   p_lds[wave][l] = p;
   __syncthreads();
-  // P.V: lane = (key group kg = l >> 3, dim group dg = l & 7); each lane walks 8 keys
-  const int kg = l >> 3, dg = l & 7;
-  constexpr int DPL = HD / 8;              // dims per lane (8 at hd 64, 16 at hd 128)
+  // P.V: lane = (key group kg, dim group dg) with DG dim groups of DPL dims (16-byte V
+  // loads); each lane walks DG keys of the wave's 64, then the KG key groups are summed.
+  constexpr int DG = HD >= 64 ? 8 : HD / 8;   // dim groups: 8 at hd 64 / 128, 4 at hd 32
+  constexpr int DPL = HD / DG;                // dims per lane: 8 (hd 32 / 64) or 16 (hd 128)
+  constexpr int KG = 64 / DG;                 // key groups
+  const int kg = l / DG, dg = l % DG;
   float o[DPL];
 #pragma unroll
   for (int j = 0; j < DPL; ++j) o[j] = 0.f;
   const int kw0 = k0 + wave * 64;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int kk = kg + 8 * i;             // key within the wave's 64
+  for (int i = 0; i < DG; ++i) {
+    const int kk = kg + KG * i;             // key within the wave's 64
     const float pk = p_lds[wave][kk];
     if (kw0 + kk < L) {
       const bf16* vrow = vc + (((long long)b * Tmax + kw0 + kk) * H + h) * HD + dg * DPL;
@@ -94,11 +97,10 @@ __global__ __launch_bounds__(256) void attn_decode_split_k(const bf16* __restric
     }
   }
 #pragma unroll
-  for (int j = 0; j < DPL; ++j) {          // sum over the 8 key groups (lanes l ^ 8, 16, 32)
+  for (int j = 0; j < DPL; ++j) {          // sum over the key groups (lanes l ^ DG, 2 DG, ...)
     float v = o[j];
-    v += __shfl_xor(v, 8, 64);
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
+#pragma unroll
+    for (int x = DG; x < 64; x <<= 1) v += __shfl_xor(v, x, 64);
     o[j] = v;
   }
   if (kg == 0) {
@@ -141,7 +143,8 @@ __global__ __launch_bounds__(64) void attn_decode_combine_k(const float* __restr
   const float* p = part + (long long)bh * nsplit * (HD + 2);
   float M = -INFINITY;
   for (int s = 0; s < live; ++s) M = fmaxf(M, p[s * (HD + 2)]);
-  constexpr int DPL = HD / 64;
+  constexpr int DPL = HD >= 64 ? HD / 64 : 1;   // hd 32: lanes >= 32 idle
+  const bool on = (int)threadIdx.x < HD;
   float acc[DPL];
 #pragma unroll
   for (int j = 0; j < DPL; ++j) acc[j] = 0.f;
@@ -151,12 +154,14 @@ __global__ __launch_bounds__(64) void attn_decode_combine_k(const float* __restr
     const float f = __expf(ps[0] - M);
     ls += f * ps[1];
 #pragma unroll
-    for (int j = 0; j < DPL; ++j) acc[j] += f * ps[2 + threadIdx.x + 64 * j];
+    for (int j = 0; j < DPL; ++j)
+      if (on) acc[j] += f * ps[2 + threadIdx.x + 64 * j];
   }
   const float inv = 1.f / ls;
   bf16* orow = o + (long long)b * ldo + (long long)h * HD;
 #pragma unroll
-  for (int j = 0; j < DPL; ++j) orow[threadIdx.x + 64 * j] = (bf16)(acc[j] * inv);
+  for (int j = 0; j < DPL; ++j)
+    if (on) orow[threadIdx.x + 64 * j] = (bf16)(acc[j] * inv);
 }
 
 // cache[b, *len, h, :] = src rows (k and v parts of the packed qkv row of sequence b)
@@ -265,6 +270,7 @@ __global__ __launch_bounds__(256) void rope_append_k(bf16* __restrict__ qkv, lon
       const int b = i / rot_per_b, r = i - b * rot_per_b;
       const int head = r / q8, f0 = (r - head * q8) * 8;
       bf16* base = qkv + (long long)b * ld + head * HD;
+      DPFS_KASSERT(pos[b] >= 0, "decode position %lld of sequence %d", (long long)pos[b], b);
       const float* tr = tab + pos[b] * (long long)HD;
       const bf16x8 xa = *reinterpret_cast<const bf16x8*>(base + f0);
       const bf16x8 xb = *reinterpret_cast<const bf16x8*>(base + h2 + f0);
@@ -312,7 +318,11 @@ extern "C" void dpfs_attn_decode(const void* q, long long ldq, const void* kc, c
                                  hipStream_t s) {
   const int ns = dpfs_decode_nsplit(Tmax);
   const dim3 grid(ns, B * H);
-  if (HD == 64) {
+  if (HD == 32) {
+    attn_decode_split_k<32><<<grid, 256, 0, s>>>((const bf16*)q, ldq, (const bf16*)kc, (const bf16*)vc, len_ptr, H,
+                                                  Tmax, scale, part);
+    attn_decode_combine_k<32><<<B * H, 64, 0, s>>>(part, ns, len_ptr, (bf16*)o, ldo, H);
+  } else if (HD == 64) {
     attn_decode_split_k<64><<<grid, 256, 0, s>>>((const bf16*)q, ldq, (const bf16*)kc, (const bf16*)vc, len_ptr, H,
                                                   Tmax, scale, part);
     attn_decode_combine_k<64><<<B * H, 64, 0, s>>>(part, ns, len_ptr, (bf16*)o, ldo, H);

@@ -112,6 +112,7 @@ __global__ __launch_bounds__(256) void rope_vec_k(T* __restrict__ qkv, const int
     const int rem = i - row * per_row;
     const int head = rem / qn;
     const int f0 = (rem - head * qn) * N;
+    DPFS_KASSERT(pos[row] >= 0, "position %lld at row %d", (long long)pos[row], row);
     const float* tr = table + pos[row] * (long long)hd;
     T* base = qkv + (long long)row * ld + head * hd;
     float x1[N], x2[N], c[N], sn[N];

@@ -159,6 +159,8 @@ __device__ __forceinline__ Item decode(int lin, int nwg, int tiles_m, int tiles_
   it.n0 = (r / gsz) * 256;
   it.kb = it.split * kps;
   it.ke = min(K, it.kb + kps);
+  DPFS_KASSERT(it.m0 < tiles_m * 256 && it.n0 < tiles_n * 256 && it.kb < K,
+               "item %d -> tile (%d, %d) k %d", lin, it.m0, it.n0, it.kb);
   it.sel = 0;
   if (it.kb >= k_switch) {
     it.sel = 1;
@@ -203,6 +205,7 @@ __device__ __forceinline__ void epilogue(const char* bias_lds, bool has_bias, co
       });
       const int m = ci.m0 + wm * 128 + 16 * i + (l & 15);
       if (do_rope) {
+        DPFS_KASSERT(m >= M || rope.pos[m] >= 0, "rope position %lld at row %d", (long long)rope.pos[m], m);
         const float* tr = rope.tab + (m < M ? rope.pos[m] : 0) * rope.hd;
         const int half = rope.hd >> 1;
         const int hj = half >> 4;   // tiles per half head: 2 (hd 64) or 4 (hd 128)

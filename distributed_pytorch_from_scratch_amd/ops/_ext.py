@@ -22,8 +22,9 @@ def _load():
     global _C, _ERR
     if _C is not None or _ERR is not None:
         return
+    name = "_C_kassert" if kernel_assert() else "_C"
     try:
-        _C = importlib.import_module("distributed_pytorch_from_scratch_amd._C")
+        _C = importlib.import_module("distributed_pytorch_from_scratch_amd." + name)
     except Exception as e:  # pragma: no cover - depends on build state
         _ERR = e
 
@@ -46,7 +47,8 @@ def require():
     if _C is None:
         raise RuntimeError(
             "distributed_pytorch_from_scratch_amd._C (HIP kernels for gfx950) is not built or "
-            f"failed to load: {_ERR!r}. Run `python tools/build_ext.py` "
+            f"failed to load: {_ERR!r}. Run `python tools/build_ext.py"
+            f"{' --kernel-assert' if kernel_assert() else ''}` "
             "(or __graft_entry__.build()).")
     if debug_sync() or nan_check():
         if _PROXY is None:
@@ -58,6 +60,13 @@ def require():
 def so_path() -> str | None:
     _load()
     return getattr(_C, "__file__", None) if _C is not None else None
+
+
+def kernel_assert() -> bool:
+    """``DPFS_KERNEL_ASSERT=1``: load the bounds-assert build ``_C_kassert`` (built by
+    ``python tools/build_ext.py --kernel-assert``) instead of ``_C``; there is no fallback to the
+    unchecked build."""
+    return os.environ.get("DPFS_KERNEL_ASSERT", "0") == "1"
 
 
 def debug_sync() -> bool:

@@ -19,9 +19,11 @@ Sequence-parallel variants (``sequence_parallel=True``) replace the all-reduce p
 all-gather / reduce-scatter over the token dimension (Megatron-SP), the same bytes on the
 wire but norms/residuals then run on ``T/tp`` tokens per rank.
 
-All GEMMs go through the kernel API (``ops.dispatch.K``): hand-written MFMA kernels on GPU,
-fp32 torch on CPU.  The weight is an fp32 master parameter; the GEMMs read its cached bf16
-shadow (``ops.dispatch.shadow``) and write the weight gradient in fp32.
+All GEMMs go through ``ops.gemm_select`` (``GS.gemm_*``): on GPU it times, once per shape,
+our MFMA kernels (``csrc/kernels/gemm4.hip`` and ``gemm.hip``) against hipBLASLt and keeps the
+faster (``DPFS_GEMM_BACKEND=ours`` pins ours, ``blas`` pins hipBLASLt); on CPU it is fp32
+torch.  The weight is an fp32 master parameter; the GEMMs read its cached bf16 shadow
+(``ops.dispatch.shadow``) and write the weight gradient in fp32.
 """
 from __future__ import annotations
 

@@ -360,7 +360,7 @@ def test_swiglu_bwd_fused_bias_grad(C, M, F):
     assert torch.equal(dgu, C.swiglu_bwd(dh, gu))
 
 
-@pytest.mark.parametrize("hd", [64, 128])
+@pytest.mark.parametrize("hd", [32, 64, 128])
 @pytest.mark.parametrize("L", [0, 255, 256, 699])
 def test_decode_attention_and_kv_append(C, hd, L):
     """Split-K single-query attention over a KV cache (csrc/kernels/decode.hip) against the

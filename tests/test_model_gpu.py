@@ -346,3 +346,38 @@ def test_native_rccl_communicator(dist1):
     assert torch.equal(y, x) and torch.equal(part, x) and torch.equal(gat, x) and torch.equal(z, z0)
     assert c.error() is None
     c.close()
+
+
+_KASSERT_SCRIPT = r"""
+import os, torch
+from distributed_pytorch_from_scratch_amd.utils.dist import init_dist_env, destroy_dist_env
+from distributed_pytorch_from_scratch_amd.models import get_preset, Transformer
+from distributed_pytorch_from_scratch_amd.models.generation import generate
+from distributed_pytorch_from_scratch_amd.ops import _ext
+init_dist_env(rank=0, tp_size=1, world_size=1, backend="nccl")
+m = Transformer.from_args(get_preset("gpt2-small", num_layers=2)).cuda()
+m.reset_parameters()
+ids = torch.randint(0, 50257, (2, 256), device="cuda")
+pos = torch.arange(256, device="cuda").repeat(2, 1)
+m.loss(ids, pos, ids).backward()
+m.eval()
+out = generate(m, ids[:, :40], max_new_tokens=8)
+torch.cuda.synchronize()
+print("KASSERT_OK", os.path.basename(_ext.so_path()), len(out[0]))
+destroy_dist_env()
+"""
+
+
+def test_kernel_assert_build_runs_clean(tmp_path):
+    """DPFS_KERNEL_ASSERT=1 loads the bounds-assert build (_C_kassert, tools/build_ext.py
+    --kernel-assert) and a training step + KV-cache decode run through it without a trip."""
+    import glob
+    if not glob.glob(os.path.join(ROOT, "distributed_pytorch_from_scratch_amd", "_C_kassert*.so")):
+        pytest.fail("_C_kassert not built (python tools/build_ext.py --kernel-assert)")
+    env = dict(os.environ, PYTHONPATH=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT="29583", DPFS_KERNEL_ASSERT="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-c", _KASSERT_SCRIPT], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "KASSERT_OK _C_kassert" in r.stdout and " 48" in r.stdout, r.stdout

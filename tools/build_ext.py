@@ -8,8 +8,10 @@ Two-stage native build, no hipify, no JIT cache:
 3. link with the ROCm runtime, RCCL and hipBLASLt that PyTorch itself ships (``torch/lib``), so
    the process has exactly one instance of each.
 
-Usage: ``python tools/build_ext.py [--jobs N] [--force]`` (also called by
-``__graft_entry__.build()``).
+Usage: ``python tools/build_ext.py [--jobs N] [--force] [--kernel-assert]`` (also called by
+``__graft_entry__.build()``).  ``--kernel-assert`` builds the debug variant ``_C_kassert*.so``
+(``-DDPFS_KERNEL_ASSERT=1``: device-side bounds asserts, ``csrc/kernels/common.h``) next to the
+default one, from its own object directory; ``DPFS_KERNEL_ASSERT=1`` at run time loads it.
 """
 from __future__ import annotations
 
@@ -50,25 +52,26 @@ def _run(cmd):
     return r.stdout
 
 
-def ext_path() -> str:
-    return os.path.join(PKG, "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+def ext_path(kernel_assert: bool = False) -> str:
+    return os.path.join(PKG, ("_C_kassert" if kernel_assert else "_C") + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
-def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> str:
+def build(jobs: int = 8, force: bool = False, verbose: bool = True, kernel_assert: bool = False) -> str:
     import torch
     from torch.utils import cpp_extension as ce
 
-    os.makedirs(OBJ, exist_ok=True)
+    obj_dir = OBJ + ("_kassert" if kernel_assert else "")
+    os.makedirs(obj_dir, exist_ok=True)
     hipcc = _hipcc()
     headers = glob.glob(os.path.join(CSRC, "kernels", "*.h")) + glob.glob(os.path.join(CSRC, "comm", "*.h"))
     kernels = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))) + \
         sorted(glob.glob(os.path.join(CSRC, "comm", "*.hip"))) + \
         sorted(glob.glob(os.path.join(CSRC, "blas", "*.hip")))
     hip_flags = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
-                 "-munsafe-fp-atomics", "-Wno-unused-result"]
+                 "-munsafe-fp-atomics", "-Wno-unused-result"] + (["-DDPFS_KERNEL_ASSERT=1"] if kernel_assert else [])
     jobs_list = []
     for k in kernels:
-        o = os.path.join(OBJ, os.path.basename(k) + ".o")
+        o = os.path.join(obj_dir, os.path.basename(k) + ".o")
         if force or _newer([k] + headers, o):
             jobs_list.append([hipcc] + hip_flags + ["-c", k, "-o", o])
     # Host bindings: plain g++ against the torch headers (HIP runtime headers for types).
@@ -76,10 +79,10 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> str:
     py_inc = sysconfig.get_paths()["include"]
     inc = ce.include_paths(device_type="cuda") if "device_type" in ce.include_paths.__code__.co_varnames else ce.include_paths(cuda=True)
     b_src = os.path.join(CSRC, "bindings.cpp")
-    b_obj = os.path.join(OBJ, "bindings.o")
+    b_obj = os.path.join(obj_dir, "bindings.o")
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
     cxx_flags = ["-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
-                 f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+                 f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=" + ("_C_kassert" if kernel_assert else "_C"), "-DTORCH_API_INCLUDE_EXTENSION_H",
                  "-I" + py_inc, "-I" + os.path.join(rocm, "include"), "-Wno-deprecated-declarations"]
     for i in inc:
         cxx_flags.append("-I" + i)
@@ -93,8 +96,8 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> str:
                 f.result()
                 if verbose:
                     print("[build_ext] compiled", os.path.basename(c[-1]), flush=True)
-    objs = [os.path.join(OBJ, os.path.basename(k) + ".o") for k in kernels] + [b_obj]
-    out = ext_path()
+    objs = [os.path.join(obj_dir, os.path.basename(k) + ".o") for k in kernels] + [b_obj]
+    out = ext_path(kernel_assert)
     if force or jobs_list or not os.path.exists(out):
         tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
         link = ["g++", "-shared", "-o", out] + objs + [
@@ -111,8 +114,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--kernel-assert", action="store_true", help="build the bounds-assert variant _C_kassert")
     a = ap.parse_args()
-    build(a.jobs, a.force)
+    build(a.jobs, a.force, kernel_assert=a.kernel_assert)
 
 
 if __name__ == "__main__":
