@@ -26,6 +26,8 @@ void dpfs_gemm_v4_mask(int);
 void dpfs_gemm4_sched(int);
 void dpfs_gemm4_ablate(int);
 void dpfs_gemm4_diag(void*);
+void dpfs_attn_diag(void*);
+void dpfs_attn_fwd_persist(int);
 int dpfs_gemm_v4_get_mask();
 void dpfs_gemm_force(int, int);
 void dpfs_gemm_v2_sched(int);
@@ -1071,6 +1073,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "layouts on the v4 kernel (one wave per SIMD, 128x128 per wave): bit 1 NT, 2 NN, 4 TN; 0 = all on v3");
   m.def("gemm_v4_get_mask", []() { return dpfs_gemm_v4_get_mask(); });
   m.def("gemm4_ablate", [](int v) { dpfs_gemm4_ablate(v); }, "timing-only: 1 = drop stores, 2 = zero operands");
+  m.def("attn_fwd_persist", [](int v) { dpfs_attn_fwd_persist(v); },
+        "forward v3 grid: 1 = persistent (resident blocks walk the items), 0 = one block per item");
+  m.def("attn_diag", [](torch::Tensor t) { dpfs_attn_diag(t.defined() && t.numel() ? t.data_ptr() : nullptr); },
+        "int64 buffer [grid*4*4] for attn_set_impl(5): the forward's per-wave cycle split (wait / QK / softmax / PV)");
   m.def("gemm4_diag", [](torch::Tensor t) { dpfs_gemm4_diag(t.defined() && t.numel() ? t.data_ptr() : nullptr); },
         "int64 buffer [grid*4*4] for the DIAG build's per-wave cycle split (gemm4_ablate bit 16)");
   m.def("gemm4_sched", [](int v) { dpfs_gemm4_sched(v); },
@@ -1097,7 +1103,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_", &rope_, py::arg("qkv"), py::arg("positions"), py::arg("table"), py::arg("n_rot_heads"),
         py::arg("head_dim"), py::arg("inverse") = false);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("scale"), py::arg("causal") = true);
-  m.def("attn_set_impl", [](int v) { dpfs_attn_set_impl(v); }, "1 = register-staged (default), 2 = LDS-DMA ring 8-wave, 3 = LDS-DMA ring 4-wave");
+  m.def("attn_set_impl", [](int v) { dpfs_attn_set_impl(v); },
+        "forward: 0 = auto (default), 1 = 16x16x32 register-staged, 2 / 3 = LDS-DMA ring 8 / 4 waves, "
+        "4 = 32x32x16 LDS-DMA ring (hd 64 / 128), 5 = its DIAG build");
   m.def("attn_set_bwd_impl", [](int v) { dpfs_attn_set_bwd_impl(v); }, "dK/dV kernel: 2 = LDS-DMA ring (default), 1 = register-staged");
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("scale"), py::arg("causal"), py::arg("dq"), py::arg("dk"), py::arg("dv"),

@@ -24,6 +24,8 @@
 //  * causal: key tiles above the diagonal are never visited; heaviest q-blocks launch first.
 #include "common.h"
 
+#include <algorithm>
+
 namespace dpfs {
 
 constexpr float kLog2e = 1.4426950408889634f;
@@ -531,6 +533,402 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd2_k(
         *reinterpret_cast<bf16x4*>(orow + 16 * d + 4 * g) = v;
       }
       if (g == 0) LSE[((long long)b * H + h) * T + qi] = (m[c] + __log2f(ls)) * kLn2;
+    }
+  }
+}
+
+// ============================================================ forward (32x32x16 MFMA) ==
+// v_mfma_f32_32x32x16_bf16 holds the SIMD's vector issue for 8 of its 32 cycles, the
+// 16x16x32 form for 8 of 16: per FLOP the 32x32 shape leaves 3x the issue slots for the
+// softmax VALU that runs beside it (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'),
+// which is what bounds attention at head_dim 64.  Block: 4 waves x 32 queries; K/V tiles of
+// 64 keys by LDS-DMA into a 3-deep ring (tile t+2 in flight while t is computed).
+//
+//  * S^T = K Q^T per wave: 2 key halves x HD/16 k-steps; lane (r = l&31, h = l>>5) owns query
+//    column r and keys 8(i>>2) + 4h + (i&3) of each half (C/D map), so registers 8s..8s+7 of
+//    a half are, packed to bf16, directly the B operand of k-step s of O^T = V^T P^T (guide
+//    §3 'An accumulator tile as the next MFMA's operand'); the permuted k order is absorbed
+//    by the V^T fragment's transposed reads (rows 16s + 4h + 0..3 and + 8..11).
+//  * K and V tiles carry separate XOR swizzles, each conflict-free for its one read pattern:
+//    K rows by ds_read_b128 (16-lane groups span 16 rows), V by ds_read_b64_tr_b16 (32-lane
+//    groups span 4 rows x 64 B).
+//  * online softmax with the deferred rescale of attn_fwd_k (m moves only when a row's tile max
+//    exceeds it by 2^8); the row statistics of lanes l and l^32 (same query, other keys) meet
+//    in one v_permlane32_swap, only on that rare branch and in the epilogue.
+template <int HD>
+__device__ __forceinline__ int swz_k(int r, int ch) {
+  return HD == 64 ? (ch ^ ((r >> 1) & 7)) : (ch ^ (r & 15));
+}
+template <int HD>
+__device__ __forceinline__ int swz_v(int r, int ch) {
+  return HD == 64 ? (ch ^ (((r >> 1) & 1) << 2)) : (ch ^ ((r & 3) << 2));
+}
+
+// Per-lane source offsets of a wave's K/V pieces (the swizzle is a function of the tile
+// row, so they are tile-invariant); a tile's pieces then cost one scalar descriptor each.
+template <int HD, int NW>
+struct KvDma3 {
+  static constexpr int CPR = HD / 8, TILE = 64 * HD * 2, P = 2 * TILE / 1024, PW = P / NW;
+  static_assert(PW >= 2 && PW * NW == P, "pieces must divide over the waves");
+  unsigned voff[PW];
+  __device__ __forceinline__ void init(long long ldk, long long ldv) {
+    const int l = lane_id(), wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const bool isv = i >= PW / 2;                 // pieces wave + NW i: K first, then V
+      const int jj = wave + NW * i - (isv ? P / 2 : 0);
+      const int pos = jj * 64 + l;
+      const int r = pos / CPR, cp = pos % CPR;
+      const int ch = isv ? swz_v<HD>(r, cp) : swz_k<HD>(r, cp);   // XOR swizzles are involutions
+      voff[i] = (unsigned)(((long long)r * (isv ? ldv : ldk) + ch * 8) * 2);
+    }
+  }
+  // tile rows [kv0, kv0 + 64) -> stage (K at 0, V at TILE); rows >= T fall outside the
+  // descriptor's range and read as zeros.
+  __device__ __forceinline__ void issue(const bf16* kbase, const bf16* vbase, long long ldk, long long ldv, int T,
+                                        int kv0, char* stage) const {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const unsigned ks = (unsigned)(((long long)(T - 1 - kv0) * ldk + HD) * 2);
+    const unsigned vs = (unsigned)(((long long)(T - 1 - kv0) * ldv + HD) * 2);
+    const __amdgpu_buffer_rsrc_t rk =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(kbase + (long long)kv0 * ldk), (short)0, (int)ks, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(vbase + (long long)kv0 * ldv), (short)0, (int)vs, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const bool isv = i >= PW / 2;
+      const int jj = wave + NW * i - (isv ? P / 2 : 0);
+      dma16(isv ? rv : rk, stage + (isv ? TILE : 0) + jj * 1024, voff[i]);
+    }
+  }
+};
+
+#define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
+
+// max / sum of x over lanes l and l ^ 32 (the two lanes of one 32x32 C/D column).
+__device__ __forceinline__ float pair_max(float x) {
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float pair_sum(float x) {
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+// DIAG = 1: per-wave s_memtime split (wait + barrier / QK^T + mask + max / exp + pack / P.V /
+// block starts / block ends) into diag[block][wave][10] (timing build only; the stamps cost
+// ~10 %).
+__device__ __forceinline__ unsigned long long stamp_dep(float dep) {
+  unsigned long long t;
+  asm volatile("; stamp after %0" ::"v"(dep));
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+__device__ __forceinline__ unsigned long long realtime() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
+// Work cursor of the persistent forward: item it = (b, h, pair p) -> query blocks nqb-1-p
+// (heavy) then p (light), equal causal work for every pair; item it serves (b, h) index
+// 8 (it / 8 / NP) + it % 8, so with a grid that is a multiple of 8 all items of a head run on
+// one XCD (workgroups are dealt to the XCDs round-robin) and its K / V stay in that L2.
+struct FwdCur {
+  int it, sub, t, nkv, qb, bh;
+};
+__device__ __forceinline__ bool fwd_cur_fix(FwdCur& c, int n_items, int NP, int nqb, int BH, int T, int causal) {
+  while (c.it < n_items) {
+    const int rest = c.it >> 3, p = rest % NP;
+    c.bh = (rest / NP) * 8 + (c.it & 7);
+    if (c.bh < BH) {
+      const int nsub = (nqb - 1 - p == p) ? 1 : 2;
+      if (c.sub < nsub) {
+        c.qb = c.sub == 0 ? nqb - 1 - p : p;
+        c.nkv = ((causal ? min(T, (c.qb + 1) * 128) : T) + 63) / 64;
+        return true;
+      }
+    }
+    c.it += gridDim.x;
+    c.sub = 0;
+    c.t = 0;
+  }
+  return false;
+}
+__device__ __forceinline__ bool fwd_cur_next(FwdCur& c, int n_items, int NP, int nqb, int BH, int T, int causal) {
+  if (++c.t < c.nkv) return true;
+  c.t = 0;
+  ++c.sub;
+  return fwd_cur_fix(c, n_items, NP, nqb, BH, T, causal);
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (jump over the immediates 0..63).
+__device__ __forceinline__ void wait_vm_rt(int n) {
+  switch (n) {
+#define DPFS_W(N_) \
+  case N_: wait_vmcnt<N_>(); break;
+    DPFS_W(0) DPFS_W(1) DPFS_W(2) DPFS_W(3) DPFS_W(4) DPFS_W(5) DPFS_W(6) DPFS_W(7) DPFS_W(8) DPFS_W(9)
+    DPFS_W(10) DPFS_W(11) DPFS_W(12) DPFS_W(13) DPFS_W(14) DPFS_W(15) DPFS_W(16) DPFS_W(17) DPFS_W(18)
+    DPFS_W(19) DPFS_W(20) DPFS_W(21) DPFS_W(22) DPFS_W(23) DPFS_W(24) DPFS_W(25) DPFS_W(26) DPFS_W(27)
+    DPFS_W(28) DPFS_W(29) DPFS_W(30) DPFS_W(31) DPFS_W(32) DPFS_W(33) DPFS_W(34) DPFS_W(35) DPFS_W(36)
+    DPFS_W(37) DPFS_W(38) DPFS_W(39) DPFS_W(40) DPFS_W(41) DPFS_W(42) DPFS_W(43) DPFS_W(44) DPFS_W(45)
+    DPFS_W(46) DPFS_W(47) DPFS_W(48) DPFS_W(49) DPFS_W(50) DPFS_W(51) DPFS_W(52) DPFS_W(53) DPFS_W(54)
+    DPFS_W(55) DPFS_W(56) DPFS_W(57) DPFS_W(58) DPFS_W(59) DPFS_W(60) DPFS_W(61) DPFS_W(62) DPFS_W(63)
+#undef DPFS_W
+    default: wait_vmcnt<0>(); break;
+  }
+}
+
+// Persistent: each workgroup walks items (fwd_cur_fix) one query block at a time.  The K/V
+// tiles of a block come by LDS-DMA into a 3-slot ring two tiles ahead; the ring numbering runs
+// on across blocks, so in a block's last tile (after its QK^T, when Q is dead and the two
+// slots ahead are free) the workgroup already fetches the next block's Q (buffer loads, rows
+// >= T read as zeros) and its first two tiles, and the fetch flies under the softmax, P.V and
+// epilogue.  O / LSE go out as buffer stores (rows >= T dropped by the descriptor), so every
+// wave issues the same vector-memory operations and the counted vmcnt waits are exact.
+template <int HD, int DIAG = 0>
+__global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
+                                                     const bf16* __restrict__ V, bf16* __restrict__ O,
+                                                     float* __restrict__ LSE, int T, int H, int BH, long long ldq,
+                                                     long long ldk, long long ldv, long long ldo, float scale,
+                                                     int causal, unsigned long long* __restrict__ diag = nullptr) {
+  constexpr int NW = 4, BQ = 32 * NW, BKV = 64, KS = HD / 16, DTN = HD / 32, RB = HD * 2;
+  constexpr int TILE = BKV * RB, STAGE = 2 * TILE, NST = 3;
+  constexpr int PW = 2 * TILE / 1024 / NW;   // DMA pieces per wave per tile
+  constexpr int ST = DTN * 4 + 1;            // stores per wave per query block (O + LSE)
+  static_assert(PW + ST < 64, "vmcnt range");
+  __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
+  const int nqb = (T + BQ - 1) / BQ;
+  const int NP = (nqb + 1) / 2;
+  const int n_items = (BH + 7) / 8 * 8 * NP;
+  const int wave = threadIdx.x >> 6, l = lane_id(), r32 = l & 31, hf = l >> 5, g16 = l >> 4, i16 = l & 15;
+  const float c2 = scale * kLog2e;
+
+  unsigned long long d_acc[6] = {0, 0, 0, 0, 0, 0}, d_t0 = 0, d_t1 = 0, d_start = 0, d_rt0 = 0, d_sb = 0;
+  if constexpr (DIAG) {
+    d_start = stamp_dep(0.f);
+    d_rt0 = realtime();
+  }
+
+  FwdCur c = {(int)blockIdx.x, 0, 0, 0, 0, 0};
+  if (!fwd_cur_fix(c, n_items, NP, nqb, BH, T, causal)) return;   // block-uniform
+  KvDma3<HD, NW> dma;
+  dma.init(ldk, ldv);
+  int koff[2][KS];   // K A-fragment (half kh, k-step ks): row 32 kh + r32, chunk 2 ks + hf
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int r = 32 * kh + r32;
+      koff[kh][ks] = r * RB + (swz_k<HD>(r, 2 * ks + hf) << 4);
+    }
+  const unsigned qspan = (unsigned)(((long long)(T - 1) * ldq + HD) * 2);
+  const unsigned ospan = (unsigned)(((long long)(T - 1) * ldo + HD) * 2);
+  bf16x8 qf[KS];
+  // next block's Q (Q^T operand: lane holds Q[q0 + 32 wave + r32][16 ks + 8 hf + j]) and its
+  // first two tiles into ring slots s0, s0 + 1
+  auto fetch_block = [&](const FwdCur& n, int s0) __attribute__((always_inline)) {
+    const int b = n.bh / H, h = n.bh % H;
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Q + (long long)b * T * ldq + (long long)h * HD), (short)0, (int)qspan, 0x00020000);
+    const int qi = n.qb * BQ + wave * 32 + r32;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const unsigned off = (unsigned)(((long long)qi * ldq + 16 * ks + 8 * hf) * 2);
+      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(qf[ks]) : "v"(off), "s"(rq));
+    }
+    const bf16* kb = K + (long long)b * T * ldk + (long long)h * HD;
+    const bf16* vb = V + (long long)b * T * ldv + (long long)h * HD;
+    dma.issue(kb, vb, ldk, ldv, T, 0, smem + s0 * STAGE);
+    if (n.nkv > 1) dma.issue(kb, vb, ldk, ldv, T, BKV, smem + (s0 + 1 == NST ? 0 : s0 + 1) * STAGE);
+  };
+
+  fetch_block(c, 0);
+  int base = 0;          // ring slot of the block's tile 0
+  bool firstb = true;
+  while (true) {
+    const int b = c.bh / H, h = c.bh % H;
+    const bf16* kb = K + (long long)b * T * ldk + (long long)h * HD;
+    const bf16* vb = V + (long long)b * T * ldv + (long long)h * HD;
+    const int nkv = c.nkv, q0 = c.qb * BQ, wq0 = q0 + wave * 32, qi = wq0 + r32;
+    FwdCur n = c;
+    n.t = nkv - 1;
+    const bool nv = fwd_cur_next(n, n_items, NP, nqb, BH, T, causal);   // the next block, if any
+    f32x16 o[DTN];
+#pragma unroll
+    for (int d = 0; d < DTN; ++d)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[d][i] = 0.f;
+    float m = -INFINITY, lsum = 0.f;
+    int slot = base;
+    for (int t = 0; t < nkv; ++t) {
+      // tile t landed; what was issued after its DMA may still fly: the next tile (PW) and,
+      // for tiles 0 / 1 of all but the first block, the previous block's stores (ST)
+      if constexpr (DIAG) d_t0 = stamp_dep(0.f);
+      const bool nxt = t + 1 < nkv;
+      if (t >= 2 || firstb) {
+        if (nxt) wait_vmcnt<PW>();
+        else wait_vmcnt<0>();
+      } else {
+        if (nxt) wait_vmcnt<PW + ST>();
+        else wait_vmcnt<ST>();
+      }
+      __builtin_amdgcn_s_barrier();
+      if constexpr (DIAG) {
+        d_t1 = stamp_dep(0.f);
+        d_acc[0] += d_t1 - d_t0;
+      }
+      const char* lk = smem + slot * STAGE;
+      const char* lv = lk + TILE;
+      const int s1 = slot + 1 == NST ? 0 : slot + 1, s2 = s1 + 1 == NST ? 0 : s1 + 1;
+      if (t + 2 < nkv) dma.issue(kb, vb, ldk, ldv, T, (t + 2) * BKV, smem + s2 * STAGE);
+      const int kv0 = t * BKV;
+      const bool last = t + 1 == nkv;
+      const bool active = !causal || kv0 <= wq0 + 31;   // wave-uniform
+      f32x16 s[2];
+      if (active) {
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) s[kh][i] = 0.f;
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(lk + koff[kh][ks]);
+            s[kh] = MFMA32(kf, qf[ks], s[kh]);
+          }
+        }
+      }
+      if (last && nv) {
+        __builtin_amdgcn_sched_barrier(0);
+        fetch_block(n, s1);   // Q is dead; slots s1, s2 held tiles t-2, t-1 (all waves past them)
+      }
+      if (active) {
+        // V^T fragments (asm transposed reads: no compiler vmcnt(0) with the DMA in flight)
+        __builtin_amdgcn_sched_barrier(0);
+        constexpr int NVH = 2 * DTN * 4;
+        s16x4 vh[(NVH + 15) / 16 * 16];
+#pragma unroll
+        for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+          for (int k4 = 0; k4 < 4; ++k4) {
+            const int row = 16 * k4 + 4 * hf + (i16 >> 2);
+            const int col = 32 * dt + 16 * (g16 & 1) + 4 * (i16 & 3);
+            const int ch = col >> 3, bo = (col & 7) * 2;
+            vh[2 * (dt * 4 + k4)] = ds_tr16(lv + row * RB + (swz_v<HD>(row, ch) << 4) + bo);
+            vh[2 * (dt * 4 + k4) + 1] = ds_tr16(lv + (row + 8) * RB + (swz_v<HD>(row + 8, ch) << 4) + bo);
+          }
+        const bool need_mask = __builtin_amdgcn_readfirstlane(
+            (int)((causal && kv0 + BKV - 1 > wq0) || (kv0 + BKV > T)));
+        if (need_mask) {
+          // key kv0 + 32 kh + 8 (i>>2) + 4 hf + (i&3) is valid iff its tile offset <= lim
+          const int lim = (causal ? min(qi, T - 1) : T - 1) - kv0 - 4 * hf;
+#pragma unroll
+          for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              s[kh][i] = (32 * kh + 8 * (i >> 2) + (i & 3) > lim) ? -INFINITY : s[kh][i];
+        }
+        // lane max as a 4-way tree (short dependency chains)
+        float mq[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mq[j] = fmaxf(s[j >> 1][8 * (j & 1)], s[j >> 1][8 * (j & 1) + 1]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 2; i < 8; ++i) mq[j] = fmaxf(mq[j], s[j >> 1][8 * (j & 1) + i]);
+        const float mx = fmaxf(fmaxf(mq[0], mq[1]), fmaxf(mq[2], mq[3]));
+        if constexpr (DIAG) {
+          const unsigned long long t2 = stamp_dep(mx);
+          d_acc[1] += t2 - d_t1;
+          d_t1 = t2;
+        }
+        // deferred rescale (as attn_fwd_k): m moves only when a row's tile max exceeds it by 2^8;
+        // every visited tile has a valid key for every query row (kv0 <= wq0), so m is finite
+        // after the first tile
+        constexpr float kDefer = 8.f;
+        if (__builtin_amdgcn_ballot_w64(mx * c2 > m + kDefer) != 0) {
+          const float mr = pair_max(mx) * c2;   // both lanes of a row decide together
+          const float mnew = mr > m + kDefer ? mr : m;
+          const float alpha = mnew == m ? 1.f : __builtin_amdgcn_exp2f(m - mnew);
+          m = mnew;
+          lsum *= alpha;
+#pragma unroll
+          for (int d = 0; d < DTN; ++d) o[d] *= alpha;
+        }
+        float ps[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float e = __builtin_amdgcn_exp2f(fmaf(s[kh][i], c2, -m));
+            s[kh][i] = e;
+            ps[(kh * 16 + i) >> 3] += e;
+          }
+        lsum += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+        bf16x8 pk[4];
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pk[k4][j] = (bf16)s[k4 >> 1][8 * (k4 & 1) + j];
+        if constexpr (DIAG) {
+          const unsigned long long t3 = stamp_dep(__builtin_bit_cast(float, __builtin_bit_cast(u32x4, pk[3])[0]));
+          d_acc[2] += t3 - d_t1;
+          d_t1 = t3;
+        }
+#pragma unroll
+        for (int w = 0; w < (NVH + 15) / 16; ++w) tr_wait8(*reinterpret_cast<s16x4(*)[16]>(&vh[16 * w]));
+#pragma unroll
+        for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+          for (int k4 = 0; k4 < 4; ++k4) {
+            const bf16x8 vf = tr_join(vh[2 * (dt * 4 + k4)], vh[2 * (dt * 4 + k4) + 1]);
+            o[dt] = MFMA32(vf, pk[k4], o[dt]);
+          }
+        if constexpr (DIAG) d_acc[3] += stamp_dep(o[DTN - 1][15]) - d_t1;
+      }
+      slot = s1;
+    }
+    // epilogue: O[q][d] = O^T[d][q] / l (lane: rows 32 dt + 8 g + 4 hf + 0..3 of column q);
+    // lse = (m + log2 l) ln 2.  Buffer stores: rows >= T fall outside the descriptor.
+    if constexpr (DIAG) d_sb = stamp_dep(0.f);
+    {
+      const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(O + (long long)b * T * ldo + (long long)h * HD), (short)0, (int)ospan, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(LSE + (long long)c.bh * T), (short)0, T * 4, 0x00020000);
+      const float ls = pair_sum(lsum);
+      const float inv = 1.f / ls;
+#pragma unroll
+      for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 v = {(bf16)(o[dt][4 * g] * inv), (bf16)(o[dt][4 * g + 1] * inv), (bf16)(o[dt][4 * g + 2] * inv),
+                      (bf16)(o[dt][4 * g + 3] * inv)};
+          const unsigned off = (unsigned)(((long long)qi * ldo + 32 * dt + 8 * g + 4 * hf) * 2);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), ro, off, 0, 0);
+        }
+      if (hf == 0)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((m + __log2f(ls)) * kLn2), rl, (unsigned)qi * 4u, 0, 0);
+    }
+    if constexpr (DIAG) d_acc[5] += stamp_dep(0.f) - d_sb;
+    if (!nv) break;
+    base = slot;           // the slot after the last tile's
+    c = n;
+    firstb = false;
+  }
+  if constexpr (DIAG) {
+    if (l == 0) {
+      unsigned long long* dp = diag + ((long long)blockIdx.x * 4 + wave) * 10;
+      dp[0] = d_acc[0];
+      dp[1] = d_acc[1];
+      dp[2] = d_acc[2];
+      dp[3] = d_acc[3];
+      dp[4] = d_start;
+      dp[5] = stamp_dep(0.f);
+      dp[6] = d_rt0;
+      dp[7] = realtime();
+      dp[8] = d_acc[4];
+      dp[9] = d_acc[5];
     }
   }
 }
@@ -1303,8 +1701,27 @@ using namespace dpfs;
 
 extern "C" int dpfs_attn_supported_hd(int hd) { return hd == 32 || hd == 64 || hd == 128; }
 
-static int g_attn_impl = 1;  // 1 = register-staged (default, fastest measured), 2 / 3 = LDS-DMA ring with 8 / 4 waves
+// Forward implementation: 0 = auto (default: attn_fwd3_k at head_dim 64, attn_fwd_k otherwise),
+// 1 = attn_fwd_k (16x16x32, register-staged), 2 / 3 = attn_fwd2_k (LDS-DMA ring, 8 / 4 waves),
+// 4 = attn_fwd3_k (32x32x16, LDS-DMA ring, hd 64 / 128), 5 = its DIAG build (hd 64).
+static int g_attn_impl = 0;
 extern "C" void dpfs_attn_set_impl(int v) { g_attn_impl = v; }
+static int attn_cu_count() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+static unsigned long long* g_attn_diag = nullptr;
+// fwd v3 grid: 0 = one workgroup per item (default: the dispatcher refills freed slots, which
+// balances the end of the kernel), 1 = persistent (one round of resident workgroups)
+static int g_attn_fwd_persist = 0;
+extern "C" void dpfs_attn_fwd_persist(int v) { g_attn_fwd_persist = v; }   // impl 5: attn_fwd3_k DIAG build, [grid][4 waves][4]
+extern "C" void dpfs_attn_diag(void* p) { g_attn_diag = (unsigned long long*)p; }
 static int g_attn_bwd_impl = 2;  // dK/dV kernel: 2 = LDS-DMA ring (default), 1 = register-staged,
                                  // 3 = register-staged with 32 keys per wave (hd <= 64)
 extern "C" void dpfs_attn_set_bwd_impl(int v) { g_attn_bwd_impl = v; }
@@ -1312,14 +1729,30 @@ extern "C" void dpfs_attn_set_bwd_impl(int v) { g_attn_bwd_impl = v; }
 extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int T, int H,
                               int hd, long long ldq, long long ldk, long long ldv, long long ldo, float scale,
                               int causal, hipStream_t s) {
-  if (g_attn_impl == 2) {
+  if (impl == 2) {
     dim3 g8((T + 255) / 256, B * H);
     DPFS_HD_DISPATCH(hd, attn_fwd2_k<HD_, 8><<<g8, 512, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
                                                                 (bf16*)o, lse, T, H, ldq, ldk, ldv, ldo, scale,
                                                                 causal));
     return;
   }
-  if (g_attn_impl == 3) {
+  const int impl = g_attn_impl == 0 ? (hd == 64 ? 4 : 1) : g_attn_impl;
+  if ((impl == 4 || (impl == 5 && g_attn_diag)) && (hd == 64 || hd == 128)) {
+    const int nqb = (T + 127) / 128, items = (B * H + 7) / 8 * 8 * ((nqb + 1) / 2);
+    const int per_cu = hd == 64 ? 3 : 1;           // resident blocks per CU (VGPRs / LDS)
+    const int grid = g_attn_fwd_persist ? std::min(items, std::max(8, attn_cu_count() * per_cu / 8 * 8)) : items;
+    if (hd == 64 && impl == 5)
+      attn_fwd3_k<64, 1><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, T, H,
+                                              B * H, ldq, ldk, ldv, ldo, scale, causal, g_attn_diag);
+    else if (hd == 64)
+      attn_fwd3_k<64><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, T, H,
+                                           B * H, ldq, ldk, ldv, ldo, scale, causal);
+    else
+      attn_fwd3_k<128><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, T, H,
+                                            B * H, ldq, ldk, ldv, ldo, scale, causal);
+    return;
+  }
+  if (impl == 3) {
     dim3 g4((T + 127) / 128, B * H);
     DPFS_HD_DISPATCH(hd, attn_fwd2_k<HD_, 4><<<g4, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
                                                                 (bf16*)o, lse, T, H, ldq, ldk, ldv, ldo, scale,

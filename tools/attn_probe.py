@@ -22,8 +22,12 @@ def main():
     ap.add_argument("--impl", type=int, nargs="+", default=[2])
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--bwd", action="store_true")
+    ap.add_argument("--persist", type=int, default=1, help="forward v3: persistent grid (1) or one block per item (0)")
+    ap.add_argument("--diag", action="store_true",
+                    help="forward v3 DIAG build (impl 5): per-wave s_memtime split wait / QK+max / exp+pack / PV")
     a = ap.parse_args()
     C = _ext.require()
+    C.attn_fwd_persist(a.persist)
     B, T, H, hd = a.B, a.T, a.H, a.hd
     qkv = torch.randn(B * T, 3 * H * hd, device="cuda").bfloat16()
     q, k, v = (qkv[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
@@ -52,10 +56,49 @@ def main():
             oi, li = C.attn_fwd(q, k, v, scale, True)
             print(f"impl {impl} vs 1: max|dO| {(oi.float() - o1.float()).abs().max().item():.3e} "
                   f"max|dLSE| {(li - l1).abs().max().item():.3e}", flush=True)
+    if a.diag and not a.bwd:
+        grid = ((T + 127) // 128) * B * H
+        d = torch.zeros(grid * 40, dtype=torch.int64, device="cuda")
+        C.attn_diag(d)
+        C.attn_set_impl(5)
+        C.attn_fwd(q, k, v, scale, True)
+        torch.cuda.synchronize()
+        C.attn_set_impl(0)
+        C.attn_diag(torch.empty(0))
+        torch.save(d.cpu(), os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", "attn_diag.pt"))
+        w10 = d.view(-1, 10).double()
+        w10 = w10[w10[:, 7] > 0]                # the persistent grid uses fewer blocks than the item count
+        pro = w10[:, 8]
+        w8 = w10[:, :8]
+        print(f"DIAG per wave, block prologues {pro.mean():.0f} ticks, epilogues {w10[:, 9].mean():.0f} ticks", flush=True)
+        w = w8[:, :4]
+        life = w8[:, 5] - w8[:, 4]
+        span = (w8[:, 5].max() - w8[:, 4].min()).item()
+        rt = w8[:, 7] - w8[:, 6]
+        rspan = (w8[:, 7].max() - w8[:, 6].min()).item()
+        print(f"DIAG realtime (100 MHz): kernel span {rspan / 100:.1f} us, wave life mean {rt.mean() / 100:.2f} us; "
+              f"s_memtime ticks per us {(life / rt).mean() * 100:.0f}; sum of wave lives / (span x 12 waves x 256 CUs) "
+              f"{rt.sum().item() / rspan / (256 * 12) * 100:.1f}%", flush=True)
+        ev = torch.cat([torch.stack([w8[:, 6], torch.ones_like(rt)], 1), torch.stack([w8[:, 7], -torch.ones_like(rt)], 1)])
+        ev = ev[ev[:, 0].argsort()]
+        conc = ev[:, 1].cumsum(0)
+        tq = [(w8[:, 6].min() + f * rspan).item() for f in (0.1, 0.25, 0.5, 0.75, 0.9)]
+        cq = [conc[(ev[:, 0] <= x).nonzero().max()].item() for x in tq]
+        print(f"DIAG resident waves: max {conc.max().item():.0f}; at 10/25/50/75/90% of the span {cq}", flush=True)
+        print(f"DIAG kernel span {span:.0f} ticks; wave life mean {life.mean():.0f} (loop share "
+              f"{(w.sum(1) / life).mean() * 100:.1f}%), sum of wave lives / (span x resident waves) "
+              f"{life.sum().item() / span / (256 * 12) * 100:.1f}%", flush=True)
+        tot = w.sum(1)
+        names = ["wait+barrier", "QK+mask+max", "exp+pack", "PV"]
+        print("DIAG per wave (s_memtime ticks): " + "  ".join(
+            f"{n} {w[:, i].mean():.0f} ({(w[:, i] / tot).mean() * 100:.1f}%)" for i, n in enumerate(names)), flush=True)
+        heavy = w[tot > tot.quantile(0.9)]
+        print("DIAG heaviest 10% waves: " + "  ".join(f"{n} {heavy[:, i].mean():.0f}" for i, n in enumerate(names)),
+              flush=True)
     res = timeit({impl: mk(impl) for impl in a.impl}, iters=a.iters, rounds=5)  # interleaved, median
     for impl, ms in res.items():
         print(f"impl {impl} {'bwd' if a.bwd else 'fwd'}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF", flush=True)
-    C.attn_set_impl(1)
+    C.attn_set_impl(0)
     C.attn_set_bwd_impl(2)
 
 
