@@ -1729,6 +1729,7 @@ extern "C" void dpfs_attn_set_bwd_impl(int v) { g_attn_bwd_impl = v; }
 extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int T, int H,
                               int hd, long long ldq, long long ldk, long long ldv, long long ldo, float scale,
                               int causal, hipStream_t s) {
+  const int impl = g_attn_impl == 0 ? (hd == 64 ? 4 : 1) : g_attn_impl;
   if (impl == 2) {
     dim3 g8((T + 255) / 256, B * H);
     DPFS_HD_DISPATCH(hd, attn_fwd2_k<HD_, 8><<<g8, 512, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
@@ -1736,7 +1737,6 @@ extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void*
                                                                 causal));
     return;
   }
-  const int impl = g_attn_impl == 0 ? (hd == 64 ? 4 : 1) : g_attn_impl;
   if ((impl == 4 || (impl == 5 && g_attn_diag)) && (hd == 64 || hd == 128)) {
     const int nqb = (T + 127) / 128, items = (B * H + 7) / 8 * 8 * ((nqb + 1) / 2);
     const int per_cu = hd == 64 ? 3 : 1;           // resident blocks per CU (VGPRs / LDS)
