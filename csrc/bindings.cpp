@@ -1106,7 +1106,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_set_impl", [](int v) { dpfs_attn_set_impl(v); },
         "forward: 0 = auto (default), 1 = 16x16x32 register-staged, 2 / 3 = LDS-DMA ring 8 / 4 waves, "
         "4 = 32x32x16 LDS-DMA ring (hd 64 / 128), 5 = its DIAG build");
-  m.def("attn_set_bwd_impl", [](int v) { dpfs_attn_set_bwd_impl(v); }, "dK/dV kernel: 2 = LDS-DMA ring (default), 1 = register-staged");
+  m.def("attn_set_bwd_impl", [](int v) { dpfs_attn_set_bwd_impl(v); }, "dK/dV kernel: 0 = auto (default), 1 = register-staged, 2 = LDS-DMA ring, 3 = 32 keys per wave, 4 = 32x32x16 key-on-lane (hd 64)");
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("scale"), py::arg("causal"), py::arg("dq"), py::arg("dk"), py::arg("dv"),
         py::arg("rope_pos") = py::none(), py::arg("rope_tab") = py::none(), py::arg("dbias") = py::none());

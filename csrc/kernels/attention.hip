@@ -1444,6 +1444,302 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv2_k(
   }
 }
 
+// ======================================================== bwd: dK, dV (32x32x16 MFMA) ==
+// Key on the lane (guide §B 'Attention backward'): a wave owns 32 keys; S = Q K^T and dP =
+// dO V^T are computed with the queries as the 32x32 C rows, so their accumulators, packed to
+// bf16, are directly the B operands of dV^T += dO^T P and dK^T += Q^T dS (registers 8s..8s+7
+// = k-step s over queries, §3 'An accumulator tile as the next MFMA's operand'), and dK^T /
+// dV^T stay in registers for the whole query sweep.  The row constants -lse/scale and
+// -delta enter as the initial accumulators of S and dP (read from the LDS stage), so
+// p = exp2(c2 S') and dS = p dP' need no per-element subtraction.  Q and dO tiles (64 rows)
+// stream through a 3-slot LDS-DMA ring; each tile is read by rows (A operands of S / dP) and
+// transposed (A operands of dV^T / dK^T, ds_read_b64_tr_b16), so both use one XOR swizzle
+// that is conflict-free for both patterns (swz_u).  A workgroup = 4 waves x 32 keys and
+// handles a causal pair of key blocks (p, nkb-1-p): the same work for every workgroup.
+template <int HD>
+__device__ __forceinline__ int swz_u(int r, int ch) {
+  const int m = r >> 1;
+  return ch ^ ((m & 7) ^ ((m & 1) << 2));   // hd 64: 8 chunks per row
+}
+
+// Q / dO rows [q0, q0 + 64) and the 64 lse / delta values of a query tile into one stage:
+// [Q tile | dO tile | lse (256 B) | delta (256 B) | dummy (512 B)].
+template <int HD>
+struct QdoDma3 {
+  static constexpr int CPR = HD / 8, TILE = 64 * HD * 2, P = 2 * TILE / 1024, PW = P / 4;
+  unsigned voff[PW];
+  __device__ __forceinline__ void init(long long ldq, long long lddo) {
+    const int l = lane_id(), wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const bool isdo = i >= PW / 2;
+      const int jj = wave + 4 * i - (isdo ? P / 2 : 0);
+      const int pos = jj * 64 + l;
+      const int r = pos / CPR, cp = pos % CPR;
+      voff[i] = (unsigned)(((long long)r * (isdo ? lddo : ldq) + swz_u<HD>(r, cp) * 8) * 2);
+    }
+  }
+  __device__ __forceinline__ void issue(const bf16* qb, const bf16* dob, const float* lsb, const float* dlb,
+                                        long long ldq, long long lddo, int T, int q0, char* stage) const {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = lane_id();
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(qb + (long long)q0 * ldq), (short)0, (int)(((long long)(T - 1 - q0) * ldq + HD) * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rdo = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(dob + (long long)q0 * lddo), (short)0, (int)(((long long)(T - 1 - q0) * lddo + HD) * 2), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const bool isdo = i >= PW / 2;
+      const int jj = wave + 4 * i - (isdo ? P / 2 : 0);
+      dma16(isdo ? rdo : rq, stage + (isdo ? TILE : 0) + jj * 1024, voff[i]);
+    }
+    // wave 0: lse, wave 1: delta, waves 2 / 3: a dummy piece (every wave issues PW + 1)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((wave == 1 ? dlb : lsb) + q0), (short)0, (T - q0) * 4, 0x00020000);
+    const unsigned soff = wave < 2 ? (unsigned)l * 4u : kOOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(stage + 2 * TILE + wave * 256),
+                                             4, soff, 0, 0, 0);
+  }
+};
+
+template <int HD>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv3_k(
+    const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V, const bf16* __restrict__ dO,
+    const float* __restrict__ LSN, const float* __restrict__ NDEL, bf16* __restrict__ dK, bf16* __restrict__ dV,
+    int T, int H, int BH, long long ldq, long long ldk, long long ldv, long long lddo, long long lddk,
+    long long lddv, float scale, int causal, const int64_t* __restrict__ rpos, const float* __restrict__ rtab,
+    float* __restrict__ BPK, float* __restrict__ BPV) {
+  // LSN = -lse log2(e) and NDEL = -delta per query row (written by attn_bwd_dq3_k).  BPK / BPV
+  // (optional): per (b, h, key block, wave) column sums of the stored dK / dV rows.
+  static_assert(HD == 64, "dK/dV v3: head_dim 64");
+  constexpr int BK = 128, BQ = 64, KS = HD / 16, DTN = HD / 32, RB = HD * 2;
+  constexpr int TILE = BQ * RB, BUF = 2 * TILE + 1024, NST = 3;
+  constexpr int PWV = QdoDma3<HD>::PW + 1;   // DMA instructions per wave per tile
+  __shared__ __attribute__((aligned(1024))) char smem[NST * BUF];
+  const int nkb = (T + BK - 1) / BK;
+  const int NP = (nkb + 1) / 2;
+  const int it = blockIdx.x;
+  const int bh = (it >> 3) / NP * 8 + (it & 7), p = (it >> 3) % NP;
+  if (bh >= BH) return;
+  const int b = bh / H, h = bh % H;
+  const int wave = threadIdx.x >> 6, l = lane_id(), r32 = l & 31, hf = l >> 5, g16 = l >> 4, i16 = l & 15;
+  const float c2 = scale * kLog2e;
+  const bf16* qbase = Q + (long long)b * T * ldq + (long long)h * HD;
+  const bf16* dobase = dO + (long long)b * T * lddo + (long long)h * HD;
+  const float* lsb = LSN + (long long)bh * T;
+  const float* dlb = NDEL + (long long)bh * T;
+  QdoDma3<HD> dma;
+  dma.init(ldq, lddo);
+  // lane-constant LDS offsets: row reads (row 32 qt + r32, chunk 2 ks + hf; the swizzle of
+  // row + 32 equals that of row, so qt is an immediate) and transposed reads (rows 16 s4 + 4 hf
+  // + (i16 >> 2) [+ 8], d columns 32 dt + 16 (g16 & 1) + 4 (i16 & 3); s4 is an immediate)
+  int roff[KS], toff[DTN][2];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) roff[ks] = r32 * RB + (swz_u<HD>(r32, 2 * ks + hf) << 4);
+#pragma unroll
+  for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int row = 4 * hf + (i16 >> 2) + 8 * e;
+      const int col = 32 * dt + 16 * (g16 & 1) + 4 * (i16 & 3);
+      toff[dt][e] = row * RB + (swz_u<HD>(row, col >> 3) << 4) + (col & 7) * 2;
+    }
+
+  for (int sub = 0; sub < 2; ++sub) {
+    const int kb = sub == 0 ? p : nkb - 1 - p;
+    if (sub == 1 && kb == p) break;
+    if (sub == 1) __syncthreads();   // the previous key block's ring slots are read
+    const int k0 = kb * BK, kw0 = k0 + 32 * wave, key = kw0 + r32;
+    const int qstart = causal ? (k0 / BQ) * BQ : 0;
+    const int nq = (T - qstart + BQ - 1) / BQ;
+    if (nq > 0) dma.issue(qbase, dobase, lsb, dlb, ldq, lddo, T, qstart, smem);
+    if (nq > 1) dma.issue(qbase, dobase, lsb, dlb, ldq, lddo, T, qstart + BQ, smem + BUF);
+    // K^T / V^T operands (B of S = Q K^T, dP = dO V^T): lane holds K[key][16 ks + 8 hf + j]
+    bf16x8 kf[KS], vf[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 a = {}, c = {};
+      if (key < T) {
+        a = *reinterpret_cast<const bf16x8*>(K + ((long long)b * T + key) * ldk + (long long)h * HD + 16 * ks + 8 * hf);
+        c = *reinterpret_cast<const bf16x8*>(V + ((long long)b * T + key) * ldv + (long long)h * HD + 16 * ks + 8 * hf);
+      }
+      kf[ks] = a;
+      vf[ks] = c;
+    }
+    wait_vmcnt<0>();
+    f32x16 dkt[DTN], dvt[DTN];
+#pragma unroll
+    for (int d = 0; d < DTN; ++d)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        dkt[d][i] = 0.f;
+        dvt[d][i] = 0.f;
+      }
+    int cur = 0;
+    for (int t = 0; t < nq; ++t) {
+      if (t + 1 < nq) wait_vmcnt<PWV>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      const char* lq = smem + cur * BUF;
+      const char* ldo_ = lq + TILE;
+      const float* ls = reinterpret_cast<const float*>(lq + 2 * TILE);
+      const float* ds = ls + 64;
+      int nb = cur + 2;
+      if (nb >= NST) nb -= NST;
+      cur = (cur + 1 == NST) ? 0 : cur + 1;
+      const int q0 = qstart + t * BQ;
+      if (t + 2 < nq) dma.issue(qbase, dobase, lsb, dlb, ldq, lddo, T, q0 + 2 * BQ, smem + nb * BUF);
+      if (causal && q0 + BQ - 1 < kw0) continue;   // wave-uniform: every query of the tile < every key
+      // S = Q K^T, dP = dO V^T (rows = queries 32 qt + 8 (i>>2) + 4 hf + (i&3), lane = key)
+      f32x16 sc[2], dp[2];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          sc[qt][i] = 0.f;
+          dp[qt][i] = 0.f;
+        }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          sc[qt] = MFMA32(*reinterpret_cast<const bf16x8*>(lq + roff[ks] + 32 * qt * RB), kf[ks], sc[qt]);
+          dp[qt] = MFMA32(*reinterpret_cast<const bf16x8*>(ldo_ + roff[ks] + 32 * qt * RB), vf[ks], dp[qt]);
+        }
+      }
+      // dO^T fragments (A of dV^T: lane d = 32 dt + r32, queries 16 s + 4 hf + 0..3 / 8..11)
+      __builtin_amdgcn_sched_barrier(0);
+      constexpr int NH = 2 * DTN * 4;
+      s16x4 th[(NH + 15) / 16 * 16];
+#pragma unroll
+      for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          th[2 * (dt * 4 + s4)] = ds_tr16(ldo_ + toff[dt][0] + 16 * s4 * RB);
+          th[2 * (dt * 4 + s4) + 1] = ds_tr16(ldo_ + toff[dt][1] + 16 * s4 * RB);
+        }
+      // p = exp2(c2 S - lse log2 e), dS = p (dP - delta): the row constants per register come
+      // from the stage (rows 32 qt + 8 g + 4 hf + 0..3 are 4 consecutive floats)
+      bf16x8 pp[4], pd[4];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        f32x4 lsr[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) lsr[g] = *reinterpret_cast<const f32x4*>(ls + 32 * qt + 8 * g + 4 * hf);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[qt][i] = __builtin_amdgcn_exp2f(fmaf(sc[qt][i], c2, lsr[i >> 2][i & 3]));
+      }
+      const bool need_mask = __builtin_amdgcn_readfirstlane(
+          (int)((causal && kw0 + 31 > q0) || (q0 + BQ > T) || (kw0 + 32 > T)));
+      if (need_mask) {
+        // row c = 8 (i>>2) + (i&3) of q-tile qt is query q0 + 32 qt + 4 hf + c: p = 0 when the
+        // key is past it (causal: c < key - q0 - 32 qt - 4 hf), or the query / key is >= T
+        const int vk = key >= T ? 0x7fffffff : (causal ? key - q0 - 4 * hf : -0x7fffffff);
+        const int uq = T - 1 - q0 - 4 * hf;
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int c = 32 * qt + 8 * (i >> 2) + (i & 3);
+            sc[qt][i] = (c < vk || c > uq) ? 0.f : sc[qt][i];
+          }
+      }
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        f32x4 dsr[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) dsr[g] = *reinterpret_cast<const f32x4*>(ds + 32 * qt + 8 * g + 4 * hf);
+#pragma unroll
+        for (int s1 = 0; s1 < 2; ++s1)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int i = 8 * s1 + j;
+            const float pv = sc[qt][i];
+            pp[2 * qt + s1][j] = (bf16)pv;
+            pd[2 * qt + s1][j] = (bf16)(pv * (dp[qt][i] + dsr[i >> 2][i & 3]));
+          }
+      }
+#pragma unroll
+      for (int w = 0; w < (NH + 15) / 16; ++w) tr_wait8(*reinterpret_cast<s16x4(*)[16]>(&th[16 * w]));
+#pragma unroll
+      for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+          dvt[dt] = MFMA32(tr_join(th[2 * (dt * 4 + s4)], th[2 * (dt * 4 + s4) + 1]), pp[s4], dvt[dt]);
+      // Q^T fragments (A of dK^T), read after the dV^T MFMAs are issued
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          th[2 * (dt * 4 + s4)] = ds_tr16(lq + toff[dt][0] + 16 * s4 * RB);
+          th[2 * (dt * 4 + s4) + 1] = ds_tr16(lq + toff[dt][1] + 16 * s4 * RB);
+        }
+#pragma unroll
+      for (int w = 0; w < (NH + 15) / 16; ++w) tr_wait8(*reinterpret_cast<s16x4(*)[16]>(&th[16 * w]));
+#pragma unroll
+      for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+          dkt[dt] = MFMA32(tr_join(th[2 * (dt * 4 + s4)], th[2 * (dt * 4 + s4) + 1]), pd[s4], dkt[dt]);
+    }
+    // epilogue: lane = key, registers = d rows 32 dt + 8 g + 4 hf + j.  dK *= scale, inverse
+    // RoPE (d pairs with d + HD/2: tile dt with dt + DTN/2, same register), 8-byte stores.
+#pragma unroll
+    for (int d = 0; d < DTN; ++d) dkt[d] *= scale;
+    if (rpos && key < T) {
+      DPFS_KASSERT(rpos[(long long)b * T + key] >= 0, "rope position at key %d", key);
+      const float* tr = rtab + rpos[(long long)b * T + key] * HD;
+#pragma unroll
+      for (int dt = 0; dt < DTN / 2; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 cs = *reinterpret_cast<const f32x4*>(tr + 32 * dt + 8 * g + 4 * hf);
+          const f32x4 sn = *reinterpret_cast<const f32x4*>(tr + HD / 2 + 32 * dt + 8 * g + 4 * hf);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float x1 = dkt[dt][4 * g + j], x2 = dkt[dt + DTN / 2][4 * g + j];
+            dkt[dt][4 * g + j] = x1 * cs[j] + x2 * sn[j];
+            dkt[dt + DTN / 2][4 * g + j] = x2 * cs[j] - x1 * sn[j];
+          }
+        }
+    }
+    if (key < T) {
+      bf16* krow = dK + ((long long)b * T + key) * lddk + (long long)h * HD;
+      bf16* vrow = dV + ((long long)b * T + key) * lddv + (long long)h * HD;
+#pragma unroll
+      for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const bf16x4 a = {(bf16)dkt[dt][4 * g], (bf16)dkt[dt][4 * g + 1], (bf16)dkt[dt][4 * g + 2],
+                            (bf16)dkt[dt][4 * g + 3]};
+          const bf16x4 c = {(bf16)dvt[dt][4 * g], (bf16)dvt[dt][4 * g + 1], (bf16)dvt[dt][4 * g + 2],
+                            (bf16)dvt[dt][4 * g + 3]};
+          *reinterpret_cast<bf16x4*>(krow + 32 * dt + 8 * g + 4 * hf) = a;
+          *reinterpret_cast<bf16x4*>(vrow + 32 * dt + 8 * g + 4 * hf) = c;
+        }
+    }
+    if (BPK) {
+      // per-wave column sums over the 32 keys: registers summed across the 32 lanes of each half
+      // (keys >= T hold zeros), then the two halves hold disjoint d rows.
+      const long long row = (((long long)h * (BH / H) + b) * nkb + kb) * 4 + wave;
+#pragma unroll
+      for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float a = key < T ? dkt[dt][i] : 0.f, c = key < T ? dvt[dt][i] : 0.f;
+#pragma unroll
+          for (int o = 1; o < 32; o <<= 1) {
+            a += __shfl_xor(a, o, 64);
+            c += __shfl_xor(c, o, 64);
+          }
+          if (r32 == 0) {
+            const int d = 32 * dt + 8 * (i >> 2) + 4 * hf + (i & 3);
+            BPK[row * HD + d] = a;
+            BPV[row * HD + d] = c;
+          }
+        }
+    }
+  }
+}
+
 // ============================================================================ bwd: dQ ==
 // Block: 4 waves x 32 queries = 128 queries; K/V tiles of 64 keys staged in LDS.
 template <int HD>
@@ -1661,6 +1957,230 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
   }
 }
 
+// ========================================================== bwd: dQ (32x32x16 MFMA) ==
+// Query on the lane (as attn_fwd3_k): S^T = K Q^T and dP^T = V dO^T with the keys as the
+// 32x32 C rows, so dS^T packed to bf16 is directly the B operand of dQ^T += K^T dS^T (K^T by
+// transposed reads of the same K tile).  Also computes delta = rowsum(dO * O) per query and
+// writes -lse/scale and -delta for the dK / dV kernel.  K / V tiles (64 keys) by LDS-DMA into
+// a 3-slot ring; a workgroup = 4 waves x 32 queries and handles a causal pair of query blocks.
+template <int HD>
+struct KvDmaU {   // K / V tile rows [kv0, kv0 + 64) into a stage (K at 0, V at TILE), swz_u both
+  static constexpr int CPR = HD / 8, TILE = 64 * HD * 2, P = 2 * TILE / 1024, PW = P / 4;
+  unsigned voff[PW];
+  __device__ __forceinline__ void init(long long ldk, long long ldv) {
+    const int l = lane_id(), wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const bool isv = i >= PW / 2;
+      const int jj = wave + 4 * i - (isv ? P / 2 : 0);
+      const int pos = jj * 64 + l;
+      const int r = pos / CPR, cp = pos % CPR;
+      voff[i] = (unsigned)(((long long)r * (isv ? ldv : ldk) + swz_u<HD>(r, cp) * 8) * 2);
+    }
+  }
+  __device__ __forceinline__ void issue(const bf16* kb, const bf16* vb, long long ldk, long long ldv, int T, int kv0,
+                                        char* stage) const {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(kb + (long long)kv0 * ldk), (short)0, (int)(((long long)(T - 1 - kv0) * ldk + HD) * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(vb + (long long)kv0 * ldv), (short)0, (int)(((long long)(T - 1 - kv0) * ldv + HD) * 2), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const bool isv = i >= PW / 2;
+      const int jj = wave + 4 * i - (isv ? P / 2 : 0);
+      dma16(isv ? rv : rk, stage + (isv ? TILE : 0) + jj * 1024, voff[i]);
+    }
+  }
+};
+
+template <int HD>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq3_k(
+    const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V, const bf16* __restrict__ dO,
+    const bf16* __restrict__ Og, const float* __restrict__ LSE, float* __restrict__ NDEL_OUT,
+    float* __restrict__ LSN_OUT, bf16* __restrict__ dQ, int T, int H, int BH, long long ldq, long long ldk,
+    long long ldv, long long lddo, long long ldo, long long lddq, float scale, int causal,
+    const int64_t* __restrict__ rpos, const float* __restrict__ rtab, float* __restrict__ BPQ) {
+  static_assert(HD == 64, "dQ v3: head_dim 64");
+  constexpr int BQ = 128, BKV = 64, KS = HD / 16, DTN = HD / 32, RB = HD * 2;
+  constexpr int TILE = BKV * RB, STAGE = 2 * TILE, NST = 3;
+  constexpr int PW = KvDmaU<HD>::PW;
+  __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
+  const int nqb = (T + BQ - 1) / BQ;
+  const int NP = (nqb + 1) / 2;
+  const int it = blockIdx.x;
+  const int bh = (it >> 3) / NP * 8 + (it & 7), p = (it >> 3) % NP;
+  if (bh >= BH) return;
+  const int b = bh / H, h = bh % H;
+  const int wave = threadIdx.x >> 6, l = lane_id(), r32 = l & 31, hf = l >> 5, g16 = l >> 4, i16 = l & 15;
+  const float c2 = scale * kLog2e;
+  const bf16* kbase = K + (long long)b * T * ldk + (long long)h * HD;
+  const bf16* vbase = V + (long long)b * T * ldv + (long long)h * HD;
+  KvDmaU<HD> dma;
+  dma.init(ldk, ldv);
+  int koff[2][KS];   // K / V A-fragment row reads: row 32 kh + r32, chunk 2 ks + hf
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int r = 32 * kh + r32;
+      koff[kh][ks] = r * RB + (swz_u<HD>(r, 2 * ks + hf) << 4);
+    }
+
+  for (int sub = 0; sub < 2; ++sub) {
+    const int qb = sub == 0 ? nqb - 1 - p : p;
+    if (sub == 1 && qb == nqb - 1 - p) break;
+    if (sub == 1) __syncthreads();
+    const int q0 = qb * BQ, wq0 = q0 + 32 * wave, qi = wq0 + r32;
+    const int kv_end = causal ? min(T, q0 + BQ) : T;
+    const int nkv = (kv_end + BKV - 1) / BKV;
+    dma.issue(kbase, vbase, ldk, ldv, T, 0, smem);
+    if (nkv > 1) dma.issue(kbase, vbase, ldk, ldv, T, BKV, smem + STAGE);
+    // Q^T / dO^T operands (B of S^T, dP^T): lane holds X[qi][16 ks + 8 hf + j]
+    bf16x8 qf[KS], df[KS];
+    float dsum = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 a = {}, c = {}, ov = {};
+      if (qi < T) {
+        a = *reinterpret_cast<const bf16x8*>(Q + ((long long)b * T + qi) * ldq + (long long)h * HD + 16 * ks + 8 * hf);
+        c = *reinterpret_cast<const bf16x8*>(dO + ((long long)b * T + qi) * lddo + (long long)h * HD + 16 * ks + 8 * hf);
+        ov = *reinterpret_cast<const bf16x8*>(Og + ((long long)b * T + qi) * ldo + (long long)h * HD + 16 * ks + 8 * hf);
+      }
+      qf[ks] = a;
+      df[ks] = c;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dsum += (float)c[j] * (float)ov[j];
+    }
+    const float lc = qi < T ? -LSE[(long long)bh * T + qi] * kLog2e : 0.f;   // p = exp2(c2 S + lc)
+    wait_vmcnt<0>();
+    const float ndel = -pair_sum(dsum);                                      // dP' = dP - delta
+    if (hf == 0 && qi < T) {
+      LSN_OUT[(long long)bh * T + qi] = lc;
+      NDEL_OUT[(long long)bh * T + qi] = ndel;
+    }
+    f32x16 dq[DTN];
+#pragma unroll
+    for (int d = 0; d < DTN; ++d)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dq[d][i] = 0.f;
+    int cur = 0;
+    for (int t = 0; t < nkv; ++t) {
+      if (t + 1 < nkv) wait_vmcnt<PW>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      const char* lk = smem + cur * STAGE;
+      const char* lv = lk + TILE;
+      int nb = cur + 2;
+      if (nb >= NST) nb -= NST;
+      cur = (cur + 1 == NST) ? 0 : cur + 1;
+      const int kv0 = t * BKV;
+      if (t + 2 < nkv) dma.issue(kbase, vbase, ldk, ldv, T, kv0 + 2 * BKV, smem + nb * STAGE);
+      if (causal && kv0 > wq0 + 31) continue;   // wave-uniform
+      f32x16 sc[2], dp[2];
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          sc[kh][i] = 0.f;
+          dp[kh][i] = 0.f;
+        }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          sc[kh] = MFMA32(*reinterpret_cast<const bf16x8*>(lk + koff[kh][ks]), qf[ks], sc[kh]);
+          dp[kh] = MFMA32(*reinterpret_cast<const bf16x8*>(lv + koff[kh][ks]), df[ks], dp[kh]);
+        }
+      }
+      // K^T fragments (A of dQ^T: lane d = 32 dt + r32, keys 16 s + 4 hf + 0..3 / 8..11)
+      __builtin_amdgcn_sched_barrier(0);
+      constexpr int NH = 2 * DTN * 4;
+      s16x4 th[(NH + 15) / 16 * 16];
+#pragma unroll
+      for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int row = 16 * s4 + 4 * hf + (i16 >> 2);
+          const int col = 32 * dt + 16 * (g16 & 1) + 4 * (i16 & 3);
+          const int ch = col >> 3, bo = (col & 7) * 2;
+          th[2 * (dt * 4 + s4)] = ds_tr16(lk + row * RB + (swz_u<HD>(row, ch) << 4) + bo);
+          th[2 * (dt * 4 + s4) + 1] = ds_tr16(lk + (row + 8) * RB + (swz_u<HD>(row + 8, ch) << 4) + bo);
+        }
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[kh][i] = __builtin_amdgcn_exp2f(fmaf(sc[kh][i], c2, lc));
+      const bool need_mask = __builtin_amdgcn_readfirstlane(
+          (int)((causal && kv0 + BKV - 1 > wq0) || (kv0 + BKV > T)));
+      if (need_mask) {
+        const int lim = (causal ? min(qi, T - 1) : T - 1) - kv0 - 4 * hf;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            sc[kh][i] = (32 * kh + 8 * (i >> 2) + (i & 3) > lim) ? 0.f : sc[kh][i];
+      }
+      bf16x8 pd[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int kh = s4 >> 1, i = 8 * (s4 & 1) + j;
+          pd[s4][j] = (bf16)(sc[kh][i] * (dp[kh][i] + ndel));
+        }
+#pragma unroll
+      for (int w = 0; w < (NH + 15) / 16; ++w) tr_wait8(*reinterpret_cast<s16x4(*)[16]>(&th[16 * w]));
+#pragma unroll
+      for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+          dq[dt] = MFMA32(tr_join(th[2 * (dt * 4 + s4)], th[2 * (dt * 4 + s4) + 1]), pd[s4], dq[dt]);
+    }
+    // epilogue: lane = query, registers = d rows 32 dt + 8 g + 4 hf + j: scale, inverse RoPE
+#pragma unroll
+    for (int d = 0; d < DTN; ++d) dq[d] *= scale;
+    if (rpos && qi < T) {
+      DPFS_KASSERT(rpos[(long long)b * T + qi] >= 0, "rope position at query %d", qi);
+      const float* tr = rtab + rpos[(long long)b * T + qi] * HD;
+#pragma unroll
+      for (int dt = 0; dt < DTN / 2; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 cs = *reinterpret_cast<const f32x4*>(tr + 32 * dt + 8 * g + 4 * hf);
+          const f32x4 sn = *reinterpret_cast<const f32x4*>(tr + HD / 2 + 32 * dt + 8 * g + 4 * hf);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float x1 = dq[dt][4 * g + j], x2 = dq[dt + DTN / 2][4 * g + j];
+            dq[dt][4 * g + j] = x1 * cs[j] + x2 * sn[j];
+            dq[dt + DTN / 2][4 * g + j] = x2 * cs[j] - x1 * sn[j];
+          }
+        }
+    }
+    if (qi < T) {
+      bf16* row = dQ + ((long long)b * T + qi) * lddq + (long long)h * HD;
+#pragma unroll
+      for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const bf16x4 v = {(bf16)dq[dt][4 * g], (bf16)dq[dt][4 * g + 1], (bf16)dq[dt][4 * g + 2],
+                            (bf16)dq[dt][4 * g + 3]};
+          *reinterpret_cast<bf16x4*>(row + 32 * dt + 8 * g + 4 * hf) = v;
+        }
+    }
+    if (BPQ) {
+      const long long prow = (((long long)h * (BH / H) + b) * nqb + qb) * 4 + wave;
+#pragma unroll
+      for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float a = qi < T ? dq[dt][i] : 0.f;
+#pragma unroll
+          for (int o = 1; o < 32; o <<= 1) a += __shfl_xor(a, o, 64);
+          if (r32 == 0) BPQ[prow * HD + 32 * dt + 8 * (i >> 2) + 4 * hf + (i & 3)] = a;
+        }
+    }
+  }
+}
+
 // Bias gradient of the packed QKV projection from the attention backward's per-wave column
 // sums: out[seg * H * HD + h * HD + col] = sum over the R rows of head h's partial (seg 0 = q
 // with Rq rows, 1 / 2 = k / v with Rk rows).  One 1024-thread block per (seg, head, 16-column
@@ -1722,8 +2242,11 @@ static unsigned long long* g_attn_diag = nullptr;
 static int g_attn_fwd_persist = 0;
 extern "C" void dpfs_attn_fwd_persist(int v) { g_attn_fwd_persist = v; }   // impl 5: attn_fwd3_k DIAG build, [grid][4 waves][4]
 extern "C" void dpfs_attn_diag(void* p) { g_attn_diag = (unsigned long long*)p; }
-static int g_attn_bwd_impl = 2;  // dK/dV kernel: 2 = LDS-DMA ring (default), 1 = register-staged,
-                                 // 3 = register-staged with 32 keys per wave (hd <= 64)
+// dK/dV kernel: 0 = auto (default: 4 at head_dim 64, 2 otherwise), 1 = register-staged,
+// 2 = LDS-DMA ring (16x16x32), 3 = register-staged with 32 keys per wave (hd <= 64),
+// 4 = attn_bwd_dkdv3_k (32x32x16, key on the lane, hd 64)
+static int g_attn_bwd_impl = 0;
+
 extern "C" void dpfs_attn_set_bwd_impl(int v) { g_attn_bwd_impl = v; }
 
 extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int T, int H,
@@ -1773,18 +2296,38 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
                               float* bws) {
   // The QKV bias gradient rides on the default kernel pair (dQ + LDS-DMA dK/dV); with another
   // dK/dV variant the caller computes it with a separate column sum.
-  const bool bias = dbias != nullptr && bws != nullptr && g_attn_bwd_impl == 2;
+  const int bimpl = g_attn_bwd_impl == 0 ? (hd == 64 ? 4 : 2) : g_attn_bwd_impl;
+  const bool bias = dbias != nullptr && bws != nullptr && (bimpl == 2 || (bimpl == 4 && hd == 64));
   const int nqb = (T + 127) / 128, nkb = (T + 63) / 64;
   float* pq = bias ? bws : nullptr;
   float* pk = bias ? bws + (long long)H * B * nqb * 4 * hd : nullptr;
   float* pv = bias ? pk + (long long)H * B * nkb * 4 * hd : nullptr;
   dim3 gq(nqb, B * H);
+  if (bimpl == 4 && hd == 64) {   // (attn_bwd_dkdv3_k reads the -lse log2 e this kernel writes)
+    const int items = (B * H + 7) / 8 * 8 * ((nqb + 1) / 2);
+    attn_bwd_dq3_k<64><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,
+                                             (const bf16*)o, lse, delta, delta + (long long)B * H * T, (bf16*)dq, T,
+                                             H, B * H, ldq, ldk, ldv, lddo, ldo, lddq, scale, causal, rope_pos,
+                                             rope_tab, pq);
+  } else
   DPFS_HD_DISPATCH(hd, attn_bwd_dq_k<HD_><<<gq, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
                                                              (const bf16*)dout, (const bf16*)o, lse, delta,
                                                              delta + (long long)B * H * T, (bf16*)dq,
                                                              T, H, ldq, ldk, ldv, lddo, ldo, lddq, scale, causal,
                                                              rope_pos, rope_tab, pq));
-  if (g_attn_bwd_impl == 3 && hd <= 64) {
+  if (bimpl == 4 && hd == 64) {
+    const int nkb3 = (T + 127) / 128, items = (B * H + 7) / 8 * 8 * ((nkb3 + 1) / 2);
+    attn_bwd_dkdv3_k<64><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,
+                                               delta + (long long)B * H * T, delta, (bf16*)dk, (bf16*)dv, T, H, B * H,
+                                               ldq, ldk, ldv, lddo, lddk, lddv, scale, causal, rope_pos, rope_tab,
+                                               pk, pv);
+    if (bias) {
+      attn_bias_grad_k<64><<<3 * H * 4, 1024, 0, s>>>(pq, pk, pv, dbias, H, B * nqb * 4, B * nkb3 * 4);
+      return 1;
+    }
+    return 0;
+  }
+  if (bimpl == 3 && hd <= 64) {
     dim3 gk2((T + 127) / 128, B * H);
     if (hd == 64)
       attn_bwd_dkdv_k<64, 2><<<gk2, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,
@@ -1797,7 +2340,7 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
     return 0;
   }
   dim3 gk((T + 63) / 64, B * H);
-  if (g_attn_bwd_impl == 2) {
+  if (bimpl == 2) {
     DPFS_HD_DISPATCH(hd, attn_bwd_dkdv2_k<HD_><<<gk, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
                                                                   (const bf16*)dout, delta + (long long)B * H * T,
                                                                   delta, (bf16*)dk,

@@ -193,12 +193,12 @@ def test_cross_entropy_kernels(C, V, valid, start):
 @pytest.mark.parametrize("impl", [2, 3, 1, 4])
 def test_attention(C, B, T, H, hd, impl):
     C.attn_set_impl(impl)            # forward variants
-    C.attn_set_bwd_impl(1 if impl == 3 else 2)   # dK/dV: register-staged and LDS-DMA ring
+    C.attn_set_bwd_impl({3: 1, 4: 4}.get(impl, 2))   # dK/dV: register-staged, LDS-DMA ring, 32x32 key-on-lane
     try:
         _check_attention(C, B, T, H, hd)
     finally:
         C.attn_set_impl(0)
-        C.attn_set_bwd_impl(2)
+        C.attn_set_bwd_impl(0)
 
 
 @pytest.mark.parametrize("B,T,H,hd", [(2, 256, 4, 64), (1, 300, 2, 64), (1, 1000, 2, 64), (2, 200, 3, 32)])
@@ -208,7 +208,7 @@ def test_attention_bwd_dkdv_32_keys_per_wave(C, B, T, H, hd):
     try:
         _check_attention(C, B, T, H, hd)
     finally:
-        C.attn_set_bwd_impl(2)
+        C.attn_set_bwd_impl(0)
 
 
 def _check_attention(C, B, T, H, hd):

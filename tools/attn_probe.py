@@ -42,7 +42,7 @@ def main():
     def mk(impl):
         def g():
             C.attn_set_impl(impl)
-            C.attn_set_bwd_impl(impl if a.bwd else 2)
+            C.attn_set_bwd_impl(impl if a.bwd else 0)
             if a.bwd:
                 C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv)
             else:
@@ -99,7 +99,7 @@ def main():
     for impl, ms in res.items():
         print(f"impl {impl} {'bwd' if a.bwd else 'fwd'}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF", flush=True)
     C.attn_set_impl(0)
-    C.attn_set_bwd_impl(2)
+    C.attn_set_bwd_impl(0)
 
 
 if __name__ == "__main__":
