@@ -24,6 +24,8 @@ void dpfs_gemm_nt_rope(const void*, const void*, void*, const float*, int, int, 
                        const float*, int, int, hipStream_t);
 void dpfs_gemm_v4_mask(int);
 void dpfs_gemm4_sched(int);
+void dpfs_gemm4_group_m(int);
+void dpfs_gemm4_bn(int);
 void dpfs_gemm4_ablate(int);
 void dpfs_gemm4_diag(void*);
 void dpfs_attn_diag(void*);
@@ -1080,8 +1082,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm4_diag", [](torch::Tensor t) { dpfs_gemm4_diag(t.defined() && t.numel() ? t.data_ptr() : nullptr); },
         "int64 buffer [grid*4*4] for the DIAG build's per-wave cycle split (gemm4_ablate bit 16)");
   m.def("gemm4_sched", [](int v) { dpfs_gemm4_sched(v); },
-        "v4 main-loop schedule: 0 compiler order, 1 = 8 chunks (DMA piece + 2 fragment reads + 8 MFMAs), "
-        "2 = MFMA pairs interleaved with single reads / DMA pieces (precomputed DMA offsets)");
+        "v4 main-loop variant: 0 = default (descriptor-advancing DMA where K ranges allow, one piece per MFMA "
+        "row), 1 = two pieces per row in rows 4-7, 2 = per-lane K checks everywhere (the pre-FAST stream)");
+  m.def("gemm4_bn", [](int v) { dpfs_gemm4_bn(v); }, "v4 tile width of non-split bf16 GEMMs: 0 per shape, 256 / 192 forced");
+  m.def("gemm4_group_m", [](int v) { dpfs_gemm4_group_m(v); }, "v4 tile-row group size of the item order (default 4)");
   m.def("gemm_v2_sched", [](int v) { dpfs_gemm_v2_sched(v); }, "v2 256x256 schedule (-1 per-layout default, 0..4 see gemm2_k SCHED)");
   m.def("gemm_set_impl", [](int v) { dpfs_gemm_set_impl(v); }, "1 = v1 (128x128 register-staged), 2 = v2 (LDS-DMA, one tile per workgroup), 3 = v3 (persistent v2, default)");
   m.def("gemm_tn2", &gemm_tn2, "fp32 c (+)= a0^T b0 + a1^T b1 (reduction dim over two buffers), one split-K launch; None if the plan does not fit",

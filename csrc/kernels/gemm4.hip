@@ -91,25 +91,33 @@ __device__ __forceinline__ s16x4 ds_tr16(const char* p) {
   return r;
 }
 
-template <bool KMAJ>
+// BN: the operand tile's MN extent (256, or 192 for the B operand of a 256 x 192 tile).  An
+// MN-major image keeps BN * 2 bytes per k row; at BN = 192 the chunk swizzle stays inside
+// each aligned group of 8 chunks, so a swizzled chunk index never leaves the row's 24.
+template <int BN>
+__device__ __forceinline__ int mn_swz(int k) {
+  return BN == 256 ? mnh(k) << 1 : (mnh(k) & 3) << 1;
+}
+
+template <bool KMAJ, int BN = 256>
 struct Opnd;
-template <>
-struct Opnd<true> {
+template <int BN>
+struct Opnd<true, BN> {
   bf16x8 v[8];
   __device__ __forceinline__ void load(int i, const char* half, int rb, int l) { v[i] = frag_k(half, rb, l); }
   __device__ __forceinline__ bf16x8 get(int i) const { return v[i]; }
   __device__ __forceinline__ void pin() {}
 };
-template <>
-struct Opnd<false> {
+template <int BN>
+struct Opnd<false, BN> {
   s16x4 lo[8], hi[8];
   __device__ __forceinline__ void load(int i, const char* half, int rb, int l) {
     const int ii = l & 15, q = ii >> 2, p = ii & 3;
     const int chunk = (rb + 4 * p) >> 3;
     const int k_lo = 8 * (l >> 4) + q;
     const int k_hi = k_lo + 4;
-    lo[i] = ds_tr16(half + k_lo * 512 + ((chunk ^ (mnh(k_lo) << 1)) << 4) + (p & 1) * 8);
-    hi[i] = ds_tr16(half + k_hi * 512 + ((chunk ^ (mnh(k_hi) << 1)) << 4) + (p & 1) * 8);
+    lo[i] = ds_tr16(half + k_lo * (2 * BN) + ((chunk ^ mn_swz<BN>(k_lo)) << 4) + (p & 1) * 8);
+    hi[i] = ds_tr16(half + k_hi * (2 * BN) + ((chunk ^ mn_swz<BN>(k_hi)) << 4) + (p & 1) * 8);
   }
   __device__ __forceinline__ bf16x8 get(int i) const {
     typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -126,18 +134,18 @@ struct Opnd<false> {
   }
 };
 
-template <bool AK, bool BKM>
+template <bool AK, bool BKM, int BN>
 struct Frags {
   Opnd<AK> a;
-  Opnd<BKM> b;
+  Opnd<BKM, BN> b;
 };
 
-template <bool AK, bool BKM>
-__device__ __forceinline__ void read_frags(Frags<AK, BKM>& f, const char* slot, int wm, int wn, int l) {
+template <bool AK, bool BKM, int BN>
+__device__ __forceinline__ void read_frags(Frags<AK, BKM, BN>& f, const char* slot, int wm, int wn, int l) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) f.a.load(i, slot, wm * 128 + 16 * i, l);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) f.b.load(j, slot + 16384, wn * 128 + 16 * j, l);
+  for (int j = 0; j < BN / 32; ++j) f.b.load(j, slot + 16384, wn * (BN / 2) + 16 * j, l);
 }
 
 // Work item -> tile origin and K range (grouped order as gemm.hip's gemmp_k).
@@ -145,6 +153,7 @@ struct Item {
   int m0, n0, kb, ke, split, sel;
 };
 
+template <int BN>
 __device__ __forceinline__ Item decode(int lin, int nwg, int tiles_m, int tiles_n, int group_m, int K, int kps,
                                        int k_switch) {
   Item it;
@@ -156,10 +165,10 @@ __device__ __forceinline__ Item decode(int lin, int nwg, int tiles_m, int tiles_
   const int gsz = min(tiles_m - first_m, group_m);
   const int r = wg - gid * per_group;
   it.m0 = (first_m + r % gsz) * 256;
-  it.n0 = (r / gsz) * 256;
+  it.n0 = (r / gsz) * BN;
   it.kb = it.split * kps;
   it.ke = min(K, it.kb + kps);
-  DPFS_KASSERT(it.m0 < tiles_m * 256 && it.n0 < tiles_n * 256 && it.kb < K,
+  DPFS_KASSERT(it.m0 < tiles_m * 256 && it.n0 < tiles_n * BN && it.kb <= K,
                "item %d -> tile (%d, %d) k %d", lin, it.m0, it.n0, it.kb);
   it.sel = 0;
   if (it.kb >= k_switch) {
@@ -181,24 +190,26 @@ __device__ __forceinline__ int nsteps(const Item& it) {
 // 16-column tiles so each lane holds 8 consecutive columns and writes them with ONE 16-byte
 // buffer store (16 rows x 64 contiguous bytes per instruction; the two halves of a row's
 // 128-byte line are written by consecutive instructions).  OUT 1: fp32, each lane's 4 columns
-// per tile as one 16-byte store.  Exactly STORES (32 / 64) buffer stores per wave
-// (out-of-range lanes get an offset past the descriptor), which the next item's first wait
-// counts.
-template <int OUT>
+// per tile as one 16-byte store.  Exactly STORES (4 / 8 per 16-row block at BN 256, 3 / 6 at
+// 192) buffer stores per wave (out-of-range lanes get an offset past the descriptor), which
+// the next item's first wait counts.  The wave's tile is 128 x BN/2 (NJ = BN/32 16-column
+// tiles); RoPE only at BN 256 (a 64-wide head never straddles two waves there).
+template <int OUT, int BN, bool ROPE>
 __device__ __forceinline__ void epilogue(const char* bias_lds, bool has_bias, const Item& ci, void* C,
                                          const Rope& rope, int M, int N, int ldc, long long slab_stride,
                                          unsigned c_bytes, int wm, int wn, int l) {
+  constexpr int NJ = BN / 32;
   const int g = l >> 4;
-  const int wcol0 = ci.n0 + wn * 128;
+  const int wcol0 = ci.n0 + wn * (BN / 2);
   acc_drain();
   if constexpr (OUT == 0) {
-    const bool do_rope = rope.cols > 0 && wcol0 < rope.cols;
+    const bool do_rope = ROPE && BN == 256 && rope.cols > 0 && wcol0 < rope.cols;
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(C, (short)0, (int)c_bytes, 0x00020000);
     const int colg = 16 * (g & 1) + 8 * (g >> 1);
     static_for<0, 8>([&](auto I) {
       constexpr int i = decltype(I)::value;
       f32x4 v[8];
-      static_for<0, 8>([&](auto J) {
+      static_for<0, NJ>([&](auto J) {
         constexpr int j = decltype(J)::value;
         v[j] = acc_read<i, j>();
         if (has_bias) v[j] += *reinterpret_cast<const f32x4*>(bias_lds + 64 * j + 16 * g);
@@ -222,7 +233,7 @@ __device__ __forceinline__ void epilogue(const char* bias_lds, bool has_bias, co
         }
       }
 #pragma unroll
-      for (int jp = 0; jp < 4; ++jp) {
+      for (int jp = 0; jp < NJ / 2; ++jp) {
         const bf16x4 o0 = {(bf16)v[2 * jp][0], (bf16)v[2 * jp][1], (bf16)v[2 * jp][2], (bf16)v[2 * jp][3]};
         const bf16x4 o1 = {(bf16)v[2 * jp + 1][0], (bf16)v[2 * jp + 1][1], (bf16)v[2 * jp + 1][2],
                            (bf16)v[2 * jp + 1][3]};
@@ -242,7 +253,7 @@ __device__ __forceinline__ void epilogue(const char* bias_lds, bool has_bias, co
     static_for<0, 8>([&](auto I) {
       constexpr int i = decltype(I)::value;
       const int m = ci.m0 + wm * 128 + 16 * i + (l & 15);
-      static_for<0, 8>([&](auto J) {
+      static_for<0, NJ>([&](auto J) {
         constexpr int j = decltype(J)::value;
         const int n = wcol0 + 16 * j + 4 * g;
         const bool ok = m < M && n < N;
@@ -255,7 +266,18 @@ __device__ __forceinline__ void epilogue(const char* bias_lds, bool has_bias, co
 
 // OUT: 0 = bf16 C (+ fp32 bias[n], + RoPE); 1 = fp32 C / split-K slab.
 // dbg (timing-only ablations, tools/gemm4_probe.py): 4 = no DMA wait, 8 = no step barrier.
-template <bool AK, bool BKM, int OUT, int DIAG = 0>
+// FAST (every item's K range a multiple of 64, so no step reads past K): the DMA stream
+// advances the buffer descriptors' base address and record count by SALU once per stage
+// (hipBLASLt's form) and every piece reuses its per-item lane offset: no VALU, no per-lane
+// K check in front of a DMA piece; rows past M / N still land past the record count.
+// SCHED 1: the stage's DMA pieces one per MFMA row (rows 0-7) instead of two per row in rows
+// 4-7.
+// BN: tile columns, 256 (waves 128 x 128) or 192 (waves 128 x 96: the N = 768 projections
+// become 512 tiles, two per CU, instead of 384 = 1.5 per CU).  Per stage a wave issues NQ =
+// 4 + BN/64 DMA pieces (4 of A, 4 or 3 of B).
+// ROPE: the RoPE epilogue is compiled in (QKV projection only: its code and SGPR pressure
+// stay out of the plain kernels).
+template <bool AK, bool BKM, int OUT, int DIAG = 0, bool FAST = false, int SCHED = 0, int BN = 256, bool ROPE = false>
 __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                   void* __restrict__ C, const float* __restrict__ bias, int M, int N,
                                                   int K, int lda, int ldb, int ldc, int kps, int splits,
@@ -263,9 +285,13 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
                                                   unsigned c_bytes, Rope rope, int group_m, Dual dual, int dbg,
                                                   unsigned long long* diag) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_TOTAL];
-  constexpr int STORES = OUT == 0 ? 32 : 64;   // store instructions per wave per item
+  constexpr int NJ = BN / 32;                  // 16-column MFMA tiles per wave
+  constexpr int NBQ = BN / 64;                 // B pieces per wave per stage
+  constexpr int NQ = 4 + NBQ;                  // DMA pieces per wave per stage
+  constexpr int STORES = OUT == 0 ? 4 * NJ : 8 * NJ;   // store instructions per wave per item
+  static_assert(BN == 256 || BN == 192, "tile width");
 
-  const int tiles_n = (N + 255) / 256;
+  const int tiles_n = (N + BN - 1) / BN;
   const int tiles_m = (M + 255) / 256;
   const int nwg = tiles_m * tiles_n;
   const int total = nwg * splits;
@@ -290,17 +316,19 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
 
   // ---- producer cursor: the DMA stream runs 3 steps ahead of the consumer, across items.
   int p_it = it;
-  Item pi = decode(p_it, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
+  Item pi = decode<BN>(p_it, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
   int p_t = 0, p_nk = nsteps(pi);
   int p_slot = 0;
-  // Per-item lane offsets of the wave's 8 DMA pieces (4 of A, 4 of B): a step adds one
-  // uniform term per operand and checks the K bound against a lane constant (kpos).
+  // Per-item lane offsets of the wave's NQ DMA pieces (4 of A, NBQ of B): a step adds one
+  // uniform term per operand and checks the K bound against a lane constant (kpos).  Piece
+  // j of an operand covers LDS bytes [1 KiB j, 1 KiB (j + 1)) of its half of the slot; an
+  // MN-major image has 2 * (tile extent) bytes per k row (A: 256, B: BN).
   unsigned pbase[8];
   auto rebase = [&]() {
     const bool s2 = pi.sel != 0;
     const int la = s2 ? lda2 : lda, lb = s2 ? ldb2 : ldb;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < NQ; ++q) {
       const bool isA = q < 4;
       const bool km = isA ? AK : BKM;
       const int j = wave + 4 * (q & 3);
@@ -310,10 +338,15 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
         const int row = 16 * j + (l >> 2);
         const int c = (l & 3) ^ kh(row);
         pbase[q] = (unsigned)(((long long)(r0 + row) * ld + 8 * c) * 2);
-      } else {
+      } else if (isA || BN == 256) {
         const int lin = j * 64 + l;
         const int row = lin >> 5;
         const int c = (lin & 31) ^ (mnh(row) << 1);
+        pbase[q] = (unsigned)(((long long)row * ld + r0 + 8 * c) * 2);
+      } else {
+        const int lin = j * 64 + l;
+        const int row = lin / (BN / 8);
+        const int c = (lin - row * (BN / 8)) ^ mn_swz<BN>(row);
         pbase[q] = (unsigned)(((long long)row * ld + r0 + 8 * c) * 2);
       }
     }
@@ -325,11 +358,34 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
       const int row = 16 * j + (l >> 2);
       return 8 * ((l & 3) ^ kh(row));
     }
-    return (j * 64 + l) >> 5;
+    return (q < 4 || BN == 256) ? (j * 64 + l) >> 5 : (j * 64 + l) / (BN / 8);
   };
   rebase();
+  // FAST: descriptors of the producer's current stage (base advanced to its first k)
+  __amdgpu_buffer_rsrc_t sra = ra, srb = rb;
+  auto stage_rsrc = [&]() {
+    if constexpr (FAST) {
+      const bool s2 = pi.sel != 0;
+      const int k0 = pi.kb + 32 * p_t;
+      const bool live = p_it < total && k0 < pi.ke;   // (an empty trailing split reads zeros)
+      const long long adv_a = AK ? (long long)k0 * 2 : (long long)k0 * (s2 ? lda2 : lda) * 2;
+      const long long adv_b = BKM ? (long long)k0 * 2 : (long long)k0 * (s2 ? ldb2 : ldb) * 2;
+      const char* pa = reinterpret_cast<const char*>(s2 ? dual.A2 : A) + adv_a;
+      const char* pb = reinterpret_cast<const char*>(s2 ? dual.B2 : B) + adv_b;
+      const unsigned na = live ? (s2 ? dual.a2_bytes : a_bytes) - (unsigned)adv_a : 0u;
+      const unsigned nb = live ? (s2 ? dual.b2_bytes : b_bytes) - (unsigned)adv_b : 0u;
+      sra = __builtin_amdgcn_make_buffer_rsrc((void*)pa, (short)0, (int)na, 0x00020000);
+      srb = __builtin_amdgcn_make_buffer_rsrc((void*)pb, (short)0, (int)nb, 0x00020000);
+    }
+  };
+  stage_rsrc();
   // DMA piece q (< 8) of the producer's current stage
   auto issue = [&](int q) {
+    if constexpr (FAST) {
+      if constexpr (DIAG == 2) return;
+      dma16(q < 4 ? sra : srb, smem + p_slot * SLOT + (q < 4 ? 0 : 16384) + (wave + 4 * (q & 3)) * 1024, pbase[q]);
+      return;
+    }
     const bool live = p_it < total;
     const int krem = (live ? pi.ke : 0) - (pi.kb + 32 * p_t);   // valid k in this stage
     const int k0 = pi.kb + 32 * p_t;
@@ -349,20 +405,21 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
       p_it += G;
       p_t = 0;
       if (p_it < total) {
-        pi = decode(p_it, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
+        pi = decode<BN>(p_it, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
         p_nk = nsteps(pi);
         rebase();
       }
     }
+    stage_rsrc();
   };
 #pragma unroll
   for (int s0 = 0; s0 < 3; ++s0) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) issue(q);
+    for (int q = 0; q < NQ; ++q) issue(q);
     advance();
   }
 
-  Frags<AK, BKM> F0, F1;
+  Frags<AK, BKM, BN> F0, F1;
   int c_slot = 0;
   // DIAG build only (timing diagnosis, never the production kernel): cycles spent in the
   // step-entry waits + barrier, in the step bodies and in the epilogues, per wave.
@@ -374,16 +431,16 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
     __builtin_amdgcn_sched_barrier(0);
     return t;
   };
-  // fragments of the first step: stage 0 landed (two younger stages of 8 pieces in flight)
-  wait_vmcnt<16>();
+  // fragments of the first step: stage 0 landed (two younger stages of NQ pieces in flight)
+  wait_vmcnt<2 * NQ>();
   __builtin_amdgcn_s_barrier();
-  read_frags<AK, BKM>(F0, smem, wm, wn, l);
+  read_frags<AK, BKM, BN>(F0, smem, wm, wn, l);
   if constexpr (DIAG) t_mark = stamp();
 
   // One consumer step on `cur`, prefetching the next step's fragments into `nxt`.
-  // Entry wait: stage s+1 landed for this wave (younger: stage s+2 = 8 pieces, plus the
+  // Entry wait: stage s+1 landed for this wave (younger: stage s+2 = NQ pieces, plus the
   // previous item's epilogue stores on an item's first step), then the step barrier.
-  auto step = [&](Frags<AK, BKM>& cur, Frags<AK, BKM>& nxt, bool first, auto zero, bool last, int bcol0) {
+  auto step = [&](Frags<AK, BKM, BN>& cur, Frags<AK, BKM, BN>& nxt, bool first, auto zero, bool last, int bcol0) {
     constexpr bool ZR = decltype(zero)::value;
     if constexpr (DIAG) {
       const unsigned long long t = stamp();
@@ -395,8 +452,8 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
     cur.a.pin();
     cur.b.pin();
     if (dbg & 4) wait_vmcnt<63>();   // timing-only: no wait for the DMA (wrong results)
-    else if (first) wait_vmcnt<(8 + STORES < 63 ? 8 + STORES : 63)>();
-    else wait_vmcnt<8>();
+    else if (first) wait_vmcnt<(NQ + STORES < 63 ? NQ + STORES : 63)>();
+    else wait_vmcnt<NQ>();
     if (!(dbg & 8)) __builtin_amdgcn_s_barrier();
     if constexpr (DIAG) {
       const unsigned long long t = stamp();
@@ -404,9 +461,9 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
       t_mark = t;
     }
     if (OUT == 0 && last && bias) {
-      // the epilogue's 128 bias values of this wave into its LDS area by two 256-byte LDS-DMA
-      // pieces, ahead of this step's 8 ring pieces (the epilogue waits vmcnt(8), no barrier:
-      // the wave reads only what it loaded)
+      // the epilogue's bias values of this wave (128, of which BN/2 used) into its LDS area by
+      // two 256-byte LDS-DMA pieces, ahead of this step's NQ ring pieces (the epilogue waits
+      // vmcnt(NQ), no barrier: the wave reads only what it loaded)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int n = bcol0 + 64 * h + l;
@@ -416,52 +473,42 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
     }
     c_slot = (c_slot + 1) & 3;
     const char* src = smem + c_slot * SLOT;
-    // every fragment read of the next step in the first half, the DMA pieces in the second
+    // Rows q of NJ MFMAs (A fragment q against every B fragment).  Rows 0-3 read the next
+    // step's fragments (A 2q, 2q+1; B 2q, 2q+1 while < NJ).  DMA pieces: SCHED 0 two per row in
+    // rows 4-7, SCHED 1 one per row.  At NJ = 8 this is the hand-placed order of the 256-wide
+    // kernel: MFMA j, then the event after it.
     static_for<0, 8>([&](auto Q) {
       constexpr int q = decltype(Q)::value;
-      if constexpr (q < 4) {
-        acc_mfma<q, 0, ZR>(cur.b.get(0), cur.a.get(q));
+      static_for<0, NJ>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        acc_mfma<q, j, ZR>(cur.b.get(j), cur.a.get(q));
         __builtin_amdgcn_sched_barrier(0);
-        nxt.a.load(2 * q, src, wm * 128 + 32 * q, l);
+        if constexpr (q < 4) {
+          // read slots after MFMA 0 / 2 / 4 / 6 (NJ 8) or 0 / 2 / 3 / 5 (NJ 6)
+          constexpr int r0 = 0, r1 = 2, r2 = NJ == 8 ? 4 : 3, r3 = NJ == 8 ? 6 : 5;
+          if constexpr (j == r0) nxt.a.load(2 * q, src, wm * 128 + 32 * q, l);
+          if constexpr (j == r1 && 2 * q < NJ) nxt.b.load(2 * q, src + 16384, wn * (BN / 2) + 32 * q, l);
+          if constexpr (j == r2) nxt.a.load(2 * q + 1, src, wm * 128 + 32 * q + 16, l);
+          if constexpr (j == r3 && 2 * q + 1 < NJ)
+            nxt.b.load(2 * q + 1, src + 16384, wn * (BN / 2) + 32 * q + 16, l);
+        }
+        if constexpr (SCHED == 1) {
+          if constexpr (j == 3 && q < NQ) issue(q);
+        } else if constexpr (q >= 4) {
+          constexpr int d0 = 1, d1 = NJ == 8 ? 5 : 4;
+          if constexpr (j == d0 && 2 * (q - 4) < NQ) issue(2 * (q - 4));
+          if constexpr (j == d1 && 2 * (q - 4) + 1 < NQ) issue(2 * (q - 4) + 1);
+        }
         __builtin_amdgcn_sched_barrier(0);
-        acc_mfma<q, 1, ZR>(cur.b.get(1), cur.a.get(q));
-        acc_mfma<q, 2, ZR>(cur.b.get(2), cur.a.get(q));
-        __builtin_amdgcn_sched_barrier(0);
-        nxt.b.load(2 * q, src + 16384, wn * 128 + 32 * q, l);
-        __builtin_amdgcn_sched_barrier(0);
-        acc_mfma<q, 3, ZR>(cur.b.get(3), cur.a.get(q));
-        acc_mfma<q, 4, ZR>(cur.b.get(4), cur.a.get(q));
-        __builtin_amdgcn_sched_barrier(0);
-        nxt.a.load(2 * q + 1, src, wm * 128 + 32 * q + 16, l);
-        __builtin_amdgcn_sched_barrier(0);
-        acc_mfma<q, 5, ZR>(cur.b.get(5), cur.a.get(q));
-        acc_mfma<q, 6, ZR>(cur.b.get(6), cur.a.get(q));
-        __builtin_amdgcn_sched_barrier(0);
-        nxt.b.load(2 * q + 1, src + 16384, wn * 128 + 32 * q + 16, l);
-        __builtin_amdgcn_sched_barrier(0);
-        acc_mfma<q, 7, ZR>(cur.b.get(7), cur.a.get(q));
-        __builtin_amdgcn_sched_barrier(0);
-      } else {
-        static_for<0, 2>([&](auto H) {
-          constexpr int h = decltype(H)::value;
-          acc_mfma<q, 4 * h, ZR>(cur.b.get(4 * h), cur.a.get(q));
-          acc_mfma<q, 4 * h + 1, ZR>(cur.b.get(4 * h + 1), cur.a.get(q));
-          __builtin_amdgcn_sched_barrier(0);
-          issue(2 * (q - 4) + h);
-          __builtin_amdgcn_sched_barrier(0);
-          acc_mfma<q, 4 * h + 2, ZR>(cur.b.get(4 * h + 2), cur.a.get(q));
-          acc_mfma<q, 4 * h + 3, ZR>(cur.b.get(4 * h + 3), cur.a.get(q));
-          __builtin_amdgcn_sched_barrier(0);
-        });
-      }
+      });
     });
     advance();
   };
 
   for (bool first = true; it < total; it += G, first = false) {
-    const Item ci = decode(it, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
+    const Item ci = decode<BN>(it, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
     const int nk = nsteps(ci);
-    const int bcol0 = ci.n0 + wn * 128;
+    const int bcol0 = ci.n0 + wn * (BN / 2);
     step(F0, F1, !first, std::true_type{}, false, bcol0);
     step(F1, F0, false, std::false_type{}, nk == 2, bcol0);
     for (int t = 2; t < nk; t += 2) {
@@ -473,8 +520,8 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
       t_body += t - t_mark;
       t_mark = t;
     }
-    if (OUT == 0 && bias) wait_vmcnt<8>();   // this wave's bias DMA landed (8 younger ring pieces)
-    epilogue<OUT>(bias_lds, bias != nullptr, ci, C, rope, M, N, ldc, slab_stride, c_bytes, wm, wn, l);
+    if (OUT == 0 && bias) wait_vmcnt<NQ>();   // this wave's bias DMA landed (NQ younger ring pieces)
+    epilogue<OUT, BN, ROPE>(bias_lds, bias != nullptr, ci, C, rope, M, N, ldc, slab_stride, c_bytes, wm, wn, l);
     if constexpr (DIAG) {
       const unsigned long long t = stamp();
       t_epi += t - t_mark;
@@ -521,7 +568,13 @@ static int g_g4_ablate = 0;
 static unsigned long long* g_g4_diag = nullptr;   // [grid][4 waves][wait, body, epilogue, valid]
 extern "C" void dpfs_gemm4_ablate(int v) { g_g4_ablate = v; }
 extern "C" void dpfs_gemm4_diag(void* p) { g_g4_diag = (unsigned long long*)p; }
-extern "C" void dpfs_gemm4_sched(int) {}   // one schedule since the asm-owned accumulators
+// Main-loop variant (tools/gemm4_probe.py A/B): 0 = one DMA piece per MFMA row (default),
+// 1 = two pieces per row in rows 4-7; 2 = per-lane K checks even where FAST applies.
+static int g_g4_sched = 0;
+extern "C" void dpfs_gemm4_sched(int v) { g_g4_sched = v; }
+// Tile width of non-split bf16 GEMMs: 0 = chosen per shape (g4_pick_bn), 256 / 192 forced.
+static int g_g4_bn = 0;
+extern "C" void dpfs_gemm4_bn(int v) { g_g4_bn = v; }
 extern "C" void dpfs_gemm4_group_m(int g) { g_g4_group_m = g > 0 ? g : 4; }
 
 // Launch v4.  layout: 0 = NT (A K-major, B K-major), 1 = NN (B MN-major), 2 = TN (both
@@ -539,29 +592,74 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
   if (kps % 32) return false;
   const long long cspan = ((long long)(M - 1) * ldc + N) * (out_f32 ? 4 : 2);
   if (cspan >= (1ll << 32) - 16) return false;
-  const long long items = (long long)((M + 255) / 256) * ((N + 255) / 256) * splits;
+  // 256 x 192 tiles where whole waves of tiles over the CUs come out shorter: 384 tiles of
+  // 256 x 256 (N = 768 at 32k rows) are 1.5 per CU, i.e. two rounds on half the chip; 512
+  // tiles of 256 x 192 are two full rounds of 3/4 the work.  Priced at 0.8 of a 256-wide
+  // tile (its 7 DMA pieces per 48 MFMAs vs 8 per 64).
+  const int cus = g4_cu_count();
+  int bn = 256;
+  if (!out_f32 && splits == 1 && rope_cols == 0) {
+    if (g_g4_bn == 192) {
+      bn = 192;
+    } else if (g_g4_bn == 0) {
+      const long long tm = (M + 255) / 256;
+      const long long r256 = (tm * ((N + 255) / 256) + cus - 1) / cus;
+      const long long r192 = (tm * ((N + 191) / 192) + cus - 1) / cus;
+      if (r192 * 0.8 < r256 * 0.95) bn = 192;
+    }
+  }
+  const long long items = (long long)((M + 255) / 256) * ((N + bn - 1) / bn) * splits;
   if (items <= 0 || items >= (1ll << 31)) return false;
-  const int grid = (int)std::min<long long>(items, g4_cu_count());
+  const int grid = (int)std::min<long long>(items, cus);
   const Rope rope = {rope_pos, rope_tab, rope_cols, rope_hd};
   const Dual dual = {(const bf16*)A2, (const bf16*)B2, A2 ? k_switch : 0x7fffffff, lda2, ldb2, a2_bytes, b2_bytes};
   const unsigned cb = (g_g4_ablate & 1) ? 0u : (unsigned)cspan;
   if (g_g4_ablate & 2) {
     a_bytes = b_bytes = a2_bytes = b2_bytes = 0u;
   }
-#define DPFS_G4(AK_, BK_, OUT_)                                                                                  \
-  gemm4_k<AK_, BK_, OUT_><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, \
-                                               kps, splits, slab_stride, a_bytes, b_bytes, cb, rope,            \
-                                               g_g4_group_m, dual, g_g4_ablate & ~3, nullptr)
-  if ((g_g4_ablate & 32) && g_g4_diag && layout == 0 && !out_f32) {
-    gemm4_k<true, true, 0, 2><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb,
-                                                   ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb, rope,
-                                                   g_g4_group_m, dual, g_g4_ablate & ~51, g_g4_diag);
+  // FAST (descriptor-advancing DMA stream): every item's K range a multiple of 64
+  const bool fast = g_g4_sched != 2 && K % 64 == 0 && kps % 64 == 0 && (!A2 || k_switch % 64 == 0);
+  const int sched = g_g4_sched == 1 ? 0 : 1;
+#define DPFS_G4_ARGS                                                                                            \
+  (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb, \
+      rope, g_g4_group_m, dual, g_g4_ablate & ~3, nullptr
+#define DPFS_G4(AK_, BK_, OUT_)                                                                    \
+  do {                                                                                            \
+    if constexpr (AK_ && BK_ && OUT_ == 0) {                                                      \
+      if (rope_cols > 0) {                                                                        \
+        if (fast)                                                                                 \
+          gemm4_k<AK_, BK_, OUT_, 0, true, 1, 256, true><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);      \
+        else                                                                                      \
+          gemm4_k<AK_, BK_, OUT_, 0, false, 0, 256, true><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);     \
+        break;                                                                                    \
+      }                                                                                           \
+    }                                                                                             \
+    if (fast && sched == 1) {                                                                     \
+      if (OUT_ == 0 && bn == 192)                                                                 \
+        gemm4_k<AK_, BK_, OUT_, 0, true, 1, (OUT_ == 0 ? 192 : 256)><<<grid, 256, 0, s>>>(DPFS_G4_ARGS); \
+      else                                                                                        \
+        gemm4_k<AK_, BK_, OUT_, 0, true, 1><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);                   \
+    } else if (fast) {                                                                            \
+      if (OUT_ == 0 && bn == 192)                                                                 \
+        gemm4_k<AK_, BK_, OUT_, 0, true, 0, (OUT_ == 0 ? 192 : 256)><<<grid, 256, 0, s>>>(DPFS_G4_ARGS); \
+      else                                                                                        \
+        gemm4_k<AK_, BK_, OUT_, 0, true, 0><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);                   \
+    } else if (OUT_ == 0 && bn == 192) {                                                          \
+      gemm4_k<AK_, BK_, OUT_, 0, false, 0, (OUT_ == 0 ? 192 : 256)><<<grid, 256, 0, s>>>(DPFS_G4_ARGS); \
+    } else {                                                                                      \
+      gemm4_k<AK_, BK_, OUT_><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);                                 \
+    }                                                                                             \
+  } while (0)
+  if ((g_g4_ablate & 32) && g_g4_diag && layout == 0 && !out_f32 && bn == 256) {
+    gemm4_k<true, true, 0, 2, true, 1><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda,
+                                                            ldb, ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb,
+                                                            rope, g_g4_group_m, dual, g_g4_ablate & ~51, g_g4_diag);
     return true;
   }
-  if ((g_g4_ablate & 16) && g_g4_diag && layout == 0 && !out_f32) {
-    gemm4_k<true, true, 0, 1><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb,
-                                                      ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb, rope,
-                                                      g_g4_group_m, dual, g_g4_ablate & ~19, g_g4_diag);
+  if ((g_g4_ablate & 16) && g_g4_diag && layout == 0 && !out_f32 && bn == 256 && fast) {
+    gemm4_k<true, true, 0, 1, true, 1><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda,
+                                                            ldb, ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb,
+                                                            rope, g_g4_group_m, dual, g_g4_ablate & ~19, g_g4_diag);
     return true;
   }
   if (layout == 0) {
@@ -574,6 +672,7 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
     if (!out_f32) return false;
     DPFS_G4(false, false, 1);
   }
+#undef DPFS_G4_ARGS
 #undef DPFS_G4
   return true;
 }

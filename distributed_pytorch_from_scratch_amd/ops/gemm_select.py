@@ -1,26 +1,25 @@
-"""Per-shape choice between our MFMA GEMM kernels and hipBLASLt for *plain* GEMMs.
+"""Per-shape choice among our MFMA GEMM kernels (``csrc/kernels/gemm4.hip``, ``gemm.hip``).
 
-Our kernels (``csrc/kernels/gemm.hip``) carry every GEMM with a fused epilogue: RoPE in the QKV
-projection, the fp32 split-K weight-gradient GEMMs that accumulate in place. For the plain
-bf16 GEMMs (the forward projections with at most a bias, the NN data-gradient GEMMs) and the
-fp32-output weight-gradient GEMMs, the first call on a new (layout, M, N, K, bias) shape times
-the candidates on the live operands and every later call uses the fastest:
+Every GEMM of the training step runs on our kernels: the forward projections (bias, RoPE in
+the QKV epilogue), the NN data-gradient GEMMs and the fp32 split-K weight-gradient GEMMs
+(reference ``models/layers.py:49,93`` and their autograd backward).  The first call on a new
+(layout, M, N, K, bias) shape times our variants on the live operands and every later call
+uses the fastest:
 
-* ``ours``  -- our kernel;
-* ``blas``  -- hipBLASLt through ``torch.nn.functional.linear`` / ``torch.matmul`` /
-  ``torch.mm(out_dtype=fp32)`` (the library heuristic's first algorithm);
-* ``ltN``   -- hipBLASLt driven directly (``csrc/blas/blaslt.hip``) with algorithm N of its
-  heuristic list: every algorithm gets one quick timing, the two fastest enter the final
-  round.  In the GPT-2-small step it wins the small projections by 4-10 % over torch's
-  algorithm (Wo / down forward, Wo / QKV data gradient); our split-K kernel keeps every
-  weight-gradient GEMM (profiles/r2_blaslt_probe.txt).
+* ``ours``     -- the v4 kernel (one wave per SIMD, 128-row wave tiles) with its per-shape
+  tile width (256 x 256, or 256 x 192 where whole rounds of tiles over the CUs come out
+  shorter, e.g. the N = 768 projections);
+* ``ours256`` / ``ours192`` -- v4 with the tile width forced (kept only if it measures faster
+  than the width the launcher's round model picked);
+* ``ours3``    -- the v3 kernel (8 waves, 128 x 64 per wave).
 
-A library candidate must beat ``ours`` by 3 % to be chosen.  The measured per-shape winners
-are in ``choices()`` and in ``profiles/``.
+hipBLASLt stays reachable for A/B runs and for operands our kernels do not take (a
+contiguous dimension that is not a multiple of 8, e.g. an uneven vocab shard): ``DPFS_GEMM_LIB=1``
+adds it to the ``auto`` candidates (``blas``: through ``torch.nn.functional.linear`` /
+``torch.matmul`` / ``torch.mm(out_dtype=fp32)``; ``ltN``: algorithm N of its heuristic list
+through ``csrc/blas/blaslt.hip``), where it must beat ours by 3 % to be chosen.
 
-``DPFS_GEMM_BACKEND`` = ``auto`` (default) | ``ours`` | ``blas`` | ``lt`` pins the choice (tests
-pin ``ours`` to exercise the HIP kernels, ``lt`` runs hipBLASLt's first algorithm through our
-binding).  ``DPFS_GEMM_LT=0`` leaves the direct hipBLASLt candidates out of ``auto``.
+``DPFS_GEMM_BACKEND`` = ``auto`` (default) | ``ours`` | ``blas`` | ``lt`` pins the choice.
 """
 from __future__ import annotations
 
@@ -62,9 +61,14 @@ def _ms(fn: Callable[[], torch.Tensor], reps: int = 3) -> float:
 _LT_FINALISTS = 2
 
 
+def _lib() -> bool:
+    """hipBLASLt among the ``auto`` candidates (opt-in A/B: DPFS_GEMM_LIB=1)."""
+    return os.environ.get("DPFS_GEMM_LIB", "0") == "1"
+
+
 def _lt_count(k, layout: int, M: int, N: int, K: int, bias: bool) -> int:
     """Algorithms hipBLASLt offers for this problem through our binding (0: none / disabled)."""
-    if os.environ.get("DPFS_GEMM_LT", "1") == "0" or not hasattr(k, "lt_algos"):
+    if not _lib() or os.environ.get("DPFS_GEMM_LT", "1") == "0" or not hasattr(k, "lt_algos"):
         return 0
     return int(k.lt_algos(layout, M, N, K, bias))
 
@@ -104,33 +108,41 @@ def _lt_index(c: str) -> int:
 _V4_BIT = {"nt": 1, "nn": 2, "tn": 4}
 
 
-def _ours_variants(k, layout: str, fn: Callable[[], torch.Tensor]) -> Dict[str, Callable]:
-    """Our candidates for one call: ``ours`` = the v4 kernel (one wave per SIMD, 128 x 128 per
-    wave, csrc/kernels/gemm4.hip), ``ours3`` = the v3 kernel (8 waves, gemm.hip).  Which of
-    the two wins depends on the shape (the epilogue / K-loop balance), so both are timed."""
+def _ours_variants(k, layout: str, fn: Callable[[], torch.Tensor], widths: bool = False) -> Dict[str, Callable]:
+    """Our candidates for one call: ``ours`` = the v4 kernel (one wave per SIMD, 128-row wave
+    tiles, csrc/kernels/gemm4.hip) at its per-shape tile width, ``ours256`` / ``ours192`` =
+    v4 with the width forced (``widths``: non-split bf16 NT / NN), ``ours3`` = the v3 kernel
+    (8 waves, gemm.hip).  Which wins depends on the shape (epilogue / K-loop balance, tile
+    rounds over the CUs), so all are timed."""
     if not hasattr(k, "gemm_v4_mask"):
         return {"ours": fn}
     bit = _V4_BIT[layout]
 
-    def with_mask(on: bool):
+    def with_mask(on: bool, bn: int = 0):
         def run():
             old = k.gemm_v4_get_mask()
             k.gemm_v4_mask((old | bit) if on else (old & ~bit))
+            if bn:
+                k.gemm4_bn(bn)
             try:
                 return fn()
             finally:
                 k.gemm_v4_mask(old)
+                if bn:
+                    k.gemm4_bn(0)
         return run
-    return {"ours": with_mask(True), "ours3": with_mask(False)}
+    out = {"ours": with_mask(True), "ours3": with_mask(False)}
+    if widths and hasattr(k, "gemm4_bn"):
+        out.update({"ours256": with_mask(True, 256), "ours192": with_mask(True, 192)})
+    return out
 
 
-def _run_ours(k, layout: str, choice: str, fn: Callable[[], torch.Tensor]):
-    return _ours_variants(k, layout, fn).get(choice, fn)()
+def _run_ours(k, layout: str, choice: str, fn: Callable[[], torch.Tensor], widths: bool = False):
+    return _ours_variants(k, layout, fn, widths).get(choice, fn)()
 
 
-# Below this many rows (decode steps, tiny batches) our 256-row tiles are mostly padding and
-# the library's GEMV-class kernels win; timing cannot tell them apart there (a launch-bound
-# loop measures the host launch cost, which favours the thinner pybind path).
+# Below this many rows (decode steps, tiny batches) a host-timed loop measures launch cost, not
+# the kernels: no per-shape timing there, the default variant runs.
 _MIN_ROWS = 256
 
 
@@ -155,7 +167,9 @@ def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, out=None) -> torch.T
     if fw is not None:          # fp8 step (ModelArgs.fp8): e4m3 operands, hipBLASLt fp8 GEMM
         return F8.nt(x, fw, bias, out=out)
     m = mode()
-    if k is reference or not x.is_cuda or (m == "ours" and _aligned(x.shape[1], w.shape[0])):
+    if k is reference or not x.is_cuda or (m in ("ours", "auto") and _aligned(x.shape[1], w.shape[0])
+                                           and x.shape[0] < _MIN_ROWS) or \
+            (m == "ours" and _aligned(x.shape[1], w.shape[0])):
         return k.gemm_nt(x, w, bias, out=out)
     bb = shadow(bias, x.dtype) if bias is not None else None
 
@@ -165,7 +179,7 @@ def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, out=None) -> torch.T
         if bb is None:
             return torch.mm(x, w.t(), out=out)
         return torch.addmm(bb, x, w.t(), out=out)
-    if not _aligned(x.shape[1], w.shape[0]) or x.shape[0] < _MIN_ROWS:
+    if not _aligned(x.shape[1], w.shape[0]):
         return blas()
     M, N, K = x.shape[0], w.shape[0], x.shape[1]
     lt_ok = _lt_operands_ok(x, w, out) and _lt_bias_ok(bias)
@@ -184,10 +198,10 @@ def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, out=None) -> torch.T
     if m == "lt":
         return lt(0)() if lt_ok and _lt_count(k, 0, M, N, K, bias is not None) else blas()
     key = ("nt", M, N, K, bias is not None, x.device.index)
-    c = _pick(key, {**_ours_variants(k, "nt", ours), "blas": blas},
+    c = _pick(key, {**_ours_variants(k, "nt", ours, True), **({"blas": blas} if _lib() else {})},
               lambda: _lt_count(k, 0, M, N, K, bias is not None), lt if lt_ok else None)
     if c.startswith("ours") or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
-        return _run_ours(k, "nt", c, ours)
+        return _run_ours(k, "nt", c, ours, True)
     return blas() if c == "blas" else lt(_lt_index(c))()
 
 
@@ -210,12 +224,14 @@ def gemm_nn(k, a: torch.Tensor, b: torch.Tensor, out=None) -> torch.Tensor:
     if fw is not None:          # fp8 step: e5m2 gradient x e4m3 weight
         return F8.nn(a, fw, out=out)
     m = mode()
-    if k is reference or not a.is_cuda or (m == "ours" and _aligned(a.shape[1], b.shape[1])):
+    if k is reference or not a.is_cuda or (m in ("ours", "auto") and _aligned(a.shape[1], b.shape[1])
+                                           and a.shape[0] < _MIN_ROWS) or \
+            (m == "ours" and _aligned(a.shape[1], b.shape[1])):
         return k.gemm_nn(a, b, out=out)
 
     def blas():
         return torch.matmul(a, b) if out is None else torch.matmul(a, b, out=out)
-    if not _aligned(a.shape[1], b.shape[1]) or a.shape[0] < _MIN_ROWS:
+    if not _aligned(a.shape[1], b.shape[1]):
         return blas()
     M, N, K = a.shape[0], b.shape[1], a.shape[1]
     lt_ok = _lt_operands_ok(a, b, out)
@@ -234,17 +250,17 @@ def gemm_nn(k, a: torch.Tensor, b: torch.Tensor, out=None) -> torch.Tensor:
     if m == "lt":
         return lt(0)() if lt_ok and _lt_count(k, 1, M, N, K, False) else blas()
     key = ("nn", M, N, K, a.device.index)
-    c = _pick(key, {**_ours_variants(k, "nn", ours), "blas": blas}, lambda: _lt_count(k, 1, M, N, K, False),
-              lt if lt_ok else None)
+    c = _pick(key, {**_ours_variants(k, "nn", ours, True), **({"blas": blas} if _lib() else {})},
+              lambda: _lt_count(k, 1, M, N, K, False), lt if lt_ok else None)
     if c.startswith("ours") or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
-        return _run_ours(k, "nn", c, ours)
+        return _run_ours(k, "nn", c, ours, True)
     return blas() if c == "blas" else lt(_lt_index(c))()
 
 
 def gemm_nt_rope(k, x: torch.Tensor, w: torch.Tensor, bias, pos, tab, rot_heads: int, hd: int) -> torch.Tensor:
     """Packed QKV projection with rotate-half RoPE on the first ``rot_heads`` heads: our NT
-    kernel with the rotation in its epilogue, or hipBLASLt (through torch or directly)
-    followed by the in-place RoPE kernel (timed per shape like every plain GEMM)."""
+    kernel with the rotation in its epilogue (v4 or v3, timed per shape); with
+    ``DPFS_GEMM_LIB=1`` also hipBLASLt followed by the in-place RoPE kernel."""
     fw = F8.lookup(w)
     if fw is not None:          # fp8 step: fp8 GEMM, then the RoPE pass
         y = F8.nt(x, fw, bias)
@@ -278,7 +294,7 @@ def gemm_nt_rope(k, x: torch.Tensor, w: torch.Tensor, bias, pos, tab, rot_heads:
     if m == "lt":
         return lt(0)() if lt_ok and _lt_count(k, 0, M, N, K, bias is not None) else blas()
     key = ("nt_rope", M, N, K, hd, x.device.index)
-    c = _pick(key, {**_ours_variants(k, "nt", ours), "blas": blas},
+    c = _pick(key, {**_ours_variants(k, "nt", ours), **({"blas": blas} if _lib() else {})},
               lambda: _lt_count(k, 0, M, N, K, bias is not None), lt if lt_ok else None)
     if c.startswith("ours") or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
         return _run_ours(k, "nt", c, ours)
@@ -318,10 +334,10 @@ def _tn_blas_ok(a, b) -> bool:
 
 
 def gemm_tn(k, a: torch.Tensor, b: torch.Tensor, out=None, accumulate: bool = False) -> torch.Tensor:
-    """fp32 c[M,N] (+)= a[K,M]^T b[K,N] (weight gradients): our split-K kernel, hipBLASLt through
-    torch (fp32 output) or hipBLASLt directly (accumulating in place, beta = 1), timed per
-    (shape, accumulate) on a scratch output (an accumulating candidate must not be timed into
-    the live gradient)."""
+    """fp32 c[M,N] (+)= a[K,M]^T b[K,N] (weight gradients): our split-K kernel (v4 / v3), and
+    with ``DPFS_GEMM_LIB=1`` hipBLASLt through torch (fp32 output) or directly (accumulating
+    in place, beta = 1), timed per (shape, accumulate) on a scratch output (an accumulating
+    candidate must not be timed into the live gradient)."""
     if k is reference or not a.is_cuda:
         return k.gemm_tn(a, b, out, accumulate) if out is not None else k.gemm_tn(a, b)
     if not _aligned(a.shape[1], b.shape[1]):
@@ -349,7 +365,7 @@ def gemm_tn(k, a: torch.Tensor, b: torch.Tensor, out=None, accumulate: bool = Fa
     m = mode()
     if m == "ours" or a.shape[0] < _MIN_ROWS:
         return run("ours", out, accumulate)
-    blas_ok = _tn_blas_ok(a, b)
+    blas_ok = (m == "blas" or _lib()) and _tn_blas_ok(a, b)
     if m == "blas" and blas_ok:
         return run("blas", out, accumulate)
     if m == "lt":
@@ -362,7 +378,7 @@ def gemm_tn(k, a: torch.Tensor, b: torch.Tensor, out=None, accumulate: bool = Fa
         cands = {"ours": lambda: run("ours", scratch, accumulate)}
         if hasattr(k, "gemm_v4_mask"):
             cands["ours3"] = lambda: run("ours3", scratch, accumulate)
-        if blas_ok:
+        if blas_ok and _lib():
             cands["blas"] = lambda: run("blas", scratch, accumulate)
         c = _pick(key, cands, lambda: _lt_count(k, 2, M, N, K, False),
                   (lambda i: (lambda: run(f"lt{i}", scratch, accumulate))) if lt_ok else None)

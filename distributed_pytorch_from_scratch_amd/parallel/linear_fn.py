@@ -19,10 +19,11 @@ Sequence-parallel variants (``sequence_parallel=True``) replace the all-reduce p
 all-gather / reduce-scatter over the token dimension (Megatron-SP), the same bytes on the
 wire but norms/residuals then run on ``T/tp`` tokens per rank.
 
-All GEMMs go through ``ops.gemm_select`` (``GS.gemm_*``): on GPU it times, once per shape,
-our MFMA kernels (``csrc/kernels/gemm4.hip`` and ``gemm.hip``) against hipBLASLt and keeps the
-faster (``DPFS_GEMM_BACKEND=ours`` pins ours, ``blas`` pins hipBLASLt); on CPU it is fp32
-torch.  The weight is an fp32 master parameter; the GEMMs read its cached bf16 shadow
+All GEMMs go through ``ops.gemm_select`` (``GS.gemm_*``): on GPU they run on our MFMA kernels
+(``csrc/kernels/gemm4.hip`` and ``gemm.hip``; the variant is timed once per shape), with
+hipBLASLt only when pinned (``DPFS_GEMM_BACKEND=blas``), opted into the timing
+(``DPFS_GEMM_LIB=1``) or for a contiguous dimension that is not a multiple of 8; on CPU it is
+fp32 torch.  The weight is an fp32 master parameter; the GEMMs read its cached bf16 shadow
 (``ops.dispatch.shadow``) and write the weight gradient in fp32.
 """
 from __future__ import annotations

@@ -707,26 +707,32 @@ def test_blaslt_direct_every_algorithm(C, layout):
         C.lt_run(layout, a, b, torch.empty(M + 1, N, device=DEV), bias, 0)
 
 
+@pytest.mark.parametrize("bn", [0, 256, 192])
 @pytest.mark.parametrize("sched", [0, 1, 2])
-@pytest.mark.parametrize("M,N,K", [(8200, 2104, 712), (1000, 776, 2304), (257, 264, 96), (4096, 768, 768)])
-def test_gemm_v4_bitwise_equals_v3(C, M, N, K, sched):
+@pytest.mark.parametrize("M,N,K", [(8200, 2104, 712), (1000, 776, 2304), (257, 264, 96), (4096, 768, 768),
+                                   (520, 1032, 128)])
+def test_gemm_v4_bitwise_equals_v3(C, M, N, K, sched, bn):
     """The v4 kernel (one wave per SIMD, 128x128 per wave, 32-deep LDS ring) accumulates every
-    output in the same k order as v3, so NT (+bias) and NN results are bit-identical."""
+    output in the same k order as v3, so NT (+bias) and NN results are bit-identical, on both
+    DMA streams (K a multiple of 64: descriptor-advancing; else per-lane K checks), at both
+    tile widths (256 x 256 and 256 x 192) and on ragged M / N."""
     torch.manual_seed(26)
     a = torch.randn(M, K, device=DEV).bfloat16()
     bt = torch.randn(N, K, device=DEV).bfloat16()
-    bn = torch.randn(K, N, device=DEV).bfloat16()
+    b_nn = torch.randn(K, N, device=DEV).bfloat16()
     bias = torch.randn(N, device=DEV)
     old = C.gemm_v4_get_mask()
     try:
         C.gemm_v4_mask(7)
         C.gemm4_sched(sched)
-        nt4, nn4 = C.gemm_nt(a, bt, bias), C.gemm_nn(a, bn)
+        C.gemm4_bn(bn)
+        nt4, nn4 = C.gemm_nt(a, bt, bias), C.gemm_nn(a, b_nn)
         C.gemm_v4_mask(0)
-        nt3, nn3 = C.gemm_nt(a, bt, bias), C.gemm_nn(a, bn)
+        nt3, nn3 = C.gemm_nt(a, bt, bias), C.gemm_nn(a, b_nn)
     finally:
         C.gemm_v4_mask(old)
-        C.gemm4_sched(2)
+        C.gemm4_sched(0)
+        C.gemm4_bn(0)
     assert _rel(nt4, R.gemm_nt(a.float(), bt.float(), bias)) < 1e-2
     assert torch.equal(nt4, nt3)
     assert torch.equal(nn4, nn3)

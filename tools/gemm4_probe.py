@@ -61,6 +61,10 @@ def main():
     ap.add_argument("--check-only", action="store_true")
     ap.add_argument("--scheds", type=int, nargs="+", default=[0, 1, 2])
     ap.add_argument("--no-blas", action="store_true")
+    ap.add_argument("--bn", type=int, nargs="*", default=[],
+                    help="extra arms: the last --scheds variant with the v4 tile width forced (256 / 192)")
+    ap.add_argument("--group-m", type=int, nargs="*", default=[],
+                    help="extra arms: the last --scheds variant with this item-order group size")
     ap.add_argument("--diag", action="store_true",
                     help="NT only: DIAG build's per-wave cycle split (step waits / bodies / epilogues), s_memtime")
     ap.add_argument("--ablate", type=int, nargs="*", default=[],
@@ -75,12 +79,15 @@ def main():
             _, _, ours, blas, ref = operands(layout, M, N, K, gen)
             want = ref() if M * N <= 50304 * 768 * 2 else None
             res = {}
-            for tag, mask, sc in [(f"v4s{sc}", 7, sc) for sc in a.scheds] + [("v3", 0, 0)]:
+            for tag, mask, sc, bn in [(f"v4s{sc}", 7, sc, 0) for sc in a.scheds] + \
+                    [(f"bn{b}", 7, a.scheds[-1], b) for b in a.bn] + [("v3", 0, 0, 0)]:
                 C.gemm_v4_mask(mask)
                 C.gemm4_sched(sc)
+                C.gemm4_bn(bn)
                 if want is not None:
                     out = ours(C).float()
                     res[tag] = ((out - want).norm() / want.norm()).item()
+                C.gemm4_bn(0)
             C.gemm_v4_mask(3)
             del want
             flops = 2.0 * M * N * K
@@ -99,6 +106,9 @@ def main():
                 C.gemm4_diag(torch.empty(0))
                 v = d.view(-1, 4).double()
                 v = v[v[:, 3] > 0]
+                if v.shape[0] == 0:   # the DIAG build covers the 256-wide FAST NT kernel only
+                    print(f"{layout} {name} DIAG: no 256-wide launch for this shape", flush=True)
+                    continue
                 tiles = ((M + 255) // 256) * ((N + 255) // 256)
                 per = tiles / (v.shape[0] / 4)
                 tot = v[:, :3].sum(1)
@@ -107,7 +117,8 @@ def main():
                       f"-> per tile wait {v[:, 0].mean() / per:.0f} body {v[:, 1].mean() / per:.0f} "
                       f"epi {v[:, 2].mean() / per:.0f}; shares wait {(v[:, 0] / tot).mean():.3f} "
                       f"epi {(v[:, 2] / tot).mean():.3f}", flush=True)
-            arms = [f"v4s{sc}" for sc in a.scheds] + [f"abl{x}" for x in a.ablate] + ["v3"] + \
+            arms = [f"v4s{sc}" for sc in a.scheds] + [f"gm{g}" for g in a.group_m] + [f"bn{b}" for b in a.bn] + \
+                [f"abl{x}" for x in a.ablate] + ["v3"] + \
                 ([] if a.no_blas else ["blas"])
             ts = {k: [] for k in arms}
             for _ in range(a.rounds):
@@ -116,6 +127,18 @@ def main():
                         C.gemm_v4_mask(7)
                         C.gemm4_sched(int(k[3:]))
                         ts[k].append(timed(lambda: ours(C), a.iters))
+                    elif k.startswith("bn"):
+                        C.gemm_v4_mask(7)
+                        C.gemm4_sched(a.scheds[-1])
+                        C.gemm4_bn(int(k[2:]))
+                        ts[k].append(timed(lambda: ours(C), a.iters))
+                        C.gemm4_bn(0)
+                    elif k.startswith("gm"):
+                        C.gemm_v4_mask(7)
+                        C.gemm4_sched(a.scheds[-1])
+                        C.gemm4_group_m(int(k[2:]))
+                        ts[k].append(timed(lambda: ours(C), a.iters))
+                        C.gemm4_group_m(4)
                     elif k.startswith("abl"):
                         C.gemm_v4_mask(7)
                         C.gemm4_sched(a.scheds[-1])
