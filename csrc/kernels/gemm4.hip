@@ -194,44 +194,73 @@ __device__ __forceinline__ int nsteps(const Item& it) {
 // 192) buffer stores per wave (out-of-range lanes get an offset past the descriptor), which
 // the next item's first wait counts.  The wave's tile is 128 x BN/2 (NJ = BN/32 16-column
 // tiles); RoPE only at BN 256 (a 64-wide head never straddles two waves there).
-template <int OUT, int BN, bool ROPE>
-__device__ __forceinline__ void epilogue(const char* bias_lds, bool has_bias, const Item& ci, void* C,
-                                         const Rope& rope, int M, int N, int ldc, long long slab_stride,
-                                         unsigned c_bytes, int wm, int wn, int l) {
+// Straight-line code: the lane's bias values are read from LDS once per item (HAS_BIAS is a
+// template flag, no per-tile branch or LDS wait), store offsets are 32-bit selects (the C span
+// fits the descriptor, so row * ldc cannot overflow), and the RoPE rows' positions and
+// cos / sin values are loaded one 16-row block ahead of their use.
+template <int OUT, int BN, int ROPE, bool HAS_BIAS>
+__device__ __forceinline__ void epilogue(const char* bias_lds, const Item& ci, void* C, const Rope& rope, int M,
+                                         int N, int ldc, long long slab_stride, unsigned c_bytes, int wm, int wn,
+                                         int l) {
   constexpr int NJ = BN / 32;
   const int g = l >> 4;
   const int wcol0 = ci.n0 + wn * (BN / 2);
+  const int row0 = ci.m0 + wm * 128 + (l & 15);
   acc_drain();
   if constexpr (OUT == 0) {
-    const bool do_rope = ROPE && BN == 256 && rope.cols > 0 && wcol0 < rope.cols;
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(C, (short)0, (int)c_bytes, 0x00020000);
     const int colg = 16 * (g & 1) + 8 * (g >> 1);
+    f32x4 bv[NJ];
+    if constexpr (HAS_BIAS) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bv[j] = *reinterpret_cast<const f32x4*>(bias_lds + 64 * j + 16 * g);
+    }
+    // RoPE (head_dim ROPE = 64 / 128): rotate-half pairs (d, d + hd/2) live in the same lane,
+    // tiles j and j + HJ.  One set of table registers: block i+1's values are loaded right
+    // after block i's rotation consumed them, under block i's conversions and stores.
+    constexpr int HD = (BN == 256) ? ROPE : 0;
+    constexpr int HJ = HD ? HD / 32 : 1;   // tiles per half head: 2 (hd 64) or 4 (hd 128)
+    const bool do_rope = HD && rope.cols > 0 && wcol0 < rope.cols;
+    f32x4 cs[HJ], sn[HJ];
+    auto rope_load = [&](int i) {
+      const int m = row0 + 16 * i;
+      const long long pp = m < M ? rope.pos[m] : 0;
+      DPFS_KASSERT(m >= M || pp >= 0, "rope position %lld at row %d", pp, m);
+      const float* tr = rope.tab + pp * HD;
+#pragma unroll
+      for (int jh = 0; jh < HJ; ++jh) {
+        cs[jh] = *reinterpret_cast<const f32x4*>(tr + 16 * jh + 4 * g);
+        sn[jh] = *reinterpret_cast<const f32x4*>(tr + HD / 2 + 16 * jh + 4 * g);
+      }
+    };
+    if constexpr (HD != 0) {
+      if (do_rope) rope_load(0);
+    }
     static_for<0, 8>([&](auto I) {
       constexpr int i = decltype(I)::value;
       f32x4 v[8];
       static_for<0, NJ>([&](auto J) {
         constexpr int j = decltype(J)::value;
         v[j] = acc_read<i, j>();
-        if (has_bias) v[j] += *reinterpret_cast<const f32x4*>(bias_lds + 64 * j + 16 * g);
+        if constexpr (HAS_BIAS) v[j] += bv[j];
       });
-      const int m = ci.m0 + wm * 128 + 16 * i + (l & 15);
-      if (do_rope) {
-        DPFS_KASSERT(m >= M || rope.pos[m] >= 0, "rope position %lld at row %d", (long long)rope.pos[m], m);
-        const float* tr = rope.tab + (m < M ? rope.pos[m] : 0) * rope.hd;
-        const int half = rope.hd >> 1;
-        const int hj = half >> 4;   // tiles per half head: 2 (hd 64) or 4 (hd 128)
+      const int m = row0 + 16 * i;
+      if constexpr (HD != 0) {
+        if (do_rope) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int jh = j % (2 * hj);
-          if (jh < hj && wcol0 + 16 * j < rope.cols) {
-            const f32x4 cs = *reinterpret_cast<const f32x4*>(tr + 16 * jh + 4 * g);
-            const f32x4 sn = *reinterpret_cast<const f32x4*>(tr + half + 16 * jh + 4 * g);
-            const f32x4 x1 = v[j], x2 = v[j + hj];
-            v[j] = x1 * cs - x2 * sn;
-            v[j + hj] = x2 * cs + x1 * sn;
+          for (int j = 0; j < 8; ++j) {
+            const int jh = j % (2 * HJ);
+            if (jh < HJ && wcol0 + 16 * j < rope.cols) {
+              const f32x4 x1 = v[j], x2 = v[j + HJ];
+              v[j] = x1 * cs[jh] - x2 * sn[jh];
+              v[j + HJ] = x2 * cs[jh] + x1 * sn[jh];
+            }
           }
+          if (i + 1 < 8) rope_load(i + 1);
         }
       }
+      const bool mok = m < M;
+      const unsigned rbase = (unsigned)(mok ? m : 0) * (unsigned)ldc * 2u;
 #pragma unroll
       for (int jp = 0; jp < NJ / 2; ++jp) {
         const bf16x4 o0 = {(bf16)v[2 * jp][0], (bf16)v[2 * jp][1], (bf16)v[2 * jp][2], (bf16)v[2 * jp][3]};
@@ -242,8 +271,7 @@ __device__ __forceinline__ void epilogue(const char* bias_lds, bool has_bias, co
         const auto sy = __builtin_amdgcn_permlane16_swap(d[1], e[1], false, false);
         const u32x4 w = {sx[0], sy[0], sx[1], sy[1]};
         const int n = wcol0 + 32 * jp + colg;
-        const bool ok = m < M && n < N;
-        const unsigned off = ok ? (unsigned)(((long long)m * ldc + n) * 2) : kOOB;
+        const unsigned off = (mok && n < N) ? rbase + (unsigned)n * 2u : kOOB;
         __builtin_amdgcn_raw_buffer_store_b128(w, rc, off, 0, 0);
       }
     });
@@ -252,12 +280,13 @@ __device__ __forceinline__ void epilogue(const char* bias_lds, bool has_bias, co
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)cbase, (short)0, (int)c_bytes, 0x00020000);
     static_for<0, 8>([&](auto I) {
       constexpr int i = decltype(I)::value;
-      const int m = ci.m0 + wm * 128 + 16 * i + (l & 15);
+      const int m = row0 + 16 * i;
+      const bool mok = m < M;
+      const unsigned rbase = (unsigned)(mok ? m : 0) * (unsigned)ldc * 4u;
       static_for<0, NJ>([&](auto J) {
         constexpr int j = decltype(J)::value;
         const int n = wcol0 + 16 * j + 4 * g;
-        const bool ok = m < M && n < N;
-        const unsigned off = ok ? (unsigned)(((long long)m * ldc + n) * 4) : kOOB;
+        const unsigned off = (mok && n < N) ? rbase + (unsigned)n * 4u : kOOB;
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc_read<i, j>()), rc, off, 0, 0);
       });
     });
@@ -275,9 +304,9 @@ __device__ __forceinline__ void epilogue(const char* bias_lds, bool has_bias, co
 // BN: tile columns, 256 (waves 128 x 128) or 192 (waves 128 x 96: the N = 768 projections
 // become 512 tiles, two per CU, instead of 384 = 1.5 per CU).  Per stage a wave issues NQ =
 // 4 + BN/64 DMA pieces (4 of A, 4 or 3 of B).
-// ROPE: the RoPE epilogue is compiled in (QKV projection only: its code and SGPR pressure
-// stay out of the plain kernels).
-template <bool AK, bool BKM, int OUT, int DIAG = 0, bool FAST = false, int SCHED = 0, int BN = 256, bool ROPE = false>
+// ROPE (head_dim 64 / 128, 0 = none): the RoPE epilogue is compiled in (QKV projection only:
+// its code and register pressure stay out of the plain kernels).
+template <bool AK, bool BKM, int OUT, int DIAG = 0, bool FAST = false, int SCHED = 0, int BN = 256, int ROPE = 0>
 __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                   void* __restrict__ C, const float* __restrict__ bias, int M, int N,
                                                   int K, int lda, int ldb, int ldc, int kps, int splits,
@@ -471,6 +500,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
                                                  4, n < N ? (unsigned)(n * 4) : kOOB, 0, 0, 0);
       }
     }
+
     c_slot = (c_slot + 1) & 3;
     const char* src = smem + c_slot * SLOT;
     // Rows q of NJ MFMAs (A fragment q against every B fragment).  Rows 0-3 read the next
@@ -521,7 +551,10 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
       t_mark = t;
     }
     if (OUT == 0 && bias) wait_vmcnt<NQ>();   // this wave's bias DMA landed (NQ younger ring pieces)
-    epilogue<OUT, BN, ROPE>(bias_lds, bias != nullptr, ci, C, rope, M, N, ldc, slab_stride, c_bytes, wm, wn, l);
+    if (OUT == 0 && bias)
+      epilogue<OUT, BN, ROPE, true>(bias_lds, ci, C, rope, M, N, ldc, slab_stride, c_bytes, wm, wn, l);
+    else
+      epilogue<OUT, BN, ROPE, false>(bias_lds, ci, C, rope, M, N, ldc, slab_stride, c_bytes, wm, wn, l);
     if constexpr (DIAG) {
       const unsigned long long t = stamp();
       t_epi += t - t_mark;
@@ -627,10 +660,14 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
   do {                                                                                            \
     if constexpr (AK_ && BK_ && OUT_ == 0) {                                                      \
       if (rope_cols > 0) {                                                                        \
-        if (fast)                                                                                 \
-          gemm4_k<AK_, BK_, OUT_, 0, true, 1, 256, true><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);      \
+        if (fast && rope_hd == 64)                                                                \
+          gemm4_k<AK_, BK_, OUT_, 0, true, 1, 256, 64><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);        \
+        else if (fast)                                                                            \
+          gemm4_k<AK_, BK_, OUT_, 0, true, 1, 256, 128><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);       \
+        else if (rope_hd == 64)                                                                   \
+          gemm4_k<AK_, BK_, OUT_, 0, false, 0, 256, 64><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);       \
         else                                                                                      \
-          gemm4_k<AK_, BK_, OUT_, 0, false, 0, 256, true><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);     \
+          gemm4_k<AK_, BK_, OUT_, 0, false, 0, 256, 128><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);      \
         break;                                                                                    \
       }                                                                                           \
     }                                                                                             \

@@ -775,3 +775,4 @@ def test_gemm_v4_split_k_bf16_long_k(C):
     finally:
         C.gemm_v4_mask(old)
     assert _rel(out, R.gemm_nn(a.float(), b.float())) < 1e-2
+

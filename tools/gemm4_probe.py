@@ -27,12 +27,14 @@ SHAPES = {
 BIT = {"nt": 1, "nn": 2, "tn": 4}
 
 
-def operands(layout, M, N, K, gen):
+def operands(layout, M, N, K, gen, bias=False):
     r = lambda *s: torch.randn(*s, device="cuda", generator=gen).bfloat16()
     if layout == "nt":
         a, b = r(M, K), r(N, K)
-        return a, b, (lambda C: C.gemm_nt(a, b, None)), (lambda: torch.nn.functional.linear(a, b)), \
-            (lambda: a.float() @ b.float().t())
+        bv = torch.randn(N, device="cuda", generator=gen) if bias else None
+        bb = bv.bfloat16() if bias else None
+        return a, b, (lambda C: C.gemm_nt(a, b, bv)), (lambda: torch.nn.functional.linear(a, b, bb)), \
+            (lambda: a.float() @ b.float().t() + (bv if bias else 0))
     if layout == "nn":
         a, b = r(M, K), r(K, N)
         return a, b, (lambda C: C.gemm_nn(a, b)), (lambda: torch.matmul(a, b)), (lambda: a.float() @ b.float())
@@ -61,6 +63,7 @@ def main():
     ap.add_argument("--check-only", action="store_true")
     ap.add_argument("--scheds", type=int, nargs="+", default=[0, 1, 2])
     ap.add_argument("--no-blas", action="store_true")
+    ap.add_argument("--bias", action="store_true", help="NT with an fp32 bias (the projections that carry one)")
     ap.add_argument("--bn", type=int, nargs="*", default=[],
                     help="extra arms: the last --scheds variant with the v4 tile width forced (256 / 192)")
     ap.add_argument("--group-m", type=int, nargs="*", default=[],
@@ -76,7 +79,7 @@ def main():
         for name, M, N, K in SHAPES[layout]:
             if a.shapes and name not in a.shapes:
                 continue
-            _, _, ours, blas, ref = operands(layout, M, N, K, gen)
+            _, _, ours, blas, ref = operands(layout, M, N, K, gen, a.bias)
             want = ref() if M * N <= 50304 * 768 * 2 else None
             res = {}
             for tag, mask, sc, bn in [(f"v4s{sc}", 7, sc, 0) for sc in a.scheds] + \
