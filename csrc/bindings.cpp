@@ -45,10 +45,12 @@ void dpfs_layernorm_fwd(int, const void*, const float*, const float*, void*, flo
 int dpfs_norm_bwd_grid(int);
 void dpfs_norm_bwd(int, int, const void*, const void*, const float*, const float*, const float*, const void*, void*,
                    float*, float*, float*, float*, int, int, hipStream_t);
-void dpfs_swiglu_fwd(int, const void*, void*, int, int, hipStream_t);
-void dpfs_swiglu_bwd(int, const void*, const void*, void*, int, int, hipStream_t);
+void dpfs_swiglu_fwd(int, const void*, void*, int, int, int, hipStream_t);
+void dpfs_swiglu_bwd(int, const void*, const void*, void*, int, int, int, hipStream_t);
 long long dpfs_swiglu_bwd_dbias_ws(int, int);
-void dpfs_swiglu_bwd_dbias(int, const void*, const void*, void*, float*, float*, int, int, hipStream_t);
+void dpfs_swiglu_bwd_dbias(int, const void*, const void*, void*, float*, float*, int, int, int, hipStream_t);
+bool dpfs_gemm4_nt_swiglu(const void*, const void*, void*, const float*, void*, int, int, int, int, int, int, int,
+                          unsigned, unsigned, hipStream_t);
 long long dpfs_ce_bwd_dbias_ws(int, int, int);
 void dpfs_ce_bwd_dbias(int, const void*, const int64_t*, const float*, const float*, void*, float*, float*, int, int,
                        long long, int, hipStream_t);
@@ -451,28 +453,57 @@ std::vector<torch::Tensor> layernorm_bwd(torch::Tensor dy, torch::Tensor x, torc
 }
 
 // ------------------------------------------------------------------------ elementwise --
-torch::Tensor swiglu_fwd(torch::Tensor gu) {
+// h = silu(gate) * up; `perm`: gu in the interleaved layout of the fused gate|up epilogue.
+torch::Tensor swiglu_fwd(torch::Tensor gu, bool perm) {
   check_rowmajor(gu, "gu");
   TORCH_CHECK(gu.is_contiguous(), "swiglu: gu must be contiguous");
   const int dt = dcode(gu);
   const int64_t M = gu.size(0), F = gu.size(1) / 2;
   TORCH_CHECK(gu.size(1) % 2 == 0 && F % (dt == 1 ? 8 : 4) == 0, "swiglu: F must be a multiple of the vector width");
+  TORCH_CHECK(!perm || F % 64 == 0, "swiglu: the interleaved layout needs F % 64 == 0");
   const at::DeviceGuard g(gu.device());
   auto h = torch::empty({M, F}, gu.options());
-  if (M) dpfs_swiglu_fwd(dt, gu.data_ptr(), h.data_ptr(), (int)M, (int)F, stream());
+  if (M) dpfs_swiglu_fwd(dt, gu.data_ptr(), h.data_ptr(), (int)M, (int)F, perm ? 1 : 0, stream());
   return h;
+}
+
+// Gate|up projection with SwiGLU in the GEMM epilogue: w's rows interleaved in 64-row blocks
+// (ops.gemm_select.gu_perm), bias likewise.  Returns [gu (interleaved), h] or [] where the
+// fused kernel does not apply (the caller runs gemm_nt + swiglu_fwd).
+std::vector<torch::Tensor> gemm_nt_swiglu(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> bias) {
+  check_rowmajor(a, "a");
+  check_rowmajor(b, "b");
+  TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16,
+              "gemm_nt_swiglu: bf16 operands");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K, "gemm_nt_swiglu: K mismatch");
+  const at::DeviceGuard g(a.device());
+  auto span = [](const torch::Tensor& t) -> long long {
+    return t.size(0) > 0 ? ((t.size(0) - 1) * t.stride(0) + t.size(1)) * 2 : 0;
+  };
+  if (M == 0 || N % 128 || K % 64 || a.stride(0) % 8 || b.stride(0) % 8 || span(a) >= (1ll << 32) - 16 ||
+      span(b) >= (1ll << 32) - 16)
+    return {};
+  auto c = torch::empty({M, N}, a.options());
+  auto h = torch::empty({M, N / 2}, a.options());
+  if (!dpfs_gemm4_nt_swiglu(a.data_ptr(), b.data_ptr(), c.data_ptr(), opt_f32(bias, N, "bias"), h.data_ptr(), (int)M,
+                            (int)N, (int)K, (int)a.stride(0), (int)b.stride(0), (int)N, (int)(N / 2),
+                            (unsigned)span(a), (unsigned)span(b), stream()))
+    return {};
+  return {c, h};
 }
 
 
 // dgu = SwiGLU'(gu) * dh; with `dbias` the gate|up bias gradient (column sums of dgu) is
 // written there by the same pass.
-torch::Tensor swiglu_bwd(torch::Tensor dh, torch::Tensor gu, c10::optional<torch::Tensor> dbias) {
+torch::Tensor swiglu_bwd(torch::Tensor dh, torch::Tensor gu, c10::optional<torch::Tensor> dbias, bool perm) {
   check_rowmajor(gu, "gu");
   const int dt = dcode(gu);
   const int64_t M = gu.size(0), F = gu.size(1) / 2;
   TORCH_CHECK(dh.is_contiguous() && dh.size(0) == M && dh.size(1) == F && dh.scalar_type() == gu.scalar_type(),
               "swiglu_bwd: dh");
   TORCH_CHECK(F % (dt == 1 ? 8 : 4) == 0, "swiglu: F must be a multiple of the vector width");
+  TORCH_CHECK(!perm || F % 64 == 0, "swiglu: the interleaved layout needs F % 64 == 0");
   const at::DeviceGuard g(gu.device());
   auto dgu = torch::empty_like(gu);
   float* db = dbias_out(dbias, 2 * F, "swiglu_bwd");
@@ -483,9 +514,9 @@ torch::Tensor swiglu_bwd(torch::Tensor dh, torch::Tensor gu, c10::optional<torch
     const long long wsn = dpfs_swiglu_bwd_dbias_ws((int)M, (int)F);
     auto ws = torch::empty({std::max<long long>(wsn, 1)}, gu.options().dtype(torch::kFloat32));
     dpfs_swiglu_bwd_dbias(dt, dh.data_ptr(), gu.data_ptr(), dgu.data_ptr(), db, ws.data_ptr<float>(), (int)M, (int)F,
-                          stream());
+                          perm ? 1 : 0, stream());
   } else {
-    dpfs_swiglu_bwd(dt, dh.data_ptr(), gu.data_ptr(), dgu.data_ptr(), (int)M, (int)F, stream());
+    dpfs_swiglu_bwd(dt, dh.data_ptr(), gu.data_ptr(), dgu.data_ptr(), (int)M, (int)F, perm ? 1 : 0, stream());
   }
   return dgu;
 }
@@ -1102,8 +1133,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dres") = py::none(), py::arg("dbias") = py::none());
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
-  m.def("swiglu_fwd", &swiglu_fwd);
-  m.def("swiglu_bwd", &swiglu_bwd, py::arg("dh"), py::arg("gu"), py::arg("dbias") = py::none());
+  m.def("swiglu_fwd", &swiglu_fwd, py::arg("gu"), py::arg("perm") = false);
+  m.def("swiglu_bwd", &swiglu_bwd, py::arg("dh"), py::arg("gu"), py::arg("dbias") = py::none(),
+        py::arg("perm") = false);
+  m.def("gemm_nt_swiglu", &gemm_nt_swiglu,
+        "gate|up NT GEMM (rows interleaved in 64-row blocks) with SwiGLU in the epilogue: [gu, h] or []",
+        py::arg("a"), py::arg("b"), py::arg("bias") = py::none());
   m.def("rope_", &rope_, py::arg("qkv"), py::arg("positions"), py::arg("table"), py::arg("n_rot_heads"),
         py::arg("head_dim"), py::arg("inverse") = false);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("scale"), py::arg("causal") = true);

@@ -18,7 +18,14 @@ static inline int cap_grid(long long work, int block) {
 
 // ---------------------------------------------------------------------------- SwiGLU --
 // gu[M, 2F] = [gate | up]  ->  h[M, F] = silu(gate) * up.   (models/model.py:94-95)
-template <typename T>
+// PERM: gu in the interleaved layout of the fused gate|up epilogue (ops.gemm_select.gu_perm:
+// columns [128 b, 128 b + 64) = gate [64 b, 64 b + 64), the next 64 = up of the same columns).
+template <bool PERM>
+__device__ __forceinline__ long long gate_col(long long c, int F) { return PERM ? ((c >> 6) << 7) + (c & 63) : c; }
+template <bool PERM>
+__device__ __forceinline__ long long up_col(long long c, int F) { return PERM ? gate_col<true>(c, F) + 64 : F + c; }
+
+template <typename T, bool PERM = false>
 __global__ __launch_bounds__(256) void swiglu_fwd_k(const T* __restrict__ gu, T* __restrict__ h, int M, int F) {
   constexpr int N = Vec<T>::N;
   const long long per_row = F / N;
@@ -26,8 +33,8 @@ __global__ __launch_bounds__(256) void swiglu_fwd_k(const T* __restrict__ gu, T*
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     const long long r = i / per_row, c = (i % per_row) * N;
     float g[N], u[N], o[N];
-    load_vec<T>(gu + r * 2 * F + c, g);
-    load_vec<T>(gu + r * 2 * F + F + c, u);
+    load_vec<T>(gu + r * 2 * F + gate_col<PERM>(c, F), g);
+    load_vec<T>(gu + r * 2 * F + up_col<PERM>(c, F), u);
 #pragma unroll
     for (int j = 0; j < N; ++j) o[j] = silu_f(g[j]) * u[j];
     store_vec<T>(h + r * F + c, o);
@@ -35,7 +42,7 @@ __global__ __launch_bounds__(256) void swiglu_fwd_k(const T* __restrict__ gu, T*
 }
 
 // dgu[:, :F] = dh * up * sig(g) * (1 + g (1 - sig(g)));  dgu[:, F:] = dh * silu(g)
-template <typename T>
+template <typename T, bool PERM = false>
 __global__ __launch_bounds__(256) void swiglu_bwd_k(const T* __restrict__ dh, const T* __restrict__ gu,
                                                     T* __restrict__ dgu, int M, int F) {
   constexpr int N = Vec<T>::N;
@@ -44,8 +51,8 @@ __global__ __launch_bounds__(256) void swiglu_bwd_k(const T* __restrict__ dh, co
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     const long long r = i / per_row, c = (i % per_row) * N;
     float g[N], u[N], d[N], og[N], ou[N];
-    load_vec<T>(gu + r * 2 * F + c, g);
-    load_vec<T>(gu + r * 2 * F + F + c, u);
+    load_vec<T>(gu + r * 2 * F + gate_col<PERM>(c, F), g);
+    load_vec<T>(gu + r * 2 * F + up_col<PERM>(c, F), u);
     load_vec<T>(dh + r * F + c, d);
 #pragma unroll
     for (int j = 0; j < N; ++j) {
@@ -53,8 +60,8 @@ __global__ __launch_bounds__(256) void swiglu_bwd_k(const T* __restrict__ dh, co
       og[j] = d[j] * u[j] * s * (1.f + g[j] * (1.f - s));
       ou[j] = d[j] * g[j] * s;
     }
-    store_vec<T>(dgu + r * 2 * F + c, og);
-    store_vec<T>(dgu + r * 2 * F + F + c, ou);
+    store_vec<T>(dgu + r * 2 * F + gate_col<PERM>(c, F), og);
+    store_vec<T>(dgu + r * 2 * F + up_col<PERM>(c, F), ou);
   }
 }
 
@@ -269,7 +276,9 @@ static int colsum_plan(int M, int cblocks, int target_blocks, int* rpc) {
 // vector and its up partner, walks its row chunk, stores dgu and accumulates both column
 // sums in fp32; the block's 8 row lanes are reduced through LDS in a fixed order and
 // written as partials[chunk][2F] (deterministic; stage 2 = colsum_stage_k<float>).
-template <typename T>
+// (PERM: dgu in the interleaved layout of gu; the bias-gradient partials stay in natural
+// [gate | up] order.)
+template <typename T, bool PERM = false>
 __global__ __launch_bounds__(256) void swiglu_bwd_colsum_k(const T* __restrict__ dh, const T* __restrict__ gu,
                                                            T* __restrict__ dgu, float* __restrict__ partial, int M,
                                                            int F, int rows_per_chunk) {
@@ -292,8 +301,8 @@ __global__ __launch_bounds__(256) void swiglu_bwd_colsum_k(const T* __restrict__
       for (int q = 0; q < U; ++q) {
         const long long rr = r + 8 * q;
         if (q == 0 || rr < r1) {
-          load_vec<T>(gu + rr * 2 * F + c0, g[q]);
-          load_vec<T>(gu + rr * 2 * F + F + c0, u[q]);
+          load_vec<T>(gu + rr * 2 * F + gate_col<PERM>(c0, F), g[q]);
+          load_vec<T>(gu + rr * 2 * F + up_col<PERM>(c0, F), u[q]);
           load_vec<T>(dh + rr * F + c0, d[q]);
         }
       }
@@ -310,8 +319,8 @@ __global__ __launch_bounds__(256) void swiglu_bwd_colsum_k(const T* __restrict__
           ag[j] += og[j];
           au[j] += ou[j];
         }
-        store_vec<T>(dgu + rr * 2 * F + c0, og);
-        store_vec<T>(dgu + rr * 2 * F + F + c0, ou);
+        store_vec<T>(dgu + rr * 2 * F + gate_col<PERM>(c0, F), og);
+        store_vec<T>(dgu + rr * 2 * F + up_col<PERM>(c0, F), ou);
       }
     }
   }
@@ -355,20 +364,28 @@ static void colsum_launch(const T* x, float* out, float* ws, int M, int N_, hipS
 
 using namespace dpfs;
 
-extern "C" void dpfs_swiglu_fwd(int dtype, const void* gu, void* h, int M, int F, hipStream_t s) {
-  if (dtype == kBF16)
-    swiglu_fwd_k<bf16><<<cap_grid((long long)M * F / 8, 256), 256, 0, s>>>((const bf16*)gu, (bf16*)h, M, F);
-  else
-    swiglu_fwd_k<float><<<cap_grid((long long)M * F / 4, 256), 256, 0, s>>>((const float*)gu, (float*)h, M, F);
+#define DPFS_PERM(P, ...) \
+  do {                    \
+    if (P) {              \
+      constexpr bool PM = true; __VA_ARGS__; \
+    } else {              \
+      constexpr bool PM = false; __VA_ARGS__; \
+    }                     \
+  } while (0)
+
+extern "C" void dpfs_swiglu_fwd(int dtype, const void* gu, void* h, int M, int F, int perm, hipStream_t s) {
+  DPFS_PERM(perm, if (dtype == kBF16) swiglu_fwd_k<bf16, PM><<<cap_grid((long long)M * F / 8, 256), 256, 0, s>>>(
+                      (const bf16*)gu, (bf16*)h, M, F);
+                  else swiglu_fwd_k<float, PM><<<cap_grid((long long)M * F / 4, 256), 256, 0, s>>>(
+                      (const float*)gu, (float*)h, M, F));
 }
 
-extern "C" void dpfs_swiglu_bwd(int dtype, const void* dh, const void* gu, void* dgu, int M, int F, hipStream_t s) {
-  if (dtype == kBF16)
-    swiglu_bwd_k<bf16><<<cap_grid((long long)M * F / 8, 256), 256, 0, s>>>((const bf16*)dh, (const bf16*)gu,
-                                                                              (bf16*)dgu, M, F);
-  else
-    swiglu_bwd_k<float><<<cap_grid((long long)M * F / 4, 256), 256, 0, s>>>((const float*)dh, (const float*)gu,
-                                                                               (float*)dgu, M, F);
+extern "C" void dpfs_swiglu_bwd(int dtype, const void* dh, const void* gu, void* dgu, int M, int F, int perm,
+                                hipStream_t s) {
+  DPFS_PERM(perm, if (dtype == kBF16) swiglu_bwd_k<bf16, PM><<<cap_grid((long long)M * F / 8, 256), 256, 0, s>>>(
+                      (const bf16*)dh, (const bf16*)gu, (bf16*)dgu, M, F);
+                  else swiglu_bwd_k<float, PM><<<cap_grid((long long)M * F / 4, 256), 256, 0, s>>>(
+                      (const float*)dh, (const float*)gu, (float*)dgu, M, F));
 }
 
 // Workspace (floats) for dpfs_swiglu_bwd_dbias: partials [chunks, 2F].
@@ -379,18 +396,16 @@ extern "C" long long dpfs_swiglu_bwd_dbias_ws(int M, int F) {
 }
 
 extern "C" void dpfs_swiglu_bwd_dbias(int dtype, const void* dh, const void* gu, void* dgu, float* dbias, float* ws,
-                                      int M, int F, hipStream_t s) {
+                                      int M, int F, int perm, hipStream_t s) {
   const int vec = dtype == kBF16 ? 8 : 4;
   const int cblocks = (F / vec + 31) / 32;
   int rpc;
   const int chunks = colsum_plan(M, cblocks, 2048, &rpc);
   float* part = chunks > 1 ? ws : dbias;
-  if (dtype == kBF16)
-    swiglu_bwd_colsum_k<bf16><<<dim3(cblocks, chunks), 256, 0, s>>>((const bf16*)dh, (const bf16*)gu, (bf16*)dgu,
-                                                                    part, M, F, rpc);
-  else
-    swiglu_bwd_colsum_k<float><<<dim3(cblocks, chunks), 256, 0, s>>>((const float*)dh, (const float*)gu, (float*)dgu,
-                                                                     part, M, F, rpc);
+  DPFS_PERM(perm, if (dtype == kBF16) swiglu_bwd_colsum_k<bf16, PM><<<dim3(cblocks, chunks), 256, 0, s>>>(
+                      (const bf16*)dh, (const bf16*)gu, (bf16*)dgu, part, M, F, rpc);
+                  else swiglu_bwd_colsum_k<float, PM><<<dim3(cblocks, chunks), 256, 0, s>>>(
+                      (const float*)dh, (const float*)gu, (float*)dgu, part, M, F, rpc));
   if (chunks > 1) colsum_rows(ws, dbias, chunks, 2 * F, s);
 }
 

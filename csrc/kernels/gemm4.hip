@@ -66,6 +66,18 @@ struct Rope {
   int hd;             // 64 or 128
 };
 
+// SwiGLU in the gate|up projection's epilogue (reference models/model.py:94-95): the packed
+// weight's rows are interleaved in 64-row blocks (ops.gemm_select.gu_perm: output columns
+// [128 b, 128 b + 64) = gate rows [64 b, 64 b + 64), the next 64 = the matching up rows), so a
+// wave's 128 columns hold 64 gate / up pairs in the same lane (tiles j and j + 4).  Besides
+// the (interleaved) gate|up output, h[:, 64 b + c] = silu(gate) * up of the bf16-rounded
+// values -- the swiglu_fwd_k arithmetic, bit for bit.
+struct SwiOut {
+  bf16* h;
+  int ldh;
+  unsigned h_bytes;
+};
+
 struct Dual {
   const bf16* A2;
   const bf16* B2;
@@ -198,10 +210,12 @@ __device__ __forceinline__ int nsteps(const Item& it) {
 // template flag, no per-tile branch or LDS wait), store offsets are 32-bit selects (the C span
 // fits the descriptor, so row * ldc cannot overflow), and the RoPE rows' positions and
 // cos / sin values are loaded one 16-row block ahead of their use.
-template <int OUT, int BN, int ROPE, bool HAS_BIAS>
+__device__ __forceinline__ float silu_ref(float g) { return g / (1.f + __expf(-g)); }
+
+template <int OUT, int BN, int ROPE, bool HAS_BIAS, bool SWIGLU = false>
 __device__ __forceinline__ void epilogue(const char* bias_lds, const Item& ci, void* C, const Rope& rope, int M,
                                          int N, int ldc, long long slab_stride, unsigned c_bytes, int wm, int wn,
-                                         int l) {
+                                         int l, const SwiOut& swo = SwiOut{}) {
   constexpr int NJ = BN / 32;
   const int g = l >> 4;
   const int wcol0 = ci.n0 + wn * (BN / 2);
@@ -261,6 +275,33 @@ __device__ __forceinline__ void epilogue(const char* bias_lds, const Item& ci, v
       }
       const bool mok = m < M;
       const unsigned rbase = (unsigned)(mok ? m : 0) * (unsigned)ldc * 2u;
+      if constexpr (SWIGLU) {
+        // h of this lane's 16 gate / up pairs -> 2 stores (exactly, every 16-row block)
+        const __amdgpu_buffer_rsrc_t rh =
+            __builtin_amdgcn_make_buffer_rsrc((void*)swo.h, (short)0, (int)swo.h_bytes, 0x00020000);
+        const unsigned hbase = (unsigned)(mok ? m : 0) * (unsigned)swo.ldh * 2u;
+        f32x4 hv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float gg = (float)(bf16)v[j][e], uu = (float)(bf16)v[j + 4][e];
+            hv[j][e] = silu_ref(gg) * uu;
+          }
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          const bf16x4 o0 = {(bf16)hv[2 * jp][0], (bf16)hv[2 * jp][1], (bf16)hv[2 * jp][2], (bf16)hv[2 * jp][3]};
+          const bf16x4 o1 = {(bf16)hv[2 * jp + 1][0], (bf16)hv[2 * jp + 1][1], (bf16)hv[2 * jp + 1][2],
+                             (bf16)hv[2 * jp + 1][3]};
+          const u32x2 d = __builtin_bit_cast(u32x2, o0), e = __builtin_bit_cast(u32x2, o1);
+          const auto sx = __builtin_amdgcn_permlane16_swap(d[0], e[0], false, false);
+          const auto sy = __builtin_amdgcn_permlane16_swap(d[1], e[1], false, false);
+          const u32x4 w = {sx[0], sy[0], sx[1], sy[1]};
+          const int hn = (wcol0 >> 1) + 32 * jp + colg;
+          const unsigned off = (mok && 2 * hn < N) ? hbase + (unsigned)hn * 2u : kOOB;
+          __builtin_amdgcn_raw_buffer_store_b128(w, rh, off, 0, 0);
+        }
+      }
 #pragma unroll
       for (int jp = 0; jp < NJ / 2; ++jp) {
         const bf16x4 o0 = {(bf16)v[2 * jp][0], (bf16)v[2 * jp][1], (bf16)v[2 * jp][2], (bf16)v[2 * jp][3]};
@@ -306,18 +347,22 @@ __device__ __forceinline__ void epilogue(const char* bias_lds, const Item& ci, v
 // 4 + BN/64 DMA pieces (4 of A, 4 or 3 of B).
 // ROPE (head_dim 64 / 128, 0 = none): the RoPE epilogue is compiled in (QKV projection only:
 // its code and register pressure stay out of the plain kernels).
-template <bool AK, bool BKM, int OUT, int DIAG = 0, bool FAST = false, int SCHED = 0, int BN = 256, int ROPE = 0>
+// SWIGLU: the gate|up form (SwiOut).
+template <bool AK, bool BKM, int OUT, int DIAG = 0, bool FAST = false, int SCHED = 0, int BN = 256, int ROPE = 0,
+          bool SWIGLU = false>
 __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                   void* __restrict__ C, const float* __restrict__ bias, int M, int N,
                                                   int K, int lda, int ldb, int ldc, int kps, int splits,
                                                   long long slab_stride, unsigned a_bytes, unsigned b_bytes,
                                                   unsigned c_bytes, Rope rope, int group_m, Dual dual, int dbg,
-                                                  unsigned long long* diag) {
+                                                  unsigned long long* diag, SwiOut swo = SwiOut{}) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_TOTAL];
   constexpr int NJ = BN / 32;                  // 16-column MFMA tiles per wave
   constexpr int NBQ = BN / 64;                 // B pieces per wave per stage
   constexpr int NQ = 4 + NBQ;                  // DMA pieces per wave per stage
-  constexpr int STORES = OUT == 0 ? 4 * NJ : 8 * NJ;   // store instructions per wave per item
+  // store instructions per wave per item (+ the SwiGLU output's 2 per 16-row block)
+  constexpr int STORES = (OUT == 0 ? 4 * NJ : 8 * NJ) + (SWIGLU ? 16 : 0);
+  static_assert(!SWIGLU || (OUT == 0 && BN == 256 && ROPE == 0), "SwiGLU epilogue: bf16 256-wide tiles");
   static_assert(BN == 256 || BN == 192, "tile width");
 
   const int tiles_n = (N + BN - 1) / BN;
@@ -552,9 +597,9 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
     }
     if (OUT == 0 && bias) wait_vmcnt<NQ>();   // this wave's bias DMA landed (NQ younger ring pieces)
     if (OUT == 0 && bias)
-      epilogue<OUT, BN, ROPE, true>(bias_lds, ci, C, rope, M, N, ldc, slab_stride, c_bytes, wm, wn, l);
+      epilogue<OUT, BN, ROPE, true, SWIGLU>(bias_lds, ci, C, rope, M, N, ldc, slab_stride, c_bytes, wm, wn, l, swo);
     else
-      epilogue<OUT, BN, ROPE, false>(bias_lds, ci, C, rope, M, N, ldc, slab_stride, c_bytes, wm, wn, l);
+      epilogue<OUT, BN, ROPE, false, SWIGLU>(bias_lds, ci, C, rope, M, N, ldc, slab_stride, c_bytes, wm, wn, l, swo);
     if constexpr (DIAG) {
       const unsigned long long t = stamp();
       t_epi += t - t_mark;
@@ -609,6 +654,28 @@ extern "C" void dpfs_gemm4_sched(int v) { g_g4_sched = v; }
 static int g_g4_bn = 0;
 extern "C" void dpfs_gemm4_bn(int v) { g_g4_bn = v; }
 extern "C" void dpfs_gemm4_group_m(int g) { g_g4_group_m = g > 0 ? g : 4; }
+
+// gate|up projection with SwiGLU in the epilogue (SwiOut): C[M, N] = A B^T + bias with B's
+// rows interleaved (ops.gemm_select.gu_perm), H[M, N / 2] = silu(gate) * up.  Returns false
+// (nothing launched) where the 256-wide FAST kernel does not apply.
+extern "C" bool dpfs_gemm4_nt_swiglu(const void* A, const void* B, void* C, const float* bias, void* H, int M, int N,
+                                     int K, int lda, int ldb, int ldc, int ldh, unsigned a_bytes, unsigned b_bytes,
+                                     hipStream_t s) {
+  if (M <= 0 || N <= 0 || (N % 128) || (K % 64) || ldh < N / 2) return false;
+  const long long cspan = ((long long)(M - 1) * ldc + N) * 2;
+  const long long hspan = ((long long)(M - 1) * ldh + N / 2) * 2;
+  if (cspan >= (1ll << 32) - 16 || hspan >= (1ll << 32) - 16) return false;
+  const long long items = (long long)((M + 255) / 256) * ((N + 255) / 256);
+  if (items <= 0 || items >= (1ll << 31)) return false;
+  const int grid = (int)std::min<long long>(items, g4_cu_count());
+  const Rope rope = {nullptr, nullptr, 0, 64};
+  const Dual dual = {nullptr, nullptr, 0x7fffffff, lda, ldb, 0u, 0u};
+  const SwiOut swo = {(bf16*)H, ldh, (unsigned)hspan};
+  gemm4_k<true, true, 0, 0, true, 1, 256, 0, true><<<grid, 256, 0, s>>>(
+      (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, K, 1, 0, a_bytes, b_bytes, (unsigned)cspan, rope,
+      g_g4_group_m, dual, 0, nullptr, swo);
+  return true;
+}
 
 // Launch v4.  layout: 0 = NT (A K-major, B K-major), 1 = NN (B MN-major), 2 = TN (both
 // MN-major, fp32 out).  Returns false (nothing launched) when a span does not fit the 32-bit

@@ -35,10 +35,12 @@ import torch.distributed as dist
 
 from ..ops import fp8 as F8
 from ..ops import gemm_select as GS
+from ..ops import reference as R
 from ..ops.dispatch import K, shadow
 from ..parallel import process_manager as pm
 from ..parallel import tp_comm
-from .fused_engine import _QKV_BIAS_IN_ATTN, _Layer, _addg, _defer_begin, _defer_end, _defer_flush, _split, _wait
+from .fused_engine import (_QKV_BIAS_IN_ATTN, _Layer, _addg, _defer_begin, _defer_end, _defer_flush,
+                           _gate_up_weights, _split, _wait)
 
 
 def _rs(full: torch.Tensor, n: int):
@@ -83,6 +85,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
         f8map = F8.prepare([W(w) for L in layers for w in (L.wqkv, L.wo, L.wgu, L.wd)] + [W(model.lm_head.weight)]) \
             if getattr(model.args, "fp8", False) else None
         F8.activate(f8map)
+        _gate_up_weights(k, layers, W)
         st = []
         for c in range(C):
             b0, b1 = bounds[c], bounds[c + 1]
@@ -121,8 +124,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
             for ci, s in enumerate(st):    # P4: gate|up, SwiGLU, down -> reduce-scatter
                 _wait(s["h"])
                 a = s["layers"][-1]
-                gu = GS.gemm_nt(k, a["h2"], W(L.wgu), L.bgu)
-                sw = k.swiglu_fwd(gu)
+                gu, sw = GS.gate_up(k, a["h2"], L.wgu_p, L.bgu_p, L.swi)   # SwiGLU in the epilogue
                 qout = GS.gemm_nt(k, sw, W(L.wd), None, out=_slot(ci, sw.size(0), d, dt))
                 a.update(gu=gu, sw=sw)
                 (s["pend"], s["h"]), s["pend_bias"] = _rs(qout, n), L.bd
@@ -265,8 +267,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
             for s in st:
                 a = s["layers"][li]
                 _wait(a.pop("hh"))
-                a["gu"] = GS.gemm_nt(k, a["h2"], W(L.wgu), L.bgu)
-                a["sw"] = k.swiglu_fwd(a["gu"])
+                a["gu"], a["sw"] = GS.gate_up(k, a["h2"], L.wgu_p, L.bgu_p, L.swi)
 
         for li in range(nL - 1, -1, -1):
             L, G = layers[li], gl[li]
@@ -281,14 +282,16 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 ds = GS.gemm_nn(k, gq, W(L.wd))
                 wd_p.append((gq, a["sw"]))
                 dbgu = ds.new_empty(a["gu"].size(1), dtype=torch.float32) if L.bgu is not None else None
-                dgu = k.swiglu_bwd(ds, a["gu"], dbgu)
-                s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dgu, W(L.wgu), out=_slot(ci, dgu.size(0), d, dt)), n)
+                dgu = k.swiglu_bwd(ds, a["gu"], dbgu, L.swi)
+                s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dgu, L.wgu_p, out=_slot(ci, dgu.size(0), d, dt)), n)
                 wgu_p.append((dgu, a["h2"]))
                 if dbgu is not None:
                     G["bgu"] = _addg(G.get("bgu"), dbgu)
                 del a["sw"], a["gu"], a["h2"], s["gfull"]
             tn_chunks(G, "wd", wd_p)       # under the chunks' reduce-scatters
             tn_chunks(G, "wgu", wgu_p)
+            if L.swi:                       # interleaved rows (fused SwiGLU epilogue) -> natural
+                G["wgu"] = R.gu_unperm(G["wgu"])
             for s in st:    # B3: norm2 backward (+ residual grad) on my rows -> all-gather
                 _wait(s["h"])
                 a = s["layers"][li]

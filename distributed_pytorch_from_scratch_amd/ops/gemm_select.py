@@ -205,6 +205,34 @@ def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, out=None) -> torch.T
     return blas() if c == "blas" else lt(_lt_index(c))()
 
 
+def swiglu_epilogue(k, w: torch.Tensor) -> bool:
+    """Whether the gate|up projection of packed weight ``w`` [2F, d] runs with SwiGLU in its GEMM
+    epilogue (``gate_up``): on the GPU by default (``DPFS_SWIGLU_EPILOGUE=0`` turns it off,
+    as do a pinned library backend and the fp8 step), on the CPU oracle only when that
+    variable is 1 (tests of the interleaved layout's plumbing)."""
+    env = os.environ.get("DPFS_SWIGLU_EPILOGUE", "")
+    if w.size(0) % 128 or env == "0":
+        return False
+    if k is reference or not w.is_cuda:
+        return env == "1"
+    return mode() in ("auto", "ours") and F8.lookup(w) is None and hasattr(k, "gemm_nt_swiglu")
+
+
+def gate_up(k, x: torch.Tensor, w_p: torch.Tensor, b_p, perm: bool):
+    """(gu, h = silu(gate) * up) of the gate|up projection.  ``perm``: ``w_p`` / ``b_p`` are
+    interleaved (reference.gu_perm) and the GEMM writes h from its epilogue (gemm_nt_swiglu;
+    gu comes out interleaved too); where the fused kernel declines the shape, the plain GEMM
+    and the interleaved SwiGLU pass give the same tensors."""
+    if perm:
+        r = k.gemm_nt_swiglu(x, w_p, b_p)
+        if r:
+            return r[0], r[1]
+        gu = gemm_nt(k, x, w_p, b_p)
+        return gu, k.swiglu_fwd(gu, True)
+    gu = gemm_nt(k, x, w_p, b_p)
+    return gu, k.swiglu_fwd(gu)
+
+
 def small_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, swiglu: bool = False) -> torch.Tensor:
     """Decode-step projection, M <= 16 rows: y = a w^T (+ bias), a = x or, with ``swiglu``,
     silu(gate) * up of the packed x = [gate | up].  The MFMA GEMV-class kernel (gemv16_k,

@@ -297,16 +297,49 @@ def attn_bwd(do, q, k, v, o, lse, scale: float, causal: bool, dq_out, dk_out, dv
 
 # ------------------------------------------------------------------------- SwiGLU ----
 
-def swiglu_fwd(gu: torch.Tensor) -> torch.Tensor:
+def gu_perm(x: torch.Tensor, dim: int = 0) -> torch.Tensor:
+    """Interleave a packed [gate | up] dimension (size 2F, F % 64 == 0) in 64-blocks: positions
+    [128 b, 128 b + 64) = gate [64 b, 64 b + 64), the next 64 = up [64 b, 64 b + 64).  The fused
+    gate|up GEMM epilogue (csrc/kernels/gemm4.hip SwiOut) then holds each gate / up pair in one
+    lane.  ``gu_unperm`` is the inverse."""
+    n = x.size(dim)
+    sh = list(x.shape)
+    v = x.reshape(sh[:dim] + [2, n // 128, 64] + sh[dim + 1:])
+    return v.transpose(dim, dim + 1).reshape(sh)
+
+
+def gu_unperm(x: torch.Tensor, dim: int = 0) -> torch.Tensor:
+    n = x.size(dim)
+    sh = list(x.shape)
+    v = x.reshape(sh[:dim] + [n // 128, 2, 64] + sh[dim + 1:])
+    return v.transpose(dim, dim + 1).reshape(sh)
+
+
+def _gate_up(gu: torch.Tensor, perm: bool):
+    if perm:
+        gu = gu_unperm(gu, gu.dim() - 1)
     F_ = gu.size(-1) // 2
-    g, u = gu[..., :F_].float(), gu[..., F_:].float()
+    return gu[..., :F_].float(), gu[..., F_:].float()
+
+
+def swiglu_fwd(gu: torch.Tensor, perm: bool = False) -> torch.Tensor:
+    """h = silu(gate) * up of a packed gate|up tensor (``perm``: interleaved, see gu_perm)."""
+    g, u = _gate_up(gu, perm)
     return (F.silu(g) * u).to(gu.dtype)
 
 
-def swiglu_bwd(dh: torch.Tensor, gu: torch.Tensor, dbias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """d gate|up; with ``dbias`` (fp32 [2F]) also writes the bias gradient (column sums)."""
-    F_ = gu.size(-1) // 2
-    g, u = gu[..., :F_].float(), gu[..., F_:].float()
+def gemm_nt_swiglu(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None):
+    """Gate|up projection with the SwiGLU of the fused GPU epilogue: b's rows (and the bias)
+    interleaved by gu_perm -> [gu (interleaved, a.dtype), h = silu(gate) * up (a.dtype)]."""
+    gu = gemm_nt(a, b, bias)
+    return [gu, swiglu_fwd(gu, True)]
+
+
+def swiglu_bwd(dh: torch.Tensor, gu: torch.Tensor, dbias: Optional[torch.Tensor] = None,
+               perm: bool = False) -> torch.Tensor:
+    """d gate|up (in gu's layout); with ``dbias`` (fp32 [2F]) also writes the bias gradient
+    (column sums, natural [gate | up] order)."""
+    g, u = _gate_up(gu, perm)
     dhf = dh.float()
     sig = torch.sigmoid(g)
     silu = g * sig
@@ -315,6 +348,8 @@ def swiglu_bwd(dh: torch.Tensor, gu: torch.Tensor, dbias: Optional[torch.Tensor]
     d = torch.cat([dg, du], dim=-1)
     if dbias is not None:
         dbias.copy_(d.sum(0))
+    if perm:
+        d = gu_perm(d, d.dim() - 1)
     return d.to(gu.dtype)
 
 
