@@ -467,9 +467,10 @@ torch::Tensor swiglu_fwd(torch::Tensor gu, bool perm) {
   return h;
 }
 
-// Gate|up projection with SwiGLU in the GEMM epilogue: w's rows interleaved in 64-row blocks
-// (ops.gemm_select.gu_perm), bias likewise.  Returns [gu (interleaved), h] or [] where the
-// fused kernel does not apply (the caller runs gemm_nt + swiglu_fwd).
+// Gate|up projection with SwiGLU in the GEMM epilogue: w / bias in the natural [gate | up]
+// layout, read with the rows interleaved in 64-row blocks (reference.gu_perm).  Returns
+// [gu (interleaved), h] or [] where the fused kernel does not apply (the caller runs the GEMM
+// on the interleaved weight + swiglu_fwd(perm)).
 std::vector<torch::Tensor> gemm_nt_swiglu(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> bias) {
   check_rowmajor(a, "a");
   check_rowmajor(b, "b");

@@ -60,8 +60,8 @@ __global__ __launch_bounds__(256) void swiglu_bwd_k(const T* __restrict__ dh, co
       og[j] = d[j] * u[j] * s * (1.f + g[j] * (1.f - s));
       ou[j] = d[j] * g[j] * s;
     }
-    store_vec<T>(dgu + r * 2 * F + gate_col<PERM>(c, F), og);
-    store_vec<T>(dgu + r * 2 * F + up_col<PERM>(c, F), ou);
+    store_vec<T>(dgu + r * 2 * F + c, og);
+    store_vec<T>(dgu + r * 2 * F + F + c, ou);
   }
 }
 
@@ -276,8 +276,8 @@ static int colsum_plan(int M, int cblocks, int target_blocks, int* rpc) {
 // vector and its up partner, walks its row chunk, stores dgu and accumulates both column
 // sums in fp32; the block's 8 row lanes are reduced through LDS in a fixed order and
 // written as partials[chunk][2F] (deterministic; stage 2 = colsum_stage_k<float>).
-// (PERM: dgu in the interleaved layout of gu; the bias-gradient partials stay in natural
-// [gate | up] order.)
+// (PERM: gu read in the interleaved layout; dgu and the bias-gradient partials are written in
+// the natural [gate | up] order, so the data / weight gradient GEMMs use the natural weight.)
 template <typename T, bool PERM = false>
 __global__ __launch_bounds__(256) void swiglu_bwd_colsum_k(const T* __restrict__ dh, const T* __restrict__ gu,
                                                            T* __restrict__ dgu, float* __restrict__ partial, int M,
@@ -319,8 +319,8 @@ __global__ __launch_bounds__(256) void swiglu_bwd_colsum_k(const T* __restrict__
           ag[j] += og[j];
           au[j] += ou[j];
         }
-        store_vec<T>(dgu + rr * 2 * F + gate_col<PERM>(c0, F), og);
-        store_vec<T>(dgu + rr * 2 * F + up_col<PERM>(c0, F), ou);
+        store_vec<T>(dgu + rr * 2 * F + c0, og);
+        store_vec<T>(dgu + rr * 2 * F + F + c0, ou);
       }
     }
   }

@@ -67,11 +67,16 @@ struct Rope {
 };
 
 // SwiGLU in the gate|up projection's epilogue (reference models/model.py:94-95): the packed
-// weight's rows are interleaved in 64-row blocks (ops.gemm_select.gu_perm: output columns
-// [128 b, 128 b + 64) = gate rows [64 b, 64 b + 64), the next 64 = the matching up rows), so a
-// wave's 128 columns hold 64 gate / up pairs in the same lane (tiles j and j + 4).  Besides
-// the (interleaved) gate|up output, h[:, 64 b + c] = silu(gate) * up of the bf16-rounded
-// values -- the swiglu_fwd_k arithmetic, bit for bit.
+// [gate | up] weight (natural layout) is read with its rows interleaved in 64-row blocks
+// (reference.gu_perm: output columns [128 b, 128 b + 64) = gate rows [64 b, 64 b + 64), the
+// next 64 = the matching up rows; the mapping is applied to the DMA pieces' row offsets and the
+// bias offsets, no copy), so a wave's 128 columns hold 64 gate / up pairs in the same lane
+// (tiles j and j + 4).  Besides the (interleaved) gate|up output, h[:, 64 b + c] =
+// silu(gate) * up of the bf16-rounded values -- the swiglu_fwd_k arithmetic, bit for bit.
+__device__ __forceinline__ int gu_nat(int c, int F) {   // interleaved column -> natural row
+  const int b = c >> 7, r = c & 127;
+  return r < 64 ? (b << 6) + r : F + (b << 6) + r - 64;
+}
 struct SwiOut {
   bf16* h;
   int ldh;
@@ -411,7 +416,8 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
       if (km) {
         const int row = 16 * j + (l >> 2);
         const int c = (l & 3) ^ kh(row);
-        pbase[q] = (unsigned)(((long long)(r0 + row) * ld + 8 * c) * 2);
+        const int rr = (SWIGLU && !isA) ? gu_nat(r0 + row, N >> 1) : r0 + row;   // (rows < N: N % 128 == 0)
+        pbase[q] = (unsigned)(((long long)rr * ld + 8 * c) * 2);
       } else if (isA || BN == 256) {
         const int lin = j * 64 + l;
         const int row = lin >> 5;
@@ -541,8 +547,9 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int n = bcol0 + 64 * h + l;
+        const int nb = SWIGLU ? gu_nat(n, N >> 1) : n;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rbias, (__attribute__((address_space(3))) void*)(bias_lds + 256 * h),
-                                                 4, n < N ? (unsigned)(n * 4) : kOOB, 0, 0, 0);
+                                                 4, n < N ? (unsigned)(nb * 4) : kOOB, 0, 0, 0);
       }
     }
 
@@ -655,9 +662,10 @@ static int g_g4_bn = 0;
 extern "C" void dpfs_gemm4_bn(int v) { g_g4_bn = v; }
 extern "C" void dpfs_gemm4_group_m(int g) { g_g4_group_m = g > 0 ? g : 4; }
 
-// gate|up projection with SwiGLU in the epilogue (SwiOut): C[M, N] = A B^T + bias with B's
-// rows interleaved (ops.gemm_select.gu_perm), H[M, N / 2] = silu(gate) * up.  Returns false
-// (nothing launched) where the 256-wide FAST kernel does not apply.
+// gate|up projection with SwiGLU in the epilogue (SwiOut): C[M, N] = A perm(B)^T + perm(bias)
+// (B / bias in the natural [gate | up] layout, read interleaved: reference.gu_perm),
+// H[M, N / 2] = silu(gate) * up.  Returns false (nothing launched) where the 256-wide FAST
+// kernel does not apply.
 extern "C" bool dpfs_gemm4_nt_swiglu(const void* A, const void* B, void* C, const float* bias, void* H, int M, int N,
                                      int K, int lda, int ldb, int ldc, int ldh, unsigned a_bytes, unsigned b_bytes,
                                      hipStream_t s) {

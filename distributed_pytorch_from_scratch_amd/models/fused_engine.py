@@ -43,7 +43,6 @@ import torch.distributed as dist
 
 from ..ops import fp8 as F8
 from ..ops import gemm_select as GS
-from ..ops import reference as R
 from ..ops.dispatch import K, shadow
 from ..parallel import process_manager as pm
 from ..parallel import tp_comm
@@ -138,17 +137,10 @@ class _Layer:
 
 def _gate_up_weights(k, layers, W):
     """Per layer: whether its gate|up projection runs with SwiGLU in the GEMM epilogue
-    (GS.swiglu_epilogue) and the weight / bias it multiplies with -- rows interleaved in 64-row
-    blocks for the fused form (reference.gu_perm: one 6 MB copy per layer and step; the weight
-    gradient comes back in that order and is un-interleaved once per step)."""
+    (GS.swiglu_epilogue: the kernel reads the natural weight with its rows interleaved in
+    64-row blocks and the backward returns natural-layout gradients, so nothing is copied)."""
     for L in layers:
-        w = W(L.wgu)
-        L.swi = GS.swiglu_epilogue(k, w)
-        if L.swi:
-            L.wgu_p = R.gu_perm(w).contiguous()
-            L.bgu_p = R.gu_perm(L.bgu).contiguous() if L.bgu is not None else None
-        else:
-            L.wgu_p, L.bgu_p = w, L.bgu
+        L.swi = GS.swiglu_epilogue(k, W(L.wgu))
 
 
 def collect_params(model) -> List[Optional[torch.Tensor]]:
@@ -216,7 +208,7 @@ class DecoderTrainFn(torch.autograd.Function):
             for ci, s in enumerate(st):
                 _wait(s["h"])
                 x2, h2, r2 = k.add_rmsnorm_fwd(s["pend"], s["pend_bias"], s["x"], L.s2, L.eps2)
-                gu, sw = GS.gate_up(k, h2, L.wgu_p, L.bgu_p, L.swi)   # SwiGLU in the epilogue
+                gu, sw = GS.gate_up(k, h2, W(L.wgu), L.bgu, L.swi)   # SwiGLU in the epilogue
                 qout = GS.gemm_nt(k, sw, W(L.wd), None, out=_slot(ci, sw.size(0), d, dt))
                 s["layers"][-1].update(x2=x2, r2=r2, h2=h2, gu=gu, sw=sw)
                 s["x"] = x2
@@ -365,7 +357,7 @@ class DecoderTrainFn(torch.autograd.Function):
                 a = s["layers"][li]
                 _wait(a.pop("hh"))
                 a["x2"], a["h2"], a["r2"] = k.add_rmsnorm_fwd(a.pop("pout"), L.bo, a["x"], L.s2, L.eps2)
-                a["gu"], a["sw"] = GS.gate_up(k, a["h2"], L.wgu_p, L.bgu_p, L.swi)
+                a["gu"], a["sw"] = GS.gate_up(k, a["h2"], W(L.wgu), L.bgu, L.swi)
 
         # ---- layers, reversed
         for li in range(nL - 1, -1, -1):
@@ -385,7 +377,7 @@ class DecoderTrainFn(torch.autograd.Function):
                 wd_p.append((gq, a["sw"]))
                 dbgu = ds.new_empty(a["gu"].size(1), dtype=torch.float32) if L.bgu is not None else None
                 dgu = k.swiglu_bwd(ds, a["gu"], dbgu, L.swi)   # + gate|up bias grad in the same pass
-                dh2 = GS.gemm_nn(k, dgu, L.wgu_p, out=_slot(ci, dgu.size(0), d, dt))
+                dh2 = GS.gemm_nn(k, dgu, W(L.wgu), out=_slot(ci, dgu.size(0), d, dt))
                 s["bh"], s["dpend"] = _ar(dh2), dh2
                 wgu_p.append((dgu, a["h2"]))
                 if dbgu is not None:
@@ -393,8 +385,6 @@ class DecoderTrainFn(torch.autograd.Function):
                 del a["sw"], a["gu"]
             tn_chunks(G, "wd", wd_p)        # under the chunks' all-reduces
             tn_chunks(G, "wgu", wgu_p)
-            if L.swi:                       # interleaved rows (fused SwiGLU epilogue) -> natural
-                G["wgu"] = R.gu_unperm(G["wgu"])
             if li + 1 < nL:
                 dp_reduce(gl[li + 1])           # layer li+1 is complete (its norm1 grad just landed)
             # b1: wait, norm2 bwd, Wo / attention / QKV grads -> AR(dh)

@@ -35,7 +35,6 @@ import torch.distributed as dist
 
 from ..ops import fp8 as F8
 from ..ops import gemm_select as GS
-from ..ops import reference as R
 from ..ops.dispatch import K, shadow
 from ..parallel import process_manager as pm
 from ..parallel import tp_comm
@@ -124,7 +123,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
             for ci, s in enumerate(st):    # P4: gate|up, SwiGLU, down -> reduce-scatter
                 _wait(s["h"])
                 a = s["layers"][-1]
-                gu, sw = GS.gate_up(k, a["h2"], L.wgu_p, L.bgu_p, L.swi)   # SwiGLU in the epilogue
+                gu, sw = GS.gate_up(k, a["h2"], W(L.wgu), L.bgu, L.swi)   # SwiGLU in the epilogue
                 qout = GS.gemm_nt(k, sw, W(L.wd), None, out=_slot(ci, sw.size(0), d, dt))
                 a.update(gu=gu, sw=sw)
                 (s["pend"], s["h"]), s["pend_bias"] = _rs(qout, n), L.bd
@@ -267,7 +266,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
             for s in st:
                 a = s["layers"][li]
                 _wait(a.pop("hh"))
-                a["gu"], a["sw"] = GS.gate_up(k, a["h2"], L.wgu_p, L.bgu_p, L.swi)
+                a["gu"], a["sw"] = GS.gate_up(k, a["h2"], W(L.wgu), L.bgu, L.swi)
 
         for li in range(nL - 1, -1, -1):
             L, G = layers[li], gl[li]
@@ -283,15 +282,13 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 wd_p.append((gq, a["sw"]))
                 dbgu = ds.new_empty(a["gu"].size(1), dtype=torch.float32) if L.bgu is not None else None
                 dgu = k.swiglu_bwd(ds, a["gu"], dbgu, L.swi)
-                s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dgu, L.wgu_p, out=_slot(ci, dgu.size(0), d, dt)), n)
+                s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dgu, W(L.wgu), out=_slot(ci, dgu.size(0), d, dt)), n)
                 wgu_p.append((dgu, a["h2"]))
                 if dbgu is not None:
                     G["bgu"] = _addg(G.get("bgu"), dbgu)
                 del a["sw"], a["gu"], a["h2"], s["gfull"]
             tn_chunks(G, "wd", wd_p)       # under the chunks' reduce-scatters
             tn_chunks(G, "wgu", wgu_p)
-            if L.swi:                       # interleaved rows (fused SwiGLU epilogue) -> natural
-                G["wgu"] = R.gu_unperm(G["wgu"])
             for s in st:    # B3: norm2 backward (+ residual grad) on my rows -> all-gather
                 _wait(s["h"])
                 a = s["layers"][li]

@@ -218,18 +218,21 @@ def swiglu_epilogue(k, w: torch.Tensor) -> bool:
     return mode() in ("auto", "ours") and F8.lookup(w) is None and hasattr(k, "gemm_nt_swiglu")
 
 
-def gate_up(k, x: torch.Tensor, w_p: torch.Tensor, b_p, perm: bool):
-    """(gu, h = silu(gate) * up) of the gate|up projection.  ``perm``: ``w_p`` / ``b_p`` are
-    interleaved (reference.gu_perm) and the GEMM writes h from its epilogue (gemm_nt_swiglu;
-    gu comes out interleaved too); where the fused kernel declines the shape, the plain GEMM
-    and the interleaved SwiGLU pass give the same tensors."""
+def gate_up(k, x: torch.Tensor, w: torch.Tensor, b, perm: bool):
+    """(gu, h = silu(gate) * up) of the gate|up projection (w / b natural [gate | up]).
+    ``perm``: the GEMM reads the weight rows interleaved in 64-row blocks (reference.gu_perm)
+    and writes h from its epilogue (gemm_nt_swiglu); gu comes out interleaved and the backward
+    reads it with ``swiglu_bwd(..., perm=True)``, which returns the natural-layout gradient.
+    Where the fused kernel declines the shape, an interleaved copy of the weight, the plain
+    GEMM and the interleaved SwiGLU pass give the same tensors."""
     if perm:
-        r = k.gemm_nt_swiglu(x, w_p, b_p)
+        r = k.gemm_nt_swiglu(x, w, b)
         if r:
             return r[0], r[1]
-        gu = gemm_nt(k, x, w_p, b_p)
+        gu = gemm_nt(k, x, reference.gu_perm(w).contiguous(),
+                     reference.gu_perm(b).contiguous() if b is not None else None)
         return gu, k.swiglu_fwd(gu, True)
-    gu = gemm_nt(k, x, w_p, b_p)
+    gu = gemm_nt(k, x, w, b)
     return gu, k.swiglu_fwd(gu)
 
 

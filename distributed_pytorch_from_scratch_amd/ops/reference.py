@@ -329,16 +329,17 @@ def swiglu_fwd(gu: torch.Tensor, perm: bool = False) -> torch.Tensor:
 
 
 def gemm_nt_swiglu(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None):
-    """Gate|up projection with the SwiGLU of the fused GPU epilogue: b's rows (and the bias)
-    interleaved by gu_perm -> [gu (interleaved, a.dtype), h = silu(gate) * up (a.dtype)]."""
-    gu = gemm_nt(a, b, bias)
+    """Gate|up projection with the SwiGLU of the fused GPU epilogue: b / bias in the natural
+    [gate | up] layout, multiplied with the rows interleaved by gu_perm -> [gu (interleaved,
+    a.dtype), h = silu(gate) * up (a.dtype)]."""
+    gu = gemm_nt(a, gu_perm(b), gu_perm(bias) if bias is not None else None)
     return [gu, swiglu_fwd(gu, True)]
 
 
 def swiglu_bwd(dh: torch.Tensor, gu: torch.Tensor, dbias: Optional[torch.Tensor] = None,
                perm: bool = False) -> torch.Tensor:
-    """d gate|up (in gu's layout); with ``dbias`` (fp32 [2F]) also writes the bias gradient
-    (column sums, natural [gate | up] order)."""
+    """d gate|up in the natural [gate | up] layout (``perm``: gu is read interleaved); with
+    ``dbias`` (fp32 [2F]) also writes the bias gradient (column sums)."""
     g, u = _gate_up(gu, perm)
     dhf = dh.float()
     sig = torch.sigmoid(g)
@@ -348,8 +349,6 @@ def swiglu_bwd(dh: torch.Tensor, gu: torch.Tensor, dbias: Optional[torch.Tensor]
     d = torch.cat([dg, du], dim=-1)
     if dbias is not None:
         dbias.copy_(d.sum(0))
-    if perm:
-        d = gu_perm(d, d.dim() - 1)
     return d.to(gu.dtype)
 
 
