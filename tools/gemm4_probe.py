@@ -66,6 +66,8 @@ def main():
     ap.add_argument("--bias", action="store_true", help="NT with an fp32 bias (the projections that carry one)")
     ap.add_argument("--bn", type=int, nargs="*", default=[],
                     help="extra arms: the last --scheds variant with the v4 tile width forced (256 / 192)")
+    ap.add_argument("--splits", type=int, nargs="*", default=[],
+                    help="extra arms (TN): the last --scheds variant with the K-split count forced (gemm_force)")
     ap.add_argument("--group-m", type=int, nargs="*", default=[],
                     help="extra arms: the last --scheds variant with this item-order group size")
     ap.add_argument("--diag", action="store_true",
@@ -120,7 +122,7 @@ def main():
                       f"-> per tile wait {v[:, 0].mean() / per:.0f} body {v[:, 1].mean() / per:.0f} "
                       f"epi {v[:, 2].mean() / per:.0f}; shares wait {(v[:, 0] / tot).mean():.3f} "
                       f"epi {(v[:, 2] / tot).mean():.3f}", flush=True)
-            arms = [f"v4s{sc}" for sc in a.scheds] + [f"gm{g}" for g in a.group_m] + [f"bn{b}" for b in a.bn] + \
+            arms = [f"v4s{sc}" for sc in a.scheds] + [f"gm{g}" for g in a.group_m] + [f"bn{b}" for b in a.bn] + [f"sp{x}" for x in a.splits] + \
                 [f"abl{x}" for x in a.ablate] + ["v3"] + \
                 ([] if a.no_blas else ["blas"])
             ts = {k: [] for k in arms}
@@ -130,6 +132,12 @@ def main():
                         C.gemm_v4_mask(7)
                         C.gemm4_sched(int(k[3:]))
                         ts[k].append(timed(lambda: ours(C), a.iters))
+                    elif k.startswith("sp"):
+                        C.gemm_v4_mask(7)
+                        C.gemm4_sched(a.scheds[-1])
+                        C.gemm_force(-1, int(k[2:]))
+                        ts[k].append(timed(lambda: ours(C), a.iters))
+                        C.gemm_force(-1, 0)
                     elif k.startswith("bn"):
                         C.gemm_v4_mask(7)
                         C.gemm4_sched(a.scheds[-1])
