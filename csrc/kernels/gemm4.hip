@@ -441,24 +441,44 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
     return (q < 4 || BN == 256) ? (j * 64 + l) >> 5 : (j * 64 + l) / (BN / 8);
   };
   rebase();
-  // FAST: descriptors of the producer's current stage (base advanced to its first k)
+  // FAST: descriptors of the producer's current stage: the item's stage-0 base / record count
+  // and per-stage byte stride are set once per item (item_rsrc), a stage adds p_t strides.
   __amdgpu_buffer_rsrc_t sra = ra, srb = rb;
-  auto stage_rsrc = [&]() {
+  unsigned long long ia = 0, ib = 0;   // (integers: pointer-typed captures stay in scratch)
+  unsigned na0 = 0, nb0 = 0, sta = 0, stb = 0;
+  int nlive = 0;   // stages of the item with k in range (an empty trailing split has none)
+  auto item_rsrc = [&]() {
     if constexpr (FAST) {
       const bool s2 = pi.sel != 0;
-      const int k0 = pi.kb + 32 * p_t;
-      const bool live = p_it < total && k0 < pi.ke;   // (an empty trailing split reads zeros)
-      const long long adv_a = AK ? (long long)k0 * 2 : (long long)k0 * (s2 ? lda2 : lda) * 2;
-      const long long adv_b = BKM ? (long long)k0 * 2 : (long long)k0 * (s2 ? ldb2 : ldb) * 2;
-      const char* pa = reinterpret_cast<const char*>(s2 ? dual.A2 : A) + adv_a;
-      const char* pb = reinterpret_cast<const char*>(s2 ? dual.B2 : B) + adv_b;
-      const unsigned na = live ? (s2 ? dual.a2_bytes : a_bytes) - (unsigned)adv_a : 0u;
-      const unsigned nb = live ? (s2 ? dual.b2_bytes : b_bytes) - (unsigned)adv_b : 0u;
-      sra = __builtin_amdgcn_make_buffer_rsrc((void*)pa, (short)0, (int)na, 0x00020000);
-      srb = __builtin_amdgcn_make_buffer_rsrc((void*)pb, (short)0, (int)nb, 0x00020000);
+      const int la = s2 ? lda2 : lda, lb = s2 ? ldb2 : ldb;
+      const long long adv_a = AK ? (long long)pi.kb * 2 : (long long)pi.kb * la * 2;
+      const long long adv_b = BKM ? (long long)pi.kb * 2 : (long long)pi.kb * lb * 2;
+      ia = reinterpret_cast<unsigned long long>(s2 ? dual.A2 : A) + adv_a;
+      ib = reinterpret_cast<unsigned long long>(s2 ? dual.B2 : B) + adv_b;
+      na0 = (s2 ? dual.a2_bytes : a_bytes) - (unsigned)adv_a;
+      nb0 = (s2 ? dual.b2_bytes : b_bytes) - (unsigned)adv_b;
+      sta = AK ? 64u : 64u * (unsigned)la;
+      stb = BKM ? 64u : 64u * (unsigned)lb;
+      nlive = (pi.ke - pi.kb + 31) / 32;
     }
   };
-  stage_rsrc();
+  item_rsrc();
+  // (one operand per call: the step places them in the shadow of its first MFMAs, see `step`)
+  // (one operand each: the step places them in the shadow of its first two MFMAs)
+  auto stage_rsrc_a = [&]() {
+    if constexpr (FAST) {
+      const unsigned off = (unsigned)p_t * sta;
+      const unsigned n = (p_t < nlive && p_it < total) ? na0 - off : 0u;
+      sra = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ia + off), (short)0, (int)n, 0x00020000);
+    }
+  };
+  auto stage_rsrc_b = [&]() {
+    if constexpr (FAST) {
+      const unsigned off = (unsigned)p_t * stb;
+      const unsigned n = (p_t < nlive && p_it < total) ? nb0 - off : 0u;
+      srb = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ib + off), (short)0, (int)n, 0x00020000);
+    }
+  };
   // DMA piece q (< 8) of the producer's current stage
   auto issue = [&](int q) {
     if constexpr (FAST) {
@@ -488,12 +508,14 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
         pi = decode<BN>(p_it, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
         p_nk = nsteps(pi);
         rebase();
+        item_rsrc();
       }
     }
-    stage_rsrc();
   };
 #pragma unroll
   for (int s0 = 0; s0 < 3; ++s0) {
+    stage_rsrc_a();
+    stage_rsrc_b();
 #pragma unroll
     for (int q = 0; q < NQ; ++q) issue(q);
     advance();
@@ -565,6 +587,9 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
         constexpr int j = decltype(J)::value;
         acc_mfma<q, j, ZR>(cur.b.get(j), cur.a.get(q));
         __builtin_amdgcn_sched_barrier(0);
+        // this step's stage descriptors (scalar work) in the shadow of the first MFMAs
+        if constexpr (q == 0 && j == 0) stage_rsrc_a();
+        if constexpr (q == 0 && j == 1) stage_rsrc_b();
         if constexpr (q < 4) {
           // read slots after MFMA 0 / 2 / 4 / 6 (NJ 8) or 0 / 2 / 3 / 5 (NJ 6)
           constexpr int r0 = 0, r1 = 2, r2 = NJ == 8 ? 4 : 3, r3 = NJ == 8 ? 6 : 5;
