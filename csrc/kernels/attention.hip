@@ -1589,23 +1589,42 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv3_k(
       const int q0 = qstart + t * BQ;
       if (t + 2 < nq) dma.issue(qbase, dobase, lsb, dlb, ldq, lddo, T, q0 + 2 * BQ, smem + nb * BUF);
       if (causal && q0 + BQ - 1 < kw0) continue;   // wave-uniform: every query of the tile < every key
-      // S = Q K^T, dP = dO V^T (rows = queries 32 qt + 8 (i>>2) + 4 hf + (i&3), lane = key)
+      // S = Q K^T, dP = dO V^T (rows = queries 32 qt + 8 (i>>2) + 4 hf + (i&3), lane = key).
+      // p = exp2(c2 S - lse log2 e) of query tile 0 is computed under tile 1's MFMAs (four
+      // elements after each pair), tile 1's after them; the row constants per register come
+      // from the stage (rows 32 qt + 8 g + 4 hf + 0..3 are 4 consecutive floats).
+      // dP starts from -delta (its accumulator's initial value), so dS = p dP' directly.
       f32x16 sc[2], dp[2];
+      f32x4 lsr[2][4];
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
+      for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          sc[qt][i] = 0.f;
-          dp[qt][i] = 0.f;
+        for (int g = 0; g < 4; ++g) {
+          lsr[qt][g] = *reinterpret_cast<const f32x4*>(ls + 32 * qt + 8 * g + 4 * hf);
+          const f32x4 dd = *reinterpret_cast<const f32x4*>(ds + 32 * qt + 8 * g + 4 * hf);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dp[qt][4 * g + j] = dd[j];
         }
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          sc[qt] = MFMA32(*reinterpret_cast<const bf16x8*>(lq + roff[ks] + 32 * qt * RB), kf[ks], sc[qt]);
-          dp[qt] = MFMA32(*reinterpret_cast<const bf16x8*>(ldo_ + roff[ks] + 32 * qt * RB), vf[ks], dp[qt]);
-        }
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[qt][i] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        sc[0] = MFMA32(*reinterpret_cast<const bf16x8*>(lq + roff[ks]), kf[ks], sc[0]);
+        dp[0] = MFMA32(*reinterpret_cast<const bf16x8*>(ldo_ + roff[ks]), vf[ks], dp[0]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        sc[1] = MFMA32(*reinterpret_cast<const bf16x8*>(lq + roff[ks] + 32 * RB), kf[ks], sc[1]);
+        dp[1] = MFMA32(*reinterpret_cast<const bf16x8*>(ldo_ + roff[ks] + 32 * RB), vf[ks], dp[1]);
+#pragma unroll
+        for (int i = 4 * ks; i < 4 * ks + 4; ++i)
+          sc[0][i] = __builtin_amdgcn_exp2f(fmaf(sc[0][i], c2, lsr[0][i >> 2][i & 3]));
+        __builtin_amdgcn_sched_barrier(0);
       }
       // dO^T fragments (A of dV^T: lane d = 32 dt + r32, queries 16 s + 4 hf + 0..3 / 8..11)
-      __builtin_amdgcn_sched_barrier(0);
       constexpr int NH = 2 * DTN * 4;
       s16x4 th[(NH + 15) / 16 * 16];
 #pragma unroll
@@ -1615,17 +1634,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv3_k(
           th[2 * (dt * 4 + s4)] = ds_tr16(ldo_ + toff[dt][0] + 16 * s4 * RB);
           th[2 * (dt * 4 + s4) + 1] = ds_tr16(ldo_ + toff[dt][1] + 16 * s4 * RB);
         }
-      // p = exp2(c2 S - lse log2 e), dS = p (dP - delta): the row constants per register come
-      // from the stage (rows 32 qt + 8 g + 4 hf + 0..3 are 4 consecutive floats)
+      // dS = p (dP - delta)
       bf16x8 pp[4], pd[4];
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        f32x4 lsr[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) lsr[g] = *reinterpret_cast<const f32x4*>(ls + 32 * qt + 8 * g + 4 * hf);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sc[qt][i] = __builtin_amdgcn_exp2f(fmaf(sc[qt][i], c2, lsr[i >> 2][i & 3]));
-      }
+      for (int i = 0; i < 16; ++i) sc[1][i] = __builtin_amdgcn_exp2f(fmaf(sc[1][i], c2, lsr[1][i >> 2][i & 3]));
       const bool need_mask = __builtin_amdgcn_readfirstlane(
           (int)((causal && kw0 + 31 > q0) || (q0 + BQ > T) || (kw0 + 32 > T)));
       if (need_mask) {
@@ -1642,10 +1654,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv3_k(
           }
       }
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        f32x4 dsr[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) dsr[g] = *reinterpret_cast<const f32x4*>(ds + 32 * qt + 8 * g + 4 * hf);
+      for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
         for (int s1 = 0; s1 < 2; ++s1)
 #pragma unroll
@@ -1653,9 +1662,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv3_k(
             const int i = 8 * s1 + j;
             const float pv = sc[qt][i];
             pp[2 * qt + s1][j] = (bf16)pv;
-            pd[2 * qt + s1][j] = (bf16)(pv * (dp[qt][i] + dsr[i >> 2][i & 3]));
+            pd[2 * qt + s1][j] = (bf16)(pv * dp[qt][i]);
           }
-      }
 #pragma unroll
       for (int w = 0; w < (NH + 15) / 16; ++w) tr_wait8(*reinterpret_cast<s16x4(*)[16]>(&th[16 * w]));
 #pragma unroll
@@ -2077,22 +2085,31 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq3_k(
       const int kv0 = t * BKV;
       if (t + 2 < nkv) dma.issue(kbase, vbase, ldk, ldv, T, kv0 + 2 * BKV, smem + nb * STAGE);
       if (causal && kv0 > wq0 + 31) continue;   // wave-uniform
+      // dP^T starts from -delta (the lane's query), so dS = p dP' directly; p of key half 0 is
+      // computed under half 1's MFMAs (four elements after each pair), half 1's after them.
       f32x16 sc[2], dp[2];
 #pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
+      for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           sc[kh][i] = 0.f;
-          dp[kh][i] = 0.f;
+          dp[kh][i] = ndel;
         }
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          sc[kh] = MFMA32(*reinterpret_cast<const bf16x8*>(lk + koff[kh][ks]), qf[ks], sc[kh]);
-          dp[kh] = MFMA32(*reinterpret_cast<const bf16x8*>(lv + koff[kh][ks]), df[ks], dp[kh]);
-        }
+      for (int ks = 0; ks < KS; ++ks) {
+        sc[0] = MFMA32(*reinterpret_cast<const bf16x8*>(lk + koff[0][ks]), qf[ks], sc[0]);
+        dp[0] = MFMA32(*reinterpret_cast<const bf16x8*>(lv + koff[0][ks]), df[ks], dp[0]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        sc[1] = MFMA32(*reinterpret_cast<const bf16x8*>(lk + koff[1][ks]), qf[ks], sc[1]);
+        dp[1] = MFMA32(*reinterpret_cast<const bf16x8*>(lv + koff[1][ks]), df[ks], dp[1]);
+#pragma unroll
+        for (int i = 4 * ks; i < 4 * ks + 4; ++i) sc[0][i] = __builtin_amdgcn_exp2f(fmaf(sc[0][i], c2, lc));
+        __builtin_amdgcn_sched_barrier(0);
       }
       // K^T fragments (A of dQ^T: lane d = 32 dt + r32, keys 16 s + 4 hf + 0..3 / 8..11)
-      __builtin_amdgcn_sched_barrier(0);
       constexpr int NH = 2 * DTN * 4;
       s16x4 th[(NH + 15) / 16 * 16];
 #pragma unroll
@@ -2106,9 +2123,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq3_k(
           th[2 * (dt * 4 + s4) + 1] = ds_tr16(lk + (row + 8) * RB + (swz_u<HD>(row + 8, ch) << 4) + bo);
         }
 #pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sc[kh][i] = __builtin_amdgcn_exp2f(fmaf(sc[kh][i], c2, lc));
+      for (int i = 0; i < 16; ++i) sc[1][i] = __builtin_amdgcn_exp2f(fmaf(sc[1][i], c2, lc));
       const bool need_mask = __builtin_amdgcn_readfirstlane(
           (int)((causal && kv0 + BKV - 1 > wq0) || (kv0 + BKV > T)));
       if (need_mask) {
@@ -2125,7 +2140,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq3_k(
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int kh = s4 >> 1, i = 8 * (s4 & 1) + j;
-          pd[s4][j] = (bf16)(sc[kh][i] * (dp[kh][i] + ndel));
+          pd[s4][j] = (bf16)(sc[kh][i] * dp[kh][i]);
         }
 #pragma unroll
       for (int w = 0; w < (NH + 15) / 16; ++w) tr_wait8(*reinterpret_cast<s16x4(*)[16]>(&th[16 * w]));
