@@ -855,16 +855,20 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
 #pragma unroll
           for (int d = 0; d < DTN; ++d) o[d] *= alpha;
         }
-        float ps[4] = {0.f, 0.f, 0.f, 0.f};
+        // row sum in packed pairs of adjacent registers (v_pk_add_f32 with no operand gathering)
+        typedef float f32x2v __attribute__((ext_vector_type(2)));
+        f32x2v ps[2] = {{0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const float e = __builtin_amdgcn_exp2f(fmaf(s[kh][i], c2, -m));
-            s[kh][i] = e;
-            ps[(kh * 16 + i) >> 3] += e;
+          for (int i = 0; i < 16; i += 2) {
+            const float e0 = __builtin_amdgcn_exp2f(fmaf(s[kh][i], c2, -m));
+            const float e1 = __builtin_amdgcn_exp2f(fmaf(s[kh][i + 1], c2, -m));
+            s[kh][i] = e0;
+            s[kh][i + 1] = e1;
+            ps[(i >> 1) & 1] += f32x2v{e0, e1};
           }
-        lsum += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+        lsum += (ps[0].x + ps[0].y) + (ps[1].x + ps[1].y);
         bf16x8 pk[4];
 #pragma unroll
         for (int k4 = 0; k4 < 4; ++k4)
