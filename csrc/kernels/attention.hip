@@ -603,6 +603,7 @@ struct KvDma3 {
   }
 };
 
+typedef float f32x2v __attribute__((ext_vector_type(2)));   // a register pair (v_pk_*_f32)
 #define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
 
 // max / sum of x over lanes l and l ^ 32 (the two lanes of one 32x32 C/D column).
@@ -856,7 +857,6 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
           for (int d = 0; d < DTN; ++d) o[d] *= alpha;
         }
         // row sum in packed pairs of adjacent registers (v_pk_add_f32 with no operand gathering)
-        typedef float f32x2v __attribute__((ext_vector_type(2)));
         f32x2v ps[2] = {{0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh)
@@ -1662,11 +1662,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv3_k(
 #pragma unroll
         for (int s1 = 0; s1 < 2; ++s1)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
+          for (int j = 0; j < 8; j += 2) {   // adjacent register pairs: one v_pk_mul_f32 each
             const int i = 8 * s1 + j;
-            const float pv = sc[qt][i];
-            pp[2 * qt + s1][j] = (bf16)pv;
-            pd[2 * qt + s1][j] = (bf16)(pv * dp[qt][i]);
+            const f32x2v pr = f32x2v{sc[qt][i], sc[qt][i + 1]} * f32x2v{dp[qt][i], dp[qt][i + 1]};
+            pp[2 * qt + s1][j] = (bf16)sc[qt][i];
+            pp[2 * qt + s1][j + 1] = (bf16)sc[qt][i + 1];
+            pd[2 * qt + s1][j] = (bf16)pr.x;
+            pd[2 * qt + s1][j + 1] = (bf16)pr.y;
           }
 #pragma unroll
       for (int w = 0; w < (NH + 15) / 16; ++w) tr_wait8(*reinterpret_cast<s16x4(*)[16]>(&th[16 * w]));
@@ -2142,9 +2144,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq3_k(
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < 8; j += 2) {   // adjacent register pairs: one v_pk_mul_f32 each
           const int kh = s4 >> 1, i = 8 * (s4 & 1) + j;
-          pd[s4][j] = (bf16)(sc[kh][i] * dp[kh][i]);
+          const f32x2v pr = f32x2v{sc[kh][i], sc[kh][i + 1]} * f32x2v{dp[kh][i], dp[kh][i + 1]};
+          pd[s4][j] = (bf16)pr.x;
+          pd[s4][j + 1] = (bf16)pr.y;
         }
 #pragma unroll
       for (int w = 0; w < (NH + 15) / 16; ++w) tr_wait8(*reinterpret_cast<s16x4(*)[16]>(&th[16 * w]));
