@@ -61,6 +61,11 @@ def parse():
     ap.add_argument("--recompute", action="store_true", help="activation recompute (layer inputs only)")
     ap.add_argument("--no-pure-tp", dest="pure_tp", action="store_false",
                     help="at N > 1 with a TP x DP headline layout, skip the extra pure-TP (tp = N) measurement")
+    ap.add_argument("--pure-tp-budget-s", type=float, default=float(os.environ.get("DPFS_PURE_TP_BUDGET_S", "180")),
+                    help="wall-clock budget of the extra pure-TP measurement; past it every rank prints / "
+                         "exits with the headline and tp_pure = {error: timeout}")
+    ap.add_argument("--pg-timeout-s", type=float, default=240.0,
+                    help="process-group (RCCL watchdog) timeout, well under the driver's lease")
     ap.add_argument("--fp8", action="store_true",
                     help="fp8 (e4m3 / e5m2) forward and data-gradient GEMMs (ops/fp8.py); NOT the bf16 headline")
     return ap.parse_args()
@@ -90,7 +95,13 @@ def measure(a, tp: int, world: int, dev, first: bool):
     from distributed_pytorch_from_scratch_amd.utils.dist import init_dist_env, set_seed
     from distributed_pytorch_from_scratch_amd.parallel import process_manager as pm, tp_comm
 
-    p = init_dist_env(rank=None, tp_size=tp, dp_size=world // tp) if first else pm.init_pgm(tp, world // tp)
+    p = init_dist_env(rank=None, tp_size=tp, dp_size=world // tp, timeout_s=a.pg_timeout_s) if first \
+        else pm.init_pgm(tp, world // tp)
+    inject = os.environ.get("DPFS_BENCH_INJECT", "")    # test hook: "raise:<rank>" | "hang:<rank>"
+    if not first and inject and int(inject.split(":")[1]) == dist.get_rank():
+        if inject.startswith("raise"):
+            raise RuntimeError("injected failure in the pure-TP layout")
+        time.sleep(3600)
     tp_comm.set_fixed_shapes(True)   # synthetic fixed-shape batches on every rank
 
     # SP is a property of the step, not of the weights: build with the SP attributes and
@@ -231,18 +242,91 @@ def main():
     os.environ.setdefault("MASTER_PORT", "29511")
     tp = resolve_tp(a.tp, a.model, world)
     if torch.cuda.is_available():
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        lr = int(os.environ.get("LOCAL_RANK", "0"))
+        # DPFS_BACKEND=gloo: the multi-rank rehearsal with several ranks on one GPU
+        torch.cuda.set_device(lr % torch.cuda.device_count() if os.environ.get("DPFS_BACKEND") == "gloo" else lr)
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
 
     head = measure(a, tp, world, dev, first=True)
     rank = dist.get_rank()
+    out = report(a, head, [head], world, dev)
     # The reference trains with tp_size == world_size (process_manager.py:13-15, recipe.sh TP 1 /
     # 2 / 4): at N > 1 the pure-TP layout is measured as well and reported next to the headline
     # layout (same contract: W warmup + K timed steps, max over ranks), each with its label.
-    layouts = [head]
+    # That layout must never cost the headline: it runs after the headline's numbers are final,
+    # any exception becomes tp_pure = {"error": ...}, and a per-rank timer bounds it (a hung
+    # collective: rank 0 prints the headline line with tp_pure = {"error": "timeout"} and every
+    # rank exits 0 before the process-group watchdog or the driver's lease fires).
     if world > 1 and tp != world and a.pure_tp:
-        layouts.append(measure(a, world, world, dev, first=False))
+        import threading
+        lock = threading.Lock()
+        done = []
 
+        def emit(o):
+            with lock:
+                if not done:
+                    done.append(1)
+                    if rank == 0:
+                        print_line(json.dumps(o))
+
+        def expire():
+            o = dict(out)
+            o["tp_pure"] = {"parallelism": f"tp{world}", "error": f"timeout after {a.pure_tp_budget_s:.0f}s"}
+            emit(o)
+            sys.stdout.flush()
+            os._exit(0)
+
+        timer = threading.Timer(a.pure_tp_budget_s, expire)
+        timer.daemon = True
+        timer.start()
+        err = None
+        try:
+            from distributed_pytorch_from_scratch_amd.parallel import tp_comm
+            tp_comm.reset()            # the headline layout's xGMI buffers / communicators
+            pure = measure(a, world, world, dev, first=False)
+            out = report(a, head, [head, pure], world, dev)
+        except Exception as e:         # noqa: BLE001 - reported, never fatal for the headline
+            err = f"{type(e).__name__}: {e}"[:500]
+            out = dict(out)
+            out["tp_pure"] = {"parallelism": f"tp{world}", "error": err}
+        timer.cancel()
+        emit(out)
+        # No teardown collective after the extra layout: a rank that failed alone has left its
+        # peers inside a collective (their timers end them), and every rank that got here is
+        # past its last collective.
+        if rank == 0:
+            show_gemm_choices()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+    elif rank == 0:
+        print_line(json.dumps(out))
+    if rank == 0:
+        show_gemm_choices()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def print_line(text: str):
+    """One write(2) of the whole line: other ranks' (and libraries') output to the same pipe
+    cannot land inside the driver's JSON line."""
+    sys.stdout.flush()
+    os.write(sys.stdout.fileno(), (text + "\n").encode())
+
+
+def show_gemm_choices():
+    if os.environ.get("DPFS_SHOW_GEMM") == "1":     # per-shape ours/hipBLASLt choices (ms)
+        from distributed_pytorch_from_scratch_amd.ops import gemm_select
+        for key, v in sorted(gemm_select.choices(with_times=True).items(), key=str):
+            print(f"[gemm] {key} -> {v}", file=sys.stderr, flush=True)
+    if os.environ.get("DPFS_BENCH_VERBOSE"):
+        from distributed_pytorch_from_scratch_amd.ops import gemm_select
+        for key, c in sorted(gemm_select.choices().items(), key=str):
+            print(f"gemm {key}: {c}", file=sys.stderr, flush=True)
+
+
+def report(a, head, layouts, world, dev):
+    """The driver's JSON line (headline = ``head``; ``layouts`` adds the labelled extras)."""
     args, T, gb = head["args"], head["T"], head["gb"]
     value, elapsed = head["value"], head["elapsed"]
     # The reference-formulation baseline was measured on GPT-2 small only; other shapes get null.
@@ -290,18 +374,7 @@ def main():
                           for L in layouts]
         pure = [L for L in out["layouts"] if L["parallelism"].split("+")[0] == f"tp{world}"]
         out["tp_pure"] = pure[0] if pure else None
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-        if os.environ.get("DPFS_SHOW_GEMM") == "1":     # per-shape ours/hipBLASLt choices (ms)
-            from distributed_pytorch_from_scratch_amd.ops import gemm_select
-            for key, v in sorted(gemm_select.choices(with_times=True).items(), key=str):
-                print(f"[gemm] {key} -> {v}", file=sys.stderr, flush=True)
-        if os.environ.get("DPFS_BENCH_VERBOSE"):
-            from distributed_pytorch_from_scratch_amd.ops import gemm_select
-            for key, c in sorted(gemm_select.choices().items(), key=str):
-                print(f"gemm {key}: {c}", file=sys.stderr, flush=True)
-    dist.barrier()
-    dist.destroy_process_group()
+    return out
 
 
 if __name__ == "__main__":

@@ -161,7 +161,8 @@ __global__ __launch_bounds__(kThreads) void xgmi_coll_k(Peers P, int op, int ran
   // ---- phase 0: copy-in of what the peers will read.  Staged (op & 8): the producer GEMM
   // wrote x straight into this rank's slot (x == slot base), so nothing is copied; its plain
   // stores may still sit dirty in the XCD L2s, hence a system-scope release (L2 write-back)
-  // by one lane of every workgroup before the start barrier (grids >= 8 reach every XCD).
+  // by one lane of every workgroup before the start barrier (dpfs_xgmi_run launches at least
+  // 8 workgroups, which the dispatcher deals one to each XCD).
   const bool staged = (op & 8) != 0;
   op &= 7;
   if (staged) {
@@ -405,6 +406,12 @@ extern "C" int dpfs_xgmi_run(void* h, int op, int dtype, const void* x, void* ou
   const long long nvec = part / N;
   int grid = (int)((nvec + kThreads - 1) / kThreads);
   if (grid > c->blocks) grid = c->blocks;
+  // At least one workgroup per XCD (workgroups are dealt round-robin over the 8 XCDs): the
+  // staged path's system-scope release writes back the L2 of the XCD it runs on only, and the
+  // producer GEMM's dirty lines may sit in any XCD's L2.  Applied to every call (not only the
+  // staged ones) so the grid is a function of the size alone, identical on every rank.
+  const int min_grid = c->blocks < 8 ? c->blocks : 8;
+  if (grid < min_grid) grid = min_grid;
   if (grid < 1) grid = 1;
   c->epoch += 1;
   if (c->epoch == 0) c->epoch = 1;

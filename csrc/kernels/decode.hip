@@ -190,7 +190,7 @@ __global__ __launch_bounds__(256) void kv_append_k(const bf16* __restrict__ ksrc
 // streamed once with all of a wave's loads issued ahead of its MFMAs; A (a few KB) stays in
 // L2.  SW: A = silu(g) * u of a packed [M, 2K] gate|up input -- the SwiGLU fused into the down
 // projection's operand load (same fp32 formula and bf16 rounding as swiglu_fwd_k).
-__device__ __forceinline__ float silu_dec(float g) { return g / (1.f + __expf(-g)); }
+__device__ __forceinline__ float silu_dec(float g) { return g * __builtin_amdgcn_rcpf(1.f + __expf(-g)); }   // = silu_f
 
 template <int KS, bool SW>
 __global__ __launch_bounds__(64 * KS) void gemv16_k(const bf16* __restrict__ A, long long lda,

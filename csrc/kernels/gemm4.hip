@@ -215,7 +215,7 @@ __device__ __forceinline__ int nsteps(const Item& it) {
 // template flag, no per-tile branch or LDS wait), store offsets are 32-bit selects (the C span
 // fits the descriptor, so row * ldc cannot overflow), and the RoPE rows' positions and
 // cos / sin values are loaded one 16-row block ahead of their use.
-__device__ __forceinline__ float silu_ref(float g) { return g / (1.f + __expf(-g)); }
+__device__ __forceinline__ float silu_ref(float g) { return g * __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
 
 template <int OUT, int BN, int ROPE, bool HAS_BIAS, bool SWIGLU = false>
 __device__ __forceinline__ void epilogue(const char* bias_lds, const Item& ci, void* C, const Rope& rope, int M,

@@ -22,6 +22,12 @@
 
 Only the TP group's activation / activation-gradient collectives go through here; DP gradient
 buckets, the CE statistics gather and init broadcasts stay on ProcessGroupNCCL.
+
+Rehearsal hook: ``DPFS_TP_COMM_AUTO_ANY_BACKEND=1`` lets ``auto`` run its whole decision
+(validation, timing, grid choice, WORLD reductions, relay candidate) on a non-``nccl`` backend,
+i.e. gloo with several ranks on one GPU (xGMI + relay candidates) or on the CPU (relay
+candidate only).  The "rccl" column is then the gloo process group.  Tests use it to pin that
+every rank reaches the same decisions before the first real multi-GPU run.
 """
 from __future__ import annotations
 
@@ -48,13 +54,22 @@ def mode() -> str:
     return m
 
 
-def _time_ms(fn, reps: int = 5) -> float:
+def _auto_any_backend() -> bool:
+    return os.environ.get("DPFS_TP_COMM_AUTO_ANY_BACKEND", "0") == "1"
+
+
+def _sync(dev_is_cuda: bool):
+    if dev_is_cuda:
+        torch.cuda.synchronize()
+
+
+def _time_ms(fn, cuda: bool = True, reps: int = 5) -> float:
     fn()
-    torch.cuda.synchronize()
+    _sync(cuda)
     t0 = time.perf_counter()
     for _ in range(reps):
         fn()
-    torch.cuda.synchronize()
+    _sync(cuda)
     return 1000 * (time.perf_counter() - t0) / reps
 
 
@@ -79,9 +94,9 @@ def _run_op(comm, op: str, x, part, gathered, timeout_s=None):
         if op == "all_reduce":
             dist.all_reduce(x, group=g)
         elif op == "reduce_scatter":
-            dist.reduce_scatter_tensor(part, x, group=g)
+            _pg_reduce_scatter(part, x, g)
         else:
-            dist.all_gather_into_tensor(gathered, part, group=g)
+            _pg_all_gather(gathered, part, g)
         return
     kw = {} if timeout_s is None else {"timeout_s": timeout_s}
     if op == "all_reduce":
@@ -92,9 +107,35 @@ def _run_op(comm, op: str, x, part, gathered, timeout_s=None):
         comm.all_gather(gathered, part, async_op=False, **kw)
 
 
+def _gloo_cuda(t: torch.Tensor, g) -> bool:
+    return t.is_cuda and dist.get_backend(g) == "gloo"
+
+
+def _pg_reduce_scatter(out: torch.Tensor, inp: torch.Tensor, g, async_op: bool = False):
+    """``dist.reduce_scatter_tensor`` on the process group; gloo with device tensors (the
+    one-GPU multi-rank rehearsal) goes through an all-reduce of a copy instead."""
+    if _gloo_cuda(inp, g):
+        tmp = inp.contiguous().clone()
+        dist.all_reduce(tmp, group=g)
+        out.view(-1).copy_(tmp.view(dist.get_world_size(g), -1)[dist.get_rank(g)])
+        return None
+    return dist.reduce_scatter_tensor(out, inp, group=g, async_op=async_op)
+
+
+def _pg_all_gather(out: torch.Tensor, inp: torch.Tensor, g, async_op: bool = False):
+    if _gloo_cuda(inp, g):
+        W, r = dist.get_world_size(g), dist.get_rank(g)
+        pad = torch.zeros(W, inp.numel(), dtype=inp.dtype, device=inp.device)
+        pad[r].copy_(inp.reshape(-1))
+        dist.all_reduce(pad, group=g)
+        out.view(-1).copy_(pad.view(-1))
+        return None
+    return dist.all_gather_into_tensor(out, inp, group=g, async_op=async_op)
+
+
 def _build(kind: str, g, forced: bool):
     """Communicator of ``kind`` on every rank of g, or None on every rank if any rank failed."""
-    ok = torch.ones(1, device="cuda")
+    ok = torch.ones(1, device="cuda" if torch.cuda.is_available() else "cpu")
     comm, why = None, ""
     try:
         if kind == "xgmi":
@@ -134,11 +175,14 @@ def _relay_possible(p) -> bool:
 def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
     m = mode()
     backend = dist.get_backend(p.tp_group)
-    if m == "rccl" or (m != "relay" and not t.is_cuda) or (m == "auto" and backend != "nccl"):
+    any_be = m == "auto" and _auto_any_backend()
+    if m == "rccl" or (m == "auto" and backend != "nccl" and not any_be):
+        return None
+    if not t.is_cuda and not (m == "relay" or any_be):
         return None
     g = p.tp_group
     W, r = p.tp_size, p.tp_rank
-    kinds = [m] if m != "auto" else ["xgmi"]
+    kinds = [m] if m != "auto" else (["xgmi"] if t.is_cuda else [])
     relay_cand = (m == "relay" or (m == "auto" and _fixed_shapes)) and _relay_possible(p)
     if m == "relay" and not _relay_possible(p):
         raise RuntimeError("DPFS_TP_COMM=relay needs TP = 2 and at least two TP pairs")
@@ -147,7 +191,7 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
     if relay_cand:
         # every decision input below is reduced over the WORLD, so every pair must hold the
         # same candidate set: drop xGMI everywhere unless every pair built it
-        have = torch.tensor([1.0 if "xgmi" in comms else 0.0], device=t.device)
+        have = torch.tensor([1.0 if "xgmi" in comms else 0.0], device=t.device if t.is_cuda and backend == "nccl" else "cpu")
         dist.all_reduce(have, op=dist.ReduceOp.MIN)
         if have.item() == 0.0:
             comms.pop("xgmi", None)
@@ -165,7 +209,7 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
         n = min(n, comms["xgmi"]._max_elems(t))
     n = max(8 * W, n - n % (8 * W))
     if relay_cand:   # relayed exchanges pair every rank with every other: one size for the WORLD
-        nt = torch.tensor([n], dtype=torch.int64, device=t.device)
+        nt = torch.tensor([n], dtype=torch.int64, device=t.device if backend == "nccl" else "cpu")
         dist.all_reduce(nt, op=dist.ReduceOp.MIN)
         n = int(nt.item())
     gen = torch.Generator(device=t.device).manual_seed(4321 + r)
@@ -187,8 +231,7 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
         _run_op(c, "all_reduce", y, None, None, to)
         _run_op(c, "reduce_scatter", x, part, None, to)
         _run_op(c, "all_gather", None, mine, gathered, to)
-        if t.is_cuda:
-            torch.cuda.synchronize()
+        _sync(t.is_cuda)
         e = [(y.float() - ref).abs().max().item(), (part.float() - ref.view(W, -1)[r]).abs().max().item(),
              (gathered.float() - pad.view(-1)).abs().max().item()]
         timed_out = k == "xgmi" and c.error() != 0
@@ -205,7 +248,7 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
     G = len(_GRIDS)
     cols = ["rccl"] + [k for k in kl if k != "xgmi"] + ([f"xgmi/{nb}" for nb in _GRIDS] if "xgmi" in comms else [])
     times = torch.zeros(3, len(cols), device=t.device)
-    timed = m == "auto" and backend == "nccl"
+    timed = m == "auto" and (backend == "nccl" or any_be)
     if timed:
         a_, ap, ag = t.detach().reshape(-1)[:n].clone(), torch.empty_like(mine), torch.empty_like(x)
         for i, op in enumerate(_OPS):
@@ -219,7 +262,7 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
                     c = comms[kind]
                     if kind == "xgmi":
                         c.set_blocks(int(col.split("/")[1]))
-                times[i, j] = _time_ms(lambda c=c, op=op: _run_op(c, op, a_, ap, ag))
+                times[i, j] = _time_ms(lambda c=c, op=op: _run_op(c, op, a_, ap, ag), t.is_cuda)
         if "xgmi" in comms:
             comms["xgmi"].check()
     dist.all_reduce(times, op=dist.ReduceOp.MAX, group=red_group)
@@ -251,6 +294,8 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
     if p.global_rank == 0 and os.environ.get("DPFS_QUIET", "0") != "1":
         print(f"[dpfs] TP collectives: {info}", file=sys.stderr, flush=True)
     if all(u == "rccl" for u in use.values()):
+        if "xgmi" in comms:      # same decision on every rank of g: release the IPC buffers
+            comms["xgmi"].close()
         return None
     ch = _Choice(comms.get("xgmi"), comms.get("native"), use)
     ch.relay = comms.get("relay")
@@ -258,13 +303,43 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
 
 
 def _comm(t: torch.Tensor, p, op: str):
-    if t.dtype not in (torch.bfloat16, torch.float32) or (not t.is_cuda and mode() != "relay"):
+    if t.dtype not in (torch.bfloat16, torch.float32):
+        return None
+    if not t.is_cuda and not (mode() == "relay" or (mode() == "auto" and _auto_any_backend())):
         return None
     key = id(p.tp_group)
     if key not in _decisions:
         _decisions[key] = _decide(t, p)
     ch = _decisions[key]
     return None if ch is None else ch.comm(op)
+
+
+def decision() -> Optional[dict]:
+    """This rank's transport per op and the xGMI grid per op (None before the first TP
+    collective or off TP): what every rank of a group must agree on."""
+    p = pm.pgm
+    if p is None or id(p.tp_group) not in _decisions:
+        return None
+    inf = _info.get(id(p.tp_group))
+    if inf is None:              # no candidate transport was built: the process group
+        return {"use": {op: "rccl" for op in _OPS}, "op_blocks": None}
+    blocks = {op: inf[op].get("xgmi_blocks") for op in _OPS}
+    return {"use": {op: inf[op]["transport"] for op in _OPS},
+            "op_blocks": blocks if any(v is not None for v in blocks.values()) else None}
+
+
+def reset():
+    """Release every communicator built by the decisions (xGMI IPC buffers, the native RCCL
+    communicator) and forget them, e.g. between two layouts measured in one process.
+    Collective over each TP group that has decided (every rank must call it)."""
+    for key, ch in list(_decisions.items()):
+        if ch is not None:
+            if ch.xgmi is not None:
+                ch.xgmi.close()
+            if ch.native is not None and hasattr(ch.native, "close"):
+                ch.native.close()
+        _decisions.pop(key, None)
+        _info.pop(key, None)
 
 
 def info() -> Optional[dict]:
@@ -298,7 +373,7 @@ def reduce_scatter(out: torch.Tensor, inp: torch.Tensor, async_op: bool = True):
         return None
     c = _comm(inp, p, "reduce_scatter")
     if c is None or not _fits(c, inp, 8 * p.tp_size):
-        return dist.reduce_scatter_tensor(out, inp, group=p.tp_group, async_op=async_op)
+        return _pg_reduce_scatter(out, inp, p.tp_group, async_op)
     return c.reduce_scatter(out, inp, async_op=async_op)
 
 
@@ -310,7 +385,7 @@ def all_gather(out: torch.Tensor, inp: torch.Tensor, async_op: bool = True):
         return None
     c = _comm(inp, p, "all_gather")
     if c is None or not _fits(c, inp, 8):
-        return dist.all_gather_into_tensor(out, inp, group=p.tp_group, async_op=async_op)
+        return _pg_all_gather(out, inp, p.tp_group, async_op)
     return c.all_gather(out, inp, async_op=async_op)
 
 

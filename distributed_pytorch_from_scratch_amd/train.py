@@ -175,6 +175,7 @@ def train(rank, args: Namespace):
     dist.barrier()
     done = False
     for epoch in range(start_epoch, max_epoch):
+        hb.beat(n, force=True)     # the loader restart at an epoch boundary is not a stall
         for batch in loader:
             ids = batch["input_ids"].to(dev, non_blocking=True)
             tgt = batch["target_ids"].to(dev, non_blocking=True)
@@ -209,11 +210,12 @@ def train(rank, args: Namespace):
                 accum_host += float(accum.item())
                 accum.zero_()
                 avg = accum_host / (n - start_step)
-                if p.dp_rank == 0:
-                    path = ck.save_checkpoint(model, args.save_dir, p.tp_rank, n, avg, opt, sched,
-                                              keep_last_n=args.reserv_last_n_ckpts)
-                    print(f"[TP rank {p.tp_rank}]: Model saved to {path}", flush=True)
-                dist.barrier()
+                with hb.hold(n):       # the save and the barrier behind it take no steps
+                    if p.dp_rank == 0:
+                        path = ck.save_checkpoint(model, args.save_dir, p.tp_rank, n, avg, opt, sched,
+                                                  keep_last_n=args.reserv_last_n_ckpts)
+                        print(f"[TP rank {p.tp_rank}]: Model saved to {path}", flush=True)
+                    dist.barrier()
             if n >= args.max_steps:
                 done = True
                 break

@@ -11,6 +11,7 @@
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import threading
 import time
@@ -49,15 +50,33 @@ class Heartbeat:
             self._thread = threading.Thread(target=self._watch, daemon=True)
             self._thread.start()
 
-    def beat(self, step: int) -> None:
+    def beat(self, step: int, force: bool = False) -> None:
         now = time.time()
-        if self.store is None or now - self._last < self.interval_s:
+        if self.store is None or (not force and now - self._last < self.interval_s):
             return
         self._last = now
+        self._step = step
         try:
             self.store.set(f"dpfs_hb/{self.rank}", f"{step}:{now}")
         except Exception:
             pass
+
+    @contextlib.contextmanager
+    def hold(self, step: int):
+        """A phase that legitimately runs longer than ``stale_s`` without steps (checkpoint
+        save and the barrier behind it, evaluation, an epoch-boundary loader restart): this
+        rank is not judged stale inside it (the process-group watchdog still bounds a hung
+        collective), and it beats on entry and exit."""
+        self.beat(step, force=True)
+        if self.store is not None:
+            try:
+                self.store.set(f"dpfs_hb/{self.rank}", f"{step}:hold")
+            except Exception:
+                pass
+        try:
+            yield
+        finally:
+            self.beat(step, force=True)
 
     def _watch(self):
         while not self._stop.wait(self.interval_s):
@@ -67,6 +86,8 @@ class Heartbeat:
                     if not self.store.check([f"dpfs_hb/{r}"]):
                         continue
                     _, ts = self.store.get(f"dpfs_hb/{r}").decode().split(":")
+                    if ts == "hold":
+                        continue
                     if now - float(ts) > self.stale_s:
                         stale.append(r)
                 except Exception:

@@ -82,6 +82,25 @@ def test_bench_tp_dp_layout():
     assert d["tp_pure"]["ms_per_step"] > 0
 
 
+@pytest.mark.parametrize("inject", ["raise:0", "hang:3"])
+def test_bench_pure_tp_failure_keeps_headline(inject):
+    """A failure (exception on one rank) or a hang (one rank never arrives) in the extra pure-TP
+    layout still yields exactly one JSON line with the headline numbers, tp_pure = {error}, and
+    exit status 0 on every rank."""
+    from dist_helpers import _free_port
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+           "--gpus", "4", "--tp", "2", "--model", "plumbing", "--steps", "2", "--warmup", "1", "--seq-len", "64",
+           "--batch-per-gpu", "2", "--pure-tp-budget-s", "25"]
+    env = dict(_env(), DPFS_BENCH_INJECT=inject)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    (d,) = _json_lines(r.stdout)
+    assert d["config"]["parallelism"].startswith("tp2dp2") and d["value"] > 0
+    assert d["tp_pure"]["parallelism"] == "tp4" and "error" in d["tp_pure"]
+    assert ("injected" in d["tp_pure"]["error"]) if inject.startswith("raise") else ("timeout" in d["tp_pure"]["error"])
+
+
 def test_resolve_tp():
     sys.path.insert(0, ROOT)
     from bench import resolve_tp

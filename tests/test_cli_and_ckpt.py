@@ -280,3 +280,19 @@ def test_heartbeat_aborts_on_stale_rank(tmp_path):
     assert r.returncode != 0, r.stdout + r.stderr
     assert "stale ranks" in (r.stdout + r.stderr)
     assert time.time() - t0 < 25
+
+
+_HB_HOLD_SCRIPT = _HB_SCRIPT.replace(
+    "        time.sleep(30)          # hung rank: no more heartbeats",
+    "        with hb.hold(1):        # a long checkpoint save: no beats, but not a stall\n"
+    "            time.sleep(5)").replace("range(200)", "range(60)")
+
+
+def test_heartbeat_hold_is_not_stale(tmp_path):
+    """A rank inside ``Heartbeat.hold`` (checkpoint save + barrier, evaluation) for longer
+    than ``stale_s`` does not abort the job."""
+    script = tmp_path / "hb_hold.py"
+    script.write_text(_HB_HOLD_SCRIPT)
+    r = _run([str(script), _port(), ROOT], timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "stale ranks" not in (r.stdout + r.stderr)

@@ -1,0 +1,107 @@
+"""The ``auto`` transport decision of parallel/tp_comm.py, exercised without RCCL.
+
+On a real node ``auto`` validates every candidate transport (xGMI kernels, the relayed TP = 2
+exchange) against an fp32 process-group sum, times them against the process group, picks a
+grid per op and reduces every input of the decision over the TP group (or over the WORLD when
+the relay is a candidate), so that every rank takes the same transport for every op.  A rank
+that decided differently would issue a different collective sequence and hang its group, so
+this is what the first 8-GPU run depends on.  ``DPFS_TP_COMM_AUTO_ANY_BACKEND=1`` runs the
+same decision over gloo: on the CPU (relay candidate only) and, marked gpu, with several ranks
+sharing one MI355X (xGMI kernels + relay).  Each case checks: identical decisions (transport
+and xGMI grid per op) on every rank, the collectives' results against fp32 sums after the
+decision, and the decision record (``tp_comm.info``) the bench line reports.
+"""
+import os
+
+import pytest
+import torch
+
+from dist_helpers import run_distributed
+
+
+def _decide(rank, world, dev, n):
+    os.environ["DPFS_TP_COMM"] = "auto"
+    os.environ["DPFS_TP_COMM_AUTO_ANY_BACKEND"] = "1"
+    os.environ["DPFS_QUIET"] = "1"
+    import torch.distributed as dist
+    if dev == "cuda":
+        torch.cuda.set_device(0)
+    from distributed_pytorch_from_scratch_amd.parallel import process_manager as pm, tp_comm
+    tp_comm.set_fixed_shapes(True)
+    p = pm.get_pgm()
+    W = p.tp_size
+    errs = []
+    for i in range(2):                       # the first call decides, the second reuses it
+        g = torch.Generator().manual_seed(77 * i + rank)
+        x = torch.randn(n, generator=g).to(torch.bfloat16 if dev == "cuda" else torch.float32).to(dev)
+        ref = x.float().clone()
+        dist.all_reduce(ref, group=p.tp_group)
+        part = torch.empty(n // W, dtype=x.dtype, device=dev)
+        h = tp_comm.reduce_scatter(part, x, async_op=True)
+        if h is not None:
+            h.wait()
+        full = torch.empty(n, dtype=x.dtype, device=dev)
+        h = tp_comm.all_gather(full, part, async_op=True)
+        if h is not None:
+            h.wait()
+        y = x.clone()
+        h = tp_comm.all_reduce(y, async_op=True)
+        if h is not None:
+            h.wait()
+        if dev == "cuda":
+            torch.cuda.synchronize()
+        errs += [(part.float() - ref.view(W, -1)[p.tp_rank]).abs().max().item(),
+                 (full.float() - ref).abs().max().item(), (y.float() - ref).abs().max().item()]
+    tp_comm.check()
+    info = tp_comm.info()
+    dec = tp_comm.decision()
+    tp_comm.reset()
+    return dict(err=max(errs), scale=ref.abs().max().item(), dec=dec, info=info, tp_rank=p.tp_rank,
+                dp_rank=p.dp_rank)
+
+
+def _check_same(res, tp):
+    decs = {r: v["dec"] for r, v in res.items()}
+    first = next(iter(decs.values()))
+    assert first is not None
+    for r, d in decs.items():
+        assert d == first, (r, d, first)        # every rank: same transport and grid per op
+    for r, v in res.items():
+        assert v["err"] <= 2e-2 * max(1.0, v["scale"]), (r, v["err"])
+        assert v["info"] is not None and set(v["info"]) >= {"all_reduce", "reduce_scatter", "all_gather",
+                                                            "transport"}
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_auto_decision_relay_candidate_cpu(world):
+    """tp2 x dp(world/2) on the CPU: the relay is the one candidate; its validation and timing
+    are reduced over the WORLD, so every pair takes the same decision."""
+    res = run_distributed(_decide, world, "cpu", 4096, tp_size=2)
+    _check_same(res, 2)
+    for v in res.values():
+        assert "relay_ms" in v["info"]["all_reduce"] and "rccl_ms" in v["info"]["all_reduce"]
+
+
+def test_auto_decision_without_candidates_cpu():
+    """Pure TP 4 on the CPU: no candidate transport, the process group carries everything."""
+    res = run_distributed(_decide, 4, "cpu", 4096, tp_size=4)
+    for v in res.values():
+        assert v["dec"] == {"use": {"all_reduce": "rccl", "reduce_scatter": "rccl", "all_gather": "rccl"},
+                            "op_blocks": None}
+        assert v["err"] < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,tp", [(4, 2), (4, 4), (8, 8)])
+def test_auto_decision_on_one_gpu(world, tp):
+    """Several ranks on one MI355X over gloo: xGMI kernels at every grid width (and the relay
+    when tp = 2 with other pairs) are validated and timed; every rank must reach the same
+    transport and the same xGMI grid per op (8 ranks at tp 8 is the driver's pure-TP layout)."""
+    n = 8 * tp * 4096
+    res = run_distributed(_decide, world, "cuda", n, tp_size=tp)
+    _check_same(res, tp)
+    for v in res.values():
+        assert v["dec"]["op_blocks"] is not None            # xGMI was built and timed
+        assert "xgmi_blocks" in v["info"]["all_reduce"]
+        if tp == 2:
+            assert "relay_ms" in v["info"]["all_reduce"]
