@@ -49,6 +49,9 @@ void dpfs_swiglu_fwd(int, const void*, void*, int, int, int, hipStream_t);
 void dpfs_swiglu_bwd(int, const void*, const void*, void*, int, int, int, hipStream_t);
 long long dpfs_swiglu_bwd_dbias_ws(int, int);
 void dpfs_swiglu_bwd_dbias(int, const void*, const void*, void*, float*, float*, int, int, int, hipStream_t);
+void dpfs_colsum_rows_small(const float*, float*, int, int, hipStream_t);
+bool dpfs_gemm4_nn_swiglu_bwd(const void*, const void*, const void*, void*, float*, int, int, int, int, int, int, int,
+                              int, unsigned, unsigned, hipStream_t);
 bool dpfs_gemm4_nt_swiglu(const void*, const void*, void*, const float*, void*, int, int, int, int, int, int, int,
                           unsigned, unsigned, hipStream_t);
 long long dpfs_ce_bwd_dbias_ws(int, int, int);
@@ -520,6 +523,41 @@ torch::Tensor swiglu_bwd(torch::Tensor dh, torch::Tensor gu, c10::optional<torch
     dpfs_swiglu_bwd(dt, dh.data_ptr(), gu.data_ptr(), dgu.data_ptr(), (int)M, (int)F, perm ? 1 : 0, stream());
   }
   return dgu;
+}
+
+// Down-projection data gradient with the SwiGLU backward in its epilogue: dgu = SwiGLU'(gu) *
+// (dy w) in the natural [gate | up] layout without materialising dy w (gu interleaved when
+// `perm`); with `dbias` also the gate|up bias gradient (column sums of dgu) from the same
+// kernel's partials.  Returns [] where the fused kernel does not apply (the caller runs
+// gemm_nn + swiglu_bwd).
+std::vector<torch::Tensor> gemm_nn_swiglu_bwd(torch::Tensor dy, torch::Tensor w, torch::Tensor gu,
+                                              c10::optional<torch::Tensor> dbias, bool perm) {
+  check_rowmajor(dy, "dy");
+  check_rowmajor(w, "w");
+  check_rowmajor(gu, "gu");
+  TORCH_CHECK(dy.scalar_type() == torch::kBFloat16 && w.scalar_type() == torch::kBFloat16 &&
+                  gu.scalar_type() == torch::kBFloat16, "gemm_nn_swiglu_bwd: bf16 operands");
+  const int64_t M = dy.size(0), K = dy.size(1), F = w.size(1);
+  TORCH_CHECK(w.size(0) == K && gu.size(0) == M && gu.size(1) == 2 * F, "gemm_nn_swiglu_bwd: shapes");
+  const at::DeviceGuard g(dy.device());
+  auto span = [](const torch::Tensor& t) -> long long {
+    return t.size(0) > 0 ? ((t.size(0) - 1) * t.stride(0) + t.size(1)) * 2 : 0;
+  };
+  if (M == 0 || F % 64 || K % 64 || dy.stride(0) % 8 || w.stride(0) % 8 || gu.stride(0) % 8 ||
+      span(dy) >= (1ll << 32) - 16 || span(w) >= (1ll << 32) - 16)
+    return {};
+  float* db = dbias_out(dbias, 2 * F, "gemm_nn_swiglu_bwd");
+  auto dgu = torch::empty({M, 2 * F}, gu.options());
+  const int64_t prow = 2 * ((M + 255) / 256);
+  torch::Tensor part;
+  if (db) part = torch::empty({prow, 2 * F}, gu.options().dtype(torch::kFloat32));
+  if (!dpfs_gemm4_nn_swiglu_bwd(dy.data_ptr(), w.data_ptr(), gu.data_ptr(), dgu.data_ptr(),
+                                db ? part.data_ptr<float>() : nullptr, (int)M, (int)F, (int)K, (int)dy.stride(0),
+                                (int)w.stride(0), (int)gu.stride(0), (int)(2 * F), perm ? 1 : 0, (unsigned)span(dy),
+                                (unsigned)span(w), stream()))
+    return {};
+  if (db) dpfs_colsum_rows_small(part.data_ptr<float>(), db, (int)prow, (int)(2 * F), stream());
+  return {dgu};
 }
 
 torch::Tensor rope_(torch::Tensor qkv, torch::Tensor positions, torch::Tensor table, int64_t n_rot_heads,
@@ -1137,6 +1175,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("swiglu_fwd", &swiglu_fwd, py::arg("gu"), py::arg("perm") = false);
   m.def("swiglu_bwd", &swiglu_bwd, py::arg("dh"), py::arg("gu"), py::arg("dbias") = py::none(),
         py::arg("perm") = false);
+  m.def("gemm_nn_swiglu_bwd", &gemm_nn_swiglu_bwd, py::arg("dy"), py::arg("w"), py::arg("gu"),
+        py::arg("dbias") = py::none(), py::arg("perm") = true);
   m.def("gemm_nt_swiglu", &gemm_nt_swiglu,
         "gate|up NT GEMM (rows interleaved in 64-row blocks) with SwiGLU in the epilogue: [gu, h] or []",
         py::arg("a"), py::arg("b"), py::arg("bias") = py::none());

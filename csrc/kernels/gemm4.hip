@@ -83,6 +83,24 @@ struct SwiOut {
   unsigned h_bytes;
 };
 
+// SwiGLU backward in the down projection's data-gradient epilogue (NN layout; reference
+// models/model.py:94-95, differentiated): the GEMM's C = ds = dy W_down (the gradient wrt
+// h = silu(gate) * up) never reaches memory.  Per element the epilogue rounds ds to bf16 (the
+// value the separate pass would have read), loads gate / up from the forward's gu (interleaved
+// 64-column blocks when `perm`, else natural [gate | up]) and writes
+//   dgate = ds * up * s * (1 + gate * (1 - s)),  dup = ds * gate * s,  s = sigmoid(gate)
+// to dgu in the natural [gate | up] layout -- the swiglu_bwd_colsum_k arithmetic.  The gate|up
+// bias gradient (column sums of dgu) comes out as fp32 partials, one row per wave's 128 rows:
+// part[(m0 + 128 wm) / 128][2F], summed over the lane's 8 row blocks in registers and over the
+// 16 lanes of a DPP row (fixed order, deterministic); colsum_rows reduces the partial rows.
+struct SwiBwd {
+  const bf16* gu;
+  bf16* dgu;
+  float* part;
+  int ldgu, lddgu, perm;
+  unsigned gu_bytes, dgu_bytes, part_bytes;
+};
+
 struct Dual {
   const bf16* A2;
   const bf16* B2;
@@ -339,6 +357,168 @@ __device__ __forceinline__ void epilogue(const char* bias_lds, const Item& ci, v
   }
 }
 
+template <int R>
+__device__ __forceinline__ float ror16(float x) {   // value of lane (l + R) % 16 of the same 16-lane row
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x120 + R, 0xF, 0xF, false));
+}
+
+// asm-issued 16-byte buffer load: invisible to hipcc's vmcnt bookkeeping (which would drain the
+// next item's in-flight LDS-DMA stages at the first use); waited by `pin_vm` with an explicit
+// count.
+__device__ __forceinline__ u32x4 ld16_asm(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  u32x4 v;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r));
+  return v;
+}
+
+template <int N_>
+__device__ __forceinline__ void pin_vm(u32x4& g, u32x4& u) {
+  asm volatile("s_waitcnt vmcnt(%2)" : "+v"(g), "+v"(u) : "n"(N_));
+}
+
+// DPP within 8-lane halves of a 16-lane row: lane i <-> 7 - i, and quad lane xor 2 / xor 1.
+__device__ __forceinline__ float dpp_half_mirror(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x141, 0xF, 0xF, false));
+}
+template <int P>
+__device__ __forceinline__ float dpp_quad(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), P, 0xF, 0xF, false));
+}
+
+// SWB epilogue of one item: 8 blocks of 16 rows.  Loads roll per column group jp: block i+1's
+// gate / up vectors of group jp are issued as soon as block i has consumed that group's, so one
+// set of 8 vectors is live and every wait has a static count (12 younger VMEM ops in steady
+// state).  Column sums: per block, lanes l and l + 8 of a DPP row add their values (row_ror 8);
+// lanes 0-7 of the row keep the gate sums, lanes 8-15 the up sums (32 accumulators per lane,
+// not 64); at the item's end a mirror / quad butterfly sums each 8-lane half and lanes 0 / 8 of
+// every row write the 32 + 32 column partials (fixed order: deterministic).
+// Exactly 8 * 8 + 8 stores per wave (out-of-range lanes get an offset past the descriptor).
+constexpr int SWB_STORES = 8 * 8 + 8;
+// v = x + s (s wave-uniform) as an opaque instruction: hipcc cannot precompute every block's
+// offsets ahead of the unrolled epilogue (which would hold 64 of them in VGPRs at once).
+__device__ __forceinline__ unsigned opaque_add(unsigned x, unsigned s) {
+  unsigned r;
+  asm volatile("v_add_u32 %0, %1, %2" : "=v"(r) : "v"(x), "s"(s));
+  return r;
+}
+
+// acc += mine + (other of lane (l + 8) % 16 of the DPP row), as volatile asm: ordered with the
+// epilogue's other asm (hipcc otherwise sinks the whole accumulation chain to the end of the
+// unrolled epilogue and keeps every block's operands live).  s_nop 1: the DPP read of a VGPR
+// written by the VALU just before needs two wait states (not inserted for inline asm).
+__device__ __forceinline__ void acc_pair(float& acc, float mine, float other) {
+  asm volatile("s_nop 1\n\tv_add_f32_dpp %1, %2, %1 row_ror:8 row_mask:0xf bank_mask:0xf\n\tv_add_f32 %0, %0, %1"
+               : "+v"(acc), "+v"(mine)
+               : "v"(other));
+}
+
+__device__ __forceinline__ void epilogue_swb(const Item& ci, int M, int F, const SwiBwd& sb, int wm, int wn, int l) {
+  const int g = l >> 4;
+  const int wcol0 = ci.n0 + wn * 128;
+  const int row0 = ci.m0 + wm * 128 + (l & 15);
+  const int colg = 16 * (g & 1) + 8 * (g >> 1);
+  const bool upper = (l & 8) != 0;   // lanes 8-15 of the DPP row accumulate the up sums
+  acc_drain();
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)sb.gu, (short)0, (int)sb.gu_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)sb.dgu, (short)0, (int)sb.dgu_bytes, 0x00020000);
+  const int c0 = wcol0 + colg;            // this lane's first natural column (jp = 0)
+  // gate / up byte offsets of column group jp within a gu row: jp adds 32 columns, which in
+  // the interleaved layout is 64 elements when the group crosses into the next 64-block pair
+  const unsigned gcol0 = (unsigned)(sb.perm ? ((c0 >> 6) << 7) + (c0 & 63) : c0) * 2u;
+  const unsigned uadd = (unsigned)(sb.perm ? 64 : F) * 2u;
+  const unsigned gstride = (unsigned)sb.ldgu * 32u, dstride = (unsigned)sb.lddgu * 32u;   // 16 rows
+  unsigned goff = (unsigned)row0 * (unsigned)sb.ldgu * 2u + gcol0;   // block 0, group 0 (gate)
+  unsigned doff = (unsigned)row0 * (unsigned)sb.lddgu * 2u + (unsigned)c0 * 2u;
+  u32x4 G[4], U[4];
+  float acc[4][8];
+#pragma unroll
+  for (int jp = 0; jp < 4; ++jp)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[jp][e] = 0.f;
+  // column group jp of a row: natural column c0 + 32 jp; interleaved: + 64 jp elements (c0 and
+  // c0 + 32 jp share the 64-column block parity: 32 jp < 128, and (c0 & 63) + 32 jp stays in
+  // one gate block only for jp even -> use the exact mapping)
+  auto gdelta = [&](int jp) -> unsigned {
+    if (!sb.perm) return (unsigned)(32 * jp) * 2u;
+    const int c = c0 + 32 * jp;
+    return (unsigned)(((c >> 6) << 7) + (c & 63)) * 2u - gcol0;
+  };
+  auto load = [&](int m, unsigned base, int jp) __attribute__((always_inline)) {
+    const bool ok = m < M && c0 + 32 * jp < F;
+    const unsigned o = base + gdelta(jp);
+    G[jp] = ld16_asm(rg, ok ? o : kOOB);
+    U[jp] = ld16_asm(rg, ok ? o + uadd : kOOB);
+  };
+#pragma unroll
+  for (int jp = 0; jp < 4; ++jp) load(row0, goff, jp);
+  static_for<0, 8>([&](auto I) __attribute__((always_inline)) {
+    constexpr int i = decltype(I)::value;
+    const int m = row0 + 16 * i;
+    const bool mok = m < M;
+    const unsigned gnext = i + 1 < 8 ? opaque_add(goff, gstride) : goff;
+    static_for<0, 4>([&](auto JP) __attribute__((always_inline)) {
+      constexpr int jp = decltype(JP)::value;
+      // VMEM ops younger than (block i, group jp)'s two loads
+      constexpr int YOUNGER = i == 0 ? 6 + 2 * jp : (i == 7 ? 12 - 2 * jp : 12);
+      pin_vm<YOUNGER>(G[jp], U[jp]);
+      const f32x4 v0 = acc_read<i, 2 * jp>(), v1 = acc_read<i, 2 * jp + 1>();
+      const bf16x4 o0 = {(bf16)v0[0], (bf16)v0[1], (bf16)v0[2], (bf16)v0[3]};
+      const bf16x4 o1 = {(bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
+      const u32x2 d2 = __builtin_bit_cast(u32x2, o0), e2 = __builtin_bit_cast(u32x2, o1);
+      const auto sx = __builtin_amdgcn_permlane16_swap(d2[0], e2[0], false, false);
+      const auto sy = __builtin_amdgcn_permlane16_swap(d2[1], e2[1], false, false);
+      const u32x4 w = {sx[0], sy[0], sx[1], sy[1]};
+      const bf16x8 dv = __builtin_bit_cast(bf16x8, w);
+      const bf16x8 gv = __builtin_bit_cast(bf16x8, G[jp]);
+      const bf16x8 uv = __builtin_bit_cast(bf16x8, U[jp]);
+      bf16x8 og, ou;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = (float)dv[e], gg = (float)gv[e], uu = (float)uv[e];
+        const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-gg));
+        const float a = d * uu * sg * (1.f + gg * (1.f - sg));
+        const float b = d * gg * sg;
+        og[e] = (bf16)a;
+        ou[e] = (bf16)b;
+        // lanes l, l + 8 (rows r, r + 8): lower half keeps gate pair sums, upper half up
+        const float mine = upper ? b : a, other = upper ? a : b;
+        acc_pair(acc[jp][e], mine, other);
+      }
+      const bool ok = mok && c0 + 32 * jp < F;
+      const unsigned od = doff + (unsigned)(64 * jp);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, og), rd, ok ? od : kOOB, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ou), rd, ok ? od + (unsigned)F * 2u : kOOB, 0, 0);
+      if constexpr (i + 1 < 8) load(m + 16, gnext, jp);
+    });
+    goff = gnext;
+    if constexpr (i + 1 < 8) doff = opaque_add(doff, dstride);
+  });
+#pragma unroll
+  for (int jp = 0; jp < 4; ++jp)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float a = acc[jp][e];
+      a += dpp_half_mirror(a);
+      a += dpp_quad<0x4E>(a);   // quad_perm [2, 3, 0, 1]: xor 2
+      a += dpp_quad<0xB1>(a);   // quad_perm [1, 0, 3, 2]: xor 1
+      acc[jp][e] = a;
+    }
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)sb.part, (short)0, (int)sb.part_bytes, 0x00020000);
+  const unsigned pbase = (unsigned)((ci.m0 >> 7) + wm) * (unsigned)(2 * F) * 4u;
+  const bool writer = (l & 7) == 0;    // lane 0 (gate) and lane 8 (up) of every DPP row
+#pragma unroll
+  for (int jp = 0; jp < 4; ++jp) {
+    const int c = c0 + 32 * jp + (upper ? F : 0);
+    const bool ok = writer && c0 + 32 * jp < F;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x4 v = {acc[jp][4 * h], acc[jp][4 * h + 1], acc[jp][4 * h + 2], acc[jp][4 * h + 3]};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rp,
+                                             ok ? pbase + (unsigned)(c + 4 * h) * 4u : kOOB, 0, 0);
+    }
+  }
+}
+
 // OUT: 0 = bf16 C (+ fp32 bias[n], + RoPE); 1 = fp32 C / split-K slab.
 // dbg (timing-only ablations, tools/gemm4_probe.py): 4 = no DMA wait, 8 = no step barrier.
 // FAST (every item's K range a multiple of 64, so no step reads past K): the DMA stream
@@ -354,20 +534,22 @@ __device__ __forceinline__ void epilogue(const char* bias_lds, const Item& ci, v
 // its code and register pressure stay out of the plain kernels).
 // SWIGLU: the gate|up form (SwiOut).
 template <bool AK, bool BKM, int OUT, int DIAG = 0, bool FAST = false, int SCHED = 0, int BN = 256, int ROPE = 0,
-          bool SWIGLU = false>
+          bool SWIGLU = false, bool SWB = false>
 __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                   void* __restrict__ C, const float* __restrict__ bias, int M, int N,
                                                   int K, int lda, int ldb, int ldc, int kps, int splits,
                                                   long long slab_stride, unsigned a_bytes, unsigned b_bytes,
                                                   unsigned c_bytes, Rope rope, int group_m, Dual dual, int dbg,
-                                                  unsigned long long* diag, SwiOut swo = SwiOut{}) {
+                                                  unsigned long long* diag, SwiOut swo = SwiOut{},
+                                                  SwiBwd swb = SwiBwd{}) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_TOTAL];
   constexpr int NJ = BN / 32;                  // 16-column MFMA tiles per wave
   constexpr int NBQ = BN / 64;                 // B pieces per wave per stage
   constexpr int NQ = 4 + NBQ;                  // DMA pieces per wave per stage
   // store instructions per wave per item (+ the SwiGLU output's 2 per 16-row block)
-  constexpr int STORES = (OUT == 0 ? 4 * NJ : 8 * NJ) + (SWIGLU ? 16 : 0);
+  constexpr int STORES = SWB ? SWB_STORES : (OUT == 0 ? 4 * NJ : 8 * NJ) + (SWIGLU ? 16 : 0);
   static_assert(!SWIGLU || (OUT == 0 && BN == 256 && ROPE == 0), "SwiGLU epilogue: bf16 256-wide tiles");
+  static_assert(!SWB || (OUT == 0 && BN == 256 && ROPE == 0 && !SWIGLU), "SwiGLU-backward epilogue: bf16 256-wide tiles");
   static_assert(BN == 256 || BN == 192, "tile width");
 
   const int tiles_n = (N + BN - 1) / BN;
@@ -542,8 +724,10 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   // One consumer step on `cur`, prefetching the next step's fragments into `nxt`.
   // Entry wait: stage s+1 landed for this wave (younger: stage s+2 = NQ pieces, plus the
   // previous item's epilogue stores on an item's first step), then the step barrier.
-  auto step = [&](Frags<AK, BKM, BN>& cur, Frags<AK, BKM, BN>& nxt, bool first, auto zero, bool last, int bcol0) {
+  auto step = [&](Frags<AK, BKM, BN>& cur, Frags<AK, BKM, BN>& nxt, bool first, auto zero, auto nopf, bool last,
+                  int bcol0) {
     constexpr bool ZR = decltype(zero)::value;
+    constexpr bool NOPF = decltype(nopf)::value;   // no next-step fragment reads (item end, SWB)
     if constexpr (DIAG) {
       const unsigned long long t = stamp();
       t_body += t - t_mark;
@@ -590,7 +774,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
         // this step's stage descriptors (scalar work) in the shadow of the first MFMAs
         if constexpr (q == 0 && j == 0) stage_rsrc_a();
         if constexpr (q == 0 && j == 1) stage_rsrc_b();
-        if constexpr (q < 4) {
+        if constexpr (q < 4 && !NOPF) {
           // read slots after MFMA 0 / 2 / 4 / 6 (NJ 8) or 0 / 2 / 3 / 5 (NJ 6)
           constexpr int r0 = 0, r1 = 2, r2 = NJ == 8 ? 4 : 3, r3 = NJ == 8 ? 6 : 5;
           if constexpr (j == r0) nxt.a.load(2 * q, src, wm * 128 + 32 * q, l);
@@ -616,11 +800,27 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
     const Item ci = decode<BN>(it, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
     const int nk = nsteps(ci);
     const int bcol0 = ci.n0 + wn * (BN / 2);
-    step(F0, F1, !first, std::true_type{}, false, bcol0);
-    step(F1, F0, false, std::false_type{}, nk == 2, bcol0);
+    constexpr std::false_type NO{};
+    if constexpr (SWB) {
+      // The register-hungry SwiGLU-backward epilogue: the item's last step reads no fragments
+      // (F0 / F1 are dead across the epilogue); the next item's first-step fragments are read
+      // after it from the slot that step would have read (landed at its entry wait, rewritten
+      // only by a DMA issued behind the next step's barrier).
+      step(F0, F1, !first, std::true_type{}, NO, false, bcol0);
+      for (int t = 1; t < nk - 1; t += 2) {
+        step(F1, F0, false, NO, NO, false, bcol0);
+        step(F0, F1, false, NO, NO, false, bcol0);
+      }
+      step(F1, F0, false, NO, std::true_type{}, true, bcol0);
+      epilogue_swb(ci, M, N, swb, wm, wn, l);
+      read_frags<AK, BKM, BN>(F0, smem + c_slot * SLOT, wm, wn, l);
+      continue;
+    }
+    step(F0, F1, !first, std::true_type{}, NO, false, bcol0);
+    step(F1, F0, false, NO, NO, nk == 2, bcol0);
     for (int t = 2; t < nk; t += 2) {
-      step(F0, F1, false, std::false_type{}, false, bcol0);
-      step(F1, F0, false, std::false_type{}, t + 2 >= nk, bcol0);
+      step(F0, F1, false, NO, NO, false, bcol0);
+      step(F1, F0, false, NO, NO, t + 2 >= nk, bcol0);
     }
     if constexpr (DIAG) {
       const unsigned long long t = stamp();
@@ -707,6 +907,33 @@ extern "C" bool dpfs_gemm4_nt_swiglu(const void* A, const void* B, void* C, cons
   gemm4_k<true, true, 0, 0, true, 1, 256, 0, true><<<grid, 256, 0, s>>>(
       (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, K, 1, 0, a_bytes, b_bytes, (unsigned)cspan, rope,
       g_g4_group_m, dual, 0, nullptr, swo);
+  return true;
+}
+
+// Down-projection data gradient with the SwiGLU backward in the epilogue (SwiBwd): A = dy
+// [M, K] (K-major), B = W_down [K, F] (F contiguous), gu [M, 2F] (interleaved if perm), dgu
+// [M, 2F] natural, part [2 * ceil(M / 256), 2F] fp32 (every row written).  Returns false
+// (nothing launched) where the 256-wide FAST kernel does not apply.
+extern "C" bool dpfs_gemm4_nn_swiglu_bwd(const void* A, const void* B, const void* gu, void* dgu, float* part, int M,
+                                         int F, int K, int lda, int ldb, int ldgu, int lddgu, int perm,
+                                         unsigned a_bytes, unsigned b_bytes, hipStream_t s) {
+  if (M <= 0 || F <= 0 || (F % 64) || (K % 64) || lda % 8 || ldb % 8 || ldgu % 8 || lddgu % 8) return false;
+  if (ldgu < 2 * F || lddgu < 2 * F) return false;
+  const long long guspan = ((long long)(M - 1) * ldgu + 2 * F) * 2;
+  const long long dspan = ((long long)(M - 1) * lddgu + 2 * F) * 2;
+  const long long tiles_m = (M + 255) / 256;
+  const long long pspan = tiles_m * 2 * 2LL * F * 4;
+  if (guspan >= (1ll << 32) - 16 || dspan >= (1ll << 32) - 16 || pspan >= (1ll << 32) - 16) return false;
+  const long long items = tiles_m * ((F + 255) / 256);
+  if (items <= 0 || items >= (1ll << 31)) return false;
+  const int grid = (int)std::min<long long>(items, g4_cu_count());
+  const Rope rope = {nullptr, nullptr, 0, 64};
+  const Dual dual = {nullptr, nullptr, 0x7fffffff, lda, ldb, 0u, 0u};
+  const SwiBwd swb = {(const bf16*)gu, (bf16*)dgu, part, ldgu, lddgu, perm ? 1 : 0, (unsigned)guspan, (unsigned)dspan,
+                      (unsigned)pspan};
+  gemm4_k<true, false, 0, 0, true, 1, 256, 0, false, true><<<grid, 256, 0, s>>>(
+      (const bf16*)A, (const bf16*)B, nullptr, nullptr, M, F, K, lda, ldb, F, K, 1, 0, a_bytes, b_bytes, 0u, rope,
+      g_g4_group_m, dual, 0, nullptr, SwiOut{}, swb);
   return true;
 }
 

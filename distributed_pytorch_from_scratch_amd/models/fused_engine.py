@@ -373,10 +373,10 @@ class DecoderTrainFn(torch.autograd.Function):
                 gq = s["g"]
                 if not s.pop("bd_done", False):
                     bias_acc(G, "bd", gq, L.bd)
-                ds = GS.gemm_nn(k, gq, W(L.wd))
                 wd_p.append((gq, a["sw"]))
-                dbgu = ds.new_empty(a["gu"].size(1), dtype=torch.float32) if L.bgu is not None else None
-                dgu = k.swiglu_bwd(ds, a["gu"], dbgu, L.swi)   # + gate|up bias grad in the same pass
+                dbgu = gq.new_empty(a["gu"].size(1), dtype=torch.float32) if L.bgu is not None else None
+                # down dgrad with the SwiGLU backward (+ gate|up bias grad) in its epilogue
+                dgu = GS.down_dgrad_swiglu(k, gq, W(L.wd), a["gu"], dbgu, L.swi)
                 dh2 = GS.gemm_nn(k, dgu, W(L.wgu), out=_slot(ci, dgu.size(0), d, dt))
                 s["bh"], s["dpend"] = _ar(dh2), dh2
                 wgu_p.append((dgu, a["h2"]))

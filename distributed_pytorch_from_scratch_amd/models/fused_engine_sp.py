@@ -278,10 +278,10 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 a, gq = s["layers"][li], s["gfull"]
                 # (bd's grad, partial over my rows and summed over TP by TrainStep, came out of
                 # the norm backward above this layer)
-                ds = GS.gemm_nn(k, gq, W(L.wd))
                 wd_p.append((gq, a["sw"]))
-                dbgu = ds.new_empty(a["gu"].size(1), dtype=torch.float32) if L.bgu is not None else None
-                dgu = k.swiglu_bwd(ds, a["gu"], dbgu, L.swi)
+                dbgu = gq.new_empty(a["gu"].size(1), dtype=torch.float32) if L.bgu is not None else None
+                # down dgrad with the SwiGLU backward (+ gate|up bias grad) in its epilogue
+                dgu = GS.down_dgrad_swiglu(k, gq, W(L.wd), a["gu"], dbgu, L.swi)
                 s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dgu, W(L.wgu), out=_slot(ci, dgu.size(0), d, dt)), n)
                 wgu_p.append((dgu, a["h2"]))
                 if dbgu is not None:

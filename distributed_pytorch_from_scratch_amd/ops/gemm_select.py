@@ -236,6 +236,21 @@ def gate_up(k, x: torch.Tensor, w: torch.Tensor, b, perm: bool):
     return gu, k.swiglu_fwd(gu)
 
 
+def down_dgrad_swiglu(k, dy: torch.Tensor, w: torch.Tensor, gu: torch.Tensor, dbias, perm: bool) -> torch.Tensor:
+    """d gate|up (natural layout) = SwiGLU'(gu) * (dy w): the down projection's data gradient
+    with the SwiGLU backward in the GEMM epilogue (gemm_nn_swiglu_bwd: dy w never reaches
+    memory; the gate|up bias gradient comes from the same kernel into ``dbias``).  Falls back to
+    gemm_nn + swiglu_bwd where the fused kernel declines the shape, for the fp8 step, a pinned
+    library backend, or with ``DPFS_SWIGLU_BWD_EPILOGUE=0`` (A/B runs)."""
+    fused = (k is not reference and dy.is_cuda and mode() in ("auto", "ours") and F8.lookup(w, dgrad=True) is None
+             and os.environ.get("DPFS_SWIGLU_BWD_EPILOGUE", "1") != "0" and hasattr(k, "gemm_nn_swiglu_bwd"))
+    if fused:
+        r = k.gemm_nn_swiglu_bwd(dy, w, gu, dbias, perm)
+        if r:
+            return r[0]
+    return k.swiglu_bwd(gemm_nn(k, dy, w), gu, dbias, perm)
+
+
 def small_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, swiglu: bool = False) -> torch.Tensor:
     """Decode-step projection, M <= 16 rows: y = a w^T (+ bias), a = x or, with ``swiglu``,
     silu(gate) * up of the packed x = [gate | up].  The MFMA GEMV-class kernel (gemv16_k,

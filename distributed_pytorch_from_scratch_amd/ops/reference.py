@@ -352,6 +352,14 @@ def swiglu_bwd(dh: torch.Tensor, gu: torch.Tensor, dbias: Optional[torch.Tensor]
     return d.to(gu.dtype)
 
 
+def gemm_nn_swiglu_bwd(dy: torch.Tensor, w: torch.Tensor, gu: torch.Tensor, dbias: Optional[torch.Tensor] = None,
+                       perm: bool = True):
+    """The down projection's data gradient fused with the SwiGLU backward (the GPU kernel's
+    epilogue form): ds = dy w rounded to dy.dtype, then swiglu_bwd(ds, gu, dbias, perm).
+    Returns [dgu]."""
+    return [swiglu_bwd(gemm_nn(dy, w), gu, dbias, perm)]
+
+
 # ---------------------------------------------------------------------- embedding ----
 
 def embedding_fwd(ids: torch.Tensor, weight: torch.Tensor, vocab_start: int,
