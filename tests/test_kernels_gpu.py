@@ -830,9 +830,11 @@ def test_gemm_nn_swiglu_bwd_epilogue(C, M, F_, K, perm):
     assert torch.equal(dgu, C.swiglu_bwd(ds, gu, db2, perm))
     db_ref = torch.empty(2 * F_, device=DEV)
     gu_nat = R.gu_unperm(gu.float(), 1) if perm else gu.float()
-    dgu_ref = R.swiglu_bwd(R.gemm_nn(dy.float(), w.float()), gu_nat, db_ref)
+    dgu_ref = R.swiglu_bwd(R.gemm_nn(dy.float(), w.float()), gu_nat, None)
     assert _rel(dgu.float(), dgu_ref) < 1e-2
-    assert _rel(db, db_ref) < 1e-3 and torch.isfinite(db).all()
+    # bias grad: the oracle's column sums over the same bf16-rounded dy w the kernel uses
+    R.swiglu_bwd(ds.float(), gu_nat, db_ref)
+    assert _rel(db, db_ref) < 1e-4 and torch.isfinite(db).all()
     assert _rel(db, db2) < 1e-5
     # without a bias gradient the kernel writes no partials and the same dgu
     assert torch.equal(C.gemm_nn_swiglu_bwd(dy, w, gu, None, perm)[0], dgu)
