@@ -14,30 +14,27 @@
 #include <vector>
 
 extern "C" {
-void dpfs_gemm_nt(const void*, const void*, void*, const float*, int, int, int, int, int, int, hipStream_t);
-void dpfs_gemm_nn(const void*, const void*, void*, int, int, int, int, int, int, hipStream_t);
+void dpfs_gemm_nt(const void*, const void*, void*, const float*, int, int, int, int, int, int, int, hipStream_t);
+void dpfs_gemm_nn(const void*, const void*, void*, int, int, int, int, int, int, int, hipStream_t);
 int dpfs_gemm_tn_splits(int, int, int);
 long long dpfs_gemm_tn_ws(int, int, int, int);
 void dpfs_gemm_set_impl(int);
-int dpfs_gemm_rope_fusable(int, int, int, int);
+int dpfs_gemm_rope_fusable(int, int, int, int, int);
 void dpfs_gemm_nt_rope(const void*, const void*, void*, const float*, int, int, int, int, int, int, const int64_t*,
-                       const float*, int, int, hipStream_t);
-void dpfs_gemm_v4_mask(int);
+                       const float*, int, int, int, hipStream_t);
 void dpfs_gemm4_sched(int);
 void dpfs_gemm4_group_m(int);
-void dpfs_gemm4_bn(int);
 void dpfs_gemm4_ablate(int);
 void dpfs_gemm4_diag(void*);
 void dpfs_attn_diag(void*);
 void dpfs_attn_fwd_persist(int);
-int dpfs_gemm_v4_get_mask();
 void dpfs_gemm_force(int, int);
 void dpfs_gemm_v2_sched(int);
 void dpfs_gemm_set_workspace(float*, long long);
 long long dpfs_gemm_bf16_ws(int, int, int);
-void dpfs_gemm_tn(const void*, const void*, float*, float*, int, int, int, int, int, int, hipStream_t);
+void dpfs_gemm_tn(const void*, const void*, float*, float*, int, int, int, int, int, int, int, hipStream_t);
 int dpfs_gemm_tn2(const void*, const void*, const void*, const void*, float*, float*, int, int, int, int, int, int, int,
-                  int, int, hipStream_t);
+                  int, int, int, hipStream_t);
 long long dpfs_gemm_tn2_ws(int, int, int, int);
 void dpfs_rmsnorm_fwd(int, const void*, const float*, void*, float*, int, int, float, hipStream_t);
 void dpfs_layernorm_fwd(int, const void*, const float*, const float*, void*, float*, float*, int, int, float,
@@ -177,8 +174,9 @@ torch::Tensor gemm_out(const c10::optional<torch::Tensor>& out, const torch::Ten
 
 torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> bias,
                       c10::optional<torch::Tensor> rope_pos, c10::optional<torch::Tensor> rope_tab,
-                      int64_t rope_heads, int64_t rope_hd, c10::optional<torch::Tensor> out) {
+                      int64_t rope_heads, int64_t rope_hd, c10::optional<torch::Tensor> out, int64_t variant) {
   check_rowmajor(a, "a");
+  TORCH_CHECK(variant >= 0 && variant <= 3, "gemm: variant 0 (v4), 1 (v4 256-wide), 2 (v4 192-wide) or 3 (v3)");
   check_rowmajor(b, "b");
   TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "gemm_nt: bf16 operands");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
@@ -195,7 +193,7 @@ torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
   if (wsn > 0) ws = torch::empty({wsn}, a.options().dtype(torch::kFloat32));
   dpfs_gemm_set_workspace(wsn > 0 ? ws.data_ptr<float>() : nullptr, wsn);
   const bool want_rope = rope_pos.has_value() && rope_pos->defined() && rope_heads > 0;
-  if (want_rope && dpfs_gemm_rope_fusable((int)M, (int)N, (int)K, (int)rope_hd)) {
+  if (want_rope && dpfs_gemm_rope_fusable((int)M, (int)N, (int)K, (int)rope_hd, (int)variant)) {
     TORCH_CHECK(rope_pos->scalar_type() == torch::kInt64 && rope_pos->is_contiguous() && rope_pos->numel() == M,
                 "gemm_nt: rope_pos must be contiguous int64 [M]");
     TORCH_CHECK(rope_tab.has_value() && rope_tab->scalar_type() == torch::kFloat32 && rope_tab->is_contiguous() &&
@@ -203,18 +201,19 @@ torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
                 "gemm_nt: rope_tab must be fp32 [maxlen, hd]");
     dpfs_gemm_nt_rope(a.data_ptr(), b.data_ptr(), c.data_ptr(), opt_f32(bias, N, "bias"), (int)M, (int)N, (int)K,
                       (int)a.stride(0), (int)b.stride(0), (int)N, rope_pos->data_ptr<int64_t>(),
-                      rope_tab->data_ptr<float>(), (int)(rope_heads * rope_hd), (int)rope_hd, stream());
+                      rope_tab->data_ptr<float>(), (int)(rope_heads * rope_hd), (int)rope_hd, (int)variant, stream());
   } else {
     dpfs_gemm_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), opt_f32(bias, N, "bias"), (int)M, (int)N, (int)K,
-                 (int)a.stride(0), (int)b.stride(0), (int)N, stream());
+                 (int)a.stride(0), (int)b.stride(0), (int)N, (int)variant, stream());
     if (want_rope) rope_(c, *rope_pos, *rope_tab, rope_heads, rope_hd, false);
   }
   dpfs_gemm_set_workspace(nullptr, 0);
   return c;
 }
 
-torch::Tensor gemm_nn(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> out) {
+torch::Tensor gemm_nn(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> out, int64_t variant) {
   check_rowmajor(a, "a");
+  TORCH_CHECK(variant >= 0 && variant <= 3, "gemm: variant 0 (v4), 1 (v4 256-wide), 2 (v4 192-wide) or 3 (v3)");
   check_rowmajor(b, "b");
   TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "gemm_nn: bf16 operands");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(1);
@@ -230,14 +229,16 @@ torch::Tensor gemm_nn(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
   if (wsn > 0) ws = torch::empty({wsn}, a.options().dtype(torch::kFloat32));
   dpfs_gemm_set_workspace(wsn > 0 ? ws.data_ptr<float>() : nullptr, wsn);
   dpfs_gemm_nn(a.data_ptr(), b.data_ptr(), c.data_ptr(), (int)M, (int)N, (int)K, (int)a.stride(0), (int)b.stride(0),
-               (int)N, stream());
+               (int)N, (int)variant, stream());
   dpfs_gemm_set_workspace(nullptr, 0);
   return c;
 }
 
 // c[M,N] fp32 = a[K,M]^T b[K,N]
-torch::Tensor gemm_tn(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> out, bool accumulate) {
+torch::Tensor gemm_tn(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> out, bool accumulate,
+                      int64_t variant) {
   check_rowmajor(a, "a");
+  TORCH_CHECK(variant == 0 || variant == 3, "gemm_tn: variant 0 (v4) or 3 (v3)");
   check_rowmajor(b, "b");
   TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "gemm_tn: bf16 operands");
   const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
@@ -263,14 +264,15 @@ torch::Tensor gemm_tn(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
   torch::Tensor ws;
   if (wsn > 0) ws = torch::empty({(int64_t)wsn}, c.options());
   dpfs_gemm_tn(a.data_ptr(), b.data_ptr(), c.data_ptr<float>(), ws.defined() ? ws.data_ptr<float>() : nullptr, (int)M,
-               (int)N, (int)K, (int)a.stride(0), (int)b.stride(0), accumulate ? 1 : 0, stream());
+               (int)N, (int)K, (int)a.stride(0), (int)b.stride(0), accumulate ? 1 : 0, (int)variant, stream());
   return c;
 }
 
 // c[M,N] fp32 (+)= a0[K0,M]^T b0[K0,N] + a1[K1,M]^T b1[K1,N] in one split-K launch; None
 // (nothing written) when the K-split plan does not fit the two buffers.
 c10::optional<torch::Tensor> gemm_tn2(torch::Tensor a0, torch::Tensor b0, torch::Tensor a1, torch::Tensor b1,
-                                      c10::optional<torch::Tensor> out, bool accumulate) {
+                                      c10::optional<torch::Tensor> out, bool accumulate, int64_t variant) {
+  TORCH_CHECK(variant == 0 || variant == 3, "gemm_tn2: variant 0 (v4) or 3 (v3)");
   for (auto* t : {&a0, &b0, &a1, &b1}) {
     check_rowmajor(*t, "gemm_tn2 operand");
     TORCH_CHECK(t->scalar_type() == torch::kBFloat16 && t->stride(0) % 8 == 0, "gemm_tn2: bf16, row stride % 8");
@@ -296,7 +298,8 @@ c10::optional<torch::Tensor> gemm_tn2(torch::Tensor a0, torch::Tensor b0, torch:
   auto ws = torch::empty({wsn}, c.options());
   const int ok = dpfs_gemm_tn2(a0.data_ptr(), b0.data_ptr(), a1.data_ptr(), b1.data_ptr(), c.data_ptr<float>(),
                                ws.data_ptr<float>(), (int)M, (int)N, (int)K0, (int)K1, (int)a0.stride(0),
-                               (int)b0.stride(0), (int)a1.stride(0), (int)b1.stride(0), accumulate ? 1 : 0, stream());
+                               (int)b0.stride(0), (int)a1.stride(0), (int)b1.stride(0), accumulate ? 1 : 0,
+                               (int)variant, stream());
   if (!ok) return c10::nullopt;
   return c;
 }
@@ -1137,13 +1140,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels of distributed_pytorch_from_scratch_amd";
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("bias") = py::none(),
         py::arg("rope_pos") = py::none(), py::arg("rope_tab") = py::none(), py::arg("rope_heads") = 0,
-        py::arg("rope_hd") = 0, py::arg("out") = py::none());
-  m.def("gemm_nn", &gemm_nn, py::arg("a"), py::arg("b"), py::arg("out") = py::none());
+        py::arg("rope_hd") = 0, py::arg("out") = py::none(), py::arg("variant") = 0);
+  m.def("gemm_nn", &gemm_nn, py::arg("a"), py::arg("b"), py::arg("out") = py::none(), py::arg("variant") = 0);
   m.def("gemm_force", [](int cfg, int splits) { dpfs_gemm_force(cfg, splits); },
         "force the v2 tile config (-1 auto, 0 = 256x256, 1 = 256x128) and K-splits (0 auto)");
-  m.def("gemm_v4_mask", [](int v) { dpfs_gemm_v4_mask(v); },
-        "layouts on the v4 kernel (one wave per SIMD, 128x128 per wave): bit 1 NT, 2 NN, 4 TN; 0 = all on v3");
-  m.def("gemm_v4_get_mask", []() { return dpfs_gemm_v4_get_mask(); });
   m.def("gemm4_ablate", [](int v) { dpfs_gemm4_ablate(v); }, "timing-only: 1 = drop stores, 2 = zero operands");
   m.def("attn_fwd_persist", [](int v) { dpfs_attn_fwd_persist(v); },
         "forward v3 grid: 1 = persistent (resident blocks walk the items), 0 = one block per item");
@@ -1154,14 +1154,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm4_sched", [](int v) { dpfs_gemm4_sched(v); },
         "v4 main-loop variant: 0 = default (descriptor-advancing DMA where K ranges allow, one piece per MFMA "
         "row), 1 = two pieces per row in rows 4-7, 2 = per-lane K checks everywhere (the pre-FAST stream)");
-  m.def("gemm4_bn", [](int v) { dpfs_gemm4_bn(v); }, "v4 tile width of non-split bf16 GEMMs: 0 per shape, 256 / 192 forced");
   m.def("gemm4_group_m", [](int v) { dpfs_gemm4_group_m(v); }, "v4 tile-row group size of the item order (default 4)");
   m.def("gemm_v2_sched", [](int v) { dpfs_gemm_v2_sched(v); }, "v2 256x256 schedule (-1 per-layout default, 0..4 see gemm2_k SCHED)");
   m.def("gemm_set_impl", [](int v) { dpfs_gemm_set_impl(v); }, "1 = v1 (128x128 register-staged), 2 = v2 (LDS-DMA, one tile per workgroup), 3 = v3 (persistent v2, default)");
   m.def("gemm_tn2", &gemm_tn2, "fp32 c (+)= a0^T b0 + a1^T b1 (reduction dim over two buffers), one split-K launch; None if the plan does not fit",
         py::arg("a0"), py::arg("b0"), py::arg("a1"), py::arg("b1"), py::arg("out") = py::none(),
-        py::arg("accumulate") = false);
-  m.def("gemm_tn", &gemm_tn, py::arg("a"), py::arg("b"), py::arg("out") = py::none(), py::arg("accumulate") = false);
+        py::arg("accumulate") = false, py::arg("variant") = 0);
+  m.def("gemm_tn", &gemm_tn, py::arg("a"), py::arg("b"), py::arg("out") = py::none(), py::arg("accumulate") = false,
+        py::arg("variant") = 0);
   m.def("bias_grad", &bias_grad);
   m.def("add_bias_", &add_bias_);
   m.def("bias_residual", &bias_residual);

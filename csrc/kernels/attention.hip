@@ -1462,8 +1462,18 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv2_k(
 // handles a causal pair of key blocks (p, nkb-1-p): the same work for every workgroup.
 template <int HD>
 __device__ __forceinline__ int swz_u(int r, int ch) {
-  const int m = r >> 1;
-  return ch ^ ((m & 7) ^ ((m & 1) << 2));   // hd 64: 8 chunks per row
+  if constexpr (HD == 64) {
+    const int m = r >> 1;
+    return ch ^ ((m & 7) ^ ((m & 1) << 2));   // hd 64: 8 chunks per row
+  } else {
+    // hd 128: 16 chunks of 16 B per 256-B row, so every row starts a bank row.  Row reads (16
+    // lanes = 16 consecutive rows, one chunk): the XOR term must be a permutation over any 16
+    // aligned rows; transposed reads (32 lanes = 4 aligned rows x 4 consecutive chunks of one
+    // 64-B span): its bits 2-3 must differ over any 4 aligned rows.  Bit rotation of r & 15
+    // does both, and depends on r & 15 only (row + 16 s / + 32 qt stay immediates).
+    static_assert(HD == 128, "swz_u: head_dim 64 or 128");
+    return ch ^ (((r & 3) << 2) | ((r >> 2) & 3));
+  }
 }
 
 // Q / dO rows [q0, q0 + 64) and the 64 lse / delta values of a query tile into one stage:
@@ -1506,7 +1516,7 @@ struct QdoDma3 {
 };
 
 template <int HD>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv3_k(
+__global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
     const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V, const bf16* __restrict__ dO,
     const float* __restrict__ LSN, const float* __restrict__ NDEL, bf16* __restrict__ dK, bf16* __restrict__ dV,
     int T, int H, int BH, long long ldq, long long ldk, long long ldv, long long lddo, long long lddk,
@@ -1514,7 +1524,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv3_k(
     float* __restrict__ BPK, float* __restrict__ BPV) {
   // LSN = -lse log2(e) and NDEL = -delta per query row (written by attn_bwd_dq3_k).  BPK / BPV
   // (optional): per (b, h, key block, wave) column sums of the stored dK / dV rows.
-  static_assert(HD == 64, "dK/dV v3: head_dim 64");
+  static_assert(HD == 64 || HD == 128, "dK/dV v3: head_dim 64 or 128");
   constexpr int BK = 128, BQ = 64, KS = HD / 16, DTN = HD / 32, RB = HD * 2;
   constexpr int TILE = BQ * RB, BUF = 2 * TILE + 1024, NST = 3;
   constexpr int PWV = QdoDma3<HD>::PW + 1;   // DMA instructions per wave per tile
@@ -1624,7 +1634,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv3_k(
         sc[1] = MFMA32(*reinterpret_cast<const bf16x8*>(lq + roff[ks] + 32 * RB), kf[ks], sc[1]);
         dp[1] = MFMA32(*reinterpret_cast<const bf16x8*>(ldo_ + roff[ks] + 32 * RB), vf[ks], dp[1]);
 #pragma unroll
-        for (int i = 4 * ks; i < 4 * ks + 4; ++i)
+        for (int i = (16 / KS) * ks; i < (16 / KS) * (ks + 1); ++i)
           sc[0][i] = __builtin_amdgcn_exp2f(fmaf(sc[0][i], c2, lsr[0][i >> 2][i & 3]));
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -2009,13 +2019,13 @@ struct KvDmaU {   // K / V tile rows [kv0, kv0 + 64) into a stage (K at 0, V at 
 };
 
 template <int HD>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq3_k(
+__global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
     const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V, const bf16* __restrict__ dO,
     const bf16* __restrict__ Og, const float* __restrict__ LSE, float* __restrict__ NDEL_OUT,
     float* __restrict__ LSN_OUT, bf16* __restrict__ dQ, int T, int H, int BH, long long ldq, long long ldk,
     long long ldv, long long lddo, long long ldo, long long lddq, float scale, int causal,
     const int64_t* __restrict__ rpos, const float* __restrict__ rtab, float* __restrict__ BPQ) {
-  static_assert(HD == 64, "dQ v3: head_dim 64");
+  static_assert(HD == 64 || HD == 128, "dQ v3: head_dim 64 or 128");
   constexpr int BQ = 128, BKV = 64, KS = HD / 16, DTN = HD / 32, RB = HD * 2;
   constexpr int TILE = BKV * RB, STAGE = 2 * TILE, NST = 3;
   constexpr int PW = KvDmaU<HD>::PW;
@@ -2112,7 +2122,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq3_k(
         sc[1] = MFMA32(*reinterpret_cast<const bf16x8*>(lk + koff[1][ks]), qf[ks], sc[1]);
         dp[1] = MFMA32(*reinterpret_cast<const bf16x8*>(lv + koff[1][ks]), df[ks], dp[1]);
 #pragma unroll
-        for (int i = 4 * ks; i < 4 * ks + 4; ++i) sc[0][i] = __builtin_amdgcn_exp2f(fmaf(sc[0][i], c2, lc));
+        for (int i = (16 / KS) * ks; i < (16 / KS) * (ks + 1); ++i)
+          sc[0][i] = __builtin_amdgcn_exp2f(fmaf(sc[0][i], c2, lc));
         __builtin_amdgcn_sched_barrier(0);
       }
       // K^T fragments (A of dQ^T: lane d = 32 dt + r32, keys 16 s + 4 hf + 0..3 / 8..11)
@@ -2319,33 +2330,43 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
                               float* bws) {
   // The QKV bias gradient rides on the default kernel pair (dQ + LDS-DMA dK/dV); with another
   // dK/dV variant the caller computes it with a separate column sum.
+  const bool v3ok = hd == 64 || hd == 128;
   const int bimpl = g_attn_bwd_impl == 0 ? (hd == 64 ? 4 : 2) : g_attn_bwd_impl;
-  const bool bias = dbias != nullptr && bws != nullptr && (bimpl == 2 || (bimpl == 4 && hd == 64));
+  const bool bias = dbias != nullptr && bws != nullptr && (bimpl == 2 || (bimpl == 4 && v3ok));
   const int nqb = (T + 127) / 128, nkb = (T + 63) / 64;
   float* pq = bias ? bws : nullptr;
   float* pk = bias ? bws + (long long)H * B * nqb * 4 * hd : nullptr;
   float* pv = bias ? pk + (long long)H * B * nkb * 4 * hd : nullptr;
   dim3 gq(nqb, B * H);
-  if (bimpl == 4 && hd == 64) {   // (attn_bwd_dkdv3_k reads the -lse log2 e this kernel writes)
+  if (bimpl == 4 && v3ok) {   // (attn_bwd_dkdv3_k reads the -lse log2 e this kernel writes)
     const int items = (B * H + 7) / 8 * 8 * ((nqb + 1) / 2);
-    attn_bwd_dq3_k<64><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,
-                                             (const bf16*)o, lse, delta, delta + (long long)B * H * T, (bf16*)dq, T,
-                                             H, B * H, ldq, ldk, ldv, lddo, ldo, lddq, scale, causal, rope_pos,
-                                             rope_tab, pq);
+#define DPFS_DQ3(HD_)                                                                                             \
+  attn_bwd_dq3_k<HD_><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,   \
+                                            (const bf16*)o, lse, delta, delta + (long long)B * H * T, (bf16*)dq, T, \
+                                            H, B * H, ldq, ldk, ldv, lddo, ldo, lddq, scale, causal, rope_pos,     \
+                                            rope_tab, pq)
+    if (hd == 64) DPFS_DQ3(64);
+    else DPFS_DQ3(128);
+#undef DPFS_DQ3
   } else
   DPFS_HD_DISPATCH(hd, attn_bwd_dq_k<HD_><<<gq, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
                                                              (const bf16*)dout, (const bf16*)o, lse, delta,
                                                              delta + (long long)B * H * T, (bf16*)dq,
                                                              T, H, ldq, ldk, ldv, lddo, ldo, lddq, scale, causal,
                                                              rope_pos, rope_tab, pq));
-  if (bimpl == 4 && hd == 64) {
+  if (bimpl == 4 && v3ok) {
     const int nkb3 = (T + 127) / 128, items = (B * H + 7) / 8 * 8 * ((nkb3 + 1) / 2);
-    attn_bwd_dkdv3_k<64><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,
-                                               delta + (long long)B * H * T, delta, (bf16*)dk, (bf16*)dv, T, H, B * H,
-                                               ldq, ldk, ldv, lddo, lddk, lddv, scale, causal, rope_pos, rope_tab,
-                                               pk, pv);
+#define DPFS_DKDV3(HD_)                                                                                           \
+  attn_bwd_dkdv3_k<HD_><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, \
+                                              delta + (long long)B * H * T, delta, (bf16*)dk, (bf16*)dv, T, H,     \
+                                              B * H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal, rope_pos,     \
+                                              rope_tab, pk, pv)
+    if (hd == 64) DPFS_DKDV3(64);
+    else DPFS_DKDV3(128);
+#undef DPFS_DKDV3
     if (bias) {
-      attn_bias_grad_k<64><<<3 * H * 4, 1024, 0, s>>>(pq, pk, pv, dbias, H, B * nqb * 4, B * nkb3 * 4);
+      if (hd == 64) attn_bias_grad_k<64><<<3 * H * 4, 1024, 0, s>>>(pq, pk, pv, dbias, H, B * nqb * 4, B * nkb3 * 4);
+      else attn_bias_grad_k<128><<<3 * H * 8, 1024, 0, s>>>(pq, pk, pv, dbias, H, B * nqb * 4, B * nkb3 * 4);
       return 1;
     }
     return 0;

@@ -913,10 +913,15 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
                                   long long slab_stride, unsigned a_bytes, unsigned b_bytes, const int64_t* rope_pos,
                                   const float* rope_tab, int rope_cols, int rope_hd, const void* A2, const void* B2,
                                   int k_switch, int lda2, int ldb2, unsigned a2_bytes, unsigned b2_bytes,
-                                  hipStream_t s);
-static int g_v4_mask = 3;
-extern "C" void dpfs_gemm_v4_mask(int m) { g_v4_mask = m; }
-extern "C" int dpfs_gemm_v4_get_mask() { return g_v4_mask; }
+                                  int bn_force, hipStream_t s);
+
+// Per-call kernel variant (an argument of every GEMM entry point, never process state):
+//   0 = v4 with its per-shape tile width (the default for every layout),
+//   1 / 2 = v4 with the 256 / 192 tile width forced (non-split bf16 NT / NN),
+//   3 = the v3 kernel (8 waves, 128 x 64 per wave).
+// Where the v4 launcher declines a shape (32-bit spans, alignment) the v3 kernel runs.
+static bool use_v4(int variant) { return g_gemm_impl >= 3 && variant != 3; }
+static int v4_bn(int variant) { return variant == 1 ? 256 : (variant == 2 ? 192 : 0); }
 
 extern "C" long long dpfs_gemm_bf16_ws(int M, int N, int K) {
   const int S = bf16_splits(M, N, K);
@@ -925,16 +930,17 @@ extern "C" long long dpfs_gemm_bf16_ws(int M, int N, int K) {
 
 template <bool BKM>
 static void bf16_gemm(const void* A, const void* B, void* C, const float* bias, int M, int N, int K, int lda, int ldb,
-                      int ldc, unsigned ab, unsigned bb, hipStream_t s, RopeArgs rope = RopeArgs{nullptr, nullptr, 0}) {
+                      int ldc, unsigned ab, unsigned bb, int variant, hipStream_t s,
+                      RopeArgs rope = RopeArgs{nullptr, nullptr, 0}) {
   const int S = bf16_splits(M, N, K);
-  const bool v4 = g_gemm_impl >= 3 && (g_v4_mask & (BKM ? 1 : 2)) != 0;
+  const bool v4 = use_v4(variant);
   const int lay = BKM ? 0 : 1;
   if (S > 1 && g_ws && g_ws_floats >= (long long)S * M * N) {
     int kps = (K + S - 1) / S;
     kps = ((kps + BKK - 1) / BKK) * BKK;
     const bool done4 = v4 && dpfs_gemm4_launch(lay, 1, A, B, g_ws, nullptr, M, N, K, lda, ldb, N, kps, S,
                                                (long long)M * N, ab, bb, nullptr, nullptr, 0, 64, nullptr, nullptr, 0,
-                                               0, 0, 0u, 0u, s);
+                                               0, 0, 0u, 0u, 0, s);
     if (!done4 && (g_gemm_impl != 3 || !launchp<true, BKM, 1>(pick_cfg(M, N, S), A, B, g_ws, nullptr, M, N, K, lda,
                                                                ldb, N, S, kps, (long long)M * N, ab, bb, s)))
       launch2<true, BKM, 1>(pick_cfg(M, N, S), A, B, g_ws, nullptr, M, N, K, lda, ldb, N, S, kps, (long long)M * N, ab,
@@ -946,10 +952,10 @@ static void bf16_gemm(const void* A, const void* B, void* C, const float* bias, 
     return;
   }
   if (v4 && dpfs_gemm4_launch(lay, 0, A, B, C, bias, M, N, K, lda, ldb, ldc, ((K + 31) / 32) * 32, 1, 0, ab, bb,
-                               rope.pos, rope.tab, rope.cols, rope.hd, nullptr, nullptr, 0, 0, 0, 0u, 0u, s))
+                               rope.pos, rope.tab, rope.cols, rope.hd, nullptr, nullptr, 0, 0, 0, 0u, 0u, v4_bn(variant), s))
     return;
   if (rope.cols > 0 && rope.hd != 64) {   // v3's epilogue rotates 64-wide heads only
-    bf16_gemm<BKM>(A, B, C, bias, M, N, K, lda, ldb, ldc, ab, bb, s);
+    bf16_gemm<BKM>(A, B, C, bias, M, N, K, lda, ldb, ldc, ab, bb, variant, s);
     dpfs_rope_after_gemm(C, rope, M, ldc, s);
     return;
   }
@@ -961,39 +967,39 @@ static void bf16_gemm(const void* A, const void* B, void* C, const float* bias, 
 
 // Whether dpfs_gemm_nt_rope fuses the rotation into the GEMM epilogue (hd 64; otherwise it
 // runs the separate RoPE kernel after the GEMM — same result).
-extern "C" int dpfs_gemm_rope_fusable(int M, int N, int K, int hd) {
+extern "C" int dpfs_gemm_rope_fusable(int M, int N, int K, int hd, int variant) {
   if (g_gemm_impl == 1) return 0;
   if (hd == 64) return N % 64 == 0;
-  return hd == 128 && (g_v4_mask & 1) && N % 128 == 0;
+  return hd == 128 && use_v4(variant) && N % 128 == 0;
 }
 
 extern "C" void dpfs_gemm_nt_rope(const void* A, const void* B, void* C, const float* bias, int M, int N, int K,
                                   int lda, int ldb, int ldc, const int64_t* pos, const float* tab, int rope_cols,
-                                  int rope_hd, hipStream_t s) {
-  bf16_gemm<true>(A, B, C, bias, M, N, K, lda, ldb, ldc, span_bytes(M, lda, K), span_bytes(N, ldb, K), s,
+                                  int rope_hd, int variant, hipStream_t s) {
+  bf16_gemm<true>(A, B, C, bias, M, N, K, lda, ldb, ldc, span_bytes(M, lda, K), span_bytes(N, ldb, K), variant, s,
                   RopeArgs{pos, tab, rope_cols, rope_hd});
 }
 
 // NT: C[M,N] bf16 = A[M,K] B[N,K]^T (+ bias)
 extern "C" void dpfs_gemm_nt(const void* A, const void* B, void* C, const float* bias, int M, int N, int K, int lda,
-                             int ldb, int ldc, hipStream_t s) {
+                             int ldb, int ldc, int variant, hipStream_t s) {
   if (g_gemm_impl == 1) {
     gemm_k<true, true, 0><<<dim3(tiles_of(M, N), 1), 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K,
                                                                  lda, ldb, ldc, K, 0);
     return;
   }
-  bf16_gemm<true>(A, B, C, bias, M, N, K, lda, ldb, ldc, span_bytes(M, lda, K), span_bytes(N, ldb, K), s);
+  bf16_gemm<true>(A, B, C, bias, M, N, K, lda, ldb, ldc, span_bytes(M, lda, K), span_bytes(N, ldb, K), variant, s);
 }
 
 // NN: C[M,N] bf16 = A[M,K] B[K,N]
 extern "C" void dpfs_gemm_nn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
-                             hipStream_t s) {
+                             int variant, hipStream_t s) {
   if (g_gemm_impl == 1) {
     gemm_k<true, false, 0><<<dim3(tiles_of(M, N), 1), 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, nullptr, M, N,
                                                                   K, lda, ldb, ldc, K, 0);
     return;
   }
-  bf16_gemm<false>(A, B, C, nullptr, M, N, K, lda, ldb, ldc, span_bytes(M, lda, K), span_bytes(K, ldb, N), s);
+  bf16_gemm<false>(A, B, C, nullptr, M, N, K, lda, ldb, ldc, span_bytes(M, lda, K), span_bytes(K, ldb, N), variant, s);
 }
 
 // TN (wgrad) plan.  Outputs are small (weight shards) and K = tokens is long, so the K-split
@@ -1079,7 +1085,7 @@ extern "C" long long dpfs_gemm_tn_ws(int M, int N, int K, int accumulate) {
 
 // TN: C[M,N] fp32 (+)= A[K,M]^T B[K,N].  ws: splits*M*N floats when splits > 1 or accumulate.
 extern "C" void dpfs_gemm_tn(const void* A, const void* B, float* C, float* ws, int M, int N, int K, int lda, int ldb,
-                             int accumulate, hipStream_t s) {
+                             int accumulate, int variant, hipStream_t s) {
   const long long n = (long long)M * N;
   int cfg;
   const int S = tn_plan(M, N, K, &cfg);
@@ -1087,7 +1093,7 @@ extern "C" void dpfs_gemm_tn(const void* A, const void* B, float* C, float* ws, 
   kps = ((kps + BKK - 1) / BKK) * BKK;
   const bool direct = (S == 1 && !accumulate);
   float* dst = direct ? C : ws;
-  if ((g_v4_mask & 4) && g_gemm_impl >= 3) {
+  if (use_v4(variant)) {
     const int S4 = g_force_splits > 0 ? g_force_splits : tn_v2_splits(M, N, K);
     if (S4 == S || (S4 < S)) {   // v4 plans with 256 x 256 tiles; its split count never needs more slabs
       int kps4 = (K + S4 - 1) / S4;
@@ -1095,7 +1101,7 @@ extern "C" void dpfs_gemm_tn(const void* A, const void* B, float* C, float* ws, 
       const bool direct4 = (S4 == 1 && !accumulate);
       if (dpfs_gemm4_launch(2, 1, A, B, direct4 ? C : ws, nullptr, M, N, K, lda, ldb, N, direct4 ? ((K + 31) / 32) * 32 : kps4,
                             S4, direct4 ? 0 : n, span_bytes(K, lda, M), span_bytes(K, ldb, N), nullptr, nullptr, 0, 64,
-                            nullptr, nullptr, 0, 0, 0, 0u, 0u, s)) {
+                            nullptr, nullptr, 0, 0, 0, 0u, 0u, 0, s)) {
         if (direct4) return;
         long long g = (n / 4 + 255) / 256;
         if (g > 4096) g = 4096;
@@ -1163,17 +1169,17 @@ extern "C" long long dpfs_gemm_tn2_ws(int M, int N, int K0, int K1) {
 
 extern "C" int dpfs_gemm_tn2(const void* A0, const void* B0, const void* A1, const void* B1, float* C, float* ws,
                              int M, int N, int K0, int K1, int lda0, int ldb0, int lda1, int ldb1, int accumulate,
-                             hipStream_t s) {
+                             int variant, hipStream_t s) {
   int cfg, kps;
   const int S = tn2_plan(M, N, K0, K1, &cfg, &kps);
   if (S == 0) return 0;
   const int K = K0 + K1;
   const long long n = (long long)M * N;
   const Dual d = {(const bf16*)A1, (const bf16*)B1, K0, lda1, ldb1, span_bytes(K1, lda1, M), span_bytes(K1, ldb1, N)};
-  const bool done4 = (g_v4_mask & 4) &&
+  const bool done4 = use_v4(variant) &&
                      dpfs_gemm4_launch(2, 1, A0, B0, ws, nullptr, M, N, K, lda0, ldb0, N, kps, S, n,
                                        span_bytes(K0, lda0, M), span_bytes(K0, ldb0, N), nullptr, nullptr, 0, 64, A1,
-                                       B1, K0, lda1, ldb1, d.a2_bytes, d.b2_bytes, s);
+                                       B1, K0, lda1, ldb1, d.a2_bytes, d.b2_bytes, 0, s);
   if (!done4 && !launchp<false, false, 1>(cfg, A0, B0, ws, nullptr, M, N, K, lda0, ldb0, N, S, kps, n, span_bytes(K0, lda0, M),
                                 span_bytes(K0, ldb0, N), s, RopeArgs{nullptr, nullptr, 0}, d))
     return 0;

@@ -882,9 +882,6 @@ extern "C" void dpfs_gemm4_diag(void* p) { g_g4_diag = (unsigned long long*)p; }
 // 1 = two pieces per row in rows 4-7; 2 = per-lane K checks even where FAST applies.
 static int g_g4_sched = 0;
 extern "C" void dpfs_gemm4_sched(int v) { g_g4_sched = v; }
-// Tile width of non-split bf16 GEMMs: 0 = chosen per shape (g4_pick_bn), 256 / 192 forced.
-static int g_g4_bn = 0;
-extern "C" void dpfs_gemm4_bn(int v) { g_g4_bn = v; }
 extern "C" void dpfs_gemm4_group_m(int g) { g_g4_group_m = g > 0 ? g : 4; }
 
 // gate|up projection with SwiGLU in the epilogue (SwiOut): C[M, N] = A perm(B)^T + perm(bias)
@@ -945,7 +942,8 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
                                   long long slab_stride, unsigned a_bytes, unsigned b_bytes, const int64_t* rope_pos,
                                   const float* rope_tab, int rope_cols, int rope_hd, const void* A2, const void* B2,
                                   int k_switch, int lda2, int ldb2, unsigned a2_bytes, unsigned b2_bytes,
-                                  hipStream_t s) {
+                                  int bn_force, hipStream_t s) {
+  // bn_force: tile width of a non-split bf16 GEMM, 0 = chosen per shape, 256 / 192 forced
   if (M <= 0 || N <= 0 || (N % 8) || (K % 8)) return false;
   if (layout == 2 && (M % 8)) return false;
   if (rope_cols > 0 && rope_hd != 64 && rope_hd != 128) return false;
@@ -959,9 +957,9 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
   const int cus = g4_cu_count();
   int bn = 256;
   if (!out_f32 && splits == 1 && rope_cols == 0) {
-    if (g_g4_bn == 192) {
+    if (bn_force == 192) {
       bn = 192;
-    } else if (g_g4_bn == 0) {
+    } else if (bn_force == 0) {
       const long long tm = (M + 255) / 256;
       const long long r256 = (tm * ((N + 255) / 256) + cus - 1) / cus;
       const long long r192 = (tm * ((N + 191) / 192) + cus - 1) / cus;

@@ -105,40 +105,25 @@ def _lt_index(c: str) -> int:
     return int(c[2:])
 
 
-_V4_BIT = {"nt": 1, "nn": 2, "tn": 4}
+# Per-call kernel variant of our GEMM entry points (an argument, never process state):
+# 0 = v4 at its per-shape tile width, 1 / 2 = v4 with the 256 / 192 width forced, 3 = v3.
+_VARIANT = {"ours": 0, "ours256": 1, "ours192": 2, "ours3": 3}
 
 
-def _ours_variants(k, layout: str, fn: Callable[[], torch.Tensor], widths: bool = False) -> Dict[str, Callable]:
+def _ours_variants(call: Callable[[int], torch.Tensor], widths: bool = False) -> Dict[str, Callable]:
     """Our candidates for one call: ``ours`` = the v4 kernel (one wave per SIMD, 128-row wave
-    tiles, csrc/kernels/gemm4.hip) at its per-shape tile width, ``ours256`` / ``ours192`` =
-    v4 with the width forced (``widths``: non-split bf16 NT / NN), ``ours3`` = the v3 kernel
-    (8 waves, gemm.hip).  Which wins depends on the shape (epilogue / K-loop balance, tile
-    rounds over the CUs), so all are timed."""
-    if not hasattr(k, "gemm_v4_mask"):
-        return {"ours": fn}
-    bit = _V4_BIT[layout]
-
-    def with_mask(on: bool, bn: int = 0):
-        def run():
-            old = k.gemm_v4_get_mask()
-            k.gemm_v4_mask((old | bit) if on else (old & ~bit))
-            if bn:
-                k.gemm4_bn(bn)
-            try:
-                return fn()
-            finally:
-                k.gemm_v4_mask(old)
-                if bn:
-                    k.gemm4_bn(0)
-        return run
-    out = {"ours": with_mask(True), "ours3": with_mask(False)}
-    if widths and hasattr(k, "gemm4_bn"):
-        out.update({"ours256": with_mask(True, 256), "ours192": with_mask(True, 192)})
+    tiles, csrc/kernels/gemm4.hip) at its per-shape tile width and, with ``widths`` (non-split
+    bf16 NT / NN), ``ours256`` / ``ours192`` = v4 with the width forced.  The v3 kernel
+    (variant 3) lost to v4 on every step shape (profiles/r3_gemm_v4_probe_salu.txt) and is no
+    longer a candidate; it remains the fallback for shapes the v4 launcher declines."""
+    out = {"ours": lambda: call(0)}
+    if widths:
+        out.update({"ours256": lambda: call(1), "ours192": lambda: call(2)})
     return out
 
 
-def _run_ours(k, layout: str, choice: str, fn: Callable[[], torch.Tensor], widths: bool = False):
-    return _ours_variants(k, layout, fn, widths).get(choice, fn)()
+def _run_ours(call: Callable[[int], torch.Tensor], choice: str):
+    return call(_VARIANT.get(choice, 0))
 
 
 # Below this many rows (decode steps, tiny batches) a host-timed loop measures launch cost, not
@@ -191,17 +176,17 @@ def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, out=None) -> torch.T
             return y
         return run
 
-    def ours():
-        return k.gemm_nt(x, w, bias, out=out)
+    def ours(variant: int = 0):
+        return k.gemm_nt(x, w, bias, out=out, variant=variant)
     if m == "blas":
         return blas()
     if m == "lt":
         return lt(0)() if lt_ok and _lt_count(k, 0, M, N, K, bias is not None) else blas()
     key = ("nt", M, N, K, bias is not None, x.device.index)
-    c = _pick(key, {**_ours_variants(k, "nt", ours, True), **({"blas": blas} if _lib() else {})},
+    c = _pick(key, {**_ours_variants(ours, True), **({"blas": blas} if _lib() else {})},
               lambda: _lt_count(k, 0, M, N, K, bias is not None), lt if lt_ok else None)
     if c.startswith("ours") or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
-        return _run_ours(k, "nt", c, ours, True)
+        return _run_ours(ours, c)
     return blas() if c == "blas" else lt(_lt_index(c))()
 
 
@@ -289,17 +274,17 @@ def gemm_nn(k, a: torch.Tensor, b: torch.Tensor, out=None) -> torch.Tensor:
             return y
         return run
 
-    def ours():
-        return k.gemm_nn(a, b, out=out)
+    def ours(variant: int = 0):
+        return k.gemm_nn(a, b, out=out, variant=variant)
     if m == "blas":
         return blas()
     if m == "lt":
         return lt(0)() if lt_ok and _lt_count(k, 1, M, N, K, False) else blas()
     key = ("nn", M, N, K, a.device.index)
-    c = _pick(key, {**_ours_variants(k, "nn", ours, True), **({"blas": blas} if _lib() else {})},
+    c = _pick(key, {**_ours_variants(ours, True), **({"blas": blas} if _lib() else {})},
               lambda: _lt_count(k, 1, M, N, K, False), lt if lt_ok else None)
     if c.startswith("ours") or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
-        return _run_ours(k, "nn", c, ours, True)
+        return _run_ours(ours, c)
     return blas() if c == "blas" else lt(_lt_index(c))()
 
 
@@ -333,17 +318,17 @@ def gemm_nt_rope(k, x: torch.Tensor, w: torch.Tensor, bias, pos, tab, rot_heads:
             return y
         return run
 
-    def ours():
-        return k.gemm_nt(x, w, bias, pos, tab, rot_heads, hd)
+    def ours(variant: int = 0):
+        return k.gemm_nt(x, w, bias, pos, tab, rot_heads, hd, variant=variant)
     if m == "blas":
         return blas()
     if m == "lt":
         return lt(0)() if lt_ok and _lt_count(k, 0, M, N, K, bias is not None) else blas()
     key = ("nt_rope", M, N, K, hd, x.device.index)
-    c = _pick(key, {**_ours_variants(k, "nt", ours), **({"blas": blas} if _lib() else {})},
+    c = _pick(key, {**_ours_variants(ours), **({"blas": blas} if _lib() else {})},
               lambda: _lt_count(k, 0, M, N, K, bias is not None), lt if lt_ok else None)
     if c.startswith("ours") or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
-        return _run_ours(k, "nt", c, ours)
+        return _run_ours(ours, c)
     return blas() if c == "blas" else lt(_lt_index(c))()
 
 
@@ -404,10 +389,8 @@ def gemm_tn(k, a: torch.Tensor, b: torch.Tensor, out=None, accumulate: bool = Fa
                 dst, acc = torch.empty(M, N, device=a.device, dtype=torch.float32), False
             k.lt_run(2, a, b, dst, None, _lt_index(kind), acc)
             return dst
-        if kind == "ours3" or kind == "ours":
-            fn = (lambda: k.gemm_tn(a, b, dst, acc)) if dst is not None else (lambda: k.gemm_tn(a, b))
-            return _run_ours(k, "tn", kind, fn)
-        return k.gemm_tn(a, b, dst, acc) if dst is not None else k.gemm_tn(a, b)
+        v = _VARIANT.get(kind, 0)
+        return k.gemm_tn(a, b, dst, acc, variant=v) if dst is not None else k.gemm_tn(a, b, variant=v)
     m = mode()
     if m == "ours" or a.shape[0] < _MIN_ROWS:
         return run("ours", out, accumulate)
@@ -422,8 +405,6 @@ def gemm_tn(k, a: torch.Tensor, b: torch.Tensor, out=None, accumulate: bool = Fa
     if c is None:
         scratch = torch.zeros(M, N, device=a.device, dtype=torch.float32)
         cands = {"ours": lambda: run("ours", scratch, accumulate)}
-        if hasattr(k, "gemm_v4_mask"):
-            cands["ours3"] = lambda: run("ours3", scratch, accumulate)
         if blas_ok and _lib():
             cands["blas"] = lambda: run("blas", scratch, accumulate)
         c = _pick(key, cands, lambda: _lt_count(k, 2, M, N, K, False),

@@ -189,7 +189,7 @@ def test_cross_entropy_kernels(C, V, valid, start):
 
 
 @pytest.mark.parametrize("B,T,H,hd", [(2, 256, 4, 64), (1, 300, 2, 64), (2, 130, 3, 128), (1, 64, 2, 32),
-                                      (1, 1000, 2, 64)])
+                                      (1, 1000, 2, 64), (1, 1000, 2, 128), (2, 384, 2, 128)])
 @pytest.mark.parametrize("impl", [2, 3, 1, 4])
 def test_attention(C, B, T, H, hd, impl):
     C.attn_set_impl(impl)            # forward variants
@@ -721,18 +721,13 @@ def test_gemm_v4_bitwise_equals_v3(C, M, N, K, sched, bn):
     bt = torch.randn(N, K, device=DEV).bfloat16()
     b_nn = torch.randn(K, N, device=DEV).bfloat16()
     bias = torch.randn(N, device=DEV)
-    old = C.gemm_v4_get_mask()
+    v = {0: 0, 256: 1, 192: 2}[bn]      # per-call variant: v4 at its own / a forced tile width
     try:
-        C.gemm_v4_mask(7)
         C.gemm4_sched(sched)
-        C.gemm4_bn(bn)
-        nt4, nn4 = C.gemm_nt(a, bt, bias), C.gemm_nn(a, b_nn)
-        C.gemm_v4_mask(0)
-        nt3, nn3 = C.gemm_nt(a, bt, bias), C.gemm_nn(a, b_nn)
+        nt4, nn4 = C.gemm_nt(a, bt, bias, variant=v), C.gemm_nn(a, b_nn, variant=v)
+        nt3, nn3 = C.gemm_nt(a, bt, bias, variant=3), C.gemm_nn(a, b_nn, variant=3)
     finally:
-        C.gemm_v4_mask(old)
         C.gemm4_sched(0)
-        C.gemm4_bn(0)
     assert _rel(nt4, R.gemm_nt(a.float(), bt.float(), bias)) < 1e-2
     assert torch.equal(nt4, nt3)
     assert torch.equal(nn4, nn3)
@@ -745,19 +740,17 @@ def test_gemm_v4_tn(C, M, N, K, splits):
     torch.manual_seed(27)
     a = torch.randn(K, M, device=DEV).bfloat16()
     b = torch.randn(K, N, device=DEV).bfloat16()
-    old = C.gemm_v4_get_mask()
     try:
-        C.gemm_v4_mask(7)
         C.gemm_force(-1, splits)
-        out = C.gemm_tn(a, b)
+        out = C.gemm_tn(a, b)                       # variant 0: v4 (the default for every layout)
         ref = R.gemm_tn(a.float(), b.float())
         assert _rel(out, ref) < 1e-5
+        assert torch.equal(out, C.gemm_tn(a, b, variant=3)) or _rel(C.gemm_tn(a, b, variant=3), ref) < 1e-5
         acc = torch.randn(M, N, device=DEV)
         want = acc + ref
         C.gemm_tn(a, b, acc, True)
         assert _rel(acc, want) < 1e-5
     finally:
-        C.gemm_v4_mask(old)
         C.gemm_force(-1, 0)
 
 
@@ -768,12 +761,7 @@ def test_gemm_v4_split_k_bf16_long_k(C):
     M, N, K = 2048, 768, 50304
     a = (torch.randn(M, K, device=DEV) / 16).bfloat16()
     b = (torch.randn(K, N, device=DEV) / 16).bfloat16()
-    old = C.gemm_v4_get_mask()
-    try:
-        C.gemm_v4_mask(7)
-        out = C.gemm_nn(a, b)
-    finally:
-        C.gemm_v4_mask(old)
+    out = C.gemm_nn(a, b)
     assert _rel(out, R.gemm_nn(a.float(), b.float())) < 1e-2
 
 

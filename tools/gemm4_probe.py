@@ -24,7 +24,13 @@ SHAPES = {
     "tn": [("qkv", 2304, 768, T), ("wo", 768, 768, T), ("gateup", 4096, 768, T), ("down", 768, 2048, T),
            ("lmhead", 50304, 768, T)],
 }
-BIT = {"nt": 1, "nn": 2, "tn": 4}
+# per-call kernel variant of the next `ours` call (0 = v4 at its own width, 1 / 2 = v4 256 / 192
+# wide, 3 = v3): an argument of the kernel entry points, set here per arm
+VAR = [0]
+
+
+def set_variant(mask_or_v4: int, bn: int = 0):
+    VAR[0] = 3 if not mask_or_v4 else {0: 0, 256: 1, 192: 2}[bn]
 
 
 def operands(layout, M, N, K, gen, bias=False):
@@ -33,13 +39,13 @@ def operands(layout, M, N, K, gen, bias=False):
         a, b = r(M, K), r(N, K)
         bv = torch.randn(N, device="cuda", generator=gen) if bias else None
         bb = bv.bfloat16() if bias else None
-        return a, b, (lambda C: C.gemm_nt(a, b, bv)), (lambda: torch.nn.functional.linear(a, b, bb)), \
+        return a, b, (lambda C: C.gemm_nt(a, b, bv, variant=VAR[0])), (lambda: torch.nn.functional.linear(a, b, bb)), \
             (lambda: a.float() @ b.float().t() + (bv if bias else 0))
     if layout == "nn":
         a, b = r(M, K), r(K, N)
-        return a, b, (lambda C: C.gemm_nn(a, b)), (lambda: torch.matmul(a, b)), (lambda: a.float() @ b.float())
+        return a, b, (lambda C: C.gemm_nn(a, b, variant=VAR[0])), (lambda: torch.matmul(a, b)), (lambda: a.float() @ b.float())
     a, b = r(K, M), r(K, N)
-    return a, b, (lambda C: C.gemm_tn(a, b)), (lambda: torch.mm(a.t(), b, out_dtype=torch.float32)), \
+    return a, b, (lambda C: C.gemm_tn(a, b, variant=0 if VAR[0] != 3 else 3)), (lambda: torch.mm(a.t(), b, out_dtype=torch.float32)), \
         (lambda: a.float().t() @ b.float())
 
 
@@ -86,14 +92,12 @@ def main():
             res = {}
             for tag, mask, sc, bn in [(f"v4s{sc}", 7, sc, 0) for sc in a.scheds] + \
                     [(f"bn{b}", 7, a.scheds[-1], b) for b in a.bn] + [("v3", 0, 0, 0)]:
-                C.gemm_v4_mask(mask)
+                set_variant(mask, bn)
                 C.gemm4_sched(sc)
-                C.gemm4_bn(bn)
                 if want is not None:
                     out = ours(C).float()
                     res[tag] = ((out - want).norm() / want.norm()).item()
-                C.gemm4_bn(0)
-            C.gemm_v4_mask(3)
+            set_variant(1)
             del want
             flops = 2.0 * M * N * K
             print(f"{layout} {name} {M}x{N}x{K}: rel err " + " ".join(f"{k} {v:.2e}" for k, v in res.items()),
@@ -103,7 +107,7 @@ def main():
             for dmode in ((16, 32) if a.diag and layout == "nt" else ()):
                 d = torch.zeros(256 * 4 * 4, dtype=torch.int64, device="cuda")
                 C.gemm4_diag(d)
-                C.gemm_v4_mask(7)
+                set_variant(1)
                 C.gemm4_ablate(dmode)
                 ours(C)
                 torch.cuda.synchronize()
@@ -129,39 +133,39 @@ def main():
             for _ in range(a.rounds):
                 for k in arms:
                     if k.startswith("v4s"):
-                        C.gemm_v4_mask(7)
+                        set_variant(1)
                         C.gemm4_sched(int(k[3:]))
                         ts[k].append(timed(lambda: ours(C), a.iters))
                     elif k.startswith("sp"):
-                        C.gemm_v4_mask(7)
+                        set_variant(1)
                         C.gemm4_sched(a.scheds[-1])
                         C.gemm_force(-1, int(k[2:]))
                         ts[k].append(timed(lambda: ours(C), a.iters))
                         C.gemm_force(-1, 0)
                     elif k.startswith("bn"):
-                        C.gemm_v4_mask(7)
+                        set_variant(1)
                         C.gemm4_sched(a.scheds[-1])
-                        C.gemm4_bn(int(k[2:]))
+                        set_variant(1, int(k[2:]))
                         ts[k].append(timed(lambda: ours(C), a.iters))
-                        C.gemm4_bn(0)
+                        set_variant(1)
                     elif k.startswith("gm"):
-                        C.gemm_v4_mask(7)
+                        set_variant(1)
                         C.gemm4_sched(a.scheds[-1])
                         C.gemm4_group_m(int(k[2:]))
                         ts[k].append(timed(lambda: ours(C), a.iters))
                         C.gemm4_group_m(4)
                     elif k.startswith("abl"):
-                        C.gemm_v4_mask(7)
+                        set_variant(1)
                         C.gemm4_sched(a.scheds[-1])
                         C.gemm4_ablate(int(k[3:]))
                         ts[k].append(timed(lambda: ours(C), a.iters))
                         C.gemm4_ablate(0)
                     elif k == "v3":
-                        C.gemm_v4_mask(0)
+                        set_variant(0)
                         ts[k].append(timed(lambda: ours(C), a.iters))
                     else:
                         ts[k].append(timed(blas, a.iters))
-            C.gemm_v4_mask(3)
+            set_variant(1)
             C.gemm4_sched(a.scheds[-1])
             line = "   ".join(f"{k} {statistics.median(v):.4f} ms (min {min(v):.4f}) "
                                f"{flops / statistics.median(v) / 1e9:.0f} TF" for k, v in ts.items())

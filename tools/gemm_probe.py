@@ -23,20 +23,20 @@ def main():
     ap.add_argument("--sched", type=int, nargs="+", default=[-1])
     ap.add_argument("--cfg", type=int, nargs="+", default=[-1])
     ap.add_argument("--blas", action="store_true", help="also time hipBLASLt (torch) on the same layout")
-    ap.add_argument("--v4", type=int, default=None, help="v4 layout mask (gemm_v4_mask) for impl 3")
+    ap.add_argument("--v4", type=int, default=None, help="kernel variant for impl 3 (0 v4, 1 / 2 v4 256 / 192 wide, 3 v3)")
     ap.add_argument("--sched4", type=int, default=None, help="v4 schedule (gemm4_sched)")
     ap.add_argument("--check", action="store_true", help="relative error of each implementation vs fp32 torch")
     a = ap.parse_args()
     C = _ext.require()
-    if a.v4 is not None:
-        C.gemm_v4_mask(a.v4)
+    var = a.v4 or 0
     if a.sched4 is not None:
         C.gemm4_sched(a.sched4)
     M, N, K = a.M, a.N, a.K
     x = torch.randn(M, K, device="cuda").bfloat16()
     w = torch.randn(N, K, device="cuda").bfloat16()
     dy = torch.randn(M, N, device="cuda").bfloat16()
-    fn = {"nt": lambda: C.gemm_nt(x, w, None), "nn": lambda: C.gemm_nn(dy, w), "tn": lambda: C.gemm_tn(dy, x)}[a.layout]
+    fn = {"nt": lambda: C.gemm_nt(x, w, None, variant=var), "nn": lambda: C.gemm_nn(dy, w, variant=var),
+          "tn": lambda: C.gemm_tn(dy, x, variant=0 if var != 3 else 3)}[a.layout]
     ref = {"nt": lambda: x.float() @ w.float().t(), "nn": lambda: dy.float() @ w.float(),
            "tn": lambda: dy.float().t() @ x.float()}[a.layout]() if a.check else None
     for impl, sched, cfg in [(i, sc, cf) for i in a.impl for sc in (a.sched if i >= 2 else [0]) for cf in a.cfg]:
