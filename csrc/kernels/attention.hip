@@ -2255,7 +2255,7 @@ using namespace dpfs;
 
 extern "C" int dpfs_attn_supported_hd(int hd) { return hd == 32 || hd == 64 || hd == 128; }
 
-// Forward implementation: 0 = auto (default: attn_fwd3_k at head_dim 64, attn_fwd_k otherwise),
+// Forward implementation: 0 = auto (default: attn_fwd3_k at head_dim 64 / 128, attn_fwd_k otherwise),
 // 1 = attn_fwd_k (16x16x32, register-staged), 2 / 3 = attn_fwd2_k (LDS-DMA ring, 8 / 4 waves),
 // 4 = attn_fwd3_k (32x32x16, LDS-DMA ring, hd 64 / 128), 5 = its DIAG build (hd 64).
 static int g_attn_impl = 0;
@@ -2276,9 +2276,9 @@ static unsigned long long* g_attn_diag = nullptr;
 static int g_attn_fwd_persist = 0;
 extern "C" void dpfs_attn_fwd_persist(int v) { g_attn_fwd_persist = v; }   // impl 5: attn_fwd3_k DIAG build, [grid][4 waves][4]
 extern "C" void dpfs_attn_diag(void* p) { g_attn_diag = (unsigned long long*)p; }
-// dK/dV kernel: 0 = auto (default: 4 at head_dim 64, 2 otherwise), 1 = register-staged,
+// dK/dV kernel: 0 = auto (default: 4 at head_dim 64 / 128, 2 otherwise), 1 = register-staged,
 // 2 = LDS-DMA ring (16x16x32), 3 = register-staged with 32 keys per wave (hd <= 64),
-// 4 = attn_bwd_dkdv3_k (32x32x16, key on the lane, hd 64)
+// 4 = attn_bwd_dq3_k + attn_bwd_dkdv3_k (32x32x16, query / key on the lane, hd 64 / 128)
 static int g_attn_bwd_impl = 0;
 
 extern "C" void dpfs_attn_set_bwd_impl(int v) { g_attn_bwd_impl = v; }
@@ -2286,7 +2286,7 @@ extern "C" void dpfs_attn_set_bwd_impl(int v) { g_attn_bwd_impl = v; }
 extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int T, int H,
                               int hd, long long ldq, long long ldk, long long ldv, long long ldo, float scale,
                               int causal, hipStream_t s) {
-  const int impl = g_attn_impl == 0 ? (hd == 64 ? 4 : 1) : g_attn_impl;
+  const int impl = g_attn_impl == 0 ? ((hd == 64 || hd == 128) ? 4 : 1) : g_attn_impl;
   if (impl == 2) {
     dim3 g8((T + 255) / 256, B * H);
     DPFS_HD_DISPATCH(hd, attn_fwd2_k<HD_, 8><<<g8, 512, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
@@ -2331,7 +2331,7 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
   // The QKV bias gradient rides on the default kernel pair (dQ + LDS-DMA dK/dV); with another
   // dK/dV variant the caller computes it with a separate column sum.
   const bool v3ok = hd == 64 || hd == 128;
-  const int bimpl = g_attn_bwd_impl == 0 ? (hd == 64 ? 4 : 2) : g_attn_bwd_impl;
+  const int bimpl = g_attn_bwd_impl == 0 ? (v3ok ? 4 : 2) : g_attn_bwd_impl;
   const bool bias = dbias != nullptr && bws != nullptr && (bimpl == 2 || (bimpl == 4 && v3ok));
   const int nqb = (T + 127) / 128, nkb = (T + 63) / 64;
   float* pq = bias ? bws : nullptr;

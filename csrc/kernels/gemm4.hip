@@ -724,19 +724,10 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   // One consumer step on `cur`, prefetching the next step's fragments into `nxt`.
   // Entry wait: stage s+1 landed for this wave (younger: stage s+2 = NQ pieces, plus the
   // previous item's epilogue stores on an item's first step), then the step barrier.
-  // SCHED 2 (PAIR): a barrier every OTHER step.  Even steps (cur = F0) wait for the two stages
-  // the next two steps read (both issued two steps earlier), pass the barrier and issue the
-  // DMA of two stages (s + 3 into slot s - 1, s + 4 into slot s: the slots whose fragments every
-  // wave retired before this barrier); odd steps neither wait, sync nor issue.  Same prefetch
-  // distance, half the barriers (one per 64 of K, hipBLASLt's MT...x64).  Items have an even
-  // step count, so an item always starts on an even step.
-  constexpr bool PAIR = SCHED == 2;
   auto step = [&](Frags<AK, BKM, BN>& cur, Frags<AK, BKM, BN>& nxt, bool first, auto zero, auto nopf, bool last,
-                  int bcol0, auto odd) {
+                  int bcol0) {
     constexpr bool ZR = decltype(zero)::value;
     constexpr bool NOPF = decltype(nopf)::value;   // no next-step fragment reads (item end, SWB)
-    constexpr bool ODD = decltype(odd)::value;
-    constexpr bool SYNC = !PAIR || !ODD;            // this step waits, syncs and issues DMA
     if constexpr (DIAG) {
       const unsigned long long t = stamp();
       t_body += t - t_mark;
@@ -746,15 +737,10 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
     cur.a.pin();
     cur.b.pin();
-    if constexpr (SYNC) {
-      if (dbg & 4) wait_vmcnt<63>();   // timing-only: no wait for the DMA (wrong results)
-      else if constexpr (PAIR) {
-        if (first) wait_vmcnt<(STORES < 63 ? STORES : 63)>();
-        else wait_vmcnt<0>();
-      } else if (first) wait_vmcnt<(NQ + STORES < 63 ? NQ + STORES : 63)>();
-      else wait_vmcnt<NQ>();
-      if (!(dbg & 8)) __builtin_amdgcn_s_barrier();
-    }
+    if (dbg & 4) wait_vmcnt<63>();   // timing-only: no wait for the DMA (wrong results)
+    else if (first) wait_vmcnt<(NQ + STORES < 63 ? NQ + STORES : 63)>();
+    else wait_vmcnt<NQ>();
+    if (!(dbg & 8)) __builtin_amdgcn_s_barrier();
     if constexpr (DIAG) {
       const unsigned long long t = stamp();
       t_wait += t - t_mark;
@@ -786,8 +772,8 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
         acc_mfma<q, j, ZR>(cur.b.get(j), cur.a.get(q));
         __builtin_amdgcn_sched_barrier(0);
         // this step's stage descriptors (scalar work) in the shadow of the first MFMAs
-        if constexpr (SYNC && (q == 0 || (PAIR && q == 4)) && j == 0) stage_rsrc_a();
-        if constexpr (SYNC && (q == 0 || (PAIR && q == 4)) && j == 1) stage_rsrc_b();
+        if constexpr (q == 0 && j == 0) stage_rsrc_a();
+        if constexpr (q == 0 && j == 1) stage_rsrc_b();
         if constexpr (q < 4 && !NOPF) {
           // read slots after MFMA 0 / 2 / 4 / 6 (NJ 8) or 0 / 2 / 3 / 5 (NJ 6)
           constexpr int r0 = 0, r1 = 2, r2 = NJ == 8 ? 4 : 3, r3 = NJ == 8 ? 6 : 5;
@@ -797,13 +783,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
           if constexpr (j == r3 && 2 * q + 1 < NJ)
             nxt.b.load(2 * q + 1, src + 16384, wn * (BN / 2) + 32 * q + 16, l);
         }
-        if constexpr (PAIR) {
-          // rows 0-3: the first stage's pieces, two per row; rows 4-7: the second stage's
-          constexpr int d1 = NJ == 8 ? 7 : 5;
-          constexpr int pq = 2 * (q & 3) + (j == 3 ? 0 : 1);
-          if constexpr (SYNC && (j == 3 || j == d1) && pq < NQ) issue(pq);
-          if constexpr (SYNC && q == 3 && j == NJ - 1) advance();   // the second stage's pieces follow
-        } else if constexpr (SCHED == 1) {
+        if constexpr (SCHED == 1) {
           if constexpr (j == 3 && q < NQ) issue(q);
         } else if constexpr (q >= 4) {
           constexpr int d0 = 1, d1 = NJ == 8 ? 5 : 4;
@@ -813,43 +793,41 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
         __builtin_amdgcn_sched_barrier(0);
       });
     });
-    if constexpr (SYNC) advance();
+    advance();
   };
 
   for (bool first = true; it < total; it += G, first = false) {
     const Item ci = decode<BN>(it, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
     const int nk = nsteps(ci);
     const int bcol0 = ci.n0 + wn * (BN / 2);
-    constexpr std::false_type NO{}, EVEN{};
-    constexpr std::true_type ODDS{};
+    constexpr std::false_type NO{};
     if constexpr (SWB) {
       // The register-hungry SwiGLU-backward epilogue: the item's last step reads no fragments
       // (F0 / F1 are dead across the epilogue); the next item's first-step fragments are read
       // after it from the slot that step would have read (landed at its entry wait, rewritten
       // only by a DMA issued behind the next step's barrier).
-      step(F0, F1, !first, std::true_type{}, NO, false, bcol0, EVEN);
+      step(F0, F1, !first, std::true_type{}, NO, false, bcol0);
       for (int t = 1; t < nk - 1; t += 2) {
-        step(F1, F0, false, NO, NO, false, bcol0, ODDS);
-        step(F0, F1, false, NO, NO, false, bcol0, EVEN);
+        step(F1, F0, false, NO, NO, false, bcol0);
+        step(F0, F1, false, NO, NO, false, bcol0);
       }
-      step(F1, F0, false, NO, std::true_type{}, true, bcol0, ODDS);
+      step(F1, F0, false, NO, std::true_type{}, true, bcol0);
       epilogue_swb(ci, M, N, swb, wm, wn, l);
       read_frags<AK, BKM, BN>(F0, smem + c_slot * SLOT, wm, wn, l);
       continue;
     }
-    step(F0, F1, !first, std::true_type{}, NO, false, bcol0, EVEN);
-    step(F1, F0, false, NO, NO, nk == 2, bcol0, ODDS);
+    step(F0, F1, !first, std::true_type{}, NO, false, bcol0);
+    step(F1, F0, false, NO, NO, nk == 2, bcol0);
     for (int t = 2; t < nk; t += 2) {
-      step(F0, F1, false, NO, NO, false, bcol0, EVEN);
-      step(F1, F0, false, NO, NO, t + 2 >= nk, bcol0, ODDS);
+      step(F0, F1, false, NO, NO, false, bcol0);
+      step(F1, F0, false, NO, NO, t + 2 >= nk, bcol0);
     }
     if constexpr (DIAG) {
       const unsigned long long t = stamp();
       t_body += t - t_mark;
       t_mark = t;
     }
-    // this wave's bias DMA landed (NQ younger ring pieces; none under PAIR: the last step is odd)
-    if (OUT == 0 && bias) wait_vmcnt<(PAIR ? 0 : NQ)>();
+    if (OUT == 0 && bias) wait_vmcnt<NQ>();   // this wave's bias DMA landed (NQ younger ring pieces)
     if (OUT == 0 && bias)
       epilogue<OUT, BN, ROPE, true, SWIGLU>(bias_lds, ci, C, rope, M, N, ldc, slab_stride, c_bytes, wm, wn, l, swo);
     else
@@ -901,8 +879,7 @@ static unsigned long long* g_g4_diag = nullptr;   // [grid][4 waves][wait, body,
 extern "C" void dpfs_gemm4_ablate(int v) { g_g4_ablate = v; }
 extern "C" void dpfs_gemm4_diag(void* p) { g_g4_diag = (unsigned long long*)p; }
 // Main-loop variant (tools/gemm4_probe.py A/B): 0 = one DMA piece per MFMA row (default),
-// 1 = two pieces per row in rows 4-7; 2 = per-lane K checks even where FAST applies; 3 = PAIR
-// (a barrier every other 32-deep step, two stages' DMA per barrier: SCHED 2).
+// 1 = two pieces per row in rows 4-7; 2 = per-lane K checks even where FAST applies.
 static int g_g4_sched = 0;
 extern "C" void dpfs_gemm4_sched(int v) { g_g4_sched = v; }
 extern "C" void dpfs_gemm4_group_m(int g) { g_g4_group_m = g > 0 ? g : 4; }
@@ -1001,7 +978,7 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
   }
   // FAST (descriptor-advancing DMA stream): every item's K range a multiple of 64
   const bool fast = g_g4_sched != 2 && K % 64 == 0 && kps % 64 == 0 && (!A2 || k_switch % 64 == 0);
-  const int sched = g_g4_sched == 1 ? 0 : (g_g4_sched == 3 ? 2 : 1);
+  const int sched = g_g4_sched == 1 ? 0 : 1;
 #define DPFS_G4_ARGS                                                                                            \
   (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb, \
       rope, g_g4_group_m, dual, g_g4_ablate & ~3, nullptr
@@ -1020,12 +997,7 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
         break;                                                                                    \
       }                                                                                           \
     }                                                                                             \
-    if (fast && sched == 2) {                                                                     \
-      if (OUT_ == 0 && bn == 192)                                                                 \
-        gemm4_k<AK_, BK_, OUT_, 0, true, 2, (OUT_ == 0 ? 192 : 256)><<<grid, 256, 0, s>>>(DPFS_G4_ARGS); \
-      else                                                                                        \
-        gemm4_k<AK_, BK_, OUT_, 0, true, 2><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);                   \
-    } else if (fast && sched == 1) {                                                              \
+    if (fast && sched == 1) {                                                                     \
       if (OUT_ == 0 && bn == 192)                                                                 \
         gemm4_k<AK_, BK_, OUT_, 0, true, 1, (OUT_ == 0 ? 192 : 256)><<<grid, 256, 0, s>>>(DPFS_G4_ARGS); \
       else                                                                                        \
@@ -1045,12 +1017,6 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
     gemm4_k<true, true, 0, 2, true, 1><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda,
                                                             ldb, ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb,
                                                             rope, g_g4_group_m, dual, g_g4_ablate & ~51, g_g4_diag);
-    return true;
-  }
-  if ((g_g4_ablate & 16) && g_g4_diag && layout == 0 && !out_f32 && bn == 256 && fast && sched == 2) {
-    gemm4_k<true, true, 0, 1, true, 2><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda,
-                                                            ldb, ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb,
-                                                            rope, g_g4_group_m, dual, g_g4_ablate & ~19, g_g4_diag);
     return true;
   }
   if ((g_g4_ablate & 16) && g_g4_diag && layout == 0 && !out_f32 && bn == 256 && fast) {
