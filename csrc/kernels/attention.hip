@@ -1515,13 +1515,17 @@ struct QdoDma3 {
   }
 };
 
-template <int HD>
+// DIAG = 1: per-wave s_memtime split into diag[block][wave][10]: wait + barrier / S, dP + first
+// exp half / second exp half + mask + dS + packs / dO^T reads + dV^T / Q^T reads + dK^T /
+// epilogues / prologues (K, V to registers) / tiles computed / start / end (timing build only:
+// each stamp waits for the value it depends on).
+template <int HD, int DIAG = 0>
 __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
     const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V, const bf16* __restrict__ dO,
     const float* __restrict__ LSN, const float* __restrict__ NDEL, bf16* __restrict__ dK, bf16* __restrict__ dV,
     int T, int H, int BH, long long ldq, long long ldk, long long ldv, long long lddo, long long lddk,
     long long lddv, float scale, int causal, const int64_t* __restrict__ rpos, const float* __restrict__ rtab,
-    float* __restrict__ BPK, float* __restrict__ BPV) {
+    float* __restrict__ BPK, float* __restrict__ BPV, unsigned long long* __restrict__ diag = nullptr) {
   // LSN = -lse log2(e) and NDEL = -delta per query row (written by attn_bwd_dq3_k).  BPK / BPV
   // (optional): per (b, h, key block, wave) column sums of the stored dK / dV rows.
   static_assert(HD == 64 || HD == 128, "dK/dV v3: head_dim 64 or 128");
@@ -1558,9 +1562,12 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
       toff[dt][e] = row * RB + (swz_u<HD>(row, col >> 3) << 4) + (col & 7) * 2;
     }
 
+  unsigned long long d_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, d_t0 = 0, d_start = 0;
+  if constexpr (DIAG) d_start = stamp_dep(0.f);
   for (int sub = 0; sub < 2; ++sub) {
     const int kb = sub == 0 ? p : nkb - 1 - p;
     if (sub == 1 && kb == p) break;
+    if constexpr (DIAG) d_t0 = stamp_dep(0.f);
     if (sub == 1) __syncthreads();   // the previous key block's ring slots are read
     const int k0 = kb * BK, kw0 = k0 + 32 * wave, key = kw0 + r32;
     const int qstart = causal ? (k0 / BQ) * BQ : 0;
@@ -1580,6 +1587,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
       vf[ks] = c;
     }
     wait_vmcnt<0>();
+    if constexpr (DIAG) d_acc[6] += stamp_dep(__builtin_bit_cast(float, __builtin_bit_cast(u32x4, vf[KS - 1])[3])) - d_t0;
     f32x16 dkt[DTN], dvt[DTN];
 #pragma unroll
     for (int d = 0; d < DTN; ++d)
@@ -1590,9 +1598,15 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
       }
     int cur = 0;
     for (int t = 0; t < nq; ++t) {
+      if constexpr (DIAG) d_t0 = stamp_dep(0.f);
       if (t + 1 < nq) wait_vmcnt<PWV>();
       else wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
+      if constexpr (DIAG) {
+        const unsigned long long t1 = stamp_dep(0.f);
+        d_acc[0] += t1 - d_t0;
+        d_t0 = t1;
+      }
       const char* lq = smem + cur * BUF;
       const char* ldo_ = lq + TILE;
       const float* ls = reinterpret_cast<const float*>(lq + 2 * TILE);
@@ -1603,6 +1617,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
       const int q0 = qstart + t * BQ;
       if (t + 2 < nq) dma.issue(qbase, dobase, lsb, dlb, ldq, lddo, T, q0 + 2 * BQ, smem + nb * BUF);
       if (causal && q0 + BQ - 1 < kw0) continue;   // wave-uniform: every query of the tile < every key
+      if constexpr (DIAG) d_acc[7] += 1;
       // S = Q K^T, dP = dO V^T (rows = queries 32 qt + 8 (i>>2) + 4 hf + (i&3), lane = key).
       // p = exp2(c2 S - lse log2 e) of query tile 0 is computed under tile 1's MFMAs (four
       // elements after each pair), tile 1's after them; the row constants per register come
@@ -1637,6 +1652,11 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
         for (int i = (16 / KS) * ks; i < (16 / KS) * (ks + 1); ++i)
           sc[0][i] = __builtin_amdgcn_exp2f(fmaf(sc[0][i], c2, lsr[0][i >> 2][i & 3]));
         __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (DIAG) {
+        const unsigned long long t1 = stamp_dep(sc[0][15] + dp[1][15]);
+        d_acc[1] += t1 - d_t0;
+        d_t0 = t1;
       }
       // dO^T fragments (A of dV^T: lane d = 32 dt + r32, queries 16 s + 4 hf + 0..3 / 8..11)
       constexpr int NH = 2 * DTN * 4;
@@ -1680,6 +1700,11 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
             pd[2 * qt + s1][j] = (bf16)pr.x;
             pd[2 * qt + s1][j + 1] = (bf16)pr.y;
           }
+      if constexpr (DIAG) {
+        const unsigned long long t1 = stamp_dep(__builtin_bit_cast(float, __builtin_bit_cast(u32x4, pd[3])[3]));
+        d_acc[2] += t1 - d_t0;
+        d_t0 = t1;
+      }
 #pragma unroll
       for (int w = 0; w < (NH + 15) / 16; ++w) tr_wait8(*reinterpret_cast<s16x4(*)[16]>(&th[16 * w]));
 #pragma unroll
@@ -1687,6 +1712,11 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4)
           dvt[dt] = MFMA32(tr_join(th[2 * (dt * 4 + s4)], th[2 * (dt * 4 + s4) + 1]), pp[s4], dvt[dt]);
+      if constexpr (DIAG) {
+        const unsigned long long t1 = stamp_dep(dvt[DTN - 1][15]);
+        d_acc[3] += t1 - d_t0;
+        d_t0 = t1;
+      }
       // Q^T fragments (A of dK^T), read after the dV^T MFMAs are issued
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1703,7 +1733,9 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4)
           dkt[dt] = MFMA32(tr_join(th[2 * (dt * 4 + s4)], th[2 * (dt * 4 + s4) + 1]), pd[s4], dkt[dt]);
+      if constexpr (DIAG) d_acc[4] += stamp_dep(dkt[DTN - 1][15]) - d_t0;
     }
+    if constexpr (DIAG) d_t0 = stamp_dep(0.f);
     // epilogue: lane = key, registers = d rows 32 dt + 8 g + 4 hf + j.  dK *= scale, inverse
     // RoPE (d pairs with d + HD/2: tile dt with dt + DTN/2, same register), 8-byte stores.
 #pragma unroll
@@ -1760,6 +1792,16 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
             BPV[row * HD + d] = c;
           }
         }
+    }
+    if constexpr (DIAG) d_acc[5] += stamp_dep(0.f) - d_t0;
+  }
+  if constexpr (DIAG) {
+    if (l == 0) {
+      unsigned long long* dp = diag + ((long long)blockIdx.x * 4 + wave) * 10;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dp[i] = d_acc[i];
+      dp[8] = d_start;
+      dp[9] = stamp_dep(0.f);
     }
   }
 }
@@ -2280,6 +2322,9 @@ extern "C" void dpfs_attn_diag(void* p) { g_attn_diag = (unsigned long long*)p; 
 // 2 = LDS-DMA ring (16x16x32), 3 = register-staged with 32 keys per wave (hd <= 64),
 // 4 = attn_bwd_dq3_k + attn_bwd_dkdv3_k (32x32x16, query / key on the lane, hd 64 / 128)
 static int g_attn_bwd_impl = 0;
+// 1: the dK/dV v3 kernel runs its DIAG build (hd 64) into the attn_diag buffer
+static int g_attn_bwd_diag = 0;
+extern "C" void dpfs_attn_bwd_diag(int v) { g_attn_bwd_diag = v; }
 
 extern "C" void dpfs_attn_set_bwd_impl(int v) { g_attn_bwd_impl = v; }
 
@@ -2361,7 +2406,12 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
                                               delta + (long long)B * H * T, delta, (bf16*)dk, (bf16*)dv, T, H,     \
                                               B * H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal, rope_pos,     \
                                               rope_tab, pk, pv)
-    if (hd == 64) DPFS_DKDV3(64);
+    if (hd == 64 && g_attn_bwd_diag && g_attn_diag)
+      attn_bwd_dkdv3_k<64, 1><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,
+                                                     delta + (long long)B * H * T, delta, (bf16*)dk, (bf16*)dv, T, H,
+                                                     B * H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal, rope_pos,
+                                                     rope_tab, pk, pv, g_attn_diag);
+    else if (hd == 64) DPFS_DKDV3(64);
     else DPFS_DKDV3(128);
 #undef DPFS_DKDV3
     if (bias) {

@@ -27,6 +27,14 @@ def _load():
         _C = importlib.import_module("distributed_pytorch_from_scratch_amd." + name)
     except Exception as e:  # pragma: no cover - depends on build state
         _ERR = e
+        return
+    # A/B switches of the attention kernel generation, read once at load (same-box comparisons
+    # of whole-model runs; the per-head-dim defaults are the measured winners):
+    # DPFS_ATTN_IMPL (forward, csrc/kernels/attention.hip dpfs_attn_fwd) and
+    # DPFS_ATTN_BWD_IMPL (backward, dpfs_attn_bwd); 0 / unset = the default.
+    for var, fn in (("DPFS_ATTN_IMPL", "attn_set_impl"), ("DPFS_ATTN_BWD_IMPL", "attn_set_bwd_impl")):
+        if os.environ.get(var):
+            getattr(_C, fn)(int(os.environ[var]))
 
 
 def available() -> bool:

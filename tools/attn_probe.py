@@ -95,6 +95,27 @@ def main():
         heavy = w[tot > tot.quantile(0.9)]
         print("DIAG heaviest 10% waves: " + "  ".join(f"{n} {heavy[:, i].mean():.0f}" for i, n in enumerate(names)),
               flush=True)
+    if a.diag and a.bwd:
+        items = (B * H + 7) // 8 * 8 * (((T + 127) // 128 + 1) // 2)
+        d = torch.zeros(items * 4 * 10, dtype=torch.int64, device="cuda")
+        C.attn_diag(d)
+        C.attn_bwd_diag(1)
+        C.attn_set_bwd_impl(4)
+        C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv)
+        torch.cuda.synchronize()
+        C.attn_bwd_diag(0)
+        C.attn_diag(torch.empty(0))
+        w = d.view(-1, 10).double()
+        w = w[w[:, 9] > 0]
+        life = w[:, 9] - w[:, 8]
+        names = ["wait+barrier", "S,dP+exp0", "exp1+mask+dS+pack", "dO^T+dV", "Q^T+dK", "epilogue", "prologue"]
+        nt = w[:, 7]
+        print(f"DIAG dK/dV: {w.shape[0]} waves, wave life mean {life.mean():.0f} ticks, tiles per wave "
+              f"{nt.mean():.2f}, per tile: " + "  ".join(f"{n} {(w[:, i] / nt).mean():.0f}" for i, n in
+                                                        enumerate(names[:5])), flush=True)
+        print("DIAG dK/dV per wave (ticks, share of life): " + "  ".join(
+            f"{n} {w[:, i].mean():.0f} ({(w[:, i] / life).mean() * 100:.1f}%)" for i, n in enumerate(names)),
+            flush=True)
     res = timeit({impl: mk(impl) for impl in a.impl}, iters=a.iters, rounds=5)  # interleaved, median
     for impl, ms in res.items():
         print(f"impl {impl} {'bwd' if a.bwd else 'fwd'}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF", flush=True)
