@@ -1478,6 +1478,51 @@ __device__ __forceinline__ int swz_u(int r, int ch) {
 
 // Q / dO rows [q0, q0 + 64) and the 64 lse / delta values of a query tile into one stage:
 // [Q tile | dO tile | lse (256 B) | delta (256 B) | dummy (512 B)].
+// Epilogue of the v3 backward kernels: a wave's 32 x HD accumulator block (lane = row r32,
+// registers = columns 32 dt + 8 g + 4 hf + j) goes out as whole rows.  Stored per lane, every
+// store instruction touches 32 rows (one 8-byte piece each); staged through the wave's own LDS
+// rows (padded: the 32 rows start 16 bytes apart in the banks) each 16-byte read-back covers
+// HD / 8 lanes of one row, so a store instruction writes 64 / (HD / 8) whole rows.
+template <int HD>
+struct RowStage {
+  static constexpr int EPR = HD * 2 + 16, BYTES = 32 * EPR, CPR = HD / 8;
+  __device__ __forceinline__ static void put(char* ep, const f32x16 (&acc)[HD / 32]) {
+    const int l = lane_id(), r32 = l & 31, hf = l >> 5;
+#pragma unroll
+    for (int dt = 0; dt < HD / 32; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const bf16x4 v = {(bf16)acc[dt][4 * g], (bf16)acc[dt][4 * g + 1], (bf16)acc[dt][4 * g + 2],
+                          (bf16)acc[dt][4 * g + 3]};
+        *reinterpret_cast<bf16x4*>(ep + r32 * EPR + (32 * dt + 8 * g + 4 * hf) * 2) = v;
+      }
+  }
+  static constexpr int NI = 32 * CPR / 64;   // 16-byte pieces per lane
+  // read the wave's rows back, lane l taking pieces 64 i + l (row = piece / CPR): all reads
+  // before any store, so no store's data registers are overwritten while it is in flight
+  __device__ __forceinline__ static void get(const char* ep, u32x4 (&v)[NI]) {
+    const int l = lane_id();
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int idx = 64 * i + l;
+      v[i] = *reinterpret_cast<const u32x4*>(ep + (idx / CPR) * EPR + (idx % CPR) * 16);
+    }
+  }
+  // rows row0 + [0, 32) of the T rows at dst (row stride ld elements), by buffer stores: rows
+  // >= T fall past the descriptor's record count and are dropped (no branches)
+  __device__ __forceinline__ static void put_rows(const u32x4 (&v)[NI], bf16* dst, long long ld, int row0, int T) {
+    const int l = lane_id();
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)dst, (short)0, (int)(((long long)(T - 1) * ld + HD) * 2), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int idx = 64 * i + l, row = row0 + idx / CPR;
+      const unsigned off = row < T ? (unsigned)(((long long)row * ld + (idx % CPR) * 8) * 2) : kOOB;
+      __builtin_amdgcn_raw_buffer_store_b128(v[i], r, off, 0, 0);
+    }
+  }
+};
+
 template <int HD>
 struct QdoDma3 {
   static constexpr int CPR = HD / 8, TILE = 64 * HD * 2, P = 2 * TILE / 1024, PW = P / 4;
@@ -1532,7 +1577,9 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
   constexpr int BK = 128, BQ = 64, KS = HD / 16, DTN = HD / 32, RB = HD * 2;
   constexpr int TILE = BQ * RB, BUF = 2 * TILE + 1024, NST = 3;
   constexpr int PWV = QdoDma3<HD>::PW + 1;   // DMA instructions per wave per tile
-  __shared__ __attribute__((aligned(1024))) char smem[NST * BUF];
+  // the ring, then each wave's epilogue rows (one array: a second LDS object made the compiler
+  // wait for every LDS-DMA in flight before the ring reads)
+  __shared__ __attribute__((aligned(1024))) char smem[NST * BUF + 4 * RowStage<HD>::BYTES];
   const int nkb = (T + BK - 1) / BK;
   const int NP = (nkb + 1) / 2;
   const int it = blockIdx.x;
@@ -1540,6 +1587,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
   if (bh >= BH) return;
   const int b = bh / H, h = bh % H;
   const int wave = threadIdx.x >> 6, l = lane_id(), r32 = l & 31, hf = l >> 5, g16 = l >> 4, i16 = l & 15;
+  char* ep = smem + NST * BUF + wave * RowStage<HD>::BYTES;
   const float c2 = scale * kLog2e;
   const bf16* qbase = Q + (long long)b * T * ldq + (long long)h * HD;
   const bf16* dobase = dO + (long long)b * T * lddo + (long long)h * HD;
@@ -1757,20 +1805,16 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
           }
         }
     }
-    if (key < T) {
-      bf16* krow = dK + ((long long)b * T + key) * lddk + (long long)h * HD;
-      bf16* vrow = dV + ((long long)b * T + key) * lddv + (long long)h * HD;
-#pragma unroll
-      for (int dt = 0; dt < DTN; ++dt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const bf16x4 a = {(bf16)dkt[dt][4 * g], (bf16)dkt[dt][4 * g + 1], (bf16)dkt[dt][4 * g + 2],
-                            (bf16)dkt[dt][4 * g + 3]};
-          const bf16x4 c = {(bf16)dvt[dt][4 * g], (bf16)dvt[dt][4 * g + 1], (bf16)dvt[dt][4 * g + 2],
-                            (bf16)dvt[dt][4 * g + 3]};
-          *reinterpret_cast<bf16x4*>(krow + 32 * dt + 8 * g + 4 * hf) = a;
-          *reinterpret_cast<bf16x4*>(vrow + 32 * dt + 8 * g + 4 * hf) = c;
-        }
+    // whole-row stores through the wave's LDS rows (dK, then dV in the same rows: one wave's
+    // LDS operations run in order)
+    {
+      u32x4 rk[RowStage<HD>::NI], rv[RowStage<HD>::NI];
+      RowStage<HD>::put(ep, dkt);
+      RowStage<HD>::get(ep, rk);
+      RowStage<HD>::put(ep, dvt);
+      RowStage<HD>::get(ep, rv);
+      RowStage<HD>::put_rows(rk, dK + (long long)b * T * lddk + (long long)h * HD, lddk, kw0, T);
+      RowStage<HD>::put_rows(rv, dV + (long long)b * T * lddv + (long long)h * HD, lddv, kw0, T);
     }
     if (BPK) {
       // per-wave column sums over the 32 keys: registers summed across the 32 lanes of each half
@@ -2071,7 +2115,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
   constexpr int BQ = 128, BKV = 64, KS = HD / 16, DTN = HD / 32, RB = HD * 2;
   constexpr int TILE = BKV * RB, STAGE = 2 * TILE, NST = 3;
   constexpr int PW = KvDmaU<HD>::PW;
-  __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
+  __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE + 4 * RowStage<HD>::BYTES];   // ring, epilogue rows
   const int nqb = (T + BQ - 1) / BQ;
   const int NP = (nqb + 1) / 2;
   const int it = blockIdx.x;
@@ -2079,6 +2123,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
   if (bh >= BH) return;
   const int b = bh / H, h = bh % H;
   const int wave = threadIdx.x >> 6, l = lane_id(), r32 = l & 31, hf = l >> 5, g16 = l >> 4, i16 = l & 15;
+  char* ep = smem + NST * STAGE + wave * RowStage<HD>::BYTES;
   const float c2 = scale * kLog2e;
   const bf16* kbase = K + (long long)b * T * ldk + (long long)h * HD;
   const bf16* vbase = V + (long long)b * T * ldv + (long long)h * HD;
@@ -2231,16 +2276,11 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
           }
         }
     }
-    if (qi < T) {
-      bf16* row = dQ + ((long long)b * T + qi) * lddq + (long long)h * HD;
-#pragma unroll
-      for (int dt = 0; dt < DTN; ++dt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const bf16x4 v = {(bf16)dq[dt][4 * g], (bf16)dq[dt][4 * g + 1], (bf16)dq[dt][4 * g + 2],
-                            (bf16)dq[dt][4 * g + 3]};
-          *reinterpret_cast<bf16x4*>(row + 32 * dt + 8 * g + 4 * hf) = v;
-        }
+    {   // whole-row stores through the wave's LDS rows
+      u32x4 rq[RowStage<HD>::NI];
+      RowStage<HD>::put(ep, dq);
+      RowStage<HD>::get(ep, rq);
+      RowStage<HD>::put_rows(rq, dQ + (long long)b * T * lddq + (long long)h * HD, lddq, wq0, T);
     }
     if (BPQ) {
       const long long prow = (((long long)h * (BH / H) + b) * nqb + qb) * 4 + wave;
