@@ -340,203 +340,6 @@ __global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd_k(const b
   }
 }
 
-// ==================================================================== forward (LDS-DMA) ==
-// NW waves x 32 queries per block; K/V tiles of 64 keys arrive by LDS-DMA
-// (buffer_load ... lds, 1 KiB per wave-instruction, swizzle applied on the source address)
-// into a 3-deep ring: tile t+2 is in flight while tile t is computed, one barrier per tile,
-// counted vmcnt (never 0 in steady state).  Rows >= T get an out-of-range offset -> zeros.
-template <int HD, int NW>
-__device__ __forceinline__ void kv_dma(__amdgpu_buffer_rsrc_t rk, __amdgpu_buffer_rsrc_t rv, char* stage, int kv0,
-                                       int T, long long ldk, long long ldv) {
-  constexpr int CPR = HD / 8;                 // 16-byte chunks per row
-  constexpr int TILE = 64 * HD * 2;
-  constexpr int P = 2 * TILE / 1024;          // pieces per K+V tile
-  constexpr int PW = P / NW;                  // per wave
-  static_assert(PW >= 1 && PW * NW == P, "pieces must divide over the waves");
-  const int l = lane_id();
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#pragma unroll
-  for (int i = 0; i < PW; ++i) {
-    const int j = wave + NW * i;              // piece index
-    const bool isv = j >= P / 2;
-    const int jj = isv ? j - P / 2 : j;
-    const int pos = jj * 64 + l;              // physical chunk position in the tile
-    const int r = pos / CPR, cp = pos % CPR;
-    const int ch = ((sw_off<HD>(r, cp) - r * HD * 2) >> 4);  // XOR swizzle is an involution
-    const int row = kv0 + r;
-    const long long ld = isv ? ldv : ldk;
-    const unsigned off = row < T ? (unsigned)(((long long)row * ld + ch * 8) * 2) : kOOB;
-    dma16(isv ? rv : rk, stage + (isv ? TILE : 0) + jj * 1024, off);
-  }
-}
-
-template <int HD, int NW>
-__global__ __launch_bounds__(64 * NW, (HD > 64 ? 1 : 2)) void attn_fwd2_k(
-    const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V, bf16* __restrict__ O,
-    float* __restrict__ LSE, int T, int H, long long ldq, long long ldk, long long ldv, long long ldo, float scale,
-    int causal) {
-  constexpr int BQ = 32 * NW, BKV = 64, KT = HD / 32, DT = HD / 16;
-  constexpr int TILE = BKV * HD * 2, STAGE = 2 * TILE, NST = 3;
-  constexpr int PW = 2 * TILE / 1024 / NW;
-  __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
-  const int nqb = (T + BQ - 1) / BQ;
-  // XCD-aware order (as attn_fwd_k): the blocks of one (b, h) run on one XCD; heaviest first.
-  const int xl = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
-  const int qb = nqb - 1 - xl % gridDim.x;
-  const int bh = xl / gridDim.x, b = bh / H, h = bh % H;
-  const int q0 = qb * BQ;
-  const int wave = threadIdx.x >> 6, l = lane_id(), g = l >> 4;
-  const int wq0 = q0 + wave * 32;
-  const float c2 = scale * kLog2e;
-
-  const bf16* qbase = Q + (long long)b * T * ldq + (long long)h * HD;
-  const bf16* kbase = K + (long long)b * T * ldk + (long long)h * HD;
-  const bf16* vbase = V + (long long)b * T * ldv + (long long)h * HD;
-  const unsigned kspan = (unsigned)(((long long)(T - 1) * ldk + HD) * 2);
-  const unsigned vspan = (unsigned)(((long long)(T - 1) * ldv + HD) * 2);
-  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, (short)0, (int)kspan, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, (short)0, (int)vspan, 0x00020000);
-
-  const int kv_end = causal ? min(T, q0 + BQ) : T;
-  const int nkv = (kv_end + BKV - 1) / BKV;
-  kv_dma<HD, NW>(rk, rv, smem, 0, T, ldk, ldv);
-  if (nkv > 1) kv_dma<HD, NW>(rk, rv, smem + STAGE, BKV, T, ldk, ldv);
-
-  // Q^T operand in registers: lane holds Q[wq0 + 16c + (l&15)][32kk + 8g + j].
-  bf16x8 qf[2][KT];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int qi = wq0 + 16 * c + (l & 15);
-#pragma unroll
-    for (int kk = 0; kk < KT; ++kk) {
-      bf16x8 v = {};
-      if (qi < T) v = *reinterpret_cast<const bf16x8*>(qbase + (long long)qi * ldq + 32 * kk + 8 * g);
-      qf[c][kk] = v;
-    }
-  }
-
-  f32x4 o[2][DT];
-#pragma unroll
-  for (int c = 0; c < 2; ++c)
-#pragma unroll
-    for (int d = 0; d < DT; ++d) o[c][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float m[2] = {-INFINITY, -INFINITY}, lsum[2] = {0.f, 0.f};
-
-  int cur = 0;
-  for (int t = 0; t < nkv; ++t) {
-    // tile t landed (tile t+1's pieces may still be in flight), then one barrier.
-    if (t + 1 < nkv) wait_vmcnt<PW>();
-    else wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    const char* lk = smem + cur * STAGE;
-    const char* lv = lk + TILE;
-    int nb = cur + 2;
-    if (nb >= NST) nb -= NST;
-    cur = (cur + 1 == NST) ? 0 : cur + 1;
-    const int kv0 = t * BKV;
-    const bool active = !causal || kv0 <= wq0 + 31;  // wave-uniform
-    if (t + 2 < nkv) kv_dma<HD, NW>(rk, rv, smem + nb * STAGE, (t + 2) * BKV, T, ldk, ldv);
-    if (!active) continue;
-    f32x4 s[4][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      s[i][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      s[i][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < KT; ++kk) {
-        const bf16x8 kf = row_frag<HD>(lk, 16 * i, 32 * kk);  // b128 reads: no compiler vmcnt(0)
-        s[i][0] = MFMA(kf, qf[0][kk], s[i][0]);
-        s[i][1] = MFMA(kf, qf[1][kk], s[i][1]);
-      }
-    }
-    // V^T fragments via asm transposed reads (no compiler vmcnt(0) in front of them, see
-    // tr_frag_asm), issued after QK^T is under way so they land during the softmax; the
-    // sched_barrier keeps them below the compiler's lgkmcnt wait for the K reads.
-    __builtin_amdgcn_sched_barrier(0);
-    constexpr int NVH = 4 * DT;                // s16x4 halves of the 2*DT V^T fragments
-    s16x4 vh[(NVH + 15) / 16 * 16];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int d = 0; d < DT; ++d) tr_frag_asm<HD>(lv, 32 * ks, 16 * d, vh[2 * (ks * DT + d)], vh[2 * (ks * DT + d) + 1]);
-    const bool need_mask = __builtin_amdgcn_readfirstlane(
-        (int)((causal && kv0 + BKV - 1 > wq0) || (kv0 + BKV > T)));
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int qi = wq0 + 16 * c + (l & 15);
-      if (need_mask) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int ki = kv0 + 16 * i + 4 * g + j;
-            const bool z = (ki >= T) | (causal & (ki > qi));
-            s[i][c][j] = z ? -INFINITY : s[i][c][j];
-          }
-      }
-      float mx = s[0][c][0];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) mx = fmaxf(mx, s[i][c][j]);
-      mx = group4_max(mx);
-      // deferred rescale (as attn_fwd_k): m moves only when the tile max exceeds it by > 2^8
-      constexpr float kDefer = 8.f;
-      const bool grow = mx * c2 > m[c] + kDefer;
-      if (__builtin_amdgcn_ballot_w64(grow) != 0) {
-        const float mnew = grow ? mx * c2 : m[c];
-        const float alpha = __builtin_amdgcn_exp2f(m[c] - mnew);
-        m[c] = mnew;
-        lsum[c] *= alpha;
-#pragma unroll
-        for (int d = 0; d < DT; ++d) o[c][d] *= alpha;
-      }
-      const float mc = m[c];
-      float ps = 0.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float pv = __builtin_amdgcn_exp2f(fmaf(s[i][c][j], c2, -mc));
-          s[i][c][j] = pv;
-          ps += pv;
-        }
-      lsum[c] += ps;
-    }
-#pragma unroll
-    for (int w = 0; w < (NVH + 15) / 16; ++w) tr_wait8(*reinterpret_cast<s16x4(*)[16]>(&vh[16 * w]));
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 p0 = pack_pt(s[2 * ks][0], s[2 * ks + 1][0]);
-      const bf16x8 p1 = pack_pt(s[2 * ks][1], s[2 * ks + 1][1]);
-#pragma unroll
-      for (int d = 0; d < DT; ++d) {
-        const bf16x8 vf = tr_join(vh[2 * (ks * DT + d)], vh[2 * (ks * DT + d) + 1]);
-        o[0][d] = MFMA(vf, p0, o[0][d]);
-        o[1][d] = MFMA(vf, p1, o[1][d]);
-      }
-    }
-  }
-
-
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const float ls = group4_sum(lsum[c]);
-    const int qi = wq0 + 16 * c + (l & 15);
-    if (qi < T) {
-      const float inv = 1.f / ls;
-      bf16* orow = O + ((long long)b * T + qi) * ldo + (long long)h * HD;
-#pragma unroll
-      for (int d = 0; d < DT; ++d) {
-        bf16x4 v = {(bf16)(o[c][d][0] * inv), (bf16)(o[c][d][1] * inv), (bf16)(o[c][d][2] * inv),
-                    (bf16)(o[c][d][3] * inv)};
-        *reinterpret_cast<bf16x4*>(orow + 16 * d + 4 * g) = v;
-      }
-      if (g == 0) LSE[((long long)b * H + h) * T + qi] = (m[c] + __log2f(ls)) * kLn2;
-    }
-  }
-}
-
 // ============================================================ forward (32x32x16 MFMA) ==
 // v_mfma_f32_32x32x16_bf16 holds the SIMD's vector issue for 8 of its 32 cycles, the
 // 16x16x32 form for 8 of 16: per FLOP the 32x32 shape leaves 3x the issue slots for the
@@ -941,207 +744,6 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
 // HD/2 frequencies; column d < HD/2 pairs with d + HD/2, which lives in the same lane
 // (accumulator tile d + DT/2), so the transpose rotation is applied in registers.
 //   dx1 = dy1 c + dy2 s ;  dx2 = dy2 c - dy1 s
-// ========================================================================= bwd: dK, dV ==
-// Block: 4 waves x 16*KW keys of one (b,h); query tiles of 64 (Q and dO staged in LDS,
-// double buffered; lse/delta staged alongside).  KW = key tiles per wave: every Q / dO
-// fragment read from LDS (row reads for S / dP, transposed reads for dV / dK) feeds KW key
-// tiles, so KW = 2 halves the LDS traffic per MFMA (the KW = 1 kernel issues ~32 KiB of LDS
-// reads per 32 MFMAs per wave: at 8 waves per CU the LDS port, not the MFMA pipe, set its
-// pace) and the global Q / dO tile loads are shared by 128 keys.
-template <int HD, int KW = 1>
-__global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
-                                                          const bf16* __restrict__ V, const bf16* __restrict__ dO,
-                                                          const float* __restrict__ LSE,
-                                                          const float* __restrict__ DELTA, bf16* __restrict__ dK,
-                                                          bf16* __restrict__ dV, int T, int H, long long ldq,
-                                                          long long ldk, long long ldv, long long lddo,
-                                                          long long lddk, long long lddv, float scale, int causal,
-                                                          const int64_t* __restrict__ rpos, const float* __restrict__ rtab) {
-  constexpr int BKV = 64 * KW, BQ = 64, KT = HD / 32, DT = HD / 16;
-  constexpr int TILE = BQ * HD * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * (2 * TILE + 2 * BQ * 4)];
-  constexpr int BUF = 2 * TILE + 2 * BQ * 4;
-  const int kb = blockIdx.x;  // light-to-heavy is fine: causal work per block = T - k0
-  const int bh = blockIdx.y, b = bh / H, h = bh % H;
-  const int k0 = kb * BKV;
-  const int wave = threadIdx.x >> 6, l = lane_id(), g = l >> 4;
-  const int wk0 = k0 + wave * 16 * KW;  // this wave's 16*KW keys
-  const float c2 = scale * kLog2e;
-
-  const bf16* qbase = Q + (long long)b * T * ldq + (long long)h * HD;
-  const bf16* dobase = dO + (long long)b * T * lddo + (long long)h * HD;
-  const float* lse_b = LSE + ((long long)b * H + h) * T;
-  const float* del_b = DELTA + ((long long)b * H + h) * T;
-
-  // K^T and V^T B-operands in registers: lane holds K[wk0 + 16kt + (l&15)][32kk + 8g + j].
-  bf16x8 kf[KW][KT], vf[KW][KT];
-#pragma unroll
-  for (int kt = 0; kt < KW; ++kt) {
-    const int ki = wk0 + 16 * kt + (l & 15);
-#pragma unroll
-    for (int kk = 0; kk < KT; ++kk) {
-      bf16x8 a = {}, c = {};
-      if (ki < T) {
-        a = *reinterpret_cast<const bf16x8*>(K + ((long long)b * T + ki) * ldk + (long long)h * HD + 32 * kk + 8 * g);
-        c = *reinterpret_cast<const bf16x8*>(V + ((long long)b * T + ki) * ldv + (long long)h * HD + 32 * kk + 8 * g);
-      }
-      kf[kt][kk] = a;
-      vf[kt][kk] = c;
-    }
-  }
-  f32x4 dk[KW][DT], dv[KW][DT];
-#pragma unroll
-  for (int kt = 0; kt < KW; ++kt)
-#pragma unroll
-    for (int d = 0; d < DT; ++d) {
-      dk[kt][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      dv[kt][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-
-  const int qstart = causal ? (k0 / BQ) * BQ : 0;
-  const int nq = (T - qstart + BQ - 1) / BQ;
-  Stage<HD, BQ> sq, sdo;
-  auto stage_stats = [&](char* buf, int qq0) {
-    float* ls = reinterpret_cast<float*>(buf + 2 * TILE);
-    float* ds = ls + BQ;
-    if (threadIdx.x < BQ) {
-      const int qi = qq0 + threadIdx.x;
-      ls[threadIdx.x] = qi < T ? lse_b[qi] * kLog2e : 0.f;
-      ds[threadIdx.x] = qi < T ? del_b[qi] : 0.f;
-    }
-  };
-  if (nq > 0) {
-    sq.load(qbase + (long long)qstart * ldq, ldq, min(BQ, T - qstart));
-    sdo.load(dobase + (long long)qstart * lddo, lddo, min(BQ, T - qstart));
-    sq.store(smem);
-    sdo.store(smem + TILE);
-    stage_stats(smem, qstart);
-  }
-  __syncthreads();
-
-  for (int t = 0; t < nq; ++t) {
-    const int cur = t & 1;
-    const char* lq = smem + cur * BUF;
-    const char* ldo_ = lq + TILE;
-    const float* ls = reinterpret_cast<const float*>(lq + 2 * TILE);
-    const float* ds = ls + BQ;
-    const int qq0 = qstart + t * BQ;
-    const bool more = t + 1 < nq;
-    if (more) {
-      const int n0 = qq0 + BQ;
-      sq.load(qbase + (long long)n0 * ldq, ldq, min(BQ, T - n0));
-      sdo.load(dobase + (long long)n0 * lddo, lddo, min(BQ, T - n0));
-    }
-    const bool wave_active = !causal || (qq0 + BQ - 1 >= wk0);
-    if (wave_active) {
-      // S[q][k] and dP[q][k] for 4 query tiles of 16 x KW key tiles.
-      f32x4 s[KW][4], dp[KW][4];
-#pragma unroll
-      for (int qt = 0; qt < 4; ++qt) {
-#pragma unroll
-        for (int kt = 0; kt < KW; ++kt) {
-          s[kt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-          dp[kt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        }
-#pragma unroll
-        for (int kk = 0; kk < KT; ++kk) {
-          const bf16x8 qa = row_frag<HD>(lq, 16 * qt, 32 * kk);
-          const bf16x8 da = row_frag<HD>(ldo_, 16 * qt, 32 * kk);
-#pragma unroll
-          for (int kt = 0; kt < KW; ++kt) {
-            s[kt][qt] = MFMA(qa, kf[kt][kk], s[kt][qt]);
-            dp[kt][qt] = MFMA(da, vf[kt][kk], dp[kt][qt]);
-          }
-        }
-      }
-      const bool need_mask = (causal && wk0 + 16 * KW - 1 > qq0) || (qq0 + BQ > T) || (wk0 + 16 * KW > T);
-#pragma unroll
-      for (int qt = 0; qt < 4; ++qt) {
-        const f32x4 lsv = *reinterpret_cast<const f32x4*>(ls + 16 * qt + 4 * g);
-        const f32x4 dsv = *reinterpret_cast<const f32x4*>(ds + 16 * qt + 4 * g);
-#pragma unroll
-        for (int kt = 0; kt < KW; ++kt) {
-          const int ki = wk0 + 16 * kt + (l & 15);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            float p = __builtin_amdgcn_exp2f(fmaf(s[kt][qt][j], c2, -lsv[j]));
-            if (need_mask) {
-              const int qi = qq0 + 16 * qt + 4 * g + j;
-              if (qi >= T || ki >= T || (causal && ki > qi)) p = 0.f;
-            }
-            s[kt][qt][j] = p;
-            dp[kt][qt][j] = p * (dp[kt][qt][j] + dsv[j]);   // DELTA holds -delta
-          }
-        }
-      }
-      // dV[k][d] += P^T dO ;  dK[k][d] += dS^T Q
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 pa[KW], sa[KW];
-#pragma unroll
-        for (int kt = 0; kt < KW; ++kt) {
-          pa[kt] = pack_pt(s[kt][2 * ks], s[kt][2 * ks + 1]);
-          sa[kt] = pack_pt(dp[kt][2 * ks], dp[kt][2 * ks + 1]);
-        }
-#pragma unroll
-        for (int d = 0; d < DT; ++d) {
-          const bf16x8 dob = tr_frag<HD>(ldo_, 32 * ks, 16 * d);
-          const bf16x8 qb = tr_frag<HD>(lq, 32 * ks, 16 * d);
-#pragma unroll
-          for (int kt = 0; kt < KW; ++kt) {
-            dv[kt][d] = MFMA(pa[kt], dob, dv[kt][d]);
-            dk[kt][d] = MFMA(sa[kt], qb, dk[kt][d]);
-          }
-        }
-      }
-    }
-    if (more) {
-      char* nb = smem + (cur ^ 1) * BUF;
-      sq.store(nb);
-      sdo.store(nb + TILE);
-      stage_stats(nb, qq0 + BQ);
-    }
-    __syncthreads();
-  }
-  // Write dK (scaled), dV: C layout col = d (l&15), rows = keys 16kt + 4g + j.
-#pragma unroll
-  for (int kt = 0; kt < KW; ++kt) {
-#pragma unroll
-    for (int d = 0; d < DT; ++d)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) dk[kt][d][j] *= scale;
-    if (rpos) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int ki = wk0 + 16 * kt + 4 * g + j;
-        if (ki < T) {
-          DPFS_KASSERT(rpos[(long long)b * T + ki] >= 0, "rope position at key %d", ki);
-          const float* tr = rtab + rpos[(long long)b * T + ki] * HD;
-#pragma unroll
-          for (int d = 0; d < DT / 2; ++d) {
-            const float c = tr[16 * d + (l & 15)], sn = tr[HD / 2 + 16 * d + (l & 15)];
-            const float x1 = dk[kt][d][j], x2 = dk[kt][d + DT / 2][j];
-            dk[kt][d][j] = x1 * c + x2 * sn;
-            dk[kt][d + DT / 2][j] = x2 * c - x1 * sn;
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int d = 0; d < DT; ++d) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int ki = wk0 + 16 * kt + 4 * g + j;
-        if (ki < T) {
-          const long long col = (long long)h * HD + 16 * d + (l & 15);
-          dK[((long long)b * T + ki) * lddk + col] = (bf16)dk[kt][d][j];
-          dV[((long long)b * T + ki) * lddv + col] = (bf16)dv[kt][d][j];
-        }
-      }
-    }
-  }
-}
-
 // ================================================================ bwd: dK, dV (LDS-DMA) ==
 // Same math and block shape as attn_bwd_dkdv_k (4 waves x 16 keys, query tiles of 64), but
 // Q / dO tiles and their LSE / delta rows arrive by LDS-DMA into a 3-deep ring: tile t+2
@@ -1571,7 +1173,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
     int T, int H, int BH, long long ldq, long long ldk, long long ldv, long long lddo, long long lddk,
     long long lddv, float scale, int causal, const int64_t* __restrict__ rpos, const float* __restrict__ rtab,
     float* __restrict__ BPK, float* __restrict__ BPV, unsigned long long* __restrict__ diag = nullptr) {
-  // LSN = -lse log2(e) and NDEL = -delta per query row (written by attn_bwd_dq3_k).  BPK / BPV
+  // LSN = -lse / scale and NDEL = -delta per query row (written by attn_bwd_dq3_k).  BPK / BPV
   // (optional): per (b, h, key block, wave) column sums of the stored dK / dV rows.
   static_assert(HD == 64 || HD == 128, "dK/dV v3: head_dim 64 or 128");
   constexpr int BK = 128, BQ = 64, KS = HD / 16, DTN = HD / 32, RB = HD * 2;
@@ -1666,26 +1268,27 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
       if (t + 2 < nq) dma.issue(qbase, dobase, lsb, dlb, ldq, lddo, T, q0 + 2 * BQ, smem + nb * BUF);
       if (causal && q0 + BQ - 1 < kw0) continue;   // wave-uniform: every query of the tile < every key
       if constexpr (DIAG) d_acc[7] += 1;
+      constexpr int NH = 2 * DTN * 4;
+      s16x4 th[(NH + 15) / 16 * 16];
+      bf16x8 pd[4];
       // S = Q K^T, dP = dO V^T (rows = queries 32 qt + 8 (i>>2) + 4 hf + (i&3), lane = key).
-      // p = exp2(c2 S - lse log2 e) of query tile 0 is computed under tile 1's MFMAs (four
-      // elements after each pair), tile 1's after them; the row constants per register come
-      // from the stage (rows 32 qt + 8 g + 4 hf + 0..3 are 4 consecutive floats).
-      // dP starts from -delta (its accumulator's initial value), so dS = p dP' directly.
+      // Both row constants are the accumulators' initial values, read from the stage (rows
+      // 32 qt + 8 g + 4 hf + 0..3 are 4 consecutive floats): S' = S - lse / scale and
+      // dP' = dP - delta, so p = exp2(c2 S') and dS = p dP'.  p of query tile 0 is computed
+      // under tile 1's MFMAs (four elements after each pair), tile 1's after them.
       f32x16 sc[2], dp[2];
-      f32x4 lsr[2][4];
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          lsr[qt][g] = *reinterpret_cast<const f32x4*>(ls + 32 * qt + 8 * g + 4 * hf);
+          const f32x4 lv = *reinterpret_cast<const f32x4*>(ls + 32 * qt + 8 * g + 4 * hf);
           const f32x4 dd = *reinterpret_cast<const f32x4*>(ds + 32 * qt + 8 * g + 4 * hf);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) dp[qt][4 * g + j] = dd[j];
+          for (int j = 0; j < 4; ++j) {
+            sc[qt][4 * g + j] = lv[j];
+            dp[qt][4 * g + j] = dd[j];
+          }
         }
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sc[qt][i] = 0.f;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         sc[0] = MFMA32(*reinterpret_cast<const bf16x8*>(lq + roff[ks]), kf[ks], sc[0]);
@@ -1698,7 +1301,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
         dp[1] = MFMA32(*reinterpret_cast<const bf16x8*>(ldo_ + roff[ks] + 32 * RB), vf[ks], dp[1]);
 #pragma unroll
         for (int i = (16 / KS) * ks; i < (16 / KS) * (ks + 1); ++i)
-          sc[0][i] = __builtin_amdgcn_exp2f(fmaf(sc[0][i], c2, lsr[0][i >> 2][i & 3]));
+          sc[0][i] = __builtin_amdgcn_exp2f(sc[0][i] * c2);
         __builtin_amdgcn_sched_barrier(0);
       }
       if constexpr (DIAG) {
@@ -1707,8 +1310,6 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
         d_t0 = t1;
       }
       // dO^T fragments (A of dV^T: lane d = 32 dt + r32, queries 16 s + 4 hf + 0..3 / 8..11)
-      constexpr int NH = 2 * DTN * 4;
-      s16x4 th[(NH + 15) / 16 * 16];
 #pragma unroll
       for (int dt = 0; dt < DTN; ++dt)
 #pragma unroll
@@ -1717,9 +1318,9 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
           th[2 * (dt * 4 + s4) + 1] = ds_tr16(ldo_ + toff[dt][1] + 16 * s4 * RB);
         }
       // dS = p (dP - delta)
-      bf16x8 pp[4], pd[4];
+      bf16x8 pp[4];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) sc[1][i] = __builtin_amdgcn_exp2f(fmaf(sc[1][i], c2, lsr[1][i >> 2][i & 3]));
+      for (int i = 0; i < 16; ++i) sc[1][i] = __builtin_amdgcn_exp2f(sc[1][i] * c2);
       const bool need_mask = __builtin_amdgcn_readfirstlane(
           (int)((causal && kw0 + 31 > q0) || (q0 + BQ > T) || (kw0 + 32 > T)));
       if (need_mask) {
@@ -2167,7 +1768,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
     wait_vmcnt<0>();
     const float ndel = -pair_sum(dsum);                                      // dP' = dP - delta
     if (hf == 0 && qi < T) {
-      LSN_OUT[(long long)bh * T + qi] = lc;
+      LSN_OUT[(long long)bh * T + qi] = -LSE[(long long)bh * T + qi] / scale;   // dK/dV: S' = S - lse / scale
       NDEL_OUT[(long long)bh * T + qi] = ndel;
     }
     f32x16 dq[DTN];
@@ -2338,8 +1939,9 @@ using namespace dpfs;
 extern "C" int dpfs_attn_supported_hd(int hd) { return hd == 32 || hd == 64 || hd == 128; }
 
 // Forward implementation: 0 = auto (default: attn_fwd3_k at head_dim 64 / 128, attn_fwd_k otherwise),
-// 1 = attn_fwd_k (16x16x32, register-staged), 2 / 3 = attn_fwd2_k (LDS-DMA ring, 8 / 4 waves),
-// 4 = attn_fwd3_k (32x32x16, LDS-DMA ring, hd 64 / 128), 5 = its DIAG build (hd 64).
+// 1 = attn_fwd_k (16x16x32, register-staged), 4 = attn_fwd3_k (32x32x16, LDS-DMA ring, hd 64 /
+// 128), 5 = its DIAG build (hd 64).  (Round 4 retired impl 2 / 3, the 16x16x32 LDS-DMA forward:
+// slower than impl 4 at every head_dim it supported.)
 static int g_attn_impl = 0;
 extern "C" void dpfs_attn_set_impl(int v) { g_attn_impl = v; }
 static int attn_cu_count() {
@@ -2358,9 +1960,10 @@ static unsigned long long* g_attn_diag = nullptr;
 static int g_attn_fwd_persist = 0;
 extern "C" void dpfs_attn_fwd_persist(int v) { g_attn_fwd_persist = v; }   // impl 5: attn_fwd3_k DIAG build, [grid][4 waves][4]
 extern "C" void dpfs_attn_diag(void* p) { g_attn_diag = (unsigned long long*)p; }
-// dK/dV kernel: 0 = auto (default: 4 at head_dim 64 / 128, 2 otherwise), 1 = register-staged,
-// 2 = LDS-DMA ring (16x16x32), 3 = register-staged with 32 keys per wave (hd <= 64),
-// 4 = attn_bwd_dq3_k + attn_bwd_dkdv3_k (32x32x16, query / key on the lane, hd 64 / 128)
+// Backward kernel pair: 0 = auto (default: 4 at head_dim 64 / 128, 2 otherwise), 2 =
+// attn_bwd_dq_k + attn_bwd_dkdv2_k (16x16x32, LDS-DMA ring), 4 = attn_bwd_dq3_k +
+// attn_bwd_dkdv3_k (32x32x16, query / key on the lane, hd 64 / 128).  (Round 4 retired the
+// register-staged dK/dV kernels, impl 1 / 3.)
 static int g_attn_bwd_impl = 0;
 // 1: the dK/dV v3 kernel runs its DIAG build (hd 64) into the attn_diag buffer
 static int g_attn_bwd_diag = 0;
@@ -2372,13 +1975,6 @@ extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void*
                               int hd, long long ldq, long long ldk, long long ldv, long long ldo, float scale,
                               int causal, hipStream_t s) {
   const int impl = g_attn_impl == 0 ? ((hd == 64 || hd == 128) ? 4 : 1) : g_attn_impl;
-  if (impl == 2) {
-    dim3 g8((T + 255) / 256, B * H);
-    DPFS_HD_DISPATCH(hd, attn_fwd2_k<HD_, 8><<<g8, 512, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
-                                                                (bf16*)o, lse, T, H, ldq, ldk, ldv, ldo, scale,
-                                                                causal));
-    return;
-  }
   if ((impl == 4 || (impl == 5 && g_attn_diag)) && (hd == 64 || hd == 128)) {
     const int nqb = (T + 127) / 128, items = (B * H + 7) / 8 * 8 * ((nqb + 1) / 2);
     const int per_cu = hd == 64 ? 3 : 1;           // resident blocks per CU (VGPRs / LDS)
@@ -2394,13 +1990,6 @@ extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void*
                                             B * H, ldq, ldk, ldv, ldo, scale, causal);
     return;
   }
-  if (impl == 3) {
-    dim3 g4((T + 127) / 128, B * H);
-    DPFS_HD_DISPATCH(hd, attn_fwd2_k<HD_, 4><<<g4, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
-                                                                (bf16*)o, lse, T, H, ldq, ldk, ldv, ldo, scale,
-                                                                causal));
-    return;
-  }
   dim3 grid((T + 127) / 128, B * H);
   DPFS_HD_DISPATCH(hd, attn_fwd_k<HD_><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o,
                                                             lse, T, H, ldq, ldk, ldv, ldo, scale, causal));
@@ -2413,17 +2002,17 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
                               long long lddq, long long lddk, long long lddv, float scale, int causal,
                               const int64_t* rope_pos, const float* rope_tab, hipStream_t s, float* dbias,
                               float* bws) {
-  // The QKV bias gradient rides on the default kernel pair (dQ + LDS-DMA dK/dV); with another
-  // dK/dV variant the caller computes it with a separate column sum.
+  // The QKV bias gradient rides on both kernel pairs' epilogues (per-wave column sums + one
+  // reduction kernel).
   const bool v3ok = hd == 64 || hd == 128;
   const int bimpl = g_attn_bwd_impl == 0 ? (v3ok ? 4 : 2) : g_attn_bwd_impl;
-  const bool bias = dbias != nullptr && bws != nullptr && (bimpl == 2 || (bimpl == 4 && v3ok));
+  const bool bias = dbias != nullptr && bws != nullptr;
   const int nqb = (T + 127) / 128, nkb = (T + 63) / 64;
   float* pq = bias ? bws : nullptr;
   float* pk = bias ? bws + (long long)H * B * nqb * 4 * hd : nullptr;
   float* pv = bias ? pk + (long long)H * B * nkb * 4 * hd : nullptr;
   dim3 gq(nqb, B * H);
-  if (bimpl == 4 && v3ok) {   // (attn_bwd_dkdv3_k reads the -lse log2 e this kernel writes)
+  if (bimpl == 4 && v3ok) {   // (attn_bwd_dkdv3_k reads the -lse / scale this kernel writes)
     const int items = (B * H + 7) / 8 * 8 * ((nqb + 1) / 2);
 #define DPFS_DQ3(HD_)                                                                                             \
   attn_bwd_dq3_k<HD_><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,   \
@@ -2441,18 +2030,14 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
                                                              rope_pos, rope_tab, pq));
   if (bimpl == 4 && v3ok) {
     const int nkb3 = (T + 127) / 128, items = (B * H + 7) / 8 * 8 * ((nkb3 + 1) / 2);
-#define DPFS_DKDV3(HD_)                                                                                           \
-  attn_bwd_dkdv3_k<HD_><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, \
-                                              delta + (long long)B * H * T, delta, (bf16*)dk, (bf16*)dv, T, H,     \
-                                              B * H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal, rope_pos,     \
-                                              rope_tab, pk, pv)
-    if (hd == 64 && g_attn_bwd_diag && g_attn_diag)
-      attn_bwd_dkdv3_k<64, 1><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,
-                                                     delta + (long long)B * H * T, delta, (bf16*)dk, (bf16*)dv, T, H,
-                                                     B * H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal, rope_pos,
-                                                     rope_tab, pk, pv, g_attn_diag);
-    else if (hd == 64) DPFS_DKDV3(64);
-    else DPFS_DKDV3(128);
+#define DPFS_DKDV3(HD_, DG_)                                                                                      \
+  attn_bwd_dkdv3_k<HD_, DG_><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, \
+                                                   delta + (long long)B * H * T, delta, (bf16*)dk, (bf16*)dv, T, H,     \
+                                                   B * H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal, rope_pos,     \
+                                                   rope_tab, pk, pv, DG_ ? g_attn_diag : nullptr)
+    if (hd == 64 && g_attn_bwd_diag && g_attn_diag) DPFS_DKDV3(64, 1);
+    else if (hd == 64) DPFS_DKDV3(64, 0);
+    else DPFS_DKDV3(128, 0);
 #undef DPFS_DKDV3
     if (bias) {
       if (hd == 64) attn_bias_grad_k<64><<<3 * H * 4, 1024, 0, s>>>(pq, pk, pv, dbias, H, B * nqb * 4, B * nkb3 * 4);
@@ -2461,36 +2046,17 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
     }
     return 0;
   }
-  if (bimpl == 3 && hd <= 64) {
-    dim3 gk2((T + 127) / 128, B * H);
-    if (hd == 64)
-      attn_bwd_dkdv_k<64, 2><<<gk2, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,
-                                                 lse, delta, (bf16*)dk, (bf16*)dv, T, H, ldq, ldk, ldv, lddo, lddk,
-                                                 lddv, scale, causal, rope_pos, rope_tab);
-    else
-      attn_bwd_dkdv_k<32, 2><<<gk2, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,
-                                                 lse, delta, (bf16*)dk, (bf16*)dv, T, H, ldq, ldk, ldv, lddo, lddk,
-                                                 lddv, scale, causal, rope_pos, rope_tab);
-    return 0;
-  }
   dim3 gk((T + 63) / 64, B * H);
-  if (bimpl == 2) {
-    DPFS_HD_DISPATCH(hd, attn_bwd_dkdv2_k<HD_><<<gk, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
-                                                                  (const bf16*)dout, delta + (long long)B * H * T,
-                                                                  delta, (bf16*)dk,
-                                                                  (bf16*)dv, T, H, ldq, ldk, ldv, lddo, lddk, lddv,
-                                                                  scale, causal, rope_pos, rope_tab, pk, pv));
-    if (bias) {
-      DPFS_HD_DISPATCH(hd, attn_bias_grad_k<HD_><<<3 * H * (HD_ / 16), 1024, 0, s>>>(pq, pk, pv, dbias, H,
-                                                                                       B * nqb * 4, B * nkb * 4));
-      return 1;
-    }
-    return 0;
+  DPFS_HD_DISPATCH(hd, attn_bwd_dkdv2_k<HD_><<<gk, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
+                                                                (const bf16*)dout, delta + (long long)B * H * T,
+                                                                delta, (bf16*)dk,
+                                                                (bf16*)dv, T, H, ldq, ldk, ldv, lddo, lddk, lddv,
+                                                                scale, causal, rope_pos, rope_tab, pk, pv));
+  if (bias) {
+    DPFS_HD_DISPATCH(hd, attn_bias_grad_k<HD_><<<3 * H * (HD_ / 16), 1024, 0, s>>>(pq, pk, pv, dbias, H,
+                                                                                     B * nqb * 4, B * nkb * 4));
+    return 1;
   }
-  DPFS_HD_DISPATCH(hd, attn_bwd_dkdv_k<HD_><<<gk, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
-                                                               (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv, T,
-                                                               H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal,
-                                                               rope_pos, rope_tab));
   return 0;
 }
 

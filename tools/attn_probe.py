@@ -1,6 +1,6 @@
 """Run the attention kernels repeatedly with chosen implementations (for rocprofv3 PMC runs).
 
-    python tools/attn_probe.py --B 32 --T 1024 --H 12 --hd 64 --impl 1 2 --iters 10 [--bwd]
+    python tools/attn_probe.py --B 32 --T 1024 --H 12 --hd 64 --impl 1 4 --iters 10 [--bwd]
 """
 import argparse
 import math
@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--T", type=int, default=1024)
     ap.add_argument("--H", type=int, default=12)
     ap.add_argument("--hd", type=int, default=64)
-    ap.add_argument("--impl", type=int, nargs="+", default=[2])
+    ap.add_argument("--impl", type=int, nargs="+", default=[4])
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--bwd", action="store_true")
     ap.add_argument("--persist", type=int, default=1, help="forward v3: persistent grid (1) or one block per item (0)")

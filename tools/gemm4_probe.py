@@ -60,6 +60,27 @@ def timed(fn, iters):
     return s.elapsed_time(e) / iters
 
 
+_FLUSH = []
+
+
+def timed_cold(fn, iters):
+    """Per-call time with the caches flushed before every call (a 512 MB write evicts the L2s and
+    the Infinity Cache), as in the training step where the operands come from HBM."""
+    if not _FLUSH:
+        _FLUSH.append(torch.empty(128 * 1024 * 1024, dtype=torch.float32, device="cuda"))
+    fn()
+    tot = 0.0
+    for _ in range(iters):
+        _FLUSH[0].fill_(1.0)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        e.synchronize()
+        tot += s.elapsed_time(e)
+    return tot / iters
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=7)
@@ -80,7 +101,11 @@ def main():
                     help="NT only: DIAG build's per-wave cycle split (step waits / bodies / epilogues), s_memtime")
     ap.add_argument("--ablate", type=int, nargs="*", default=[],
                     help="extra v4 arms with timing-only ablations (bits: 1 no stores, 2 zero operands, 4 no DMA wait, 8 no step barrier)")
+    ap.add_argument("--cold", action="store_true", help="flush the caches before every timed call")
     a = ap.parse_args()
+    if a.cold:
+        global timed
+        timed = timed_cold
     C = _ext.require()
     gen = torch.Generator(device="cuda").manual_seed(0)
     for layout in a.layouts:

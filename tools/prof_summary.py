@@ -61,6 +61,25 @@ def load(path: str, after: str = None, skip: int = 0, span=None):
     return rows
 
 
+def sequence(path: str, pattern: str, step_mark: str = None):
+    """The dispatches of the last step (after the last ``step_mark`` dispatch but one) whose name
+    contains ``pattern``: order, us, grid columns (whatever the rocpd view calls them)."""
+    con = sqlite3.connect(path)
+    cur = con.execute("select * from kernels order by start")
+    cols = [d[0] for d in cur.description]
+    recs = cur.fetchall()
+    ix = {c: i for i, c in enumerate(cols)}
+    gcols = [c for c in cols if "grid" in c.lower() or "workgroup" in c.lower()]
+    marks = [i for i, r in enumerate(recs) if step_mark and step_mark in r[ix["name"]]]
+    lo = marks[-2] + 1 if len(marks) >= 2 else 0
+    hi = marks[-1] + 1 if marks else len(recs)
+    print(f"# last step's dispatches matching {pattern!r} (columns: {', '.join(gcols)})")
+    for k, r in enumerate(recs[lo:hi]):
+        if pattern in r[ix["name"]]:
+            print(f"{k:5d} {(r[ix['end']] - r[ix['start']]) / 1e3:9.1f} us  "
+                  + " ".join(str(r[ix[c]]) for c in gcols) + "  " + _short(r[ix["name"]], 70))
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("path")
@@ -69,7 +88,12 @@ def main(argv=None):
     ap.add_argument("--csv", default=None)
     ap.add_argument("--after", default=None, help="keep dispatches after the --skip'th one containing this")
     ap.add_argument("--skip", type=int, default=0)
+    ap.add_argument("--sequence", default=None, metavar="PATTERN",
+                    help="(rocpd database) also list the last step's dispatches whose name contains "
+                         "PATTERN, in order, with duration and grid size")
     a = ap.parse_args(argv)
+    if a.sequence and a.path.endswith(".db"):
+        sequence(a.path, a.sequence, a.after)
     span = []
     rows = load(a.path, a.after, a.skip, span)
     tot = sum(v[0] for v in rows.values())
