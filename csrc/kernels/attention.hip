@@ -490,7 +490,7 @@ __device__ __forceinline__ void wait_vm_rt(int n) {
 // >= T read as zeros) and its first two tiles, and the fetch flies under the softmax, P.V and
 // epilogue.  O / LSE go out as buffer stores (rows >= T dropped by the descriptor), so every
 // wave issues the same vector-memory operations and the counted vmcnt waits are exact.
-template <int HD, int DIAG = 0>
+template <int HD, int DIAG = 0, bool KR = true>
 __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ V, bf16* __restrict__ O,
                                                      float* __restrict__ LSE, int T, int H, int BH, long long ldq,
@@ -591,14 +591,36 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
       const bool active = !causal || kv0 <= wq0 + 31;   // wave-uniform
       f32x16 s[2];
       if (active) {
+        if (HD > 64 && KR) {
+          // one wave per SIMD (hd 128): key half 0's K fragments all read before its first
+          // MFMA, half 1's under half 0's MFMAs (at hd 64, three waves per SIMD leave no
+          // register room for it and the other waves hide the LDS latency)
+          bf16x8 ka[KS], kb[KS];
 #pragma unroll
-        for (int kh = 0; kh < 2; ++kh) {
+          for (int ks = 0; ks < KS; ++ks) ka[ks] = *reinterpret_cast<const bf16x8*>(lk + koff[0][ks]);
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int i = 0; i < 16; ++i) s[kh][i] = 0.f;
+          for (int i = 0; i < 16; ++i) s[0][i] = 0.f;
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks) {
-            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(lk + koff[kh][ks]);
-            s[kh] = MFMA32(kf, qf[ks], s[kh]);
+            s[0] = MFMA32(ka[ks], qf[ks], s[0]);
+            kb[ks] = *reinterpret_cast<const bf16x8*>(lk + koff[1][ks]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+#pragma unroll
+          for (int i = 0; i < 16; ++i) s[1][i] = 0.f;
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) s[1] = MFMA32(kb[ks], qf[ks], s[1]);
+        } else {
+#pragma unroll
+          for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s[kh][i] = 0.f;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+              const bf16x8 kf = *reinterpret_cast<const bf16x8*>(lk + koff[kh][ks]);
+              s[kh] = MFMA32(kf, qf[ks], s[kh]);
+            }
           }
         }
       }
@@ -1277,28 +1299,51 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
       // dP' = dP - delta, so p = exp2(c2 S') and dS = p dP'.  p of query tile 0 is computed
       // under tile 1's MFMAs (four elements after each pair), tile 1's after them.
       f32x16 sc[2], dp[2];
+      // Every LDS read of query tile 0 issued before its first MFMA (row constants, then
+      // the Q / dO fragments in MFMA order), tile 1's under tile 0's MFMAs: one LDS latency
+      // per half instead of one per MFMA pair
+      bf16x8 fa[KS], fb[KS];
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 lv = *reinterpret_cast<const f32x4*>(ls + 8 * g + 4 * hf);
+        const f32x4 dd = *reinterpret_cast<const f32x4*>(ds + 8 * g + 4 * hf);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 lv = *reinterpret_cast<const f32x4*>(ls + 32 * qt + 8 * g + 4 * hf);
-          const f32x4 dd = *reinterpret_cast<const f32x4*>(ds + 32 * qt + 8 * g + 4 * hf);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            sc[qt][4 * g + j] = lv[j];
-            dp[qt][4 * g + j] = dd[j];
-          }
+        for (int j = 0; j < 4; ++j) {
+          sc[0][4 * g + j] = lv[j];
+          dp[0][4 * g + j] = dd[j];
         }
+      }
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        sc[0] = MFMA32(*reinterpret_cast<const bf16x8*>(lq + roff[ks]), kf[ks], sc[0]);
-        dp[0] = MFMA32(*reinterpret_cast<const bf16x8*>(ldo_ + roff[ks]), vf[ks], dp[0]);
+        fa[ks] = *reinterpret_cast<const bf16x8*>(lq + roff[ks]);
+        fb[ks] = *reinterpret_cast<const bf16x8*>(ldo_ + roff[ks]);
       }
       __builtin_amdgcn_sched_barrier(0);
+      bf16x8 ga[KS], gb[KS];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        sc[1] = MFMA32(*reinterpret_cast<const bf16x8*>(lq + roff[ks] + 32 * RB), kf[ks], sc[1]);
-        dp[1] = MFMA32(*reinterpret_cast<const bf16x8*>(ldo_ + roff[ks] + 32 * RB), vf[ks], dp[1]);
+        sc[0] = MFMA32(fa[ks], kf[ks], sc[0]);
+        dp[0] = MFMA32(fb[ks], vf[ks], dp[0]);
+        ga[ks] = *reinterpret_cast<const bf16x8*>(lq + roff[ks] + 32 * RB);
+        gb[ks] = *reinterpret_cast<const bf16x8*>(ldo_ + roff[ks] + 32 * RB);
+        if (ks < 2) {
+#pragma unroll
+          for (int g = 2 * ks; g < 2 * ks + 2; ++g) {
+            const f32x4 lv = *reinterpret_cast<const f32x4*>(ls + 32 + 8 * g + 4 * hf);
+            const f32x4 dd = *reinterpret_cast<const f32x4*>(ds + 32 + 8 * g + 4 * hf);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              sc[1][4 * g + j] = lv[j];
+              dp[1][4 * g + j] = dd[j];
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        sc[1] = MFMA32(ga[ks], kf[ks], sc[1]);
+        dp[1] = MFMA32(gb[ks], vf[ks], dp[1]);
 #pragma unroll
         for (int i = (16 / KS) * ks; i < (16 / KS) * (ks + 1); ++i)
           sc[0][i] = __builtin_amdgcn_exp2f(sc[0][i] * c2);
@@ -1799,16 +1844,27 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
           sc[kh][i] = 0.f;
           dp[kh][i] = ndel;
         }
+      // Key half 0's K / V fragments all read before its first MFMA, half 1's under
+      // half 0's MFMAs (one LDS latency per half instead of one per MFMA pair)
+      bf16x8 fa[KS], fb[KS], ga[KS], gb[KS];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        sc[0] = MFMA32(*reinterpret_cast<const bf16x8*>(lk + koff[0][ks]), qf[ks], sc[0]);
-        dp[0] = MFMA32(*reinterpret_cast<const bf16x8*>(lv + koff[0][ks]), df[ks], dp[0]);
+        fa[ks] = *reinterpret_cast<const bf16x8*>(lk + koff[0][ks]);
+        fb[ks] = *reinterpret_cast<const bf16x8*>(lv + koff[0][ks]);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        sc[1] = MFMA32(*reinterpret_cast<const bf16x8*>(lk + koff[1][ks]), qf[ks], sc[1]);
-        dp[1] = MFMA32(*reinterpret_cast<const bf16x8*>(lv + koff[1][ks]), df[ks], dp[1]);
+        sc[0] = MFMA32(fa[ks], qf[ks], sc[0]);
+        dp[0] = MFMA32(fb[ks], df[ks], dp[0]);
+        ga[ks] = *reinterpret_cast<const bf16x8*>(lk + koff[1][ks]);
+        gb[ks] = *reinterpret_cast<const bf16x8*>(lv + koff[1][ks]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        sc[1] = MFMA32(ga[ks], qf[ks], sc[1]);
+        dp[1] = MFMA32(gb[ks], df[ks], dp[1]);
 #pragma unroll
         for (int i = (16 / KS) * ks; i < (16 / KS) * (ks + 1); ++i)
           sc[0][i] = __builtin_amdgcn_exp2f(fmaf(sc[0][i], c2, lc));
@@ -1955,6 +2011,9 @@ static int attn_cu_count() {
   return n;
 }
 static unsigned long long* g_attn_diag = nullptr;
+// forward v3 at hd 128 (A/B runs): 1 = a key half's K fragments read ahead of its MFMAs
+static int g_attn_fwd_kr = 1;
+extern "C" void dpfs_attn_fwd_kr(int v) { g_attn_fwd_kr = v; }
 // fwd v3 grid: 0 = one workgroup per item (default: the dispatcher refills freed slots, which
 // balances the end of the kernel), 1 = persistent (one round of resident workgroups)
 static int g_attn_fwd_persist = 0;
@@ -1985,9 +2044,12 @@ extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void*
     else if (hd == 64)
       attn_fwd3_k<64><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, T, H,
                                            B * H, ldq, ldk, ldv, ldo, scale, causal);
-    else
+    else if (g_attn_fwd_kr)
       attn_fwd3_k<128><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, T, H,
                                             B * H, ldq, ldk, ldv, ldo, scale, causal);
+    else
+      attn_fwd3_k<128, 0, false><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse,
+                                                      T, H, B * H, ldq, ldk, ldv, ldo, scale, causal);
     return;
   }
   dim3 grid((T + 127) / 128, B * H);

@@ -36,6 +36,9 @@ def test_bench_8_ranks_on_one_gpu():
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-3000:]
     d = lines[0]
+    if os.environ.get("DPFS_REHEARSAL_OUT"):     # keep the line (profiles/ record of the rehearsal)
+        with open(os.environ["DPFS_REHEARSAL_OUT"], "w") as f:
+            f.write(json.dumps(d) + "\n")
     assert d["n_gpus"] == 8 and d["value"] > 0
     assert d["config"]["parallelism"].startswith("tp2dp4")
     assert [L["parallelism"].split("+")[0] for L in d["layouts"]] == ["tp2dp4", "tp8"], d["layouts"]

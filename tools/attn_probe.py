@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--persist", type=int, default=1, help="forward v3: persistent grid (1) or one block per item (0)")
     ap.add_argument("--diag", action="store_true",
                     help="forward v3 DIAG build (impl 5): per-wave s_memtime split wait / QK+max / exp+pack / PV")
+    ap.add_argument("--ab", default=None, help="backward: name of an int kernel switch of _C to A/B (e.g. attn_bwd_er)")
+    ap.add_argument("--ab-vals", type=int, nargs="+", default=[0, 1])
     a = ap.parse_args()
     C = _ext.require()
     C.attn_fwd_persist(a.persist)
@@ -116,6 +118,43 @@ def main():
         print("DIAG dK/dV per wave (ticks, share of life): " + "  ".join(
             f"{n} {w[:, i].mean():.0f} ({(w[:, i] / life).mean() * 100:.1f}%)" for i, n in enumerate(names)),
             flush=True)
+    if a.ab and not a.bwd:   # a forward build switch, interleaved, bitwise check
+        sw = getattr(C, a.ab)
+
+        def mkf(x):
+            def g():
+                C.attn_set_impl(4)
+                sw(x)
+                return C.attn_fwd(q, k, v, scale, True)
+            return g
+        o0, l0 = mkf(a.ab_vals[0])()
+        for x in a.ab_vals[1:]:
+            o1, l1 = mkf(x)()
+            print(f"{a.ab} {x} vs {a.ab_vals[0]} bitwise equal: {torch.equal(o0, o1) and torch.equal(l0, l1)}", flush=True)
+        r = timeit({f"{a.ab}={x}": mkf(x) for x in a.ab_vals}, iters=a.iters, rounds=7)
+        for kk, ms in r.items():
+            print(f"fwd {kk}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF", flush=True)
+        sw(1)
+    if a.ab and a.bwd:   # a dK/dV v3 build switch (C.<name>(0 / 1)), interleaved, bitwise check
+        sw = getattr(C, a.ab)
+
+        def mkab(x):
+            def g():
+                C.attn_set_bwd_impl(4)
+                sw(x)
+                C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv)
+            return g
+        vals = a.ab_vals
+        mkab(vals[0])()
+        ref = [t.clone() for t in (dq, dk, dv)]
+        for x in vals[1:]:
+            mkab(x)()
+            print(f"{a.ab} {x} vs {vals[0]} bitwise equal: " +
+                  str(all(torch.equal(u, w) for u, w in zip(ref, (dq, dk, dv)))), flush=True)
+        r = timeit({f"{a.ab}={x}": mkab(x) for x in vals}, iters=a.iters, rounds=7)
+        for kk, ms in r.items():
+            print(f"bwd {kk}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF", flush=True)
+        sw(0)
     res = timeit({impl: mk(impl) for impl in a.impl}, iters=a.iters, rounds=5)  # interleaved, median
     for impl, ms in res.items():
         print(f"impl {impl} {'bwd' if a.bwd else 'fwd'}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF", flush=True)
