@@ -44,6 +44,7 @@ import torch.distributed as dist
 from ..ops import fp8 as F8
 from ..ops import gemm_select as GS
 from ..ops.dispatch import K, shadow
+from ..parallel import grad_sync as GSY
 from ..parallel import process_manager as pm
 from ..parallel import tp_comm
 
@@ -294,23 +295,18 @@ class DecoderTrainFn(torch.autograd.Function):
                 return
             key_dict[key] = _addg(key_dict.get(key), k.bias_grad(dy))
 
-        # DP: each layer's gradients are averaged over the data-parallel group by one async
-        # all-reduce of a flat fp32 buffer, issued as soon as the layer's backward completes,
-        # so it overlaps the remaining layers (DataParallelGradSync's hooks would only fire
-        # after this Function returns).
+        # DP: each layer's gradients are queued for the data-parallel average as soon as the
+        # layer's backward completes and go out as async all-reduces of flat fp32 buckets, so
+        # they overlap the remaining layers (DataParallelGradSync's hooks would only fire after
+        # this Function returns).
         pg = pm.pgm
         dp = pg.dp_size if pg is not None else 1
-        dp_pending = []
-
-        def dp_reduce(d: dict, keys=None):
-            if dp <= 1:
-                return
-            _defer_flush()
-            keys = [key for key in (keys or sorted(d)) if d.get(key) is not None]
-            if not keys:
-                return
-            flat = torch.cat([d[key].reshape(-1) for key in keys])
-            dp_pending.append((dist.all_reduce(flat, group=pg.dp_group, async_op=True), flat, d, keys))
+        # buckets of at least the measured knee of the DP group's all-reduce curve
+        # (parallel/grad_sync.dp_bucket_bytes; small per-layer groups are merged)
+        dpb = GSY.DPBucketer(pg.dp_group if dp > 1 else None, dp,
+                             GSY.dp_bucket_bytes(pg.dp_group, gscale_all.device) if dp > 1 else 0,
+                             before_pack=_defer_flush)
+        dp_reduce = dpb.add
 
         # ---- head: CE backward in place over the logits, lm_head dgrad -> async AR
         lm_p = []
@@ -428,16 +424,8 @@ class DecoderTrainFn(torch.autograd.Function):
         dp_reduce(g, ("emb",))
         _defer_end()
         tp_comm.check()   # an xGMI barrier that timed out raises here (host-mapped flag, no sync)
-        if dp_pending:
+        if dpb.finish():
             model._dpfs_dp_reduced = True   # DataParallelGradSync hooks skip this step
-        for h, flat, d, keys in dp_pending:
-            h.wait()
-            flat /= dp
-            off = 0
-            for key in keys:
-                n = d[key].numel()
-                d[key] = flat[off:off + n].view_as(d[key])
-                off += n
         ctx.st = None
         grads = [g["emb"]]
         for li, L in enumerate(layers):

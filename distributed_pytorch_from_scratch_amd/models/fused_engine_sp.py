@@ -36,6 +36,7 @@ import torch.distributed as dist
 from ..ops import fp8 as F8
 from ..ops import gemm_select as GS
 from ..ops.dispatch import K, shadow
+from ..parallel import grad_sync as GSY
 from ..parallel import process_manager as pm
 from ..parallel import tp_comm
 from .fused_engine import (_QKV_BIAS_IN_ATTN, _Layer, _addg, _defer_begin, _defer_end, _defer_flush,
@@ -200,16 +201,12 @@ class DecoderTrainFnSP(torch.autograd.Function):
 
         pg = pm.pgm
         dp = pg.dp_size
-        dp_pending = []
-
-        def dp_reduce(d: dict, keys=None):
-            if dp <= 1:
-                return
-            _defer_flush()
-            keys = [key for key in (keys or sorted(d)) if d.get(key) is not None]
-            if keys:
-                flat = torch.cat([d[key].reshape(-1) for key in keys])
-                dp_pending.append((dist.all_reduce(flat, group=pg.dp_group, async_op=True), flat, d, keys))
+        # buckets of at least the measured knee of the DP group's all-reduce curve
+        # (parallel/grad_sync.dp_bucket_bytes; small per-layer groups are merged)
+        dpb = GSY.DPBucketer(pg.dp_group if dp > 1 else None, dp,
+                             GSY.dp_bucket_bytes(pg.dp_group, gscale_all.device) if dp > 1 else 0,
+                             before_pack=_defer_flush)
+        dp_reduce = dpb.add
 
         d = model.args.attn_dim
         lm_p = []
@@ -337,16 +334,8 @@ class DecoderTrainFnSP(torch.autograd.Function):
         dp_reduce(g, ("emb", "nf"))
         _defer_end()
         tp_comm.check()
-        if dp_pending:
-            model._dpfs_dp_reduced = True
-        for h, flat, d, keys in dp_pending:
-            h.wait()
-            flat /= dp
-            off = 0
-            for key in keys:
-                num = d[key].numel()
-                d[key] = flat[off:off + num].view_as(d[key])
-                off += num
+        if dpb.finish():
+            model._dpfs_dp_reduced = True   # DataParallelGradSync hooks skip this step
         ctx.st = None
         grads = [g["emb"]]
         for li, L in enumerate(layers):

@@ -14,12 +14,133 @@
 """
 from __future__ import annotations
 
-from typing import Dict, List, Optional
+import os
+from typing import Callable, Dict, List, Optional
 
 import torch
 import torch.distributed as dist
 
 from . import process_manager as pm
+
+# ---------------------------------------------------------------- bucket size for DP all-reduce
+# A ring all-reduce over the 8-GPU xGMI mesh moves 2 (W-1)/W of the message per GPU in W-1
+# steps over one link per direction; below some size each step is latency-bound and the bus
+# rate collapses.  ``dp_bucket_bytes`` picks the bucket as the smallest message that reaches
+# ``DP_BUCKET_FRACTION`` of the best measured bus rate on the live DP group (the knee of the
+# curve on this node, RCCL protocol and channel count included), so the fused engines merge
+# small per-layer gradient groups (e.g. at TP 8, ~3.5 MB per GPT-2-small layer and rank) into
+# buckets that run at link speed, while large groups still start as soon as they are complete.
+DP_BUCKET_SIZES_MB = (1, 2, 4, 8, 16, 32, 64)
+DP_BUCKET_FRACTION = 0.85
+_BUCKET_CACHE: Dict[int, int] = {}
+
+
+def measure_bucket_knee(group, device, sizes_mb=DP_BUCKET_SIZES_MB, frac: float = DP_BUCKET_FRACTION,
+                        reps: int = 3) -> int:
+    """Bytes of the smallest all-reduce message whose bus rate (max time over the group's ranks)
+    is within ``frac`` of the best of ``sizes_mb``.  Every rank returns the same value (the
+    times are MAX-reduced before the choice)."""
+    cuda = device.type == "cuda"
+    times = []
+    for mb in sizes_mb:
+        buf = torch.zeros(int(mb * 2 ** 20) // 4, dtype=torch.float32, device=device)
+        dist.all_reduce(buf, group=group)                 # warm the protocol / channels
+        if cuda:
+            torch.cuda.synchronize(device)
+        dist.barrier(group=group)
+        if cuda:
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(reps):
+                dist.all_reduce(buf, group=group)
+            e.record()
+            e.synchronize()
+            ms = s.elapsed_time(e) / reps
+        else:
+            import time
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                dist.all_reduce(buf, group=group)
+            ms = (time.perf_counter() - t0) * 1e3 / reps
+        times.append(ms)
+    t = torch.tensor(times, dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    rates = [mb / max(ms, 1e-9) for mb, ms in zip(sizes_mb, t.tolist())]
+    best = max(rates)
+    for mb, r in zip(sizes_mb, rates):
+        if r >= frac * best:
+            return int(mb * 2 ** 20)
+    return int(sizes_mb[-1] * 2 ** 20)
+
+
+def dp_bucket_bytes(group, device) -> int:
+    """DP bucket size of the fused engines: ``DPFS_DP_BUCKET_MB`` = a number of MB (0: every
+    gradient group is its own all-reduce, the pre-bucketing behaviour), or ``auto`` (default on
+    RCCL: ``measure_bucket_knee`` once per group; on gloo 0)."""
+    key = id(group)
+    if key in _BUCKET_CACHE:
+        return _BUCKET_CACHE[key]
+    env = os.environ.get("DPFS_DP_BUCKET_MB", "auto").strip().lower()
+    if env == "auto":
+        nb = measure_bucket_knee(group, device) if dist.get_backend(group) == "nccl" else 0
+    else:
+        nb = int(float(env) * 2 ** 20)
+    _BUCKET_CACHE[key] = nb
+    return nb
+
+
+class DPBucketer:
+    """The fused engines' DP gradient averaging: gradient groups (a dict of fp32 tensors and the
+    keys to reduce) are queued as the backward completes them and launched as ONE async
+    all-reduce of a flat buffer once the queued bytes reach ``bucket_bytes`` (0: every group at
+    once); ``finish`` launches the rest, waits, averages and writes the values back into the
+    dicts (the flat buffer's views replace the tensors).  ``before_pack`` runs before a bucket
+    is packed (the engines flush their deferred gradient sums there)."""
+
+    def __init__(self, group, dp: int, bucket_bytes: int, before_pack: Optional[Callable[[], None]] = None):
+        self.group, self.dp, self.bucket_bytes, self.before_pack = group, dp, bucket_bytes, before_pack
+        self._queued: List[tuple] = []
+        self._bytes = 0
+        self._pending: List[tuple] = []
+        self.launches = 0
+
+    def add(self, d: dict, keys=None) -> None:
+        if self.dp <= 1:
+            return
+        keys = [k for k in (keys or sorted(d)) if d.get(k) is not None]
+        if not keys:
+            return
+        self._queued.append((d, keys))
+        self._bytes += sum(d[k].numel() * 4 for k in keys)
+        if self._bytes >= self.bucket_bytes:
+            self._launch()
+
+    def _launch(self) -> None:
+        if not self._queued:
+            return
+        if self.before_pack is not None:
+            self.before_pack()
+        flat = torch.cat([d[k].reshape(-1).float() for d, keys in self._queued for k in keys])
+        h = dist.all_reduce(flat, group=self.group, async_op=True)
+        self._pending.append((h, flat, self._queued))
+        self._queued, self._bytes = [], 0
+        self.launches += 1
+
+    def finish(self) -> bool:
+        """Launch what is queued, wait for every bucket, average; True if anything was reduced."""
+        self._launch()
+        done = bool(self._pending)
+        for h, flat, groups in self._pending:
+            h.wait()
+            flat /= self.dp
+            off = 0
+            for d, keys in groups:
+                for k in keys:
+                    n = d[k].numel()
+                    d[k] = flat[off:off + n].view_as(d[k])
+                    off += n
+        self._pending = []
+        return done
 
 
 def _flat_allreduce(tensors: List[torch.Tensor], group, average_by: int = 1) -> None:

@@ -81,6 +81,37 @@ def _oracle():
     (2, True, False),    # modular SP + DP hooks (the DP finish must precede the SP sum over TP)
 ])
 def test_dp_matches_single_rank(tp, sp, fused):
+    _check_dp(tp, sp, fused)
+
+
+@pytest.mark.parametrize("bucket_mb", ["0", "1000"])
+@pytest.mark.parametrize("tp,sp", [(1, False), (2, True)])
+def test_dp_fused_buckets(tp, sp, bucket_mb, monkeypatch):
+    """The fused engines' DP buckets (parallel/grad_sync.DPBucketer): every layer its own
+    all-reduce (0) or all layers merged into one bucket (1000 MB) give the single-rank result."""
+    monkeypatch.setenv("DPFS_DP_BUCKET_MB", bucket_mb)
+    _check_dp(tp, sp, True)
+
+
+def _knee(rank, world):
+    import torch.distributed as dist
+    from distributed_pytorch_from_scratch_amd.parallel import grad_sync as GSY
+    from distributed_pytorch_from_scratch_amd.parallel import process_manager as pm
+    nb = GSY.measure_bucket_knee(pm.get_pgm().dp_group, torch.device("cpu"), sizes_mb=(0.0625, 0.25, 1), reps=2)
+    t = torch.tensor([float(nb)])
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return dict(nb=nb, mx=t.item())
+
+
+def test_bucket_knee_agrees_across_ranks():
+    """The measured bucket size is the same on every rank (times are MAX-reduced first) and is
+    one of the candidate sizes."""
+    res = run_distributed(_knee, 2, tp_size=1)
+    for r in res.values():
+        assert r["nb"] == r["mx"] and r["nb"] in (int(0.0625 * 2 ** 20), int(0.25 * 2 ** 20), 2 ** 20)
+
+
+def _check_dp(tp, sp, fused):
     ref = _oracle()
     world = 2 * tp
     res = run_distributed(_step, world, tp, sp, fused, tp_size=tp)
