@@ -29,7 +29,6 @@ void dpfs_gemm4_diag(void*);
 void dpfs_attn_diag(void*);
 void dpfs_attn_fwd_persist(int);
 void dpfs_attn_bwd_diag(int);
-void dpfs_attn_fwd_kr(int);
 void dpfs_gemm_force(int, int);
 void dpfs_gemm_v2_sched(int);
 void dpfs_gemm_set_workspace(float*, long long);
@@ -1149,7 +1148,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm4_ablate", [](int v) { dpfs_gemm4_ablate(v); }, "timing-only: 1 = drop stores, 2 = zero operands");
   m.def("attn_fwd_persist", [](int v) { dpfs_attn_fwd_persist(v); },
         "forward v3 grid: 1 = persistent (resident blocks walk the items), 0 = one block per item");
-  m.def("attn_fwd_kr", [](int v) { dpfs_attn_fwd_kr(v); }, "forward v3 hd 128 K-read order for A/B runs (1 = ahead)");
   m.def("attn_bwd_diag", [](int v) { dpfs_attn_bwd_diag(v); },
         "1: the dK/dV v3 kernel (hd 64) writes its per-wave s_memtime split into the attn_diag buffer");
   m.def("attn_diag", [](torch::Tensor t) { dpfs_attn_diag(t.defined() && t.numel() ? t.data_ptr() : nullptr); },

@@ -490,7 +490,7 @@ __device__ __forceinline__ void wait_vm_rt(int n) {
 // >= T read as zeros) and its first two tiles, and the fetch flies under the softmax, P.V and
 // epilogue.  O / LSE go out as buffer stores (rows >= T dropped by the descriptor), so every
 // wave issues the same vector-memory operations and the counted vmcnt waits are exact.
-template <int HD, int DIAG = 0, bool KR = true>
+template <int HD, int DIAG = 0>
 __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ V, bf16* __restrict__ O,
                                                      float* __restrict__ LSE, int T, int H, int BH, long long ldq,
@@ -591,7 +591,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
       const bool active = !causal || kv0 <= wq0 + 31;   // wave-uniform
       f32x16 s[2];
       if (active) {
-        if (HD > 64 && KR) {
+        if constexpr (HD > 64) {
           // one wave per SIMD (hd 128): key half 0's K fragments all read before its first
           // MFMA, half 1's under half 0's MFMAs (at hd 64, three waves per SIMD leave no
           // register room for it and the other waves hide the LDS latency)
@@ -2011,9 +2011,7 @@ static int attn_cu_count() {
   return n;
 }
 static unsigned long long* g_attn_diag = nullptr;
-// forward v3 at hd 128 (A/B runs): 1 = a key half's K fragments read ahead of its MFMAs
-static int g_attn_fwd_kr = 1;
-extern "C" void dpfs_attn_fwd_kr(int v) { g_attn_fwd_kr = v; }
+
 // fwd v3 grid: 0 = one workgroup per item (default: the dispatcher refills freed slots, which
 // balances the end of the kernel), 1 = persistent (one round of resident workgroups)
 static int g_attn_fwd_persist = 0;
@@ -2044,12 +2042,9 @@ extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void*
     else if (hd == 64)
       attn_fwd3_k<64><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, T, H,
                                            B * H, ldq, ldk, ldv, ldo, scale, causal);
-    else if (g_attn_fwd_kr)
+    else
       attn_fwd3_k<128><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, T, H,
                                             B * H, ldq, ldk, ldv, ldo, scale, causal);
-    else
-      attn_fwd3_k<128, 0, false><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse,
-                                                      T, H, B * H, ldq, ldk, ldv, ldo, scale, causal);
     return;
   }
   dim3 grid((T + 127) / 128, B * H);
