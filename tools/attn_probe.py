@@ -134,7 +134,7 @@ def main():
         r = timeit({f"{a.ab}={x}": mkf(x) for x in a.ab_vals}, iters=a.iters, rounds=7)
         for kk, ms in r.items():
             print(f"fwd {kk}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF", flush=True)
-        sw(1)
+        sw(a.ab_vals[0])
     if a.ab and a.bwd:   # a dK/dV v3 build switch (C.<name>(0 / 1)), interleaved, bitwise check
         sw = getattr(C, a.ab)
 
@@ -154,7 +154,7 @@ def main():
         r = timeit({f"{a.ab}={x}": mkab(x) for x in vals}, iters=a.iters, rounds=7)
         for kk, ms in r.items():
             print(f"bwd {kk}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF", flush=True)
-        sw(0)
+        sw(a.ab_vals[0])
     res = timeit({impl: mk(impl) for impl in a.impl}, iters=a.iters, rounds=5)  # interleaved, median
     for impl, ms in res.items():
         print(f"impl {impl} {'bwd' if a.bwd else 'fwd'}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF", flush=True)
