@@ -122,6 +122,17 @@ def main():
                 if want is not None:
                     out = ours(C).float()
                     res[tag] = ((out - want).norm() / want.norm()).item()
+            for x in a.ablate:   # the non-destructive switches (64 = W8 epilogue stores) are checked too
+                if want is not None and not (x & 15):
+                    set_variant(1)
+                    C.gemm4_ablate(x)
+                    out = ours(C).float()
+                    C.gemm4_ablate(0)
+                    res[f"abl{x}"] = ((out - want).norm() / want.norm()).item()
+                    C.gemm4_ablate(x)
+                    o2 = ours(C)
+                    C.gemm4_ablate(0)
+                    res[f"abl{x}_bitwise_vs_default"] = float(torch.equal(o2, ours(C)))
             set_variant(1)
             del want
             flops = 2.0 * M * N * K
