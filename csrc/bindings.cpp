@@ -27,8 +27,6 @@ void dpfs_gemm4_group_m(int);
 void dpfs_gemm4_ablate(int);
 void dpfs_gemm4_diag(void*);
 void dpfs_attn_diag(void*);
-void dpfs_attn_fwd_persist(int);
-void dpfs_attn_bwd_diag(int);
 void dpfs_gemm_force(int, int);
 void dpfs_gemm_v2_sched(int);
 void dpfs_gemm_set_workspace(float*, long long);
@@ -74,13 +72,11 @@ void dpfs_adam_step(const void*, const int*, int, float, float, float, float, fl
                     hipStream_t);
 void dpfs_grad_sumsq(const void*, const int*, int, float*, hipStream_t);
 int dpfs_attn_supported_hd(int);
-void dpfs_attn_set_impl(int);
-void dpfs_attn_set_bwd_impl(int);
 void dpfs_attn_fwd(const void*, const void*, const void*, void*, float*, int, int, int, int, long long, long long,
-                   long long, long long, float, int, hipStream_t);
+                   long long, long long, float, int, int, hipStream_t);
 int dpfs_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, float*, void*, void*,
                    void*, int, int, int, int, long long, long long, long long, long long, long long, long long,
-                   long long, long long, float, int, const int64_t*, const float*, hipStream_t, float*, float*);
+                   long long, long long, float, int, const int64_t*, const float*, hipStream_t, float*, float*, int);
 long long dpfs_attn_bias_ws(int, int, int, int);
 // kernels/decode.hip
 int dpfs_decode_nsplit(int);
@@ -598,7 +594,8 @@ View4 check_bthd(const torch::Tensor& t, const char* name, int64_t B, int64_t T,
   return {(long long)t.stride(1)};
 }
 
-std::vector<torch::Tensor> attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, double scale, bool causal) {
+std::vector<torch::Tensor> attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, double scale, bool causal,
+                                    int64_t impl) {
   const int64_t B = q.size(0), T = q.size(1), H = q.size(2), hd = q.size(3);
   TORCH_CHECK(dpfs_attn_supported_hd((int)hd), "attn: head_dim ", hd, " not supported (32/64/128)");
   auto vq = check_bthd(q, "q", B, T, H, hd), vk = check_bthd(k, "k", B, T, H, hd), vv = check_bthd(v, "v", B, T, H, hd);
@@ -607,7 +604,7 @@ std::vector<torch::Tensor> attn_fwd(torch::Tensor q, torch::Tensor k, torch::Ten
   auto lse = torch::empty({B, H, T}, q.options().dtype(torch::kFloat32));
   if (B * T * H)
     dpfs_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), (int)B, (int)T,
-                  (int)H, (int)hd, vq.ld, vk.ld, vv.ld, H * hd, (float)scale, causal ? 1 : 0, stream());
+                  (int)H, (int)hd, vq.ld, vk.ld, vv.ld, H * hd, (float)scale, causal ? 1 : 0, (int)impl, stream());
   return {o, lse};
 }
 
@@ -617,7 +614,7 @@ std::vector<torch::Tensor> attn_fwd(torch::Tensor q, torch::Tensor k, torch::Ten
 bool attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Tensor o,
               torch::Tensor lse, double scale, bool causal, torch::Tensor dq, torch::Tensor dk, torch::Tensor dv,
               c10::optional<torch::Tensor> rope_pos, c10::optional<torch::Tensor> rope_tab,
-              c10::optional<torch::Tensor> dbias) {
+              c10::optional<torch::Tensor> dbias, int64_t impl) {
   const int64_t B = q.size(0), T = q.size(1), H = q.size(2), hd = q.size(3);
   TORCH_CHECK(dpfs_attn_supported_hd((int)hd), "attn: head_dim not supported");
   auto vq = check_bthd(q, "q", B, T, H, hd), vk = check_bthd(k, "k", B, T, H, hd), vv = check_bthd(v, "v", B, T, H, hd);
@@ -655,7 +652,7 @@ bool attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tenso
   return dpfs_attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
                        delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), (int)B, (int)T, (int)H,
                        (int)hd, vdo.ld, vq.ld, vk.ld, vv.ld, vo.ld, vdq.ld, vdk.ld, vdv.ld, (float)scale, causal ? 1 : 0,
-                       rp, rt, stream(), db, db ? bws.data_ptr<float>() : nullptr) != 0;
+                       rp, rt, stream(), db, db ? bws.data_ptr<float>() : nullptr, (int)impl) != 0;
 }
 
 // ------------------------------------------------------------------- embedding / CE --
@@ -1146,12 +1143,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_force", [](int cfg, int splits) { dpfs_gemm_force(cfg, splits); },
         "force the v2 tile config (-1 auto, 0 = 256x256, 1 = 256x128) and K-splits (0 auto)");
   m.def("gemm4_ablate", [](int v) { dpfs_gemm4_ablate(v); }, "timing-only: 1 = drop stores, 2 = zero operands");
-  m.def("attn_fwd_persist", [](int v) { dpfs_attn_fwd_persist(v); },
-        "forward v3 grid: 1 = persistent (resident blocks walk the items), 0 = one block per item");
-  m.def("attn_bwd_diag", [](int v) { dpfs_attn_bwd_diag(v); },
-        "1: the dK/dV v3 kernel (hd 64) writes its per-wave s_memtime split into the attn_diag buffer");
   m.def("attn_diag", [](torch::Tensor t) { dpfs_attn_diag(t.defined() && t.numel() ? t.data_ptr() : nullptr); },
-        "int64 buffer [grid*4*4] for attn_set_impl(5): the forward's per-wave cycle split (wait / QK / softmax / PV)");
+        "int64 buffer of the DIAG builds (attn_fwd / attn_bwd impl 5): per-wave s_memtime splits");
   m.def("gemm4_diag", [](torch::Tensor t) { dpfs_gemm4_diag(t.defined() && t.numel() ? t.data_ptr() : nullptr); },
         "int64 buffer [grid*4*4] for the DIAG build's per-wave cycle split (gemm4_ablate bit 16)");
   m.def("gemm4_sched", [](int v) { dpfs_gemm4_sched(v); },
@@ -1185,14 +1178,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a"), py::arg("b"), py::arg("bias") = py::none());
   m.def("rope_", &rope_, py::arg("qkv"), py::arg("positions"), py::arg("table"), py::arg("n_rot_heads"),
         py::arg("head_dim"), py::arg("inverse") = false);
-  m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("scale"), py::arg("causal") = true);
-  m.def("attn_set_impl", [](int v) { dpfs_attn_set_impl(v); },
-        "forward: 0 = auto (default), 1 = 16x16x32 register-staged, 2 / 3 = LDS-DMA ring 8 / 4 waves, "
-        "4 = 32x32x16 LDS-DMA ring (hd 64 / 128), 5 = its DIAG build");
-  m.def("attn_set_bwd_impl", [](int v) { dpfs_attn_set_bwd_impl(v); }, "dK/dV kernel: 0 = auto (default), 1 = register-staged, 2 = LDS-DMA ring, 3 = 32 keys per wave, 4 = 32x32x16 key-on-lane (hd 64)");
+  m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("scale"), py::arg("causal") = true,
+        py::arg("impl") = 0,
+        "flash attention forward; impl (per call): 0 = auto (32x32x16 LDS-DMA ring at hd 64 / 128, "
+        "16x16x32 register-staged at hd 32), 1 = 16x16x32 register-staged, 4 = 32x32x16 ring, 5 = its DIAG build");
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("scale"), py::arg("causal"), py::arg("dq"), py::arg("dk"), py::arg("dv"),
-        py::arg("rope_pos") = py::none(), py::arg("rope_tab") = py::none(), py::arg("dbias") = py::none());
+        py::arg("rope_pos") = py::none(), py::arg("rope_tab") = py::none(), py::arg("dbias") = py::none(),
+        py::arg("impl") = 0,
+        "flash attention backward; impl (per call): 0 = auto (dq3 + dkdv3 at hd 64 / 128, dq + dkdv2 at hd 32), "
+        "2 = dq + dkdv2 (16x16x32), 4 = dq3 + dkdv3 (32x32x16), 5 = 4 with the dK/dV DIAG build");
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("ce_fwd_stats", &ce_fwd_stats);

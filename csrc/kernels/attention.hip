@@ -1994,48 +1994,24 @@ using namespace dpfs;
 
 extern "C" int dpfs_attn_supported_hd(int hd) { return hd == 32 || hd == 64 || hd == 128; }
 
-// Forward implementation: 0 = auto (default: attn_fwd3_k at head_dim 64 / 128, attn_fwd_k otherwise),
-// 1 = attn_fwd_k (16x16x32, register-staged), 4 = attn_fwd3_k (32x32x16, LDS-DMA ring, hd 64 /
-// 128), 5 = its DIAG build (hd 64).  (Round 4 retired impl 2 / 3, the 16x16x32 LDS-DMA forward:
-// slower than impl 4 at every head_dim it supported.)
-static int g_attn_impl = 0;
-extern "C" void dpfs_attn_set_impl(int v) { g_attn_impl = v; }
-static int attn_cu_count() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    if (n <= 0) n = 256;
-  }
-  return n;
-}
+// Kernel selection is a per-call argument (`impl`), never process state.
+// Forward: 0 = auto (attn_fwd3_k at head_dim 64 / 128, attn_fwd_k otherwise), 1 = attn_fwd_k
+// (16x16x32, register-staged), 4 = attn_fwd3_k (32x32x16, LDS-DMA ring, hd 64 / 128), 5 = its
+// DIAG build (hd 64, timing diagnosis into the attn_diag buffer).  (Round 4 retired impl 2 / 3,
+// the 16x16x32 LDS-DMA forward: slower than impl 4 at every head_dim it supported.)
+// The DIAG builds' output buffer (tools/attn_probe.py --diag) is the one piece of state: it is
+// read only by a call that asks for a DIAG build.
 static unsigned long long* g_attn_diag = nullptr;
-
-// fwd v3 grid: 0 = one workgroup per item (default: the dispatcher refills freed slots, which
-// balances the end of the kernel), 1 = persistent (one round of resident workgroups)
-static int g_attn_fwd_persist = 0;
-extern "C" void dpfs_attn_fwd_persist(int v) { g_attn_fwd_persist = v; }   // impl 5: attn_fwd3_k DIAG build, [grid][4 waves][4]
 extern "C" void dpfs_attn_diag(void* p) { g_attn_diag = (unsigned long long*)p; }
-// Backward kernel pair: 0 = auto (default: 4 at head_dim 64 / 128, 2 otherwise), 2 =
-// attn_bwd_dq_k + attn_bwd_dkdv2_k (16x16x32, LDS-DMA ring), 4 = attn_bwd_dq3_k +
-// attn_bwd_dkdv3_k (32x32x16, query / key on the lane, hd 64 / 128).  (Round 4 retired the
-// register-staged dK/dV kernels, impl 1 / 3.)
-static int g_attn_bwd_impl = 0;
-// 1: the dK/dV v3 kernel runs its DIAG build (hd 64) into the attn_diag buffer
-static int g_attn_bwd_diag = 0;
-extern "C" void dpfs_attn_bwd_diag(int v) { g_attn_bwd_diag = v; }
-
-extern "C" void dpfs_attn_set_bwd_impl(int v) { g_attn_bwd_impl = v; }
 
 extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int T, int H,
                               int hd, long long ldq, long long ldk, long long ldv, long long ldo, float scale,
-                              int causal, hipStream_t s) {
-  const int impl = g_attn_impl == 0 ? ((hd == 64 || hd == 128) ? 4 : 1) : g_attn_impl;
+                              int causal, int impl_req, hipStream_t s) {
+  const int impl = impl_req == 0 ? ((hd == 64 || hd == 128) ? 4 : 1) : impl_req;
   if ((impl == 4 || (impl == 5 && g_attn_diag)) && (hd == 64 || hd == 128)) {
-    const int nqb = (T + 127) / 128, items = (B * H + 7) / 8 * 8 * ((nqb + 1) / 2);
-    const int per_cu = hd == 64 ? 3 : 1;           // resident blocks per CU (VGPRs / LDS)
-    const int grid = g_attn_fwd_persist ? std::min(items, std::max(8, attn_cu_count() * per_cu / 8 * 8)) : items;
+    // one workgroup per item (the dispatcher refills freed slots, which balances the end of
+    // the kernel; a persistent grid measured slower)
+    const int nqb = (T + 127) / 128, grid = (B * H + 7) / 8 * 8 * ((nqb + 1) / 2);
     if (hd == 64 && impl == 5)
       attn_fwd3_k<64, 1><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, T, H,
                                               B * H, ldq, ldk, ldv, ldo, scale, causal, g_attn_diag);
@@ -2053,16 +2029,22 @@ extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void*
 }
 
 // delta: workspace [2][B, H, T] fp32: -delta (rowsum(dO*O)) and -lse/scale, written by the dQ kernel.
+// Backward kernel pair (`impl`): 0 = auto (4 at head_dim 64 / 128, 2 otherwise), 2 =
+// attn_bwd_dq_k + attn_bwd_dkdv2_k (16x16x32, LDS-DMA ring), 4 = attn_bwd_dq3_k +
+// attn_bwd_dkdv3_k (32x32x16, query / key on the lane, hd 64 / 128), 5 = 4 with the dK/dV DIAG
+// build (hd 64, into the attn_diag buffer).  (Round 4 retired the register-staged dK/dV
+// kernels, impl 1 / 3.)
 extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o,
                               const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int T, int H,
                               int hd, long long lddo, long long ldq, long long ldk, long long ldv, long long ldo,
                               long long lddq, long long lddk, long long lddv, float scale, int causal,
                               const int64_t* rope_pos, const float* rope_tab, hipStream_t s, float* dbias,
-                              float* bws) {
+                              float* bws, int impl_req) {
   // The QKV bias gradient rides on both kernel pairs' epilogues (per-wave column sums + one
   // reduction kernel).
   const bool v3ok = hd == 64 || hd == 128;
-  const int bimpl = g_attn_bwd_impl == 0 ? (v3ok ? 4 : 2) : g_attn_bwd_impl;
+  const bool diag = impl_req == 5 && g_attn_diag != nullptr;
+  const int bimpl = impl_req == 0 ? (v3ok ? 4 : 2) : (impl_req == 5 ? 4 : impl_req);
   const bool bias = dbias != nullptr && bws != nullptr;
   const int nqb = (T + 127) / 128, nkb = (T + 63) / 64;
   float* pq = bias ? bws : nullptr;
@@ -2092,7 +2074,7 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
                                                    delta + (long long)B * H * T, delta, (bf16*)dk, (bf16*)dv, T, H,     \
                                                    B * H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal, rope_pos,     \
                                                    rope_tab, pk, pv, DG_ ? g_attn_diag : nullptr)
-    if (hd == 64 && g_attn_bwd_diag && g_attn_diag) DPFS_DKDV3(64, 1);
+    if (hd == 64 && diag) DPFS_DKDV3(64, 1);
     else if (hd == 64) DPFS_DKDV3(64, 0);
     else DPFS_DKDV3(128, 0);
 #undef DPFS_DKDV3

@@ -28,13 +28,12 @@ def _load():
     except Exception as e:  # pragma: no cover - depends on build state
         _ERR = e
         return
-    # A/B switches of the attention kernel generation, read once at load (same-box comparisons
-    # of whole-model runs; the per-head-dim defaults are the measured winners):
-    # DPFS_ATTN_IMPL (forward, csrc/kernels/attention.hip dpfs_attn_fwd) and
-    # DPFS_ATTN_BWD_IMPL (backward, dpfs_attn_bwd); 0 / unset = the default.
-    for var, fn in (("DPFS_ATTN_IMPL", "attn_set_impl"), ("DPFS_ATTN_BWD_IMPL", "attn_set_bwd_impl")):
-        if os.environ.get(var):
-            getattr(_C, fn)(int(os.environ[var]))
+    # The attention kernel generation is a per-call argument (``impl`` of attn_fwd / attn_bwd,
+    # 0 = the per-head-dim default, the measured winner).  For same-box A/B runs of whole models
+    # DPFS_ATTN_IMPL / DPFS_ATTN_BWD_IMPL, read once here, become the default of that argument.
+    fi, bi = int(os.environ.get("DPFS_ATTN_IMPL") or 0), int(os.environ.get("DPFS_ATTN_BWD_IMPL") or 0)
+    if fi or bi:
+        _C = _AttnImplDefaults(_C, fi, bi)
 
 
 def available() -> bool:
@@ -83,6 +82,25 @@ def debug_sync() -> bool:
 
 def nan_check() -> bool:
     return os.environ.get("DPFS_NAN_CHECK", "0") == "1"
+
+
+class _AttnImplDefaults:
+    """The native module with fixed default ``impl`` arguments for attn_fwd / attn_bwd (an
+    explicit ``impl=`` still wins); everything else passes through."""
+
+    def __init__(self, mod, fwd_impl: int, bwd_impl: int):
+        self._mod, self._fi, self._bi = mod, fwd_impl, bwd_impl
+
+    def attn_fwd(self, *args, **kw):
+        kw.setdefault("impl", self._fi)
+        return self._mod.attn_fwd(*args, **kw)
+
+    def attn_bwd(self, *args, **kw):
+        kw.setdefault("impl", self._bi)
+        return self._mod.attn_bwd(*args, **kw)
+
+    def __getattr__(self, name):
+        return getattr(self._mod, name)
 
 
 class _DebugProxy:

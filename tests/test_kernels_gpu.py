@@ -192,23 +192,19 @@ def test_cross_entropy_kernels(C, V, valid, start):
                                       (1, 1000, 2, 64), (1, 1000, 2, 128), (2, 384, 2, 128)])
 @pytest.mark.parametrize("impl", [1, 4])
 def test_attention(C, B, T, H, hd, impl):
-    C.attn_set_impl(impl)            # forward: 16x16x32 register-staged / 32x32x16 LDS-DMA ring
-    C.attn_set_bwd_impl(4 if impl == 4 else 2)   # backward pair: 16x16x32 / 32x32x16 key-on-lane
-    try:
-        _check_attention(C, B, T, H, hd)
-    finally:
-        C.attn_set_impl(0)
-        C.attn_set_bwd_impl(0)
+    # per call: forward 16x16x32 register-staged / 32x32x16 LDS-DMA ring, backward pair
+    # 16x16x32 / 32x32x16 key-on-lane (hd 32 has only the first of each)
+    _check_attention(C, B, T, H, hd, impl, 4 if impl == 4 else 2)
 
 
-def _check_attention(C, B, T, H, hd):
+def _check_attention(C, B, T, H, hd, fimpl=0, bimpl=0):
     torch.manual_seed(10)
     qkv = torch.randn(B * T, 3 * H * hd, device=DEV).bfloat16()
     q = qkv[:, : H * hd].view(B, T, H, hd)
     k = qkv[:, H * hd: 2 * H * hd].view(B, T, H, hd)
     v = qkv[:, 2 * H * hd:].view(B, T, H, hd)
     scale = 1 / math.sqrt(hd)
-    o, lse = C.attn_fwd(q, k, v, scale, True)
+    o, lse = C.attn_fwd(q, k, v, scale, True, impl=fimpl)
     orf, lser = R.attn_fwd(q.float(), k.float(), v.float(), scale, True)
     assert _rel(o, orf) < 2e-2
     assert (lse - lser).abs().max().item() < 2e-2
@@ -217,7 +213,7 @@ def _check_attention(C, B, T, H, hd):
     dq = dqkv[:, : H * hd].view(B, T, H, hd)
     dk = dqkv[:, H * hd: 2 * H * hd].view(B, T, H, hd)
     dv = dqkv[:, 2 * H * hd:].view(B, T, H, hd)
-    C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv)
+    C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv, impl=bimpl)
     rq, rk, rv = (torch.empty(B, T, H, hd, device=DEV) for _ in range(3))
     R.attn_bwd(do.float(), q.float(), k.float(), v.float(), o.float(), lse, scale, True, rq, rk, rv)
     assert _rel(dq, rq) < 3e-2 and _rel(dk, rk) < 3e-2 and _rel(dv, rv) < 3e-2
@@ -238,11 +234,7 @@ def test_attention_fwd_rescale_branch(C, impl, hd):
         k[:, t] = 4 * q[:, t + 3 if t + 3 < T else t]
     v = torch.randn(B, T, H, hd, device=DEV)
     q, k, v = q.bfloat16(), k.bfloat16(), v.bfloat16()
-    C.attn_set_impl(impl)
-    try:
-        o, lse = C.attn_fwd(q, k, v, 1 / math.sqrt(hd), True)
-    finally:
-        C.attn_set_impl(0)
+    o, lse = C.attn_fwd(q, k, v, 1 / math.sqrt(hd), True, impl=impl)
     orf, lser = R.attn_fwd(q.float(), k.float(), v.float(), 1 / math.sqrt(hd), True)
     assert _rel(o, orf) < 2e-2, _rel(o, orf)
     assert (lse - lser).abs().max().item() < 5e-2 * max(1.0, lser.abs().max().item() / 10)

@@ -22,14 +22,12 @@ def main():
     ap.add_argument("--impl", type=int, nargs="+", default=[4])
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--bwd", action="store_true")
-    ap.add_argument("--persist", type=int, default=1, help="forward v3: persistent grid (1) or one block per item (0)")
     ap.add_argument("--diag", action="store_true",
                     help="forward v3 DIAG build (impl 5): per-wave s_memtime split wait / QK+max / exp+pack / PV")
-    ap.add_argument("--ab", default=None, help="backward: name of an int kernel switch of _C to A/B (e.g. attn_bwd_er)")
+    ap.add_argument("--ab", default=None, help="name of a temporary int kernel switch of _C to A/B (forward or --bwd)")
     ap.add_argument("--ab-vals", type=int, nargs="+", default=[0, 1])
     a = ap.parse_args()
     C = _ext.require()
-    C.attn_fwd_persist(a.persist)
     B, T, H, hd = a.B, a.T, a.H, a.hd
     qkv = torch.randn(B * T, 3 * H * hd, device="cuda").bfloat16()
     q, k, v = (qkv[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
@@ -43,33 +41,27 @@ def main():
 
     def mk(impl):
         def g():
-            C.attn_set_impl(impl)
-            C.attn_set_bwd_impl(impl if a.bwd else 0)
             if a.bwd:
-                C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv)
+                C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv, impl=impl)
             else:
-                C.attn_fwd(q, k, v, scale, True)
+                C.attn_fwd(q, k, v, scale, True, impl=impl)
         return g
     if not a.bwd:   # forward outputs of every implementation against impl 1
-        C.attn_set_impl(1)
-        o1, l1 = C.attn_fwd(q, k, v, scale, True)
+        o1, l1 = C.attn_fwd(q, k, v, scale, True, impl=1)
         for impl in a.impl:
-            C.attn_set_impl(impl)
-            oi, li = C.attn_fwd(q, k, v, scale, True)
+            oi, li = C.attn_fwd(q, k, v, scale, True, impl=impl)
             print(f"impl {impl} vs 1: max|dO| {(oi.float() - o1.float()).abs().max().item():.3e} "
                   f"max|dLSE| {(li - l1).abs().max().item():.3e}", flush=True)
     if a.diag and not a.bwd:
         grid = ((T + 127) // 128) * B * H
         d = torch.zeros(grid * 40, dtype=torch.int64, device="cuda")
         C.attn_diag(d)
-        C.attn_set_impl(5)
-        C.attn_fwd(q, k, v, scale, True)
+        C.attn_fwd(q, k, v, scale, True, impl=5)
         torch.cuda.synchronize()
-        C.attn_set_impl(0)
         C.attn_diag(torch.empty(0))
         torch.save(d.cpu(), os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", "attn_diag.pt"))
         w10 = d.view(-1, 10).double()
-        w10 = w10[w10[:, 7] > 0]                # the persistent grid uses fewer blocks than the item count
+        w10 = w10[w10[:, 7] > 0]                # (rows of the buffer past the grid stay zero)
         pro = w10[:, 8]
         w8 = w10[:, :8]
         print(f"DIAG per wave, block prologues {pro.mean():.0f} ticks, epilogues {w10[:, 9].mean():.0f} ticks", flush=True)
@@ -101,11 +93,8 @@ def main():
         items = (B * H + 7) // 8 * 8 * (((T + 127) // 128 + 1) // 2)
         d = torch.zeros(items * 4 * 10, dtype=torch.int64, device="cuda")
         C.attn_diag(d)
-        C.attn_bwd_diag(1)
-        C.attn_set_bwd_impl(4)
-        C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv)
+        C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv, impl=5)
         torch.cuda.synchronize()
-        C.attn_bwd_diag(0)
         C.attn_diag(torch.empty(0))
         w = d.view(-1, 10).double()
         w = w[w[:, 9] > 0]
@@ -123,9 +112,8 @@ def main():
 
         def mkf(x):
             def g():
-                C.attn_set_impl(4)
                 sw(x)
-                return C.attn_fwd(q, k, v, scale, True)
+                return C.attn_fwd(q, k, v, scale, True, impl=4)
             return g
         o0, l0 = mkf(a.ab_vals[0])()
         for x in a.ab_vals[1:]:
@@ -140,9 +128,8 @@ def main():
 
         def mkab(x):
             def g():
-                C.attn_set_bwd_impl(4)
                 sw(x)
-                C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv)
+                C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv, impl=4)
             return g
         vals = a.ab_vals
         mkab(vals[0])()
@@ -158,8 +145,6 @@ def main():
     res = timeit({impl: mk(impl) for impl in a.impl}, iters=a.iters, rounds=5)  # interleaved, median
     for impl, ms in res.items():
         print(f"impl {impl} {'bwd' if a.bwd else 'fwd'}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF", flush=True)
-    C.attn_set_impl(0)
-    C.attn_set_bwd_impl(0)
 
 
 if __name__ == "__main__":

@@ -95,16 +95,9 @@ def main():
             out = F.scaled_dot_product_attention(qt, kt, vt, is_causal=True)
             out.backward(do.transpose(1, 2))
 
-        def with_impl(f, impl):
-            def g():
-                C.attn_set_impl(impl)
-                f()
-                C.attn_set_impl(1)
-            return g
         t = timeit({
             "fwd": lambda: C.attn_fwd(q, k, v, scale, True),
-            "fwd_dma8": with_impl(lambda: C.attn_fwd(q, k, v, scale, True), 2),
-            "fwd_w4": with_impl(lambda: C.attn_fwd(q, k, v, scale, True), 3),
+            "fwd_r1": lambda: C.attn_fwd(q, k, v, scale, True, impl=1),
             "fwd_ref": lambda: F.scaled_dot_product_attention(qt.detach(), kt.detach(), vt.detach(), is_causal=True),
             "bwd": lambda: C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv),
             "fwdbwd_ref": ref_fb,
