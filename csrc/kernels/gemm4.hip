@@ -977,7 +977,10 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
     a_bytes = b_bytes = a2_bytes = b2_bytes = 0u;
   }
   // FAST (descriptor-advancing DMA stream): every item's K range a multiple of 64
-  const bool fast = g_g4_sched != 2 && K % 64 == 0 && kps % 64 == 0 && (!A2 || k_switch % 64 == 0);
+  // (not under the zero-operand ablation: FAST's per-item record counts are the bytes past the
+  // item's K offset, which a zero-record descriptor would underflow)
+  const bool fast = g_g4_sched != 2 && !(g_g4_ablate & 2) && K % 64 == 0 && kps % 64 == 0 &&
+                    (!A2 || k_switch % 64 == 0);
   const int sched = g_g4_sched == 1 ? 0 : 1;
 #define DPFS_G4_ARGS                                                                                            \
   (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb, \
