@@ -520,7 +520,10 @@ __device__ __forceinline__ void epilogue_swb(const Item& ci, int M, int F, const
 }
 
 // OUT: 0 = bf16 C (+ fp32 bias[n], + RoPE); 1 = fp32 C / split-K slab.
-// dbg (timing-only ablations, tools/gemm4_probe.py): 4 = no DMA wait, 8 = no step barrier.
+// DIAG: 0 = production; 1 / 2 = the timing builds (per-wave s_memtime split; 2 without DMA);
+// 3 = the ablation build that reads `dbg` (timing-only, tools/gemm4_probe.py): 4 = no DMA
+// wait, 8 = no step barrier.  Only DIAG 3 tests dbg, so the production step has no runtime
+// branch on it.
 // FAST (every item's K range a multiple of 64, so no step reads past K): the DMA stream
 // advances the buffer descriptors' base address and record count by SALU once per stage
 // (hipBLASLt's form) and every piece reuses its per-item lane offset: no VALU, no per-lane
@@ -543,6 +546,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
                                                   unsigned long long* diag, SwiOut swo = SwiOut{},
                                                   SwiBwd swb = SwiBwd{}) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_TOTAL];
+  constexpr bool TIMED = DIAG == 1 || DIAG == 2;   // the s_memtime builds
   constexpr int NJ = BN / 32;                  // 16-column MFMA tiles per wave
   constexpr int NBQ = BN / 64;                 // B pieces per wave per stage
   constexpr int NQ = 4 + NBQ;                  // DMA pieces per wave per stage
@@ -719,7 +723,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   wait_vmcnt<2 * NQ>();
   __builtin_amdgcn_s_barrier();
   read_frags<AK, BKM, BN>(F0, smem, wm, wn, l);
-  if constexpr (DIAG) t_mark = stamp();
+  if constexpr (TIMED) t_mark = stamp();
 
   // One consumer step on `cur`, prefetching the next step's fragments into `nxt`.
   // Entry wait: stage s+1 landed for this wave (younger: stage s+2 = NQ pieces, plus the
@@ -728,7 +732,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
                   int bcol0) {
     constexpr bool ZR = decltype(zero)::value;
     constexpr bool NOPF = decltype(nopf)::value;   // no next-step fragment reads (item end, SWB)
-    if constexpr (DIAG) {
+    if constexpr (TIMED) {
       const unsigned long long t = stamp();
       t_body += t - t_mark;
       t_mark = t;
@@ -737,11 +741,11 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
     cur.a.pin();
     cur.b.pin();
-    if (dbg & 4) wait_vmcnt<63>();   // timing-only: no wait for the DMA (wrong results)
+    if (DIAG == 3 && (dbg & 4)) wait_vmcnt<63>();   // timing-only: no wait for the DMA (wrong results)
     else if (first) wait_vmcnt<(NQ + STORES < 63 ? NQ + STORES : 63)>();
     else wait_vmcnt<NQ>();
-    if (!(dbg & 8)) __builtin_amdgcn_s_barrier();
-    if constexpr (DIAG) {
+    if (!(DIAG == 3 && (dbg & 8))) __builtin_amdgcn_s_barrier();
+    if constexpr (TIMED) {
       const unsigned long long t = stamp();
       t_wait += t - t_mark;
       t_mark = t;
@@ -822,7 +826,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
       step(F0, F1, false, NO, NO, false, bcol0);
       step(F1, F0, false, NO, NO, t + 2 >= nk, bcol0);
     }
-    if constexpr (DIAG) {
+    if constexpr (TIMED) {
       const unsigned long long t = stamp();
       t_body += t - t_mark;
       t_mark = t;
@@ -832,13 +836,13 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
       epilogue<OUT, BN, ROPE, true, SWIGLU>(bias_lds, ci, C, rope, M, N, ldc, slab_stride, c_bytes, wm, wn, l, swo);
     else
       epilogue<OUT, BN, ROPE, false, SWIGLU>(bias_lds, ci, C, rope, M, N, ldc, slab_stride, c_bytes, wm, wn, l, swo);
-    if constexpr (DIAG) {
+    if constexpr (TIMED) {
       const unsigned long long t = stamp();
       t_epi += t - t_mark;
       t_mark = t;
     }
   }
-  if constexpr (DIAG) {
+  if constexpr (TIMED) {
     if (l == 0) {
       unsigned long long* d = diag + (blockIdx.x * 4 + wave) * 4;
       d[0] = t_wait;
@@ -874,6 +878,8 @@ static int g_g4_group_m = 4;
 // Timing-only ablations (tools/gemm4_probe.py --ablate): bit 1 = output descriptor with zero
 // records (every store dropped), bit 2 = operand descriptors with zero records (every DMA
 // returns zeros, no memory traffic), 4 = no DMA wait, 8 = no step barrier (wrong results).
+// Bits 4 / 8 (and 1024: none) run the DIAG-3 build of the NT 256-wide kernel, the only one
+// that reads them.
 static int g_g4_ablate = 0;
 static unsigned long long* g_g4_diag = nullptr;   // [grid][4 waves][wait, body, epilogue, valid]
 extern "C" void dpfs_gemm4_ablate(int v) { g_g4_ablate = v; }
@@ -1020,6 +1026,13 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
     gemm4_k<true, true, 0, 2, true, 1><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda,
                                                             ldb, ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb,
                                                             rope, g_g4_group_m, dual, g_g4_ablate & ~51, g_g4_diag);
+    return true;
+  }
+  if ((g_g4_ablate & (4 | 8 | 1024)) && layout == 0 && !out_f32 && bn == 256 && fast && rope_cols == 0) {
+    // the ablation build (1024: the same build with no ablation, the cost of its branches)
+    gemm4_k<true, true, 0, 3, true, 1><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda,
+                                                            ldb, ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb,
+                                                            rope, g_g4_group_m, dual, g_g4_ablate, nullptr);
     return true;
   }
   if ((g_g4_ablate & 16) && g_g4_diag && layout == 0 && !out_f32 && bn == 256 && fast) {
