@@ -414,6 +414,11 @@ extern "C" void dpfs_swiglu_bwd_dbias(int dtype, const void* dh, const void* gu,
 extern "C" void dpfs_colsum_rows_small(const float* part, float* out, int rows, int N, hipStream_t s) {
   colsum_rows(part, out, rows, N, s);
 }
+// ... with columns >= split going to out2 (one launch for two side-by-side column sums).
+extern "C" void dpfs_colsum_rows_split(const float* part, float* out, float* out2, int split, int rows, int N,
+                                       hipStream_t s) {
+  colsum_rows(part, out, rows, N, s, out2, split);
+}
 
 extern "C" int dpfs_colsum_plan(int M, int cblocks, int target_blocks, int* rpc) {
   return colsum_plan(M, cblocks, target_blocks, rpc);

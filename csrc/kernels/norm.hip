@@ -308,16 +308,19 @@ int norm_bwd_grid(int M) {
 using namespace dpfs;
 
 extern "C" void dpfs_colsum_f32(const float* x, float* out, float* ws, int M, int N, hipStream_t s);
+extern "C" void dpfs_colsum_rows_small(const float* part, float* out, int rows, int N, hipStream_t s);
+extern "C" void dpfs_colsum_rows_split(const float* part, float* out, float* out2, int split, int rows, int N,
+                                       hipStream_t s);
 extern "C" void dpfs_colsum_f32_split(const float* x, float* out, float* out2, int split, float* ws, int M, int N,
                                       hipStream_t s);
 extern "C" long long dpfs_colsum_ws(int M, int N);
 
 extern "C" int dpfs_norm_bwd_grid(int M) { return norm_bwd_grid(M); }
-// Total fp32 workspace of dpfs_norm_bwd: block partials (x2 for LayerNorm) + stage-2 partials.
+// Total fp32 workspace of dpfs_norm_bwd: the block partials (x2 for LayerNorm / mode 2).
 extern "C" long long dpfs_norm_bwd_ws(int mode, int M, int D) {
   const int G = norm_bwd_grid(M);
   const int cols = D * (mode != 0 ? 2 : 1);
-  return (long long)G * cols + dpfs_colsum_ws(G, cols);
+  return (long long)G * cols;
 }
 
 extern "C" void dpfs_rmsnorm_fwd(int dtype, const void* x, const float* w, void* y, float* rstd, int M, int D,
@@ -373,9 +376,8 @@ extern "C" void dpfs_norm_bwd(int mode, int dtype, const void* dy, const void* x
     if (mode == 0) DPFS_NB(float, 0); else if (mode == 1) DPFS_NB(float, 1); else DPFS_NB(float, 2);
   }
 #undef DPFS_NB
-  // Stage 2 (fixed-order 2-D column reduction over the G block partials).  The workspace
-  // for its own partials lives after the G*D block partials (dpfs_norm_bwd_ws).
-  float* ws2 = partial_w + (size_t)G * D * (mode != 0 ? 2 : 1);
-  if (mode != 0) dpfs_colsum_f32_split(partial_w, dw, db, D, ws2, G, 2 * D, s);
-  else dpfs_colsum_f32(partial_w, dw, ws2, G, D, s);
+  // Stage 2: one fixed-order column reduction of the G (<= 1024) block partials, 64 row lanes
+  // per column group (a chunked two-launch reduction cost ~2x its time at these sizes).
+  if (mode != 0) dpfs_colsum_rows_split(partial_w, dw, db, D, G, 2 * D, s);
+  else dpfs_colsum_rows_small(partial_w, dw, G, D, s);
 }
