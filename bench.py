@@ -97,8 +97,12 @@ def measure(a, tp: int, world: int, dev, first: bool):
 
     p = init_dist_env(rank=None, tp_size=tp, dp_size=world // tp, timeout_s=a.pg_timeout_s) if first \
         else pm.init_pgm(tp, world // tp)
-    inject = os.environ.get("DPFS_BENCH_INJECT", "")    # test hook: "raise:<rank>" | "hang:<rank>"
-    if not first and inject and int(inject.split(":")[1]) == dist.get_rank():
+    # test hooks: "raise:<rank>" | "hang:<rank>" in the pure-TP layout, "raise_head" in the
+    # headline layout on every rank
+    inject = os.environ.get("DPFS_BENCH_INJECT", "")
+    if first and inject == "raise_head" and tp > 1:
+        raise RuntimeError("injected failure in the headline layout")
+    if not first and inject and inject != "raise_head" and int(inject.split(":")[1]) == dist.get_rank():
         if inject.startswith("raise"):
             raise RuntimeError("injected failure in the pure-TP layout")
         time.sleep(3600)
@@ -247,7 +251,22 @@ def main():
         torch.cuda.set_device(lr % torch.cuda.device_count() if os.environ.get("DPFS_BACKEND") == "gloo" else lr)
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
 
-    head = measure(a, tp, world, dev, first=True)
+    try:
+        head = measure(a, tp, world, dev, first=True)
+    except Exception as e:   # noqa: BLE001
+        # The TP x DP layout failed on every rank alike (an exception, not a hang: a hang ends
+        # at the process-group timeout): measure pure data parallelism instead, so the run
+        # still yields a scaling point, and report the failure next to it.
+        if world == 1 or tp == 1 or a.impl != "ours" or not dist.is_initialized():
+            raise
+        err = f"{type(e).__name__}: {e}"[:500]
+        print(f"[bench] headline layout tp{tp}dp{world // tp} failed ({err}); measuring dp{world}",
+              file=sys.stderr, flush=True)
+        from distributed_pytorch_from_scratch_amd.parallel import tp_comm
+        tp_comm.reset()
+        head = measure(a, 1, world, dev, first=False)
+        head["headline_error"] = {"parallelism": f"tp{tp}dp{world // tp}", "error": err}
+        a.pure_tp = False
     rank = dist.get_rank()
     out = report(a, head, [head], world, dev)
     # The reference trains with tp_size == world_size (process_manager.py:13-15, recipe.sh TP 1 /
@@ -366,6 +385,8 @@ def report(a, head, layouts, world, dev):
         "mfu_vs_2.5pf_dense_bf16": round(value * mflops / world / 2.5e15, 4),
         "final_loss": round(head["final_loss"], 4),
     }
+    if head.get("headline_error"):
+        out["headline_error"] = head["headline_error"]
     if world > 1:
         out["layouts"] = [{"parallelism": L["parallelism"], "value": round(L["value"], 1),
                            "ms_per_step": round(1000 * L["elapsed"] / a.steps, 3),
