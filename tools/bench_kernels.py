@@ -19,9 +19,17 @@ from distributed_pytorch_from_scratch_amd.ops import _ext  # noqa: E402
 
 
 def timeit(fns, iters=20, rounds=5):
+    """Interleaved timing, median over rounds.  One untimed pass over every arm first, and the
+    arm order rotates per round: the arm timed first in a round read ~2.5 % slow
+    (profiles/r4_kernel_experiments.txt item 18)."""
     res = {k: [] for k in fns}
-    for _ in range(rounds):
-        for k, f in fns.items():
+    keys = list(fns)
+    for f in fns.values():
+        f()
+    torch.cuda.synchronize()
+    for rd in range(rounds):
+        for k in keys[rd % len(keys):] + keys[:rd % len(keys)]:
+            f = fns[k]
             f()
             torch.cuda.synchronize()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -166,8 +166,9 @@ def main():
                 [f"abl{x}" for x in a.ablate] + ["v3"] + \
                 ([] if a.no_blas else ["blas"])
             ts = {k: [] for k in arms}
-            for _ in range(a.rounds):
-                for k in arms:
+            for rd in range(a.rounds):
+                # (the arm order rotates per round: the first-timed arm of a round reads slow)
+                for k in arms[rd % len(arms):] + arms[:rd % len(arms)]:
                     if k.startswith("v4s"):
                         set_variant(1)
                         C.gemm4_sched(int(k[3:]))
