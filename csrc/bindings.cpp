@@ -169,6 +169,17 @@ torch::Tensor gemm_out(const c10::optional<torch::Tensor>& out, const torch::Ten
   return *out;
 }
 
+// NT output: `out` may also be a row-major column slice of a wider buffer (unit column stride,
+// row stride >= N and a multiple of 8), e.g. the V columns of the packed QKV output.
+torch::Tensor gemm_out_rows(const c10::optional<torch::Tensor>& out, const torch::Tensor& a, int64_t M, int64_t N) {
+  if (!out.has_value() || !out->defined()) return torch::empty({M, N}, a.options());
+  check_cuda(*out, "out");
+  TORCH_CHECK(out->dim() == 2 && out->size(0) == M && out->size(1) == N && out->scalar_type() == a.scalar_type() &&
+                  (N <= 1 || out->stride(1) == 1) && out->stride(0) >= N && out->stride(0) % 8 == 0,
+              "gemm_nt: out must be a row-major [M, N] tensor (or column slice) of the operand dtype");
+  return *out;
+}
+
 torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> bias,
                       c10::optional<torch::Tensor> rope_pos, c10::optional<torch::Tensor> rope_tab,
                       int64_t rope_heads, int64_t rope_hd, c10::optional<torch::Tensor> out, int64_t variant) {
@@ -181,10 +192,11 @@ torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
   TORCH_CHECK(K % 8 == 0, "gemm_nt: K must be a multiple of 8, got ", K);
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm_nt: row strides must be multiples of 8");
   const at::DeviceGuard g(a.device());
-  auto c = gemm_out(out, a, M, N);
+  auto c = gemm_out_rows(out, a, M, N);
   if (M == 0 || N == 0) return c;
   if (K == 0) return c.zero_();
   TORCH_CHECK(N % 4 == 0, "gemm_nt: N must be a multiple of 4, got ", N);
+  const int ldc = (int)(M > 1 ? c.stride(0) : N);
   const long long wsn = dpfs_gemm_bf16_ws((int)M, (int)N, (int)K);
   torch::Tensor ws;
   if (wsn > 0) ws = torch::empty({wsn}, a.options().dtype(torch::kFloat32));
@@ -197,11 +209,12 @@ torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
                     rope_tab->size(1) == rope_hd,
                 "gemm_nt: rope_tab must be fp32 [maxlen, hd]");
     dpfs_gemm_nt_rope(a.data_ptr(), b.data_ptr(), c.data_ptr(), opt_f32(bias, N, "bias"), (int)M, (int)N, (int)K,
-                      (int)a.stride(0), (int)b.stride(0), (int)N, rope_pos->data_ptr<int64_t>(),
+                      (int)a.stride(0), (int)b.stride(0), ldc, rope_pos->data_ptr<int64_t>(),
                       rope_tab->data_ptr<float>(), (int)(rope_heads * rope_hd), (int)rope_hd, (int)variant, stream());
   } else {
+    TORCH_CHECK(!want_rope || ldc == N, "gemm_nt: the separate RoPE pass needs a contiguous output");
     dpfs_gemm_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), opt_f32(bias, N, "bias"), (int)M, (int)N, (int)K,
-                 (int)a.stride(0), (int)b.stride(0), (int)N, (int)variant, stream());
+                 (int)a.stride(0), (int)b.stride(0), ldc, (int)variant, stream());
     if (want_rope) rope_(c, *rope_pos, *rope_tab, rope_heads, rope_hd, false);
   }
   dpfs_gemm_set_workspace(nullptr, 0);

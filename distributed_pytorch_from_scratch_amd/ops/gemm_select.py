@@ -320,13 +320,29 @@ def gemm_nt_rope(k, x: torch.Tensor, w: torch.Tensor, bias, pos, tab, rot_heads:
 
     def ours(variant: int = 0):
         return k.gemm_nt(x, w, bias, pos, tab, rot_heads, hd, variant=variant)
+
+    # The rotated Q|K columns and the V columns as two launches into one output: at GPT-2
+    # small's 2304 columns one launch is 1152 tiles of 256 x 256 = 4.5 rounds of the CUs, the
+    # pair 768 tiles (3 rounds) + 512 tiles of 256 x 192 (2 rounds of 3/4 the work).
+    rot = rot_heads * hd
+    split_ok = 0 < rot < N and rot % 256 == 0 and (N - rot) % 64 == 0 and w.is_contiguous() and \
+        os.environ.get("DPFS_QKV_SPLIT", "1") != "0"
+
+    def ours_split():
+        y = torch.empty(M, N, device=x.device, dtype=x.dtype)
+        k.gemm_nt(x, w[:rot], bias[:rot] if bias is not None else None, pos, tab, rot_heads, hd, out=y[:, :rot])
+        k.gemm_nt(x, w[rot:], bias[rot:] if bias is not None else None, out=y[:, rot:])
+        return y
     if m == "blas":
         return blas()
     if m == "lt":
         return lt(0)() if lt_ok and _lt_count(k, 0, M, N, K, bias is not None) else blas()
     key = ("nt_rope", M, N, K, hd, x.device.index)
-    c = _pick(key, {**_ours_variants(ours), **({"blas": blas} if _lib() else {})},
+    c = _pick(key, {**_ours_variants(ours), **({"ours_split": ours_split} if split_ok else {}),
+                    **({"blas": blas} if _lib() else {})},
               lambda: _lt_count(k, 0, M, N, K, bias is not None), lt if lt_ok else None)
+    if c == "ours_split":
+        return ours_split()
     if c.startswith("ours") or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
         return _run_ours(ours, c)
     return blas() if c == "blas" else lt(_lt_index(c))()

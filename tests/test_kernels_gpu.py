@@ -748,6 +748,26 @@ def test_gemm_v4_split_k_bf16_long_k(C):
 
 
 
+@pytest.mark.parametrize("M,K", [(4096, 768), (300, 256)])
+def test_gemm_nt_column_slice_out(C, M, K):
+    """The packed QKV projection as two launches into one buffer (ops/gemm_select.gemm_nt_rope
+    "ours_split"): the rotated Q|K columns (RoPE epilogue) and the V columns written through
+    row-strided column slices are bit-identical to the single fused launch."""
+    torch.manual_seed(46)
+    H, hd = 12, 64
+    N, rot = 3 * H * hd, 2 * H * hd
+    x = (torch.randn(M, K, device=DEV) / 4).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / 4).bfloat16()
+    b = torch.randn(N, device=DEV)
+    pos = torch.arange(M, device=DEV) % 1024
+    tab = R.rope_table(1024, hd, 10000.0, device=DEV)
+    ref = C.gemm_nt(x, w, b, pos, tab, 2 * H, hd)
+    y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    C.gemm_nt(x, w[:rot], b[:rot], pos, tab, 2 * H, hd, out=y[:, :rot])
+    C.gemm_nt(x, w[rot:], b[rot:], out=y[:, rot:])
+    assert torch.equal(y, ref)
+
+
 @pytest.mark.parametrize("M,F_,K,with_bias", [(4096, 2048, 768, True), (1000, 256, 512, False)])
 def test_gemm_nt_swiglu_epilogue(C, M, F_, K, with_bias):
     """Gate|up GEMM with SwiGLU in the epilogue (gemm4.hip SwiOut): the natural [gate | up]
