@@ -325,8 +325,10 @@ def gemm_nt_rope(k, x: torch.Tensor, w: torch.Tensor, bias, pos, tab, rot_heads:
     # small's 2304 columns one launch is 1152 tiles of 256 x 256 = 4.5 rounds of the CUs, the
     # pair 768 tiles (3 rounds) + 512 tiles of 256 x 192 (2 rounds of 3/4 the work).
     rot = rot_heads * hd
-    split_ok = 0 < rot < N and rot % 256 == 0 and (N - rot) % 64 == 0 and w.is_contiguous() and \
-        os.environ.get("DPFS_QKV_SPLIT", "1") != "0"
+    # (only where the rotation is fused into the Q|K launch's epilogue: the separate RoPE pass
+    # of other head dims needs a contiguous output)
+    split_ok = hd in (64, 128) and 0 < rot < N and rot % 256 == 0 and (N - rot) % 64 == 0 and \
+        w.is_contiguous() and os.environ.get("DPFS_QKV_SPLIT", "1") != "0"
 
     def ours_split():
         y = torch.empty(M, N, device=x.device, dtype=x.dtype)
