@@ -58,7 +58,9 @@ def parse():
     ap.add_argument("--impl", choices=["ours", "reference"], default="ours")
     ap.add_argument("--layers", type=int, default=None, help="debug only: not a valid headline number")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--recompute", action="store_true", help="activation recompute (layer inputs only)")
+    ap.add_argument("--recompute", nargs="?", const="on", default="auto", choices=["auto", "on", "off"],
+                    help="activation recompute (layer inputs only); auto = the HBM planner's choice "
+                         "(utils/memory.py: on only when the layout does not fit without it)")
     ap.add_argument("--no-pure-tp", dest="pure_tp", action="store_false",
                     help="at N > 1 with a TP x DP headline layout, skip the extra pure-TP (tp = N) measurement")
     ap.add_argument("--pure-tp-budget-s", type=float, default=float(os.environ.get("DPFS_PURE_TP_BUDGET_S", "180")),
@@ -113,8 +115,6 @@ def measure(a, tp: int, world: int, dev, first: bool):
     overrides = dict(sequence_parallel=tp > 1 and a.sp != "off")
     if a.layers:
         overrides["num_layers"] = a.layers
-    if a.recompute:
-        overrides["recompute"] = True
     if a.fp8:
         overrides["fp8"] = True
     args = get_preset(a.model, **overrides)
@@ -124,6 +124,16 @@ def measure(a, tp: int, world: int, dev, first: bool):
     assert gb % p.dp_size == 0, f"global batch {gb} not divisible by DP {p.dp_size}"
     lb = gb // p.dp_size          # sequences per TP group (= per DP replica) per step
     V = args.vocab_size
+    # HBM plan (utils/memory.py) before anything is allocated: recompute on only where the
+    # layout does not fit without it; a layout that does not fit at all is refused here.
+    from distributed_pytorch_from_scratch_amd.utils import memory as MEM
+    lay = MEM.Layout(tp=tp, dp=p.dp_size, sp=False, seq=T, batch=lb, chunks=2 if tp > 1 else 1)
+    want = {"auto": None, "on": True, "off": False}[a.recompute]
+    free = MEM.device_free_bytes() if dev.type == "cuda" else None
+    rc, est = MEM.plan(args, lay, free, want) if a.impl == "ours" else (False, MEM.estimate(args, lay))
+    args.recompute = bool(rc)
+    if dev.type == "cuda":
+        torch.cuda.reset_peak_memory_stats(dev)
 
     set_seed(a.seed)
     # same synthetic data on every rank of a TP group, a different stream per DP replica
@@ -222,7 +232,9 @@ def measure(a, tp: int, world: int, dev, first: bool):
         value=gb * T * a.steps / elapsed, elapsed=elapsed, gb=gb, T=T, args=args,
         parallelism=f"tp{tp}" + (f"dp{p.dp_size}" if p.dp_size > 1 else "") + ("+sp" if sp_used else ""),
         final_loss=float(loss.float().item()), tp_comm=tp_comm.info(),
-        chunks=model.overlap_chunks() if a.impl == "ours" else None,
+        chunks=model.overlap_chunks() if a.impl == "ours" else None, recompute=bool(rc),
+        peak_mem_gb_est=round(est.gb(), 2),
+        peak_mem_gb=round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2) if dev.type == "cuda" else None,
         trial={f"{'sp' if k[0] else 'nosp'}/c{k[1]}": round(1000 * v, 2) for k, v in trial.items()} or None)
     del model, opt, pool
     if a.impl == "ours":
@@ -251,12 +263,14 @@ def main():
         torch.cuda.set_device(lr % torch.cuda.device_count() if os.environ.get("DPFS_BACKEND") == "gloo" else lr)
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
 
+    failed = False
     try:
         head = measure(a, tp, world, dev, first=True)
     except Exception as e:   # noqa: BLE001
         # The TP x DP layout failed on every rank alike (an exception, not a hang: a hang ends
-        # at the process-group timeout): measure pure data parallelism instead, so the run
-        # still yields a scaling point, and report the failure next to it.
+        # at the process-group timeout).  Pure data parallelism is measured for the record, but
+        # it is NOT the requested layout: the line carries value = null, the DP numbers under
+        # "fallback", the failure under "headline_error", and every rank exits 1.
         if world == 1 or tp == 1 or a.impl != "ours" or not dist.is_initialized():
             raise
         err = f"{type(e).__name__}: {e}"[:500]
@@ -267,8 +281,15 @@ def main():
         head = measure(a, 1, world, dev, first=False)
         head["headline_error"] = {"parallelism": f"tp{tp}dp{world // tp}", "error": err}
         a.pure_tp = False
+        failed = True
     rank = dist.get_rank()
     out = report(a, head, [head], world, dev)
+    if failed:
+        out["fallback"] = {"parallelism": out["config"]["parallelism"], "value": out["value"],
+                           "ms_per_step": out["ms_per_step"]}
+        out.update(value=None, ms_per_step=None, vs_baseline=None, tflops_per_gpu=None)
+        out["mfu_vs_2.5pf_dense_bf16"] = None
+        out["config"]["parallelism"] = head["headline_error"]["parallelism"]
     # The reference trains with tp_size == world_size (process_manager.py:13-15, recipe.sh TP 1 /
     # 2 / 4): at N > 1 the pure-TP layout is measured as well and reported next to the headline
     # layout (same contract: W warmup + K timed steps, max over ranks), each with its label.
@@ -324,6 +345,8 @@ def main():
         show_gemm_choices()
     dist.barrier()
     dist.destroy_process_group()
+    if failed:
+        sys.exit(1)
 
 
 def print_line(text: str):
@@ -338,10 +361,6 @@ def show_gemm_choices():
         from distributed_pytorch_from_scratch_amd.ops import gemm_select
         for key, v in sorted(gemm_select.choices(with_times=True).items(), key=str):
             print(f"[gemm] {key} -> {v}", file=sys.stderr, flush=True)
-    if os.environ.get("DPFS_BENCH_VERBOSE"):
-        from distributed_pytorch_from_scratch_amd.ops import gemm_select
-        for key, c in sorted(gemm_select.choices().items(), key=str):
-            print(f"gemm {key}: {c}", file=sys.stderr, flush=True)
 
 
 def report(a, head, layouts, world, dev):
@@ -374,7 +393,7 @@ def report(a, head, layouts, world, dev):
             "seq_len": T,
             "parallelism": head["parallelism"],
             "impl": a.impl,
-            "recompute": bool(a.recompute),
+            "recompute": head["recompute"],
             "fp8": bool(a.fp8),
             "params_matmul": args.matmul_params(),
             "tp_comm": head["tp_comm"],
@@ -384,6 +403,8 @@ def report(a, head, layouts, world, dev):
         "tflops_per_gpu": round(value * mflops / world / 1e12, 2),
         "mfu_vs_2.5pf_dense_bf16": round(value * mflops / world / 2.5e15, 4),
         "final_loss": round(head["final_loss"], 4),
+        "peak_mem_gb_est": head["peak_mem_gb_est"],
+        "peak_mem_gb": head["peak_mem_gb"],
     }
     if head.get("headline_error"):
         out["headline_error"] = head["headline_error"]

@@ -23,6 +23,7 @@ int dpfs_gemm_rope_fusable(int, int, int, int, int);
 void dpfs_gemm_nt_rope(const void*, const void*, void*, const float*, int, int, int, int, int, int, const int64_t*,
                        const float*, int, int, int, hipStream_t);
 void dpfs_gemm4_sched(int);
+void dpfs_gemm4_br(int);
 void dpfs_gemm4_group_m(int);
 void dpfs_gemm4_ablate(int);
 void dpfs_gemm4_diag(void*);
@@ -99,6 +100,7 @@ void* dpfs_xgmi_slot(void*, int);
 int dpfs_xgmi_open(void*, const void*);
 void dpfs_xgmi_set_blocks(void*, int);
 long long dpfs_xgmi_capacity(void*);
+long long dpfs_xgmi_one_shot_capacity(void*);
 int dpfs_xgmi_error(void*);
 void dpfs_xgmi_clear_error(void*);
 int dpfs_xgmi_run(void*, int, int, const void*, void*, long long, long long, double, int, hipStream_t);
@@ -686,14 +688,25 @@ torch::Tensor embedding_fwd(torch::Tensor ids, torch::Tensor weight, int64_t voc
   return out;
 }
 
-torch::Tensor embedding_bwd(torch::Tensor dout, torch::Tensor ids, int64_t v_local, int64_t vocab_start) {
+// fp32 dW[v_local, D] of the masked embedding; with ``out`` the rows are ADDED to it (the
+// engines' gradient arena: zeroed once per step, every chunk accumulates).
+torch::Tensor embedding_bwd(torch::Tensor dout, torch::Tensor ids, int64_t v_local, int64_t vocab_start,
+                            c10::optional<torch::Tensor> out) {
   check_rowmajor(dout, "dout");
   TORCH_CHECK(dout.is_contiguous(), "embedding_bwd: dout contiguous");
   TORCH_CHECK(ids.scalar_type() == torch::kInt64 && ids.is_contiguous() && ids.numel() == dout.size(0),
               "embedding_bwd: ids");
   const at::DeviceGuard g(dout.device());
   const int64_t M = dout.size(0), D = dout.size(1);
-  auto dw = torch::zeros({v_local, D}, dout.options().dtype(torch::kFloat32));
+  torch::Tensor dw;
+  if (out.has_value()) {
+    dw = *out;
+    TORCH_CHECK(dw.scalar_type() == torch::kFloat32 && dw.is_contiguous() && dw.dim() == 2 && dw.size(0) == v_local &&
+                    dw.size(1) == D && dw.device() == dout.device(),
+                "embedding_bwd: out must be contiguous fp32 [v_local, D] on the device of dout");
+  } else {
+    dw = torch::zeros({v_local, D}, dout.options().dtype(torch::kFloat32));
+  }
   if (M) dpfs_embedding_bwd(dcode(dout), dout.data_ptr(), ids.data_ptr<int64_t>(), dw.data_ptr<float>(), (int)M,
                             (int)D, vocab_start, (int)v_local, stream());
   return dw;
@@ -974,7 +987,8 @@ void xgmi_open(int64_t h, py::bytes all_handles) {
 }
 
 // op 0 all-reduce (out may be x), 1 reduce-scatter (out = x.numel()/W elements),
-// 2 all-gather (out = W * x.numel() elements); launched on the current stream.
+// 2 all-gather (out = W * x.numel() elements), 3 one-shot all-reduce (out may be x; up to the
+// one-shot capacity, unstaged); launched on the current stream.
 // A staging slot as a non-owning uint8 tensor of `cap` bytes on `device` (the communicator
 // owns the memory; the Python side keeps the communicator alive as long as the views).
 torch::Tensor xgmi_slot_tensor(int64_t h, int64_t slot, int64_t cap, torch::Device device) {
@@ -985,7 +999,7 @@ torch::Tensor xgmi_slot_tensor(int64_t h, int64_t slot, int64_t cap, torch::Devi
 
 void xgmi_run(int64_t h, int64_t op, torch::Tensor x, torch::Tensor out, int64_t world, double timeout_s,
               int64_t slot) {
-  TORCH_CHECK(op >= 0 && op <= 2, "xgmi_run: op");
+  TORCH_CHECK(op >= 0 && op <= 3, "xgmi_run: op");
   check_cuda(x, "x");
   check_cuda(out, "out");
   TORCH_CHECK(x.is_contiguous() && out.is_contiguous(), "xgmi_run: contiguous tensors");
@@ -998,7 +1012,11 @@ void xgmi_run(int64_t h, int64_t op, torch::Tensor x, torch::Tensor out, int64_t
   const int64_t n = x.numel();
   TORCH_CHECK(n > 0 && n % vec == 0, "xgmi_run: numel must be a positive multiple of ", vec);
   int64_t total, part;
-  if (op == 0) {
+  if (op == 3) {
+    TORCH_CHECK(out.numel() == n && slot < 0, "xgmi one-shot all_reduce: out numel, no staging");
+    total = n;
+    part = n;
+  } else if (op == 0) {
     TORCH_CHECK(out.numel() == n, "xgmi all_reduce: out numel");
     total = n;
     part = ((n + world * vec - 1) / (world * vec)) * vec;
@@ -1160,6 +1178,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "int64 buffer of the DIAG builds (attn_fwd / attn_bwd impl 5): per-wave s_memtime splits");
   m.def("gemm4_diag", [](torch::Tensor t) { dpfs_gemm4_diag(t.defined() && t.numel() ? t.data_ptr() : nullptr); },
         "int64 buffer [grid*4*4] for the DIAG build's per-wave cycle split (gemm4_ablate bit 16)");
+  m.def("gemm4_br", [](int v) { dpfs_gemm4_br(v); },
+        "rows of MFMAs before each step's barrier in the plain v4 kernels (0, 1, 2; A/B runs)");
   m.def("gemm4_sched", [](int v) { dpfs_gemm4_sched(v); },
         "v4 main-loop variant: 0 = default (descriptor-advancing DMA where K ranges allow, one piece per MFMA "
         "row), 1 = two pieces per row in rows 4-7, 2 = per-lane K checks everywhere (the pre-FAST stream)");
@@ -1202,7 +1222,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "flash attention backward; impl (per call): 0 = auto (dq3 + dkdv3 at hd 64 / 128, dq + dkdv2 at hd 32), "
         "2 = dq + dkdv2 (16x16x32), 4 = dq3 + dkdv3 (32x32x16), 5 = 4 with the dK/dV DIAG build");
   m.def("embedding_fwd", &embedding_fwd);
-  m.def("embedding_bwd", &embedding_bwd);
+  m.def("embedding_bwd", &embedding_bwd, py::arg("dout"), py::arg("ids"), py::arg("v_local"), py::arg("vocab_start"),
+        py::arg("out") = py::none());
   m.def("ce_fwd_stats", &ce_fwd_stats);
   m.def("ce_bwd", &ce_bwd, py::arg("logits"), py::arg("targets"), py::arg("lse"), py::arg("gscale"),
         py::arg("vocab_start"), py::arg("vocab_valid"), py::arg("out"), py::arg("dbias") = py::none());
@@ -1229,6 +1250,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xgmi_open", &xgmi_open, "map every peer's buffers (rank-ordered concatenated handle bytes)");
   m.def("xgmi_run", &xgmi_run, py::arg("h"), py::arg("op"), py::arg("x"), py::arg("out"), py::arg("world"),
         py::arg("timeout_s") = 120.0, py::arg("slot") = -1);
+  m.def("xgmi_one_shot_capacity", [](int64_t h) { return dpfs_xgmi_one_shot_capacity(xgmi_ptr(h)); });
   m.def("xgmi_slot_tensor", &xgmi_slot_tensor, py::arg("h"), py::arg("slot"), py::arg("cap"), py::arg("device"));
   m.def("xgmi_set_blocks", [](int64_t h, int b) { dpfs_xgmi_set_blocks(xgmi_ptr(h), b); });
   m.def("xgmi_capacity", [](int64_t h) { return dpfs_xgmi_capacity(xgmi_ptr(h)); });

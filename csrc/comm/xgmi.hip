@@ -8,6 +8,10 @@
 //   all-reduce  (two-shot)  copy-in | barrier | rank r sums slice r of every peer's buffer in
 //                           fixed rank order (fp32) -> own slice + tmp | barrier | gather the
 //                           other W-1 reduced slices from the peers' tmp
+//   all-reduce  (one-shot)  copy-in | barrier | every rank reads the WHOLE buffer of every peer
+//                           and sums all W in the same fixed rank order (small messages: one
+//                           barrier instead of two, (W-1) n bytes read per rank instead of
+//                           2 (W-1) n / W; bit-identical to the two-shot result)
 //   reduce-scatter          the first two phases of the all-reduce
 //   all-gather              copy-in | barrier | read every peer's buffer
 //
@@ -29,7 +33,10 @@
 // workgroups passed the second barrier of call k, which every peer workgroup signals only after
 // its phase-1 reads of `in` completed.  `tmp` is rewritten in phase 1 of call k+1, after the
 // start barrier of k+1, which a peer workgroup signals only once that peer's kernel k (and its
-// phase-2 reads of tmp) completed (same stream).
+// phase-2 reads of tmp) completed (same stream).  The one-shot all-reduce has no second barrier,
+// so its input alternates between two regions by the epoch's parity: rank r rewrites region
+// (k & 1) only in the copy-in of call k + 2, after passing the start barrier of call k + 1,
+// which every peer signals only after its kernel k -- and its reads of r's region -- completed.
 //
 // Every wait is bounded (s_memrealtime, 100 MHz): on timeout the kernel records an error in a
 // host-mapped word and exits, so a broken peer can never hang the GPU.
@@ -158,6 +165,36 @@ __global__ __launch_bounds__(kThreads) void xgmi_coll_k(Peers P, int op, int ran
     rtmp[s] = rsrc(P.data[s < W ? s : 0] + tmp_off, cap);
   }
 
+  if (op == 3) {   // one-shot all-reduce: in_off = this call's parity region, whole message
+    const long long tv = (n + N - 1) / N;
+    const long long bv = (tv + gridDim.x - 1) / gridDim.x;
+    const long long w0 = (long long)blockIdx.x * bv, w1 = w0 + bv < tv ? w0 + bv : tv;
+    for (long long v = w0 + threadIdx.x; v < w1; v += kThreads) st_sys(r_in, (unsigned)(v * 16), xv[v]);
+    barrier(P, rank, W, 0, epoch, deadline, err);
+    for (long long v = w0 + threadIdx.x; v < w1; v += kThreads) {
+      u32x4 raw[kMaxRanks];
+#pragma unroll
+      for (int s = 0; s < kMaxRanks; ++s)   // every peer's load before the first add
+        if (s < W && s != rank) raw[s] = ld_sys(rin[s], (unsigned)(v * 16));
+      const u32x4 self = xv[v];
+#pragma unroll
+      for (int s = 0; s < kMaxRanks; ++s)
+        if (s == rank) raw[s] = self;
+      float acc[N], f[N];
+      V16<T>::unpack(raw[0], acc);
+#pragma unroll
+      for (int s = 1; s < kMaxRanks; ++s) {
+        if (s < W) {
+          V16<T>::unpack(raw[s], f);
+#pragma unroll
+          for (int i = 0; i < N; ++i) acc[i] += f[i];
+        }
+      }
+      ov[v] = V16<T>::pack(acc);
+    }
+    return;
+  }
+
   // ---- phase 0: copy-in of what the peers will read.  Staged (op & 8): the producer GEMM
   // wrote x straight into this rank's slot (x == slot base), so nothing is copied; its plain
   // stores may still sit dirty in the XCD L2s, hence a system-scope release (L2 write-back)
@@ -254,6 +291,7 @@ __global__ __launch_bounds__(kThreads) void xgmi_coll_k(Peers P, int op, int ran
 struct Comm {
   int rank = 0, world = 1;
   long long cap = 0;          // bytes of each region
+  long long os_cap = 0;       // bytes of each of the two one-shot input regions
   int nslots = 0;             // staging slots (producer GEMMs write here: no copy-in)
   char* data = nullptr;       // own [slot 0 .. slot S-1 | stage | tmp], cap bytes each
   uint32_t* sig = nullptr;    // own signals (uncached)
@@ -283,6 +321,8 @@ extern "C" long long dpfs_xgmi_handle_bytes() { return 2 * (long long)sizeof(hip
 
 static long long stage_off(const Comm* c) { return (long long)c->nslots * c->cap; }
 static long long tmp_off(const Comm* c) { return (long long)(c->nslots + 1) * c->cap; }
+static long long os_off(const Comm* c, int parity) { return (long long)(c->nslots + 2) * c->cap + parity * c->os_cap; }
+static const long long kOneShotCap = 16LL << 20;   // one-shot all-reduce: messages up to 16 MiB
 
 // Allocate this rank's buffers; writes [data handle | signal handle] to handles_out.
 extern "C" void* dpfs_xgmi_create(int rank, int world, long long cap_bytes, int nslots, void* handles_out) {
@@ -303,7 +343,8 @@ extern "C" void* dpfs_xgmi_create(int rank, int world, long long cap_bytes, int 
   c->world = world;
   c->cap = cap_bytes;
   c->nslots = nslots;
-  if (!ok(hipMalloc((void**)&c->data, (nslots + 2) * cap_bytes), "hipMalloc(data)")) {
+  c->os_cap = cap_bytes < kOneShotCap ? cap_bytes : kOneShotCap;
+  if (!ok(hipMalloc((void**)&c->data, (nslots + 2) * cap_bytes + 2 * c->os_cap), "hipMalloc(data)")) {
     delete c;
     return nullptr;
   }
@@ -370,6 +411,7 @@ extern "C" void dpfs_xgmi_set_blocks(void* h, int blocks) {
 }
 
 extern "C" long long dpfs_xgmi_capacity(void* h) { return ((Comm*)h)->cap; }
+extern "C" long long dpfs_xgmi_one_shot_capacity(void* h) { return ((Comm*)h)->os_cap; }
 
 // Device address of staging slot `slot` (cap bytes), or null.
 extern "C" void* dpfs_xgmi_slot(void* h, int slot) {
@@ -384,10 +426,35 @@ extern "C" void dpfs_xgmi_clear_error(void* h) { __atomic_store_n(((Comm*)h)->er
 
 // One collective on `stream`.  dtype 1 = bf16, 0 = fp32.  Element counts as in xgmi_coll_k;
 // the caller guarantees n*elt <= cap (op 0/1) / W*part*elt <= ... (op 2: part*elt <= cap) and
-// 16-byte alignment of x and out.
+// 16-byte alignment of x and out.  op 3 = one-shot all-reduce (n*elt <= the one-shot capacity,
+// never staged: peers read the input after this rank's kernel may have finished).
 extern "C" int dpfs_xgmi_run(void* h, int op, int dtype, const void* x, void* out, long long n, long long part,
                              double timeout_s, int slot, hipStream_t stream) {
   Comm* c = (Comm*)h;
+  if (op == 3) {
+    const int elt1 = dtype == 1 ? 2 : 4;
+    const long long nb = ((n * elt1 + 15) / 16) * 16;
+    if (slot >= 0 || n <= 0 || nb > c->os_cap || (n * elt1) % 16) {
+      snprintf(g_msg, sizeof(g_msg), "xgmi_run: one-shot all-reduce of %lld B (one-shot capacity %lld B, unstaged, "
+               "16-byte multiple)", n * elt1, c->os_cap);
+      return -1;
+    }
+    const long long tv = nb / 16;
+    int grid = (int)((tv + kThreads - 1) / kThreads);
+    if (grid > c->blocks) grid = c->blocks;
+    if (grid < 1) grid = 1;
+    c->epoch += 1;
+    if (c->epoch == 0) c->epoch = 1;
+    const unsigned long long ticks = (unsigned long long)(timeout_s * 1e8);
+    const long long io = os_off(c, (int)(c->epoch & 1));
+    if (dtype == 1)
+      hipLaunchKernelGGL(xgmi_coll_k<__bf16>, dim3(grid), dim3(kThreads), 0, stream, c->peers, 3, c->rank, c->world,
+                         (const __bf16*)x, (__bf16*)out, n, n, io, tmp_off(c), c->os_cap, c->epoch, ticks, c->err_dev);
+    else
+      hipLaunchKernelGGL(xgmi_coll_k<float>, dim3(grid), dim3(kThreads), 0, stream, c->peers, 3, c->rank, c->world,
+                         (const float*)x, (float*)out, n, n, io, tmp_off(c), c->os_cap, c->epoch, ticks, c->err_dev);
+    return ok(hipGetLastError(), "xgmi_coll_k launch") ? 0 : -1;
+  }
   long long in_off = stage_off(c);
   if (slot >= 0) {   // staged input: x must be the slot itself (reduce-scatter / all-reduce)
     if (slot >= c->nslots || x != c->data + (long long)slot * c->cap || op == 2) {

@@ -469,16 +469,16 @@ __device__ __forceinline__ bool fwd_cur_next(FwdCur& c, int n_items, int NP, int
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n (jump over the immediates 0..63).
 __device__ __forceinline__ void wait_vm_rt(int n) {
   switch (n) {
-#define DPFS_W(N_) \
+#define ATT_W(N_) \
   case N_: wait_vmcnt<N_>(); break;
-    DPFS_W(0) DPFS_W(1) DPFS_W(2) DPFS_W(3) DPFS_W(4) DPFS_W(5) DPFS_W(6) DPFS_W(7) DPFS_W(8) DPFS_W(9)
-    DPFS_W(10) DPFS_W(11) DPFS_W(12) DPFS_W(13) DPFS_W(14) DPFS_W(15) DPFS_W(16) DPFS_W(17) DPFS_W(18)
-    DPFS_W(19) DPFS_W(20) DPFS_W(21) DPFS_W(22) DPFS_W(23) DPFS_W(24) DPFS_W(25) DPFS_W(26) DPFS_W(27)
-    DPFS_W(28) DPFS_W(29) DPFS_W(30) DPFS_W(31) DPFS_W(32) DPFS_W(33) DPFS_W(34) DPFS_W(35) DPFS_W(36)
-    DPFS_W(37) DPFS_W(38) DPFS_W(39) DPFS_W(40) DPFS_W(41) DPFS_W(42) DPFS_W(43) DPFS_W(44) DPFS_W(45)
-    DPFS_W(46) DPFS_W(47) DPFS_W(48) DPFS_W(49) DPFS_W(50) DPFS_W(51) DPFS_W(52) DPFS_W(53) DPFS_W(54)
-    DPFS_W(55) DPFS_W(56) DPFS_W(57) DPFS_W(58) DPFS_W(59) DPFS_W(60) DPFS_W(61) DPFS_W(62) DPFS_W(63)
-#undef DPFS_W
+    ATT_W(0) ATT_W(1) ATT_W(2) ATT_W(3) ATT_W(4) ATT_W(5) ATT_W(6) ATT_W(7) ATT_W(8) ATT_W(9)
+    ATT_W(10) ATT_W(11) ATT_W(12) ATT_W(13) ATT_W(14) ATT_W(15) ATT_W(16) ATT_W(17) ATT_W(18)
+    ATT_W(19) ATT_W(20) ATT_W(21) ATT_W(22) ATT_W(23) ATT_W(24) ATT_W(25) ATT_W(26) ATT_W(27)
+    ATT_W(28) ATT_W(29) ATT_W(30) ATT_W(31) ATT_W(32) ATT_W(33) ATT_W(34) ATT_W(35) ATT_W(36)
+    ATT_W(37) ATT_W(38) ATT_W(39) ATT_W(40) ATT_W(41) ATT_W(42) ATT_W(43) ATT_W(44) ATT_W(45)
+    ATT_W(46) ATT_W(47) ATT_W(48) ATT_W(49) ATT_W(50) ATT_W(51) ATT_W(52) ATT_W(53) ATT_W(54)
+    ATT_W(55) ATT_W(56) ATT_W(57) ATT_W(58) ATT_W(59) ATT_W(60) ATT_W(61) ATT_W(62) ATT_W(63)
+#undef ATT_W
     default: wait_vmcnt<0>(); break;
   }
 }
@@ -1017,7 +1017,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv2_k(
     for (int j = 0; j < 4; ++j) {
       const int ki = wk0 + 4 * g + j;
       if (ki < T) {
-        DPFS_KASSERT(rpos[(long long)b * T + ki] >= 0, "rope position at key %d", ki);
+        KASSERT(rpos[(long long)b * T + ki] >= 0, "rope position at key %d", ki);
         const float* tr = rtab + rpos[(long long)b * T + ki] * HD;
 #pragma unroll
         for (int d = 0; d < DT / 2; ++d) {
@@ -1435,7 +1435,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
 #pragma unroll
     for (int d = 0; d < DTN; ++d) dkt[d] *= scale;
     if (rpos && key < T) {
-      DPFS_KASSERT(rpos[(long long)b * T + key] >= 0, "rope position at key %d", key);
+      KASSERT(rpos[(long long)b * T + key] >= 0, "rope position at key %d", key);
       const float* tr = rtab + rpos[(long long)b * T + key] * HD;
 #pragma unroll
       for (int dt = 0; dt < DTN / 2; ++dt)
@@ -1672,7 +1672,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq_k(const bf
 #pragma unroll
       for (int d = 0; d < DT; ++d) dq[c][d] *= scale;
       if (rpos) {
-        DPFS_KASSERT(rpos[(long long)b * T + qi] >= 0, "rope position at query %d", qi);
+        KASSERT(rpos[(long long)b * T + qi] >= 0, "rope position at query %d", qi);
         const float* tr = rtab + rpos[(long long)b * T + qi] * HD;
 #pragma unroll
         for (int d = 0; d < DT / 2; ++d) {
@@ -1917,7 +1917,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
 #pragma unroll
     for (int d = 0; d < DTN; ++d) dq[d] *= scale;
     if (rpos && qi < T) {
-      DPFS_KASSERT(rpos[(long long)b * T + qi] >= 0, "rope position at query %d", qi);
+      KASSERT(rpos[(long long)b * T + qi] >= 0, "rope position at query %d", qi);
       const float* tr = rtab + rpos[(long long)b * T + qi] * HD;
 #pragma unroll
       for (int dt = 0; dt < DTN / 2; ++dt)
@@ -1985,7 +1985,7 @@ __global__ __launch_bounds__(1024) void attn_bias_grad_k(const float* __restrict
 
 using namespace dpfs;
 
-#define DPFS_HD_DISPATCH(HDV, ...)                           \
+#define HD_DISPATCH(HDV, ...)                           \
   do {                                                       \
     if ((HDV) == 64) { constexpr int HD_ = 64; __VA_ARGS__; } \
     else if ((HDV) == 128) { constexpr int HD_ = 128; __VA_ARGS__; } \
@@ -2024,7 +2024,7 @@ extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void*
     return;
   }
   dim3 grid((T + 127) / 128, B * H);
-  DPFS_HD_DISPATCH(hd, attn_fwd_k<HD_><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o,
+  HD_DISPATCH(hd, attn_fwd_k<HD_><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o,
                                                             lse, T, H, ldq, ldk, ldv, ldo, scale, causal));
 }
 
@@ -2053,31 +2053,31 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
   dim3 gq(nqb, B * H);
   if (bimpl == 4 && v3ok) {   // (attn_bwd_dkdv3_k reads the -lse / scale this kernel writes)
     const int items = (B * H + 7) / 8 * 8 * ((nqb + 1) / 2);
-#define DPFS_DQ3(HD_)                                                                                             \
+#define DQ3_LAUNCH(HD_)                                                                                             \
   attn_bwd_dq3_k<HD_><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,   \
                                             (const bf16*)o, lse, delta, delta + (long long)B * H * T, (bf16*)dq, T, \
                                             H, B * H, ldq, ldk, ldv, lddo, ldo, lddq, scale, causal, rope_pos,     \
                                             rope_tab, pq)
-    if (hd == 64) DPFS_DQ3(64);
-    else DPFS_DQ3(128);
-#undef DPFS_DQ3
+    if (hd == 64) DQ3_LAUNCH(64);
+    else DQ3_LAUNCH(128);
+#undef DQ3_LAUNCH
   } else
-  DPFS_HD_DISPATCH(hd, attn_bwd_dq_k<HD_><<<gq, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
+  HD_DISPATCH(hd, attn_bwd_dq_k<HD_><<<gq, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
                                                              (const bf16*)dout, (const bf16*)o, lse, delta,
                                                              delta + (long long)B * H * T, (bf16*)dq,
                                                              T, H, ldq, ldk, ldv, lddo, ldo, lddq, scale, causal,
                                                              rope_pos, rope_tab, pq));
   if (bimpl == 4 && v3ok) {
     const int nkb3 = (T + 127) / 128, items = (B * H + 7) / 8 * 8 * ((nkb3 + 1) / 2);
-#define DPFS_DKDV3(HD_, DG_)                                                                                      \
+#define DKDV3_LAUNCH(HD_, DG_)                                                                                      \
   attn_bwd_dkdv3_k<HD_, DG_><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, \
                                                    delta + (long long)B * H * T, delta, (bf16*)dk, (bf16*)dv, T, H,     \
                                                    B * H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal, rope_pos,     \
                                                    rope_tab, pk, pv, DG_ ? g_attn_diag : nullptr)
-    if (hd == 64 && diag) DPFS_DKDV3(64, 1);
-    else if (hd == 64) DPFS_DKDV3(64, 0);
-    else DPFS_DKDV3(128, 0);
-#undef DPFS_DKDV3
+    if (hd == 64 && diag) DKDV3_LAUNCH(64, 1);
+    else if (hd == 64) DKDV3_LAUNCH(64, 0);
+    else DKDV3_LAUNCH(128, 0);
+#undef DKDV3_LAUNCH
     if (bias) {
       if (hd == 64) attn_bias_grad_k<64><<<3 * H * 4, 1024, 0, s>>>(pq, pk, pv, dbias, H, B * nqb * 4, B * nkb3 * 4);
       else attn_bias_grad_k<128><<<3 * H * 8, 1024, 0, s>>>(pq, pk, pv, dbias, H, B * nqb * 4, B * nkb3 * 4);
@@ -2086,13 +2086,13 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
     return 0;
   }
   dim3 gk((T + 63) / 64, B * H);
-  DPFS_HD_DISPATCH(hd, attn_bwd_dkdv2_k<HD_><<<gk, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
+  HD_DISPATCH(hd, attn_bwd_dkdv2_k<HD_><<<gk, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,
                                                                 (const bf16*)dout, delta + (long long)B * H * T,
                                                                 delta, (bf16*)dk,
                                                                 (bf16*)dv, T, H, ldq, ldk, ldv, lddo, lddk, lddv,
                                                                 scale, causal, rope_pos, rope_tab, pk, pv));
   if (bias) {
-    DPFS_HD_DISPATCH(hd, attn_bias_grad_k<HD_><<<3 * H * (HD_ / 16), 1024, 0, s>>>(pq, pk, pv, dbias, H,
+    HD_DISPATCH(hd, attn_bias_grad_k<HD_><<<3 * H * (HD_ / 16), 1024, 0, s>>>(pq, pk, pv, dbias, H,
                                                                                      B * nqb * 4, B * nkb * 4));
     return 1;
   }

@@ -19,7 +19,7 @@
 // wave (the launch fails with a device exception at the next synchronisation).  In the
 // default build the macro is empty, so the hot kernels carry no extra instruction.
 #if defined(DPFS_KERNEL_ASSERT) && DPFS_KERNEL_ASSERT
-#define DPFS_KASSERT(cond, fmt, ...)                                                             \
+#define KASSERT(cond, fmt, ...)                                                             \
   do {                                                                                          \
     if (!(cond)) {                                                                              \
       printf("[dpfs kernel assert] %s:%d: %s (block %d, thread %d): " fmt "\n", __FILE__, __LINE__, \
@@ -28,7 +28,7 @@
     }                                                                                           \
   } while (0)
 #else
-#define DPFS_KASSERT(cond, fmt, ...) \
+#define KASSERT(cond, fmt, ...) \
   do {                               \
   } while (0)
 #endif
@@ -121,4 +121,4 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 }  // namespace dpfs
 
-#define DPFS_LAUNCH_CHECK() (void)hipGetLastError()
+#define LAUNCH_CHECK() (void)hipGetLastError()

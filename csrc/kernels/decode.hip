@@ -270,7 +270,7 @@ __global__ __launch_bounds__(256) void rope_append_k(bf16* __restrict__ qkv, lon
       const int b = i / rot_per_b, r = i - b * rot_per_b;
       const int head = r / q8, f0 = (r - head * q8) * 8;
       bf16* base = qkv + (long long)b * ld + head * HD;
-      DPFS_KASSERT(pos[b] >= 0, "decode position %lld of sequence %d", (long long)pos[b], b);
+      KASSERT(pos[b] >= 0, "decode position %lld of sequence %d", (long long)pos[b], b);
       const float* tr = tab + pos[b] * (long long)HD;
       const bf16x8 xa = *reinterpret_cast<const bf16x8*>(base + f0);
       const bf16x8 xb = *reinterpret_cast<const bf16x8*>(base + h2 + f0);

@@ -120,7 +120,7 @@ __global__ __launch_bounds__(256) void rope_vec_k(T* __restrict__ qkv, const int
     const int rem = i - row * per_row;
     const int head = rem / qn;
     const int f0 = (rem - head * qn) * N;
-    DPFS_KASSERT(pos[row] >= 0, "position %lld at row %d", (long long)pos[row], row);
+    KASSERT(pos[row] >= 0, "position %lld at row %d", (long long)pos[row], row);
     const float* tr = table + pos[row] * (long long)hd;
     T* base = qkv + (long long)row * ld + head * hd;
     float x1[N], x2[N], c[N], sn[N];
@@ -365,7 +365,7 @@ static void colsum_launch(const T* x, float* out, float* ws, int M, int N_, hipS
 
 using namespace dpfs;
 
-#define DPFS_PERM(P, ...) \
+#define PERM_DISPATCH(P, ...) \
   do {                    \
     if (P) {              \
       constexpr bool PM = true; __VA_ARGS__; \
@@ -375,7 +375,7 @@ using namespace dpfs;
   } while (0)
 
 extern "C" void dpfs_swiglu_fwd(int dtype, const void* gu, void* h, int M, int F, int perm, hipStream_t s) {
-  DPFS_PERM(perm, if (dtype == kBF16) swiglu_fwd_k<bf16, PM><<<cap_grid((long long)M * F / 8, 256), 256, 0, s>>>(
+  PERM_DISPATCH(perm, if (dtype == kBF16) swiglu_fwd_k<bf16, PM><<<cap_grid((long long)M * F / 8, 256), 256, 0, s>>>(
                       (const bf16*)gu, (bf16*)h, M, F);
                   else swiglu_fwd_k<float, PM><<<cap_grid((long long)M * F / 4, 256), 256, 0, s>>>(
                       (const float*)gu, (float*)h, M, F));
@@ -383,7 +383,7 @@ extern "C" void dpfs_swiglu_fwd(int dtype, const void* gu, void* h, int M, int F
 
 extern "C" void dpfs_swiglu_bwd(int dtype, const void* dh, const void* gu, void* dgu, int M, int F, int perm,
                                 hipStream_t s) {
-  DPFS_PERM(perm, if (dtype == kBF16) swiglu_bwd_k<bf16, PM><<<cap_grid((long long)M * F / 8, 256), 256, 0, s>>>(
+  PERM_DISPATCH(perm, if (dtype == kBF16) swiglu_bwd_k<bf16, PM><<<cap_grid((long long)M * F / 8, 256), 256, 0, s>>>(
                       (const bf16*)dh, (const bf16*)gu, (bf16*)dgu, M, F);
                   else swiglu_bwd_k<float, PM><<<cap_grid((long long)M * F / 4, 256), 256, 0, s>>>(
                       (const float*)dh, (const float*)gu, (float*)dgu, M, F));
@@ -403,7 +403,7 @@ extern "C" void dpfs_swiglu_bwd_dbias(int dtype, const void* dh, const void* gu,
   int rpc;
   const int chunks = colsum_plan(M, cblocks, 2048, &rpc);
   float* part = chunks > 1 ? ws : dbias;
-  DPFS_PERM(perm, if (dtype == kBF16) swiglu_bwd_colsum_k<bf16, PM><<<dim3(cblocks, chunks), 256, 0, s>>>(
+  PERM_DISPATCH(perm, if (dtype == kBF16) swiglu_bwd_colsum_k<bf16, PM><<<dim3(cblocks, chunks), 256, 0, s>>>(
                       (const bf16*)dh, (const bf16*)gu, (bf16*)dgu, part, M, F, rpc);
                   else swiglu_bwd_colsum_k<float, PM><<<dim3(cblocks, chunks), 256, 0, s>>>(
                       (const float*)dh, (const float*)gu, (float*)dgu, part, M, F, rpc));

@@ -23,7 +23,7 @@ __global__ __launch_bounds__(256) void embedding_fwd_k(const int64_t* __restrict
   const int lane = threadIdx.x & 63;
   const int nv = D / 4;
   for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += gridDim.x * 4) {
-    DPFS_KASSERT(ids[row] >= 0, "token id %lld at row %d", (long long)ids[row], row);
+    KASSERT(ids[row] >= 0, "token id %lld at row %d", (long long)ids[row], row);
     const long long loc = ids[row] - vstart;
     const bool hit = loc >= 0 && loc < vlocal;
     TO* o = out + (long long)row * D;
@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256) void embedding_bwd_k(const TI* __restrict__ do
                                                        int vlocal) {
   const int lane = threadIdx.x & 63;
   for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += gridDim.x * 4) {
-    DPFS_KASSERT(ids[row] >= 0, "token id %lld at row %d", (long long)ids[row], row);
+    KASSERT(ids[row] >= 0, "token id %lld at row %d", (long long)ids[row], row);
     const long long loc = ids[row] - vstart;
     if (loc < 0 || loc >= vlocal) continue;
     const TI* g = dout + (long long)row * D;
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void ce_stats_k(const T* __restrict__ logits, 
   if (threadIdx.x == 0) {
     MaxSum r = red[0];
     for (int i = 1; i < 4; ++i) r = merge(r, red[i]);
-    DPFS_KASSERT(tgt[row] >= -1, "target %lld at row %d (ignore_index is -1)", (long long)tgt[row], row);
+    KASSERT(tgt[row] >= -1, "target %lld at row %d (ignore_index is -1)", (long long)tgt[row], row);
     const long long loc = tgt[row] - vstart;
     const float tl = (loc >= 0 && loc < vvalid) ? to_f(x[loc]) : 0.f;
     stats[row * 3 + 0] = r.m;

@@ -844,18 +844,18 @@ static bool launchp(int cfg, const void* A, const void* B, void* C, const float*
   const int grid = (int)std::min<long long>(items, cu_count());
   const int sched = v2_sched<AK, BKM>() == 4 ? 4 : 2;
   const unsigned cb = (unsigned)cspan;
-#define DPFS_GEMMP(BN_, WM_, SC_)                                                                                    \
+#define GEMMP_LAUNCH(BN_, WM_, SC_)                                                                                    \
   gemmp_k<256, BN_, WM_, AK, BKM, OUT, SC_><<<grid, 512, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K,  \
                                                                 lda, ldb, ldc, kps, splits, slab, ab, bb, cb, rope, \
                                                                 g_group_m, dual)
   if (cfg == 0) {
-    if (sched == 4) DPFS_GEMMP(256, 2, 4);
-    else DPFS_GEMMP(256, 2, 2);
+    if (sched == 4) GEMMP_LAUNCH(256, 2, 4);
+    else GEMMP_LAUNCH(256, 2, 2);
   } else {
-    if (sched == 4) DPFS_GEMMP(128, 4, 4);
-    else DPFS_GEMMP(128, 4, 2);
+    if (sched == 4) GEMMP_LAUNCH(128, 4, 4);
+    else GEMMP_LAUNCH(128, 4, 2);
   }
-#undef DPFS_GEMMP
+#undef GEMMP_LAUNCH
   return true;
 }
 

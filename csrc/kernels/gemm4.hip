@@ -203,7 +203,7 @@ __device__ __forceinline__ Item decode(int lin, int nwg, int tiles_m, int tiles_
   it.n0 = (r / gsz) * BN;
   it.kb = it.split * kps;
   it.ke = min(K, it.kb + kps);
-  DPFS_KASSERT(it.m0 < tiles_m * 256 && it.n0 < tiles_n * BN && it.kb <= K,
+  KASSERT(it.m0 < tiles_m * 256 && it.n0 < tiles_n * BN && it.kb <= K,
                "item %d -> tile (%d, %d) k %d", lin, it.m0, it.n0, it.kb);
   it.sel = 0;
   if (it.kb >= k_switch) {
@@ -262,7 +262,7 @@ __device__ __forceinline__ void epilogue(const char* bias_lds, const Item& ci, v
     auto rope_load = [&](int i) {
       const int m = row0 + 16 * i;
       const long long pp = m < M ? rope.pos[m] : 0;
-      DPFS_KASSERT(m >= M || pp >= 0, "rope position %lld at row %d", pp, m);
+      KASSERT(m >= M || pp >= 0, "rope position %lld at row %d", pp, m);
       const float* tr = rope.tab + pp * HD;
 #pragma unroll
       for (int jh = 0; jh < HJ; ++jh) {
@@ -536,8 +536,14 @@ __device__ __forceinline__ void epilogue_swb(const Item& ci, int M, int F, const
 // ROPE (head_dim 64 / 128, 0 = none): the RoPE epilogue is compiled in (QKV projection only:
 // its code and register pressure stay out of the plain kernels).
 // SWIGLU: the gate|up form (SwiOut).
+// BR: rows of MFMAs (NJ each) a step issues BEFORE its DMA wait + barrier.  0 = the barrier
+// opens the step.  BR > 0: the step's first rows run on fragments already in registers, the
+// wave reaches the barrier with MFMAs in flight and the next-step fragment reads follow it
+// (rows BR .. BR + 3), so the barrier / wait time overlaps matrix work instead of draining
+// the pipe once per 32-deep step.  (Safe: the DMA a step issues writes the slot read two
+// steps earlier, retired before the previous step's barrier.)
 template <bool AK, bool BKM, int OUT, int DIAG = 0, bool FAST = false, int SCHED = 0, int BN = 256, int ROPE = 0,
-          bool SWIGLU = false, bool SWB = false>
+          bool SWIGLU = false, bool SWB = false, int BR = 0>
 __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                   void* __restrict__ C, const float* __restrict__ bias, int M, int N,
                                                   int K, int lda, int ldb, int ldc, int kps, int splits,
@@ -555,6 +561,10 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   static_assert(!SWIGLU || (OUT == 0 && BN == 256 && ROPE == 0), "SwiGLU epilogue: bf16 256-wide tiles");
   static_assert(!SWB || (OUT == 0 && BN == 256 && ROPE == 0 && !SWIGLU), "SwiGLU-backward epilogue: bf16 256-wide tiles");
   static_assert(BN == 256 || BN == 192, "tile width");
+  static_assert(BR >= 0 && BR <= 4 && (BR == 0 || DIAG == 0), "barrier row");
+  // ring pieces issued before the step's barrier (their count joins the wait, and the bias
+  // DMA issued after the barrier has NQ - PBB younger ring pieces)
+  constexpr int PBB = SCHED == 1 ? (BR < NQ ? BR : NQ) : 0;
 
   const int tiles_n = (N + BN - 1) / BN;
   const int tiles_m = (M + 255) / 256;
@@ -741,34 +751,40 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
     cur.a.pin();
     cur.b.pin();
-    if (DIAG == 3 && (dbg & 4)) wait_vmcnt<63>();   // timing-only: no wait for the DMA (wrong results)
-    else if (first) wait_vmcnt<(NQ + STORES < 63 ? NQ + STORES : 63)>();
-    else wait_vmcnt<NQ>();
-    if (!(DIAG == 3 && (dbg & 8))) __builtin_amdgcn_s_barrier();
-    if constexpr (TIMED) {
-      const unsigned long long t = stamp();
-      t_wait += t - t_mark;
-      t_mark = t;
-    }
-    if (OUT == 0 && last && bias) {
-      // the epilogue's bias values of this wave (128, of which BN/2 used) into its LDS area by
-      // two 256-byte LDS-DMA pieces, ahead of this step's NQ ring pieces (the epilogue waits
-      // vmcnt(NQ), no barrier: the wave reads only what it loaded)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int n = bcol0 + 64 * h + l;
-        const int nb = SWIGLU ? gu_nat(n, N >> 1) : n;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rbias, (__attribute__((address_space(3))) void*)(bias_lds + 256 * h),
-                                                 4, n < N ? (unsigned)(nb * 4) : kOOB, 0, 0, 0);
+    // Stage s+1 landed for this wave (younger: stage s+2 = NQ pieces, the PBB pieces of stage
+    // s+3 issued before the barrier, plus the previous item's epilogue stores on an item's
+    // first step), then the step barrier; the bias DMA of the item's last step after it.
+    auto sync = [&]() __attribute__((always_inline)) {
+      if (DIAG == 3 && (dbg & 4)) wait_vmcnt<63>();   // timing-only: no wait for the DMA (wrong results)
+      else if (first) wait_vmcnt<(NQ + PBB + STORES < 63 ? NQ + PBB + STORES : 63)>();
+      else wait_vmcnt<NQ + PBB>();
+      if (!(DIAG == 3 && (dbg & 8))) __builtin_amdgcn_s_barrier();
+      if constexpr (TIMED) {
+        const unsigned long long t = stamp();
+        t_wait += t - t_mark;
+        t_mark = t;
       }
-    }
+      if (OUT == 0 && last && bias) {
+        // the epilogue's bias values of this wave (128, of which BN/2 used) into its LDS area
+        // by two 256-byte LDS-DMA pieces, ahead of this step's remaining NQ - PBB ring pieces
+        // (the epilogue waits vmcnt(NQ - PBB), no barrier: the wave reads only what it loaded)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int n = bcol0 + 64 * h + l;
+          const int nb = SWIGLU ? gu_nat(n, N >> 1) : n;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rbias, (__attribute__((address_space(3))) void*)(bias_lds + 256 * h),
+                                                   4, n < N ? (unsigned)(nb * 4) : kOOB, 0, 0, 0);
+        }
+      }
+    };
+    if constexpr (BR == 0) sync();
 
     c_slot = (c_slot + 1) & 3;
     const char* src = smem + c_slot * SLOT;
-    // Rows q of NJ MFMAs (A fragment q against every B fragment).  Rows 0-3 read the next
-    // step's fragments (A 2q, 2q+1; B 2q, 2q+1 while < NJ).  DMA pieces: SCHED 0 two per row in
-    // rows 4-7, SCHED 1 one per row.  At NJ = 8 this is the hand-placed order of the 256-wide
-    // kernel: MFMA j, then the event after it.
+    // Rows q of NJ MFMAs (A fragment q against every B fragment).  Rows BR .. BR+3 read the
+    // next step's fragments (A 2r, 2r+1; B 2r, 2r+1 while < NJ; r = q - BR).  DMA pieces:
+    // SCHED 0 two per row in rows 4-7, SCHED 1 one per row.  At NJ = 8 this is the hand-placed
+    // order of the 256-wide kernel: MFMA j, then the event after it.
     static_for<0, 8>([&](auto Q) {
       constexpr int q = decltype(Q)::value;
       static_for<0, NJ>([&](auto J) {
@@ -778,14 +794,16 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
         // this step's stage descriptors (scalar work) in the shadow of the first MFMAs
         if constexpr (q == 0 && j == 0) stage_rsrc_a();
         if constexpr (q == 0 && j == 1) stage_rsrc_b();
-        if constexpr (q < 4 && !NOPF) {
+        if constexpr (BR > 0 && q == BR - 1 && j == NJ - 1) sync();
+        constexpr int rq = q - BR;
+        if constexpr (rq >= 0 && rq < 4 && !NOPF) {
           // read slots after MFMA 0 / 2 / 4 / 6 (NJ 8) or 0 / 2 / 3 / 5 (NJ 6)
           constexpr int r0 = 0, r1 = 2, r2 = NJ == 8 ? 4 : 3, r3 = NJ == 8 ? 6 : 5;
-          if constexpr (j == r0) nxt.a.load(2 * q, src, wm * 128 + 32 * q, l);
-          if constexpr (j == r1 && 2 * q < NJ) nxt.b.load(2 * q, src + 16384, wn * (BN / 2) + 32 * q, l);
-          if constexpr (j == r2) nxt.a.load(2 * q + 1, src, wm * 128 + 32 * q + 16, l);
-          if constexpr (j == r3 && 2 * q + 1 < NJ)
-            nxt.b.load(2 * q + 1, src + 16384, wn * (BN / 2) + 32 * q + 16, l);
+          if constexpr (j == r0) nxt.a.load(2 * rq, src, wm * 128 + 32 * rq, l);
+          if constexpr (j == r1 && 2 * rq < NJ) nxt.b.load(2 * rq, src + 16384, wn * (BN / 2) + 32 * rq, l);
+          if constexpr (j == r2) nxt.a.load(2 * rq + 1, src, wm * 128 + 32 * rq + 16, l);
+          if constexpr (j == r3 && 2 * rq + 1 < NJ)
+            nxt.b.load(2 * rq + 1, src + 16384, wn * (BN / 2) + 32 * rq + 16, l);
         }
         if constexpr (SCHED == 1) {
           if constexpr (j == 3 && q < NQ) issue(q);
@@ -831,7 +849,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
       t_body += t - t_mark;
       t_mark = t;
     }
-    if (OUT == 0 && bias) wait_vmcnt<NQ>();   // this wave's bias DMA landed (NQ younger ring pieces)
+    if (OUT == 0 && bias) wait_vmcnt<NQ - PBB>();   // this wave's bias DMA landed (younger: the ring pieces after it)
     if (OUT == 0 && bias)
       epilogue<OUT, BN, ROPE, true, SWIGLU>(bias_lds, ci, C, rope, M, N, ldc, slab_stride, c_bytes, wm, wn, l, swo);
     else
@@ -888,6 +906,9 @@ extern "C" void dpfs_gemm4_diag(void* p) { g_g4_diag = (unsigned long long*)p; }
 // 1 = two pieces per row in rows 4-7; 2 = per-lane K checks even where FAST applies.
 static int g_g4_sched = 0;
 extern "C" void dpfs_gemm4_sched(int v) { g_g4_sched = v; }
+// Rows of MFMAs before each step's barrier (gemm4_k's BR) of the plain FAST kernels: 0, 1, 2.
+static int g_g4_br = 0;
+extern "C" void dpfs_gemm4_br(int v) { g_g4_br = (v >= 0 && v <= 2) ? v : 0; }
 extern "C" void dpfs_gemm4_group_m(int g) { g_g4_group_m = g > 0 ? g : 4; }
 
 // gate|up projection with SwiGLU in the epilogue (SwiOut): C[M, N] = A perm(B)^T + perm(bias)
@@ -988,38 +1009,50 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
   const bool fast = g_g4_sched != 2 && !(g_g4_ablate & 2) && K % 64 == 0 && kps % 64 == 0 &&
                     (!A2 || k_switch % 64 == 0);
   const int sched = g_g4_sched == 1 ? 0 : 1;
-#define DPFS_G4_ARGS                                                                                            \
+#define G4_ARGS                                                                                            \
   (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb, \
       rope, g_g4_group_m, dual, g_g4_ablate & ~3, nullptr
-#define DPFS_G4(AK_, BK_, OUT_)                                                                    \
+#define G4_LAUNCH(AK_, BK_, OUT_)                                                                    \
   do {                                                                                            \
     if constexpr (AK_ && BK_ && OUT_ == 0) {                                                      \
       if (rope_cols > 0) {                                                                        \
         if (fast && rope_hd == 64)                                                                \
-          gemm4_k<AK_, BK_, OUT_, 0, true, 1, 256, 64><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);        \
+          gemm4_k<AK_, BK_, OUT_, 0, true, 1, 256, 64><<<grid, 256, 0, s>>>(G4_ARGS);        \
         else if (fast)                                                                            \
-          gemm4_k<AK_, BK_, OUT_, 0, true, 1, 256, 128><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);       \
+          gemm4_k<AK_, BK_, OUT_, 0, true, 1, 256, 128><<<grid, 256, 0, s>>>(G4_ARGS);       \
         else if (rope_hd == 64)                                                                   \
-          gemm4_k<AK_, BK_, OUT_, 0, false, 0, 256, 64><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);       \
+          gemm4_k<AK_, BK_, OUT_, 0, false, 0, 256, 64><<<grid, 256, 0, s>>>(G4_ARGS);       \
         else                                                                                      \
-          gemm4_k<AK_, BK_, OUT_, 0, false, 0, 256, 128><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);      \
+          gemm4_k<AK_, BK_, OUT_, 0, false, 0, 256, 128><<<grid, 256, 0, s>>>(G4_ARGS);      \
         break;                                                                                    \
       }                                                                                           \
     }                                                                                             \
     if (fast && sched == 1) {                                                                     \
-      if (OUT_ == 0 && bn == 192)                                                                 \
-        gemm4_k<AK_, BK_, OUT_, 0, true, 1, (OUT_ == 0 ? 192 : 256)><<<grid, 256, 0, s>>>(DPFS_G4_ARGS); \
-      else                                                                                        \
-        gemm4_k<AK_, BK_, OUT_, 0, true, 1><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);                   \
+      if (OUT_ == 0 && bn == 192) {                                                               \
+        if (g_g4_br == 1)                                                                         \
+          gemm4_k<AK_, BK_, OUT_, 0, true, 1, (OUT_ == 0 ? 192 : 256), 0, false, false, 1>         \
+              <<<grid, 256, 0, s>>>(G4_ARGS);                                                     \
+        else if (g_g4_br == 2)                                                                    \
+          gemm4_k<AK_, BK_, OUT_, 0, true, 1, (OUT_ == 0 ? 192 : 256), 0, false, false, 2>         \
+              <<<grid, 256, 0, s>>>(G4_ARGS);                                                     \
+        else                                                                                      \
+          gemm4_k<AK_, BK_, OUT_, 0, true, 1, (OUT_ == 0 ? 192 : 256)><<<grid, 256, 0, s>>>(G4_ARGS); \
+      } else if (g_g4_br == 1) {                                                                  \
+        gemm4_k<AK_, BK_, OUT_, 0, true, 1, 256, 0, false, false, 1><<<grid, 256, 0, s>>>(G4_ARGS); \
+      } else if (g_g4_br == 2) {                                                                  \
+        gemm4_k<AK_, BK_, OUT_, 0, true, 1, 256, 0, false, false, 2><<<grid, 256, 0, s>>>(G4_ARGS); \
+      } else {                                                                                    \
+        gemm4_k<AK_, BK_, OUT_, 0, true, 1><<<grid, 256, 0, s>>>(G4_ARGS);                   \
+      }                                                                                           \
     } else if (fast) {                                                                            \
       if (OUT_ == 0 && bn == 192)                                                                 \
-        gemm4_k<AK_, BK_, OUT_, 0, true, 0, (OUT_ == 0 ? 192 : 256)><<<grid, 256, 0, s>>>(DPFS_G4_ARGS); \
+        gemm4_k<AK_, BK_, OUT_, 0, true, 0, (OUT_ == 0 ? 192 : 256)><<<grid, 256, 0, s>>>(G4_ARGS); \
       else                                                                                        \
-        gemm4_k<AK_, BK_, OUT_, 0, true, 0><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);                   \
+        gemm4_k<AK_, BK_, OUT_, 0, true, 0><<<grid, 256, 0, s>>>(G4_ARGS);                   \
     } else if (OUT_ == 0 && bn == 192) {                                                          \
-      gemm4_k<AK_, BK_, OUT_, 0, false, 0, (OUT_ == 0 ? 192 : 256)><<<grid, 256, 0, s>>>(DPFS_G4_ARGS); \
+      gemm4_k<AK_, BK_, OUT_, 0, false, 0, (OUT_ == 0 ? 192 : 256)><<<grid, 256, 0, s>>>(G4_ARGS); \
     } else {                                                                                      \
-      gemm4_k<AK_, BK_, OUT_><<<grid, 256, 0, s>>>(DPFS_G4_ARGS);                                 \
+      gemm4_k<AK_, BK_, OUT_><<<grid, 256, 0, s>>>(G4_ARGS);                                 \
     }                                                                                             \
   } while (0)
   if ((g_g4_ablate & 32) && g_g4_diag && layout == 0 && !out_f32 && bn == 256) {
@@ -1042,16 +1075,16 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
     return true;
   }
   if (layout == 0) {
-    if (out_f32) DPFS_G4(true, true, 1);
-    else DPFS_G4(true, true, 0);
+    if (out_f32) G4_LAUNCH(true, true, 1);
+    else G4_LAUNCH(true, true, 0);
   } else if (layout == 1) {
-    if (out_f32) DPFS_G4(true, false, 1);
-    else DPFS_G4(true, false, 0);
+    if (out_f32) G4_LAUNCH(true, false, 1);
+    else G4_LAUNCH(true, false, 0);
   } else {
     if (!out_f32) return false;
-    DPFS_G4(false, false, 1);
+    G4_LAUNCH(false, false, 1);
   }
-#undef DPFS_G4_ARGS
-#undef DPFS_G4
+#undef G4_ARGS
+#undef G4_LAUNCH
   return true;
 }

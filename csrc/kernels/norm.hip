@@ -285,7 +285,7 @@ static int vpl_for(int D) {
   return (nvec + 63) / 64;
 }
 
-#define DPFS_VPL_DISPATCH(VPL_VALUE, ...)                                   \
+#define VPL_DISPATCH(VPL_VALUE, ...)                                   \
   do {                                                                      \
     const int _v = (VPL_VALUE);                                             \
     if (_v <= 1) { constexpr int VPL = 1; __VA_ARGS__; }                    \
@@ -327,10 +327,10 @@ extern "C" void dpfs_rmsnorm_fwd(int dtype, const void* x, const float* w, void*
                                  float eps, hipStream_t s) {
   dim3 grid((M + kRowsPerBlock - 1) / kRowsPerBlock);
   if (dtype == kBF16) {
-    DPFS_VPL_DISPATCH(vpl_for<bf16>(D), rmsnorm_fwd_k<bf16, VPL><<<grid, 256, 0, s>>>(
+    VPL_DISPATCH(vpl_for<bf16>(D), rmsnorm_fwd_k<bf16, VPL><<<grid, 256, 0, s>>>(
         (const bf16*)x, w, (bf16*)y, rstd, M, D, eps));
   } else {
-    DPFS_VPL_DISPATCH(vpl_for<float>(D), rmsnorm_fwd_k<float, VPL><<<grid, 256, 0, s>>>(
+    VPL_DISPATCH(vpl_for<float>(D), rmsnorm_fwd_k<float, VPL><<<grid, 256, 0, s>>>(
         (const float*)x, w, (float*)y, rstd, M, D, eps));
   }
 }
@@ -339,10 +339,10 @@ extern "C" void dpfs_add_rmsnorm_fwd(int dtype, const void* yin, const float* bi
                                      void* xo, void* y, float* rstd, int M, int D, float eps, hipStream_t s) {
   dim3 grid((M + kRowsPerBlock - 1) / kRowsPerBlock);
   if (dtype == kBF16) {
-    DPFS_VPL_DISPATCH(vpl_for<bf16>(D), add_rmsnorm_fwd_k<bf16, VPL><<<grid, 256, 0, s>>>(
+    VPL_DISPATCH(vpl_for<bf16>(D), add_rmsnorm_fwd_k<bf16, VPL><<<grid, 256, 0, s>>>(
         (const bf16*)yin, bias, (const bf16*)res, w, (bf16*)xo, (bf16*)y, rstd, M, D, eps));
   } else {
-    DPFS_VPL_DISPATCH(vpl_for<float>(D), add_rmsnorm_fwd_k<float, VPL><<<grid, 256, 0, s>>>(
+    VPL_DISPATCH(vpl_for<float>(D), add_rmsnorm_fwd_k<float, VPL><<<grid, 256, 0, s>>>(
         (const float*)yin, bias, (const float*)res, w, (float*)xo, (float*)y, rstd, M, D, eps));
   }
 }
@@ -351,10 +351,10 @@ extern "C" void dpfs_layernorm_fwd(int dtype, const void* x, const float* w, con
                                    float* rstd, int M, int D, float eps, hipStream_t s) {
   dim3 grid((M + kRowsPerBlock - 1) / kRowsPerBlock);
   if (dtype == kBF16) {
-    DPFS_VPL_DISPATCH(vpl_for<bf16>(D), layernorm_fwd_k<bf16, VPL><<<grid, 256, 0, s>>>(
+    VPL_DISPATCH(vpl_for<bf16>(D), layernorm_fwd_k<bf16, VPL><<<grid, 256, 0, s>>>(
         (const bf16*)x, w, b, (bf16*)y, mean, rstd, M, D, eps));
   } else {
-    DPFS_VPL_DISPATCH(vpl_for<float>(D), layernorm_fwd_k<float, VPL><<<grid, 256, 0, s>>>(
+    VPL_DISPATCH(vpl_for<float>(D), layernorm_fwd_k<float, VPL><<<grid, 256, 0, s>>>(
         (const float*)x, w, b, (float*)y, mean, rstd, M, D, eps));
   }
 }
@@ -367,15 +367,15 @@ extern "C" void dpfs_norm_bwd(int mode, int dtype, const void* dy, const void* x
                               float* partial_b, int M, int D, hipStream_t s) {
   const int G = norm_bwd_grid(M);
   const size_t lds = (size_t)(mode != 0 ? 2 : 1) * D * sizeof(float);
-#define DPFS_NB(T, MODE_)                                                                                  \
-  DPFS_VPL_DISPATCH(vpl_for<T>(D), norm_bwd_k<T, VPL, MODE_><<<G, 256, lds, s>>>(                           \
+#define NB_LAUNCH(T, MODE_)                                                                                  \
+  VPL_DISPATCH(vpl_for<T>(D), norm_bwd_k<T, VPL, MODE_><<<G, 256, lds, s>>>(                           \
       (const T*)dy, (const T*)x, w, mean, rstd, (const T*)dres, (T*)dx, partial_w, partial_b, M, D))
   if (dtype == kBF16) {
-    if (mode == 0) DPFS_NB(bf16, 0); else if (mode == 1) DPFS_NB(bf16, 1); else DPFS_NB(bf16, 2);
+    if (mode == 0) NB_LAUNCH(bf16, 0); else if (mode == 1) NB_LAUNCH(bf16, 1); else NB_LAUNCH(bf16, 2);
   } else {
-    if (mode == 0) DPFS_NB(float, 0); else if (mode == 1) DPFS_NB(float, 1); else DPFS_NB(float, 2);
+    if (mode == 0) NB_LAUNCH(float, 0); else if (mode == 1) NB_LAUNCH(float, 1); else NB_LAUNCH(float, 2);
   }
-#undef DPFS_NB
+#undef NB_LAUNCH
   // Stage 2: one fixed-order column reduction of the G (<= 1024) block partials, 64 row lanes
   // per column group (a chunked two-launch reduction cost ~2x its time at these sizes).
   if (mode != 0) dpfs_colsum_rows_split(partial_w, dw, db, D, G, 2 * D, s);

@@ -26,7 +26,7 @@ import torch
 
 from .models.transformer import Transformer
 from .parallel import process_manager as pm
-from .parallel.grad_sync import DataParallelGradSync, allreduce_sequence_parallel_grads
+from .parallel.grad_sync import DataParallelGradSync, allreduce_sequence_parallel_grads, setup_dp_buckets
 from .utils import comm_check
 
 
@@ -54,6 +54,10 @@ class TrainStep:
         # The fused engine averages DP gradients itself, overlapped with its backward.
         use_hooks = p is not None and p.dp_size > 1 and not model.fused_supported()
         self.dp = DataParallelGradSync(model, dp_bucket_mb) if use_hooks else None
+        if p is not None and p.dp_size > 1 and model.fused_supported():
+            # the fused engines' DP bucket size: measured once here, outside the backward, and
+            # MAX-reduced over every rank so all DP groups use one size
+            setup_dp_buckets(next(model.parameters()).device)
         self.checker = comm_check.from_env()
         self.steps = 0
         self._ev = None

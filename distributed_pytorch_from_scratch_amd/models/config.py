@@ -25,7 +25,7 @@ of the softmax and sliced off any returned logits.
 from __future__ import annotations
 
 from dataclasses import asdict, dataclass, replace
-from typing import Dict
+from typing import Dict, Optional
 
 
 @dataclass
@@ -56,6 +56,10 @@ class ModelArgs:
     # projections with per-tensor e4m3 / e5m2 operands on hipBLASLt's fp8 kernels; weight
     # gradients, attention, norms and the optimizer stay bf16 / fp32.  Off by default.
     fp8: bool = False
+    # SwiGLU in the gate|up GEMM epilogue (weight rows read interleaved in 64-row blocks,
+    # ops/gemm_select.swiglu_epilogue): None = on for the GPU kernels, off on the CPU oracle;
+    # True also runs the interleaved layout on the CPU oracle (tests of its plumbing).
+    swiglu_epilogue: Optional[bool] = None
 
     @property
     def head_dim(self) -> int:

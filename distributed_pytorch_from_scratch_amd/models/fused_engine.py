@@ -35,7 +35,6 @@ presets).  ``ModelArgs.sequence_parallel`` / LayerNorm models use the modular au
 from __future__ import annotations
 
 import math
-import os
 from typing import List, Optional
 
 import torch
@@ -108,10 +107,16 @@ def _defer_end():
     _DEFER = None
 
 
-def _addg(acc, g):
+def _addg(acc, g, view=None):
+    """acc + g with the fp32 gradient accumulator ``acc`` (None: g is the first contribution; it
+    lands in ``view``, the gradient's slot in the arena, unless it was written there already)."""
     if g is None:
         return acc
     if acc is None:
+        if view is not None:
+            if g is not view:
+                view.copy_(g)
+            return view
         return g.float() if g.dtype != torch.float32 else g   # fresh kernel output: take ownership
     if _DEFER is not None and g.dtype == torch.float32 and g.device == acc.device:
         _DEFER.q.append((acc, g))
@@ -136,12 +141,12 @@ class _Layer:
         return [self.s1, self.wqkv, self.bqkv, self.wo, self.bo, self.s2, self.wgu, self.bgu, self.wd, self.bd]
 
 
-def _gate_up_weights(k, layers, W):
+def _gate_up_weights(k, layers, W, want=None):
     """Per layer: whether its gate|up projection runs with SwiGLU in the GEMM epilogue
     (GS.swiglu_epilogue: the kernel reads the natural weight with its rows interleaved in
     64-row blocks and the backward returns natural-layout gradients, so nothing is copied)."""
     for L in layers:
-        L.swi = GS.swiglu_epilogue(k, W(L.wgu))
+        L.swi = GS.swiglu_epilogue(k, W(L.wgu), want)
 
 
 def collect_params(model) -> List[Optional[torch.Tensor]]:
@@ -150,6 +155,51 @@ def collect_params(model) -> List[Optional[torch.Tensor]]:
         ps += _Layer(layer).params()
     ps += [model.norm.scale, model.lm_head.weight, model.lm_head.bias]
     return ps
+
+
+_LAYER_KEYS = ("s1", "wqkv", "bqkv", "wo", "bo", "s2", "wgu", "bgu", "wd", "bd")
+
+
+def arena_groups(model, layers, sp: bool):
+    """Gradient groups in the order the engine's backward completes them (parallel/grad_sync
+    GradArena): the head, the layers top-down (layer 0 after the embedding in the all-reduce
+    engine, whose embedding gradient is produced before layer 0's weight gradients), and the
+    embedding (+ final norm under SP, whose grad is summed over TP after the step)."""
+    head = model.lm_head
+    lay = lambda li: (f"L{li}", list(zip(_LAYER_KEYS, layers[li].params())))
+    nL = len(layers)
+    if sp:
+        return ([("head", [("lm_w", head.weight), ("lm_b", head.bias)])] + [lay(li) for li in range(nL - 1, -1, -1)]
+                + [("tail", [("emb", model.embedding.weight), ("nf", model.norm.scale)])])
+    return ([("head", [("nf", model.norm.scale), ("lm_w", head.weight), ("lm_b", head.bias)])]
+            + [lay(li) for li in range(nL - 1, 0, -1)] + [("emb", [("emb", model.embedding.weight)]), lay(0)])
+
+
+def arena_begin(model, arena) -> bool:
+    """Start of a backward over the arena.  True (the common case, ``zero_grad(set_to_none)``
+    before the backward): the engine assigns the arena views as the parameters' ``.grad`` itself
+    and returns no gradients to autograd (nothing is copied).  False: some ``.grad`` already
+    holds an accumulated gradient -- a ``.grad`` that still aliases the arena is detached
+    (cloned) first, since this backward overwrites the arena, and the gradients go back through
+    autograd, which adds them."""
+    params = [p for p in collect_params(model) if p is not None]
+    if all(p.grad is None for p in params):
+        return True
+    lo, hi = arena.buf.data_ptr(), arena.buf.data_ptr() + 4 * arena.numel
+    for p in params:
+        if p.grad is not None and lo <= p.grad.data_ptr() < hi:
+            p.grad = p.grad.clone()
+    return False
+
+
+def arena_end(model, grads, assign: bool):
+    """The gradients to return from the engine's backward (see ``arena_begin``)."""
+    if not assign:
+        return grads
+    for p, gr in zip(collect_params(model), grads):
+        if p is not None and gr is not None:
+            p.grad = gr
+    return [None] * len(grads)
 
 
 class DecoderTrainFn(torch.autograd.Function):
@@ -178,7 +228,7 @@ class DecoderTrainFn(torch.autograd.Function):
         f8map = F8.prepare([W(w) for L in layers for w in (L.wqkv, L.wo, L.wgu, L.wd)] + [W(model.lm_head.weight)]) \
             if getattr(model.args, "fp8", False) else None
         F8.activate(f8map)
-        _gate_up_weights(k, layers, W)
+        _gate_up_weights(k, layers, W, getattr(model.args, "swiglu_epilogue", None))
         st = []  # per-chunk saved state
         for c in range(C):
             b0, b1 = bounds[c], bounds[c + 1]
@@ -261,14 +311,25 @@ class DecoderTrainFn(torch.autograd.Function):
         tab = ctx.tab
         gscale_all = (gloss.float() / ctx.n_valid)
         nL = len(layers)
-        # fp32 grad accumulators
+        # fp32 gradients: every one is written straight into its slot of the model's gradient
+        # arena (parallel/grad_sync.GradArena; the first chunk's contribution in place, later
+        # chunks accumulated), so the DP all-reduce runs on arena slices with no pack / copy
+        arena = GSY.arena_for(model, arena_groups(model, layers, False), "tp")
+        assign = arena_begin(model, arena)
         g = {"emb": None, "nf": None, "lm_w": None, "lm_b": None}
         gl = [dict() for _ in range(nL)]
+        gname = {id(g): "head"}
+        gname.update({id(gl[li]): f"L{li}" for li in range(nL)})
+        V = lambda d_, key: arena.view(gname[id(d_)] if key != "emb" else "emb", key)
+
+        def first(d_, key, like, n):
+            """fp32 output buffer of a gradient kernel: the arena slot for the first chunk."""
+            return V(d_, key) if d_.get(key) is None else like.new_empty(n, dtype=torch.float32)
 
         def tn(key_dict, key, dy, x):
             acc = key_dict.get(key)
             if acc is None:
-                key_dict[key] = GS.gemm_tn(k, dy, x)
+                key_dict[key] = GS.gemm_tn(k, dy, x, V(key_dict, key))
             else:
                 GS.gemm_tn(k, dy, x, acc, True)
 
@@ -281,7 +342,7 @@ class DecoderTrainFn(torch.autograd.Function):
                 if i + 1 < len(pairs):
                     (a0, b0), (a1, b1) = pairs[i], pairs[i + 1]
                     if key_dict.get(key) is None:
-                        key_dict[key] = GS.gemm_tn_pair(k, a0, b0, a1, b1)
+                        key_dict[key] = GS.gemm_tn_pair(k, a0, b0, a1, b1, V(key_dict, key), False)
                     else:
                         GS.gemm_tn_pair(k, a0, b0, a1, b1, key_dict[key], True)
                     i += 2
@@ -293,19 +354,17 @@ class DecoderTrainFn(torch.autograd.Function):
         def bias_acc(key_dict, key, dy, present):
             if present is None:
                 return
-            key_dict[key] = _addg(key_dict.get(key), k.bias_grad(dy))
+            key_dict[key] = _addg(key_dict.get(key), k.bias_grad(dy), V(key_dict, key))
 
-        # DP: each layer's gradients are queued for the data-parallel average as soon as the
-        # layer's backward completes and go out as async all-reduces of flat fp32 buckets, so
-        # they overlap the remaining layers (DataParallelGradSync's hooks would only fire after
-        # this Function returns).
+        # DP: each layer's gradients are marked complete as soon as the layer's backward is
+        # done and go out as async all-reduces of contiguous arena slices (buckets of at least
+        # the measured knee of the DP group's all-reduce curve, parallel/grad_sync), so they
+        # overlap the remaining layers.
         pg = pm.pgm
         dp = pg.dp_size if pg is not None else 1
-        # buckets of at least the measured knee of the DP group's all-reduce curve
-        # (parallel/grad_sync.dp_bucket_bytes; small per-layer groups are merged)
-        dpb = GSY.DPBucketer(pg.dp_group if dp > 1 else None, dp,
+        dpb = GSY.DPBucketer(arena, pg.dp_group if dp > 1 else None, dp,
                              GSY.dp_bucket_bytes(pg.dp_group, gscale_all.device) if dp > 1 else 0,
-                             before_pack=_defer_flush)
+                             before_launch=_defer_flush)
         dp_reduce = dpb.add
 
         # ---- head: CE backward in place over the logits, lm_head dgrad -> async AR
@@ -313,29 +372,29 @@ class DecoderTrainFn(torch.autograd.Function):
         for ci, s in enumerate(st):
             gs = s["valid"].float() * gscale_all
             dl = s["logits"]
-            db = dl.new_empty(dl.size(1), dtype=torch.float32) if head.bias is not None else None
+            db = first(g, "lm_b", dl, dl.size(1)) if head.bias is not None else None
             k.ce_bwd(dl, s["tgt"], s["ce_lse"], gs, vst, vvalid, dl, db)    # + lm_head bias grad
             dh = GS.gemm_nn(k, dl, W(head.weight), out=_slot(ci, dl.size(0), d, dt))
             s["bh"] = _ar(dh)
             s["dpend"] = dh
             lm_p.append((dl, s["hf"]))
             if db is not None:
-                g["lm_b"] = _addg(g["lm_b"], db)
+                g["lm_b"] = _addg(g["lm_b"], db, V(g, "lm_b"))
             del s["logits"]
         tn_chunks(g, "lm_w", lm_p)
         for s in st:
             _wait(s["bh"])
-            Lt = layers[-1]
-            dbd = s["dpend"].new_empty(s["dpend"].size(1), dtype=torch.float32) if Lt.bd is not None else None
+            Lt, Gt = layers[-1], gl[nL - 1]
+            dbd = first(Gt, "bd", s["dpend"], s["dpend"].size(1)) if Lt.bd is not None else None
             dxf, dsf = k.rmsnorm_bwd(s["dpend"], s["xf"], model.norm.scale, s["rf"], None, dbd)
             if dbd is not None:   # bias grad of the last layer's down projection, same pass
-                gl[nL - 1]["bd"] = _addg(gl[nL - 1].get("bd"), dbd)
+                Gt["bd"] = _addg(Gt.get("bd"), dbd, V(Gt, "bd"))
                 s["bd_done"] = True
-            g["nf"] = _addg(g["nf"], dsf)
+            g["nf"] = _addg(g["nf"], dsf, V(g, "nf"))
             s["g"] = dxf            # grad wrt the last layer's output (residual stream)
             s["dpend"] = None
             del s["xf"], s["hf"]
-        dp_reduce(g, ("nf", "lm_w", "lm_b"))
+        dp_reduce("head")
 
         def rebuild(L, li):
             """Activation recompute: re-run layer li's forward from its saved input up to the
@@ -364,45 +423,42 @@ class DecoderTrainFn(torch.autograd.Function):
             wd_p, wgu_p = [], []
             for ci, s in enumerate(st):
                 if s["dpend"] is not None:     # finish the upper layer: wait, norm1 bwd, residual
-                    _finish_norm1(k, s, layers[li + 1], gl[li + 1], li + 1, (G, L.bd))
+                    _finish_norm1(k, s, layers[li + 1], gl[li + 1], li + 1, (G, L.bd), V=V)
                 a = s["layers"][li]
                 gq = s["g"]
                 if not s.pop("bd_done", False):
                     bias_acc(G, "bd", gq, L.bd)
                 wd_p.append((gq, a["sw"]))
-                dbgu = gq.new_empty(a["gu"].size(1), dtype=torch.float32) if L.bgu is not None else None
+                dbgu = first(G, "bgu", gq, a["gu"].size(1)) if L.bgu is not None else None
                 # down dgrad with the SwiGLU backward (+ gate|up bias grad) in its epilogue
                 dgu = GS.down_dgrad_swiglu(k, gq, W(L.wd), a["gu"], dbgu, L.swi)
                 dh2 = GS.gemm_nn(k, dgu, W(L.wgu), out=_slot(ci, dgu.size(0), d, dt))
                 s["bh"], s["dpend"] = _ar(dh2), dh2
                 wgu_p.append((dgu, a["h2"]))
                 if dbgu is not None:
-                    G["bgu"] = _addg(G.get("bgu"), dbgu)
+                    G["bgu"] = _addg(G.get("bgu"), dbgu, V(G, "bgu"))
                 del a["sw"], a["gu"]
             tn_chunks(G, "wd", wd_p)        # under the chunks' all-reduces
             tn_chunks(G, "wgu", wgu_p)
             if li + 1 < nL:
-                dp_reduce(gl[li + 1])           # layer li+1 is complete (its norm1 grad just landed)
+                dp_reduce(f"L{li + 1}")         # layer li+1 is complete (its norm1 grad just landed)
             # b1: wait, norm2 bwd, Wo / attention / QKV grads -> AR(dh)
             wo_p, wqkv_p = [], []
             for ci, s in enumerate(st):
                 a = s["layers"][li]
                 _wait(s["bh"])
-                dbo = None
-                if L.bo is not None:
-                    dbo = s["dpend"].new_empty(s["dpend"].size(1), dtype=torch.float32)
+                dbo = first(G, "bo", s["dpend"], s["dpend"].size(1)) if L.bo is not None else None
                 g2, ds2 = k.rmsnorm_bwd(s["dpend"], a["x2"], L.s2, a["r2"], s["g"], dbo)  # + residual grad, bo grad
-                G["s2"] = _addg(G.get("s2"), ds2)
+                G["s2"] = _addg(G.get("s2"), ds2, V(G, "s2"))
                 if dbo is not None:
-                    G["bo"] = _addg(G.get("bo"), dbo)
+                    G["bo"] = _addg(G.get("bo"), dbo, V(G, "bo"))
                 do = GS.gemm_nn(k, g2, W(L.wo))
                 wo_p.append((g2, a["o"].view(g2.size(0), -1)))
                 Bc = s["B"]
                 q, kk, v = _split(a["qkv"], Bc, T, L.h, L.hd)
                 dqkv = torch.empty_like(a["qkv"])
                 dq, dk, dv = _split(dqkv, Bc, T, L.h, L.hd)
-                dbq = dqkv.new_empty(dqkv.size(1), dtype=torch.float32) \
-                    if L.bqkv is not None and _QKV_BIAS_IN_ATTN else None
+                dbq = first(G, "bqkv", dqkv, dqkv.size(1)) if L.bqkv is not None else None
                 # inverse RoPE fused into the dq/dk stores, the QKV bias grad into their epilogues
                 bq_fused = k.attn_bwd(do.view(Bc, T, L.h, L.hd), q, kk, v, a["o"], a["lse"], 1.0 / math.sqrt(L.hd),
                                       True, dq, dk, dv, s["pos"], tab, dbias=dbq)
@@ -410,18 +466,25 @@ class DecoderTrainFn(torch.autograd.Function):
                 s["bh"], s["dpend"] = _ar(dh), dh
                 wqkv_p.append((dqkv, a["h1"]))
                 if L.bqkv is not None:
-                    G["bqkv"] = _addg(G.get("bqkv"), dbq if bq_fused else k.bias_grad(dqkv))
+                    G["bqkv"] = _addg(G.get("bqkv"), dbq if bq_fused else k.bias_grad(dqkv), V(G, "bqkv"))
                 s["g"] = g2
                 for key in ("x2", "r2", "h2", "qkv", "o", "lse"):
                     a.pop(key, None)
-            tn_chunks(G, "wo", wo_p)
-            tn_chunks(G, "wqkv", wqkv_p)
+            if li > 0:
+                tn_chunks(G, "wo", wo_p)
+                tn_chunks(G, "wqkv", wqkv_p)
+        # layer 0: the embedding gradient first, so its all-reduce (the largest DP bucket) runs
+        # under layer 0's Wo / QKV weight-gradient GEMMs
+        ev = arena.view("emb", "emb")
+        ev.zero_()
         for s in st:
-            _finish_norm1(k, s, layers[0], gl[0], 0)
-            dwe = k.embedding_bwd(s["g"], s["ids"], model.embedding.weight.size(0), model.embedding.vocab_st_idx)
-            g["emb"] = _addg(g["emb"], dwe)
-        dp_reduce(gl[0])
-        dp_reduce(g, ("emb",))
+            _finish_norm1(k, s, layers[0], gl[0], 0, V=V)
+            k.embedding_bwd(s["g"], s["ids"], model.embedding.weight.size(0), model.embedding.vocab_st_idx, out=ev)
+        g["emb"] = ev
+        dp_reduce("emb")
+        tn_chunks(gl[0], "wo", wo_p)
+        tn_chunks(gl[0], "wqkv", wqkv_p)
+        dp_reduce("L0")
         _defer_end()
         tp_comm.check()   # an xGMI barrier that timed out raises here (host-mapped flag, no sync)
         if dpb.finish():
@@ -436,32 +499,31 @@ class DecoderTrainFn(torch.autograd.Function):
                       G.get("bd") if L.bd is not None else None]
         grads += [g["nf"], g["lm_w"], g["lm_b"] if head.bias is not None else None]
         F8.activate(None)
-        return (None, None, None, None, None, None) + tuple(grads)
+        return (None, None, None, None, None, None) + tuple(arena_end(model, grads, assign))
 
 
-def _finish_norm1(k, s, L, G, li, below=None):
+def _finish_norm1(k, s, L, G, li, below=None, V=None):
     """Wait for the all-reduce of layer li's norm1 input-grad, run the norm1 backward and add
     it to the residual-stream grad (-> grad wrt layer li's input).  ``below`` = (grad dict,
     bias) of layer li-1's down projection: its bias grad (column sums of that residual grad)
-    comes out of the same norm-backward pass."""
+    comes out of the same norm-backward pass.  ``V(dict, key)``: the gradient's arena slot."""
     a = s["layers"][li]
     _wait(s["bh"])
     db = None
+    view = V if V is not None else (lambda d_, key: None)
     if below is not None and below[1] is not None:
-        db = s["g"].new_empty(s["g"].size(1), dtype=torch.float32)
+        Gb = below[0]
+        db = view(Gb, "bd") if Gb.get("bd") is None else None
+        if db is None:
+            db = s["g"].new_empty(s["g"].size(1), dtype=torch.float32)
     s["g"], ds1 = k.rmsnorm_bwd(s["dpend"], a["x"], L.s1, a["r1"], s["g"], db)   # fused residual-grad add
     if db is not None:
-        below[0]["bd"] = _addg(below[0].get("bd"), db)
+        below[0]["bd"] = _addg(below[0].get("bd"), db, view(below[0], "bd"))
         s["bd_done"] = True
-    G["s1"] = _addg(G.get("s1"), ds1)
+    G["s1"] = _addg(G.get("s1"), ds1, view(G, "s1"))
     s["dpend"] = None
     for key in ("x", "r1", "h1"):
         a.pop(key, None)
-
-
-# The QKV bias gradient from the attention backward's epilogues (default) or a separate column
-# sum over d(QKV) (DPFS_QKV_BIAS_IN_ATTN=0, A/B runs).
-_QKV_BIAS_IN_ATTN = os.environ.get("DPFS_QKV_BIAS_IN_ATTN", "1") != "0"
 
 
 def _split(qkv, B, T, h, hd):

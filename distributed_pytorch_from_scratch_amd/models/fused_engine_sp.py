@@ -39,7 +39,7 @@ from ..ops.dispatch import K, shadow
 from ..parallel import grad_sync as GSY
 from ..parallel import process_manager as pm
 from ..parallel import tp_comm
-from .fused_engine import (_QKV_BIAS_IN_ATTN, _Layer, _addg, _defer_begin, _defer_end, _defer_flush,
+from .fused_engine import (_Layer, arena_begin, arena_end, arena_groups, _addg, _defer_begin, _defer_end, _defer_flush,
                            _gate_up_weights, _split, _wait)
 
 
@@ -85,7 +85,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
         f8map = F8.prepare([W(w) for L in layers for w in (L.wqkv, L.wo, L.wgu, L.wd)] + [W(model.lm_head.weight)]) \
             if getattr(model.args, "fp8", False) else None
         F8.activate(f8map)
-        _gate_up_weights(k, layers, W)
+        _gate_up_weights(k, layers, W, getattr(model.args, "swiglu_epilogue", None))
         st = []
         for c in range(C):
             b0, b1 = bounds[c], bounds[c + 1]
@@ -172,12 +172,22 @@ class DecoderTrainFnSP(torch.autograd.Function):
         tab = ctx.tab
         gscale_all = gloss.float() / ctx.n_valid
         nL = len(layers)
+        # fp32 gradients straight into the model's gradient arena (parallel/grad_sync.GradArena):
+        # DP all-reduces run on contiguous slices of it, no pack / copy back
+        arena = GSY.arena_for(model, arena_groups(model, layers, True), "sp")
+        assign = arena_begin(model, arena)
         g = {"emb": None, "nf": None, "lm_w": None, "lm_b": None}
         gl = [dict() for _ in range(nL)]
+        gname = {id(gl[li]): f"L{li}" for li in range(nL)}
+        V = lambda d_, key: arena.view(gname.get(id(d_)) or ("tail" if key in ("emb", "nf") else "head"), key)
+
+        def first(d_, key, like, n):
+            """fp32 output buffer of a gradient kernel: the arena slot for the first chunk."""
+            return V(d_, key) if d_.get(key) is None else like.new_empty(n, dtype=torch.float32)
 
         def tn(d, key, dy, x):
             if d.get(key) is None:
-                d[key] = GS.gemm_tn(k, dy, x)
+                d[key] = GS.gemm_tn(k, dy, x, V(d, key))
             else:
                 GS.gemm_tn(k, dy, x, d[key], True)
 
@@ -190,7 +200,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 if i + 1 < len(pairs):
                     (a0, b0), (a1, b1) = pairs[i], pairs[i + 1]
                     if d.get(key) is None:
-                        d[key] = GS.gemm_tn_pair(k, a0, b0, a1, b1)
+                        d[key] = GS.gemm_tn_pair(k, a0, b0, a1, b1, V(d, key), False)
                     else:
                         GS.gemm_tn_pair(k, a0, b0, a1, b1, d[key], True)
                     i += 2
@@ -203,9 +213,9 @@ class DecoderTrainFnSP(torch.autograd.Function):
         dp = pg.dp_size
         # buckets of at least the measured knee of the DP group's all-reduce curve
         # (parallel/grad_sync.dp_bucket_bytes; small per-layer groups are merged)
-        dpb = GSY.DPBucketer(pg.dp_group if dp > 1 else None, dp,
+        dpb = GSY.DPBucketer(arena, pg.dp_group if dp > 1 else None, dp,
                              GSY.dp_bucket_bytes(pg.dp_group, gscale_all.device) if dp > 1 else 0,
-                             before_pack=_defer_flush)
+                             before_launch=_defer_flush)
         dp_reduce = dpb.add
 
         d = model.args.attn_dim
@@ -213,31 +223,31 @@ class DecoderTrainFnSP(torch.autograd.Function):
         for ci, s in enumerate(st):    # CE backward in place, lm_head dgrad -> reduce-scatter, lm_head wgrad
             gs = s["valid"].float() * gscale_all
             dl = s["logits"]
-            db = dl.new_empty(dl.size(1), dtype=torch.float32) if head.bias is not None else None
+            db = first(g, "lm_b", dl, dl.size(1)) if head.bias is not None else None
             k.ce_bwd(dl, s["tgt"], s["ce_lse"], gs, vst, vvalid, dl, db)
             s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dl, W(head.weight), out=_slot(ci, dl.size(0), d, dt)), n)
             lm_p.append((dl, s["hf"]))
             if db is not None:
-                g["lm_b"] = _addg(g["lm_b"], db)
+                g["lm_b"] = _addg(g["lm_b"], db, V(g, "lm_b"))
             del s["logits"], s["hf"]
         tn_chunks(g, "lm_w", lm_p)
         def norm_bwd(dy, x, w, r, dres, bias_below, below_key):
             """RMSNorm backward on my rows (+ residual grad); the bias grad of the projection
             whose output feeds this residual (column sums of the result) from the same pass."""
-            db = dy.new_empty(dy.size(1), dtype=torch.float32) if bias_below is not None else None
+            db = first(below_key[0], below_key[1], dy, dy.size(1)) if bias_below is not None else None
             out, ds = k.rmsnorm_bwd(dy, x, w, r, dres, db)
             if db is not None:
-                below_key[0][below_key[1]] = _addg(below_key[0].get(below_key[1]), db)
+                below_key[0][below_key[1]] = _addg(below_key[0].get(below_key[1]), db, V(*below_key))
             return out, ds
 
         for s in st:    # final norm backward on my rows -> all-gather the residual grad
             _wait(s["h"])
             s["g"], dsf = norm_bwd(s["dpend"], s["xf"], model.norm.scale, s["rf"], None,
                                    layers[-1].bd, (gl[nL - 1], "bd"))
-            g["nf"] = _addg(g["nf"], dsf)
+            g["nf"] = _addg(g["nf"], dsf, V(g, "nf"))
             s["gfull"], s["h"] = _ag(s["g"], n)
             del s["xf"], s["rf"], s["dpend"]
-        dp_reduce(g, ("lm_w", "lm_b"))
+        dp_reduce("head")
 
         def rebuild(L, li):
             """Activation recompute: re-run layer li's forward (with its collectives) from the
@@ -276,13 +286,13 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 # (bd's grad, partial over my rows and summed over TP by TrainStep, came out of
                 # the norm backward above this layer)
                 wd_p.append((gq, a["sw"]))
-                dbgu = gq.new_empty(a["gu"].size(1), dtype=torch.float32) if L.bgu is not None else None
+                dbgu = first(G, "bgu", gq, a["gu"].size(1)) if L.bgu is not None else None
                 # down dgrad with the SwiGLU backward (+ gate|up bias grad) in its epilogue
                 dgu = GS.down_dgrad_swiglu(k, gq, W(L.wd), a["gu"], dbgu, L.swi)
                 s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dgu, W(L.wgu), out=_slot(ci, dgu.size(0), d, dt)), n)
                 wgu_p.append((dgu, a["h2"]))
                 if dbgu is not None:
-                    G["bgu"] = _addg(G.get("bgu"), dbgu)
+                    G["bgu"] = _addg(G.get("bgu"), dbgu, V(G, "bgu"))
                 del a["sw"], a["gu"], a["h2"], s["gfull"]
             tn_chunks(G, "wd", wd_p)       # under the chunks' reduce-scatters
             tn_chunks(G, "wgu", wgu_p)
@@ -290,7 +300,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 _wait(s["h"])
                 a = s["layers"][li]
                 s["g"], ds2 = norm_bwd(s["dpend"], a["x2"], L.s2, a["r2"], s["g"], L.bo, (G, "bo"))
-                G["s2"] = _addg(G.get("s2"), ds2)
+                G["s2"] = _addg(G.get("s2"), ds2, V(G, "s2"))
                 s["gfull"], s["h"] = _ag(s["g"], n)
                 del a["x2"], a["r2"], s["dpend"]
             wo_p, wqkv_p = [], []
@@ -303,14 +313,13 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 q, kk, v = _split(a["qkv"], Bc, T, L.h, L.hd)
                 dqkv = torch.empty_like(a["qkv"])
                 dq, dk, dv = _split(dqkv, Bc, T, L.h, L.hd)
-                dbq = dqkv.new_empty(dqkv.size(1), dtype=torch.float32) \
-                    if L.bqkv is not None and _QKV_BIAS_IN_ATTN else None
+                dbq = first(G, "bqkv", dqkv, dqkv.size(1)) if L.bqkv is not None else None
                 bq_fused = k.attn_bwd(do.view(Bc, T, L.h, L.hd), q, kk, v, a["o"], a["lse"], 1.0 / math.sqrt(L.hd),
                                       True, dq, dk, dv, s["pos"], tab, dbias=dbq)
                 s["dpend"], s["h"] = _rs(GS.gemm_nn(k, dqkv, W(L.wqkv), out=_slot(ci, dqkv.size(0), d, dt)), n)
                 wqkv_p.append((dqkv, a["h1"]))
                 if L.bqkv is not None:
-                    G["bqkv"] = _addg(G.get("bqkv"), dbq if bq_fused else k.bias_grad(dqkv))
+                    G["bqkv"] = _addg(G.get("bqkv"), dbq if bq_fused else k.bias_grad(dqkv), V(G, "bqkv"))
                 for key in ("qkv", "o", "lse", "h1"):
                     a.pop(key, None)
                 del s["gfull"]
@@ -321,17 +330,19 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 a = s["layers"][li]
                 s["g"], ds1 = norm_bwd(s["dpend"], a["x"], L.s1, a["r1"], s["g"],
                                        layers[li - 1].bd if li > 0 else None, (gl[li - 1], "bd"))
-                G["s1"] = _addg(G.get("s1"), ds1)
+                G["s1"] = _addg(G.get("s1"), ds1, V(G, "s1"))
                 s["gfull"], s["h"] = _ag(s["g"], n)
                 del a["x"], a["r1"], s["dpend"]
-            dp_reduce(G)
+            dp_reduce(f"L{li}")
+        ev = arena.view("tail", "emb")
+        ev.zero_()
         for s in st:    # embedding backward over all rows of the chunk (vocab-sharded table)
             _wait(s["h"])
-            dwe = k.embedding_bwd(s["gfull"], s["ids"], model.embedding.weight.size(0),
-                                  model.embedding.vocab_st_idx)
-            g["emb"] = _addg(g["emb"], dwe)
+            k.embedding_bwd(s["gfull"], s["ids"], model.embedding.weight.size(0), model.embedding.vocab_st_idx,
+                            out=ev)
             del s["gfull"]
-        dp_reduce(g, ("emb", "nf"))
+        g["emb"] = ev
+        dp_reduce("tail")
         _defer_end()
         tp_comm.check()
         if dpb.finish():
@@ -346,4 +357,4 @@ class DecoderTrainFnSP(torch.autograd.Function):
                       G.get("bd") if L.bd is not None else None]
         grads += [g["nf"], g["lm_w"], g["lm_b"] if head.bias is not None else None]
         F8.activate(None)
-        return (None, None, None, None, None, None) + tuple(grads)
+        return (None, None, None, None, None, None) + tuple(arena_end(model, grads, assign))

@@ -28,6 +28,10 @@ from typing import List, Optional
 
 import torch
 
+# decode steps captured per HIP graph replay (the host reads the tokens / checks EOS once per
+# replay; profiles/r2_decode_bench.jsonl)
+_GRAPH_STEPS = 8
+
 from ..ops import gemm_select as GS
 from ..ops.dispatch import K, shadow
 from ..parallel import comm_ops
@@ -122,7 +126,7 @@ def decode_step(model, ids: torch.Tensor, pos: torch.Tensor, cache: KVCache):
     x = model.embedding(ids).reshape(B, -1).to(dt)
     tab = model.rope_table(dev)
     pend = pend_bias = None
-    small = B <= 16 and os.environ.get("DPFS_DECODE_GEMV", "1") != "0"
+    small = B <= 16
 
     def proj(a, w, bias=None, swiglu=False):
         if small:   # MFMA GEMV-class kernel, SwiGLU fused into the down projection's operand
@@ -279,7 +283,7 @@ def generate(model, prompt: torch.Tensor, max_new_tokens: int, eos_id: Optional[
     nxt = logits_step(model, prompt, cache).argmax(-1)
     cache.sync_device_len()
     pos = torch.full((B,), cache.len, dtype=torch.int64, device=dev)
-    chunk = max(1, int(os.environ.get("DPFS_DECODE_GRAPH_STEPS", "8")))
+    chunk = _GRAPH_STEPS
     n_gen = 0
 
     def emit(row) -> bool:

@@ -30,8 +30,9 @@ def _load():
         return
     # The attention kernel generation is a per-call argument (``impl`` of attn_fwd / attn_bwd,
     # 0 = the per-head-dim default, the measured winner).  For same-box A/B runs of whole models
-    # DPFS_ATTN_IMPL / DPFS_ATTN_BWD_IMPL, read once here, become the default of that argument.
-    fi, bi = int(os.environ.get("DPFS_ATTN_IMPL") or 0), int(os.environ.get("DPFS_ATTN_BWD_IMPL") or 0)
+    # DPFS_ATTN_IMPL = "<fwd>[,<bwd>]", read once here, becomes the default of that argument.
+    spec = (os.environ.get("DPFS_ATTN_IMPL") or "0").split(",")
+    fi, bi = int(spec[0] or 0), int(spec[1] if len(spec) > 1 and spec[1] else 0)
     if fi or bi:
         _C = _AttnImplDefaults(_C, fi, bi)
 

@@ -68,7 +68,7 @@ def _lib() -> bool:
 
 def _lt_count(k, layout: int, M: int, N: int, K: int, bias: bool) -> int:
     """Algorithms hipBLASLt offers for this problem through our binding (0: none / disabled)."""
-    if not _lib() or os.environ.get("DPFS_GEMM_LT", "1") == "0" or not hasattr(k, "lt_algos"):
+    if not _lib() or not hasattr(k, "lt_algos"):
         return 0
     return int(k.lt_algos(layout, M, N, K, bias))
 
@@ -190,16 +190,16 @@ def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, out=None) -> torch.T
     return blas() if c == "blas" else lt(_lt_index(c))()
 
 
-def swiglu_epilogue(k, w: torch.Tensor) -> bool:
+def swiglu_epilogue(k, w: torch.Tensor, want: Optional[bool] = None) -> bool:
     """Whether the gate|up projection of packed weight ``w`` [2F, d] runs with SwiGLU in its GEMM
-    epilogue (``gate_up``): on the GPU by default (``DPFS_SWIGLU_EPILOGUE=0`` turns it off,
-    as do a pinned library backend and the fp8 step), on the CPU oracle only when that
-    variable is 1 (tests of the interleaved layout's plumbing)."""
-    env = os.environ.get("DPFS_SWIGLU_EPILOGUE", "")
-    if w.size(0) % 128 or env == "0":
+    epilogue (``gate_up``).  ``want`` = ``ModelArgs.swiglu_epilogue``: None (default) = on the
+    GPU kernels (not with a pinned library backend or the fp8 step), off on the CPU oracle;
+    True runs the interleaved layout on the CPU oracle too (tests of its plumbing); False
+    turns it off."""
+    if w.size(0) % 128 or want is False:
         return False
     if k is reference or not w.is_cuda:
-        return env == "1"
+        return bool(want)
     return mode() in ("auto", "ours") and F8.lookup(w) is None and hasattr(k, "gemm_nt_swiglu")
 
 
@@ -225,10 +225,11 @@ def down_dgrad_swiglu(k, dy: torch.Tensor, w: torch.Tensor, gu: torch.Tensor, db
     """d gate|up (natural layout) = SwiGLU'(gu) * (dy w): the down projection's data gradient
     with the SwiGLU backward in the GEMM epilogue (gemm_nn_swiglu_bwd: dy w never reaches
     memory; the gate|up bias gradient comes from the same kernel into ``dbias``).  Falls back to
-    gemm_nn + swiglu_bwd where the fused kernel declines the shape, for the fp8 step, a pinned
-    library backend, or with ``DPFS_SWIGLU_BWD_EPILOGUE=0`` (A/B runs)."""
+    gemm_nn + swiglu_bwd where the fused kernel declines the shape, for the fp8 step or a pinned
+    library backend (profiles/r4_swiglu_bwd_epilogue_ab.txt: the fused form is 0.40 ms/step
+    faster)."""
     fused = (k is not reference and dy.is_cuda and mode() in ("auto", "ours") and F8.lookup(w, dgrad=True) is None
-             and os.environ.get("DPFS_SWIGLU_BWD_EPILOGUE", "1") != "0" and hasattr(k, "gemm_nn_swiglu_bwd"))
+             and hasattr(k, "gemm_nn_swiglu_bwd"))
     if fused:
         r = k.gemm_nn_swiglu_bwd(dy, w, gu, dbias, perm)
         if r:
@@ -328,7 +329,7 @@ def gemm_nt_rope(k, x: torch.Tensor, w: torch.Tensor, bias, pos, tab, rot_heads:
     # (only where the rotation is fused into the Q|K launch's epilogue: the separate RoPE pass
     # of other head dims needs a contiguous output)
     split_ok = hd in (64, 128) and 0 < rot < N and rot % 256 == 0 and (N - rot) % 64 == 0 and \
-        w.is_contiguous() and os.environ.get("DPFS_QKV_SPLIT", "1") != "0"
+        w.is_contiguous() and (bias is None or bias.is_contiguous())
 
     def ours_split():
         y = torch.empty(M, N, device=x.device, dtype=x.dtype)
@@ -339,11 +340,13 @@ def gemm_nt_rope(k, x: torch.Tensor, w: torch.Tensor, bias, pos, tab, rot_heads:
         return blas()
     if m == "lt":
         return lt(0)() if lt_ok and _lt_count(k, 0, M, N, K, bias is not None) else blas()
-    key = ("nt_rope", M, N, K, hd, x.device.index)
+    # (rot and split_ok in the key: a cached ``ours_split`` choice is only reused where the
+    # split form applies to this call)
+    key = ("nt_rope", M, N, K, hd, rot, split_ok, x.device.index)
     c = _pick(key, {**_ours_variants(ours), **({"ours_split": ours_split} if split_ok else {}),
                     **({"blas": blas} if _lib() else {})},
               lambda: _lt_count(k, 0, M, N, K, bias is not None), lt if lt_ok else None)
-    if c == "ours_split":
+    if c == "ours_split" and split_ok:
         return ours_split()
     if c.startswith("ours") or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
         return _run_ours(ours, c)
@@ -438,13 +441,12 @@ def gemm_tn_pair(k, a0: torch.Tensor, b0: torch.Tensor, a1: torch.Tensor, b1: to
     chunked step.  Candidates, timed per shape like the others: ``pair`` = ONE split-K launch
     whose K-splits read either chunk's buffers and ONE slab reduction (``gemm_tn2``: the plan
     of a single tall GEMM), ``split`` = two :func:`gemm_tn` calls (two under-filled grids,
-    two reductions).  ``DPFS_TN_PAIR=0`` always splits (A/B runs)."""
+    two reductions)."""
     def split(dst, acc):
         c = gemm_tn(k, a0, b0, dst, acc)
         return gemm_tn(k, a1, b1, c, True)
 
-    if k is reference or not a0.is_cuda or not hasattr(k, "gemm_tn2") or mode() not in ("auto", "ours") \
-            or os.environ.get("DPFS_TN_PAIR", "1") == "0":
+    if k is reference or not a0.is_cuda or not hasattr(k, "gemm_tn2") or mode() not in ("auto", "ours"):
         return split(out, accumulate)
     M, N = a0.shape[1], b0.shape[1]
     if not _aligned(M, N) or min(a0.shape[0], a1.shape[0]) < _MIN_ROWS:

@@ -373,10 +373,12 @@ def embedding_fwd(ids: torch.Tensor, weight: torch.Tensor, vocab_start: int,
     return out.to(out_dtype)
 
 
-def embedding_bwd(dout: torch.Tensor, ids: torch.Tensor, v_local: int, vocab_start: int) -> torch.Tensor:
+def embedding_bwd(dout: torch.Tensor, ids: torch.Tensor, v_local: int, vocab_start: int,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 dW[v_local, D] of the masked embedding (rows ADDED to ``out`` when given)."""
     local = ids.long() - vocab_start
     m = (local >= 0) & (local < v_local)
-    dw = torch.zeros(v_local, dout.size(-1), dtype=torch.float32, device=dout.device)
+    dw = out if out is not None else torch.zeros(v_local, dout.size(-1), dtype=torch.float32, device=dout.device)
     dw.index_add_(0, local[m], dout[m].float())
     return dw
 

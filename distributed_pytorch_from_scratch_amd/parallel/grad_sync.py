@@ -73,72 +73,159 @@ def measure_bucket_knee(group, device, sizes_mb=DP_BUCKET_SIZES_MB, frac: float 
     return int(sizes_mb[-1] * 2 ** 20)
 
 
-def dp_bucket_bytes(group, device) -> int:
+def _bucket_env() -> Optional[float]:
+    """``DPFS_DP_BUCKET_MB``: None = auto, else MB (validated here, outside any autograd pass)."""
+    env = os.environ.get("DPFS_DP_BUCKET_MB", "auto").strip().lower()
+    if env == "auto":
+        return None
+    try:
+        mb = float(env)
+    except ValueError:
+        raise ValueError(f"DPFS_DP_BUCKET_MB must be 'auto' or a number of MB, got {env!r}") from None
+    if mb < 0:
+        raise ValueError(f"DPFS_DP_BUCKET_MB must be >= 0, got {mb}")
+    return mb
+
+
+def dp_bucket_bytes(group, device, world_max: bool = False) -> int:
     """DP bucket size of the fused engines: ``DPFS_DP_BUCKET_MB`` = a number of MB (0: every
     gradient group is its own all-reduce, the pre-bucketing behaviour), or ``auto`` (default on
-    RCCL: ``measure_bucket_knee`` once per group; on gloo 0)."""
+    RCCL: ``measure_bucket_knee`` once per group; on gloo 0).  ``world_max``: the value is
+    MAX-reduced over the default (WORLD) group, so every DP group of a TP x DP grid uses one
+    size -- every rank must call it then (``setup_dp_buckets``, at step construction)."""
     key = id(group)
     if key in _BUCKET_CACHE:
         return _BUCKET_CACHE[key]
-    env = os.environ.get("DPFS_DP_BUCKET_MB", "auto").strip().lower()
-    if env == "auto":
+    mb = _bucket_env()
+    if mb is None:
         nb = measure_bucket_knee(group, device) if dist.get_backend(group) == "nccl" else 0
     else:
-        nb = int(float(env) * 2 ** 20)
+        nb = int(mb * 2 ** 20)
+    if world_max and dist.get_world_size() > 1:
+        t = torch.tensor([float(nb)], dtype=torch.float64,
+                         device=device if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        nb = int(t.item())
     _BUCKET_CACHE[key] = nb
     return nb
 
 
-class DPBucketer:
-    """The fused engines' DP gradient averaging: gradient groups (a dict of fp32 tensors and the
-    keys to reduce) are queued as the backward completes them and launched as ONE async
-    all-reduce of a flat buffer once the queued bytes reach ``bucket_bytes`` (0: every group at
-    once); ``finish`` launches the rest, waits, averages and writes the values back into the
-    dicts (the flat buffer's views replace the tensors).  ``before_pack`` runs before a bucket
-    is packed (the engines flush their deferred gradient sums there)."""
+def setup_dp_buckets(device) -> None:
+    """Measure (or read) the DP bucket size once at step construction, outside the backward,
+    on every rank (MAX over the WORLD group)."""
+    p = pm.pgm
+    if p is not None and p.dp_size > 1:
+        dp_bucket_bytes(p.dp_group, device, world_max=True)
 
-    def __init__(self, group, dp: int, bucket_bytes: int, before_pack: Optional[Callable[[], None]] = None):
-        self.group, self.dp, self.bucket_bytes, self.before_pack = group, dp, bucket_bytes, before_pack
-        self._queued: List[tuple] = []
-        self._bytes = 0
+
+def reset() -> None:
+    """Forget the cached bucket sizes (a new process-group layout)."""
+    _BUCKET_CACHE.clear()
+
+
+class GradArena:
+    """One flat fp32 buffer holding every gradient of the fused engines' step, laid out in the
+    order the backward completes them (``groups``: a list of (group name, [(key, param), ...])).
+
+    The engines write each gradient straight into its view (the weight-gradient GEMMs, the bias /
+    norm / embedding reductions take it as their output; later ping-pong chunks accumulate into
+    it), the parameters' ``.grad`` become those views, and a DP bucket is a contiguous range of
+    the buffer: the data-parallel all-reduce runs on it in place -- no pack, no copy back.  The
+    buffer lives with the model (allocated once), so the previous step's gradients and this
+    step's share the same 4 bytes per parameter (utils/memory.py)."""
+
+    def __init__(self, groups, device):
+        self.order = [name for name, _ in groups]
+        self.ranges: Dict[str, tuple] = {}
+        self.slots: Dict[tuple, tuple] = {}       # (group, key) -> (offset, shape)
+        off = 0
+        for name, items in groups:
+            start = off
+            for key, p in items:
+                if p is None:
+                    continue
+                self.slots[(name, key)] = (off, tuple(p.shape))
+                off += p.numel()
+            self.ranges[name] = (start, off)
+        self.numel = off
+        self.buf = torch.empty(off, dtype=torch.float32, device=device)
+        self.signature = None
+
+    def view(self, name, key) -> Optional[torch.Tensor]:
+        s = self.slots.get((name, key))
+        if s is None:
+            return None
+        off, shape = s
+        n = 1
+        for d in shape:
+            n *= d
+        return self.buf[off:off + n].view(shape)
+
+
+def arena_for(model, groups, tag: str) -> GradArena:
+    """The model's gradient arena for this engine layout (``tag``), rebuilt when a parameter is
+    replaced, moved or resized."""
+    sig = (tag,) + tuple((name, key, id(p), tuple(p.shape), str(p.device)) for name, items in groups
+                         for key, p in items if p is not None)
+    a = getattr(model, "_dpfs_grad_arena", None)
+    if a is None or a.signature != sig:
+        dev = next(p for _, items in groups for _, p in items if p is not None).device
+        a = GradArena(groups, dev)
+        a.signature = sig
+        model._dpfs_grad_arena = a
+    return a
+
+
+class DPBucketer:
+    """The fused engines' DP gradient averaging over a :class:`GradArena`: gradient groups are
+    marked complete (``add(name)``) in arena order as the backward finishes them, and a bucket
+    -- the contiguous range of completed groups -- goes out as ONE async all-reduce of that slice
+    of the arena, in place, once it holds ``bucket_bytes`` (0: every group at once).  ``finish``
+    launches the rest, waits and averages in place.  ``before_launch`` runs before a bucket is
+    launched (the engines flush their deferred gradient sums there)."""
+
+    def __init__(self, arena: Optional[GradArena], group, dp: int, bucket_bytes: int,
+                 before_launch: Optional[Callable[[], None]] = None):
+        self.arena, self.group, self.dp, self.bucket_bytes = arena, group, dp, bucket_bytes
+        self.before_launch = before_launch
+        self._lo = self._hi = None
         self._pending: List[tuple] = []
         self.launches = 0
 
-    def add(self, d: dict, keys=None) -> None:
-        if self.dp <= 1:
+    def add(self, name: str) -> None:
+        if self.dp <= 1 or self.arena is None:
             return
-        keys = [k for k in (keys or sorted(d)) if d.get(k) is not None]
-        if not keys:
+        a, b = self.arena.ranges[name]
+        if b == a:
             return
-        self._queued.append((d, keys))
-        self._bytes += sum(d[k].numel() * 4 for k in keys)
-        if self._bytes >= self.bucket_bytes:
+        if self._hi is not None and a != self._hi:    # not adjacent to the open bucket: close it
+            self._launch()
+        if self._lo is None:
+            self._lo = a
+        self._hi = b
+        if 4 * (self._hi - self._lo) >= self.bucket_bytes:
             self._launch()
 
     def _launch(self) -> None:
-        if not self._queued:
+        if self._lo is None or self._hi == self._lo:
+            self._lo = self._hi = None
             return
-        if self.before_pack is not None:
-            self.before_pack()
-        flat = torch.cat([d[k].reshape(-1).float() for d, keys in self._queued for k in keys])
-        h = dist.all_reduce(flat, group=self.group, async_op=True)
-        self._pending.append((h, flat, self._queued))
-        self._queued, self._bytes = [], 0
+        if self.before_launch is not None:
+            self.before_launch()
+        sl = self.arena.buf[self._lo:self._hi]
+        h = dist.all_reduce(sl, group=self.group, async_op=True)
+        self._pending.append((h, sl))
+        self._lo = self._hi = None
         self.launches += 1
 
     def finish(self) -> bool:
-        """Launch what is queued, wait for every bucket, average; True if anything was reduced."""
+        """Launch what is open, wait for every bucket, average in place; True if anything was
+        reduced."""
         self._launch()
         done = bool(self._pending)
-        for h, flat, groups in self._pending:
+        for h, sl in self._pending:
             h.wait()
-            flat /= self.dp
-            off = 0
-            for d, keys in groups:
-                for k in keys:
-                    n = d[k].numel()
-                    d[k] = flat[off:off + n].view_as(d[k])
-                    off += n
+            sl.div_(self.dp)
         self._pending = []
         return done
 

@@ -13,12 +13,17 @@
 * ``auto``: on the first TP collective of the process, every TP rank builds the xGMI
   communicator and, for each of all-reduce, reduce-scatter and all-gather separately, checks
   its results against an fp32 ProcessGroupNCCL sum on a rank-dependent tensor of the live
-  message size and times both (xGMI at several grid widths).  An op leaves ProcessGroupNCCL
-  only if xGMI was correct on every rank and at least 3 % faster (max over ranks).  Every
-  rank reaches the same decisions (they are computed from all-reduced numbers), so the call
+  message size, then times the candidates per op AND per size class (``SIZE_CLASSES``: small
+  messages <= 1 MiB, medium <= 16 MiB, large; one representative size each): ProcessGroupNCCL,
+  the xGMI two-shot kernels at several grid widths, the xGMI one-shot all-reduce (one barrier;
+  small / medium classes) and the relay.  An (op, class) leaves ProcessGroupNCCL only if the
+  candidate was correct on every rank and at least 3 % faster (max over ranks).  Every rank
+  reaches the same decisions (they are computed from all-reduced numbers), so the call
   sequence stays identical across the group.  (``native`` runs the same RCCL kernels as
-  ProcessGroupNCCL, so ``auto`` does not open a second RCCL communicator: two communicators
-  with kernels in flight at once are only safe while the GPU can hold both.)
+  ProcessGroupNCCL and is not an ``auto`` candidate: a second RCCL communicator whose kernels
+  run while ProcessGroupNCCL's (DP buckets, CE statistics) are in flight can deadlock when the
+  GPU cannot hold both at once, and RCCL refuses two ranks on one device, so it cannot be
+  timed on a one-GPU rehearsal either; it stays an explicit opt-in.)
 
 Only the TP group's activation / activation-gradient collectives go through here; DP gradient
 buckets, the CE statistics gather and init broadcasts stay on ProcessGroupNCCL.
@@ -43,6 +48,15 @@ from . import process_manager as pm
 
 _OPS = ("all_reduce", "reduce_scatter", "all_gather")
 _GRIDS = (8, 16, 32, 64)
+# (class, upper bound in bytes, representative size timed for it)
+SIZE_CLASSES = (("s", 1 << 20, 512 << 10), ("m", 16 << 20, 8 << 20), ("l", None, 32 << 20))
+
+
+def size_class(nbytes: int) -> str:
+    for name, hi, _ in SIZE_CLASSES:
+        if hi is None or nbytes <= hi:
+            return name
+    return SIZE_CLASSES[-1][0]
 _decisions: Dict[int, Optional["_Choice"]] = {}   # id(tp_group) -> per-op transport (None = RCCL)
 _info: Dict[int, dict] = {}
 
@@ -74,16 +88,30 @@ def _time_ms(fn, cuda: bool = True, reps: int = 5) -> float:
 
 
 class _Choice:
-    """The group's communicators and which transport each op uses ("rccl" = ProcessGroupNCCL)."""
+    """The group's communicators and the transport of each (op, size class): "rccl" =
+    ProcessGroupNCCL, "xgmi" = the two-shot kernels, "xgmi1" = the one-shot all-reduce,
+    "native", "relay"; ``blocks`` = the xGMI grid of each (op, class)."""
 
-    def __init__(self, xgmi, native, use: Dict[str, str]):
+    def __init__(self, xgmi, native, use: Dict[tuple, str], blocks: Optional[Dict[tuple, int]] = None):
         self.xgmi, self.native, self.use = xgmi, native, use
+        self.blocks = blocks or {}
 
     relay = None
 
-    def comm(self, op: str):
-        u = self.use[op]
-        return {"xgmi": self.xgmi, "native": self.native, "relay": self.relay}.get(u)
+    def route(self, op: str, nbytes: int):
+        """(communicator, call kwargs) for a message of ``nbytes``, or None = ProcessGroupNCCL."""
+        key = (op, size_class(nbytes))
+        u = self.use[key]
+        if u in ("xgmi", "xgmi1"):
+            nb = self.blocks.get(key)
+            if nb is not None and nb != self.xgmi._blocks:   # same call sequence on every rank
+                self.xgmi.set_blocks(nb)
+            return self.xgmi, ({"one_shot": True} if u == "xgmi1" else {})
+        c = {"native": self.native, "relay": self.relay}.get(u)
+        return None if c is None else (c, {})
+
+    def uses(self, op: str, transport: str) -> bool:
+        return any(v == transport for (o, _), v in self.use.items() if o == op)
 
 
 def _run_op(comm, op: str, x, part, gathered, timeout_s=None):
@@ -242,54 +270,111 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
     dist.all_reduce(bad, op=dist.ReduceOp.MAX, group=red_group)
     if m != "auto" and bad.sum().item() > 0:
         raise RuntimeError(f"DPFS_TP_COMM={m}: collectives failed validation (max errors {errs[m]})")
-    # Timing (ProcessGroupNCCL backend only).  xGMI workgroups per call (1024 threads each):
-    # every CU that holds one cannot also hold a 2-wave-per-SIMD GEMM block, so per op take
-    # the narrowest grid within 10 % of the fastest one measured in isolation.
+    # One-shot all-reduce (xGMI): bit-identical to the two-shot form (same fp32 rank-order
+    # sums), checked on a message that fits its capacity.
+    one_shot = "xgmi" in comms and not bad[kl.index("xgmi"), 0]
+    if one_shot:
+        c = comms["xgmi"]
+        n1 = max(8 * W, min(n, c.one_shot_cap // x.element_size()) // (8 * W) * (8 * W))
+        y1, y2 = x[:n1].clone(), x[:n1].clone()
+        _run_op(c, "all_reduce", y1, None, None, 30.0)
+        c.all_reduce(y2, async_op=False, timeout_s=30.0, one_shot=True)
+        _sync(t.is_cuda)
+        ok1 = torch.tensor([1.0 if (torch.equal(y1, y2) and c.error() == 0) else 0.0], device=t.device)
+        dist.all_reduce(ok1, op=dist.ReduceOp.MIN, group=red_group)
+        one_shot = ok1.item() == 1.0
+    # Timing (ProcessGroupNCCL backend only), per op and size class at one representative
+    # size per class.  xGMI workgroups per call (1024 threads each): every CU that holds one
+    # cannot also hold a 2-wave-per-SIMD GEMM block, so per (op, class) take the narrowest grid
+    # within 10 % of the fastest one measured in isolation.
     G = len(_GRIDS)
-    cols = ["rccl"] + [k for k in kl if k != "xgmi"] + ([f"xgmi/{nb}" for nb in _GRIDS] if "xgmi" in comms else [])
-    times = torch.zeros(3, len(cols), device=t.device)
+    xg = "xgmi" in comms
+    cols = ["rccl"] + [k for k in kl if k != "xgmi"] + ([f"xgmi/{nb}" for nb in _GRIDS] if xg else []) \
+        + ([f"xgmi1/{nb}" for nb in _GRIDS] if one_shot else [])
+    NC = len(SIZE_CLASSES)
+    times = torch.full((3, NC, len(cols)), float("inf"), device=t.device)
     timed = m == "auto" and (backend == "nccl" or any_be)
+    cap_el = comms["xgmi"]._max_elems(t) if xg else None
+    sizes = []
+    for ci, (cname, hi, rep) in enumerate(SIZE_CLASSES):
+        ne = max(8 * W, rep // t.element_size())
+        if cap_el is not None:
+            ne = min(ne, cap_el)
+        ne -= ne % (8 * W)
+        sizes.append(ne)
+    if relay_cand:   # one size per class for the WORLD (relayed exchanges pair every rank)
+        st_ = torch.tensor(sizes, dtype=torch.int64, device=t.device if backend == "nccl" else "cpu")
+        dist.all_reduce(st_, op=dist.ReduceOp.MIN)
+        sizes = [int(v) for v in st_.tolist()]
     if timed:
-        a_, ap, ag = t.detach().reshape(-1)[:n].clone(), torch.empty_like(mine), torch.empty_like(x)
-        for i, op in enumerate(_OPS):
-            for j, col in enumerate(cols):
-                kind = col.split("/")[0]
-                if kind != "rccl" and bad[kl.index(kind), i] > 0:
-                    continue
-                if col == "rccl":
-                    c = (None, g)
-                else:
-                    c = comms[kind]
-                    if kind == "xgmi":
-                        c.set_blocks(int(col.split("/")[1]))
-                times[i, j] = _time_ms(lambda c=c, op=op: _run_op(c, op, a_, ap, ag), t.is_cuda)
-        if "xgmi" in comms:
+        for ci in range(NC):
+            ne = sizes[ci]
+            gen2 = torch.Generator(device=t.device).manual_seed(99 + r)
+            a_ = torch.randn(ne, generator=gen2, device=t.device).to(t.dtype)
+            ap, ag = torch.empty(ne // W, dtype=t.dtype, device=t.device), torch.empty_like(a_)
+            for i, op in enumerate(_OPS):
+                for j, col in enumerate(cols):
+                    kind = col.split("/")[0]
+                    base = "xgmi" if kind == "xgmi1" else kind
+                    if kind != "rccl" and bad[kl.index(base), i] > 0:
+                        continue
+                    if kind == "xgmi1" and (op != "all_reduce" or ne * t.element_size() > comms["xgmi"].one_shot_cap):
+                        continue
+                    if col == "rccl":
+                        fn = (lambda op=op: _run_op((None, g), op, a_, ap, ag))
+                    elif kind in ("xgmi", "xgmi1"):
+                        c = comms["xgmi"]
+
+                        def fn(c=c, op=op, nb=int(col.split("/")[1]), one=kind == "xgmi1"):
+                            c.set_blocks(nb)
+                            if one:
+                                c.all_reduce(a_, async_op=False, one_shot=True)
+                            else:
+                                _run_op(c, op, a_, ap, ag)
+                    else:
+                        fn = (lambda c=comms[kind], op=op: _run_op(c, op, a_, ap, ag))
+                    times[i, ci, j] = _time_ms(fn, t.is_cuda)
+        if xg:
             comms["xgmi"].check()
     dist.all_reduce(times, op=dist.ReduceOp.MAX, group=red_group)
-    use, info = {}, dict(bytes=n * x.element_size())
+    use, blocks, info = {}, {}, dict(bytes=n * x.element_size(),
+                                     class_bytes={c[0]: sizes[i] * x.element_size() for i, c in enumerate(SIZE_CLASSES)})
     for i, op in enumerate(_OPS):
-        row = times[i].tolist()
+        info[op] = {}
         ok = {k: bad[a, i].item() == 0 for a, k in enumerate(kl)}
-        cand = {"rccl": row[0]}
-        for k in ("native", "relay"):
-            if k in comms and ok[k]:
-                cand[k] = row[cols.index(k)]
-        if "xgmi" in comms:
-            xt = row[len(cols) - G:]
-            jx = min(j for j, tt in enumerate(xt) if tt <= 1.1 * min(xt)) if timed else _GRIDS.index(32)
-            comms["xgmi"].op_blocks[op] = _GRIDS[jx]
-            if ok["xgmi"]:
-                cand["xgmi"] = xt[jx]
-        if m != "auto":
-            choice = m
-        else:
-            fastest = min(cand, key=cand.get)
-            choice = fastest if fastest != "rccl" and cand[fastest] < 0.97 * cand["rccl"] else "rccl"
-        use[op] = choice
-        info[op] = dict(transport=choice, **{f"{k}_ms": round(v, 3) for k, v in cand.items()})
-        if "xgmi" in comms:
-            info[op]["xgmi_blocks"] = comms["xgmi"].op_blocks[op]
-    info["transport"] = "/".join(f"{op}:{use[op]}" for op in _OPS)
+        for ci, (cname, _, _) in enumerate(SIZE_CLASSES):
+            row = times[i, ci].tolist()
+            cand = {"rccl": row[0]}
+            for k in ("native", "relay"):
+                if k in comms and ok[k]:
+                    cand[k] = row[cols.index(k)]
+            grid = {}
+            for kind in ("xgmi", "xgmi1"):
+                js = [j for j, c_ in enumerate(cols) if c_.split("/")[0] == kind]
+                if not js or not ok.get("xgmi", False):
+                    continue
+                xt = [row[j] for j in js]
+                if min(xt) == float("inf"):
+                    continue
+                jx = min(j for j, tt in enumerate(xt) if tt <= 1.1 * min(xt)) if timed else _GRIDS.index(32)
+                grid[kind] = _GRIDS[jx]
+                cand[kind] = xt[jx]
+            if m == "auto":
+                fastest = min(cand, key=cand.get)
+                choice = fastest if fastest != "rccl" and cand[fastest] < 0.97 * cand["rccl"] else "rccl"
+            else:
+                choice = m if m != "xgmi" or "xgmi" in grid or not timed else m
+            use[(op, cname)] = choice
+            if choice in grid:
+                blocks[(op, cname)] = grid[choice]
+            elif choice == "xgmi":
+                blocks[(op, cname)] = grid.get("xgmi", 32)
+            info[op][cname] = dict(transport=choice, **{f"{k}_ms": round(v, 3) for k, v in cand.items()
+                                                         if v != float("inf")})
+            if (op, cname) in blocks:
+                info[op][cname]["xgmi_blocks"] = blocks[(op, cname)]
+    info["transport"] = "/".join(f"{op}:" + ",".join(f"{c[0]}={use[(op, c[0])]}" for c in SIZE_CLASSES)
+                                 for op in _OPS)
     _info[id(g)] = info
     if p.global_rank == 0 and os.environ.get("DPFS_QUIET", "0") != "1":
         print(f"[dpfs] TP collectives: {info}", file=sys.stderr, flush=True)
@@ -297,12 +382,13 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
         if "xgmi" in comms:      # same decision on every rank of g: release the IPC buffers
             comms["xgmi"].close()
         return None
-    ch = _Choice(comms.get("xgmi"), comms.get("native"), use)
+    ch = _Choice(comms.get("xgmi"), comms.get("native"), use, blocks)
     ch.relay = comms.get("relay")
     return ch
 
 
-def _comm(t: torch.Tensor, p, op: str):
+def _comm(t: torch.Tensor, p, op: str, nbytes: Optional[int] = None):
+    """(communicator, kwargs) for this op and message size, or None (ProcessGroupNCCL)."""
     if t.dtype not in (torch.bfloat16, torch.float32):
         return None
     if not t.is_cuda and not (mode() == "relay" or (mode() == "auto" and _auto_any_backend())):
@@ -311,21 +397,22 @@ def _comm(t: torch.Tensor, p, op: str):
     if key not in _decisions:
         _decisions[key] = _decide(t, p)
     ch = _decisions[key]
-    return None if ch is None else ch.comm(op)
+    return None if ch is None else ch.route(op, t.numel() * t.element_size() if nbytes is None else nbytes)
 
 
 def decision() -> Optional[dict]:
-    """This rank's transport per op and the xGMI grid per op (None before the first TP
+    """This rank's transport and xGMI grid per op and size class (None before the first TP
     collective or off TP): what every rank of a group must agree on."""
     p = pm.pgm
     if p is None or id(p.tp_group) not in _decisions:
         return None
+    keys = [f"{op}/{c[0]}" for op in _OPS for c in SIZE_CLASSES]
     inf = _info.get(id(p.tp_group))
     if inf is None:              # no candidate transport was built: the process group
-        return {"use": {op: "rccl" for op in _OPS}, "op_blocks": None}
-    blocks = {op: inf[op].get("xgmi_blocks") for op in _OPS}
-    return {"use": {op: inf[op]["transport"] for op in _OPS},
-            "op_blocks": blocks if any(v is not None for v in blocks.values()) else None}
+        return {"use": {k: "rccl" for k in keys}, "op_blocks": None}
+    use = {f"{op}/{c}": inf[op][c]["transport"] for op in _OPS for c, _, _ in SIZE_CLASSES}
+    blocks = {f"{op}/{c}": inf[op][c].get("xgmi_blocks") for op in _OPS for c, _, _ in SIZE_CLASSES}
+    return {"use": use, "op_blocks": blocks if any(v is not None for v in blocks.values()) else None}
 
 
 def reset():
@@ -340,6 +427,8 @@ def reset():
                 ch.native.close()
         _decisions.pop(key, None)
         _info.pop(key, None)
+    from . import grad_sync
+    grad_sync.reset()      # cached DP bucket sizes are keyed by the (replaced) process groups
 
 
 def info() -> Optional[dict]:
@@ -359,10 +448,11 @@ def all_reduce(t: torch.Tensor, async_op: bool = True):
     p = pm.pgm
     if p is None or p.tp_size == 1:
         return None
-    c = _comm(t, p, "all_reduce")
-    if c is None:
+    r = _comm(t, p, "all_reduce")
+    if r is None:
         return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=p.tp_group, async_op=async_op)
-    return c.all_reduce(t, async_op=async_op)
+    c, kw = r
+    return c.all_reduce(t, async_op=async_op, **kw)
 
 
 def reduce_scatter(out: torch.Tensor, inp: torch.Tensor, async_op: bool = True):
@@ -371,10 +461,10 @@ def reduce_scatter(out: torch.Tensor, inp: torch.Tensor, async_op: bool = True):
     if p is None or p.tp_size == 1:
         out.copy_(inp.view_as(out))
         return None
-    c = _comm(inp, p, "reduce_scatter")
-    if c is None or not _fits(c, inp, 8 * p.tp_size):
+    r = _comm(inp, p, "reduce_scatter")
+    if r is None or not _fits(r[0], inp, 8 * p.tp_size):
         return _pg_reduce_scatter(out, inp, p.tp_group, async_op)
-    return c.reduce_scatter(out, inp, async_op=async_op)
+    return r[0].reduce_scatter(out, inp, async_op=async_op)
 
 
 def all_gather(out: torch.Tensor, inp: torch.Tensor, async_op: bool = True):
@@ -383,10 +473,10 @@ def all_gather(out: torch.Tensor, inp: torch.Tensor, async_op: bool = True):
     if p is None or p.tp_size == 1:
         out.copy_(inp.view_as(out))
         return None
-    c = _comm(inp, p, "all_gather")
-    if c is None or not _fits(c, inp, 8):
+    r = _comm(inp, p, "all_gather", out.numel() * out.element_size())   # class of the gathered size
+    if r is None or not _fits(r[0], inp, 8):
         return _pg_all_gather(out, inp, p.tp_group, async_op)
-    return c.all_gather(out, inp, async_op=async_op)
+    return r[0].all_gather(out, inp, async_op=async_op)
 
 
 def staging(slot: int, shape, dtype: torch.dtype, op: str = "all_reduce") -> Optional[torch.Tensor]:
@@ -396,10 +486,18 @@ def staging(slot: int, shape, dtype: torch.dtype, op: str = "all_reduce") -> Opt
     does not fit.  Use one slot per in-flight chunk; a slot may be rewritten once the
     collective that read it has been waited."""
     p = pm.pgm
-    if p is None or p.tp_size == 1 or os.environ.get("DPFS_XGMI_STAGING", "1") == "0":
+    if p is None or p.tp_size == 1:
         return None
     ch = _decisions.get(id(p.tp_group))
-    if ch is None or ch.use[op] != "xgmi":
+    if ch is None:
+        return None
+    numel = 1
+    for d_ in shape:
+        numel *= d_
+    nbytes = numel * torch.empty((), dtype=dtype).element_size()
+    # staged only where this size runs on the two-shot kernels (the one-shot form reads its
+    # input after barriers the staging slot's reuse does not wait for)
+    if ch.use.get((op, size_class(nbytes))) != "xgmi":
         return None
     return ch.xgmi.staging(slot, shape, dtype)
 

@@ -26,8 +26,8 @@ import torch.distributed as dist
 
 from ..ops import _ext
 
-_ALL_REDUCE, _REDUCE_SCATTER, _ALL_GATHER = 0, 1, 2
-_NAMES = ("all_reduce", "reduce_scatter", "all_gather")
+_ALL_REDUCE, _REDUCE_SCATTER, _ALL_GATHER, _ALL_REDUCE_1 = 0, 1, 2, 3
+_NAMES = ("all_reduce", "reduce_scatter", "all_gather", "all_reduce")
 
 
 class _Work:
@@ -60,7 +60,7 @@ class XgmiComm:
         cap = cap_bytes or int(os.environ.get("DPFS_XGMI_CAP_MB", "256")) * (1 << 20)
         self.cap = cap
         self.timeout_s = timeout_s
-        self.nslots = int(os.environ.get("DPFS_XGMI_SLOTS", "4")) if nslots is None else nslots
+        self.nslots = 4 if nslots is None else nslots
         self.h, handle = C.xgmi_create(self.rank, self.world, cap, self.nslots)
         handles: List[Optional[bytes]] = [None] * self.world
         dist.all_gather_object(handles, handle, group=group)
@@ -77,6 +77,7 @@ class XgmiComm:
         # Staging slots: producer GEMMs write their output straight into one (``staging``), so
         # the reduce-scatter / all-reduce of it skips the copy-in.
         self._slots = [C.xgmi_slot_tensor(self.h, i, cap, dev) for i in range(self.nslots)]
+        self.one_shot_cap = int(C.xgmi_one_shot_capacity(self.h))
         dist.barrier(group=group)
 
     # ------------------------------------------------------------------------ core ----
@@ -122,10 +123,25 @@ class XgmiComm:
         per = self.cap // t.element_size()
         return (per // (self.world * vec)) * (self.world * vec)
 
-    def all_reduce(self, t: torch.Tensor, async_op: bool = True, timeout_s: Optional[float] = None):
+    def one_shot_ok(self, t: torch.Tensor) -> bool:
+        """Whether ``t`` can take the one-shot all-reduce (unstaged, within its capacity)."""
+        nb = t.numel() * t.element_size()
+        return 0 < nb <= self.one_shot_cap and nb % 16 == 0 and self._slot_of(t) < 0
+
+    def all_reduce(self, t: torch.Tensor, async_op: bool = True, timeout_s: Optional[float] = None,
+                   one_shot: bool = False):
         """In-place SUM over the group (bf16/fp32, fp32 accumulation in rank order, so every
-        rank receives bitwise-identical values)."""
+        rank receives bitwise-identical values).  ``one_shot``: every rank reads every peer's
+        whole message after ONE barrier (small messages; the same values as the two-shot form);
+        falls back to two-shot where it does not apply."""
         assert t.is_contiguous()
+        if one_shot and self.one_shot_ok(t):
+            flat = t.view(-1)
+            work = self._launch(_ALL_REDUCE_1, flat, flat, timeout_s)
+            if not async_op:
+                work.wait()
+                return None
+            return work
         slot = self._slot_of(t)
         if slot >= 0:                      # produced in a staging slot: no copy-in
             work = self._launch(_ALL_REDUCE, t.view(-1), t.view(-1), timeout_s, slot)

@@ -33,6 +33,7 @@ from .models import Transformer, get_preset
 from .ops.optim import FusedAdam
 from .parallel import process_manager as pm
 from .utils import checkpoint as ck
+from .utils import memory as MEM
 from .utils.dist import destroy_dist_env, init_dist_env, set_seed, free_port
 from .utils.fault import Heartbeat, maybe_inject_fault
 from .utils.tb import SummaryWriter
@@ -54,7 +55,9 @@ def get_train_args(argv=None) -> Namespace:
     g.add_argument("--tp_size", type=int, default=2)
     g.add_argument("--dp_size", type=int, default=1)
     g.add_argument("--sp", action="store_true", help="Megatron sequence parallelism")
-    g.add_argument("--recompute", action="store_true", help="activation recompute (layer inputs only)")
+    g.add_argument("--recompute", nargs="?", const="on", default="auto", choices=["auto", "on", "off"],
+                   help="activation recompute (layer inputs only); auto = the HBM planner's choice "
+                        "(utils/memory.py: on only when the layout does not fit without it)")
     g.add_argument("--master_addr", type=str, default="127.0.0.1")
     g.add_argument("--master_port", type=str, default="25555")
     g = p.add_argument_group("training")
@@ -106,8 +109,17 @@ def train(rank, args: Namespace):
     log0 = (lambda *a_: print(*a_, flush=True)) if grank == 0 else (lambda *a_: None)
     log0(f"{'Enable' if compute_dtype == torch.bfloat16 else 'Disable'} bf16 training  [{p}]")
 
-    margs = replace(get_preset(args.model), sequence_parallel=args.sp,
-                    recompute=getattr(args, "recompute", False), fp8=getattr(args, "fp8", False))
+    margs = replace(get_preset(args.model), sequence_parallel=args.sp, fp8=getattr(args, "fp8", False))
+    seq_len = args.seq_len or margs.maxlen
+    # HBM plan before the model exists (utils/memory.py): recompute on only where the layout
+    # does not fit without it; a layout that does not fit at all is refused with the numbers.
+    rc = getattr(args, "recompute", "auto")
+    rc = {"auto": None, "on": True, "off": False}.get(rc, rc if isinstance(rc, bool) else None)
+    lay = MEM.Layout(tp=p.tp_size, dp=p.dp_size, sp=args.sp, seq=seq_len, batch=args.batch_size,
+                     chunks=2 if p.tp_size > 1 else 1)
+    rc, est = MEM.plan(margs, lay, MEM.device_free_bytes(dev) if use_cuda else None, rc)
+    margs = replace(margs, recompute=bool(rc))
+    log0(f"HBM plan: peak {est.gb():.2f} GiB per rank estimated ({est.phase}), recompute={'on' if rc else 'off'}")
     model = Transformer.from_args(margs).to(dev)
     model.set_compute_dtype(compute_dtype)
     if margs.fp8 and not (model.fused_supported() and use_cuda):
@@ -121,7 +133,6 @@ def train(rank, args: Namespace):
     log0(model)
     log0(f"Number of parameters: {nparam / 1e6:.4f} million (global)")
 
-    seq_len = args.seq_len or margs.maxlen
     if args.synthetic:
         from .parallel import tp_comm
         tp_comm.set_fixed_shapes(True)   # every rank's batches have the same shape
@@ -175,8 +186,10 @@ def train(rank, args: Namespace):
     dist.barrier()
     done = False
     for epoch in range(start_epoch, max_epoch):
-        hb.beat(n, force=True)     # the loader restart at an epoch boundary is not a stall
-        for batch in loader:
+        it = iter(loader)
+        with hb.hold(n):           # the loader restart at an epoch boundary is not a stall
+            batch = next(it, None)
+        while batch is not None:
             ids = batch["input_ids"].to(dev, non_blocking=True)
             tgt = batch["target_ids"].to(dev, non_blocking=True)
             pos = batch["position_ids"].to(dev, non_blocking=True)
@@ -219,6 +232,7 @@ def train(rank, args: Namespace):
             if n >= args.max_steps:
                 done = True
                 break
+            batch = next(it, None)
         log0(f"Epoch {epoch + 1}/{max_epoch} finished.")
         if done:
             break

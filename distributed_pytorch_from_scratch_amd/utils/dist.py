@@ -87,8 +87,7 @@ def init_dist_env(args: Optional[Namespace] = None, rank: Optional[int] = None, 
         # RCCL collectives on a high-priority HIP stream: they overlap the other ping-pong
         # chunk's compute and are on its critical path.
         opts = dist.ProcessGroupNCCL.Options()
-        opts.is_high_priority_stream = True
-        opts._timeout = datetime.timedelta(seconds=timeout_s)   # the same limit as the kwarg below
+        opts.is_high_priority_stream = True     # (the timeout is the init_process_group kwarg)
         kw["pg_options"] = opts
     elif os.environ.get("DPFS_BACKEND") == "gloo" and torch.cuda.is_available():
         torch.cuda.set_device(local_rank % torch.cuda.device_count())

@@ -32,8 +32,10 @@ def maybe_inject_fault(fault_step: int, step: int, rank: int, target_rank: int =
 
 
 class Heartbeat:
-    def __init__(self, interval_s: float = 30.0, stale_s: float = 600.0, abort_on_stale: bool = False):
+    def __init__(self, interval_s: float = 30.0, stale_s: float = 600.0, abort_on_stale: bool = False,
+                 max_hold_s: float = 3600.0):
         self.interval_s, self.stale_s, self.abort = interval_s, stale_s, abort_on_stale
+        self.max_hold_s = max_hold_s
         self.store = None
         self._last = 0.0
         self._stop = threading.Event()
@@ -65,12 +67,13 @@ class Heartbeat:
     def hold(self, step: int):
         """A phase that legitimately runs longer than ``stale_s`` without steps (checkpoint
         save and the barrier behind it, evaluation, an epoch-boundary loader restart): this
-        rank is not judged stale inside it (the process-group watchdog still bounds a hung
-        collective), and it beats on entry and exit."""
+        rank is not judged stale inside it until ``max_hold_s`` has passed (the marker carries
+        that deadline, so a rank killed inside a hold -- no exit beat -- is flagged once it
+        expires), and it beats on entry and exit."""
         self.beat(step, force=True)
         if self.store is not None:
             try:
-                self.store.set(f"dpfs_hb/{self.rank}", f"{step}:hold")
+                self.store.set(f"dpfs_hb/{self.rank}", f"{step}:hold:{time.time() + self.max_hold_s}")
             except Exception:
                 pass
         try:
@@ -85,10 +88,12 @@ class Heartbeat:
                 try:
                     if not self.store.check([f"dpfs_hb/{r}"]):
                         continue
-                    _, ts = self.store.get(f"dpfs_hb/{r}").decode().split(":")
-                    if ts == "hold":
+                    parts = self.store.get(f"dpfs_hb/{r}").decode().split(":")
+                    if len(parts) == 3 and parts[1] == "hold":   # step:hold:deadline
+                        if now > float(parts[2]):
+                            stale.append(r)
                         continue
-                    if now - float(ts) > self.stale_s:
+                    if now - float(parts[1]) > self.stale_s:
                         stale.append(r)
                 except Exception:
                     continue

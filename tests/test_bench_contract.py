@@ -101,10 +101,11 @@ def test_bench_pure_tp_failure_keeps_headline(inject):
     assert ("injected" in d["tp_pure"]["error"]) if inject.startswith("raise") else ("timeout" in d["tp_pure"]["error"])
 
 
-def test_bench_headline_failure_falls_back_to_dp():
+def test_bench_headline_failure_is_not_a_result():
     """An exception in the TP x DP headline layout on every rank: the bench measures pure data
-    parallelism instead and prints exactly one JSON line for it, with the failure reported
-    under headline_error (parallelism dp4, no pure-TP extra), exit status 0."""
+    parallelism for the record, but prints value = null for the requested layout (the DP
+    numbers under "fallback", the failure under headline_error, no pure-TP extra) and exits
+    non-zero, so a driver reading only value and the exit status cannot take it for a result."""
     from dist_helpers import _free_port
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
@@ -112,9 +113,10 @@ def test_bench_headline_failure_falls_back_to_dp():
            "--batch-per-gpu", "2"]
     env = dict(_env(), DPFS_BENCH_INJECT="raise_head")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert r.returncode != 0, r.stdout[-2000:] + r.stderr[-2000:]
     (d,) = _json_lines(r.stdout)
-    assert d["config"]["parallelism"] == "tp1dp4" and d["value"] > 0
+    assert d["value"] is None and d["ms_per_step"] is None and d["config"]["parallelism"] == "tp2dp2"
+    assert d["fallback"]["parallelism"] == "tp1dp4" and d["fallback"]["value"] > 0
     assert d["headline_error"]["parallelism"] == "tp2dp2" and "injected" in d["headline_error"]["error"]
     assert d.get("tp_pure") is None
 

@@ -296,3 +296,24 @@ def test_heartbeat_hold_is_not_stale(tmp_path):
     r = _run([str(script), _port(), ROOT], timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "stale ranks" not in (r.stdout + r.stderr)
+
+
+_HB_DEAD_IN_HOLD_SCRIPT = _HB_SCRIPT.replace(
+    "hb = Heartbeat(interval_s=0.3, stale_s=2.0, abort_on_stale=True)",
+    "hb = Heartbeat(interval_s=0.3, stale_s=2.0, abort_on_stale=True, max_hold_s=3.0)").replace(
+    "        time.sleep(30)          # hung rank: no more heartbeats",
+    "        with hb.hold(1):        # killed inside a checkpoint save: the exit beat never comes\n"
+    "            time.sleep(30)")
+
+
+def test_heartbeat_expired_hold_is_stale(tmp_path):
+    """A rank that dies (or hangs) inside ``Heartbeat.hold`` leaves its hold marker behind: once
+    the marker's deadline (``max_hold_s``) passes, the watcher flags it like any stale rank."""
+    import time
+    script = tmp_path / "hb_dead_hold.py"
+    script.write_text(_HB_DEAD_IN_HOLD_SCRIPT)
+    t0 = time.time()
+    r = _run([str(script), _port(), ROOT], timeout=120)
+    assert r.returncode != 0, r.stdout + r.stderr
+    assert "stale ranks" in (r.stdout + r.stderr)
+    assert time.time() - t0 < 25

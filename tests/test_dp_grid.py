@@ -43,6 +43,12 @@ def _step(rank, world, tp, sp, fused):
     per = B // p.dp_size
     sl = slice(p.dp_rank * per, (p.dp_rank + 1) * per)
     loss = step(ids[sl], pos[sl], tgt[sl])
+    if fused:
+        # pack-free DP: every gradient is a view of the model's gradient arena, which the DP
+        # all-reduce ran on in place (parallel/grad_sync.GradArena / DPBucketer)
+        buf = m._dpfs_grad_arena.buf
+        lo, hi = buf.data_ptr(), buf.data_ptr() + 4 * buf.numel()
+        assert all(lo <= q.grad.data_ptr() < hi for q in m.parameters())
     # grads in the reference layout: write them into the params, export, restore
     with torch.no_grad():
         saved = [q.detach().clone() for q in m.parameters()]

@@ -187,13 +187,11 @@ def test_swiglu_epilogue_layout_matches(world, sp, recompute, monkeypatch):
     """The layout of the fused gate|up + SwiGLU GEMM epilogue (ops.reference.gu_perm: weight
     rows, bias and gate|up activations interleaved in 64-blocks; the weight gradient
     un-interleaved once per layer and step), run through the CPU oracle with
-    DPFS_SWIGLU_EPILOGUE=1 in both engines (and the recompute path): the same loss trajectory
-    and parameters as the natural layout."""
+    ModelArgs.swiglu_epilogue=True in both engines (and the recompute path): the same loss
+    trajectory and parameters as the natural layout."""
     cfg = dict(CFG, recompute=recompute)
-    monkeypatch.setenv("DPFS_SWIGLU_EPILOGUE", "0")
-    base = run_distributed(_train_parallel, world, cfg, 3, sp, True, True)
-    monkeypatch.setenv("DPFS_SWIGLU_EPILOGUE", "1")
-    fused = run_distributed(_train_parallel, world, cfg, 3, sp, True, True)
+    base = run_distributed(_train_parallel, world, dict(cfg, swiglu_epilogue=False), 3, sp, True, True)
+    fused = run_distributed(_train_parallel, world, dict(cfg, swiglu_epilogue=True), 3, sp, True, True)
     for r in range(world):
         assert torch.allclose(torch.tensor(fused[r][0]), torch.tensor(base[r][0]), atol=1e-6), (fused[r][0], base[r][0])
         for key, v in base[r][1].items():

@@ -52,7 +52,7 @@ def test_relay_collectives_match_pairwise(world):
     res = run_distributed(_collectives, world, sizes, tp_size=2)
     for r, (err, transport) in res.items():
         assert err < 1e-5, (r, err)
-        assert transport == "all_reduce:relay/reduce_scatter:relay/all_gather:relay"
+        assert transport == "/".join(f"{op}:s=relay,m=relay,l=relay" for op in ("all_reduce", "reduce_scatter", "all_gather"))
 
 
 def _train(rank, world, transport, sp):

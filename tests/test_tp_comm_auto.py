@@ -7,9 +7,11 @@ the relay is a candidate), so that every rank takes the same transport for every
 that decided differently would issue a different collective sequence and hang its group, so
 this is what the first 8-GPU run depends on.  ``DPFS_TP_COMM_AUTO_ANY_BACKEND=1`` runs the
 same decision over gloo: on the CPU (relay candidate only) and, marked gpu, with several ranks
-sharing one MI355X (xGMI kernels + relay).  Each case checks: identical decisions (transport
-and xGMI grid per op) on every rank, the collectives' results against fp32 sums after the
-decision, and the decision record (``tp_comm.info``) the bench line reports.
+sharing one MI355X (xGMI kernels + relay).  The decision is per op AND per message-size class
+(``tp_comm.SIZE_CLASSES``: <= 1 MiB, <= 16 MiB, larger), so every case drives messages of all
+three classes through the collectives after the decision.  Each case checks: identical
+decisions (transport and xGMI grid per op and class) on every rank, the collectives' results
+against fp32 sums, and the decision record (``tp_comm.info``) the bench line reports.
 """
 import os
 
@@ -19,7 +21,7 @@ import torch
 from dist_helpers import run_distributed
 
 
-def _decide(rank, world, dev, n):
+def _decide(rank, world, dev, sizes):
     os.environ["DPFS_TP_COMM"] = "auto"
     os.environ["DPFS_TP_COMM_AUTO_ANY_BACKEND"] = "1"
     os.environ["DPFS_QUIET"] = "1"
@@ -31,7 +33,7 @@ def _decide(rank, world, dev, n):
     p = pm.get_pgm()
     W = p.tp_size
     errs = []
-    for i in range(2):                       # the first call decides, the second reuses it
+    for i, n in enumerate(sizes):            # the first call decides, the others reuse it
         g = torch.Generator().manual_seed(77 * i + rank)
         x = torch.randn(n, generator=g).to(torch.bfloat16 if dev == "cuda" else torch.float32).to(dev)
         ref = x.float().clone()
@@ -72,36 +74,50 @@ def _check_same(res, tp):
                                                             "transport"}
 
 
+# fp32 on the CPU: 16 KiB, 4 MiB, 20 MiB -> classes s, m, l (the first call decides)
+CPU_SIZES = [4096, 1 << 20, 5 << 20]
+
+
 @pytest.mark.parametrize("world", [4, 8])
 def test_auto_decision_relay_candidate_cpu(world):
     """tp2 x dp(world/2) on the CPU: the relay is the one candidate; its validation and timing
-    are reduced over the WORLD, so every pair takes the same decision."""
-    res = run_distributed(_decide, world, "cpu", 4096, tp_size=2)
+    are reduced over the WORLD, so every pair takes the same decision per size class."""
+    res = run_distributed(_decide, world, "cpu", CPU_SIZES, tp_size=2)
     _check_same(res, 2)
     for v in res.values():
-        assert "relay_ms" in v["info"]["all_reduce"] and "rccl_ms" in v["info"]["all_reduce"]
+        for c in ("s", "m", "l"):
+            assert "relay_ms" in v["info"]["all_reduce"][c] and "rccl_ms" in v["info"]["all_reduce"][c]
+        assert "s=" in v["info"]["transport"] and "l=" in v["info"]["transport"]
 
 
 def test_auto_decision_without_candidates_cpu():
     """Pure TP 4 on the CPU: no candidate transport, the process group carries everything."""
-    res = run_distributed(_decide, 4, "cpu", 4096, tp_size=4)
+    res = run_distributed(_decide, 4, "cpu", CPU_SIZES[:2], tp_size=4)
     for v in res.values():
-        assert v["dec"] == {"use": {"all_reduce": "rccl", "reduce_scatter": "rccl", "all_gather": "rccl"},
-                            "op_blocks": None}
+        assert set(v["dec"]["use"].values()) == {"rccl"} and len(v["dec"]["use"]) == 9
+        assert v["dec"]["op_blocks"] is None
         assert v["err"] < 1e-4
 
 
+def test_size_classes():
+    from distributed_pytorch_from_scratch_amd.parallel import tp_comm
+    assert [tp_comm.size_class(b) for b in (1, 1 << 20, (1 << 20) + 16, 16 << 20, (16 << 20) + 16)] == \
+        ["s", "s", "m", "m", "l"]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,tp", [(4, 2), (4, 4), (8, 8)])
+@pytest.mark.parametrize("world,tp", [(2, 2), (4, 2), (4, 4), (8, 8)])
 def test_auto_decision_on_one_gpu(world, tp):
-    """Several ranks on one MI355X over gloo: xGMI kernels at every grid width (and the relay
-    when tp = 2 with other pairs) are validated and timed; every rank must reach the same
-    transport and the same xGMI grid per op (8 ranks at tp 8 is the driver's pure-TP layout)."""
-    n = 8 * tp * 4096
-    res = run_distributed(_decide, world, "cuda", n, tp_size=tp)
+    """Several ranks on one MI355X over gloo: the xGMI kernels (two-shot at every grid width,
+    the one-shot all-reduce for the small / medium classes) and the relay (tp = 2 with other
+    pairs) are validated and timed per size class; every rank must reach the same transport and
+    xGMI grid per op and class (8 ranks at tp 8 is the driver's pure-TP layout)."""
+    sizes = [8 * tp * 4096, 2 << 20, 12 << 20]     # bf16: classes s, m, l
+    res = run_distributed(_decide, world, "cuda", sizes, tp_size=tp)
     _check_same(res, tp)
     for v in res.values():
-        assert v["dec"]["op_blocks"] is not None            # xGMI was built and timed
-        assert "xgmi_blocks" in v["info"]["all_reduce"]
-        if tp == 2:
-            assert "relay_ms" in v["info"]["all_reduce"]
+        ar = v["info"]["all_reduce"]
+        assert all("xgmi_ms" in ar[c] for c in ("s", "m", "l"))     # xGMI was built and timed
+        assert "xgmi1_ms" in ar["s"] and "xgmi1_ms" in ar["m"]      # one-shot for small / medium
+        if tp == 2 and world > 2:
+            assert "relay_ms" in ar["s"]

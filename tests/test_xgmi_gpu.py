@@ -35,12 +35,17 @@ def _collectives(rank, world, cases, cap_mb):
             comm.all_reduce(y, async_op=True).wait()
             y2 = x.clone()                      # back-to-back calls reuse the buffers
             comm.all_reduce(y2, async_op=False)
+            # one-shot (one barrier, every peer's whole message; two calls in a row alternate
+            # its input regions), falling back to two-shot past its capacity: same values
+            y3, y4 = x.clone(), x.clone()
+            comm.all_reduce(y3, async_op=True, one_shot=True).wait()
+            comm.all_reduce(y4, async_op=False, one_shot=True)
             st = comm.staging(i % comm.nslots, (n,), dtype)   # produced in a staging slot
             if st is not None:
                 st.copy_(x)
                 comm.all_reduce(st, async_op=False)
                 st = st.cpu()
-            res = (y.cpu(), y2.cpu()) + ((st,) if st is not None else ())
+            res = (y.cpu(), y2.cpu(), y3.cpu(), y4.cpu()) + ((st,) if st is not None else ())
         elif op == "rs":
             y = torch.empty(n // world, dtype=dtype, device="cuda")
             comm.reduce_scatter(y, x, async_op=False)
@@ -75,8 +80,9 @@ def test_xgmi_collectives_match_fp32_sums(world):
             if op == "ar":
                 for y in got:
                     assert torch.allclose(y.float(), total, atol=2e-2, rtol=1e-2), (op, n, r)
-                # fp32 sum in rank order, rounded once: identical on every rank
-                assert torch.equal(got[0], res[0][i][0]) and torch.equal(got[0], got[1])
+                # fp32 sum in rank order, rounded once: identical on every rank, and the one-shot
+                # form bit-identical to the two-shot one
+                assert torch.equal(got[0], res[0][i][0]) and all(torch.equal(got[0], y) for y in got[1:])
             elif op == "rs":
                 sl = total.view(world, -1)[r]
                 assert torch.allclose(got[0].float(), sl, atol=2e-2, rtol=1e-2), (op, n, r)

@@ -24,6 +24,8 @@ SHAPES = {
     "tn": [("qkv", 2304, 768, T), ("wo", 768, 768, T), ("gateup", 4096, 768, T), ("down", 768, 2048, T),
            ("lmhead", 50304, 768, T)],
 }
+# square shapes (--big): the main loop's rate where prologue / epilogue costs are amortised
+BIG = {l: [("sq4k", 4096, 4096, 4096), ("sq8k", 8192, 8192, 8192)] for l in ("nt", "nn", "tn")}
 # per-call kernel variant of the next `ours` call (0 = v4 at its own width, 1 / 2 = v4 256 / 192
 # wide, 3 = v3): an argument of the kernel entry points, set here per arm
 VAR = [0]
@@ -102,6 +104,9 @@ def main():
     ap.add_argument("--ablate", type=int, nargs="*", default=[],
                     help="extra v4 arms with timing-only ablations (bits: 1 no stores, 2 zero operands, 4 no DMA wait, 8 no step barrier)")
     ap.add_argument("--cold", action="store_true", help="flush the caches before every timed call")
+    ap.add_argument("--big", action="store_true", help="also the 4096^3 / 8192^3 square shapes")
+    ap.add_argument("--br", type=int, nargs="*", default=[],
+                    help="extra arms: the last --scheds variant with BR rows of MFMAs before each step's barrier")
     a = ap.parse_args()
     if a.cold:
         global timed
@@ -109,7 +114,7 @@ def main():
     C = _ext.require()
     gen = torch.Generator(device="cuda").manual_seed(0)
     for layout in a.layouts:
-        for name, M, N, K in SHAPES[layout]:
+        for name, M, N, K in SHAPES[layout] + (BIG[layout] if a.big else []):
             if a.shapes and name not in a.shapes:
                 continue
             _, _, ours, blas, ref = operands(layout, M, N, K, gen, a.bias)
@@ -162,7 +167,15 @@ def main():
                       f"-> per tile wait {v[:, 0].mean() / per:.0f} body {v[:, 1].mean() / per:.0f} "
                       f"epi {v[:, 2].mean() / per:.0f}; shares wait {(v[:, 0] / tot).mean():.3f} "
                       f"epi {(v[:, 2] / tot).mean():.3f}", flush=True)
-            arms = [f"v4s{sc}" for sc in a.scheds] + [f"gm{g}" for g in a.group_m] + [f"bn{b}" for b in a.bn] + [f"sp{x}" for x in a.splits] + \
+            for br in a.br:                   # correctness of the BR variants
+                if want is not None:
+                    set_variant(1)
+                    C.gemm4_sched(a.scheds[-1])
+                    C.gemm4_br(br)
+                    o = ours(C)
+                    C.gemm4_br(0)
+                    res[f"br{br}_bitwise_vs_default"] = float(torch.equal(o, ours(C)))
+            arms = [f"v4s{sc}" for sc in a.scheds] + [f"br{x}" for x in a.br] + [f"gm{g}" for g in a.group_m] + [f"bn{b}" for b in a.bn] + [f"sp{x}" for x in a.splits] + \
                 [f"abl{x}" for x in a.ablate] + ["v3"] + \
                 ([] if a.no_blas else ["blas"])
             ts = {k: [] for k in arms}
@@ -173,6 +186,12 @@ def main():
                         set_variant(1)
                         C.gemm4_sched(int(k[3:]))
                         ts[k].append(timed(lambda: ours(C), a.iters))
+                    elif k.startswith("br"):
+                        set_variant(1)
+                        C.gemm4_sched(a.scheds[-1])
+                        C.gemm4_br(int(k[2:]))
+                        ts[k].append(timed(lambda: ours(C), a.iters))
+                        C.gemm4_br(0)
                     elif k.startswith("sp"):
                         set_variant(1)
                         C.gemm4_sched(a.scheds[-1])
