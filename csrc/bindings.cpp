@@ -186,7 +186,8 @@ torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
                       c10::optional<torch::Tensor> rope_pos, c10::optional<torch::Tensor> rope_tab,
                       int64_t rope_heads, int64_t rope_hd, c10::optional<torch::Tensor> out, int64_t variant) {
   check_rowmajor(a, "a");
-  TORCH_CHECK(variant >= 0 && variant <= 3, "gemm: variant 0 (v4), 1 (v4 256-wide), 2 (v4 192-wide) or 3 (v3)");
+  TORCH_CHECK(variant >= 0 && variant <= 6, "gemm: variant 0 (v4), 1 (v4 256-wide), 2 (v4 192-wide), 3 (v3); "
+              "+4: v4 with non-temporal output stores");
   check_rowmajor(b, "b");
   TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "gemm_nt: bf16 operands");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
@@ -225,7 +226,8 @@ torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
 
 torch::Tensor gemm_nn(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> out, int64_t variant) {
   check_rowmajor(a, "a");
-  TORCH_CHECK(variant >= 0 && variant <= 3, "gemm: variant 0 (v4), 1 (v4 256-wide), 2 (v4 192-wide) or 3 (v3)");
+  TORCH_CHECK(variant >= 0 && variant <= 6, "gemm: variant 0 (v4), 1 (v4 256-wide), 2 (v4 192-wide), 3 (v3); "
+              "+4: v4 with non-temporal output stores");
   check_rowmajor(b, "b");
   TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "gemm_nn: bf16 operands");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(1);

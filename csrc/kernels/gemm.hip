@@ -918,10 +918,15 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
 // Per-call kernel variant (an argument of every GEMM entry point, never process state):
 //   0 = v4 with its per-shape tile width (the default for every layout),
 //   1 / 2 = v4 with the 256 / 192 tile width forced (non-split bf16 NT / NN),
-//   3 = the v3 kernel (8 waves, 128 x 64 per wave).
+//   3 = the v3 kernel (8 waves, 128 x 64 per wave);
+//   + 4 (variants 4 / 5 / 6): the v4 bf16 output written with non-temporal (streaming)
+//   stores, so the output does not displace the operands in L2 (plain NT / NN only).
 // Where the v4 launcher declines a shape (32-bit spans, alignment) the v3 kernel runs.
-static bool use_v4(int variant) { return g_gemm_impl >= 3 && variant != 3; }
-static int v4_bn(int variant) { return variant == 1 ? 256 : (variant == 2 ? 192 : 0); }
+static bool use_v4(int variant) { return g_gemm_impl >= 3 && (variant & 3) != 3; }
+static int v4_bn(int variant) {
+  const int w = variant & 3;
+  return (w == 1 ? 256 : (w == 2 ? 192 : 0)) | ((variant & 4) ? 0x100 : 0);
+}
 
 extern "C" long long dpfs_gemm_bf16_ws(int M, int N, int K) {
   const int S = bf16_splits(M, N, K);

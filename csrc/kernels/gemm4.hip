@@ -235,7 +235,7 @@ __device__ __forceinline__ int nsteps(const Item& it) {
 // cos / sin values are loaded one 16-row block ahead of their use.
 __device__ __forceinline__ float silu_ref(float g) { return g * __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
 
-template <int OUT, int BN, int ROPE, bool HAS_BIAS, bool SWIGLU = false>
+template <int OUT, int BN, int ROPE, bool HAS_BIAS, bool SWIGLU = false, int SA = 0>
 __device__ __forceinline__ void epilogue(const char* bias_lds, const Item& ci, void* C, const Rope& rope, int M,
                                          int N, int ldc, long long slab_stride, unsigned c_bytes, int wm, int wn,
                                          int l, const SwiOut& swo = SwiOut{}) {
@@ -336,7 +336,7 @@ __device__ __forceinline__ void epilogue(const char* bias_lds, const Item& ci, v
         const u32x4 w = {sx[0], sy[0], sx[1], sy[1]};
         const int n = wcol0 + 32 * jp + colg;
         const unsigned off = (mok && n < N) ? rbase + (unsigned)n * 2u : kOOB;
-        __builtin_amdgcn_raw_buffer_store_b128(w, rc, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(w, rc, off, 0, SA);
       }
     });
   } else {
@@ -543,7 +543,7 @@ __device__ __forceinline__ void epilogue_swb(const Item& ci, int M, int F, const
 // the pipe once per 32-deep step.  (Safe: the DMA a step issues writes the slot read two
 // steps earlier, retired before the previous step's barrier.)
 template <bool AK, bool BKM, int OUT, int DIAG = 0, bool FAST = false, int SCHED = 0, int BN = 256, int ROPE = 0,
-          bool SWIGLU = false, bool SWB = false, int BR = 0>
+          bool SWIGLU = false, bool SWB = false, int BR = 0, int SA = 0>
 __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                   void* __restrict__ C, const float* __restrict__ bias, int M, int N,
                                                   int K, int lda, int ldb, int ldc, int kps, int splits,
@@ -851,9 +851,9 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
     }
     if (OUT == 0 && bias) wait_vmcnt<NQ - PBB>();   // this wave's bias DMA landed (younger: the ring pieces after it)
     if (OUT == 0 && bias)
-      epilogue<OUT, BN, ROPE, true, SWIGLU>(bias_lds, ci, C, rope, M, N, ldc, slab_stride, c_bytes, wm, wn, l, swo);
+      epilogue<OUT, BN, ROPE, true, SWIGLU, SA>(bias_lds, ci, C, rope, M, N, ldc, slab_stride, c_bytes, wm, wn, l, swo);
     else
-      epilogue<OUT, BN, ROPE, false, SWIGLU>(bias_lds, ci, C, rope, M, N, ldc, slab_stride, c_bytes, wm, wn, l, swo);
+      epilogue<OUT, BN, ROPE, false, SWIGLU, SA>(bias_lds, ci, C, rope, M, N, ldc, slab_stride, c_bytes, wm, wn, l, swo);
     if constexpr (TIMED) {
       const unsigned long long t = stamp();
       t_epi += t - t_mark;
@@ -971,7 +971,10 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
                                   const float* rope_tab, int rope_cols, int rope_hd, const void* A2, const void* B2,
                                   int k_switch, int lda2, int ldb2, unsigned a2_bytes, unsigned b2_bytes,
                                   int bn_force, hipStream_t s) {
-  // bn_force: tile width of a non-split bf16 GEMM, 0 = chosen per shape, 256 / 192 forced
+  // bn_force: tile width of a non-split bf16 GEMM, 0 = chosen per shape, 256 / 192 forced;
+  // | 0x100: the bf16 output written with non-temporal stores (plain NT / NN)
+  const bool ntst = (bn_force & 0x100) != 0;
+  bn_force &= 0xff;
   if (M <= 0 || N <= 0 || (N % 8) || (K % 8)) return false;
   if (layout == 2 && (M % 8)) return false;
   if (rope_cols > 0 && rope_hd != 64 && rope_hd != 128) return false;
@@ -1027,7 +1030,12 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
         break;                                                                                    \
       }                                                                                           \
     }                                                                                             \
-    if (fast && sched == 1) {                                                                     \
+    if (fast && sched == 1 && OUT_ == 0 && ntst && rope_cols == 0) {                             \
+      if (bn == 192)                                                                              \
+        gemm4_k<AK_, BK_, OUT_, 0, true, 1, 192, 0, false, false, 0, 2><<<grid, 256, 0, s>>>(G4_ARGS); \
+      else                                                                                        \
+        gemm4_k<AK_, BK_, OUT_, 0, true, 1, 256, 0, false, false, 0, 2><<<grid, 256, 0, s>>>(G4_ARGS); \
+    } else if (fast && sched == 1) {                                                              \
       if (OUT_ == 0 && bn == 192) {                                                               \
         if (g_g4_br == 1)                                                                         \
           gemm4_k<AK_, BK_, OUT_, 0, true, 1, (OUT_ == 0 ? 192 : 256), 0, false, false, 1>         \
@@ -1066,6 +1074,13 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
     gemm4_k<true, true, 0, 3, true, 1><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda,
                                                             ldb, ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb,
                                                             rope, g_g4_group_m, dual, g_g4_ablate, nullptr);
+    return true;
+  }
+  if ((g_g4_ablate & 128) && layout == 0 && !out_f32 && bn == 256 && fast && rope_cols == 0) {
+    // A/B: the bf16 epilogue stores with the non-temporal hint (streaming output, aux nt)
+    gemm4_k<true, true, 0, 0, true, 1, 256, 0, false, false, 0, 2><<<grid, 256, 0, s>>>(
+        (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb,
+        rope, g_g4_group_m, dual, 0, nullptr);
     return true;
   }
   if ((g_g4_ablate & 16) && g_g4_diag && layout == 0 && !out_f32 && bn == 256 && fast) {

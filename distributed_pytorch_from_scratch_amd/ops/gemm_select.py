@@ -11,6 +11,9 @@ uses the fastest:
   shorter, e.g. the N = 768 projections);
 * ``ours256`` / ``ours192`` -- v4 with the tile width forced (kept only if it measures faster
   than the width the launcher's round model picked);
+* ``ours_nt`` / ``ours256_nt`` / ``ours192_nt`` -- the same with the bf16 output written by
+  non-temporal stores (the output streams past L2 instead of displacing the operands the next
+  tiles re-read; plain NT / NN outputs);
 * ``ours3``    -- the v3 kernel (8 waves, 128 x 64 per wave).
 
 hipBLASLt stays reachable for A/B runs and for operands our kernels do not take (a
@@ -107,7 +110,7 @@ def _lt_index(c: str) -> int:
 
 # Per-call kernel variant of our GEMM entry points (an argument, never process state):
 # 0 = v4 at its per-shape tile width, 1 / 2 = v4 with the 256 / 192 width forced, 3 = v3.
-_VARIANT = {"ours": 0, "ours256": 1, "ours192": 2, "ours3": 3}
+_VARIANT = {"ours": 0, "ours256": 1, "ours192": 2, "ours3": 3, "ours_nt": 4, "ours256_nt": 5, "ours192_nt": 6}
 
 
 def _ours_variants(call: Callable[[int], torch.Tensor], widths: bool = False) -> Dict[str, Callable]:
@@ -118,7 +121,8 @@ def _ours_variants(call: Callable[[int], torch.Tensor], widths: bool = False) ->
     longer a candidate; it remains the fallback for shapes the v4 launcher declines."""
     out = {"ours": lambda: call(0)}
     if widths:
-        out.update({"ours256": lambda: call(1), "ours192": lambda: call(2)})
+        out.update({"ours256": lambda: call(1), "ours192": lambda: call(2), "ours_nt": lambda: call(4),
+                    "ours256_nt": lambda: call(5), "ours192_nt": lambda: call(6)})
     return out
 
 

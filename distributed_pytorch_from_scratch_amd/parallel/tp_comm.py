@@ -334,8 +334,18 @@ def _decide(t: torch.Tensor, p) -> Optional[_Choice]:
                     else:
                         fn = (lambda c=comms[kind], op=op: _run_op(c, op, a_, ap, ag))
                     times[i, ci, j] = _time_ms(fn, t.is_cuda)
-        if xg:
-            comms["xgmi"].check()
+    # A barrier that timed out on ANY rank while timing (its flag is per rank) takes the xGMI
+    # kernels out of the running on every rank alike, so the group still decides the same.
+    xerr = torch.tensor([float(comms["xgmi"].error()) if xg else 0.0], device=t.device)
+    dist.all_reduce(xerr, op=dist.ReduceOp.MAX, group=red_group)
+    if xerr.item() > 0:
+        comms["xgmi"].clear_error()
+        for j, c_ in enumerate(cols):
+            if c_.startswith("xgmi"):
+                times[:, :, j] = float("inf")
+        if p.global_rank == 0:
+            print("[dpfs] TP collectives: an xGMI barrier timed out while timing; xGMI is not used",
+                  file=sys.stderr, flush=True)
     dist.all_reduce(times, op=dist.ReduceOp.MAX, group=red_group)
     use, blocks, info = {}, {}, dict(bytes=n * x.element_size(),
                                      class_bytes={c[0]: sizes[i] * x.element_size() for i, c in enumerate(SIZE_CLASSES)})

@@ -192,6 +192,9 @@ class XgmiComm:
         """Non-zero once any barrier of any call timed out (host-mapped word, no sync)."""
         return int(self.C.xgmi_error(self.h))
 
+    def clear_error(self):
+        self.C.xgmi_clear_error(self.h)
+
     def check(self):
         if self.error():
             raise RuntimeError(f"xGMI collective timed out on TP rank {self.rank} (a peer never arrived)")

@@ -33,6 +33,16 @@ def _decide(rank, world, dev, sizes):
     p = pm.get_pgm()
     W = p.tp_size
     errs = []
+    trace = []
+    if dev == "cuda":    # per-rank record of every xGMI launch (op, elements, grid) for diagnosis
+        from distributed_pytorch_from_scratch_amd.parallel import xgmi as X
+        orig = X.XgmiComm._launch
+
+        def traced(self, op, x, out, timeout_s=None, slot=-1):
+            trace.append((op, x.numel(), self._blocks if self.op_blocks[X._NAMES[op]] is None
+                          else self.op_blocks[X._NAMES[op]]))
+            return orig(self, op, x, out, timeout_s, slot)
+        X.XgmiComm._launch = traced
     for i, n in enumerate(sizes):            # the first call decides, the others reuse it
         g = torch.Generator().manual_seed(77 * i + rank)
         x = torch.randn(n, generator=g).to(torch.bfloat16 if dev == "cuda" else torch.float32).to(dev)
@@ -54,15 +64,27 @@ def _decide(rank, world, dev, sizes):
             torch.cuda.synchronize()
         errs += [(part.float() - ref.view(W, -1)[p.tp_rank]).abs().max().item(),
                  (full.float() - ref).abs().max().item(), (y.float() - ref).abs().max().item()]
-    tp_comm.check()
+    ch = tp_comm._decisions.get(id(p.tp_group))
+    xerr = ch.xgmi.error() if ch is not None and ch.xgmi is not None else 0
+    anyerr = torch.tensor([float(xerr)])
+    dist.all_reduce(anyerr, op=dist.ReduceOp.MAX)
     info = tp_comm.info()
     dec = tp_comm.decision()
-    tp_comm.reset()
+    if anyerr.item() == 0:
+        tp_comm.reset()
     return dict(err=max(errs), scale=ref.abs().max().item(), dec=dec, info=info, tp_rank=p.tp_rank,
-                dp_rank=p.dp_rank)
+                dp_rank=p.dp_rank, xerr=xerr, trace=trace)
 
 
 def _check_same(res, tp):
+    traces = {r: v["trace"] for r, v in res.items()}
+    if any(v["xerr"] for v in res.values()):     # name the first launch where the ranks diverge
+        t0 = traces[0]
+        div = [(r, next((i for i, (a, b) in enumerate(zip(t0, t)) if a != b), None), len(t))
+               for r, t in traces.items()]
+        raise AssertionError(f"xGMI timeout on ranks {[r for r, v in res.items() if v['xerr']]}; "
+                             f"launches per rank / first divergence from rank 0: {div}; "
+                             f"rank 0 tail {t0[-6:]}")
     decs = {r: v["dec"] for r, v in res.items()}
     first = next(iter(decs.values()))
     assert first is not None

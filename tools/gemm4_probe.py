@@ -138,6 +138,14 @@ def main():
                     o2 = ours(C)
                     C.gemm4_ablate(0)
                     res[f"abl{x}_bitwise_vs_default"] = float(torch.equal(o2, ours(C)))
+            for br in a.br:                   # the BR variants: bit-identical to BR 0
+                if want is not None:
+                    set_variant(1)
+                    C.gemm4_sched(a.scheds[-1])
+                    C.gemm4_br(br)
+                    o = ours(C)
+                    C.gemm4_br(0)
+                    res[f"br{br}_bitwise_vs_default"] = float(torch.equal(o, ours(C)))
             set_variant(1)
             del want
             flops = 2.0 * M * N * K
@@ -145,13 +153,20 @@ def main():
                   flush=True)
             if a.check_only:
                 continue
-            for dmode in ((16, 32) if a.diag and layout == "nt" else ()):
+            for dmode in ((16, 17, 32) if a.diag and layout == "nt" else ()):
                 d = torch.zeros(256 * 4 * 4, dtype=torch.int64, device="cuda")
                 C.gemm4_diag(d)
                 set_variant(1)
                 C.gemm4_ablate(dmode)
                 ours(C)
                 torch.cuda.synchronize()
+                d.zero_()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                ours(C)
+                e1.record()
+                e1.synchronize()
+                wall_ms = e0.elapsed_time(e1)
                 C.gemm4_ablate(0)
                 C.gemm4_diag(torch.empty(0))
                 v = d.view(-1, 4).double()
@@ -162,19 +177,13 @@ def main():
                 tiles = ((M + 255) // 256) * ((N + 255) // 256)
                 per = tiles / (v.shape[0] / 4)
                 tot = v[:, :3].sum(1)
-                print(f"{layout} {name} DIAG{'' if dmode == 16 else '(no DMA issued)'} per wave (s_memtime ticks, mean over {v.shape[0]} waves, {per:.1f} tiles "
+                clk = (v[:, :3].sum(1).max().item()) / (wall_ms * 1e-3) / 1e9   # longest wave's cycles / wall
+                tagd = {16: "", 17: "(no stores)", 32: "(no DMA issued)"}[dmode]
+                print(f"{layout} {name} DIAG{tagd} wall {wall_ms:.4f} ms, clock >= {clk:.2f} GHz; per wave (s_memtime ticks, mean over {v.shape[0]} waves, {per:.1f} tiles "
                       f"per WG): wait {v[:, 0].mean():.0f}  body {v[:, 1].mean():.0f}  epilogue {v[:, 2].mean():.0f}  "
                       f"-> per tile wait {v[:, 0].mean() / per:.0f} body {v[:, 1].mean() / per:.0f} "
                       f"epi {v[:, 2].mean() / per:.0f}; shares wait {(v[:, 0] / tot).mean():.3f} "
                       f"epi {(v[:, 2] / tot).mean():.3f}", flush=True)
-            for br in a.br:                   # correctness of the BR variants
-                if want is not None:
-                    set_variant(1)
-                    C.gemm4_sched(a.scheds[-1])
-                    C.gemm4_br(br)
-                    o = ours(C)
-                    C.gemm4_br(0)
-                    res[f"br{br}_bitwise_vs_default"] = float(torch.equal(o, ours(C)))
             arms = [f"v4s{sc}" for sc in a.scheds] + [f"br{x}" for x in a.br] + [f"gm{g}" for g in a.group_m] + [f"bn{b}" for b in a.bn] + [f"sp{x}" for x in a.splits] + \
                 [f"abl{x}" for x in a.ablate] + ["v3"] + \
                 ([] if a.no_blas else ["blas"])
