@@ -24,6 +24,7 @@ void dpfs_gemm_nt_rope(const void*, const void*, void*, const float*, int, int, 
                        const float*, int, int, int, hipStream_t);
 void dpfs_gemm4_sched(int);
 void dpfs_gemm4_br(int);
+void dpfs_gemm4_m32(int);
 void dpfs_gemm4_group_m(int);
 void dpfs_gemm4_ablate(int);
 void dpfs_gemm4_diag(void*);
@@ -65,6 +66,9 @@ void dpfs_bias_grad(int, const void*, float*, float*, int, int, hipStream_t);
 void dpfs_embedding_fwd(int, const int64_t*, const float*, void*, int, int, long long, int, hipStream_t);
 void dpfs_embedding_bwd(int, const void*, const int64_t*, float*, int, int, long long, int, hipStream_t);
 void dpfs_ce_stats(int, const void*, const int64_t*, float*, int, int, long long, int, hipStream_t);
+long long dpfs_ce_fused_ws(int, int);
+int dpfs_ce_fused(int, void*, const int64_t*, const float*, float*, float*, float*, int, int, long long, int,
+                  hipStream_t);
 void dpfs_ce_bwd(int, const void*, const int64_t*, const float*, const float*, void*, int, int, long long, int,
                  hipStream_t);
 int dpfs_adam_chunk();
@@ -728,6 +732,33 @@ torch::Tensor ce_fwd_stats(torch::Tensor logits, torch::Tensor targets, int64_t 
   return stats;
 }
 
+// Single-shard CE forward + backward in one pass (TP 1): returns the ce_fwd_stats rows and
+// overwrites logits with (softmax - onehot) * gscale[row] (+ the bias gradient into dbias);
+// None (nothing launched) where the one-pass kernel does not apply.
+c10::optional<torch::Tensor> ce_fused(torch::Tensor logits, torch::Tensor targets, torch::Tensor gscale,
+                                      int64_t vocab_start, int64_t vocab_valid, c10::optional<torch::Tensor> dbias) {
+  check_rowmajor(logits, "logits");
+  TORCH_CHECK(logits.is_contiguous(), "ce_fused: logits contiguous");
+  const int64_t M = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(targets.scalar_type() == torch::kInt64 && targets.is_contiguous() && targets.numel() == M,
+              "ce_fused: targets int64 [M]");
+  TORCH_CHECK(gscale.scalar_type() == torch::kFloat32 && gscale.is_contiguous() && gscale.numel() == M,
+              "ce_fused: gscale fp32 [M]");
+  TORCH_CHECK(vocab_valid >= 0 && vocab_valid <= V, "ce_fused: vocab_valid out of range");
+  TORCH_CHECK(M < (1ll << 31) / 3, "ce_fused: too many rows");
+  const at::DeviceGuard g(logits.device());
+  float* db = dbias_out(dbias, V, "ce_fused");
+  auto stats = torch::empty({M, 3}, logits.options().dtype(torch::kFloat32));
+  torch::Tensor ws;
+  if (db) ws = torch::empty({std::max<long long>(dpfs_ce_fused_ws((int)M, (int)V), 1)}, stats.options());
+  if (db && M == 0) dbias->zero_();
+  const int ok = dpfs_ce_fused(dcode(logits), logits.data_ptr(), targets.data_ptr<int64_t>(), gscale.data_ptr<float>(),
+                               stats.data_ptr<float>(), db, db ? ws.data_ptr<float>() : nullptr, (int)M, (int)V,
+                               vocab_start, (int)vocab_valid, stream());
+  if (!ok) return c10::nullopt;
+  return stats;
+}
+
 torch::Tensor ce_bwd(torch::Tensor logits, torch::Tensor targets, torch::Tensor lse, torch::Tensor gscale,
                      int64_t vocab_start, int64_t vocab_valid, torch::Tensor out,
                      c10::optional<torch::Tensor> dbias) {
@@ -1180,6 +1211,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "int64 buffer of the DIAG builds (attn_fwd / attn_bwd impl 5): per-wave s_memtime splits");
   m.def("gemm4_diag", [](torch::Tensor t) { dpfs_gemm4_diag(t.defined() && t.numel() ? t.data_ptr() : nullptr); },
         "int64 buffer [grid*4*4] for the DIAG build's per-wave cycle split (gemm4_ablate bit 16)");
+  m.def("gemm4_m32", [](int v) { dpfs_gemm4_m32(v); },
+        "TN main loop of the v4 GEMM: 1 = 32x32x16 MFMAs (default), 0 = 16x16x32 (A/B probes)");
   m.def("gemm4_br", [](int v) { dpfs_gemm4_br(v); },
         "rows of MFMAs before each step's barrier in the plain v4 kernels (0, 1, 2; A/B runs)");
   m.def("gemm4_sched", [](int v) { dpfs_gemm4_sched(v); },
@@ -1227,6 +1260,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embedding_bwd", &embedding_bwd, py::arg("dout"), py::arg("ids"), py::arg("v_local"), py::arg("vocab_start"),
         py::arg("out") = py::none());
   m.def("ce_fwd_stats", &ce_fwd_stats);
+  m.def("ce_fused", &ce_fused, py::arg("logits"), py::arg("targets"), py::arg("gscale"), py::arg("vocab_start"),
+        py::arg("vocab_valid"), py::arg("dbias") = py::none());
   m.def("ce_bwd", &ce_bwd, py::arg("logits"), py::arg("targets"), py::arg("lse"), py::arg("gscale"),
         py::arg("vocab_start"), py::arg("vocab_valid"), py::arg("out"), py::arg("dbias") = py::none());
   m.def("adam_build", &adam_build);

@@ -223,6 +223,181 @@ __global__ __launch_bounds__(256) void ce_bwd_colsum_k(const T* logits, const in
   }
 }
 
+// Single-shard CE forward + backward in ONE pass over the logits (TP 1: the row's lse is
+// local, so d logits can be written during the forward; reference train.py:101-104 computes
+// the loss on gathered logits and backward re-reads them).  The two-pass form (ce_stats_k,
+// then ce_bwd_colsum_k in backward) reads the 3.3 GB of GPT-2-small logits twice and writes
+// them once; this one reads once and writes once:
+//   * one 512-thread workgroup per CU (2 waves per SIMD: 256 registers for the row's NV
+//     vectors and their 8 NV fp32 column sums) walks rows r = blockIdx.x + k * gridDim.x;
+//   * a row (V bf16, V % 8 == 0, V <= 8 * 512 * NV) arrives in LDS by LDS-DMA, lane-linear:
+//     vector c = 512 i + t lands at byte 16 c, written AND later read by thread t only, so no
+//     barrier guards the staging; thread t moves its NV vectors into registers, then issues the
+//     DMA of its slots of the NEXT row (same bytes: its own reads retired first), which lands
+//     while this row is reduced, differentiated and stored;
+//   * one exponential per element: e = exp(x - m_i) against its 16-byte vector's max m_i,
+//     summed in fp32 and kept as fp16 pairs in place of the bf16 input (e <= 1); after the
+//     block reduction (per thread -> wave xor butterfly -> 8 waves through LDS, double-
+//     buffered by row parity: one barrier per row) p = e * exp(m_i - lse) * gscale[row]
+//     (- gscale at the target), in place as bf16, 0 past vvalid;
+//   * the row's stores are buffer stores issued by every lane (out-of-range lanes past the
+//     descriptor), NV per wave, so the next row's entry wait leaves exactly them in flight
+//     (vmcnt(NV): the next row's DMA, issued before them, has landed);
+//   * the lm_head bias gradient: each thread sums its fixed columns over its rows in fp32;
+//     one partial row per workgroup (part[blockIdx.x][V]), reduced by colsum_rows.
+// stats[row] = {max, sum exp(x - max), target logit or 0} as ce_stats_k.
+template <int NV>
+__global__ __launch_bounds__(512) void ce_fused_k(bf16* logits, const int64_t* __restrict__ tgt,
+                                                   const float* __restrict__ gscale, float* __restrict__ stats,
+                                                   float* __restrict__ part, int M, int V, long long vstart,
+                                                   int vvalid) {
+  __shared__ __attribute__((aligned(1024))) char row_lds[NV * 8192];
+  __shared__ MaxSum red[2][8];
+  constexpr float L2E = 1.4426950408889634f;
+  const int t = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int nvec = V >> 3;
+  const unsigned row_bytes = (unsigned)V * 2u;
+  float acc[NV][8];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[i][e] = 0.f;
+  auto rsrc = [&](int row) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(logits + (long long)row * V), (short)0, (int)row_bytes,
+                                             0x00020000);
+  };
+  // byte offset of slot i's vector in a row (past the descriptor for the last slot's spare lanes)
+  auto voff = [&](int i) -> unsigned {
+    const int c = 512 * i + t;
+    return (i < NV - 1 || c < nvec) ? (unsigned)c * 16u : kOOB;
+  };
+  auto issue = [&](int row) {
+    const __amdgpu_buffer_rsrc_t r = rsrc(row);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) dma16(r, row_lds + i * 8192 + wave * 1024, voff(i));
+  };
+  // bf16 -> fp32 of slot i, -inf past vvalid (by opaque shifts / masks: hipcc would otherwise
+  // keep fp32 copies or hoist per-element masks out of the row loop, both spilling)
+  auto elems = [&](const u32x4& w, int i, float (&x)[8]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      unsigned lo, hi;
+      asm volatile("v_lshlrev_b32 %0, 16, %2\n\tv_and_b32 %1, 0xffff0000, %2" : "=&v"(lo), "=&v"(hi) : "v"(w[h]));
+      x[2 * h] = __builtin_bit_cast(float, lo);
+      x[2 * h + 1] = __builtin_bit_cast(float, hi);
+    }
+    if (8 * 512 * (i + 1) > vvalid) {
+      int nv;   // valid elements of this vector (<= 0: none)
+      asm volatile("v_sub_u32 %0, %1, %2" : "=v"(nv) : "s"(vvalid), "v"(8 * (512 * i + t)));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = e < nv ? x[e] : -INFINITY;
+    }
+  };
+  int row = blockIdx.x;
+  if (row < M) issue(row);
+  for (int it = 0; row < M; row += gridDim.x, ++it) {
+    if (it == 0) wait_vmcnt<0>();
+    else wait_vmcnt<NV>();   // this row's DMA landed; the previous row's NV stores may be in flight
+    u32x4 cur[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) cur[i] = *reinterpret_cast<const u32x4*>(row_lds + (512 * i + t) * 16);
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this thread's LDS reads retired
+    const int nrow = row + gridDim.x;
+    if (nrow < M) issue(nrow);
+    KASSERT(tgt[row] >= -1, "target %lld at row %d (ignore_index is -1)", (long long)tgt[row], row);
+    const long long loc64 = tgt[row] - vstart;
+    const int loc = (loc64 >= 0 && loc64 < vvalid) ? (int)loc64 : -1;   // target column in this shard
+    // per slot: its max m_i, e = exp(x - m_i) as fp16 pairs in place (e <= 1), the slot's sum
+    // merged into the thread's (max, sum)
+    float mi[NV];
+    MaxSum ms = {-INFINITY, 0.f};
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      float x[8];
+      elems(cur[i], i, x);
+      const int d = loc - 8 * (512 * i + t);
+      if ((unsigned)d < 8u) {
+        float tl = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) tl = e == d ? x[e] : tl;
+        stats[row * 3 + 2] = tl;
+      }
+      float m = x[0];
+#pragma unroll
+      for (int e = 1; e < 8; ++e) m = fmaxf(m, x[e]);
+      mi[i] = m;
+      const float ms_ = m == -INFINITY ? 0.f : m * L2E;
+      float sm = 0.f;
+      u32x4 ev;
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const float e0 = __builtin_amdgcn_exp2f(x[2 * h] * L2E - ms_);
+        const float e1 = __builtin_amdgcn_exp2f(x[2 * h + 1] * L2E - ms_);
+        sm += e0 + e1;
+        // (packed by opaque asm: hipcc would otherwise keep each fp16 in a register of its own)
+        unsigned pk, tmp;
+        asm volatile("v_cvt_f16_f32 %0, %2\n\tv_cvt_f16_f32 %1, %3\n\tv_pack_b32_f16 %0, %0, %1"
+                     : "=&v"(pk), "=&v"(tmp) : "v"(e0), "v"(e1));
+        ev[h] = pk;
+      }
+      cur[i] = ev;
+      if (m != -INFINITY) ms = merge(ms, {m, sm});
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ms = merge(ms, {__shfl_xor(ms.m, o, 64), __shfl_xor(ms.s, o, 64)});
+    if ((t & 63) == 0) red[it & 1][wave] = ms;
+    __syncthreads();
+    MaxSum r = red[it & 1][0];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) r = merge(r, red[it & 1][w]);
+    if (t == 0) {
+      stats[row * 3 + 0] = r.m;
+      stats[row * 3 + 1] = r.s;
+      if (loc < 0) stats[row * 3 + 2] = 0.f;
+    }
+    // p = e * exp(m_i - lse) * g  (g = 0 on ignored rows; a slot with no valid column has e = 0)
+    const float g = gscale[row];
+    const float lse2 = r.m * L2E + __log2f(r.s);
+    const __amdgpu_buffer_rsrc_t ro = rsrc(row);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const float sc = mi[i] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mi[i] * L2E - lse2) * g;
+      float p[8];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        float lo, hi;
+        asm volatile("v_cvt_f32_f16 %0, %2\n\tv_lshrrev_b32 %1, 16, %2\n\tv_cvt_f32_f16 %1, %1"
+                     : "=&v"(lo), "=&v"(hi) : "v"(cur[i][h]));
+        p[2 * h] = lo * sc;
+        p[2 * h + 1] = hi * sc;
+      }
+      const int d = loc - 8 * (512 * i + t);
+      if ((unsigned)d < 8u) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) p[e] = e == d ? p[e] - g : p[e];
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        acc[i][e] += p[e];
+        o[e] = (bf16)p[e];
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro, voff(i), 0, 0);
+    }
+  }
+  if (part != nullptr) {
+    float* pr = part + (long long)blockIdx.x * V;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = 512 * i + t;
+      if (i == NV - 1 && c >= nvec) continue;
+      *reinterpret_cast<f32x4*>(pr + 8 * c) = (f32x4){acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
+      *reinterpret_cast<f32x4*>(pr + 8 * c + 4) = (f32x4){acc[i][4], acc[i][5], acc[i][6], acc[i][7]};
+    }
+  }
+}
+
 static inline int cap_grid2(long long work, int block) {
   long long g = (work + block - 1) / block;
   if (g > 2048) g = 2048;
@@ -290,6 +465,50 @@ extern "C" void dpfs_embedding_bwd(int in_dtype, const void* dout, const int64_t
     embedding_bwd_k<bf16><<<grid, 256, 0, s>>>((const bf16*)dout, ids, dw, M, D, vstart, vlocal);
   else
     embedding_bwd_k<float><<<grid, 256, 0, s>>>((const float*)dout, ids, dw, M, D, vstart, vlocal);
+}
+
+// ce_fused_k launcher: 1 = launched; 0 = not applicable (not bf16, V % 8, V > 8 * 512 * 13:
+// the caller takes the two-pass path).  part: ce_fused_ws floats when dbias is wanted, else null.
+static int ce_fused_grid(int M) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, c = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+    cus = c;
+  }
+  return M < cus ? M : cus;
+}
+
+extern "C" long long dpfs_ce_fused_ws(int M, int V) { return (long long)ce_fused_grid(M) * V; }
+
+extern "C" int dpfs_ce_fused(int dtype, void* logits, const int64_t* tgt, const float* gscale, float* stats,
+                             float* dbias, float* part, int M, int V, long long vstart, int vvalid, hipStream_t s) {
+  if (dtype != kBF16 || V % 8 != 0 || V <= 0) return 0;
+  const int nv = (V / 8 + 511) / 512;
+  if (nv > 13) return 0;   // (V <= 53248: past 13 slots the registers spill)
+  if (M == 0) return 1;
+  const int G = ce_fused_grid(M);
+  float* pp = dbias ? part : nullptr;
+#define CEF(N_) ce_fused_k<N_><<<G, 512, 0, s>>>((bf16*)logits, tgt, gscale, stats, pp, M, V, vstart, vvalid)
+  switch (nv) {
+    case 1: CEF(1); break;
+    case 2: CEF(2); break;
+    case 3: CEF(3); break;
+    case 4: CEF(4); break;
+    case 5: CEF(5); break;
+    case 6: CEF(6); break;
+    case 7: CEF(7); break;
+    case 8: CEF(8); break;
+    case 9: CEF(9); break;
+    case 10: CEF(10); break;
+    case 11: CEF(11); break;
+    case 12: CEF(12); break;
+    default: CEF(13); break;
+  }
+#undef CEF
+  if (dbias) dpfs_colsum_rows_small(part, dbias, G, V, s);
+  return 1;
 }
 
 extern "C" void dpfs_ce_stats(int dtype, const void* logits, const int64_t* tgt, float* stats, int M, int V,

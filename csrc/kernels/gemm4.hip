@@ -169,18 +169,78 @@ struct Opnd<false, BN> {
   }
 };
 
-template <bool AK, bool BKM, int BN>
+// 32x32x16 operand of an MN-major image (the M32 main loop): fragment f = 2 nb + kk covers the
+// wave's 32-column block nb (of 4) and k-half kk: lane l holds X[k = 16 kk + 8 (l >> 5) + j]
+// [col 32 nb + (l & 31)], j < 8, from two ds_read_b64_tr_b16 (rows k, k + 4 of its 16-lane
+// group's 4 x 16 block: group g takes columns 16 (g & 1) .. + 15 and k half g >> 1).  The
+// image's 16-byte chunk c of k row r sits at c ^ ((r & 3) << 2): the four rows of a 32-lane
+// half's two blocks (64 contiguous bytes each) land on four disjoint 4-chunk bank groups.
+__device__ __forceinline__ int m32_swz(int k) { return (k & 3) << 2; }
+// transposed read at a compile-time byte offset from p (the ds instruction's offset field)
+template <int OFF>
+__device__ __forceinline__ s16x4 ds_tr16_at(const char* p) {
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2"
+               : "=v"(r)
+               : "v"((unsigned)(size_t)((__attribute__((address_space(3))) const char*)p)), "n"(OFF));
+  return r;
+}
+// Lane offset of fragment block nb (k-half 0, rows k, the lo read) in a half-slot: the other
+// three reads of the block are +2048 (rows k + 4), +8192 (k-half 1) and +10240, so a step
+// needs one address add per block (the swizzle depends on k & 3 only).
+__device__ __forceinline__ unsigned m32_off(int cb, int nb, int l) {
+  const int ii = l & 15, q = ii >> 2, p = ii & 3, g = l >> 4;
+  const int col = cb + 32 * nb + 16 * (g & 1) + 4 * p;
+  const int k = 8 * (g >> 1) + q;
+  return (unsigned)(k * 512 + (((col >> 3) ^ m32_swz(k)) << 4) + (p & 1) * 8);
+}
+struct Opnd32 {
+  s16x4 lo[8], hi[8];
+  // fragments 2 nb (k-half 0) and 2 nb + 1 (k-half 1) from base = half-slot + m32_off(nb)
+  __device__ __forceinline__ void load_nb(int nb, const char* base) {
+    lo[2 * nb] = ds_tr16_at<0>(base);
+    hi[2 * nb] = ds_tr16_at<2048>(base);
+    lo[2 * nb + 1] = ds_tr16_at<8192>(base);
+    hi[2 * nb + 1] = ds_tr16_at<10240>(base);
+  }
+  __device__ __forceinline__ bf16x8 get(int f) const {
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    s16x8 v = {lo[f][0], lo[f][1], lo[f][2], lo[f][3], hi[f][0], hi[f][1], hi[f][2], hi[f][3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+  __device__ __forceinline__ void pin() {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]), "+v"(lo[3]), "+v"(lo[4]), "+v"(lo[5]), "+v"(lo[6]),
+                   "+v"(lo[7]));
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(hi[0]), "+v"(hi[1]), "+v"(hi[2]), "+v"(hi[3]), "+v"(hi[4]), "+v"(hi[5]), "+v"(hi[6]),
+                   "+v"(hi[7]));
+  }
+};
+
+template <bool AK, bool BKM, int BN, bool M32 = false>
 struct Frags {
   Opnd<AK> a;
   Opnd<BKM, BN> b;
 };
+template <int BN>
+struct Frags<false, false, BN, true> {
+  Opnd32 a, b;
+};
 
-template <bool AK, bool BKM, int BN>
-__device__ __forceinline__ void read_frags(Frags<AK, BKM, BN>& f, const char* slot, int wm, int wn, int l) {
+template <bool AK, bool BKM, int BN, bool M32 = false>
+__device__ __forceinline__ void read_frags(Frags<AK, BKM, BN, M32>& f, const char* slot, int wm, int wn, int l) {
+  if constexpr (M32) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) f.a.load(i, slot, wm * 128 + 16 * i, l);
+    for (int nb = 0; nb < 4; ++nb) f.a.load_nb(nb, slot + m32_off(wm * 128, nb, l));
 #pragma unroll
-  for (int j = 0; j < BN / 32; ++j) f.b.load(j, slot + 16384, wn * (BN / 2) + 16 * j, l);
+    for (int nb = 0; nb < 4; ++nb) f.b.load_nb(nb, slot + 16384 + m32_off(wn * 128, nb, l));
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f.a.load(i, slot, wm * 128 + 16 * i, l);
+#pragma unroll
+    for (int j = 0; j < BN / 32; ++j) f.b.load(j, slot + 16384, wn * (BN / 2) + 16 * j, l);
+  }
 }
 
 // Work item -> tile origin and K range (grouped order as gemm.hip's gemmp_k).
@@ -234,6 +294,33 @@ __device__ __forceinline__ int nsteps(const Item& it) {
 // fits the descriptor, so row * ldc cannot overflow), and the RoPE rows' positions and
 // cos / sin values are loaded one 16-row block ahead of their use.
 __device__ __forceinline__ float silu_ref(float g) { return g * __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
+
+// fp32 epilogue of the 32x32x16 accumulators (M32): lane l holds row l & 31 of each 32 x 32
+// block, columns 8 G + 4 (l >> 5) + 0..3 in registers 4G..4G+3: one 16-byte store each, 64 per
+// wave (as the 16x16 form's OUT 1).
+__device__ __forceinline__ void epilogue_f32_m32(const Item& ci, void* C, int M, int N, int ldc,
+                                                 long long slab_stride, unsigned c_bytes, int wm, int wn, int l) {
+  acc_drain();
+  char* cbase = reinterpret_cast<char*>(C) + (long long)ci.split * slab_stride * 4;
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)cbase, (short)0, (int)c_bytes, 0x00020000);
+  const int row0 = ci.m0 + wm * 128 + (l & 31);
+  const int col0 = ci.n0 + wn * 128 + 4 * (l >> 5);
+  static_for<0, 4>([&](auto I) {
+    constexpr int bi = decltype(I)::value;
+    const int m = row0 + 32 * bi;
+    const bool mok = m < M;
+    const unsigned rbase = (unsigned)(mok ? m : 0) * (unsigned)ldc * 4u;
+    static_for<0, 4>([&](auto J) {
+      constexpr int bj = decltype(J)::value;
+      static_for<0, 4>([&](auto G) {
+        constexpr int gg = decltype(G)::value;
+        const int n = col0 + 32 * bj + 8 * gg;
+        const unsigned off = (mok && n < N) ? rbase + (unsigned)n * 4u : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc32_read<bi, bj, gg>()), rc, off, 0, 0);
+      });
+    });
+  });
+}
 
 template <int OUT, int BN, int ROPE, bool HAS_BIAS, bool SWIGLU = false, int SA = 0>
 __device__ __forceinline__ void epilogue(const char* bias_lds, const Item& ci, void* C, const Rope& rope, int M,
@@ -542,8 +629,13 @@ __device__ __forceinline__ void epilogue_swb(const Item& ci, int M, int F, const
 // (rows BR .. BR + 3), so the barrier / wait time overlaps matrix work instead of draining
 // the pipe once per 32-deep step.  (Safe: the DMA a step issues writes the slot read two
 // steps earlier, retired before the previous step's barrier.)
+// M32: the 32x32x16 MFMA main loop (TN only: both operands MN-major, fp32 out, 256-wide):
+// 32 MFMAs of 32 cycles per 32-deep step instead of 64 of 16 -- half the MFMA issue slots and
+// half the operand-register reads per FLOP, so the step's 32 transposed reads, 8 DMA pieces and
+// address / SALU work fit in the MFMA shadow (the 16x16x32 TN step issues ~1.5k cycles of
+// non-MFMA work against 1024 of matrix time).
 template <bool AK, bool BKM, int OUT, int DIAG = 0, bool FAST = false, int SCHED = 0, int BN = 256, int ROPE = 0,
-          bool SWIGLU = false, bool SWB = false, int BR = 0, int SA = 0>
+          bool SWIGLU = false, bool SWB = false, int BR = 0, int SA = 0, bool M32 = false>
 __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                   void* __restrict__ C, const float* __restrict__ bias, int M, int N,
                                                   int K, int lda, int ldb, int ldc, int kps, int splits,
@@ -562,6 +654,8 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   static_assert(!SWB || (OUT == 0 && BN == 256 && ROPE == 0 && !SWIGLU), "SwiGLU-backward epilogue: bf16 256-wide tiles");
   static_assert(BN == 256 || BN == 192, "tile width");
   static_assert(BR >= 0 && BR <= 4 && (BR == 0 || DIAG == 0), "barrier row");
+  static_assert(!M32 || (!AK && !BKM && OUT == 1 && BN == 256 && BR == 0 && SCHED == 1 && ROPE == 0),
+                "32x32x16 main loop: TN fp32, 256-wide");
   // ring pieces issued before the step's barrier (their count joins the wait, and the bias
   // DMA issued after the barrier has NQ - PBB younger ring pieces)
   constexpr int PBB = SCHED == 1 ? (BR < NQ ? BR : NQ) : 0;
@@ -617,7 +711,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
       } else if (isA || BN == 256) {
         const int lin = j * 64 + l;
         const int row = lin >> 5;
-        const int c = (lin & 31) ^ (mnh(row) << 1);
+        const int c = (lin & 31) ^ (M32 ? m32_swz(row) : (mnh(row) << 1));
         pbase[q] = (unsigned)(((long long)row * ld + r0 + 8 * c) * 2);
       } else {
         const int lin = j * 64 + l;
@@ -717,8 +811,17 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
     advance();
   }
 
-  Frags<AK, BKM, BN> F0, F1;
+  Frags<AK, BKM, BN, M32> F0, F1;
   int c_slot = 0;
+  // M32: per-lane offsets of the 4 fragment blocks of each operand in a slot (B: + 16384)
+  unsigned m32a[4] = {0, 0, 0, 0}, m32b[4] = {0, 0, 0, 0};
+  if constexpr (M32) {
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      m32a[nb] = m32_off(wm * 128, nb, l);
+      m32b[nb] = 16384u + m32_off(wn * 128, nb, l);
+    }
+  }
   // DIAG build only (timing diagnosis, never the production kernel): cycles spent in the
   // step-entry waits + barrier, in the step bodies and in the epilogues, per wave.
   unsigned long long t_wait = 0, t_body = 0, t_epi = 0, t_mark = 0;
@@ -732,13 +835,13 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   // fragments of the first step: stage 0 landed (two younger stages of NQ pieces in flight)
   wait_vmcnt<2 * NQ>();
   __builtin_amdgcn_s_barrier();
-  read_frags<AK, BKM, BN>(F0, smem, wm, wn, l);
+  read_frags<AK, BKM, BN, M32>(F0, smem, wm, wn, l);
   if constexpr (TIMED) t_mark = stamp();
 
   // One consumer step on `cur`, prefetching the next step's fragments into `nxt`.
   // Entry wait: stage s+1 landed for this wave (younger: stage s+2 = NQ pieces, plus the
   // previous item's epilogue stores on an item's first step), then the step barrier.
-  auto step = [&](Frags<AK, BKM, BN>& cur, Frags<AK, BKM, BN>& nxt, bool first, auto zero, auto nopf, bool last,
+  auto step = [&](Frags<AK, BKM, BN, M32>& cur, Frags<AK, BKM, BN, M32>& nxt, bool first, auto zero, auto nopf, bool last,
                   int bcol0) {
     constexpr bool ZR = decltype(zero)::value;
     constexpr bool NOPF = decltype(nopf)::value;   // no next-step fragment reads (item end, SWB)
@@ -781,6 +884,24 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
 
     c_slot = (c_slot + 1) & 3;
     const char* src = smem + c_slot * SLOT;
+    if constexpr (M32) {
+      // 32 MFMAs t = 16 kk + 4 bi + bj; after MFMA t < 16 the next step's fragment t (A for
+      // t < 8, B after: two transposed reads each); DMA piece q after MFMA 4 q + 2.
+      static_for<0, 32>([&](auto T) {
+        constexpr int t = decltype(T)::value;
+        constexpr int kk = t >> 4, bi = (t >> 2) & 3, bj = t & 3;
+        acc32_mfma<bi, bj, ZR && kk == 0>(cur.b.get(2 * bj + kk), cur.a.get(2 * bi + kk));
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (t == 0) stage_rsrc_a();
+        if constexpr (t == 1) stage_rsrc_b();
+        // next step's fragments: block nb of A after MFMA 2 nb, of B after MFMA 8 + 2 nb
+        if constexpr (!NOPF && t < 8 && (t & 1) == 0) nxt.a.load_nb(t >> 1, src + m32a[t >> 1]);
+        if constexpr (!NOPF && t >= 8 && t < 16 && (t & 1) == 0) nxt.b.load_nb((t - 8) >> 1, src + m32b[(t - 8) >> 1]);
+        if constexpr ((t & 3) == 2 && (t >> 2) < NQ) issue(t >> 2);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      advance();
+    } else {
     // Rows q of NJ MFMAs (A fragment q against every B fragment).  Rows BR .. BR+3 read the
     // next step's fragments (A 2r, 2r+1; B 2r, 2r+1 while < NJ; r = q - BR).  DMA pieces:
     // SCHED 0 two per row in rows 4-7, SCHED 1 one per row.  At NJ = 8 this is the hand-placed
@@ -816,6 +937,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
       });
     });
     advance();
+    }
   };
 
   for (bool first = true; it < total; it += G, first = false) {
@@ -835,7 +957,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
       }
       step(F1, F0, false, NO, std::true_type{}, true, bcol0);
       epilogue_swb(ci, M, N, swb, wm, wn, l);
-      read_frags<AK, BKM, BN>(F0, smem + c_slot * SLOT, wm, wn, l);
+      read_frags<AK, BKM, BN, M32>(F0, smem + c_slot * SLOT, wm, wn, l);
       continue;
     }
     step(F0, F1, !first, std::true_type{}, NO, false, bcol0);
@@ -848,6 +970,10 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
       const unsigned long long t = stamp();
       t_body += t - t_mark;
       t_mark = t;
+    }
+    if constexpr (M32) {
+      epilogue_f32_m32(ci, C, M, N, ldc, slab_stride, c_bytes, wm, wn, l);
+      continue;
     }
     if (OUT == 0 && bias) wait_vmcnt<NQ - PBB>();   // this wave's bias DMA landed (younger: the ring pieces after it)
     if (OUT == 0 && bias)
@@ -910,6 +1036,9 @@ extern "C" void dpfs_gemm4_sched(int v) { g_g4_sched = v; }
 static int g_g4_br = 0;
 extern "C" void dpfs_gemm4_br(int v) { g_g4_br = (v >= 0 && v <= 2) ? v : 0; }
 extern "C" void dpfs_gemm4_group_m(int g) { g_g4_group_m = g > 0 ? g : 4; }
+// TN main loop: 1 = the 32x32x16 form (gemm4_k's M32, default), 0 = 16x16x32 (A/B probes).
+static int g_g4_m32 = 1;
+extern "C" void dpfs_gemm4_m32(int v) { g_g4_m32 = v ? 1 : 0; }
 
 // gate|up projection with SwiGLU in the epilogue (SwiOut): C[M, N] = A perm(B)^T + perm(bias)
 // (B / bias in the natural [gate | up] layout, read interleaved: reference.gu_perm),
@@ -1027,6 +1156,13 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
           gemm4_k<AK_, BK_, OUT_, 0, false, 0, 256, 64><<<grid, 256, 0, s>>>(G4_ARGS);       \
         else                                                                                      \
           gemm4_k<AK_, BK_, OUT_, 0, false, 0, 256, 128><<<grid, 256, 0, s>>>(G4_ARGS);      \
+        break;                                                                                    \
+      }                                                                                           \
+    }                                                                                             \
+    if constexpr (!AK_ && !BK_ && OUT_ == 1) {                                                    \
+      if (fast && sched == 1 && g_g4_m32) {                                                       \
+        gemm4_k<false, false, 1, 0, true, 1, 256, 0, false, false, 0, 0, true>                    \
+            <<<grid, 256, 0, s>>>(G4_ARGS);                                                       \
         break;                                                                                    \
       }                                                                                           \
     }                                                                                             \

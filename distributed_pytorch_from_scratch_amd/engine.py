@@ -73,7 +73,7 @@ class TrainStep:
                  target_ids: torch.Tensor) -> torch.Tensor:
         e0 = self._event()
         with roctx("fwd"):
-            loss = self.model.loss(input_ids, position_ids, target_ids)
+            loss = self.model.loss(input_ids, position_ids, target_ids, unit_grad=True)
         e1 = self._event()
         self.optimizer.zero_grad(set_to_none=True)
         with roctx("bwd"):

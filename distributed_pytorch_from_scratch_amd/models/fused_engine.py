@@ -266,14 +266,27 @@ class DecoderTrainFn(torch.autograd.Function):
                 s["pend"], s["pend_bias"], s["h"] = qout, L.bd, _ar(qout)
                 if recompute:          # keep only the layer input; the rest is rebuilt in backward
                     s["layers"][-1] = {"x": s["layers"][-1]["x"]}
-        # head: residual, final norm, lm_head shard, vocab-parallel CE statistics
+        # head: residual, final norm, lm_head shard, vocab-parallel CE statistics.  TP 1 with a
+        # unit loss gradient (engine.TrainStep): d logits is written in the same pass over the
+        # logits as the statistics (k.ce_fused), so backward does not read them again.
         losses_sum = torch.zeros((), device=dev, dtype=torch.float32)
         n_valid_total = torch.zeros((), device=dev, dtype=torch.float32)
+        fuse_ce = tp == 1 and getattr(model, "_ce_unit_grad", False) and hasattr(k, "ce_fused")
+        if fuse_ce:
+            n_valid_all = (tgt != ignore_index).sum().float().clamp_min(1.0)
         for s in st:
             _wait(s["h"])
             xf, hf, rf = k.add_rmsnorm_fwd(s["pend"], s["pend_bias"], s["x"], model.norm.scale, model.norm.eps)
             logits = GS.gemm_nt(k, hf, W(head.weight), head.bias)
-            stats = k.ce_fwd_stats(logits, s["tgt"], vst, vvalid)
+            stats = None
+            if fuse_ce:
+                gs = (s["tgt"] != ignore_index).float() / n_valid_all
+                db = torch.empty(logits.size(1), device=dev, dtype=torch.float32) if head.bias is not None else None
+                stats = k.ce_fused(logits, s["tgt"], gs, vst, vvalid, db)
+                if stats is not None:
+                    s.update(ce_done=True, ce_db=db)
+            if stats is None:
+                stats = k.ce_fwd_stats(logits, s["tgt"], vst, vvalid)
             if tp > 1:
                 allst = stats.new_empty((tp * stats.size(0), 3))
                 dist.all_gather_into_tensor(allst, stats, group=p.tp_group)
@@ -370,10 +383,13 @@ class DecoderTrainFn(torch.autograd.Function):
         # ---- head: CE backward in place over the logits, lm_head dgrad -> async AR
         lm_p = []
         for ci, s in enumerate(st):
-            gs = s["valid"].float() * gscale_all
             dl = s["logits"]
-            db = first(g, "lm_b", dl, dl.size(1)) if head.bias is not None else None
-            k.ce_bwd(dl, s["tgt"], s["ce_lse"], gs, vst, vvalid, dl, db)    # + lm_head bias grad
+            if s.pop("ce_done", False):     # d logits (and its column sums) came with the forward
+                db = s.pop("ce_db")
+            else:
+                gs = s["valid"].float() * gscale_all
+                db = first(g, "lm_b", dl, dl.size(1)) if head.bias is not None else None
+                k.ce_bwd(dl, s["tgt"], s["ce_lse"], gs, vst, vvalid, dl, db)    # + lm_head bias grad
             dh = GS.gemm_nn(k, dl, W(head.weight), out=_slot(ci, dl.size(0), d, dt))
             s["bh"] = _ar(dh)
             s["dpend"] = dh

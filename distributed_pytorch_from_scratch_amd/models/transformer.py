@@ -251,13 +251,16 @@ class Transformer(nn.Module):
         return 2 if (p is not None and p.tp_size > 1) else 1
 
     def loss(self, input_ids: torch.Tensor, position_ids: torch.Tensor, target_ids: torch.Tensor,
-             ignore_index: int = IGNORE_INDEX) -> torch.Tensor:
+             ignore_index: int = IGNORE_INDEX, unit_grad: bool = False) -> torch.Tensor:
         """Mean next-token CE via the vocab-parallel cross-entropy (no logits all-gather).
 
         Runs the explicit-schedule engine (``models/fused_engine.py``: ping-pong chunks with
         all-reduces overlapped by the other chunk's compute) when supported, else the modular
-        autograd path."""
+        autograd path.  ``unit_grad``: the caller differentiates the returned loss with a unit
+        gradient (``loss.backward()``, as ``engine.TrainStep`` does), so at TP 1 the engine may
+        compute d logits in the forward, in the same pass over the logits as the loss."""
         if self.fused_supported():
+            self._ce_unit_grad = bool(unit_grad)
             from .fused_engine import DecoderTrainFn, collect_params
             assert input_ids.size(1) <= self.args.maxlen
             p = pm.pgm

@@ -430,6 +430,17 @@ def ce_bwd(logits: torch.Tensor, targets: torch.Tensor, lse: torch.Tensor, gscal
     return out
 
 
+def ce_fused(logits: torch.Tensor, targets: torch.Tensor, gscale: torch.Tensor, vocab_start: int,
+             vocab_valid: int, dbias: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """Single-shard CE forward and backward in one pass (TP 1: the shard is the whole vocab, so
+    the row's lse is local): returns the :func:`ce_fwd_stats` rows and overwrites ``logits``
+    with :func:`ce_bwd`'s (softmax - onehot) * gscale[row] (+ the column sums into ``dbias``)."""
+    stats = ce_fwd_stats(logits, targets, vocab_start, vocab_valid)
+    lse = stats[:, 0] + torch.log(stats[:, 1])
+    ce_bwd(logits, targets, lse, gscale, vocab_start, vocab_valid, logits, dbias)
+    return stats
+
+
 # -------------------------------------------------------------------------- Adam ----
 
 def adam_step(params, grads, exp_avgs, exp_avg_sqs, shadows, lr: float, beta1: float,

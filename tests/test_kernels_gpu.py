@@ -488,6 +488,42 @@ def test_ce_bwd_fused_bias_grad(C, M, V, valid, start):
     assert _rel(out, rout) < 1e-2 and _rel(db, rdb) < 1e-3
 
 
+@pytest.mark.parametrize("M,V,valid", [(4096, 50304, 50257), (777, 32000, 32000), (300, 1000, 997),
+                                       (50, 4096 * 13, 4096 * 13), (3, 8, 5), (600, 2048, 100)])
+@pytest.mark.parametrize("bias", [True, False])
+def test_ce_fused_one_pass(C, M, V, valid, bias):
+    """TP-1 CE forward + backward in one pass over the logits (ce_fused_k): the ce_fwd_stats rows
+    and the in-place (softmax - onehot) * g (+ column sums) against the fp32 oracle, with ignored
+    rows (target -1, g = 0) and a padded vocab tail (valid < V)."""
+    torch.manual_seed(17)
+    logits = (3 * torch.randn(M, V, device=DEV)).bfloat16()
+    tgt = torch.randint(0, valid, (M,), device=DEV)
+    tgt[::7] = -1
+    gs = (tgt >= 0).float() / max(1, int((tgt >= 0).sum()))
+    ref_in = logits.float()
+    x = logits.clone()
+    db = torch.empty(V, device=DEV) if bias else None
+    st = C.ce_fused(x, tgt, gs, 0, valid, db)
+    assert st is not None
+    rdb = torch.empty(V, device=DEV) if bias else None
+    rst = R.ce_fused(ref_in, tgt, gs, 0, valid, rdb)
+    lse, rlse = st[:, 0] + torch.log(st[:, 1]), rst[:, 0] + torch.log(rst[:, 1])
+    assert torch.allclose(lse, rlse, rtol=0, atol=1e-4)
+    assert torch.equal(st[:, 2], rst[:, 2])
+    assert _rel(x, ref_in) < 1e-2
+    assert x[:, valid:].abs().max().item() == 0 if valid < V else True
+    if bias:
+        assert _rel(db, rdb) < 1e-3
+
+
+def test_ce_fused_declines_what_it_cannot_run(C):
+    x = torch.randn(4, 13, device=DEV).bfloat16()           # V % 8 != 0: the two-pass path
+    t = torch.zeros(4, dtype=torch.long, device=DEV)
+    assert C.ce_fused(x, t, torch.ones(4, device=DEV), 0, 13) is None
+    x = torch.randn(2, 8 * 512 * 14, device=DEV).bfloat16()   # past 13 slots per thread
+    assert C.ce_fused(x, t[:2], torch.ones(2, device=DEV), 0, x.size(1)) is None
+
+
 @pytest.mark.parametrize("M,N,K0,K1", [(768, 768, 8192, 8192), (1000, 776, 4096, 2048), (2304, 768, 32768, 32768)])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_gemm_tn2_two_buffer_reduction(C, M, N, K0, K1, accumulate):
@@ -734,6 +770,28 @@ def test_gemm_v4_tn(C, M, N, K, splits):
         assert _rel(acc, want) < 1e-5
     finally:
         C.gemm_force(-1, 0)
+
+
+@pytest.mark.parametrize("M,N,K", [(2304, 768, 32768), (768, 2048, 8192), (4096, 768, 4096), (1000, 776, 2048)])
+def test_gemm_tn_m32_matches_16x16_form(C, M, N, K):
+    """The 32x32x16 TN main loop (default) against the 16x16x32 one and the fp32 oracle, with
+    split-K slabs and accumulate (the weight-gradient shapes of GPT-2 small)."""
+    torch.manual_seed(31)
+    a = torch.randn(K, M, device=DEV).bfloat16()
+    b = torch.randn(K, N, device=DEV).bfloat16()
+    ref = R.gemm_tn(a.float(), b.float())
+    try:
+        C.gemm4_m32(0)
+        o16 = C.gemm_tn(a, b)
+    finally:
+        C.gemm4_m32(1)
+    o32 = C.gemm_tn(a, b)
+    assert _rel(o32, ref) < 1e-5 and _rel(o16, ref) < 1e-5
+    assert _rel(o32, o16) < 1e-5
+    acc = torch.randn(M, N, device=DEV)
+    want = acc + ref
+    C.gemm_tn(a, b, acc, True)
+    assert _rel(acc, want) < 1e-5
 
 
 def test_gemm_v4_split_k_bf16_long_k(C):

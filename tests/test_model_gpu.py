@@ -33,9 +33,11 @@ def _models(args):
 
 
 @pytest.mark.parametrize("preset,T", [("plumbing", 128), ("gpt2-small", 256)])
-def test_gpu_loss_and_grads_match_cpu(dist1, monkeypatch, preset, T):
+@pytest.mark.parametrize("unit", [False, True])
+def test_gpu_loss_and_grads_match_cpu(dist1, monkeypatch, preset, T, unit):
     """Every GEMM on our kernels (gemm.hip / gemm4.hip, no hipBLASLt candidate): loss within
-    1 % and every parameter gradient within 2 % (relative L2) of the fp32 CPU oracle."""
+    1 % and every parameter gradient within 2 % (relative L2) of the fp32 CPU oracle.  ``unit``:
+    the TrainStep form (d logits in the forward's one pass, ce_fused_k)."""
     from distributed_pytorch_from_scratch_amd.models import get_preset
     monkeypatch.setenv("DPFS_GEMM_BACKEND", "ours")
     args = get_preset(preset, num_layers=2)
@@ -47,7 +49,7 @@ def test_gpu_loss_and_grads_match_cpu(dist1, monkeypatch, preset, T):
     pos = torch.arange(T).repeat(B, 1)
     lc = cpu.loss(ids, pos, tgt)
     lc.backward()
-    lg = gpu.loss(ids.cuda(), pos.cuda(), tgt.cuda())
+    lg = gpu.loss(ids.cuda(), pos.cuda(), tgt.cuda(), unit_grad=unit)
     lg.backward()
     assert abs(lc.item() - lg.item()) < 1e-2 * max(1.0, abs(lc.item()))
     gc = dict(cpu.named_parameters())
