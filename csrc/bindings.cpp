@@ -17,6 +17,9 @@ extern "C" {
 void dpfs_gemm_nt(const void*, const void*, void*, const float*, int, int, int, int, int, int, int, hipStream_t);
 void dpfs_gemm_nn(const void*, const void*, void*, int, int, int, int, int, int, int, hipStream_t);
 int dpfs_gemm_tn_splits(int, int, int);
+long long dpfs_gemm_tn_group_ws(int, const int*, const int*, const int*, const int*, int, const int*);
+int dpfs_gemm_tn_group(int, const void* const*, const void* const*, float* const*, const int*, const int*, const int*,
+                       const int*, const int*, int, float*, long long, hipStream_t);
 long long dpfs_gemm_tn_ws(int, int, int, int);
 void dpfs_gemm_set_impl(int);
 int dpfs_gemm_rope_fusable(int, int, int, int, int);
@@ -284,6 +287,47 @@ torch::Tensor gemm_tn(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
   dpfs_gemm_tn(a.data_ptr(), b.data_ptr(), c.data_ptr<float>(), ws.defined() ? ws.data_ptr<float>() : nullptr, (int)M,
                (int)N, (int)K, (int)a.stride(0), (int)b.stride(0), accumulate ? 1 : 0, (int)variant, stream());
   return c;
+}
+
+// outs[g] fp32 (+= when acc[g]) a[g][K, M_g]^T b[g][K, N_g] for up to 4 GEMMs over one K as
+// one grouped launch (+ one reduction); False (nothing written) where the group does not apply.
+bool gemm_tn_group(std::vector<torch::Tensor> a, std::vector<torch::Tensor> b, std::vector<torch::Tensor> outs,
+                   std::vector<int64_t> acc) {
+  const size_t n = a.size();
+  TORCH_CHECK(n >= 1 && n <= 4 && b.size() == n && outs.size() == n && acc.size() == n, "gemm_tn_group: 1..4 GEMMs");
+  const int64_t K = a[0].size(0);
+  const void* pa[4];
+  const void* pb[4];
+  float* pc[4];
+  int M[4], N[4], lda[4], ldb[4], ac[4];
+  for (size_t g = 0; g < n; ++g) {
+    check_rowmajor(a[g], "gemm_tn_group a");
+    check_rowmajor(b[g], "gemm_tn_group b");
+    TORCH_CHECK(a[g].scalar_type() == torch::kBFloat16 && b[g].scalar_type() == torch::kBFloat16,
+                "gemm_tn_group: bf16 operands");
+    TORCH_CHECK(a[g].size(0) == K && b[g].size(0) == K, "gemm_tn_group: one K for the group");
+    TORCH_CHECK(a[g].device() == a[0].device() && b[g].device() == a[0].device() && outs[g].device() == a[0].device(),
+                "gemm_tn_group: one device");
+    M[g] = (int)a[g].size(1);
+    N[g] = (int)b[g].size(1);
+    TORCH_CHECK(outs[g].scalar_type() == torch::kFloat32 && outs[g].is_contiguous() && outs[g].dim() == 2 &&
+                    outs[g].size(0) == M[g] && outs[g].size(1) == N[g],
+                "gemm_tn_group: out must be contiguous fp32 [M,N]");
+    lda[g] = (int)a[g].stride(0);
+    ldb[g] = (int)b[g].stride(0);
+    ac[g] = acc[g] ? 1 : 0;
+    pa[g] = a[g].data_ptr();
+    pb[g] = b[g].data_ptr();
+    pc[g] = outs[g].data_ptr<float>();
+  }
+  if (K <= 0 || K >= (1ll << 31)) return false;
+  const long long wsn = dpfs_gemm_tn_group_ws((int)n, M, N, lda, ldb, (int)K, ac);
+  if (wsn < 0) return false;
+  const at::DeviceGuard dg(a[0].device());
+  torch::Tensor ws;
+  if (wsn > 0) ws = torch::empty({(int64_t)wsn}, outs[0].options());
+  return dpfs_gemm_tn_group((int)n, pa, pb, pc, M, N, lda, ldb, ac, (int)K, ws.defined() ? ws.data_ptr<float>() : nullptr,
+                            wsn, stream()) != 0;
 }
 
 // c[M,N] fp32 (+)= a0[K0,M]^T b0[K0,N] + a1[K1,M]^T b1[K1,N] in one split-K launch; None
@@ -1211,6 +1255,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "int64 buffer of the DIAG builds (attn_fwd / attn_bwd impl 5): per-wave s_memtime splits");
   m.def("gemm4_diag", [](torch::Tensor t) { dpfs_gemm4_diag(t.defined() && t.numel() ? t.data_ptr() : nullptr); },
         "int64 buffer [grid*4*4] for the DIAG build's per-wave cycle split (gemm4_ablate bit 16)");
+  m.def("gemm_tn_group", &gemm_tn_group, py::arg("a"), py::arg("b"), py::arg("outs"), py::arg("acc"));
+  m.def("gemm_tn_splits", [](int M, int N, int K) { return dpfs_gemm_tn_splits(M, N, K); },
+        "K-split count of the TN (weight-gradient) plan for an M x N output over K");
   m.def("gemm4_m32", [](int v) { dpfs_gemm4_m32(v); },
         "TN main loop of the v4 GEMM: 1 = 32x32x16 MFMAs (default), 0 = 16x16x32 (A/B probes)");
   m.def("gemm4_br", [](int v) { dpfs_gemm4_br(v); },

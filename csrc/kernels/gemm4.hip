@@ -245,7 +245,23 @@ __device__ __forceinline__ void read_frags(Frags<AK, BKM, BN, M32>& f, const cha
 
 // Work item -> tile origin and K range (grouped order as gemm.hip's gemmp_k).
 struct Item {
-  int m0, n0, kb, ke, split, sel;
+  int m0, n0, kb, ke, split, sel, g;
+};
+
+// A group of up to 4 TN GEMMs over the same K (a layer's weight gradients), one launch: item
+// lin belongs to GEMM g with item0[g] <= lin < item0[g + 1]; every GEMM uses the launch's K
+// split length kps, so all items are equally long (gemm4_k's GRP).
+struct TnGemm {
+  const bf16* A;
+  const bf16* B;
+  float* C;
+  long long slab_stride;
+  int M, N, lda, ldb, ldc, tiles_m, tiles_n, item0;
+  unsigned a_bytes, b_bytes, c_bytes, pad;
+};
+struct TnGroup {
+  int n, total;
+  TnGemm d[4];
 };
 
 template <int BN>
@@ -266,6 +282,7 @@ __device__ __forceinline__ Item decode(int lin, int nwg, int tiles_m, int tiles_
   KASSERT(it.m0 < tiles_m * 256 && it.n0 < tiles_n * BN && it.kb <= K,
                "item %d -> tile (%d, %d) k %d", lin, it.m0, it.n0, it.kb);
   it.sel = 0;
+  it.g = 0;
   if (it.kb >= k_switch) {
     it.sel = 1;
     it.kb -= k_switch;
@@ -635,14 +652,14 @@ __device__ __forceinline__ void epilogue_swb(const Item& ci, int M, int F, const
 // address / SALU work fit in the MFMA shadow (the 16x16x32 TN step issues ~1.5k cycles of
 // non-MFMA work against 1024 of matrix time).
 template <bool AK, bool BKM, int OUT, int DIAG = 0, bool FAST = false, int SCHED = 0, int BN = 256, int ROPE = 0,
-          bool SWIGLU = false, bool SWB = false, int BR = 0, int SA = 0, bool M32 = false>
+          bool SWIGLU = false, bool SWB = false, int BR = 0, int SA = 0, bool M32 = false, bool GRP = false>
 __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                   void* __restrict__ C, const float* __restrict__ bias, int M, int N,
                                                   int K, int lda, int ldb, int ldc, int kps, int splits,
                                                   long long slab_stride, unsigned a_bytes, unsigned b_bytes,
                                                   unsigned c_bytes, Rope rope, int group_m, Dual dual, int dbg,
                                                   unsigned long long* diag, SwiOut swo = SwiOut{},
-                                                  SwiBwd swb = SwiBwd{}) {
+                                                  SwiBwd swb = SwiBwd{}, TnGroup grp = TnGroup{}) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_TOTAL];
   constexpr bool TIMED = DIAG == 1 || DIAG == 2;   // the s_memtime builds
   constexpr int NJ = BN / 32;                  // 16-column MFMA tiles per wave
@@ -656,6 +673,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   static_assert(BR >= 0 && BR <= 4 && (BR == 0 || DIAG == 0), "barrier row");
   static_assert(!M32 || (!AK && !BKM && OUT == 1 && BN == 256 && BR == 0 && SCHED == 1 && ROPE == 0),
                 "32x32x16 main loop: TN fp32, 256-wide");
+  static_assert(!GRP || (M32 && FAST), "grouped TN: the 32x32x16 FAST kernel");
   // ring pieces issued before the step's barrier (their count joins the wait, and the bias
   // DMA issued after the barrier has NQ - PBB younger ring pieces)
   constexpr int PBB = SCHED == 1 ? (BR < NQ ? BR : NQ) : 0;
@@ -663,7 +681,22 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   const int tiles_n = (N + BN - 1) / BN;
   const int tiles_m = (M + 255) / 256;
   const int nwg = tiles_m * tiles_n;
-  const int total = nwg * splits;
+  const int total = GRP ? grp.total : nwg * splits;
+  // work item -> tile / K range (GRP: of its GEMM in the group)
+  auto gdecode = [&](int lin) -> Item {
+    if constexpr (GRP) {
+      int g = 0;
+#pragma unroll
+      for (int i = 1; i < 4; ++i)
+        if (i < grp.n && lin >= grp.d[i].item0) g = i;
+      const TnGemm& d = grp.d[g];
+      Item x = decode<BN>(lin - d.item0, d.tiles_m * d.tiles_n, d.tiles_m, d.tiles_n, group_m, K, kps, 0x7fffffff);
+      x.g = g;
+      return x;
+    } else {
+      return decode<BN>(lin, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
+    }
+  };
   const int G = gridDim.x;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -685,7 +718,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
 
   // ---- producer cursor: the DMA stream runs 3 steps ahead of the consumer, across items.
   int p_it = it;
-  Item pi = decode<BN>(p_it, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
+  Item pi = gdecode(p_it);
   int p_t = 0, p_nk = nsteps(pi);
   int p_slot = 0;
   // Per-item lane offsets of the wave's NQ DMA pieces (4 of A, NBQ of B): a step adds one
@@ -695,7 +728,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   unsigned pbase[8];
   auto rebase = [&]() {
     const bool s2 = pi.sel != 0;
-    const int la = s2 ? lda2 : lda, lb = s2 ? ldb2 : ldb;
+    const int la = GRP ? grp.d[pi.g].lda : (s2 ? lda2 : lda), lb = GRP ? grp.d[pi.g].ldb : (s2 ? ldb2 : ldb);
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const bool isA = q < 4;
@@ -740,13 +773,15 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   auto item_rsrc = [&]() {
     if constexpr (FAST) {
       const bool s2 = pi.sel != 0;
-      const int la = s2 ? lda2 : lda, lb = s2 ? ldb2 : ldb;
+      const int la = GRP ? grp.d[pi.g].lda : (s2 ? lda2 : lda), lb = GRP ? grp.d[pi.g].ldb : (s2 ? ldb2 : ldb);
       const long long adv_a = AK ? (long long)pi.kb * 2 : (long long)pi.kb * la * 2;
       const long long adv_b = BKM ? (long long)pi.kb * 2 : (long long)pi.kb * lb * 2;
-      ia = reinterpret_cast<unsigned long long>(s2 ? dual.A2 : A) + adv_a;
-      ib = reinterpret_cast<unsigned long long>(s2 ? dual.B2 : B) + adv_b;
-      na0 = (s2 ? dual.a2_bytes : a_bytes) - (unsigned)adv_a;
-      nb0 = (s2 ? dual.b2_bytes : b_bytes) - (unsigned)adv_b;
+      const bf16* a0 = GRP ? grp.d[pi.g].A : (s2 ? dual.A2 : A);
+      const bf16* b0 = GRP ? grp.d[pi.g].B : (s2 ? dual.B2 : B);
+      ia = reinterpret_cast<unsigned long long>(a0) + adv_a;
+      ib = reinterpret_cast<unsigned long long>(b0) + adv_b;
+      na0 = (GRP ? grp.d[pi.g].a_bytes : (s2 ? dual.a2_bytes : a_bytes)) - (unsigned)adv_a;
+      nb0 = (GRP ? grp.d[pi.g].b_bytes : (s2 ? dual.b2_bytes : b_bytes)) - (unsigned)adv_b;
       sta = AK ? 64u : 64u * (unsigned)la;
       stb = BKM ? 64u : 64u * (unsigned)lb;
       nlive = (pi.ke - pi.kb + 31) / 32;
@@ -795,7 +830,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
       p_it += G;
       p_t = 0;
       if (p_it < total) {
-        pi = decode<BN>(p_it, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
+        pi = gdecode(p_it);
         p_nk = nsteps(pi);
         rebase();
         item_rsrc();
@@ -941,7 +976,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   };
 
   for (bool first = true; it < total; it += G, first = false) {
-    const Item ci = decode<BN>(it, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
+    const Item ci = gdecode(it);
     const int nk = nsteps(ci);
     const int bcol0 = ci.n0 + wn * (BN / 2);
     constexpr std::false_type NO{};
@@ -971,8 +1006,18 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
       t_body += t - t_mark;
       t_mark = t;
     }
-    if constexpr (M32) {
+    if constexpr (GRP) {
+      const TnGemm& d = grp.d[ci.g];
+      epilogue_f32_m32(ci, d.C, d.M, d.N, d.ldc, d.slab_stride, d.c_bytes, wm, wn, l);
+    } else if constexpr (M32) {
       epilogue_f32_m32(ci, C, M, N, ldc, slab_stride, c_bytes, wm, wn, l);
+    }
+    if constexpr (M32) {
+      if constexpr (TIMED) {
+        const unsigned long long t = stamp();
+        t_epi += t - t_mark;
+        t_mark = t;
+      }
       continue;
     }
     if (OUT == 0 && bias) wait_vmcnt<NQ - PBB>();   // this wave's bias DMA landed (younger: the ring pieces after it)
@@ -997,6 +1042,33 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   }
   // no LDS-DMA may still be writing when the workgroup's LDS is released
   wait_vmcnt<0>();
+}
+
+// Split-K reduction of a TN group (gemm4_k GRP): out_g[i] (+)= sum_s ws_g[s][i] for each GEMM g
+// of the launch, in a fixed order (deterministic); segment g holds elements [pre[g], pre[g+1])
+// of one flat index space (every segment a multiple of 4 long).
+struct RedGroup {
+  int n, S;
+  long long pre[5];
+  const float* ws[4];
+  float* out[4];
+  int acc[4];
+};
+__global__ __launch_bounds__(256) void splitk_reduce_group_k(RedGroup r) {
+  const long long tot = r.pre[r.n];
+  for (long long i = (blockIdx.x * (long long)blockDim.x + threadIdx.x) * 4; i < tot;
+       i += (long long)gridDim.x * blockDim.x * 4) {
+    int g = 0;
+#pragma unroll
+    for (int k = 1; k < 4; ++k)
+      if (k < r.n && i >= r.pre[k]) g = k;
+    const long long j = i - r.pre[g], ng = r.pre[g + 1] - r.pre[g];
+    float* o = r.out[g] + j;
+    f32x4 v = r.acc[g] ? *reinterpret_cast<const f32x4*>(o) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    const float* w = r.ws[g] + j;
+    for (int k = 0; k < r.S; ++k) v += *reinterpret_cast<const f32x4*>(w + k * ng);
+    *reinterpret_cast<f32x4*>(o) = v;
+  }
 }
 
 }  // namespace g4
@@ -1219,6 +1291,19 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
         rope, g_g4_group_m, dual, 0, nullptr);
     return true;
   }
+  if ((g_g4_ablate & (16 | 32)) && g_g4_diag && layout == 2 && fast && g_g4_m32) {
+    // TN 32x32x16: the DIAG builds (16: per-wave cycle split; 32: the same with no DMA issued)
+    const Rope rp = rope;
+    if (g_g4_ablate & 32)
+      gemm4_k<false, false, 1, 2, true, 1, 256, 0, false, false, 0, 0, true><<<grid, 256, 0, s>>>(
+          (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, kps, splits, slab_stride, a_bytes, b_bytes,
+          cb, rp, g_g4_group_m, dual, 0, g_g4_diag);
+    else
+      gemm4_k<false, false, 1, 1, true, 1, 256, 0, false, false, 0, 0, true><<<grid, 256, 0, s>>>(
+          (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, kps, splits, slab_stride, a_bytes, b_bytes,
+          cb, rp, g_g4_group_m, dual, 0, g_g4_diag);
+    return true;
+  }
   if ((g_g4_ablate & 16) && g_g4_diag && layout == 0 && !out_f32 && bn == 256 && fast) {
     gemm4_k<true, true, 0, 1, true, 1><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda,
                                                             ldb, ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb,
@@ -1238,4 +1323,112 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
 #undef G4_ARGS
 #undef G4_LAUNCH
   return true;
+}
+
+// ---------------------------------------------------------------- grouped weight gradients --
+// C_g (+)= A_g^T B_g for up to 4 TN GEMMs over the same K (a layer's weight gradients: A_g
+// [K, M_g], B_g [K, N_g], MN-contiguous), as ONE persistent 32x32x16 launch plus at most one
+// reduction launch: every GEMM takes the same K-split length, chosen for the group's total
+// tile count (a makespan model as tn_v2_splits: rounds of the CUs x split length, plus the
+// slabs' write + read), so all items are equally long and the rounds fill the chip; the
+// separate launches each paid a ramp / tail and one slab round trip per GEMM.
+static int tn_group_splits(int n, const int* M, const int* N, int K, long long* mn_out) {
+  long long tiles = 0, mn = 0;
+  for (int g = 0; g < n; ++g) {
+    tiles += (long long)((M[g] + 255) / 256) * ((N[g] + 255) / 256);
+    mn += (long long)M[g] * N[g];
+  }
+  *mn_out = mn;
+  const int cus = g4_cu_count();
+  int best = 1;
+  double best_t = 1e300;
+  for (int S = 1; S <= 64; ++S) {
+    if (S > 1 && K / S < 512) break;
+    const long long kps = ((K + S - 1) / S + 63) / 64;
+    const long long se = (K + kps * 64 - 1) / (kps * 64);
+    if (se != S) continue;   // (S and S - 1 giving the same split length)
+    const long long rounds = (tiles * S + cus - 1) / cus;
+    const double t = (double)rounds * kps * 1.95 + (S > 1 ? (double)S * mn * 8.0 / 4.0e6 : 0.0);
+    if (t < best_t * 0.97) {
+      best_t = t;
+      best = S;
+    }
+  }
+  return best;
+}
+
+// Floats of slab workspace dpfs_gemm_tn_group needs (0: none).  -1: the group does not run
+// grouped (K % 64, unaligned dims, spans past the 32-bit descriptors, the 16x16x32 TN form).
+extern "C" long long dpfs_gemm_tn_group_ws(int n, const int* M, const int* N, const int* lda, const int* ldb, int K,
+                                           const int* acc) {
+  if (n < 1 || n > 4 || K % 64 || !g_g4_m32 || K <= 0) return -1;
+  bool any_acc = false;
+  for (int g = 0; g < n; ++g) {
+    if (M[g] <= 0 || N[g] <= 0 || M[g] % 8 || N[g] % 8 || lda[g] < M[g] || ldb[g] < N[g]) return -1;
+    if (((long long)(K - 1) * lda[g] + M[g]) * 2 >= (1ll << 32) - 16) return -1;
+    if (((long long)(K - 1) * ldb[g] + N[g]) * 2 >= (1ll << 32) - 16) return -1;
+    if ((long long)M[g] * N[g] * 4 >= (1ll << 32) - 16) return -1;
+    any_acc |= acc[g] != 0;
+  }
+  long long mn;
+  const int S = tn_group_splits(n, M, N, K, &mn);
+  return (S > 1 || any_acc) ? (long long)S * mn : 0;
+}
+
+extern "C" int dpfs_gemm_tn_group(int n, const void* const* A, const void* const* B, float* const* C, const int* M,
+                                  const int* N, const int* lda, const int* ldb, const int* acc, int K, float* ws,
+                                  long long ws_floats, hipStream_t s) {
+  const long long need = dpfs_gemm_tn_group_ws(n, M, N, lda, ldb, K, acc);
+  if (need < 0 || (need > 0 && (ws == nullptr || ws_floats < need))) return 0;
+  long long mn;
+  const int S = tn_group_splits(n, M, N, K, &mn);
+  const bool slabs = need > 0;
+  int kps = (K + S - 1) / S;
+  kps = ((kps + 63) / 64) * 64;
+  TnGroup grp{};
+  grp.n = n;
+  RedGroup red{};
+  red.n = n;
+  red.S = S;
+  long long items = 0, off = 0;
+  for (int g = 0; g < n; ++g) {
+    TnGemm& d = grp.d[g];
+    d.A = (const bf16*)A[g];
+    d.B = (const bf16*)B[g];
+    d.M = M[g];
+    d.N = N[g];
+    d.lda = lda[g];
+    d.ldb = ldb[g];
+    d.ldc = N[g];
+    d.tiles_m = (M[g] + 255) / 256;
+    d.tiles_n = (N[g] + 255) / 256;
+    d.item0 = (int)items;
+    d.a_bytes = (unsigned)(((long long)(K - 1) * lda[g] + M[g]) * 2);
+    d.b_bytes = (unsigned)(((long long)(K - 1) * ldb[g] + N[g]) * 2);
+    d.c_bytes = (unsigned)((long long)M[g] * N[g] * 4);
+    const long long ng = (long long)M[g] * N[g];
+    d.C = slabs ? ws + off : C[g];
+    d.slab_stride = slabs ? ng : 0;
+    red.pre[g] = off / S;
+    red.ws[g] = ws + off;
+    red.out[g] = C[g];
+    red.acc[g] = acc[g];
+    if (slabs) off += S * ng;
+    items += (long long)d.tiles_m * d.tiles_n * S;
+  }
+  red.pre[n] = mn;
+  if (items >= (1ll << 31)) return 0;
+  grp.total = (int)items;
+  const int grid = (int)std::min<long long>(items, g4_cu_count());
+  const Rope rope = {nullptr, nullptr, 0, 64};
+  const Dual dual = {nullptr, nullptr, 0x7fffffff, 0, 0, 0u, 0u};
+  gemm4_k<false, false, 1, 0, true, 1, 256, 0, false, false, 0, 0, true, true><<<grid, 256, 0, s>>>(
+      grp.d[0].A, grp.d[0].B, grp.d[0].C, nullptr, 256, 256, K, lda[0], ldb[0], N[0], kps, S, 0, grp.d[0].a_bytes,
+      grp.d[0].b_bytes, grp.d[0].c_bytes, rope, g_g4_group_m, dual, 0, nullptr, SwiOut{}, SwiBwd{}, grp);
+  if (slabs) {
+    long long gr = (mn / 4 + 255) / 256;
+    if (gr > 4096) gr = 4096;
+    splitk_reduce_group_k<<<(int)gr, 256, 0, s>>>(red);
+  }
+  return 1;
 }

@@ -364,6 +364,23 @@ class DecoderTrainFn(torch.autograd.Function):
                     i += 1
             pairs.clear()
 
+        def tn_multi(key_dict, groups):
+            """Several weight gradients of one phase ((key, pairs) each): with one chunk, ONE
+            grouped launch (GS.gemm_tn_group, timed against separate calls); else per key."""
+            if all(len(pairs) == 1 for _, pairs in groups):
+                items = []
+                for key, pairs in groups:
+                    acc = key_dict.get(key)
+                    items.append((pairs[0][0], pairs[0][1], acc if acc is not None else V(key_dict, key),
+                                  acc is not None))
+                outs = GS.gemm_tn_group(k, items)
+                for (key, pairs), o in zip(groups, outs):
+                    key_dict[key] = o
+                    pairs.clear()
+                return
+            for key, pairs in groups:
+                tn_chunks(key_dict, key, pairs)
+
         def bias_acc(key_dict, key, dy, present):
             if present is None:
                 return
@@ -454,8 +471,13 @@ class DecoderTrainFn(torch.autograd.Function):
                 if dbgu is not None:
                     G["bgu"] = _addg(G.get("bgu"), dbgu, V(G, "bgu"))
                 del a["sw"], a["gu"]
-            tn_chunks(G, "wd", wd_p)        # under the chunks' all-reduces
-            tn_chunks(G, "wgu", wgu_p)
+            # With one chunk (no all-reduce to hide) the down / gate|up weight gradients wait for
+            # the Wo / QKV ones: a layer's four go out as one grouped launch at the end of b1
+            if C == 1:
+                pend_w = [("wd", wd_p), ("wgu", wgu_p)]
+            else:
+                tn_multi(G, [("wd", wd_p), ("wgu", wgu_p)])        # under the chunks' all-reduces
+                pend_w = []
             if li + 1 < nL:
                 dp_reduce(f"L{li + 1}")         # layer li+1 is complete (its norm1 grad just landed)
             # b1: wait, norm2 bwd, Wo / attention / QKV grads -> AR(dh)
@@ -487,8 +509,7 @@ class DecoderTrainFn(torch.autograd.Function):
                 for key in ("x2", "r2", "h2", "qkv", "o", "lse"):
                     a.pop(key, None)
             if li > 0:
-                tn_chunks(G, "wo", wo_p)
-                tn_chunks(G, "wqkv", wqkv_p)
+                tn_multi(G, pend_w + [("wo", wo_p), ("wqkv", wqkv_p)])
         # layer 0: the embedding gradient first, so its all-reduce (the largest DP bucket) runs
         # under layer 0's Wo / QKV weight-gradient GEMMs
         ev = arena.view("emb", "emb")
@@ -498,8 +519,7 @@ class DecoderTrainFn(torch.autograd.Function):
             k.embedding_bwd(s["g"], s["ids"], model.embedding.weight.size(0), model.embedding.vocab_st_idx, out=ev)
         g["emb"] = ev
         dp_reduce("emb")
-        tn_chunks(gl[0], "wo", wo_p)
-        tn_chunks(gl[0], "wqkv", wqkv_p)
+        tn_multi(gl[0], pend_w + [("wo", wo_p), ("wqkv", wqkv_p)])
         dp_reduce("L0")
         _defer_end()
         tp_comm.check()   # an xGMI barrier that timed out raises here (host-mapped flag, no sync)

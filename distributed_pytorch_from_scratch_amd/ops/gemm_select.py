@@ -39,6 +39,10 @@ from .dispatch import shadow
 _choice: Dict[Tuple, str] = {}
 _times: Dict[Tuple, Dict[str, float]] = {}   # key -> {candidate: ms} at selection
 
+# A/B hook for tools/ab_attr.py (same-box interleaved bench runs), not a user switch: False
+# turns the grouped weight-gradient launch (gemm_tn_group) off.
+TN_GROUP = True
+
 
 def mode() -> str:
     return os.environ.get("DPFS_GEMM_BACKEND", "auto")
@@ -469,3 +473,36 @@ def gemm_tn_pair(k, a0: torch.Tensor, b0: torch.Tensor, a1: torch.Tensor, b1: to
         if r is not None:
             return r
     return split(out, accumulate)
+
+
+def gemm_tn_group(k, items) -> list:
+    """Several weight gradients over the same rows, ``items`` = [(a, b, out, accumulate)]:
+    out (+)= a^T b each.  Candidates, timed per group shape: ``group`` = ONE persistent
+    32x32x16 launch over every GEMM's tiles with one shared K-split length and one slab
+    reduction (``gemm_tn_group``: the launches' ramps / tails and per-GEMM slab round trips of
+    the separate calls are paid once), ``each`` = one :func:`gemm_tn` per item."""
+    outs = [o for _, _, o, _ in items]
+
+    def each(dsts):
+        return [gemm_tn(k, a, b, d, acc) for (a, b, _, acc), d in zip(items, dsts)]
+
+    if (not TN_GROUP or k is reference or len(items) < 2 or any(o is None for o in outs) or not items[0][0].is_cuda
+            or not hasattr(k, "gemm_tn_group") or mode() not in ("auto", "ours")):
+        return each(outs)
+    K = items[0][0].shape[0]
+    if K < _MIN_ROWS or any(a.shape[0] != K or b.shape[0] != K for a, b, _, _ in items):
+        return each(outs)
+    A = [a for a, _, _, _ in items]
+    B = [b for _, b, _, _ in items]
+    acc = [int(bool(x)) for _, _, _, x in items]
+    key = ("tng",) + tuple((a.shape[1], b.shape[1], bool(x)) for a, b, _, x in items) + (K, A[0].device.index)
+    c = _choice.get(key)
+    if c is None:
+        scratch = [torch.zeros(a.shape[1], b.shape[1], device=a.device, dtype=torch.float32) for a, b in zip(A, B)]
+        if not k.gemm_tn_group(A, B, scratch, acc):     # the group does not apply to these shapes
+            c = _choice[key] = "each"
+        else:
+            c = _pick(key, {"each": lambda: each(scratch), "group": lambda: k.gemm_tn_group(A, B, scratch, acc)})
+    if c == "group" and k.gemm_tn_group(A, B, outs, acc):
+        return outs
+    return each(outs)

@@ -794,6 +794,29 @@ def test_gemm_tn_m32_matches_16x16_form(C, M, N, K):
     assert _rel(acc, want) < 1e-5
 
 
+@pytest.mark.parametrize("shapes,K", [([(2304, 768), (768, 768)], 32768), ([(768, 2048), (4096, 768)], 32768),
+                                      ([(2304, 768), (768, 768), (4096, 768), (768, 2048)], 8192),
+                                      ([(1000, 776), (96, 768), (256, 256)], 2048), ([(384, 768), (768, 128)], 4096)])
+def test_gemm_tn_group(C, shapes, K):
+    """A layer's weight gradients as ONE grouped 32x32x16 launch (+ one slab reduction) against
+    the fp32 oracle, the first GEMM accumulating into an existing gradient."""
+    torch.manual_seed(32)
+    A = [torch.randn(K, m, device=DEV).bfloat16() for m, _ in shapes]
+    B = [torch.randn(K, n, device=DEV).bfloat16() for _, n in shapes]
+    outs = [torch.randn(m, n, device=DEV) for m, n in shapes]
+    acc = [1] + [0] * (len(shapes) - 1)
+    want = [(o.clone() if a_ else 0) + R.gemm_tn(a.float(), b.float()) for o, a, b, a_ in zip(outs, A, B, acc)]
+    assert C.gemm_tn_group(A, B, outs, acc)
+    for o, w in zip(outs, want):
+        assert _rel(o, w) < 1e-5
+
+
+def test_gemm_tn_group_declines(C):
+    a = torch.randn(1000, 256, device=DEV).bfloat16()     # K % 64 != 0: not grouped
+    outs = [torch.empty(256, 256, device=DEV)] * 2
+    assert not C.gemm_tn_group([a, a], [a, a], outs, [0, 0])
+
+
 def test_gemm_v4_split_k_bf16_long_k(C):
     """bf16-output GEMM with a long K (the lm_head data gradient: N = d_model, K = vocab shard)
     takes the split-K fp32 slab path on v4."""

@@ -100,7 +100,7 @@ def main():
     ap.add_argument("--group-m", type=int, nargs="*", default=[],
                     help="extra arms: the last --scheds variant with this item-order group size")
     ap.add_argument("--diag", action="store_true",
-                    help="NT only: DIAG build's per-wave cycle split (step waits / bodies / epilogues), s_memtime")
+                    help="NT / TN (32x32x16): DIAG build's per-wave cycle split (step waits / bodies / epilogues), s_memtime")
     ap.add_argument("--ablate", type=int, nargs="*", default=[],
                     help="extra v4 arms with timing-only ablations (bits: 1 no stores, 2 zero operands, 4 no DMA wait, 8 no step barrier)")
     ap.add_argument("--cold", action="store_true", help="flush the caches before every timed call")
@@ -153,7 +153,7 @@ def main():
                   flush=True)
             if a.check_only:
                 continue
-            for dmode in ((16, 17, 32) if a.diag and layout == "nt" else ()):
+            for dmode in ((16, 17, 32) if a.diag and layout in ("nt", "tn") else ()):
                 d = torch.zeros(256 * 4 * 4, dtype=torch.int64, device="cuda")
                 C.gemm4_diag(d)
                 set_variant(1)
@@ -175,6 +175,8 @@ def main():
                     print(f"{layout} {name} DIAG: no 256-wide launch for this shape", flush=True)
                     continue
                 tiles = ((M + 255) // 256) * ((N + 255) // 256)
+                if layout == "tn":   # items = tiles x K-splits
+                    tiles *= max(1, C.gemm_tn_splits(M, N, K)) if hasattr(C, "gemm_tn_splits") else 1
                 per = tiles / (v.shape[0] / 4)
                 tot = v[:, :3].sum(1)
                 clk = (v[:, :3].sum(1).max().item()) / (wall_ms * 1e-3) / 1e9   # longest wave's cycles / wall
