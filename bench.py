@@ -97,6 +97,7 @@ def measure(a, tp: int, world: int, dev, first: bool):
     from distributed_pytorch_from_scratch_amd.utils.dist import init_dist_env, set_seed
     from distributed_pytorch_from_scratch_amd.parallel import process_manager as pm, tp_comm
 
+    t_build = time.perf_counter()
     p = init_dist_env(rank=None, tp_size=tp, dp_size=world // tp, timeout_s=a.pg_timeout_s) if first \
         else pm.init_pgm(tp, world // tp)
     # test hooks: "raise:<rank>" | "hang:<rank>" in the pure-TP layout, "raise_head" in the
@@ -212,6 +213,9 @@ def measure(a, tp: int, world: int, dev, first: bool):
         trial[cfg] = float(dt_.item())
         i += 2
     set_cfg(min(trial, key=trial.get) if trial else default)
+    if dist.get_rank() == 0:
+        print(f"[bench] tp{tp}dp{world // tp}: model built, trial {trial or '-'} "
+              f"({time.perf_counter() - t_build:.1f} s)", file=sys.stderr, flush=True)
     for _ in range(a.warmup - i):
         loss = run(i)
         i += 1
@@ -228,6 +232,9 @@ def measure(a, tp: int, world: int, dev, first: bool):
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
+    if dist.get_rank() == 0:
+        print(f"[bench] tp{tp}dp{world // tp}: {a.steps} steps in {elapsed:.2f} s "
+              f"({time.perf_counter() - t_build:.1f} s since the build)", file=sys.stderr, flush=True)
     res = dict(
         value=gb * T * a.steps / elapsed, elapsed=elapsed, gb=gb, T=T, args=args,
         parallelism=f"tp{tp}" + (f"dp{p.dp_size}" if p.dp_size > 1 else "") + ("+sp" if sp_used else ""),

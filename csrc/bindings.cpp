@@ -460,7 +460,8 @@ static float* dbias_out(const c10::optional<torch::Tensor>& db, int64_t n, const
 // dx = RMSNorm'(dy) (+ dres); with `dbias` also the column sums of dx (the bias grad of the
 // projection whose output gradient dx is), from the same pass.
 std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor rstd,
-                                       c10::optional<torch::Tensor> dres, c10::optional<torch::Tensor> dbias) {
+                                       c10::optional<torch::Tensor> dres, c10::optional<torch::Tensor> dbias,
+                                       c10::optional<torch::Tensor> dw_out) {
   const int dt = check_norm_x(x, w);
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.is_contiguous() && dy.scalar_type() == x.scalar_type(), "rmsnorm_bwd: dy");
   const void* rp = nullptr;
@@ -473,7 +474,15 @@ std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch:
   const int64_t M = x.size(0), D = x.size(1);
   float* db = dbias_out(dbias, x.size(1), "rmsnorm_bwd");
   auto dx = torch::empty_like(x);
-  auto dw = torch::empty({D}, w.options());
+  torch::Tensor dw;
+  if (dw_out.has_value() && dw_out->defined()) {   // the weight gradient straight into its slot
+    dw = *dw_out;
+    TORCH_CHECK(dw.scalar_type() == torch::kFloat32 && dw.is_contiguous() && dw.numel() == D &&
+                    dw.device() == x.device(),
+                "rmsnorm_bwd: dw_out must be contiguous fp32 [D] on the device of x");
+  } else {
+    dw = torch::empty({D}, w.options());
+  }
   if (M == 0) {
     if (db) dbias->zero_();
     return {dx, dw.zero_()};
@@ -1280,7 +1289,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("add_rmsnorm_fwd", &add_rmsnorm_fwd, py::arg("y"), py::arg("bias"), py::arg("res"), py::arg("w"),
         py::arg("eps"));
   m.def("rmsnorm_bwd", &rmsnorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("rstd"),
-        py::arg("dres") = py::none(), py::arg("dbias") = py::none());
+        py::arg("dres") = py::none(), py::arg("dbias") = py::none(), py::arg("dw_out") = py::none());
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("swiglu_fwd", &swiglu_fwd, py::arg("gu"), py::arg("perm") = false);

@@ -48,6 +48,10 @@ from ..parallel import process_manager as pm
 from ..parallel import tp_comm
 
 
+# A/B hook for tools/ab_attr.py, not a user switch: False keeps the two-pass CE at TP 1.
+CE_ONE_PASS = True
+
+
 def _ar(t: torch.Tensor):
     """Async TP all-reduce (RCCL or the xGMI peer-memory kernels: ``parallel/tp_comm.py``)."""
     p = pm.pgm
@@ -271,7 +275,7 @@ class DecoderTrainFn(torch.autograd.Function):
         # logits as the statistics (k.ce_fused), so backward does not read them again.
         losses_sum = torch.zeros((), device=dev, dtype=torch.float32)
         n_valid_total = torch.zeros((), device=dev, dtype=torch.float32)
-        fuse_ce = tp == 1 and getattr(model, "_ce_unit_grad", False) and hasattr(k, "ce_fused")
+        fuse_ce = CE_ONE_PASS and tp == 1 and getattr(model, "_ce_unit_grad", False) and hasattr(k, "ce_fused")
         if fuse_ce:
             n_valid_all = (tgt != ignore_index).sum().float().clamp_min(1.0)
         for s in st:
@@ -419,7 +423,8 @@ class DecoderTrainFn(torch.autograd.Function):
             _wait(s["bh"])
             Lt, Gt = layers[-1], gl[nL - 1]
             dbd = first(Gt, "bd", s["dpend"], s["dpend"].size(1)) if Lt.bd is not None else None
-            dxf, dsf = k.rmsnorm_bwd(s["dpend"], s["xf"], model.norm.scale, s["rf"], None, dbd)
+            dxf, dsf = k.rmsnorm_bwd(s["dpend"], s["xf"], model.norm.scale, s["rf"], None, dbd,
+                                     dw_out=first(g, "nf", s["xf"], s["xf"].size(1)))
             if dbd is not None:   # bias grad of the last layer's down projection, same pass
                 Gt["bd"] = _addg(Gt.get("bd"), dbd, V(Gt, "bd"))
                 s["bd_done"] = True
@@ -486,7 +491,8 @@ class DecoderTrainFn(torch.autograd.Function):
                 a = s["layers"][li]
                 _wait(s["bh"])
                 dbo = first(G, "bo", s["dpend"], s["dpend"].size(1)) if L.bo is not None else None
-                g2, ds2 = k.rmsnorm_bwd(s["dpend"], a["x2"], L.s2, a["r2"], s["g"], dbo)  # + residual grad, bo grad
+                g2, ds2 = k.rmsnorm_bwd(s["dpend"], a["x2"], L.s2, a["r2"], s["g"], dbo,   # + residual grad, bo grad
+                                        dw_out=first(G, "s2", a["x2"], a["x2"].size(1)))
                 G["s2"] = _addg(G.get("s2"), ds2, V(G, "s2"))
                 if dbo is not None:
                     G["bo"] = _addg(G.get("bo"), dbo, V(G, "bo"))
@@ -552,7 +558,8 @@ def _finish_norm1(k, s, L, G, li, below=None, V=None):
         db = view(Gb, "bd") if Gb.get("bd") is None else None
         if db is None:
             db = s["g"].new_empty(s["g"].size(1), dtype=torch.float32)
-    s["g"], ds1 = k.rmsnorm_bwd(s["dpend"], a["x"], L.s1, a["r1"], s["g"], db)   # fused residual-grad add
+    dw = view(G, "s1") if G.get("s1") is None else None      # the first chunk: straight into its slot
+    s["g"], ds1 = k.rmsnorm_bwd(s["dpend"], a["x"], L.s1, a["r1"], s["g"], db, dw_out=dw)   # + residual grad
     if db is not None:
         below[0]["bd"] = _addg(below[0].get("bd"), db, view(below[0], "bd"))
         s["bd_done"] = True

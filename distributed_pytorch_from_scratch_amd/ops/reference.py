@@ -97,9 +97,11 @@ def rmsnorm_fwd(x: torch.Tensor, w: torch.Tensor, eps: float) -> Tuple[torch.Ten
 
 
 def rmsnorm_bwd(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, rstd: torch.Tensor,
-                dres: Optional[torch.Tensor] = None, dbias: Optional[torch.Tensor] = None):
+                dres: Optional[torch.Tensor] = None, dbias: Optional[torch.Tensor] = None,
+                dw_out: Optional[torch.Tensor] = None):
     """Returns (dx [+ dres if given, fused residual-grad add], dw fp32); with ``dbias`` (fp32
-    [D]) also writes the column sums of dx there (the bias grad of the layer below)."""
+    [D]) also writes the column sums of dx there (the bias grad of the layer below); with
+    ``dw_out`` (fp32 [D]) dw is written there and returned."""
     xf, dyf, wf = x.float(), dy.float(), w.float()
     xhat = xf * rstd[:, None]
     dw = (dyf * xhat).sum(0)
@@ -110,6 +112,8 @@ def rmsnorm_bwd(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, rstd: torch.
         dx = dx + dres.float()
     if dbias is not None:
         dbias.copy_(dx.sum(0))
+    if dw_out is not None:
+        dw = dw_out.copy_(dw)
     return dx.to(x.dtype), dw
 
 

@@ -405,7 +405,12 @@ def _comm(t: torch.Tensor, p, op: str, nbytes: Optional[int] = None):
         return None
     key = id(p.tp_group)
     if key not in _decisions:
+        t0 = time.perf_counter()
         _decisions[key] = _decide(t, p)
+        if p.global_rank == 0 and os.environ.get("DPFS_QUIET") != "1":
+            tr = (_info.get(key) or {}).get("transport")
+            print(f"[dpfs] TP collectives decided in {time.perf_counter() - t0:.1f} s: {tr}", file=sys.stderr,
+                  flush=True)
     ch = _decisions[key]
     return None if ch is None else ch.route(op, t.numel() * t.element_size() if nbytes is None else nbytes)
 

@@ -42,12 +42,19 @@ def test_bench_n_ranks_on_one_gpu(n, layouts):
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
            "--gpus", str(n), "--layers", "1", "--seq-len", "128", "--batch-per-gpu", "2", "--steps", "2",
            "--warmup", "2", "--pure-tp-budget-s", "120"]
+    # the ranks' output goes to a log file as it comes (gpurun_out/ on the GPU box: a run that
+    # prints nothing for minutes is taken to be hung), read back afterwards
+    logdir = os.path.join(ROOT, "gpurun_out") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else None
+    log = os.path.join(logdir or "/tmp", f"rehearsal_n{n}.log")
     t0 = time.time()
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=290)
+    with open(log, "w") as f:
+        rc = subprocess.run(cmd, cwd=ROOT, env=env, stdout=f, stderr=subprocess.STDOUT, text=True,
+                            timeout=290).returncode
     wall = time.time() - t0
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout[-3000:]
+    out = open(log).read()
+    assert rc == 0, out[-6000:]
+    lines = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out[-3000:]
     d = lines[0]
     if os.environ.get("DPFS_REHEARSAL_OUT"):     # keep the lines (profiles/ record of the rehearsal)
         with open(os.environ["DPFS_REHEARSAL_OUT"], "a") as f:
