@@ -61,10 +61,26 @@ class XgmiComm:
         self.cap = cap
         self.timeout_s = timeout_s
         self.nslots = 4 if nslots is None else nslots
-        self.h, handle = C.xgmi_create(self.rank, self.world, cap, self.nslots)
+        # Every step below is agreed on by the whole group, so a rank whose allocation or peer
+        # mapping fails makes every rank raise together (tp_comm._build then drops xGMI on all
+        # of them) instead of leaving the others blocked in the next collective.
+        self.h, err = 0, ""
+        try:
+            self.h, handle = C.xgmi_create(self.rank, self.world, cap, self.nslots)
+        except Exception as e:   # noqa: BLE001
+            handle, err = b"", f"{type(e).__name__}: {e}"
         handles: List[Optional[bytes]] = [None] * self.world
         dist.all_gather_object(handles, handle, group=group)
-        C.xgmi_open(self.h, b"".join(handles))
+        if not all(handles):
+            self._abort(f"xGMI buffers could not be allocated on every rank ({err or 'a peer failed'})")
+        try:
+            C.xgmi_open(self.h, b"".join(handles))
+        except Exception as e:   # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"
+        ok = torch.tensor([0.0 if err else 1.0], device="cuda" if dist.get_backend(group) == "nccl" else "cpu")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+        if ok.item() == 0:
+            self._abort(f"xGMI peer buffers could not be mapped on every rank ({err or 'a peer failed'})")
         blocks = blocks or int(os.environ.get("DPFS_XGMI_BLOCKS", "32"))
         C.xgmi_set_blocks(self.h, blocks)
         self._blocks = blocks
@@ -79,6 +95,12 @@ class XgmiComm:
         self._slots = [C.xgmi_slot_tensor(self.h, i, cap, dev) for i in range(self.nslots)]
         self.one_shot_cap = int(C.xgmi_one_shot_capacity(self.h))
         dist.barrier(group=group)
+
+    def _abort(self, why: str):
+        if self.h:
+            self.C.xgmi_destroy(self.h)
+            self.h = 0
+        raise RuntimeError(why)
 
     # ------------------------------------------------------------------------ core ----
     def staging(self, slot: int, shape, dtype: torch.dtype) -> Optional[torch.Tensor]:
