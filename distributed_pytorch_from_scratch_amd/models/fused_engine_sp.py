@@ -66,7 +66,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
     def forward(ctx, model, ids, pos, tgt, chunks: int, ignore_index: int, *params):
         dev = ids.device
         dt = model.act_dtype(dev)
-        k = K(model.embedding.weight)
+        k = K(model.embedding.weight, model.act_dtype(model.embedding.weight.device))
         p = pm.pgm
         n = p.tp_size
         B, T = ids.shape
@@ -164,7 +164,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
     def backward(ctx, gloss):
         model, st, layers = ctx.model, ctx.st, ctx.layers
         T, dt, vst, vvalid, n = ctx.meta
-        k = K(model.embedding.weight)
+        k = K(model.embedding.weight, model.act_dtype(model.embedding.weight.device))
         head = model.lm_head
         W = lambda w: shadow(w, dt) if w is not None else None
         F8.activate(ctx.f8map)

@@ -120,7 +120,7 @@ def decode_step(model, ids: torch.Tensor, pos: torch.Tensor, cache: KVCache):
     B = ids.size(0)
     dev = ids.device
     dt = model.act_dtype(dev)
-    k = K(model.embedding.weight)
+    k = K(model.embedding.weight, dt)
     W = lambda w: shadow(w, dt) if w is not None else None
     model.embedding.out_dtype = dt
     x = model.embedding(ids).reshape(B, -1).to(dt)

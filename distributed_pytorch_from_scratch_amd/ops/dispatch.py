@@ -1,7 +1,8 @@
 """Device -> kernel-set selection.
 
 ``K(t)`` returns the module implementing the kernel API for tensor ``t``: the native HIP
-extension for GPU tensors (loud failure if it is not built), ``reference`` for CPU tensors.
+extension for GPU tensors (loud failure if it is not built), ``reference`` for CPU tensors and
+for fp32 compute on the GPU.
 Both expose identical function names/signatures (see ``ops/reference.py``).
 """
 from __future__ import annotations
@@ -11,8 +12,13 @@ import torch
 from . import _ext, reference
 
 
-def K(t: torch.Tensor):
-    if t.is_cuda:
+def K(t: torch.Tensor, dtype: "torch.dtype | None" = None):
+    """Kernel set for tensor ``t`` computed in ``dtype`` (default: ``t.dtype``): the native
+    HIP extension for bf16 / fp16 / integer work on the GPU, ``reference`` on the CPU and for
+    fp32 compute on the GPU -- the reference's default fp32 training (``train.py`` without
+    ``--bf16``, ``/root/reference/train.py:58-63``) runs the fp32 PyTorch oracle on the
+    device, the MFMA kernels being bf16-in / fp32-accumulate."""
+    if t.is_cuda and (dtype or t.dtype) != torch.float32:
         return _ext.require()
     return reference
 

@@ -254,7 +254,7 @@ def attach_fused(parent: nn.Module, attr: str, fused: "FusedColumnParallelLinear
 class _VocabEmbeddingFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, weight, vocab_start: int, out_dtype):
-        k = K(weight)
+        k = K(weight, out_dtype)
         out = k.embedding_fwd(ids, weight, vocab_start, out_dtype)
         ctx.save_for_backward(ids)
         ctx.meta = (weight.size(0), vocab_start, weight.dtype)

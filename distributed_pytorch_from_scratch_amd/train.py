@@ -69,7 +69,9 @@ def get_train_args(argv=None) -> Namespace:
     g.add_argument("--save_dir", type=str, default="./checkpoints")
     g.add_argument("--reserv_last_n_ckpts", type=int, default=-1)
     g.add_argument("--batch_size", "-b", type=int, default=32)
-    g.add_argument("--bf16", action="store_true", help="bf16 compute (always on for the GPU kernels)")
+    g.add_argument("--bf16", action="store_true",
+                   help="bf16 compute on the MI355X MFMA kernels (default fp32, as the reference: on the GPU the "
+                        "fp32 PyTorch kernel set)")
     g.add_argument("--fp8", action="store_true",
                    help="fp8 (e4m3 / e5m2) GEMMs for the large projections (ops/fp8.py); bf16 elsewhere")
     g.add_argument("--max_grad_norm", type=float, default=None)
@@ -105,9 +107,13 @@ def train(rank, args: Namespace):
         p = init_dist_env(args, rank, world_size=world, backend=_backend(use_cuda))
     grank = dist.get_rank()
     dev = torch.device("cuda", torch.cuda.current_device()) if use_cuda else torch.device("cpu")
-    compute_dtype = torch.bfloat16 if (use_cuda or args.bf16) else torch.float32
+    # the reference's flag semantics (train.py:58-63): fp32 unless --bf16.  On the GPU, fp32
+    # runs the fp32 PyTorch kernel set (ops.dispatch.K); --bf16 runs the MI355X MFMA kernels.
+    compute_dtype = torch.bfloat16 if args.bf16 else torch.float32
     log0 = (lambda *a_: print(*a_, flush=True)) if grank == 0 else (lambda *a_: None)
     log0(f"{'Enable' if compute_dtype == torch.bfloat16 else 'Disable'} bf16 training  [{p}]")
+    if use_cuda and compute_dtype == torch.float32:
+        log0("fp32 on the GPU: the fp32 PyTorch kernels (numerics reference); pass --bf16 for the MFMA kernels")
 
     margs = replace(get_preset(args.model), sequence_parallel=args.sp, fp8=getattr(args, "fp8", False))
     seq_len = args.seq_len or margs.maxlen

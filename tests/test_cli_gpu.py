@@ -64,7 +64,7 @@ def test_tp2_train_eval_decode_merge_cli(tmp_path):
     _progressions(data)
     ck = tmp_path / "ck"
     env = {"DPFS_BACKEND": "gloo", "DPFS_TP_COMM": "xgmi"}
-    r = _run(["train.py", "--tp_size", "2", "--data_path", str(data), "--model", "plumbing", "-b", "16",
+    r = _run(["train.py", "--tp_size", "2", "--data_path", str(data), "--model", "plumbing", "-b", "16", "--bf16",
               "--max_steps", "150", "--warmup_steps", "10", "--lr", "3e-3", "--log_interval", "50",
               "--save_interval", "150", "--save_dir", str(ck), "--master_port", _free_port()], env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

@@ -1,0 +1,43 @@
+"""fp32 training on the GPU (the reference's default without --bf16, /root/reference/train.py:
+58-63): the engines run the fp32 PyTorch kernel set on the device (ops.dispatch.K with an fp32
+compute dtype), and TP stays numerically transparent -- the SURVEY §0 invariant checked on the
+MI355X: TP = 1 / 2 / 4 (and SP) losses over Adam steps equal the vanilla fp32 model's on the
+CPU to 2e-5.  Ranks share one GPU over gloo."""
+import pytest
+import torch
+
+from dist_helpers import run_distributed
+from test_model_tp_equivalence import CFG, _batch, _train_vanilla
+
+pytestmark = pytest.mark.gpu
+
+
+def _train_gpu(rank, world, cfg, steps, sp):
+    torch.cuda.set_device(0)
+    from distributed_pytorch_from_scratch_amd.models import Transformer, ModelArgs
+    from distributed_pytorch_from_scratch_amd.utils.dist import set_seed
+    m = Transformer.from_args(ModelArgs(**cfg, vocab_pad_to=1, sequence_parallel=sp))
+    set_seed(0)
+    m.reset_parameters()            # on the CPU: the vanilla model's RNG order
+    m = m.cuda().set_compute_dtype(torch.float32)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    losses = []
+    for s in range(steps):
+        ids, pos, tgt = (t.cuda() for t in _batch(cfg["vocab_size"], 2, 16, seed=100 + s))
+        loss = m.loss(ids, pos, tgt)
+        opt.zero_grad()
+        loss.backward()
+        if sp:
+            from distributed_pytorch_from_scratch_amd.parallel.grad_sync import allreduce_sequence_parallel_grads
+            allreduce_sequence_parallel_grads(m)
+        opt.step()
+        losses.append(loss.item())
+    return losses
+
+
+@pytest.mark.parametrize("world,sp", [(1, False), (2, False), (4, False), (2, True)])
+def test_fp32_gpu_tp_transparent(world, sp):
+    van, _ = _train_vanilla(CFG, 3)
+    res = run_distributed(_train_gpu, world, CFG, 3, sp, timeout=240)
+    for r in range(world):
+        assert torch.allclose(torch.tensor(res[r]), torch.tensor(van), atol=2e-5), (res[r], van)

@@ -150,7 +150,7 @@ def test_train_cli_on_gpu(tmp_path):
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, "train.py", "--tp_size", "1", "--synthetic", "--model", "reference",
-                        "--seq_len", "256", "-b", "8", "--max_steps", "20", "--log_interval", "10",
+                        "--seq_len", "256", "-b", "8", "--bf16", "--max_steps", "20", "--log_interval", "10",
                         "--save_interval", "20", "--save_dir", str(tmp_path), "--master_port", "29577"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

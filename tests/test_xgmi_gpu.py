@@ -112,3 +112,41 @@ def test_engine_over_xgmi_follows_single_rank(monkeypatch, world, sp, rc):
         for a, b in zip(losses, ref):
             assert abs(a - b) < 2e-2 * max(1.0, abs(b)), (r, losses, ref)
     assert len({tuple(v) for v in res.values()}) == 1
+
+
+def _setup_failure(rank, world, where):
+    """One rank's allocation (``create``) or peer mapping (``open``) fails: every rank must raise
+    (no rank left blocked in the next collective), and tp_comm's builder drops xGMI everywhere."""
+    torch.cuda.set_device(0)
+    from distributed_pytorch_from_scratch_amd.ops import _ext
+    from distributed_pytorch_from_scratch_amd.parallel import process_manager as pm, tp_comm
+    from distributed_pytorch_from_scratch_amd.parallel.xgmi import XgmiComm
+    C = _ext.require()
+
+    class Faulty:   # the native module with one entry point failing on rank 1
+        def __getattr__(self, name):
+            f = getattr(C, name)
+            if name == f"xgmi_{where}" and rank == 1:
+                def fail(*a, **k):
+                    raise RuntimeError(f"injected {name} failure")
+                return fail
+            return f
+    real = _ext.require
+    _ext.require = lambda: Faulty()
+    try:
+        try:
+            XgmiComm(pm.pgm.tp_group, cap_bytes=1 << 20, timeout_s=10.0)
+            raised = False
+        except RuntimeError as e:
+            raised = "every rank" in str(e)
+        built = tp_comm._build("xgmi", pm.pgm.tp_group, forced=False)
+    finally:
+        _ext.require = real
+    return dict(raised=raised, built=built is not None)
+
+
+@pytest.mark.parametrize("where", ["create", "open"])
+def test_xgmi_setup_failure_is_group_consistent(where):
+    res = run_distributed(_setup_failure, 2, where, tp_size=2, timeout=120)
+    assert all(v["raised"] for v in res.values()), res
+    assert not any(v["built"] for v in res.values()), res
