@@ -209,6 +209,21 @@ class DecoderTrainFnSP(torch.autograd.Function):
                     i += 1
             pairs.clear()
 
+        def tn_multi(d, groups):
+            """A phase's weight gradients ((key, pairs) each): with one chunk ONE grouped launch
+            (GS.gemm_tn_group, timed against separate calls), else per key."""
+            if all(len(pairs) == 1 for _, pairs in groups):
+                items = []
+                for key, pairs in groups:
+                    acc = d.get(key)
+                    items.append((pairs[0][0], pairs[0][1], acc if acc is not None else V(d, key), acc is not None))
+                for (key, pairs), o in zip(groups, GS.gemm_tn_group(k, items)):
+                    d[key] = o
+                    pairs.clear()
+                return
+            for key, pairs in groups:
+                tn_chunks(d, key, pairs)
+
         pg = pm.pgm
         dp = pg.dp_size
         # buckets of at least the measured knee of the DP group's all-reduce curve
@@ -294,8 +309,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 if dbgu is not None:
                     G["bgu"] = _addg(G.get("bgu"), dbgu, V(G, "bgu"))
                 del a["sw"], a["gu"], a["h2"], s["gfull"]
-            tn_chunks(G, "wd", wd_p)       # under the chunks' reduce-scatters
-            tn_chunks(G, "wgu", wgu_p)
+            tn_multi(G, [("wd", wd_p), ("wgu", wgu_p)])       # under the chunks' reduce-scatters
             for s in st:    # B3: norm2 backward (+ residual grad) on my rows -> all-gather
                 _wait(s["h"])
                 a = s["layers"][li]
@@ -323,8 +337,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 for key in ("qkv", "o", "lse", "h1"):
                     a.pop(key, None)
                 del s["gfull"]
-            tn_chunks(G, "wo", wo_p)
-            tn_chunks(G, "wqkv", wqkv_p)
+            tn_multi(G, [("wo", wo_p), ("wqkv", wqkv_p)])
             for s in st:    # B1: norm1 backward (+ residual grad) on my rows -> all-gather
                 _wait(s["h"])
                 a = s["layers"][li]
