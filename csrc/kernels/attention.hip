@@ -1194,7 +1194,8 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
     const float* __restrict__ LSN, const float* __restrict__ NDEL, bf16* __restrict__ dK, bf16* __restrict__ dV,
     int T, int H, int BH, long long ldq, long long ldk, long long ldv, long long lddo, long long lddk,
     long long lddv, float scale, int causal, const int64_t* __restrict__ rpos, const float* __restrict__ rtab,
-    float* __restrict__ BPK, float* __restrict__ BPV, unsigned long long* __restrict__ diag = nullptr) {
+    float* __restrict__ BPK, float* __restrict__ BPV, unsigned long long* __restrict__ diag = nullptr,
+    int prefetch = 1) {
   // LSN = -lse / scale and NDEL = -delta per query row (written by attn_bwd_dq3_k).  BPK / BPV
   // (optional): per (b, h, key block, wave) column sums of the stored dK / dV rows.
   static_assert(HD == 64 || HD == 128, "dK/dV v3: head_dim 64 or 128");
@@ -1236,6 +1237,32 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
 
   unsigned long long d_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, d_t0 = 0, d_start = 0;
   if constexpr (DIAG) d_start = stamp_dep(0.f);
+  // The ring position runs on across the two key blocks: during the first block's last two
+  // query tiles the second block's first two Q / dO tiles are fetched into the slots the
+  // first block no longer needs, and its K / V rows into the K / V registers once the last
+  // tile's S / dP MFMAs have consumed them -- the second block starts with its operands in
+  // flight or landed instead of a cold prologue.
+  const int kb1 = nkb - 1 - p;                       // the second key block (== p: none)
+  const int qstart1 = causal ? ((kb1 * BK) / BQ) * BQ : 0;
+  const int nq1 = (T - qstart1 + BQ - 1) / BQ;
+  const int key1 = kb1 * BK + 32 * wave + r32;
+  const int nq0 = (T - (causal ? ((p * BK) / BQ) * BQ : 0) + BQ - 1) / BQ;
+  // (head_dim 64 only: at 128 the one-wave-per-SIMD kernel has no register to spare for it)
+  const bool pre = HD == 64 && prefetch && kb1 != p && nq1 > 0 && nq0 >= 2;  // (uniform)
+  bf16x8 kf[KS], vf[KS];
+  auto load_kv = [&](int kk_) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 a_ = {}, c_ = {};
+      if (kk_ < T) {
+        a_ = *reinterpret_cast<const bf16x8*>(K + ((long long)b * T + kk_) * ldk + (long long)h * HD + 16 * ks + 8 * hf);
+        c_ = *reinterpret_cast<const bf16x8*>(V + ((long long)b * T + kk_) * ldv + (long long)h * HD + 16 * ks + 8 * hf);
+      }
+      kf[ks] = a_;
+      vf[ks] = c_;
+    }
+  };
+  int cur = 0;
   for (int sub = 0; sub < 2; ++sub) {
     const int kb = sub == 0 ? p : nkb - 1 - p;
     if (sub == 1 && kb == p) break;
@@ -1244,19 +1271,13 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
     const int k0 = kb * BK, kw0 = k0 + 32 * wave, key = kw0 + r32;
     const int qstart = causal ? (k0 / BQ) * BQ : 0;
     const int nq = (T - qstart + BQ - 1) / BQ;
-    if (nq > 0) dma.issue(qbase, dobase, lsb, dlb, ldq, lddo, T, qstart, smem);
-    if (nq > 1) dma.issue(qbase, dobase, lsb, dlb, ldq, lddo, T, qstart + BQ, smem + BUF);
-    // K^T / V^T operands (B of S = Q K^T, dP = dO V^T): lane holds K[key][16 ks + 8 hf + j]
-    bf16x8 kf[KS], vf[KS];
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      bf16x8 a = {}, c = {};
-      if (key < T) {
-        a = *reinterpret_cast<const bf16x8*>(K + ((long long)b * T + key) * ldk + (long long)h * HD + 16 * ks + 8 * hf);
-        c = *reinterpret_cast<const bf16x8*>(V + ((long long)b * T + key) * ldv + (long long)h * HD + 16 * ks + 8 * hf);
-      }
-      kf[ks] = a;
-      vf[ks] = c;
+    const bool fetched = sub == 1 && pre;   // tiles 0 / 1 and K / V already on their way
+    if (!fetched) {
+      const int c1 = cur + 1 == NST ? 0 : cur + 1;
+      if (nq > 0) dma.issue(qbase, dobase, lsb, dlb, ldq, lddo, T, qstart, smem + cur * BUF);
+      if (nq > 1) dma.issue(qbase, dobase, lsb, dlb, ldq, lddo, T, qstart + BQ, smem + c1 * BUF);
+      // K^T / V^T operands (B of S = Q K^T, dP = dO V^T): lane holds K[key][16 ks + 8 hf + j]
+      load_kv(key);
     }
     wait_vmcnt<0>();
     if constexpr (DIAG) d_acc[6] += stamp_dep(__builtin_bit_cast(float, __builtin_bit_cast(u32x4, vf[KS - 1])[3])) - d_t0;
@@ -1268,10 +1289,10 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
         dkt[d][i] = 0.f;
         dvt[d][i] = 0.f;
       }
-    int cur = 0;
+    const bool ahead = sub == 0 && pre;   // this block prefetches the next one's first tiles
     for (int t = 0; t < nq; ++t) {
       if constexpr (DIAG) d_t0 = stamp_dep(0.f);
-      if (t + 1 < nq) wait_vmcnt<PWV>();
+      if (t + 1 < nq || ahead) wait_vmcnt<PWV>();   // (younger: tile t+1's or the next block's tile 0)
       else wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
       if constexpr (DIAG) {
@@ -1288,7 +1309,12 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
       cur = (cur + 1 == NST) ? 0 : cur + 1;
       const int q0 = qstart + t * BQ;
       if (t + 2 < nq) dma.issue(qbase, dobase, lsb, dlb, ldq, lddo, T, q0 + 2 * BQ, smem + nb * BUF);
-      if (causal && q0 + BQ - 1 < kw0) continue;   // wave-uniform: every query of the tile < every key
+      else if (ahead && t + 2 - nq < nq1)   // the next block's tile t + 2 - nq (0 or 1)
+        dma.issue(qbase, dobase, lsb, dlb, ldq, lddo, T, qstart1 + (t + 2 - nq) * BQ, smem + nb * BUF);
+      if (causal && q0 + BQ - 1 < kw0) {   // wave-uniform: every query of the tile < every key
+        if (ahead && t == nq - 1) load_kv(key1);
+        continue;
+      }
       if constexpr (DIAG) d_acc[7] += 1;
       constexpr int NH = 2 * DTN * 4;
       s16x4 th[(NH + 15) / 16 * 16];
@@ -1349,6 +1375,8 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
           sc[0][i] = __builtin_amdgcn_exp2f(sc[0][i] * c2);
         __builtin_amdgcn_sched_barrier(0);
       }
+      // the block's last tile: K / V are consumed, load the next block's
+      if (ahead && t == nq - 1) load_kv(key1);
       if constexpr (DIAG) {
         const unsigned long long t1 = stamp_dep(sc[0][15] + dp[1][15]);
         d_acc[1] += t1 - d_t0;
@@ -2003,6 +2031,10 @@ extern "C" int dpfs_attn_supported_hd(int hd) { return hd == 32 || hd == 64 || h
 // read only by a call that asks for a DIAG build.
 static unsigned long long* g_attn_diag = nullptr;
 extern "C" void dpfs_attn_diag(void* p) { g_attn_diag = (unsigned long long*)p; }
+// dK/dV (head_dim 64): 1 = the second key block's first tiles / K / V fetched during the first
+// block's last tiles (default), 0 = a cold prologue per block (A/B probes)
+static int g_attn_prefetch = 1;
+extern "C" void dpfs_attn_prefetch(int v) { g_attn_prefetch = v ? 1 : 0; }
 
 extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int T, int H,
                               int hd, long long ldq, long long ldk, long long ldv, long long ldo, float scale,
@@ -2073,7 +2105,7 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
   attn_bwd_dkdv3_k<HD_, DG_><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, \
                                                    delta + (long long)B * H * T, delta, (bf16*)dk, (bf16*)dv, T, H,     \
                                                    B * H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal, rope_pos,     \
-                                                   rope_tab, pk, pv, DG_ ? g_attn_diag : nullptr)
+                                                   rope_tab, pk, pv, DG_ ? g_attn_diag : nullptr, g_attn_prefetch)
     if (hd == 64 && diag) DKDV3_LAUNCH(64, 1);
     else if (hd == 64) DKDV3_LAUNCH(64, 0);
     else DKDV3_LAUNCH(128, 0);
