@@ -87,7 +87,10 @@ def init_dist_env(args: Optional[Namespace] = None, rank: Optional[int] = None, 
         # RCCL collectives on a high-priority HIP stream: they overlap the other ping-pong
         # chunk's compute and are on its critical path.
         opts = dist.ProcessGroupNCCL.Options()
-        opts.is_high_priority_stream = True     # (the timeout is the init_process_group kwarg)
+        opts.is_high_priority_stream = True
+        # the timeout is the init_process_group kwarg; the options object carries the same value
+        # (torch warns whenever the two differ, and Options() defaults to its own)
+        opts._timeout = datetime.timedelta(seconds=timeout_s)
         kw["pg_options"] = opts
     elif os.environ.get("DPFS_BACKEND") == "gloo" and torch.cuda.is_available():
         torch.cuda.set_device(local_rank % torch.cuda.device_count())

@@ -4,8 +4,12 @@ import torch
 from distributed_pytorch_from_scratch_amd.ops import _ext
 
 C = _ext.require()
+import sys
 SHAPES = [("qkv", 2304, 768, 32768), ("wo", 768, 768, 32768), ("gateup", 4096, 768, 32768),
           ("down", 768, 2048, 32768), ("lmhead", 50304, 768, 32768)]
+if "--llama7b" in sys.argv:   # LLaMA-2-7B shape, seq 4096 x batch 2 = 8192 tokens
+    SHAPES = [("qkv", 12288, 4096, 8192), ("wo", 4096, 4096, 8192), ("gateup", 22016, 4096, 8192),
+              ("down", 4096, 11008, 8192), ("lmhead", 32000, 4096, 8192)]
 
 
 def t(fn, reps=20):
