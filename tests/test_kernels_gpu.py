@@ -857,13 +857,13 @@ def test_gemm_v4_split_k_bf16_long_k(C):
 
 
 
-@pytest.mark.parametrize("M,K", [(4096, 768), (300, 256)])
-def test_gemm_nt_column_slice_out(C, M, K):
+@pytest.mark.parametrize("M,K,H,hd", [(4096, 768, 12, 64), (300, 256, 12, 64), (2048, 4096, 32, 128)])
+def test_gemm_nt_column_slice_out(C, M, K, H, hd):
     """The packed QKV projection as two launches into one buffer (ops/gemm_select.gemm_nt_rope
     "ours_split"): the rotated Q|K columns (RoPE epilogue) and the V columns written through
-    row-strided column slices are bit-identical to the single fused launch."""
+    row-strided column slices are bit-identical to the single fused launch (head_dim 64, and 128
+    at the LLaMA-7B shape)."""
     torch.manual_seed(46)
-    H, hd = 12, 64
     N, rot = 3 * H * hd, 2 * H * hd
     x = (torch.randn(M, K, device=DEV) / 4).bfloat16()
     w = (torch.randn(N, K, device=DEV) / 4).bfloat16()
