@@ -489,10 +489,11 @@ __device__ __forceinline__ float dpp_quad(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), P, 0xF, 0xF, false));
 }
 
-// SWB epilogue of one item: 8 blocks of 16 rows.  Loads roll per column group jp: block i+1's
-// gate / up vectors of group jp are issued as soon as block i has consumed that group's, so one
-// set of 8 vectors is live and every wait has a static count (12 younger VMEM ops in steady
-// state).  Column sums: per block, lanes l and l + 8 of a DPP row add their values (row_ror 8);
+// SWB epilogue of one item: 8 blocks of 16 rows.  Loads roll per column group jp, SWB_D (2)
+// blocks ahead: block i+2's gate / up vectors of group jp are issued into the register set
+// block i has just consumed, so two sets of 8 vectors are live (two blocks of HBM latency
+// hidden instead of one) and every wait has a static count (swb_younger; 28 younger VMEM ops
+// in steady state).  Column sums: per block, lanes l and l + 8 of a DPP row add their values (row_ror 8);
 // lanes 0-7 of the row keep the gate sums, lanes 8-15 the up sums (32 accumulators per lane,
 // not 64); at the item's end a mirror / quad butterfly sums each 8-lane half and lanes 0 / 8 of
 // every row write the 32 + 32 column partials (fixed order: deterministic).
@@ -516,6 +517,25 @@ __device__ __forceinline__ void acc_pair(float& acc, float mine, float other) {
                : "v"(other));
 }
 
+// Row blocks of gate / up loads in flight in the SWB epilogue, and the count of VMEM ops a
+// wave issues after the two loads of step s = (block s / 4, group s % 4): the prologue loads
+// the first SWB_D blocks; step t then issues 2 stores and, while block t / 4 + SWB_D exists,
+// the 2 loads of (t / 4 + SWB_D, t % 4) into the set block t / 4 used.
+constexpr int swb_ops(int D, int t) { return 2 + (t / 4 + D <= 7 ? 2 : 0); }
+constexpr int swb_younger(int D, int s) {
+  int n = 0;
+  if (s / 4 < D) {
+    n = 8 * D - 1 - (2 * s + 1);   // prologue loads after this group's U load
+    for (int t = 0; t < s; ++t) n += swb_ops(D, t);
+  } else {
+    for (int t = s - 4 * D + 1; t < s; ++t) n += swb_ops(D, t);
+  }
+  return n;
+}
+static_assert(swb_younger(2, 0) == 14 && swb_younger(2, 31) == 14 && swb_younger(2, 12) == 28, "SWB vmcnt schedule");
+static_assert(swb_younger(1, 0) == 6 && swb_younger(1, 8) == 12 && swb_younger(1, 31) == 6, "SWB vmcnt schedule");
+
+template <int SWB_D>
 __device__ __forceinline__ void epilogue_swb(const Item& ci, int M, int F, const SwiBwd& sb, int wm, int wn, int l) {
   const int g = l >> 4;
   const int wcol0 = ci.n0 + wn * 128;
@@ -533,7 +553,8 @@ __device__ __forceinline__ void epilogue_swb(const Item& ci, int M, int F, const
   const unsigned gstride = (unsigned)sb.ldgu * 32u, dstride = (unsigned)sb.lddgu * 32u;   // 16 rows
   unsigned goff = (unsigned)row0 * (unsigned)sb.ldgu * 2u + gcol0;   // block 0, group 0 (gate)
   unsigned doff = (unsigned)row0 * (unsigned)sb.lddgu * 2u + (unsigned)c0 * 2u;
-  u32x4 G[4], U[4];
+  // gate / up vectors of the next SWB_D row blocks in flight (32 VGPRs per set)
+  u32x4 G[SWB_D][4], U[SWB_D][4];
   float acc[4][8];
 #pragma unroll
   for (int jp = 0; jp < 4; ++jp)
@@ -547,24 +568,30 @@ __device__ __forceinline__ void epilogue_swb(const Item& ci, int M, int F, const
     const int c = c0 + 32 * jp;
     return (unsigned)(((c >> 6) << 7) + (c & 63)) * 2u - gcol0;
   };
-  auto load = [&](int m, unsigned base, int jp) __attribute__((always_inline)) {
+  auto load = [&](int set, int m, unsigned base, int jp) __attribute__((always_inline)) {
     const bool ok = m < M && c0 + 32 * jp < F;
     const unsigned o = base + gdelta(jp);
-    G[jp] = ld16_asm(rg, ok ? o : kOOB);
-    U[jp] = ld16_asm(rg, ok ? o + uadd : kOOB);
+    G[set][jp] = ld16_asm(rg, ok ? o : kOOB);
+    U[set][jp] = ld16_asm(rg, ok ? o + uadd : kOOB);
   };
+  unsigned gahead = goff;   // gu offset of the next block to load
 #pragma unroll
-  for (int jp = 0; jp < 4; ++jp) load(row0, goff, jp);
+  for (int bb = 0; bb < SWB_D; ++bb) {
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) load(bb, row0 + 16 * bb, gahead, jp);
+    gahead = opaque_add(gahead, gstride);
+  }
   static_for<0, 8>([&](auto I) __attribute__((always_inline)) {
     constexpr int i = decltype(I)::value;
+    constexpr int set = i % SWB_D;
     const int m = row0 + 16 * i;
     const bool mok = m < M;
-    const unsigned gnext = i + 1 < 8 ? opaque_add(goff, gstride) : goff;
+    const unsigned gload = gahead;   // block i + SWB_D
     static_for<0, 4>([&](auto JP) __attribute__((always_inline)) {
       constexpr int jp = decltype(JP)::value;
       // VMEM ops younger than (block i, group jp)'s two loads
-      constexpr int YOUNGER = i == 0 ? 6 + 2 * jp : (i == 7 ? 12 - 2 * jp : 12);
-      pin_vm<YOUNGER>(G[jp], U[jp]);
+      constexpr int YOUNGER = swb_younger(SWB_D, 4 * i + jp);
+      pin_vm<YOUNGER>(G[set][jp], U[set][jp]);
       const f32x4 v0 = acc_read<i, 2 * jp>(), v1 = acc_read<i, 2 * jp + 1>();
       const bf16x4 o0 = {(bf16)v0[0], (bf16)v0[1], (bf16)v0[2], (bf16)v0[3]};
       const bf16x4 o1 = {(bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
@@ -573,8 +600,8 @@ __device__ __forceinline__ void epilogue_swb(const Item& ci, int M, int F, const
       const auto sy = __builtin_amdgcn_permlane16_swap(d2[1], e2[1], false, false);
       const u32x4 w = {sx[0], sy[0], sx[1], sy[1]};
       const bf16x8 dv = __builtin_bit_cast(bf16x8, w);
-      const bf16x8 gv = __builtin_bit_cast(bf16x8, G[jp]);
-      const bf16x8 uv = __builtin_bit_cast(bf16x8, U[jp]);
+      const bf16x8 gv = __builtin_bit_cast(bf16x8, G[set][jp]);
+      const bf16x8 uv = __builtin_bit_cast(bf16x8, U[set][jp]);
       bf16x8 og, ou;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -592,9 +619,9 @@ __device__ __forceinline__ void epilogue_swb(const Item& ci, int M, int F, const
       const unsigned od = doff + (unsigned)(64 * jp);
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, og), rd, ok ? od : kOOB, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ou), rd, ok ? od + (unsigned)F * 2u : kOOB, 0, 0);
-      if constexpr (i + 1 < 8) load(m + 16, gnext, jp);
+      if constexpr (i + SWB_D < 8) load(set, m + 16 * SWB_D, gload, jp);
     });
-    goff = gnext;
+    if constexpr (i + SWB_D < 8) gahead = opaque_add(gahead, gstride);
     if constexpr (i + 1 < 8) doff = opaque_add(doff, dstride);
   });
 #pragma unroll
@@ -652,7 +679,7 @@ __device__ __forceinline__ void epilogue_swb(const Item& ci, int M, int F, const
 // address / SALU work fit in the MFMA shadow (the 16x16x32 TN step issues ~1.5k cycles of
 // non-MFMA work against 1024 of matrix time).
 template <bool AK, bool BKM, int OUT, int DIAG = 0, bool FAST = false, int SCHED = 0, int BN = 256, int ROPE = 0,
-          bool SWIGLU = false, bool SWB = false, int BR = 0, int SA = 0, bool M32 = false, bool GRP = false>
+          bool SWIGLU = false, int SWB = 0, int BR = 0, int SA = 0, bool M32 = false, bool GRP = false>
 __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                   void* __restrict__ C, const float* __restrict__ bias, int M, int N,
                                                   int K, int lda, int ldb, int ldc, int kps, int splits,
@@ -991,7 +1018,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
         step(F0, F1, false, NO, NO, false, bcol0);
       }
       step(F1, F0, false, NO, std::true_type{}, true, bcol0);
-      epilogue_swb(ci, M, N, swb, wm, wn, l);
+      epilogue_swb<SWB>(ci, M, N, swb, wm, wn, l);
       read_frags<AK, BKM, BN, M32>(F0, smem + c_slot * SLOT, wm, wn, l);
       continue;
     }
@@ -1139,6 +1166,10 @@ extern "C" bool dpfs_gemm4_nt_swiglu(const void* A, const void* B, void* C, cons
 // [M, K] (K-major), B = W_down [K, F] (F contiguous), gu [M, 2F] (interleaved if perm), dgu
 // [M, 2F] natural, part [2 * ceil(M / 256), 2F] fp32 (every row written).  Returns false
 // (nothing launched) where the 256-wide FAST kernel does not apply.
+// gate / up row blocks in flight in the SWB epilogue (1 or 2; A/B hook, tools/ab_attr.py)
+static int g_g4_swb_depth = 2;
+extern "C" void dpfs_gemm4_swb_depth(int d) { g_g4_swb_depth = d == 1 ? 1 : 2; }
+
 extern "C" bool dpfs_gemm4_nn_swiglu_bwd(const void* A, const void* B, const void* gu, void* dgu, float* part, int M,
                                          int F, int K, int lda, int ldb, int ldgu, int lddgu, int perm,
                                          unsigned a_bytes, unsigned b_bytes, hipStream_t s) {
@@ -1157,9 +1188,14 @@ extern "C" bool dpfs_gemm4_nn_swiglu_bwd(const void* A, const void* B, const voi
   // no partials buffer (no bias gradient): a zero-record descriptor drops every partial store
   const SwiBwd swb = {(const bf16*)gu, (bf16*)dgu, part, ldgu, lddgu, perm ? 1 : 0, (unsigned)guspan, (unsigned)dspan,
                       part ? (unsigned)pspan : 0u};
-  gemm4_k<true, false, 0, 0, true, 1, 256, 0, false, true><<<grid, 256, 0, s>>>(
-      (const bf16*)A, (const bf16*)B, nullptr, nullptr, M, F, K, lda, ldb, F, K, 1, 0, a_bytes, b_bytes, 0u, rope,
-      g_g4_group_m, dual, 0, nullptr, SwiOut{}, swb);
+  if (g_g4_swb_depth == 1)
+    gemm4_k<true, false, 0, 0, true, 1, 256, 0, false, 1><<<grid, 256, 0, s>>>(
+        (const bf16*)A, (const bf16*)B, nullptr, nullptr, M, F, K, lda, ldb, F, K, 1, 0, a_bytes, b_bytes, 0u, rope,
+        g_g4_group_m, dual, 0, nullptr, SwiOut{}, swb);
+  else
+    gemm4_k<true, false, 0, 0, true, 1, 256, 0, false, 2><<<grid, 256, 0, s>>>(
+        (const bf16*)A, (const bf16*)B, nullptr, nullptr, M, F, K, lda, ldb, F, K, 1, 0, a_bytes, b_bytes, 0u, rope,
+        g_g4_group_m, dual, 0, nullptr, SwiOut{}, swb);
   return true;
 }
 

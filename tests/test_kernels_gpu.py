@@ -937,3 +937,11 @@ def test_gemm_nn_swiglu_bwd_epilogue(C, M, F_, K, perm):
     assert _rel(db, db2) < 1e-5
     # without a bias gradient the kernel writes no partials and the same dgu
     assert torch.equal(C.gemm_nn_swiglu_bwd(dy, w, gu, None, perm)[0], dgu)
+    # one gate / up row block in flight instead of two (the A/B hook): bit-identical
+    try:
+        C.gemm4_swb_depth(1)
+        db1 = torch.empty(2 * F_, device=DEV)
+        assert torch.equal(C.gemm_nn_swiglu_bwd(dy, w, gu, db1, perm)[0], dgu)
+        assert torch.equal(db1, db)
+    finally:
+        C.gemm4_swb_depth(2)
