@@ -30,6 +30,7 @@ void dpfs_gemm4_br(int);
 void dpfs_gemm4_m32(int);
 void dpfs_attn_prefetch(int);
 void dpfs_gemm4_swb_depth(int);
+void dpfs_gemm4_m32k(int);
 void dpfs_gemm4_group_m(int);
 void dpfs_gemm4_ablate(int);
 void dpfs_gemm4_diag(void*);
@@ -1273,6 +1274,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "dK/dV backward (head_dim 64): 1 = next key block's operands fetched ahead (default), 0 = off (A/B)");
   m.def("gemm4_swb_depth", [](int v) { dpfs_gemm4_swb_depth(v); },
         "SwiGLU-backward epilogue of the down-projection dgrad: gate / up row blocks in flight (2 default, 1 = A/B)");
+  m.def("gemm4_m32k", [](int v) { dpfs_gemm4_m32k(v); },
+        "NN / NT 256-wide main loop of the v4 GEMM: bit 0 = 32x32x16 MFMAs for the fp32 (split-K) output, bit 1 = for "
+        "the bf16 (+ bias) output, 0 = 16x16x32 (default; measured faster in the step)");
   m.def("gemm4_m32", [](int v) { dpfs_gemm4_m32(v); },
         "TN main loop of the v4 GEMM: 1 = 32x32x16 MFMAs (default), 0 = 16x16x32 (A/B probes)");
   m.def("gemm4_br", [](int v) { dpfs_gemm4_br(v); },

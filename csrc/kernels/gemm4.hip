@@ -218,6 +218,26 @@ struct Opnd32 {
   }
 };
 
+// 32x32x16 operand of a K-contiguous image ([256 rows][64 B], chunk c of row r at slot
+// c ^ kh(r)): fragment f = 2 nb + kk holds X[row 32 nb + (l & 31)][k = 16 kk + 8 (l >> 5) + j],
+// j < 8, one ds_read_b128.  kh(row) depends on row & 15 only, so block nb is +2048 bytes (an
+// immediate) from the lane's k-half offset k32_off(kk); each 16-lane group reads 16 rows of one
+// chunk, which the swizzle spreads over all 16 bank slots (as the 16x16x32 fragments).
+__device__ __forceinline__ unsigned k32_off(int rb, int kk, int l) {
+  const int r = l & 31;
+  return (unsigned)((rb + r) * 64 + (((2 * kk + (l >> 5)) ^ kh(r)) << 4));
+}
+struct Opnd32K {
+  bf16x8 v[8];
+  // fragments 2 nb and 2 nb + 1 from p0 / p1 = half-slot + k32_off(rb, 0 / 1)
+  __device__ __forceinline__ void load_nb(int nb, const char* p0, const char* p1) {
+    v[2 * nb] = *reinterpret_cast<const bf16x8*>(p0 + 2048 * nb);
+    v[2 * nb + 1] = *reinterpret_cast<const bf16x8*>(p1 + 2048 * nb);
+  }
+  __device__ __forceinline__ bf16x8 get(int f) const { return v[f]; }
+  __device__ __forceinline__ void pin() {}
+};
+
 template <bool AK, bool BKM, int BN, bool M32 = false>
 struct Frags {
   Opnd<AK> a;
@@ -227,14 +247,29 @@ template <int BN>
 struct Frags<false, false, BN, true> {
   Opnd32 a, b;
 };
+template <int BN>
+struct Frags<true, false, BN, true> {
+  Opnd32K a;
+  Opnd32 b;
+};
+template <int BN>
+struct Frags<true, true, BN, true> {
+  Opnd32K a, b;
+};
 
 template <bool AK, bool BKM, int BN, bool M32 = false>
 __device__ __forceinline__ void read_frags(Frags<AK, BKM, BN, M32>& f, const char* slot, int wm, int wn, int l) {
   if constexpr (M32) {
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) f.a.load_nb(nb, slot + m32_off(wm * 128, nb, l));
+    for (int nb = 0; nb < 4; ++nb) {
+      if constexpr (AK) f.a.load_nb(nb, slot + k32_off(wm * 128, 0, l), slot + k32_off(wm * 128, 1, l));
+      else f.a.load_nb(nb, slot + m32_off(wm * 128, nb, l));
+    }
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) f.b.load_nb(nb, slot + 16384 + m32_off(wn * 128, nb, l));
+    for (int nb = 0; nb < 4; ++nb) {
+      if constexpr (BKM) f.b.load_nb(nb, slot + 16384 + k32_off(wn * 128, 0, l), slot + 16384 + k32_off(wn * 128, 1, l));
+      else f.b.load_nb(nb, slot + 16384 + m32_off(wn * 128, nb, l));
+    }
   } else {
 #pragma unroll
     for (int i = 0; i < 8; ++i) f.a.load(i, slot, wm * 128 + 16 * i, l);
@@ -334,6 +369,47 @@ __device__ __forceinline__ void epilogue_f32_m32(const Item& ci, void* C, int M,
         const int n = col0 + 32 * bj + 8 * gg;
         const unsigned off = (mok && n < N) ? rbase + (unsigned)n * 4u : kOOB;
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc32_read<bi, bj, gg>()), rc, off, 0, 0);
+      });
+    });
+  });
+}
+
+// bf16 epilogue of the 32x32x16 accumulators (M32, OUT 0, + fp32 bias): lane l holds row l & 31
+// of each 32 x 32 block, columns 8 G + 4 h + 0..3 (h = l >> 5) in registers 4G..4G+3.  Per
+// register-group pair (2 g2, 2 g2 + 1) two v_permlane32_swap (lanes 32-63 of the first operand
+// trade with lanes 0-31 of the second) leave lane l < 32 with columns 16 g2 + 0..7 and lane
+// l + 32 with 16 g2 + 8..15: one 16-byte store each, 32 per wave (as the 16x16 form's OUT 0).
+template <bool HAS_BIAS, int SA>
+__device__ __forceinline__ void epilogue_bf16_m32(const char* bias_lds, const Item& ci, void* C, int M, int N,
+                                                  int ldc, unsigned c_bytes, int wm, int wn, int l) {
+  acc_drain();
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(C, (short)0, (int)c_bytes, 0x00020000);
+  const int h = l >> 5;
+  const int row0 = ci.m0 + wm * 128 + (l & 31);
+  const int col0 = ci.n0 + wn * 128 + 8 * h;
+  static_for<0, 4>([&](auto I) {
+    constexpr int bi = decltype(I)::value;
+    const int m = row0 + 32 * bi;
+    const bool mok = m < M;
+    const unsigned rbase = (unsigned)(mok ? m : 0) * (unsigned)ldc * 2u;
+    static_for<0, 4>([&](auto J) {
+      constexpr int bj = decltype(J)::value;
+      static_for<0, 2>([&](auto G2) {
+        constexpr int g2 = decltype(G2)::value;
+        f32x4 x = acc32_read<bi, bj, 2 * g2>(), y = acc32_read<bi, bj, 2 * g2 + 1>();
+        if constexpr (HAS_BIAS) {
+          x += *reinterpret_cast<const f32x4*>(bias_lds + 4 * (32 * bj + 16 * g2 + 4 * h));
+          y += *reinterpret_cast<const f32x4*>(bias_lds + 4 * (32 * bj + 16 * g2 + 8 + 4 * h));
+        }
+        const bf16x4 xo = {(bf16)x[0], (bf16)x[1], (bf16)x[2], (bf16)x[3]};
+        const bf16x4 yo = {(bf16)y[0], (bf16)y[1], (bf16)y[2], (bf16)y[3]};
+        const u32x2 xd = __builtin_bit_cast(u32x2, xo), yd = __builtin_bit_cast(u32x2, yo);
+        const auto s0 = __builtin_amdgcn_permlane32_swap(xd[0], yd[0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane32_swap(xd[1], yd[1], false, false);
+        const u32x4 w = {s0[0], s1[0], s0[1], s1[1]};
+        const int n = col0 + 32 * bj + 16 * g2;
+        const unsigned off = (mok && n < N) ? rbase + (unsigned)n * 2u : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b128(w, rc, off, 0, SA);
       });
     });
   });
@@ -698,8 +774,9 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   static_assert(!SWB || (OUT == 0 && BN == 256 && ROPE == 0 && !SWIGLU), "SwiGLU-backward epilogue: bf16 256-wide tiles");
   static_assert(BN == 256 || BN == 192, "tile width");
   static_assert(BR >= 0 && BR <= 4 && (BR == 0 || DIAG == 0), "barrier row");
-  static_assert(!M32 || (!AK && !BKM && OUT == 1 && BN == 256 && BR == 0 && SCHED == 1 && ROPE == 0),
-                "32x32x16 main loop: TN fp32, 256-wide");
+  static_assert(!M32 || ((AK ? true : (!BKM && OUT == 1)) && BN == 256 && BR == 0 && SCHED == 1 && ROPE == 0 &&
+                          !SWIGLU && !SWB),
+                "32x32x16 main loop: TN fp32, NN / NT fp32 or bf16 (+ bias), 256-wide");
   static_assert(!GRP || (M32 && FAST), "grouped TN: the 32x32x16 FAST kernel");
   // ring pieces issued before the step's barrier (their count joins the wait, and the bias
   // DMA issued after the barrier has NQ - PBB younger ring pieces)
@@ -875,13 +952,20 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
 
   Frags<AK, BKM, BN, M32> F0, F1;
   int c_slot = 0;
-  // M32: per-lane offsets of the 4 fragment blocks of each operand in a slot (B: + 16384)
+  // M32: per-lane offsets of the 4 fragment blocks of each MN-major operand in a slot (B:
+  // + 16384); a K-major operand's two k-half offsets (its blocks are immediates apart)
   unsigned m32a[4] = {0, 0, 0, 0}, m32b[4] = {0, 0, 0, 0};
+  unsigned k32a[2] = {0, 0}, k32b[2] = {0, 0};
   if constexpr (M32) {
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {
-      m32a[nb] = m32_off(wm * 128, nb, l);
-      m32b[nb] = 16384u + m32_off(wn * 128, nb, l);
+      if constexpr (!AK) m32a[nb] = m32_off(wm * 128, nb, l);
+      if constexpr (!BKM) m32b[nb] = 16384u + m32_off(wn * 128, nb, l);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      if constexpr (AK) k32a[kk] = k32_off(wm * 128, kk, l);
+      if constexpr (BKM) k32b[kk] = 16384u + k32_off(wn * 128, kk, l);
     }
   }
   // DIAG build only (timing diagnosis, never the production kernel): cycles spent in the
@@ -957,8 +1041,14 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
         if constexpr (t == 0) stage_rsrc_a();
         if constexpr (t == 1) stage_rsrc_b();
         // next step's fragments: block nb of A after MFMA 2 nb, of B after MFMA 8 + 2 nb
-        if constexpr (!NOPF && t < 8 && (t & 1) == 0) nxt.a.load_nb(t >> 1, src + m32a[t >> 1]);
-        if constexpr (!NOPF && t >= 8 && t < 16 && (t & 1) == 0) nxt.b.load_nb((t - 8) >> 1, src + m32b[(t - 8) >> 1]);
+        if constexpr (!NOPF && t < 8 && (t & 1) == 0) {
+          if constexpr (AK) nxt.a.load_nb(t >> 1, src + k32a[0], src + k32a[1]);
+          else nxt.a.load_nb(t >> 1, src + m32a[t >> 1]);
+        }
+        if constexpr (!NOPF && t >= 8 && t < 16 && (t & 1) == 0) {
+          if constexpr (BKM) nxt.b.load_nb((t - 8) >> 1, src + k32b[0], src + k32b[1]);
+          else nxt.b.load_nb((t - 8) >> 1, src + m32b[(t - 8) >> 1]);
+        }
         if constexpr ((t & 3) == 2 && (t >> 2) < NQ) issue(t >> 2);
         __builtin_amdgcn_sched_barrier(0);
       });
@@ -1036,8 +1126,15 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
     if constexpr (GRP) {
       const TnGemm& d = grp.d[ci.g];
       epilogue_f32_m32(ci, d.C, d.M, d.N, d.ldc, d.slab_stride, d.c_bytes, wm, wn, l);
-    } else if constexpr (M32) {
+    } else if constexpr (M32 && OUT == 1) {
       epilogue_f32_m32(ci, C, M, N, ldc, slab_stride, c_bytes, wm, wn, l);
+    } else if constexpr (M32) {
+      if (bias) {
+        wait_vmcnt<NQ - PBB>();   // this wave's bias DMA landed (younger: the ring pieces after it)
+        epilogue_bf16_m32<true, SA>(bias_lds, ci, C, M, N, ldc, c_bytes, wm, wn, l);
+      } else {
+        epilogue_bf16_m32<false, SA>(bias_lds, ci, C, M, N, ldc, c_bytes, wm, wn, l);
+      }
     }
     if constexpr (M32) {
       if constexpr (TIMED) {
@@ -1138,6 +1235,11 @@ extern "C" void dpfs_gemm4_group_m(int g) { g_g4_group_m = g > 0 ? g : 4; }
 // TN main loop: 1 = the 32x32x16 form (gemm4_k's M32, default), 0 = 16x16x32 (A/B probes).
 static int g_g4_m32 = 1;
 extern "C" void dpfs_gemm4_m32(int v) { g_g4_m32 = v ? 1 : 0; }
+// NN / NT main loop on 256-wide tiles: bit 0 = 32x32x16 for the fp32 (split-K) output, bit 1 =
+// for the bf16 (+ bias) output; 0 = 16x16x32 (default: the K-major 32x32x16 form measured
+// 0.3 ms/step slower in the GPT-2-small step, profiles/r5_m32k_ab.txt)
+static int g_g4_m32k = 0;
+extern "C" void dpfs_gemm4_m32k(int v) { g_g4_m32k = v & 3; }
 
 // gate|up projection with SwiGLU in the epilogue (SwiOut): C[M, N] = A perm(B)^T + perm(bias)
 // (B / bias in the natural [gate | up] layout, read interleaved: reference.gu_perm),
@@ -1271,6 +1373,24 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
       if (fast && sched == 1 && g_g4_m32) {                                                       \
         gemm4_k<false, false, 1, 0, true, 1, 256, 0, false, false, 0, 0, true>                    \
             <<<grid, 256, 0, s>>>(G4_ARGS);                                                       \
+        break;                                                                                    \
+      }                                                                                           \
+    }                                                                                             \
+    if constexpr (AK_ && OUT_ == 1) {                                                             \
+      if (fast && sched == 1 && (g_g4_m32k & 1)) {                                                \
+        gemm4_k<AK_, BK_, 1, 0, true, 1, 256, 0, false, false, 0, 0, true>                        \
+            <<<grid, 256, 0, s>>>(G4_ARGS);                                                       \
+        break;                                                                                    \
+      }                                                                                           \
+    }                                                                                             \
+    if constexpr (AK_ && OUT_ == 0) {                                                             \
+      if (fast && sched == 1 && (g_g4_m32k & 2) && bn == 256 && rope_cols == 0) {                 \
+        if (ntst)                                                                                 \
+          gemm4_k<AK_, BK_, 0, 0, true, 1, 256, 0, false, false, 0, 2, true>                      \
+              <<<grid, 256, 0, s>>>(G4_ARGS);                                                     \
+        else                                                                                      \
+          gemm4_k<AK_, BK_, 0, 0, true, 1, 256, 0, false, false, 0, 0, true>                      \
+              <<<grid, 256, 0, s>>>(G4_ARGS);                                                     \
         break;                                                                                    \
       }                                                                                           \
     }                                                                                             \

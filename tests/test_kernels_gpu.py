@@ -822,6 +822,57 @@ def test_gemm_tn_m32_matches_16x16_form(C, M, N, K):
     assert _rel(acc, want) < 1e-5
 
 
+@pytest.mark.parametrize("layout", ["nn", "nt"])
+@pytest.mark.parametrize("M,N,K,splits", [(2048, 768, 50304, 0), (1000, 776, 16384, 3), (520, 1032, 4096, 2)])
+def test_gemm_split_k_m32_matches_16x16_form(C, layout, M, N, K, splits):
+    """NN / NT with fp32 split-K slabs (the lm_head data gradient's path) on the 32x32x16 main
+    loop with K-major operands (the A/B form, gemm4_m32k) against the 16x16x32 loop (default)
+    and the fp32 oracle."""
+    torch.manual_seed(33)
+    a = (torch.randn(M, K, device=DEV) / 16).bfloat16()
+    b = (torch.randn(K, N, device=DEV) / 16).bfloat16() if layout == "nn" else \
+        (torch.randn(N, K, device=DEV) / 16).bfloat16()
+    run = (lambda: C.gemm_nn(a, b)) if layout == "nn" else (lambda: C.gemm_nt(a, b))
+    ref = R.gemm_nn(a.float(), b.float()) if layout == "nn" else R.gemm_nt(a.float(), b.float())
+    try:
+        C.gemm_force(-1, splits)
+        C.gemm4_m32k(0)
+        o16 = run()
+        C.gemm4_m32k(1)
+        o32 = run()
+    finally:
+        C.gemm4_m32k(0)
+        C.gemm_force(-1, 0)
+    assert _rel(o32, ref) < 1e-2 and _rel(o16, ref) < 1e-2
+    assert _rel(o32, o16) < 2e-3
+
+
+@pytest.mark.parametrize("layout", ["nn", "nt"])
+@pytest.mark.parametrize("M,N,K,with_bias", [(4096, 50304, 768, False), (1000, 1032, 512, True), (300, 264, 4096, True)])
+def test_gemm_bf16_m32_matches_16x16_form(C, layout, M, N, K, with_bias):
+    """NN / NT bf16 output (+ fp32 bias on NT) on 256-wide tiles with the 32x32x16 main loop
+    (the A/B form; the lm_head forward's shape first) against the 16x16x32 loop and the oracle,
+    ragged M / N included; the non-temporal-store form (variant 5) bit-identical."""
+    torch.manual_seed(34)
+    a = (torch.randn(M, K, device=DEV) / 8).bfloat16()
+    b = (torch.randn(K, N, device=DEV) / 8).bfloat16() if layout == "nn" else \
+        (torch.randn(N, K, device=DEV) / 8).bfloat16()
+    bias = torch.randn(N, device=DEV) if (with_bias and layout == "nt") else None
+    run = (lambda v: C.gemm_nn(a, b, variant=v)) if layout == "nn" else (lambda v: C.gemm_nt(a, b, bias, variant=v))
+    ref = R.gemm_nn(a.float(), b.float()) if layout == "nn" else R.gemm_nt(a.float(), b.float(), bias)
+    try:
+        C.gemm4_m32k(0)
+        o16 = run(1)
+        C.gemm4_m32k(3)
+        o32 = run(1)
+        o32nt = run(5)
+    finally:
+        C.gemm4_m32k(0)
+    assert _rel(o32, ref) < 1e-2 and _rel(o16, ref) < 1e-2
+    assert _rel(o32, o16) < 2e-3
+    assert torch.equal(o32, o32nt)
+
+
 @pytest.mark.parametrize("shapes,K", [([(2304, 768), (768, 768)], 32768), ([(768, 2048), (4096, 768)], 32768),
                                       ([(2304, 768), (768, 768), (4096, 768), (768, 2048)], 8192),
                                       ([(1000, 776), (96, 768), (256, 256)], 2048), ([(384, 768), (768, 128)], 4096)])
