@@ -39,6 +39,7 @@ void dpfs_gemm_force(int, int);
 void dpfs_gemm_v2_sched(int);
 void dpfs_gemm_set_workspace(float*, long long);
 long long dpfs_gemm_bf16_ws(int, int, int);
+long long dpfs_gemm4_sk_ws(int, int, int);
 void dpfs_gemm_tn(const void*, const void*, float*, float*, int, int, int, int, int, int, int, hipStream_t);
 int dpfs_gemm_tn2(const void*, const void*, const void*, const void*, float*, float*, int, int, int, int, int, int, int,
                   int, int, int, hipStream_t);
@@ -196,7 +197,8 @@ torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
                       c10::optional<torch::Tensor> rope_pos, c10::optional<torch::Tensor> rope_tab,
                       int64_t rope_heads, int64_t rope_hd, c10::optional<torch::Tensor> out, int64_t variant) {
   check_rowmajor(a, "a");
-  TORCH_CHECK(variant >= 0 && variant <= 6, "gemm: variant 0 (v4), 1 (v4 256-wide), 2 (v4 192-wide), 3 (v3); "
+  TORCH_CHECK((variant >= 0 && variant <= 6) || variant == 8 || variant == 12,
+              "gemm: variant 0 (v4), 1 (v4 256-wide), 2 (v4 192-wide), 3 (v3), 8 (v4 stream-K 256-wide); "
               "+4: v4 with non-temporal output stores");
   check_rowmajor(b, "b");
   TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "gemm_nt: bf16 operands");
@@ -210,7 +212,8 @@ torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
   if (K == 0) return c.zero_();
   TORCH_CHECK(N % 4 == 0, "gemm_nt: N must be a multiple of 4, got ", N);
   const int ldc = (int)(M > 1 ? c.stride(0) : N);
-  const long long wsn = dpfs_gemm_bf16_ws((int)M, (int)N, (int)K);
+  long long wsn = dpfs_gemm_bf16_ws((int)M, (int)N, (int)K);
+  if (variant & 8) wsn = std::max(wsn, dpfs_gemm4_sk_ws((int)M, (int)N, (int)K));   // stream-K partials / flags
   torch::Tensor ws;
   if (wsn > 0) ws = torch::empty({wsn}, a.options().dtype(torch::kFloat32));
   dpfs_gemm_set_workspace(wsn > 0 ? ws.data_ptr<float>() : nullptr, wsn);
@@ -236,7 +239,8 @@ torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
 
 torch::Tensor gemm_nn(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> out, int64_t variant) {
   check_rowmajor(a, "a");
-  TORCH_CHECK(variant >= 0 && variant <= 6, "gemm: variant 0 (v4), 1 (v4 256-wide), 2 (v4 192-wide), 3 (v3); "
+  TORCH_CHECK((variant >= 0 && variant <= 6) || variant == 8 || variant == 12,
+              "gemm: variant 0 (v4), 1 (v4 256-wide), 2 (v4 192-wide), 3 (v3), 8 (v4 stream-K 256-wide); "
               "+4: v4 with non-temporal output stores");
   check_rowmajor(b, "b");
   TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "gemm_nn: bf16 operands");
@@ -248,7 +252,8 @@ torch::Tensor gemm_nn(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
   auto c = gemm_out(out, a, M, N);
   if (M == 0 || N == 0) return c;
   if (K == 0) return c.zero_();
-  const long long wsn = dpfs_gemm_bf16_ws((int)M, (int)N, (int)K);
+  long long wsn = dpfs_gemm_bf16_ws((int)M, (int)N, (int)K);
+  if (variant & 8) wsn = std::max(wsn, dpfs_gemm4_sk_ws((int)M, (int)N, (int)K));   // stream-K partials / flags
   torch::Tensor ws;
   if (wsn > 0) ws = torch::empty({wsn}, a.options().dtype(torch::kFloat32));
   dpfs_gemm_set_workspace(wsn > 0 ? ws.data_ptr<float>() : nullptr, wsn);
@@ -1274,6 +1279,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "dK/dV backward (head_dim 64): 1 = next key block's operands fetched ahead (default), 0 = off (A/B)");
   m.def("gemm4_swb_depth", [](int v) { dpfs_gemm4_swb_depth(v); },
         "SwiGLU-backward epilogue of the down-projection dgrad: gate / up row blocks in flight (2 default, 1 = A/B)");
+  m.def("gemm_sk_applies", [](int64_t M, int64_t N, int64_t K) { return dpfs_gemm4_sk_ws((int)M, (int)N, (int)K) > 0; },
+        "whether the stream-K bf16 kernel (variant 8 / 12) applies to an M x N x K NT / NN GEMM on this device");
   m.def("gemm4_m32k", [](int v) { dpfs_gemm4_m32k(v); },
         "NN / NT 256-wide main loop of the v4 GEMM: bit 0 = 32x32x16 MFMAs for the fp32 (split-K) output, bit 1 = for "
         "the bf16 (+ bias) output, 0 = 16x16x32 (default; measured faster in the step)");

@@ -925,8 +925,9 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
 static bool use_v4(int variant) { return g_gemm_impl >= 3 && (variant & 3) != 3; }
 static int v4_bn(int variant) {
   const int w = variant & 3;
-  return (w == 1 ? 256 : (w == 2 ? 192 : 0)) | ((variant & 4) ? 0x100 : 0);
+  return (w == 1 ? 256 : (w == 2 ? 192 : 0)) | ((variant & 4) ? 0x100 : 0) | ((variant & 8) ? 0x200 : 0);
 }
+extern "C" void dpfs_gemm4_set_sk_ws(float* p, long long n);
 
 extern "C" long long dpfs_gemm_bf16_ws(int M, int N, int K) {
   const int S = bf16_splits(M, N, K);
@@ -956,9 +957,12 @@ static void bf16_gemm(const void* A, const void* B, void* C, const float* bias, 
     if (rope.cols > 0) dpfs_rope_after_gemm(C, rope, M, ldc, s);
     return;
   }
-  if (v4 && dpfs_gemm4_launch(lay, 0, A, B, C, bias, M, N, K, lda, ldb, ldc, ((K + 31) / 32) * 32, 1, 0, ab, bb,
-                               rope.pos, rope.tab, rope.cols, rope.hd, nullptr, nullptr, 0, 0, 0, 0u, 0u, v4_bn(variant), s))
-    return;
+  if (variant & 8) dpfs_gemm4_set_sk_ws(g_ws, g_ws_floats);   // (stream-K: its partials / flags)
+  const bool done4 = v4 && dpfs_gemm4_launch(lay, 0, A, B, C, bias, M, N, K, lda, ldb, ldc, ((K + 31) / 32) * 32, 1, 0,
+                                             ab, bb, rope.pos, rope.tab, rope.cols, rope.hd, nullptr, nullptr, 0, 0, 0,
+                                             0u, 0u, v4_bn(variant), s);
+  if (variant & 8) dpfs_gemm4_set_sk_ws(nullptr, 0);
+  if (done4) return;
   if (rope.cols > 0 && rope.hd != 64) {   // v3's epilogue rotates 64-wide heads only
     bf16_gemm<BKM>(A, B, C, bias, M, N, K, lda, ldb, ldc, ab, bb, variant, s);
     dpfs_rope_after_gemm(C, rope, M, ldc, s);

@@ -281,7 +281,25 @@ __device__ __forceinline__ void read_frags(Frags<AK, BKM, BN, M32>& f, const cha
 // Work item -> tile origin and K range (grouped order as gemm.hip's gemmp_k).
 struct Item {
   int m0, n0, kb, ke, split, sel, g;
+  int role;   // SK: 0 = whole tile, 1 = first K half (fp32 partial out), 2 = second K half (+ partial)
 };
+
+// Stream-K bf16 GEMM (gemm4_k's SK) for the shapes whose 256 x 256 tiles come out at 1.5 per CU
+// (N = 768 at 32k rows: 384 tiles on 256 CUs; the 256 x 192 split of the same output runs two
+// rounds of narrower, less MFMA-dense tiles).  With G workgroups and E = G / 2 extra tiles,
+// workgroup c runs two items: c < E: the first K half of extra tile G + c, then whole tile c;
+// c >= E: whole tile c, then the second K half of extra tile G + c - E.  The first half goes
+// out as an fp32 partial (write-through, system-coherent stores, drained) with a per-wave
+// flag; the second half's epilogue waits for that flag (bounded: s_memrealtime, error word on
+// timeout, never a hang) and adds the partial before bias / bf16 / stores.  The producer runs
+// its half FIRST and the consumer LAST, so the wait is normally already satisfied.
+struct SkArgs {
+  float* part;        // [E][4 waves][64 x 64 lanes x 4] fp32, lane-linear per wave
+  unsigned* flags;    // [E][4 waves], zeroed before the launch; 1 = partial written
+  unsigned* err;      // set to 1 when a wait timed out
+  int extra;          // E
+};
+constexpr int kAuxSys = 1 | 16;   // sc0 | sc1: write-through stores, L2-bypassing loads
 
 // A group of up to 4 TN GEMMs over the same K (a layer's weight gradients), one launch: item
 // lin belongs to GEMM g with item0[g] <= lin < item0[g + 1]; every GEMM uses the launch's K
@@ -318,6 +336,7 @@ __device__ __forceinline__ Item decode(int lin, int nwg, int tiles_m, int tiles_
                "item %d -> tile (%d, %d) k %d", lin, it.m0, it.n0, it.kb);
   it.sel = 0;
   it.g = 0;
+  it.role = 0;
   if (it.kb >= k_switch) {
     it.sel = 1;
     it.kb -= k_switch;
@@ -415,10 +434,46 @@ __device__ __forceinline__ void epilogue_bf16_m32(const char* bias_lds, const It
   });
 }
 
-template <int OUT, int BN, int ROPE, bool HAS_BIAS, bool SWIGLU = false, int SA = 0>
+// Stream-K, first K half (SK role 1): the wave's 128 x 128 fp32 partial, lane-linear (store
+// (i, j) of lane l at ((8 i + j) 64 + l) 16 bytes), written through to memory, drained, then
+// the wave's flag.
+__device__ __forceinline__ void epilogue_sk_part(const SkArgs& sk, int e, int wave, int l) {
+  acc_drain();
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(sk.part + ((long long)e * 4 + wave) * 16384), (short)0, 65536, 0x00020000);
+  static_for<0, 8>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    static_for<0, 8>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc_read<i, j>()), rp,
+                                             (unsigned)(((8 * i + j) * 64 + l) * 16), 0, kAuxSys);
+    });
+  });
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (l == 0) __hip_atomic_store(sk.flags + e * 4 + wave, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Stream-K, second K half (SK role 2): wait (bounded) for the first half's partial.
+__device__ __forceinline__ void sk_wait(const SkArgs& sk, int e, int wave, int l) {
+  const unsigned* f = sk.flags + e * 4 + wave;
+  const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + 200000000ull;   // 2 s at 100 MHz
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 1u) {
+    __builtin_amdgcn_s_sleep(2);
+    if (__builtin_amdgcn_s_memrealtime() > deadline) {
+      if (l == 0) __hip_atomic_store(sk.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // (the partial's loads stay below)
+}
+
+// PART (stream-K role 2): the first K half's fp32 partial (epilogue_sk_part's layout, base
+// `part` of this wave) is added to the accumulators before bias / RoPE / bf16; block i + 1's
+// 8 vectors are loaded (L2-bypassing) under block i's conversions and stores.
+template <int OUT, int BN, int ROPE, bool HAS_BIAS, bool SWIGLU = false, int SA = 0, bool PART = false>
 __device__ __forceinline__ void epilogue(const char* bias_lds, const Item& ci, void* C, const Rope& rope, int M,
                                          int N, int ldc, long long slab_stride, unsigned c_bytes, int wm, int wn,
-                                         int l, const SwiOut& swo = SwiOut{}) {
+                                         int l, const SwiOut& swo = SwiOut{}, const float* part = nullptr) {
   constexpr int NJ = BN / 32;
   const int g = l >> 4;
   const int wcol0 = ci.n0 + wn * (BN / 2);
@@ -453,12 +508,33 @@ __device__ __forceinline__ void epilogue(const char* bias_lds, const Item& ci, v
     if constexpr (HD != 0) {
       if (do_rope) rope_load(0);
     }
+    const __amdgpu_buffer_rsrc_t rp =
+        __builtin_amdgcn_make_buffer_rsrc((void*)part, (short)0, PART ? 65536 : 0, 0x00020000);
+    f32x4 pa[PART ? 8 : 1];
+    if constexpr (PART) {
+      static_assert(BN == 256, "stream-K partials: 256-wide tiles");
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        pa[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rp, (unsigned)((j * 64 + l) * 16), 0, kAuxSys));
+    }
     static_for<0, 8>([&](auto I) {
       constexpr int i = decltype(I)::value;
       f32x4 v[8];
+      f32x4 pc[PART ? 8 : 1];
+      if constexpr (PART) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pc[j] = pa[j];
+        if constexpr (i + 1 < 8) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            pa[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  rp, (unsigned)(((8 * (i + 1) + j) * 64 + l) * 16), 0, kAuxSys));
+        }
+      }
       static_for<0, NJ>([&](auto J) {
         constexpr int j = decltype(J)::value;
         v[j] = acc_read<i, j>();
+        if constexpr (PART) v[j] += pc[j];
         if constexpr (HAS_BIAS) v[j] += bv[j];
       });
       const int m = row0 + 16 * i;
@@ -755,14 +831,16 @@ __device__ __forceinline__ void epilogue_swb(const Item& ci, int M, int F, const
 // address / SALU work fit in the MFMA shadow (the 16x16x32 TN step issues ~1.5k cycles of
 // non-MFMA work against 1024 of matrix time).
 template <bool AK, bool BKM, int OUT, int DIAG = 0, bool FAST = false, int SCHED = 0, int BN = 256, int ROPE = 0,
-          bool SWIGLU = false, int SWB = 0, int BR = 0, int SA = 0, bool M32 = false, bool GRP = false>
+          bool SWIGLU = false, int SWB = 0, int BR = 0, int SA = 0, bool M32 = false, bool GRP = false,
+          bool SK = false>
 __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                   void* __restrict__ C, const float* __restrict__ bias, int M, int N,
                                                   int K, int lda, int ldb, int ldc, int kps, int splits,
                                                   long long slab_stride, unsigned a_bytes, unsigned b_bytes,
                                                   unsigned c_bytes, Rope rope, int group_m, Dual dual, int dbg,
                                                   unsigned long long* diag, SwiOut swo = SwiOut{},
-                                                  SwiBwd swb = SwiBwd{}, TnGroup grp = TnGroup{}) {
+                                                  SwiBwd swb = SwiBwd{}, TnGroup grp = TnGroup{},
+                                                  SkArgs sk = SkArgs{}) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_TOTAL];
   constexpr bool TIMED = DIAG == 1 || DIAG == 2;   // the s_memtime builds
   constexpr int NJ = BN / 32;                  // 16-column MFMA tiles per wave
@@ -778,6 +856,9 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
                           !SWIGLU && !SWB),
                 "32x32x16 main loop: TN fp32, NN / NT fp32 or bf16 (+ bias), 256-wide");
   static_assert(!GRP || (M32 && FAST), "grouped TN: the 32x32x16 FAST kernel");
+  static_assert(!SK || (AK && OUT == 0 && BN == 256 && FAST && SCHED == 1 && BR == 0 && ROPE == 0 && !SWIGLU && !SWB &&
+                        !M32 && !GRP && DIAG == 0),
+                "stream-K: plain bf16 NT / NN, 256-wide FAST kernel");
   // ring pieces issued before the step's barrier (their count joins the wait, and the bias
   // DMA issued after the barrier has NQ - PBB younger ring pieces)
   constexpr int PBB = SCHED == 1 ? (BR < NQ ? BR : NQ) : 0;
@@ -785,10 +866,29 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   const int tiles_n = (N + BN - 1) / BN;
   const int tiles_m = (M + 255) / 256;
   const int nwg = tiles_m * tiles_n;
-  const int total = GRP ? grp.total : nwg * splits;
+  const int total = GRP ? grp.total : (SK ? 2 * (int)gridDim.x : nwg * splits);
   // work item -> tile / K range (GRP: of its GEMM in the group)
   auto gdecode = [&](int lin) -> Item {
-    if constexpr (GRP) {
+    if constexpr (SK) {
+      const int Gs = gridDim.x, E = sk.extra;
+      const bool second = lin >= Gs;
+      const int c = second ? lin - Gs : lin;
+      int tile, role;
+      if (c < E) {
+        tile = second ? c : Gs + c;
+        role = second ? 0 : 1;
+      } else {
+        tile = second ? Gs + c - E : c;
+        role = second ? 2 : 0;
+      }
+      Item x = decode<BN>(tile, nwg, tiles_m, tiles_n, group_m, K, K, 0x7fffffff);
+      x.role = role;
+      x.g = tile - Gs;   // (roles 1 / 2: the extra tile's index e, its partial / flag slot)
+      const int kh = K >> 1;   // (K % 128 == 0: both halves whole 64-deep stages)
+      if (role == 1) x.ke = kh;
+      if (role == 2) x.kb = kh;
+      return x;
+    } else if constexpr (GRP) {
       int g = 0;
 #pragma unroll
       for (int i = 1; i < 4; ++i)
@@ -1097,6 +1197,36 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
     const int nk = nsteps(ci);
     const int bcol0 = ci.n0 + wn * (BN / 2);
     constexpr std::false_type NO{};
+    if constexpr (SK) {
+      // As SWB below: the item's last step reads no fragments, so F0 / F1 are dead across the
+      // epilogue (the partial-add form holds 16 vectors of the partial); the next item's first
+      // fragments are read after it.
+      step(F0, F1, !first, std::true_type{}, NO, false, bcol0);
+      for (int t = 1; t < nk - 1; t += 2) {
+        step(F1, F0, false, NO, NO, false, bcol0);
+        step(F0, F1, false, NO, NO, false, bcol0);
+      }
+      step(F1, F0, false, NO, std::true_type{}, true, bcol0);
+      if (ci.role == 1) {
+        epilogue_sk_part(sk, ci.g, wave, l);
+      } else {
+        if (bias) wait_vmcnt<NQ - PBB>();   // this wave's bias DMA landed
+        if (ci.role == 2) {
+          sk_wait(sk, ci.g, wave, l);
+          const float* pw = sk.part + ((long long)ci.g * 4 + wave) * 16384;
+          if (bias)
+            epilogue<0, 256, 0, true, false, SA, true>(bias_lds, ci, C, rope, M, N, ldc, 0, c_bytes, wm, wn, l, swo, pw);
+          else
+            epilogue<0, 256, 0, false, false, SA, true>(bias_lds, ci, C, rope, M, N, ldc, 0, c_bytes, wm, wn, l, swo, pw);
+        } else if (bias) {
+          epilogue<0, 256, 0, true, false, SA>(bias_lds, ci, C, rope, M, N, ldc, 0, c_bytes, wm, wn, l, swo);
+        } else {
+          epilogue<0, 256, 0, false, false, SA>(bias_lds, ci, C, rope, M, N, ldc, 0, c_bytes, wm, wn, l, swo);
+        }
+      }
+      read_frags<AK, BKM, BN, M32>(F0, smem + c_slot * SLOT, wm, wn, l);
+      continue;
+    }
     if constexpr (SWB) {
       // The register-hungry SwiGLU-backward epilogue: the item's last step reads no fragments
       // (F0 / F1 are dead across the epilogue); the next item's first-step fragments are read
@@ -1301,6 +1431,24 @@ extern "C" bool dpfs_gemm4_nn_swiglu_bwd(const void* A, const void* B, const voi
   return true;
 }
 
+// Stream-K (gemm4_k's SK) applicability and workspace: plain bf16 NT / NN whose 256 x 256
+// tiles number exactly 1.5 per CU, K a multiple of 128.  Floats of workspace (partials, flags,
+// error word), -1 where it does not apply.
+extern "C" long long dpfs_gemm4_sk_ws(int M, int N, int K) {
+  const int cus = g4_cu_count();
+  if (M <= 0 || N <= 0 || K <= 0 || cus % 2 || K % 128) return -1;
+  const long long tiles = (long long)((M + 255) / 256) * ((N + 255) / 256);
+  if (tiles * 2 != 3LL * cus) return -1;
+  const long long E = cus / 2;
+  return E * 4 * 16384 + E * 4 + 4;
+}
+static float* g_g4_sk_ws = nullptr;
+static long long g_g4_sk_ws_floats = 0;
+extern "C" void dpfs_gemm4_set_sk_ws(float* p, long long n) {
+  g_g4_sk_ws = p;
+  g_g4_sk_ws_floats = n;
+}
+
 // Launch v4.  layout: 0 = NT (A K-major, B K-major), 1 = NN (B MN-major), 2 = TN (both
 // MN-major, fp32 out).  Returns false (nothing launched) when a span does not fit the 32-bit
 // buffer descriptors or a contiguous dimension is not a multiple of 8.
@@ -1311,8 +1459,10 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
                                   int k_switch, int lda2, int ldb2, unsigned a2_bytes, unsigned b2_bytes,
                                   int bn_force, hipStream_t s) {
   // bn_force: tile width of a non-split bf16 GEMM, 0 = chosen per shape, 256 / 192 forced;
-  // | 0x100: the bf16 output written with non-temporal stores (plain NT / NN)
+  // | 0x100: the bf16 output written with non-temporal stores (plain NT / NN); | 0x200: the
+  // stream-K kernel where it applies (dpfs_gemm4_sk_ws, workspace set by dpfs_gemm4_set_sk_ws)
   const bool ntst = (bn_force & 0x100) != 0;
+  const bool skreq = (bn_force & 0x200) != 0;
   bn_force &= 0xff;
   if (M <= 0 || N <= 0 || (N % 8) || (K % 8)) return false;
   if (layout == 2 && (M % 8)) return false;
@@ -1427,6 +1577,31 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
       gemm4_k<AK_, BK_, OUT_><<<grid, 256, 0, s>>>(G4_ARGS);                                 \
     }                                                                                             \
   } while (0)
+  if (skreq && layout != 2 && !out_f32 && splits == 1 && rope_cols == 0 && fast && sched == 1 && !A2 && !g_g4_ablate) {
+    const long long need = dpfs_gemm4_sk_ws(M, N, K);
+    if (need > 0 && g_g4_sk_ws && g_g4_sk_ws_floats >= need) {
+      const int E = cus / 2;
+      SkArgs sk;
+      sk.part = g_g4_sk_ws;
+      sk.flags = reinterpret_cast<unsigned*>(g_g4_sk_ws + (long long)E * 4 * 16384);
+      sk.err = sk.flags + E * 4;
+      sk.extra = E;
+      if (hipMemsetAsync(sk.flags, 0, (size_t)(E * 4 + 1) * 4, s) != hipSuccess) return false;
+#define G4_SK(AK_, BK_, SA_)                                                                                  \
+  gemm4_k<AK_, BK_, 0, 0, true, 1, 256, 0, false, 0, 0, SA_, false, false, true><<<cus, 256, 0, s>>>(       \
+      (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, K, 1, 0, a_bytes, b_bytes, cb, rope, \
+      g_g4_group_m, dual, 0, nullptr, SwiOut{}, SwiBwd{}, TnGroup{}, sk)
+      if (layout == 0) {
+        if (ntst) G4_SK(true, true, 2);
+        else G4_SK(true, true, 0);
+      } else {
+        if (ntst) G4_SK(true, false, 2);
+        else G4_SK(true, false, 0);
+      }
+#undef G4_SK
+      return true;
+    }
+  }
   if ((g_g4_ablate & 32) && g_g4_diag && layout == 0 && !out_f32 && bn == 256) {
     gemm4_k<true, true, 0, 2, true, 1><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda,
                                                             ldb, ldc, kps, splits, slab_stride, a_bytes, b_bytes, cb,

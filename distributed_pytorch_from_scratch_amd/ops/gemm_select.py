@@ -114,20 +114,35 @@ def _lt_index(c: str) -> int:
 
 # Per-call kernel variant of our GEMM entry points (an argument, never process state):
 # 0 = v4 at its per-shape tile width, 1 / 2 = v4 with the 256 / 192 width forced, 3 = v3.
-_VARIANT = {"ours": 0, "ours256": 1, "ours192": 2, "ours3": 3, "ours_nt": 4, "ours256_nt": 5, "ours192_nt": 6}
+_VARIANT = {"ours": 0, "ours256": 1, "ours192": 2, "ours3": 3, "ours_nt": 4, "ours256_nt": 5, "ours192_nt": 6,
+            "ours_sk": 8, "ours_sk_nt": 12}
 
 
-def _ours_variants(call: Callable[[int], torch.Tensor], widths: bool = False) -> Dict[str, Callable]:
+def _ours_variants(call: Callable[[int], torch.Tensor], widths: bool = False, sk: bool = False) -> Dict[str, Callable]:
     """Our candidates for one call: ``ours`` = the v4 kernel (one wave per SIMD, 128-row wave
     tiles, csrc/kernels/gemm4.hip) at its per-shape tile width and, with ``widths`` (non-split
-    bf16 NT / NN), ``ours256`` / ``ours192`` = v4 with the width forced.  The v3 kernel
-    (variant 3) lost to v4 on every step shape (profiles/r3_gemm_v4_probe_salu.txt) and is no
-    longer a candidate; it remains the fallback for shapes the v4 launcher declines."""
+    bf16 NT / NN), ``ours256`` / ``ours192`` = v4 with the width forced; with ``sk`` (the shape
+    has 256-wide tiles at exactly 1.5 per CU) the stream-K kernel ``ours_sk`` as well.  The v3
+    kernel (variant 3) lost to v4 on every step shape (profiles/r3_gemm_v4_probe_salu.txt) and
+    is no longer a candidate; it remains the fallback for shapes the v4 launcher declines."""
     out = {"ours": lambda: call(0)}
     if widths:
         out.update({"ours256": lambda: call(1), "ours192": lambda: call(2), "ours_nt": lambda: call(4),
                     "ours256_nt": lambda: call(5), "ours192_nt": lambda: call(6)})
+    if widths and sk:
+        out.update({"ours_sk": lambda: call(8), "ours_sk_nt": lambda: call(12)})
     return out
+
+
+def _sk_ok(k, M: int, N: int, K: int) -> bool:
+    """Whether the stream-K bf16 kernel applies to this NT / NN shape on this device."""
+    return STREAM_K and hasattr(k, "gemm_sk_applies") and bool(k.gemm_sk_applies(M, N, K))
+
+
+# A/B hook (tools/ab_attr.py): the stream-K kernel among the per-shape candidates.  Off: on the
+# step's shapes it ties the 192-wide kernel at K = 4096 and loses at K <= 2304 (the fp32
+# partial hand-off's latency), and the step A/B is flat (profiles/r5_stream_k.txt).
+STREAM_K = False
 
 
 def _run_ours(call: Callable[[int], torch.Tensor], choice: str):
@@ -191,7 +206,7 @@ def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, out=None) -> torch.T
     if m == "lt":
         return lt(0)() if lt_ok and _lt_count(k, 0, M, N, K, bias is not None) else blas()
     key = ("nt", M, N, K, bias is not None, x.device.index)
-    c = _pick(key, {**_ours_variants(ours, True), **({"blas": blas} if _lib() else {})},
+    c = _pick(key, {**_ours_variants(ours, True, _sk_ok(k, M, N, K)), **({"blas": blas} if _lib() else {})},
               lambda: _lt_count(k, 0, M, N, K, bias is not None), lt if lt_ok else None)
     if c.startswith("ours") or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
         return _run_ours(ours, c)
@@ -290,7 +305,7 @@ def gemm_nn(k, a: torch.Tensor, b: torch.Tensor, out=None) -> torch.Tensor:
     if m == "lt":
         return lt(0)() if lt_ok and _lt_count(k, 1, M, N, K, False) else blas()
     key = ("nn", M, N, K, a.device.index)
-    c = _pick(key, {**_ours_variants(ours, True), **({"blas": blas} if _lib() else {})},
+    c = _pick(key, {**_ours_variants(ours, True, _sk_ok(k, M, N, K)), **({"blas": blas} if _lib() else {})},
               lambda: _lt_count(k, 1, M, N, K, False), lt if lt_ok else None)
     if c.startswith("ours") or (c != "blas" and not lt_ok):   # (an lt choice needs contiguous operands)
         return _run_ours(ours, c)

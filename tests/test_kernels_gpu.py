@@ -873,6 +873,35 @@ def test_gemm_bf16_m32_matches_16x16_form(C, layout, M, N, K, with_bias):
     assert torch.equal(o32, o32nt)
 
 
+@pytest.mark.parametrize("layout", ["nt", "nn"])
+@pytest.mark.parametrize("K", [768, 4096])
+def test_gemm_stream_k(C, layout, K):
+    """The stream-K bf16 kernel (variant 8; 12 = with non-temporal stores) on the N = 768
+    projections' shape: 384 tiles of 256 x 256 on 256 CUs, the 128 extra tiles split in K
+    halves between two workgroups (fp32 partial hand-off through a flag).  Against the fp32
+    oracle and the 256-wide kernel; the 32k x 768 shape is the step's (per-device CU count)."""
+    M, N = 32768, 768
+    if not C.gemm_sk_applies(M, N, K):
+        pytest.skip("stream-K needs 256 x 256 tiles at exactly 1.5 per CU on this device")
+    torch.manual_seed(35)
+    a = (torch.randn(M, K, device=DEV) / 8).bfloat16()
+    b = (torch.randn(N, K, device=DEV) / 8).bfloat16() if layout == "nt" else \
+        (torch.randn(K, N, device=DEV) / 8).bfloat16()
+    bias = torch.randn(N, device=DEV) if layout == "nt" else None
+    run = (lambda v: C.gemm_nt(a, b, bias, variant=v)) if layout == "nt" else (lambda v: C.gemm_nn(a, b, variant=v))
+    ref = R.gemm_nt(a.float(), b.float(), bias) if layout == "nt" else R.gemm_nn(a.float(), b.float())
+    o = run(8)
+    assert _rel(o, ref) < 1e-2 and torch.isfinite(o.float()).all()
+    assert _rel(o, run(1)) < 2e-3
+    assert torch.equal(run(12), o)
+    assert torch.equal(run(8), o)        # (a second launch: the flags are re-zeroed per launch)
+    # a column slice of a wider output (the xGMI staging slots' layout)
+    if layout == "nt":
+        wide = torch.zeros(M, N + 64, device=DEV, dtype=torch.bfloat16)
+        C.gemm_nt(a, b, bias, out=wide[:, :N], variant=8)
+        assert torch.equal(wide[:, :N], o) and not wide[:, N:].any()
+
+
 @pytest.mark.parametrize("shapes,K", [([(2304, 768), (768, 768)], 32768), ([(768, 2048), (4096, 768)], 32768),
                                       ([(2304, 768), (768, 768), (4096, 768), (768, 2048)], 8192),
                                       ([(1000, 776), (96, 768), (256, 256)], 2048), ([(384, 768), (768, 128)], 4096)])

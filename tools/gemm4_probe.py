@@ -105,6 +105,9 @@ def main():
                     help="extra v4 arms with timing-only ablations (bits: 1 no stores, 2 zero operands, 4 no DMA wait, 8 no step barrier)")
     ap.add_argument("--cold", action="store_true", help="flush the caches before every timed call")
     ap.add_argument("--big", action="store_true", help="also the 4096^3 / 8192^3 square shapes")
+    ap.add_argument("--sk", action="store_true", help="NT / NN: also the stream-K kernel (variant 8) where it applies")
+    ap.add_argument("--custom", type=int, nargs=3, action="append", default=[], metavar=("M", "N", "K"),
+                    help="extra shape(s) of every --layouts layout (name 'cM_N_K')")
     ap.add_argument("--br", type=int, nargs="*", default=[],
                     help="extra arms: the last --scheds variant with BR rows of MFMAs before each step's barrier")
     a = ap.parse_args()
@@ -114,8 +117,9 @@ def main():
     C = _ext.require()
     gen = torch.Generator(device="cuda").manual_seed(0)
     for layout in a.layouts:
-        for name, M, N, K in SHAPES[layout] + (BIG[layout] if a.big else []):
-            if a.shapes and name not in a.shapes:
+        for name, M, N, K in SHAPES[layout] + (BIG[layout] if a.big else []) + \
+                [(f"c{m}_{n}_{k}", m, n, k) for m, n, k in a.custom]:
+            if a.shapes and name not in a.shapes and not name.startswith("c"):
                 continue
             _, _, ours, blas, ref = operands(layout, M, N, K, gen, a.bias)
             want = ref() if M * N <= 50304 * 768 * 2 else None
@@ -188,6 +192,7 @@ def main():
                       f"epi {(v[:, 2] / tot).mean():.3f}", flush=True)
             arms = [f"v4s{sc}" for sc in a.scheds] + [f"br{x}" for x in a.br] + [f"gm{g}" for g in a.group_m] + [f"bn{b}" for b in a.bn] + [f"sp{x}" for x in a.splits] + \
                 [f"abl{x}" for x in a.ablate] + ["v3"] + \
+                (["sk"] if a.sk and layout in ("nt", "nn") and C.gemm_sk_applies(M, N, K) else []) + \
                 ([] if a.no_blas else ["blas"])
             ts = {k: [] for k in arms}
             for rd in range(a.rounds):
@@ -227,6 +232,10 @@ def main():
                         C.gemm4_ablate(int(k[3:]))
                         ts[k].append(timed(lambda: ours(C), a.iters))
                         C.gemm4_ablate(0)
+                    elif k == "sk":
+                        VAR[0] = 8
+                        ts[k].append(timed(lambda: ours(C), a.iters))
+                        set_variant(1)
                     elif k == "v3":
                         set_variant(0)
                         ts[k].append(timed(lambda: ours(C), a.iters))
