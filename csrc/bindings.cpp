@@ -1276,7 +1276,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_tn_splits", [](int M, int N, int K) { return dpfs_gemm_tn_splits(M, N, K); },
         "K-split count of the TN (weight-gradient) plan for an M x N output over K");
   m.def("attn_prefetch", [](int v) { dpfs_attn_prefetch(v); },
-        "dK/dV backward (head_dim 64): 1 = next key block's operands fetched ahead (default), 0 = off (A/B)");
+        "head_dim-64 attention backward, next block's operands fetched ahead: bit 0 = dK/dV, bit 1 = dQ (3 default; A/B)");
   m.def("gemm4_swb_depth", [](int v) { dpfs_gemm4_swb_depth(v); },
         "SwiGLU-backward epilogue of the down-projection dgrad: gate / up row blocks in flight (2 default, 1 = A/B)");
   m.def("gemm_sk_applies", [](int64_t M, int64_t N, int64_t K) { return dpfs_gemm4_sk_ws((int)M, (int)N, (int)K) > 0; },

@@ -1784,7 +1784,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
     const bf16* __restrict__ Og, const float* __restrict__ LSE, float* __restrict__ NDEL_OUT,
     float* __restrict__ LSN_OUT, bf16* __restrict__ dQ, int T, int H, int BH, long long ldq, long long ldk,
     long long ldv, long long lddo, long long ldo, long long lddq, float scale, int causal,
-    const int64_t* __restrict__ rpos, const float* __restrict__ rtab, float* __restrict__ BPQ) {
+    const int64_t* __restrict__ rpos, const float* __restrict__ rtab, float* __restrict__ BPQ, int prefetch = 1) {
   static_assert(HD == 64 || HD == 128, "dQ v3: head_dim 64 or 128");
   constexpr int BQ = 128, BKV = 64, KS = HD / 16, DTN = HD / 32, RB = HD * 2;
   constexpr int TILE = BKV * RB, STAGE = 2 * TILE, NST = 3;
@@ -1812,6 +1812,34 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
       koff[kh][ks] = r * RB + (swz_u<HD>(r, 2 * ks + hf) << 4);
     }
 
+  // The ring position runs on across the two query blocks (as dK/dV's key blocks): during the
+  // first block's last two key tiles the second block's first two K / V tiles are fetched into
+  // the slots the first block no longer needs, and its Q / dO / O rows (and LSE) into registers
+  // once the last tile's S / dP MFMAs have consumed Q / dO -- the second block starts with its
+  // operands landed instead of a cold prologue.  (head_dim 64: at 128 the one-wave-per-SIMD
+  // kernel has no registers to spare.)
+  const int qb1 = p;
+  const int nkv0 = ((causal ? min(T, (nqb - p) * BQ) : T) + BKV - 1) / BKV;
+  const int nkv1 = ((causal ? min(T, (qb1 + 1) * BQ) : T) + BKV - 1) / BKV;
+  const bool pre = HD == 64 && prefetch && qb1 != nqb - 1 - p && nkv0 >= 2 && nkv1 > 0;   // (uniform)
+  bf16x8 qf[KS], df[KS], ovr[KS];   // Q^T / dO^T operands (lane: query), O for delta
+  float lse_r = 0.f;
+  auto load_qdo = [&](int qq) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 a = {}, c = {}, ov = {};
+      if (qq < T) {
+        a = *reinterpret_cast<const bf16x8*>(Q + ((long long)b * T + qq) * ldq + (long long)h * HD + 16 * ks + 8 * hf);
+        c = *reinterpret_cast<const bf16x8*>(dO + ((long long)b * T + qq) * lddo + (long long)h * HD + 16 * ks + 8 * hf);
+        ov = *reinterpret_cast<const bf16x8*>(Og + ((long long)b * T + qq) * ldo + (long long)h * HD + 16 * ks + 8 * hf);
+      }
+      qf[ks] = a;
+      df[ks] = c;
+      ovr[ks] = ov;
+    }
+    lse_r = qq < T ? LSE[(long long)bh * T + qq] : 0.f;
+  };
+  int cur = 0;
   for (int sub = 0; sub < 2; ++sub) {
     const int qb = sub == 0 ? nqb - 1 - p : p;
     if (sub == 1 && qb == nqb - 1 - p) break;
@@ -1819,29 +1847,24 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
     const int q0 = qb * BQ, wq0 = q0 + 32 * wave, qi = wq0 + r32;
     const int kv_end = causal ? min(T, q0 + BQ) : T;
     const int nkv = (kv_end + BKV - 1) / BKV;
-    dma.issue(kbase, vbase, ldk, ldv, T, 0, smem);
-    if (nkv > 1) dma.issue(kbase, vbase, ldk, ldv, T, BKV, smem + STAGE);
-    // Q^T / dO^T operands (B of S^T, dP^T): lane holds X[qi][16 ks + 8 hf + j]
-    bf16x8 qf[KS], df[KS];
+    const bool fetched = sub == 1 && pre;   // tiles 0 / 1 and the Q / dO / O rows already on their way
+    if (!fetched) {
+      const int c1 = cur + 1 == NST ? 0 : cur + 1;
+      dma.issue(kbase, vbase, ldk, ldv, T, 0, smem + cur * STAGE);
+      if (nkv > 1) dma.issue(kbase, vbase, ldk, ldv, T, BKV, smem + c1 * STAGE);
+      // Q^T / dO^T operands (B of S^T, dP^T): lane holds X[qi][16 ks + 8 hf + j]
+      load_qdo(qi);
+    }
+    wait_vmcnt<0>();
     float dsum = 0.f;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      bf16x8 a = {}, c = {}, ov = {};
-      if (qi < T) {
-        a = *reinterpret_cast<const bf16x8*>(Q + ((long long)b * T + qi) * ldq + (long long)h * HD + 16 * ks + 8 * hf);
-        c = *reinterpret_cast<const bf16x8*>(dO + ((long long)b * T + qi) * lddo + (long long)h * HD + 16 * ks + 8 * hf);
-        ov = *reinterpret_cast<const bf16x8*>(Og + ((long long)b * T + qi) * ldo + (long long)h * HD + 16 * ks + 8 * hf);
-      }
-      qf[ks] = a;
-      df[ks] = c;
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dsum += (float)c[j] * (float)ov[j];
-    }
-    const float lc = qi < T ? -LSE[(long long)bh * T + qi] * kLog2e : 0.f;   // p = exp2(c2 S + lc)
-    wait_vmcnt<0>();
+      for (int j = 0; j < 8; ++j) dsum += (float)df[ks][j] * (float)ovr[ks][j];
+    const float lc = qi < T ? -lse_r * kLog2e : 0.f;   // p = exp2(c2 S + lc)
     const float ndel = -pair_sum(dsum);                                      // dP' = dP - delta
     if (hf == 0 && qi < T) {
-      LSN_OUT[(long long)bh * T + qi] = -LSE[(long long)bh * T + qi] / scale;   // dK/dV: S' = S - lse / scale
+      LSN_OUT[(long long)bh * T + qi] = -lse_r / scale;   // dK/dV: S' = S - lse / scale
       NDEL_OUT[(long long)bh * T + qi] = ndel;
     }
     f32x16 dq[DTN];
@@ -1849,9 +1872,10 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
     for (int d = 0; d < DTN; ++d)
 #pragma unroll
       for (int i = 0; i < 16; ++i) dq[d][i] = 0.f;
-    int cur = 0;
+    const bool ahead = sub == 0 && pre;   // this block prefetches the next one's first tiles
+    const int qi1 = qb1 * BQ + 32 * wave + r32;
     for (int t = 0; t < nkv; ++t) {
-      if (t + 1 < nkv) wait_vmcnt<PW>();
+      if (t + 1 < nkv || ahead) wait_vmcnt<PW>();   // (younger: tile t+1's or the next block's tile 0)
       else wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
       const char* lk = smem + cur * STAGE;
@@ -1861,7 +1885,12 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
       cur = (cur + 1 == NST) ? 0 : cur + 1;
       const int kv0 = t * BKV;
       if (t + 2 < nkv) dma.issue(kbase, vbase, ldk, ldv, T, kv0 + 2 * BKV, smem + nb * STAGE);
-      if (causal && kv0 > wq0 + 31) continue;   // wave-uniform
+      else if (ahead && t + 2 - nkv < nkv1)   // the next block's tile t + 2 - nkv (0 or 1)
+        dma.issue(kbase, vbase, ldk, ldv, T, (t + 2 - nkv) * BKV, smem + nb * STAGE);
+      if (causal && kv0 > wq0 + 31) {   // wave-uniform
+        if (ahead && t == nkv - 1) load_qdo(qi1);
+        continue;
+      }
       // dP^T starts from -delta (the lane's query), so dS = p dP' directly; p of key half 0 is
       // computed under half 1's MFMAs (four elements after each pair), half 1's after them.
       f32x16 sc[2], dp[2];
@@ -1898,6 +1927,8 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
           sc[0][i] = __builtin_amdgcn_exp2f(fmaf(sc[0][i], c2, lc));
         __builtin_amdgcn_sched_barrier(0);
       }
+      // the block's last tile: Q / dO are consumed, load the next block's rows
+      if (ahead && t == nkv - 1) load_qdo(qi1);
       // K^T fragments (A of dQ^T: lane d = 32 dt + r32, keys 16 s + 4 hf + 0..3 / 8..11)
       constexpr int NH = 2 * DTN * 4;
       s16x4 th[(NH + 15) / 16 * 16];
@@ -2033,8 +2064,10 @@ static unsigned long long* g_attn_diag = nullptr;
 extern "C" void dpfs_attn_diag(void* p) { g_attn_diag = (unsigned long long*)p; }
 // dK/dV (head_dim 64): 1 = the second key block's first tiles / K / V fetched during the first
 // block's last tiles (default), 0 = a cold prologue per block (A/B probes)
-static int g_attn_prefetch = 1;
-extern "C" void dpfs_attn_prefetch(int v) { g_attn_prefetch = v ? 1 : 0; }
+// Cross-block operand prefetch of the head_dim-64 backward kernels (A/B hook): bit 0 = dK/dV,
+// bit 1 = dQ (3 default)
+static int g_attn_prefetch = 3;
+extern "C" void dpfs_attn_prefetch(int v) { g_attn_prefetch = v & 3; }
 
 extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int T, int H,
                               int hd, long long ldq, long long ldk, long long ldv, long long ldo, float scale,
@@ -2089,7 +2122,7 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
   attn_bwd_dq3_k<HD_><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,   \
                                             (const bf16*)o, lse, delta, delta + (long long)B * H * T, (bf16*)dq, T, \
                                             H, B * H, ldq, ldk, ldv, lddo, ldo, lddq, scale, causal, rope_pos,     \
-                                            rope_tab, pq)
+                                            rope_tab, pq, (g_attn_prefetch >> 1) & 1)
     if (hd == 64) DQ3_LAUNCH(64);
     else DQ3_LAUNCH(128);
 #undef DQ3_LAUNCH
@@ -2105,7 +2138,7 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
   attn_bwd_dkdv3_k<HD_, DG_><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, \
                                                    delta + (long long)B * H * T, delta, (bf16*)dk, (bf16*)dv, T, H,     \
                                                    B * H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal, rope_pos,     \
-                                                   rope_tab, pk, pv, DG_ ? g_attn_diag : nullptr, g_attn_prefetch)
+                                                   rope_tab, pk, pv, DG_ ? g_attn_diag : nullptr, g_attn_prefetch & 1)
     if (hd == 64 && diag) DKDV3_LAUNCH(64, 1);
     else if (hd == 64) DKDV3_LAUNCH(64, 0);
     else DKDV3_LAUNCH(128, 0);

@@ -258,8 +258,9 @@ def test_attention_deterministic(C):
 @pytest.mark.parametrize("B,T,H", [(2, 1024, 3), (1, 1000, 2), (3, 777, 1), (2, 2048, 2), (1, 192, 2)])
 def test_attention_bwd_cross_block_prefetch_is_bit_identical(C, B, T, H):
     """dK/dV at head_dim 64 fetches the second key block's first Q / dO tiles and K / V during
-    the first block's last tiles; the arithmetic is unchanged: bit-identical to the cold-prologue
-    form, and against the fp32 oracle (ragged T: partial key blocks and query tiles)."""
+    the first block's last tiles, dQ the second query block's K / V tiles and Q / dO / O rows;
+    the arithmetic is unchanged: bit-identical to the cold-prologue forms (each alone and both),
+    and against the fp32 oracle (ragged T: partial key blocks and query tiles)."""
     torch.manual_seed(13)
     hd = 64
     qkv = torch.randn(B * T, 3 * H * hd, device=DEV).bfloat16()
@@ -268,15 +269,16 @@ def test_attention_bwd_cross_block_prefetch_is_bit_identical(C, B, T, H):
     do = torch.randn_like(o)
     outs = []
     try:
-        for pf in (1, 0):
+        for pf in (3, 0, 1, 2):
             C.attn_prefetch(pf)
             d = torch.empty_like(qkv)
             dq, dk, dv = (d[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
             C.attn_bwd(do, q, k, v, o, lse, 0.125, True, dq, dk, dv)
             outs.append((d, dq, dk, dv))
     finally:
-        C.attn_prefetch(1)
-    assert torch.equal(outs[0][0], outs[1][0])
+        C.attn_prefetch(3)
+    for x in outs[1:]:
+        assert torch.equal(outs[0][0], x[0])
     rq, rk, rv = (torch.empty(B, T, H, hd, device=DEV) for _ in range(3))
     R.attn_bwd(do.float(), q.float(), k.float(), v.float(), o.float(), lse, 0.125, True, rq, rk, rv)
     _, dq, dk, dv = outs[0]
