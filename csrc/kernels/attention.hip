@@ -83,6 +83,25 @@ __device__ __forceinline__ s16x4 ds_tr16(const char* p) {
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_u32(p)));
   return r;
 }
+// ... at a byte offset in the instruction's offset field: one address per row group instead of
+// one v_add per read.  `off` is a constant after unrolling (the switch folds away); the
+// offsets of the tiles' row steps (16 or 8 rows of 128 / 256 B) have cases, any other adds.
+template <int OFF>
+__device__ __forceinline__ s16x4 ds_tr16_at(const char* p) {
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(lds_u32(p)), "n"(OFF));
+  return r;
+}
+__device__ __forceinline__ s16x4 ds_tr16_off(const char* p, int off) {
+  switch (off) {
+#define ATT_TR(O) \
+  case O: return ds_tr16_at<O>(p);
+    ATT_TR(0) ATT_TR(1024) ATT_TR(2048) ATT_TR(3072) ATT_TR(4096) ATT_TR(5120) ATT_TR(6144) ATT_TR(7168)
+    ATT_TR(8192) ATT_TR(10240) ATT_TR(12288) ATT_TR(14336)
+#undef ATT_TR
+    default: return ds_tr16(p + off);
+  }
+}
 template <int HD>
 __device__ __forceinline__ void tr_frag_asm(const char* lds, int r0, int c0, s16x4& lo, s16x4& hi) {
   const int l = lane_id();
@@ -526,6 +545,16 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
       const int r = 32 * kh + r32;
       koff[kh][ks] = r * RB + (swz_k<HD>(r, 2 * ks + hf) << 4);
     }
+  // V^T fragment reads: rows 16 k4 + 4 hf + (i16 >> 2) [+ 8], d columns 32 dt + 16 (g16 & 1) +
+  // 4 (i16 & 3); swz_v depends on row bits the 16 k4 / + 8 steps never touch, so a lane has
+  // one offset per dt and the row steps ride the read's offset field
+  int voff[DTN];
+#pragma unroll
+  for (int dt = 0; dt < DTN; ++dt) {
+    const int row = 4 * hf + (i16 >> 2);
+    const int col = 32 * dt + 16 * (g16 & 1) + 4 * (i16 & 3);
+    voff[dt] = row * RB + (swz_v<HD>(row, col >> 3) << 4) + (col & 7) * 2;
+  }
   const unsigned qspan = (unsigned)(((long long)(T - 1) * ldq + HD) * 2);
   const unsigned ospan = (unsigned)(((long long)(T - 1) * ldo + HD) * 2);
   bf16x8 qf[KS];
@@ -634,15 +663,14 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
         constexpr int NVH = 2 * DTN * 4;
         s16x4 vh[(NVH + 15) / 16 * 16];
 #pragma unroll
-        for (int dt = 0; dt < DTN; ++dt)
+        for (int dt = 0; dt < DTN; ++dt) {
+          const char* vb = lv + voff[dt];
 #pragma unroll
           for (int k4 = 0; k4 < 4; ++k4) {
-            const int row = 16 * k4 + 4 * hf + (i16 >> 2);
-            const int col = 32 * dt + 16 * (g16 & 1) + 4 * (i16 & 3);
-            const int ch = col >> 3, bo = (col & 7) * 2;
-            vh[2 * (dt * 4 + k4)] = ds_tr16(lv + row * RB + (swz_v<HD>(row, ch) << 4) + bo);
-            vh[2 * (dt * 4 + k4) + 1] = ds_tr16(lv + (row + 8) * RB + (swz_v<HD>(row + 8, ch) << 4) + bo);
+            vh[2 * (dt * 4 + k4)] = ds_tr16_off(vb, 16 * k4 * RB);
+            vh[2 * (dt * 4 + k4) + 1] = ds_tr16_off(vb, (16 * k4 + 8) * RB);
           }
+        }
         const bool need_mask = __builtin_amdgcn_readfirstlane(
             (int)((causal && kv0 + BKV - 1 > wq0) || (kv0 + BKV > T)));
         if (need_mask) {
@@ -1387,8 +1415,8 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
       for (int dt = 0; dt < DTN; ++dt)
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
-          th[2 * (dt * 4 + s4)] = ds_tr16(ldo_ + toff[dt][0] + 16 * s4 * RB);
-          th[2 * (dt * 4 + s4) + 1] = ds_tr16(ldo_ + toff[dt][1] + 16 * s4 * RB);
+          th[2 * (dt * 4 + s4)] = ds_tr16_off(ldo_ + toff[dt][0], 16 * s4 * RB);
+          th[2 * (dt * 4 + s4) + 1] = ds_tr16_off(ldo_ + toff[dt][1], 16 * s4 * RB);
         }
       // dS = p (dP - delta)
       bf16x8 pp[4];
@@ -1445,8 +1473,8 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
       for (int dt = 0; dt < DTN; ++dt)
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
-          th[2 * (dt * 4 + s4)] = ds_tr16(lq + toff[dt][0] + 16 * s4 * RB);
-          th[2 * (dt * 4 + s4) + 1] = ds_tr16(lq + toff[dt][1] + 16 * s4 * RB);
+          th[2 * (dt * 4 + s4)] = ds_tr16_off(lq + toff[dt][0], 16 * s4 * RB);
+          th[2 * (dt * 4 + s4) + 1] = ds_tr16_off(lq + toff[dt][1], 16 * s4 * RB);
         }
 #pragma unroll
       for (int w = 0; w < (NH + 15) / 16; ++w) tr_wait8(*reinterpret_cast<s16x4(*)[16]>(&th[16 * w]));
@@ -1811,6 +1839,17 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
       const int r = 32 * kh + r32;
       koff[kh][ks] = r * RB + (swz_u<HD>(r, 2 * ks + hf) << 4);
     }
+  // K^T transposed reads: rows 16 s4 + 4 hf + (i16 >> 2) [+ 8 e], d columns 32 dt + 16 (g16 & 1)
+  // + 4 (i16 & 3); swz_u ignores the 16 s4 step (an offset-field immediate), not the + 8
+  int toffq[DTN][2];
+#pragma unroll
+  for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int row = 4 * hf + (i16 >> 2) + 8 * e;
+      const int col = 32 * dt + 16 * (g16 & 1) + 4 * (i16 & 3);
+      toffq[dt][e] = row * RB + (swz_u<HD>(row, col >> 3) << 4) + (col & 7) * 2;
+    }
 
   // The ring position runs on across the two query blocks (as dK/dV's key blocks): during the
   // first block's last two key tiles the second block's first two K / V tiles are fetched into
@@ -1936,11 +1975,8 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
       for (int dt = 0; dt < DTN; ++dt)
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
-          const int row = 16 * s4 + 4 * hf + (i16 >> 2);
-          const int col = 32 * dt + 16 * (g16 & 1) + 4 * (i16 & 3);
-          const int ch = col >> 3, bo = (col & 7) * 2;
-          th[2 * (dt * 4 + s4)] = ds_tr16(lk + row * RB + (swz_u<HD>(row, ch) << 4) + bo);
-          th[2 * (dt * 4 + s4) + 1] = ds_tr16(lk + (row + 8) * RB + (swz_u<HD>(row + 8, ch) << 4) + bo);
+          th[2 * (dt * 4 + s4)] = ds_tr16_off(lk + toffq[dt][0], 16 * s4 * RB);
+          th[2 * (dt * 4 + s4) + 1] = ds_tr16_off(lk + toffq[dt][1], 16 * s4 * RB);
         }
 #pragma unroll
       for (int i = 0; i < 16; ++i) sc[1][i] = __builtin_amdgcn_exp2f(fmaf(sc[1][i], c2, lc));
