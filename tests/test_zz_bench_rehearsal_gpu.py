@@ -1,4 +1,6 @@
-"""Rehearsal of the driver's multi-GPU bench (SCALE: N = 2, 4, 8 back to back) on one MI355X:
+"""(Named to run last in the GPU suite: the longest and most box-sensitive tests.)
+
+Rehearsal of the driver's multi-GPU bench (SCALE: N = 2, 4, 8 back to back) on one MI355X:
 ``bench.py --gpus N`` under ``torch.distributed.run`` with N ranks sharing the GPU (gloo
 bootstrap; RCCL refuses two ranks on one device), the ``auto`` TP transport decision enabled on
 gloo (``DPFS_TP_COMM_AUTO_ANY_BACKEND=1``: xGMI kernels -- two-shot and one-shot -- and, at
@@ -27,10 +29,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # The driver's lease for a bench run is 600 s, most of it for the full-size model's warmup and
 # timed steps; the reduced-model rehearsal of the protocol (bootstrap, transport decisions, both
 # layouts, teardown) must take well under half of it.
-BUDGET_S = 240
+# (N ranks time-share the one GPU here: the N = 4 rehearsal has taken 100-224 s from box to box)
+BUDGET_S = 280
 
 
-@pytest.mark.timeout(300)
+@pytest.mark.timeout(320)
 @pytest.mark.parametrize("n,layouts", [(2, ["tp2"]), (4, ["tp2dp2", "tp4"]), (8, ["tp2dp4", "tp8"])])
 def test_bench_n_ranks_on_one_gpu(n, layouts):
     from dist_helpers import _free_port
@@ -49,7 +52,7 @@ def test_bench_n_ranks_on_one_gpu(n, layouts):
     t0 = time.time()
     with open(log, "w") as f:
         rc = subprocess.run(cmd, cwd=ROOT, env=env, stdout=f, stderr=subprocess.STDOUT, text=True,
-                            timeout=290).returncode
+                            timeout=300).returncode
     wall = time.time() - t0
     out = open(log).read()
     assert rc == 0, out[-6000:]
