@@ -225,7 +225,21 @@ __global__ __launch_bounds__(256) void colsum_rows_k(const float* __restrict__ p
   const int c0 = (blockIdx.x * 4 + cv) * 4;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   if (c0 < N_) {
-    for (int r = rl; r < R; r += 64) {
+    int r = rl;
+    if constexpr (VEC) {
+      // four rows' vectors in flight per step (the same add order as one at a time: the loads
+      // only move ahead of the adds), so the walk is not one load latency per row
+      for (; r + 192 < R; r += 256) {
+        float v[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) load_vec<float>(part + (long long)(r + 64 * u) * N_ + c0, v[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[j] += v[u][j];
+      }
+    }
+    for (; r < R; r += 64) {
       const float* p = part + (long long)r * N_ + c0;
       if constexpr (VEC) {
         float v[4];
