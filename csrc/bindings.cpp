@@ -72,6 +72,7 @@ int dpfs_norm_bwd_grid(int);
 void dpfs_bias_grad(int, const void*, float*, float*, int, int, hipStream_t);
 void dpfs_embedding_fwd(int, const int64_t*, const float*, void*, int, int, long long, int, hipStream_t);
 void dpfs_embedding_bwd(int, const void*, const int64_t*, float*, int, int, long long, int, hipStream_t);
+void dpfs_embedding_bwd_seg(int, const void*, const int64_t*, const int64_t*, float*, int, int, int, hipStream_t);
 void dpfs_ce_stats(int, const void*, const int64_t*, float*, int, int, long long, int, hipStream_t);
 long long dpfs_ce_fused_ws(int, int);
 int dpfs_ce_fused(int, void*, const int64_t*, const float*, float*, float*, float*, int, int, long long, int,
@@ -779,6 +780,42 @@ torch::Tensor embedding_bwd(torch::Tensor dout, torch::Tensor ids, int64_t v_loc
   return dw;
 }
 
+// Deterministic embedding gradient (no atomics): the ids sorted (stable), each local vocab row's
+// segment found by binary search, one wave per vocab row sums its rows in row order and WRITES
+// dw (every row: no zero pass), or adds to it (`accumulate`).  D % 4 == 0 (else the atomic form).
+torch::Tensor embedding_bwd_sorted(torch::Tensor dout, torch::Tensor ids, int64_t v_local, int64_t vocab_start,
+                                   c10::optional<torch::Tensor> out, bool accumulate) {
+  check_rowmajor(dout, "dout");
+  TORCH_CHECK(dout.is_contiguous(), "embedding_bwd_sorted: dout contiguous");
+  TORCH_CHECK(ids.scalar_type() == torch::kInt64 && ids.is_contiguous() && ids.numel() == dout.size(0),
+              "embedding_bwd_sorted: ids");
+  const at::DeviceGuard g(dout.device());
+  const int64_t D = dout.size(1);
+  torch::Tensor dw;
+  if (out.has_value()) {
+    dw = *out;
+    TORCH_CHECK(dw.scalar_type() == torch::kFloat32 && dw.is_contiguous() && dw.dim() == 2 && dw.size(0) == v_local &&
+                    dw.size(1) == D && dw.device() == dout.device(),
+                "embedding_bwd_sorted: out must be contiguous fp32 [v_local, D] on the device of dout");
+  } else {
+    dw = torch::empty({v_local, D}, dout.options().dtype(torch::kFloat32));
+    accumulate = false;
+  }
+  if (v_local == 0) return dw;
+  if (D % 4) {   // (the atomic form needs a zeroed / accumulating output)
+    if (!accumulate) dw.zero_();
+    return embedding_bwd(dout, ids, v_local, vocab_start, dw);
+  }
+  auto sorted = at::sort(ids.view({-1}), /*stable=*/true, /*dim=*/0, /*descending=*/false);
+  const torch::Tensor& sid = std::get<0>(sorted);
+  const torch::Tensor perm = std::get<1>(sorted).contiguous();
+  const torch::Tensor bounds = at::arange(vocab_start, vocab_start + v_local + 1, ids.options());
+  const torch::Tensor seg = at::searchsorted(sid, bounds).contiguous();
+  dpfs_embedding_bwd_seg(dcode(dout), dout.data_ptr(), perm.data_ptr<int64_t>(), seg.data_ptr<int64_t>(),
+                         dw.data_ptr<float>(), (int)D, (int)v_local, accumulate ? 1 : 0, stream());
+  return dw;
+}
+
 torch::Tensor ce_fwd_stats(torch::Tensor logits, torch::Tensor targets, int64_t vocab_start, int64_t vocab_valid) {
   check_rowmajor(logits, "logits");
   TORCH_CHECK(logits.is_contiguous(), "ce: logits contiguous");
@@ -1330,6 +1367,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "flash attention backward; impl (per call): 0 = auto (dq3 + dkdv3 at hd 64 / 128, dq + dkdv2 at hd 32), "
         "2 = dq + dkdv2 (16x16x32), 4 = dq3 + dkdv3 (32x32x16), 5 = 4 with the dK/dV DIAG build");
   m.def("embedding_fwd", &embedding_fwd);
+  m.def("embedding_bwd_sorted", &embedding_bwd_sorted, py::arg("dout"), py::arg("ids"), py::arg("v_local"),
+        py::arg("vocab_start"), py::arg("out") = py::none(), py::arg("accumulate") = false,
+        "deterministic embedding gradient (sorted ids, one wave per vocab row; writes or adds every row)");
   m.def("embedding_bwd", &embedding_bwd, py::arg("dout"), py::arg("ids"), py::arg("v_local"), py::arg("vocab_start"),
         py::arg("out") = py::none());
   m.def("ce_fwd_stats", &ce_fwd_stats);

@@ -51,6 +51,55 @@ __global__ __launch_bounds__(256) void embedding_bwd_k(const TI* __restrict__ do
   }
 }
 
+// Deterministic form (no atomics): the rows sorted by token id (stable: ascending row order
+// within an id) and each vocab row's segment [seg[v], seg[v + 1]) of the sorted order; one wave
+// per vocab row sums its segment's gradient rows in that fixed order and WRITES the row (zeros
+// for an id no row carries), or adds it to dw (`accumulate`: the later ping-pong chunks) -- no
+// zero pass, run-to-run bit-identical.  Four rows' vectors in flight per step.
+template <typename TI>
+__device__ __forceinline__ void load4f(const TI* p, float (&x)[4]) {
+  if constexpr (sizeof(TI) == 2) {
+    typedef TI t4 __attribute__((ext_vector_type(4)));
+    const t4 v = *reinterpret_cast<const t4*>(p);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = to_f(v[k]);
+  } else {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(p);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = v[k];
+  }
+}
+template <typename TI>
+__global__ __launch_bounds__(256) void embedding_bwd_seg_k(const TI* __restrict__ dout, const int64_t* __restrict__ perm,
+                                                           const int64_t* __restrict__ seg, float* __restrict__ dw,
+                                                           int D, int vlocal, int accumulate) {
+  const int lane = threadIdx.x & 63;
+  for (int v = blockIdx.x * 4 + (threadIdx.x >> 6); v < vlocal; v += gridDim.x * 4) {
+    const long long s0 = seg[v], e0 = seg[v + 1];
+    float* dst = dw + (long long)v * D;
+    for (int c = lane * 4; c < D; c += 256) {
+      f32x4 acc = accumulate ? *reinterpret_cast<const f32x4*>(dst + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      long long j = s0;
+      for (; j + 3 < e0; j += 4) {
+        float x[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) load4f<TI>(dout + perm[j + u] * D + c, x[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) acc[k] += x[u][k];
+      }
+      for (; j < e0; ++j) {
+        float x[4];
+        load4f<TI>(dout + perm[j] * D + c, x);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] += x[k];
+      }
+      *reinterpret_cast<f32x4*>(dst + c) = acc;
+    }
+  }
+}
+
 // ------------------------------------------------------------------- cross entropy ----
 struct MaxSum {
   float m, s;
@@ -455,6 +504,17 @@ extern "C" void dpfs_embedding_fwd(int out_dtype, const int64_t* ids, const floa
     embedding_fwd_k<bf16><<<grid, 256, 0, s>>>(ids, w, (bf16*)out, M, D, vstart, vlocal);
   else
     embedding_fwd_k<float><<<grid, 256, 0, s>>>(ids, w, (float*)out, M, D, vstart, vlocal);
+}
+
+// Sorted / segmented form (embedding_bwd_seg_k): perm = the stable ascending order of the ids,
+// seg[vlocal + 1] = each local vocab row's start in it.  D % 4 == 0.
+extern "C" void dpfs_embedding_bwd_seg(int in_dtype, const void* dout, const int64_t* perm, const int64_t* seg, float* dw,
+                                       int D, int vlocal, int accumulate, hipStream_t s) {
+  const int grid = cap_grid2(vlocal, 4);
+  if (in_dtype == kBF16)
+    embedding_bwd_seg_k<bf16><<<grid, 256, 0, s>>>((const bf16*)dout, perm, seg, dw, D, vlocal, accumulate);
+  else
+    embedding_bwd_seg_k<float><<<grid, 256, 0, s>>>((const float*)dout, perm, seg, dw, D, vlocal, accumulate);
 }
 
 // dw must be zeroed by the caller.

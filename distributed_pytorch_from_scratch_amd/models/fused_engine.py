@@ -519,10 +519,11 @@ class DecoderTrainFn(torch.autograd.Function):
         # layer 0: the embedding gradient first, so its all-reduce (the largest DP bucket) runs
         # under layer 0's Wo / QKV weight-gradient GEMMs
         ev = arena.view("emb", "emb")
-        ev.zero_()
-        for s in st:
+        for ci, s in enumerate(st):
             _finish_norm1(k, s, layers[0], gl[0], 0, V=V)
-            k.embedding_bwd(s["g"], s["ids"], model.embedding.weight.size(0), model.embedding.vocab_st_idx, out=ev)
+            # deterministic (sorted ids, no atomics): chunk 0 writes every row, the rest add
+            k.embedding_bwd_sorted(s["g"], s["ids"], model.embedding.weight.size(0), model.embedding.vocab_st_idx,
+                                   out=ev, accumulate=ci > 0)
         g["emb"] = ev
         dp_reduce("emb")
         tn_multi(gl[0], pend_w + [("wo", wo_p), ("wqkv", wqkv_p)])

@@ -348,11 +348,11 @@ class DecoderTrainFnSP(torch.autograd.Function):
                 del a["x"], a["r1"], s["dpend"]
             dp_reduce(f"L{li}")
         ev = arena.view("tail", "emb")
-        ev.zero_()
-        for s in st:    # embedding backward over all rows of the chunk (vocab-sharded table)
+        for ci, s in enumerate(st):    # embedding backward over all rows of the chunk (vocab-sharded table)
             _wait(s["h"])
-            k.embedding_bwd(s["gfull"], s["ids"], model.embedding.weight.size(0), model.embedding.vocab_st_idx,
-                            out=ev)
+            # deterministic (sorted ids, no atomics): chunk 0 writes every row, the rest add
+            k.embedding_bwd_sorted(s["gfull"], s["ids"], model.embedding.weight.size(0),
+                                   model.embedding.vocab_st_idx, out=ev, accumulate=ci > 0)
             del s["gfull"]
         g["emb"] = ev
         dp_reduce("tail")

@@ -387,6 +387,17 @@ def embedding_bwd(dout: torch.Tensor, ids: torch.Tensor, v_local: int, vocab_sta
     return dw
 
 
+def embedding_bwd_sorted(dout: torch.Tensor, ids: torch.Tensor, v_local: int, vocab_start: int,
+                         out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+    """``embedding_bwd`` that WRITES every row of ``out`` (``accumulate``: adds, as the later
+    chunks of the engines), summing each vocab row's gradient rows in row order."""
+    if out is None:
+        out = torch.zeros(v_local, dout.size(-1), dtype=torch.float32, device=dout.device)
+    elif not accumulate:
+        out.zero_()
+    return embedding_bwd(dout, ids, v_local, vocab_start, out)
+
+
 # ------------------------------------------------------------ vocab-parallel CE ----
 
 def ce_fwd_stats(logits: torch.Tensor, targets: torch.Tensor, vocab_start: int,

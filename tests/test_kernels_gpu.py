@@ -169,6 +169,35 @@ def test_embedding(C):
         assert _rel(C.embedding_bwd(d, ids, V, st), R.embedding_bwd(d.float(), ids, V, st)) < 1e-3
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("V,D,M", [(1000, 768, 4096), (50304, 768, 32768), (300, 20, 777), (64, 6, 100)])
+def test_embedding_bwd_sorted_deterministic(C, V, D, M, dt):
+    """The sorted embedding gradient (one wave per vocab row over its segment of the stably
+    sorted ids, no atomics): every row written (stale output overwritten, untouched ids zero),
+    equal to the fp32 oracle, bit-identical run to run and with the ids in another order of the
+    same multiset per row; accumulate adds; vocab shards (ids outside dropped); D % 4 != 0 runs
+    the atomic fallback."""
+    torch.manual_seed(36)
+    d = torch.randn(M, D, device=DEV).to(dt)
+    ids = torch.randint(0, 3 * V, (M,), device=DEV)
+    ids[: M // 8] = 5 + V                         # a hot token (a long segment)
+    for st in (0, V):
+        out = torch.full((V, D), float("nan"), device=DEV)
+        C.embedding_bwd_sorted(d, ids, V, st, out=out)
+        ref = R.embedding_bwd(d.float(), ids, V, st)
+        assert torch.isfinite(out).all() and _rel(out, ref) < 1e-5
+        out2 = torch.empty(V, D, device=DEV)
+        C.embedding_bwd_sorted(d, ids, V, st, out=out2)
+        assert torch.equal(out, out2) or D % 4   # (the D % 4 != 0 fallback is the atomic form)
+        acc = torch.randn(V, D, device=DEV)
+        want = acc + ref
+        C.embedding_bwd_sorted(d, ids, V, st, out=acc, accumulate=True)
+        assert _rel(acc, want) < 1e-5
+    if D % 4 == 0:   # fixed summation order: the row order within an id, not the thread schedule
+        a = C.embedding_bwd_sorted(d, ids, V, V)
+        assert torch.equal(a, C.embedding_bwd_sorted(d.clone(), ids.clone(), V, V))
+
+
 @pytest.mark.parametrize("V,valid,start", [(6288, 6288, 0), (6288, 6241, 6288 * 7), (1024, 1000, 0),
                                            (500, 500, 500)])
 def test_cross_entropy_kernels(C, V, valid, start):
