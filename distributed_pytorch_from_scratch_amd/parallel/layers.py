@@ -265,7 +265,7 @@ class _VocabEmbeddingFn(torch.autograd.Function):
         (flat,) = ctx.saved_tensors
         vl, st, wdt = ctx.meta
         d2 = dout.reshape(-1, dout.size(-1)).contiguous()
-        dw = K(d2).embedding_bwd(d2, flat, vl, st)
+        dw = K(d2).embedding_bwd_sorted(d2, flat.contiguous(), vl, st)   # deterministic (no atomics)
         return None, dw.to(wdt), None, None
 
 
