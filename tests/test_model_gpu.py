@@ -129,6 +129,39 @@ def test_gpu_training_memorizes_batch(dist1):
     assert losses[-1] < 0.5 * losses[0], losses
 
 
+def test_training_steps_are_bitwise_reproducible(dist1):
+    """Two trainings from the same seed and batches are bit-identical -- losses, every
+    parameter and Adam state after 3 steps -- now that no kernel of the step reduces with
+    atomics (the embedding gradient sums each vocab row's rows in row order; split-K, column
+    sums and attention use fixed-order reductions).  (Same process: the per-shape GEMM
+    choices are shared, and the variants a choice switches between are bit-identical.)"""
+    from distributed_pytorch_from_scratch_amd.utils.dist import set_seed
+    from distributed_pytorch_from_scratch_amd.models import get_preset, Transformer
+    from distributed_pytorch_from_scratch_amd.ops.optim import FusedAdam
+    from distributed_pytorch_from_scratch_amd.engine import TrainStep
+    args = get_preset("gpt2-small", num_layers=2)
+    g = torch.Generator(device="cuda").manual_seed(7)
+    ids = torch.randint(0, args.vocab_size, (3, 4, 257), device="cuda", generator=g)
+    ids[:, :, :64] = 11                       # a hot token: a long embedding-gradient segment
+    pos = torch.arange(256, device="cuda").repeat(4, 1)
+    runs = []
+    for _ in range(2):
+        set_seed(0)
+        m = Transformer.from_args(args).cuda()
+        m.reset_parameters()
+        opt = FusedAdam(m.parameters(), lr=1e-3)
+        step = TrainStep(m, opt)
+        losses = [step(ids[i, :, :-1], pos, ids[i, :, 1:]).item() for i in range(3)]
+        state = [p.detach().clone() for p in m.parameters()]
+        state += [v.clone() for st in opt.state.values() for v in st.values() if torch.is_tensor(v) and v.dim() > 0]
+        runs.append((losses, state))
+        del m, opt, step
+    assert runs[0][0] == runs[1][0], (runs[0][0], runs[1][0])
+    assert len(runs[0][1]) == len(runs[1][1])
+    for a, b in zip(runs[0][1], runs[1][1]):
+        assert torch.equal(a, b)
+
+
 def test_gpu_logits_api_matches_loss_api(dist1):
     import torch.nn.functional as F
     from distributed_pytorch_from_scratch_amd.models import get_preset, Transformer
