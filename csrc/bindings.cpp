@@ -214,7 +214,10 @@ torch::Tensor gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
   TORCH_CHECK(N % 4 == 0, "gemm_nt: N must be a multiple of 4, got ", N);
   const int ldc = (int)(M > 1 ? c.stride(0) : N);
   long long wsn = dpfs_gemm_bf16_ws((int)M, (int)N, (int)K);
-  if (variant & 8) wsn = std::max(wsn, dpfs_gemm4_sk_ws((int)M, (int)N, (int)K));   // stream-K partials / flags
+  if (variant & 8) {   // stream-K (where it applies: it replaces the split-K slabs) -- its partials / flags
+    const long long skn = dpfs_gemm4_sk_ws((int)M, (int)N, (int)K);
+    if (skn > 0) wsn = skn;
+  }
   torch::Tensor ws;
   if (wsn > 0) ws = torch::empty({wsn}, a.options().dtype(torch::kFloat32));
   dpfs_gemm_set_workspace(wsn > 0 ? ws.data_ptr<float>() : nullptr, wsn);
@@ -254,7 +257,10 @@ torch::Tensor gemm_nn(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
   if (M == 0 || N == 0) return c;
   if (K == 0) return c.zero_();
   long long wsn = dpfs_gemm_bf16_ws((int)M, (int)N, (int)K);
-  if (variant & 8) wsn = std::max(wsn, dpfs_gemm4_sk_ws((int)M, (int)N, (int)K));   // stream-K partials / flags
+  if (variant & 8) {   // stream-K (where it applies: it replaces the split-K slabs) -- its partials / flags
+    const long long skn = dpfs_gemm4_sk_ws((int)M, (int)N, (int)K);
+    if (skn > 0) wsn = skn;
+  }
   torch::Tensor ws;
   if (wsn > 0) ws = torch::empty({wsn}, a.options().dtype(torch::kFloat32));
   dpfs_gemm_set_workspace(wsn > 0 ? ws.data_ptr<float>() : nullptr, wsn);

@@ -928,6 +928,7 @@ static int v4_bn(int variant) {
   return (w == 1 ? 256 : (w == 2 ? 192 : 0)) | ((variant & 4) ? 0x100 : 0) | ((variant & 8) ? 0x200 : 0);
 }
 extern "C" void dpfs_gemm4_set_sk_ws(float* p, long long n);
+extern "C" long long dpfs_gemm4_sk_ws(int M, int N, int K);
 
 extern "C" long long dpfs_gemm_bf16_ws(int M, int N, int K) {
   const int S = bf16_splits(M, N, K);
@@ -938,8 +939,11 @@ template <bool BKM>
 static void bf16_gemm(const void* A, const void* B, void* C, const float* bias, int M, int N, int K, int lda, int ldb,
                       int ldc, unsigned ab, unsigned bb, int variant, hipStream_t s,
                       RopeArgs rope = RopeArgs{nullptr, nullptr, 0}) {
-  const int S = bf16_splits(M, N, K);
   const bool v4 = use_v4(variant);
+  // stream-K requested where it applies: it replaces the split-K slabs (a long-K shape whose
+  // 256 x 256 tiles are 1.5 per CU, e.g. the lm_head data gradient)
+  const bool sk = v4 && (variant & 8) && rope.cols == 0 && dpfs_gemm4_sk_ws(M, N, K) > 0;
+  const int S = sk ? 1 : bf16_splits(M, N, K);
   const int lay = BKM ? 0 : 1;
   if (S > 1 && g_ws && g_ws_floats >= (long long)S * M * N) {
     int kps = (K + S - 1) / S;

@@ -135,14 +135,17 @@ def _ours_variants(call: Callable[[int], torch.Tensor], widths: bool = False, sk
 
 
 def _sk_ok(k, M: int, N: int, K: int) -> bool:
-    """Whether the stream-K bf16 kernel applies to this NT / NN shape on this device."""
-    return STREAM_K and hasattr(k, "gemm_sk_applies") and bool(k.gemm_sk_applies(M, N, K))
+    """Whether the stream-K bf16 kernel is a candidate for this NT / NN shape on this device:
+    it applies (256 x 256 tiles at 1.5 per CU) and K is long enough for its one fp32 partial
+    hand-off to undercut the split-K slabs (SK_MIN_K)."""
+    return STREAM_K and K >= SK_MIN_K and hasattr(k, "gemm_sk_applies") and bool(k.gemm_sk_applies(M, N, K))
 
 
-# A/B hook (tools/ab_attr.py): the stream-K kernel among the per-shape candidates.  Off: on the
-# step's shapes it ties the 192-wide kernel at K = 4096 and loses at K <= 2304 (the fp32
-# partial hand-off's latency), and the step A/B is flat (profiles/r5_stream_k.txt).
-STREAM_K = False
+# A/B hook (tools/ab_attr.py): the stream-K kernel among the per-shape candidates.  At K <= 4096
+# it ties or loses to the 192-wide kernel (the hand-off's latency, profiles/r5_stream_k.txt),
+# so only the long-K shapes (the lm_head data gradient, K = vocab) try it, against split-K.
+STREAM_K = True
+SK_MIN_K = 8192
 
 
 def _run_ours(call: Callable[[int], torch.Tensor], choice: str):

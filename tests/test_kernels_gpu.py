@@ -905,12 +905,13 @@ def test_gemm_bf16_m32_matches_16x16_form(C, layout, M, N, K, with_bias):
 
 
 @pytest.mark.parametrize("layout", ["nt", "nn"])
-@pytest.mark.parametrize("K", [768, 4096])
+@pytest.mark.parametrize("K", [768, 4096, 16384])
 def test_gemm_stream_k(C, layout, K):
     """The stream-K bf16 kernel (variant 8; 12 = with non-temporal stores) on the N = 768
     projections' shape: 384 tiles of 256 x 256 on 256 CUs, the 128 extra tiles split in K
     halves between two workgroups (fp32 partial hand-off through a flag).  Against the fp32
-    oracle and the 256-wide kernel; the 32k x 768 shape is the step's (per-device CU count)."""
+    oracle and the 256-wide kernel; the 32k x 768 shape is the step's (per-device CU count).
+    At a long K (the lm_head data gradient's form) it replaces the split-K slab path."""
     M, N = 32768, 768
     if not C.gemm_sk_applies(M, N, K):
         pytest.skip("stream-K needs 256 x 256 tiles at exactly 1.5 per CU on this device")
