@@ -790,7 +790,8 @@ torch::Tensor embedding_bwd(torch::Tensor dout, torch::Tensor ids, int64_t v_loc
 // segment found by binary search, one wave per vocab row sums its rows in row order and WRITES
 // dw (every row: no zero pass), or adds to it (`accumulate`).  D % 4 == 0 (else the atomic form).
 torch::Tensor embedding_bwd_sorted(torch::Tensor dout, torch::Tensor ids, int64_t v_local, int64_t vocab_start,
-                                   c10::optional<torch::Tensor> out, bool accumulate) {
+                                   c10::optional<torch::Tensor> out, bool accumulate,
+                                   c10::optional<torch::Tensor> perm_in, c10::optional<torch::Tensor> seg_in) {
   check_rowmajor(dout, "dout");
   TORCH_CHECK(dout.is_contiguous(), "embedding_bwd_sorted: dout contiguous");
   TORCH_CHECK(ids.scalar_type() == torch::kInt64 && ids.is_contiguous() && ids.numel() == dout.size(0),
@@ -812,11 +813,19 @@ torch::Tensor embedding_bwd_sorted(torch::Tensor dout, torch::Tensor ids, int64_
     if (!accumulate) dw.zero_();
     return embedding_bwd(dout, ids, v_local, vocab_start, dw);
   }
-  auto sorted = at::sort(ids.view({-1}), /*stable=*/true, /*dim=*/0, /*descending=*/false);
-  const torch::Tensor& sid = std::get<0>(sorted);
-  const torch::Tensor perm = std::get<1>(sorted).contiguous();
-  const torch::Tensor bounds = at::arange(vocab_start, vocab_start + v_local + 1, ids.options());
-  const torch::Tensor seg = at::searchsorted(sid, bounds).contiguous();
+  torch::Tensor perm, seg;
+  if (perm_in.has_value() && seg_in.has_value()) {   // sorted ahead (e.g. on a side stream in the forward)
+    perm = *perm_in;
+    seg = *seg_in;
+    TORCH_CHECK(perm.scalar_type() == torch::kInt64 && perm.is_contiguous() && perm.numel() == ids.numel() &&
+                    seg.scalar_type() == torch::kInt64 && seg.is_contiguous() && seg.numel() == v_local + 1,
+                "embedding_bwd_sorted: perm [M] / seg [v_local + 1] int64");
+  } else {
+    auto sorted = at::sort(ids.view({-1}), /*stable=*/true, /*dim=*/0, /*descending=*/false);
+    perm = std::get<1>(sorted).contiguous();
+    const torch::Tensor bounds = at::arange(vocab_start, vocab_start + v_local + 1, ids.options());
+    seg = at::searchsorted(std::get<0>(sorted), bounds).contiguous();
+  }
   dpfs_embedding_bwd_seg(dcode(dout), dout.data_ptr(), perm.data_ptr<int64_t>(), seg.data_ptr<int64_t>(),
                          dw.data_ptr<float>(), (int)D, (int)v_local, accumulate ? 1 : 0, stream());
   return dw;
@@ -1375,6 +1384,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd_sorted", &embedding_bwd_sorted, py::arg("dout"), py::arg("ids"), py::arg("v_local"),
         py::arg("vocab_start"), py::arg("out") = py::none(), py::arg("accumulate") = false,
+        py::arg("perm") = py::none(), py::arg("seg") = py::none(),
         "deterministic embedding gradient (sorted ids, one wave per vocab row; writes or adds every row)");
   m.def("embedding_bwd", &embedding_bwd, py::arg("dout"), py::arg("ids"), py::arg("v_local"), py::arg("vocab_start"),
         py::arg("out") = py::none());

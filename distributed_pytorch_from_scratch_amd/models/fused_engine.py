@@ -42,7 +42,8 @@ import torch.distributed as dist
 
 from ..ops import fp8 as F8
 from ..ops import gemm_select as GS
-from ..ops.dispatch import K, shadow
+from ..ops import reference
+from ..ops.dispatch import K, emb_sort_ahead, emb_sort_take, shadow
 from ..parallel import grad_sync as GSY
 from ..parallel import process_manager as pm
 from ..parallel import tp_comm
@@ -238,7 +239,9 @@ class DecoderTrainFn(torch.autograd.Function):
             b0, b1 = bounds[c], bounds[c + 1]
             ids_c = ids[b0:b1].reshape(-1).contiguous()
             x = k.embedding_fwd(ids_c, emb.weight, emb.vocab_st_idx, dt)
-            st.append(dict(B=b1 - b0, ids=ids_c, pos=pos[b0:b1].reshape(-1).contiguous(),
+            # the embedding backward's sort, on a side stream beside the forward
+            esort = emb_sort_ahead(ids_c, emb.vocab_st_idx, emb.weight.size(0)) if k is not reference else None
+            st.append(dict(B=b1 - b0, ids=ids_c, esort=esort, pos=pos[b0:b1].reshape(-1).contiguous(),
                            tgt=tgt[b0:b1].reshape(-1).contiguous(), x=x, h=_ar(x), pend=None,
                            pend_bias=None, layers=[]))
         for li, L in enumerate(layers):
@@ -522,8 +525,9 @@ class DecoderTrainFn(torch.autograd.Function):
         for ci, s in enumerate(st):
             _finish_norm1(k, s, layers[0], gl[0], 0, V=V)
             # deterministic (sorted ids, no atomics): chunk 0 writes every row, the rest add
+            perm, seg = emb_sort_take(s.pop("esort", None))
             k.embedding_bwd_sorted(s["g"], s["ids"], model.embedding.weight.size(0), model.embedding.vocab_st_idx,
-                                   out=ev, accumulate=ci > 0)
+                                   out=ev, accumulate=ci > 0, perm=perm, seg=seg)
         g["emb"] = ev
         dp_reduce("emb")
         tn_multi(gl[0], pend_w + [("wo", wo_p), ("wqkv", wqkv_p)])

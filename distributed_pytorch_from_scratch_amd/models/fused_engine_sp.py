@@ -35,7 +35,8 @@ import torch.distributed as dist
 
 from ..ops import fp8 as F8
 from ..ops import gemm_select as GS
-from ..ops.dispatch import K, shadow
+from ..ops import reference
+from ..ops.dispatch import K, emb_sort_ahead, emb_sort_take, shadow
 from ..parallel import grad_sync as GSY
 from ..parallel import process_manager as pm
 from ..parallel import tp_comm
@@ -92,7 +93,9 @@ class DecoderTrainFnSP(torch.autograd.Function):
             assert ((b1 - b0) * T) % n == 0, "sequence parallelism: chunk rows must divide by tp_size"
             ids_c = ids[b0:b1].reshape(-1).contiguous()
             x_s, h = _rs(k.embedding_fwd(ids_c, emb.weight, emb.vocab_st_idx, dt), n)
-            st.append(dict(B=b1 - b0, ids=ids_c, pos=pos[b0:b1].reshape(-1).contiguous(),
+            # the embedding backward's sort, on a side stream beside the forward
+            esort = emb_sort_ahead(ids_c, emb.vocab_st_idx, emb.weight.size(0)) if k is not reference else None
+            st.append(dict(B=b1 - b0, ids=ids_c, esort=esort, pos=pos[b0:b1].reshape(-1).contiguous(),
                            tgt=tgt[b0:b1].reshape(-1).contiguous(), x=x_s, h=h, pend=None, pend_bias=None,
                            layers=[]))
         for L in layers:
@@ -351,8 +354,9 @@ class DecoderTrainFnSP(torch.autograd.Function):
         for ci, s in enumerate(st):    # embedding backward over all rows of the chunk (vocab-sharded table)
             _wait(s["h"])
             # deterministic (sorted ids, no atomics): chunk 0 writes every row, the rest add
+            perm, seg = emb_sort_take(s.pop("esort", None))
             k.embedding_bwd_sorted(s["gfull"], s["ids"], model.embedding.weight.size(0),
-                                   model.embedding.vocab_st_idx, out=ev, accumulate=ci > 0)
+                                   model.embedding.vocab_st_idx, out=ev, accumulate=ci > 0, perm=perm, seg=seg)
             del s["gfull"]
         g["emb"] = ev
         dp_reduce("tail")

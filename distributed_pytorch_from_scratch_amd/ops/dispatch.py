@@ -47,3 +47,41 @@ def peek_shadow(p: torch.Tensor):
     if c is None or c[0] != p._version or c[1].shape != p.shape:
         return None
     return c[1]
+
+
+_SORT_STREAMS = {}
+
+
+def emb_sort_ahead(ids: torch.Tensor, vocab_start: int, v_local: int):
+    """The deterministic embedding backward's sort (``embedding_bwd_sorted``: the ids' stable
+    order and each local vocab row's segment start), issued at the start of the forward on a
+    side stream so it runs beside the forward's GEMMs instead of in the backward's tail.
+    Returns a handle for :func:`emb_sort_take` (None off the GPU)."""
+    if not ids.is_cuda:
+        return None
+    dev = ids.device
+    side = _SORT_STREAMS.get(dev.index)
+    if side is None:
+        side = _SORT_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+    cur = torch.cuda.current_stream(dev)
+    side.wait_stream(cur)                       # the ids are ready
+    with torch.cuda.stream(side):
+        sid, perm = torch.sort(ids.view(-1), stable=True)
+        seg = torch.searchsorted(sid, torch.arange(vocab_start, vocab_start + v_local + 1, device=dev))
+        ev = torch.cuda.Event()
+        ev.record(side)
+    ids.record_stream(side)
+    return perm, seg, ev, side
+
+
+def emb_sort_take(h):
+    """(perm, seg) of an :func:`emb_sort_ahead` handle, ordered before the current stream's
+    next work (None, None for no handle)."""
+    if h is None:
+        return None, None
+    perm, seg, ev, side = h
+    cur = torch.cuda.current_stream(perm.device)
+    cur.wait_event(ev)
+    perm.record_stream(cur)                     # (allocated on the side stream, used on this one)
+    seg.record_stream(cur)
+    return perm, seg

@@ -388,14 +388,21 @@ def embedding_bwd(dout: torch.Tensor, ids: torch.Tensor, v_local: int, vocab_sta
 
 
 def embedding_bwd_sorted(dout: torch.Tensor, ids: torch.Tensor, v_local: int, vocab_start: int,
-                         out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+                         out: Optional[torch.Tensor] = None, accumulate: bool = False, perm=None,
+                         seg=None) -> torch.Tensor:
     """``embedding_bwd`` that WRITES every row of ``out`` (``accumulate``: adds, as the later
-    chunks of the engines), summing each vocab row's gradient rows in row order."""
+    chunks of the engines), summing each vocab row's gradient rows in row order.  (``perm`` /
+    ``seg``: the native kernel's precomputed sort, see ``emb_sort_ahead``; unused here.)"""
     if out is None:
         out = torch.zeros(v_local, dout.size(-1), dtype=torch.float32, device=dout.device)
     elif not accumulate:
         out.zero_()
     return embedding_bwd(dout, ids, v_local, vocab_start, out)
+
+
+def emb_sort_ahead(ids: torch.Tensor, vocab_start: int, v_local: int):
+    """The embedding backward's sort (see ops.dispatch.emb_sort_ahead); nothing to do here."""
+    return None
 
 
 # ------------------------------------------------------------ vocab-parallel CE ----
