@@ -17,9 +17,11 @@ extern "C" {
 void dpfs_gemm_nt(const void*, const void*, void*, const float*, int, int, int, int, int, int, int, hipStream_t);
 void dpfs_gemm_nn(const void*, const void*, void*, int, int, int, int, int, int, int, hipStream_t);
 int dpfs_gemm_tn_splits(int, int, int);
-long long dpfs_gemm_tn_group_ws(int, const int*, const int*, const int*, const int*, int, const int*);
+long long dpfs_gemm_tn_group_ws(int, const int*, const int*, const int*, const int*, int, const int*, const int*,
+                                 const int*, int);
 int dpfs_gemm_tn_group(int, const void* const*, const void* const*, float* const*, const int*, const int*, const int*,
-                       const int*, const int*, int, float*, long long, hipStream_t);
+                       const int*, const int*, int, float*, long long, const void* const*, const void* const*,
+                       const int*, const int*, int, hipStream_t);
 long long dpfs_gemm_tn_ws(int, int, int, int);
 void dpfs_gemm_set_impl(int);
 int dpfs_gemm_rope_fusable(int, int, int, int, int);
@@ -305,16 +307,24 @@ torch::Tensor gemm_tn(torch::Tensor a, torch::Tensor b, c10::optional<torch::Ten
 }
 
 // outs[g] fp32 (+= when acc[g]) a[g][K, M_g]^T b[g][K, N_g] for up to 4 GEMMs over one K as
-// one grouped launch (+ one reduction); False (nothing written) where the group does not apply.
+// one grouped launch (+ one reduction); with a2 / b2 the rows continue in second buffers
+// (a chunked step's other ping-pong chunk, K1 rows each).  False (nothing written) where the
+// group does not apply.
 bool gemm_tn_group(std::vector<torch::Tensor> a, std::vector<torch::Tensor> b, std::vector<torch::Tensor> outs,
-                   std::vector<int64_t> acc) {
+                   std::vector<int64_t> acc, c10::optional<std::vector<torch::Tensor>> a2,
+                   c10::optional<std::vector<torch::Tensor>> b2) {
   const size_t n = a.size();
   TORCH_CHECK(n >= 1 && n <= 4 && b.size() == n && outs.size() == n && acc.size() == n, "gemm_tn_group: 1..4 GEMMs");
+  const bool two = a2.has_value() && b2.has_value();
+  TORCH_CHECK(!two || (a2->size() == n && b2->size() == n), "gemm_tn_group: a2 / b2 per GEMM");
   const int64_t K = a[0].size(0);
+  const int64_t K1 = two ? (*a2)[0].size(0) : 0;
   const void* pa[4];
   const void* pb[4];
+  const void* pa2[4] = {nullptr, nullptr, nullptr, nullptr};
+  const void* pb2[4] = {nullptr, nullptr, nullptr, nullptr};
   float* pc[4];
-  int M[4], N[4], lda[4], ldb[4], ac[4];
+  int M[4], N[4], lda[4], ldb[4], ac[4], lda2[4] = {0, 0, 0, 0}, ldb2[4] = {0, 0, 0, 0};
   for (size_t g = 0; g < n; ++g) {
     check_rowmajor(a[g], "gemm_tn_group a");
     check_rowmajor(b[g], "gemm_tn_group b");
@@ -334,15 +344,30 @@ bool gemm_tn_group(std::vector<torch::Tensor> a, std::vector<torch::Tensor> b, s
     pa[g] = a[g].data_ptr();
     pb[g] = b[g].data_ptr();
     pc[g] = outs[g].data_ptr<float>();
+    if (two) {
+      const torch::Tensor& x = (*a2)[g];
+      const torch::Tensor& y = (*b2)[g];
+      check_rowmajor(x, "gemm_tn_group a2");
+      check_rowmajor(y, "gemm_tn_group b2");
+      TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && y.scalar_type() == torch::kBFloat16 && x.size(0) == K1 &&
+                      y.size(0) == K1 && x.size(1) == M[g] && y.size(1) == N[g] && x.device() == a[0].device() &&
+                      y.device() == a[0].device(),
+                  "gemm_tn_group: a2 [K1, M] / b2 [K1, N] bf16 on the group's device");
+      lda2[g] = (int)x.stride(0);
+      ldb2[g] = (int)y.stride(0);
+      pa2[g] = x.data_ptr();
+      pb2[g] = y.data_ptr();
+    }
   }
-  if (K <= 0 || K >= (1ll << 31)) return false;
-  const long long wsn = dpfs_gemm_tn_group_ws((int)n, M, N, lda, ldb, (int)K, ac);
+  if (K <= 0 || K + K1 >= (1ll << 31) || (two && K1 <= 0)) return false;
+  const long long wsn = dpfs_gemm_tn_group_ws((int)n, M, N, lda, ldb, (int)K, ac, two ? lda2 : nullptr,
+                                              two ? ldb2 : nullptr, (int)K1);
   if (wsn < 0) return false;
   const at::DeviceGuard dg(a[0].device());
   torch::Tensor ws;
   if (wsn > 0) ws = torch::empty({(int64_t)wsn}, outs[0].options());
   return dpfs_gemm_tn_group((int)n, pa, pb, pc, M, N, lda, ldb, ac, (int)K, ws.defined() ? ws.data_ptr<float>() : nullptr,
-                            wsn, stream()) != 0;
+                            wsn, pa2, pb2, lda2, ldb2, (int)K1, stream()) != 0;
 }
 
 // c[M,N] fp32 (+)= a0[K0,M]^T b0[K0,N] + a1[K1,M]^T b1[K1,N] in one split-K launch; None
@@ -1324,7 +1349,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "int64 buffer of the DIAG builds (attn_fwd / attn_bwd impl 5): per-wave s_memtime splits");
   m.def("gemm4_diag", [](torch::Tensor t) { dpfs_gemm4_diag(t.defined() && t.numel() ? t.data_ptr() : nullptr); },
         "int64 buffer [grid*4*4] for the DIAG build's per-wave cycle split (gemm4_ablate bit 16)");
-  m.def("gemm_tn_group", &gemm_tn_group, py::arg("a"), py::arg("b"), py::arg("outs"), py::arg("acc"));
+  m.def("gemm_tn_group", &gemm_tn_group, py::arg("a"), py::arg("b"), py::arg("outs"), py::arg("acc"),
+        py::arg("a2") = py::none(), py::arg("b2") = py::none());
   m.def("gemm_tn_splits", [](int M, int N, int K) { return dpfs_gemm_tn_splits(M, N, K); },
         "K-split count of the TN (weight-gradient) plan for an M x N output over K");
   m.def("attn_prefetch", [](int v) { dpfs_attn_prefetch(v); },

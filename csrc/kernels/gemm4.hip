@@ -311,9 +311,16 @@ struct TnGemm {
   long long slab_stride;
   int M, N, lda, ldb, ldc, tiles_m, tiles_n, item0;
   unsigned a_bytes, b_bytes, c_bytes, pad;
+  // the second buffers of rows (a chunked step's other ping-pong chunk: K rows past k_switch)
+  const bf16* A2;
+  const bf16* B2;
+  int lda2, ldb2;
+  unsigned a2_bytes, b2_bytes;
 };
 struct TnGroup {
   int n, total;
+  int k_switch;   // rows of the first buffers (0x7fffffff: one buffer); a multiple of kps
+  int pad;
   TnGemm d[4];
 };
 
@@ -894,7 +901,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
       for (int i = 1; i < 4; ++i)
         if (i < grp.n && lin >= grp.d[i].item0) g = i;
       const TnGemm& d = grp.d[g];
-      Item x = decode<BN>(lin - d.item0, d.tiles_m * d.tiles_n, d.tiles_m, d.tiles_n, group_m, K, kps, 0x7fffffff);
+      Item x = decode<BN>(lin - d.item0, d.tiles_m * d.tiles_n, d.tiles_m, d.tiles_n, group_m, K, kps, grp.k_switch);
       x.g = g;
       return x;
     } else {
@@ -932,7 +939,8 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   unsigned pbase[8];
   auto rebase = [&]() {
     const bool s2 = pi.sel != 0;
-    const int la = GRP ? grp.d[pi.g].lda : (s2 ? lda2 : lda), lb = GRP ? grp.d[pi.g].ldb : (s2 ? ldb2 : ldb);
+    const int la = GRP ? (s2 ? grp.d[pi.g].lda2 : grp.d[pi.g].lda) : (s2 ? lda2 : lda);
+    const int lb = GRP ? (s2 ? grp.d[pi.g].ldb2 : grp.d[pi.g].ldb) : (s2 ? ldb2 : ldb);
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const bool isA = q < 4;
@@ -977,15 +985,16 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   auto item_rsrc = [&]() {
     if constexpr (FAST) {
       const bool s2 = pi.sel != 0;
-      const int la = GRP ? grp.d[pi.g].lda : (s2 ? lda2 : lda), lb = GRP ? grp.d[pi.g].ldb : (s2 ? ldb2 : ldb);
+      const int la = GRP ? (s2 ? grp.d[pi.g].lda2 : grp.d[pi.g].lda) : (s2 ? lda2 : lda);
+      const int lb = GRP ? (s2 ? grp.d[pi.g].ldb2 : grp.d[pi.g].ldb) : (s2 ? ldb2 : ldb);
       const long long adv_a = AK ? (long long)pi.kb * 2 : (long long)pi.kb * la * 2;
       const long long adv_b = BKM ? (long long)pi.kb * 2 : (long long)pi.kb * lb * 2;
-      const bf16* a0 = GRP ? grp.d[pi.g].A : (s2 ? dual.A2 : A);
-      const bf16* b0 = GRP ? grp.d[pi.g].B : (s2 ? dual.B2 : B);
+      const bf16* a0 = GRP ? (s2 ? grp.d[pi.g].A2 : grp.d[pi.g].A) : (s2 ? dual.A2 : A);
+      const bf16* b0 = GRP ? (s2 ? grp.d[pi.g].B2 : grp.d[pi.g].B) : (s2 ? dual.B2 : B);
       ia = reinterpret_cast<unsigned long long>(a0) + adv_a;
       ib = reinterpret_cast<unsigned long long>(b0) + adv_b;
-      na0 = (GRP ? grp.d[pi.g].a_bytes : (s2 ? dual.a2_bytes : a_bytes)) - (unsigned)adv_a;
-      nb0 = (GRP ? grp.d[pi.g].b_bytes : (s2 ? dual.b2_bytes : b_bytes)) - (unsigned)adv_b;
+      na0 = (GRP ? (s2 ? grp.d[pi.g].a2_bytes : grp.d[pi.g].a_bytes) : (s2 ? dual.a2_bytes : a_bytes)) - (unsigned)adv_a;
+      nb0 = (GRP ? (s2 ? grp.d[pi.g].b2_bytes : grp.d[pi.g].b_bytes) : (s2 ? dual.b2_bytes : b_bytes)) - (unsigned)adv_b;
       sta = AK ? 64u : 64u * (unsigned)la;
       stb = BKM ? 64u : 64u * (unsigned)lb;
       nlive = (pi.ke - pi.kb + 31) / 32;
@@ -1688,36 +1697,69 @@ static int tn_group_splits(int n, const int* M, const int* N, int K, long long* 
   return best;
 }
 
+// The group's K-split plan: S splits of kps rows (a multiple of 64) over K = K0 + K1 rows; with
+// a second buffer (K1 > 0) kps also divides K0, so no work item straddles the two buffers.
+// Returns false where no plan fits.
+static bool tn_group_plan(int n, const int* M, const int* N, int K0, int K1, int* S_out, int* kps_out, long long* mn) {
+  const int K = K0 + K1;
+  int S = tn_group_splits(n, M, N, K, mn);
+  int kps = ((K + S - 1) / S + 63) / 64 * 64;
+  if (K1 > 0) {
+    if (K0 % 64) return false;
+    // the multiple-of-64 divisor of K0 nearest the planned split length
+    int best = -1;
+    for (int m = 1; m <= K0 / 64; ++m) {
+      if (K0 % m || (K0 / m) % 64) continue;
+      const int c = K0 / m;
+      if (best < 0 || std::abs(c - kps) < std::abs(best - kps)) best = c;
+    }
+    if (best <= 0) return false;
+    kps = best;
+    S = (K + kps - 1) / kps;
+  }
+  *S_out = S;
+  *kps_out = kps;
+  return true;
+}
+
 // Floats of slab workspace dpfs_gemm_tn_group needs (0: none).  -1: the group does not run
 // grouped (K % 64, unaligned dims, spans past the 32-bit descriptors, the 16x16x32 TN form).
+// K1 > 0: the rows continue in second buffers (lda2 / ldb2) for K1 more rows.
 extern "C" long long dpfs_gemm_tn_group_ws(int n, const int* M, const int* N, const int* lda, const int* ldb, int K,
-                                           const int* acc) {
-  if (n < 1 || n > 4 || K % 64 || !g_g4_m32 || K <= 0) return -1;
+                                           const int* acc, const int* lda2, const int* ldb2, int K1) {
+  if (n < 1 || n > 4 || K % 64 || !g_g4_m32 || K <= 0 || K1 < 0 || (K1 && (K1 % 64 || !lda2 || !ldb2))) return -1;
   bool any_acc = false;
   for (int g = 0; g < n; ++g) {
     if (M[g] <= 0 || N[g] <= 0 || M[g] % 8 || N[g] % 8 || lda[g] < M[g] || ldb[g] < N[g]) return -1;
     if (((long long)(K - 1) * lda[g] + M[g]) * 2 >= (1ll << 32) - 16) return -1;
     if (((long long)(K - 1) * ldb[g] + N[g]) * 2 >= (1ll << 32) - 16) return -1;
+    if (K1) {
+      if (lda2[g] < M[g] || ldb2[g] < N[g] || lda2[g] % 8 || ldb2[g] % 8) return -1;
+      if (((long long)(K1 - 1) * lda2[g] + M[g]) * 2 >= (1ll << 32) - 16) return -1;
+      if (((long long)(K1 - 1) * ldb2[g] + N[g]) * 2 >= (1ll << 32) - 16) return -1;
+    }
     if ((long long)M[g] * N[g] * 4 >= (1ll << 32) - 16) return -1;
     any_acc |= acc[g] != 0;
   }
   long long mn;
-  const int S = tn_group_splits(n, M, N, K, &mn);
+  int S, kps;
+  if (!tn_group_plan(n, M, N, K, K1, &S, &kps, &mn)) return -1;
   return (S > 1 || any_acc) ? (long long)S * mn : 0;
 }
 
 extern "C" int dpfs_gemm_tn_group(int n, const void* const* A, const void* const* B, float* const* C, const int* M,
                                   const int* N, const int* lda, const int* ldb, const int* acc, int K, float* ws,
-                                  long long ws_floats, hipStream_t s) {
-  const long long need = dpfs_gemm_tn_group_ws(n, M, N, lda, ldb, K, acc);
+                                  long long ws_floats, const void* const* A2, const void* const* B2, const int* lda2,
+                                  const int* ldb2, int K1, hipStream_t s) {
+  const long long need = dpfs_gemm_tn_group_ws(n, M, N, lda, ldb, K, acc, lda2, ldb2, K1);
   if (need < 0 || (need > 0 && (ws == nullptr || ws_floats < need))) return 0;
   long long mn;
-  const int S = tn_group_splits(n, M, N, K, &mn);
+  int S, kps;
+  if (!tn_group_plan(n, M, N, K, K1, &S, &kps, &mn)) return 0;
   const bool slabs = need > 0;
-  int kps = (K + S - 1) / S;
-  kps = ((kps + 63) / 64) * 64;
   TnGroup grp{};
   grp.n = n;
+  grp.k_switch = K1 ? K : 0x7fffffff;
   RedGroup red{};
   red.n = n;
   red.S = S;
@@ -1737,6 +1779,14 @@ extern "C" int dpfs_gemm_tn_group(int n, const void* const* A, const void* const
     d.a_bytes = (unsigned)(((long long)(K - 1) * lda[g] + M[g]) * 2);
     d.b_bytes = (unsigned)(((long long)(K - 1) * ldb[g] + N[g]) * 2);
     d.c_bytes = (unsigned)((long long)M[g] * N[g] * 4);
+    if (K1) {
+      d.A2 = (const bf16*)A2[g];
+      d.B2 = (const bf16*)B2[g];
+      d.lda2 = lda2[g];
+      d.ldb2 = ldb2[g];
+      d.a2_bytes = (unsigned)(((long long)(K1 - 1) * lda2[g] + M[g]) * 2);
+      d.b2_bytes = (unsigned)(((long long)(K1 - 1) * ldb2[g] + N[g]) * 2);
+    }
     const long long ng = (long long)M[g] * N[g];
     d.C = slabs ? ws + off : C[g];
     d.slab_stride = slabs ? ng : 0;
@@ -1754,7 +1804,7 @@ extern "C" int dpfs_gemm_tn_group(int n, const void* const* A, const void* const
   const Rope rope = {nullptr, nullptr, 0, 64};
   const Dual dual = {nullptr, nullptr, 0x7fffffff, 0, 0, 0u, 0u};
   gemm4_k<false, false, 1, 0, true, 1, 256, 0, false, false, 0, 0, true, true><<<grid, 256, 0, s>>>(
-      grp.d[0].A, grp.d[0].B, grp.d[0].C, nullptr, 256, 256, K, lda[0], ldb[0], N[0], kps, S, 0, grp.d[0].a_bytes,
+      grp.d[0].A, grp.d[0].B, grp.d[0].C, nullptr, 256, 256, K + K1, lda[0], ldb[0], N[0], kps, S, 0, grp.d[0].a_bytes,
       grp.d[0].b_bytes, grp.d[0].c_bytes, rope, g_g4_group_m, dual, 0, nullptr, SwiOut{}, SwiBwd{}, grp);
   if (slabs) {
     long long gr = (mn / 4 + 255) / 256;

@@ -372,14 +372,15 @@ class DecoderTrainFn(torch.autograd.Function):
             pairs.clear()
 
         def tn_multi(key_dict, groups):
-            """Several weight gradients of one phase ((key, pairs) each): with one chunk, ONE
-            grouped launch (GS.gemm_tn_group, timed against separate calls); else per key."""
-            if all(len(pairs) == 1 for _, pairs in groups):
+            """Several weight gradients of one phase ((key, pairs) each): with one or two chunks,
+            ONE grouped launch (GS.gemm_tn_group, timed against separate calls); else per key."""
+            if all(len(pairs) == 1 for _, pairs in groups) or all(len(pairs) == 2 for _, pairs in groups):
+                # (two chunks: each item's rows continue in the other chunk's buffers)
                 items = []
                 for key, pairs in groups:
                     acc = key_dict.get(key)
                     items.append((pairs[0][0], pairs[0][1], acc if acc is not None else V(key_dict, key),
-                                  acc is not None))
+                                  acc is not None) + (tuple(pairs[1]) if len(pairs) == 2 else ()))
                 outs = GS.gemm_tn_group(k, items)
                 for (key, pairs), o in zip(groups, outs):
                     key_dict[key] = o

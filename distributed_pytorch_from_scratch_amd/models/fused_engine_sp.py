@@ -213,13 +213,15 @@ class DecoderTrainFnSP(torch.autograd.Function):
             pairs.clear()
 
         def tn_multi(d, groups):
-            """A phase's weight gradients ((key, pairs) each): with one chunk ONE grouped launch
-            (GS.gemm_tn_group, timed against separate calls), else per key."""
-            if all(len(pairs) == 1 for _, pairs in groups):
+            """A phase's weight gradients ((key, pairs) each): with one or two chunks ONE grouped
+            launch (GS.gemm_tn_group, timed against separate calls), else per key."""
+            if all(len(pairs) == 1 for _, pairs in groups) or all(len(pairs) == 2 for _, pairs in groups):
+                # (two chunks: each item's rows continue in the other chunk's buffers)
                 items = []
                 for key, pairs in groups:
                     acc = d.get(key)
-                    items.append((pairs[0][0], pairs[0][1], acc if acc is not None else V(d, key), acc is not None))
+                    items.append((pairs[0][0], pairs[0][1], acc if acc is not None else V(d, key), acc is not None)
+                                 + (tuple(pairs[1]) if len(pairs) == 2 else ()))
                 for (key, pairs), o in zip(groups, GS.gemm_tn_group(k, items)):
                     d[key] = o
                     pairs.clear()

@@ -494,33 +494,45 @@ def gemm_tn_pair(k, a0: torch.Tensor, b0: torch.Tensor, a1: torch.Tensor, b1: to
 
 
 def gemm_tn_group(k, items) -> list:
-    """Several weight gradients over the same rows, ``items`` = [(a, b, out, accumulate)]:
-    out (+)= a^T b each.  Candidates, timed per group shape: ``group`` = ONE persistent
-    32x32x16 launch over every GEMM's tiles with one shared K-split length and one slab
-    reduction (``gemm_tn_group``: the launches' ramps / tails and per-GEMM slab round trips of
-    the separate calls are paid once), ``each`` = one :func:`gemm_tn` per item."""
-    outs = [o for _, _, o, _ in items]
+    """Several weight gradients over the same rows, ``items`` = [(a, b, out, accumulate)] or
+    [(a, b, out, accumulate, a1, b1)] (a chunked step: the rows continue in the other ping-pong
+    chunk's buffers): out (+)= a^T b (+ a1^T b1) each.  Candidates, timed per group shape:
+    ``group`` = ONE persistent 32x32x16 launch over every GEMM's tiles with one shared K-split
+    length and one slab reduction (``gemm_tn_group``: the launches' ramps / tails and per-GEMM
+    slab round trips of the separate calls are paid once; with two buffers the split length
+    divides the first one's rows, so no work item straddles them), ``each`` = one
+    :func:`gemm_tn` (:func:`gemm_tn_pair`) per item."""
+    items = [tuple(it) + (None, None) if len(it) == 4 else tuple(it) for it in items]
+    two = items[0][4] is not None
+    outs = [it[2] for it in items]
 
     def each(dsts):
-        return [gemm_tn(k, a, b, d, acc) for (a, b, _, acc), d in zip(items, dsts)]
+        if two:
+            return [gemm_tn_pair(k, a, b, a1, b1, d, acc) for (a, b, _, acc, a1, b1), d in zip(items, dsts)]
+        return [gemm_tn(k, a, b, d, acc) for (a, b, _, acc, _, _), d in zip(items, dsts)]
 
     if (not TN_GROUP or k is reference or len(items) < 2 or any(o is None for o in outs) or not items[0][0].is_cuda
-            or not hasattr(k, "gemm_tn_group") or mode() not in ("auto", "ours")):
+            or not hasattr(k, "gemm_tn_group") or mode() not in ("auto", "ours")
+            or any((it[4] is not None) != two for it in items)):
         return each(outs)
     K = items[0][0].shape[0]
-    if K < _MIN_ROWS or any(a.shape[0] != K or b.shape[0] != K for a, b, _, _ in items):
+    K1 = items[0][4].shape[0] if two else 0
+    if K < _MIN_ROWS or any(it[0].shape[0] != K or it[1].shape[0] != K for it in items) or \
+            (two and any(it[4].shape[0] != K1 or it[5].shape[0] != K1 for it in items)):
         return each(outs)
-    A = [a for a, _, _, _ in items]
-    B = [b for _, b, _, _ in items]
-    acc = [int(bool(x)) for _, _, _, x in items]
-    key = ("tng",) + tuple((a.shape[1], b.shape[1], bool(x)) for a, b, _, x in items) + (K, A[0].device.index)
+    A = [it[0] for it in items]
+    B = [it[1] for it in items]
+    A2 = [it[4] for it in items] if two else None
+    B2 = [it[5] for it in items] if two else None
+    acc = [int(bool(it[3])) for it in items]
+    key = ("tng",) + tuple((a.shape[1], b.shape[1], bool(x)) for a, b, _, x, _, _ in items) + (K, K1, A[0].device.index)
     c = _choice.get(key)
     if c is None:
         scratch = [torch.zeros(a.shape[1], b.shape[1], device=a.device, dtype=torch.float32) for a, b in zip(A, B)]
-        if not k.gemm_tn_group(A, B, scratch, acc):     # the group does not apply to these shapes
+        if not k.gemm_tn_group(A, B, scratch, acc, A2, B2):     # the group does not apply to these shapes
             c = _choice[key] = "each"
         else:
-            c = _pick(key, {"each": lambda: each(scratch), "group": lambda: k.gemm_tn_group(A, B, scratch, acc)})
-    if c == "group" and k.gemm_tn_group(A, B, outs, acc):
+            c = _pick(key, {"each": lambda: each(scratch), "group": lambda: k.gemm_tn_group(A, B, scratch, acc, A2, B2)})
+    if c == "group" and k.gemm_tn_group(A, B, outs, acc, A2, B2):
         return outs
     return each(outs)

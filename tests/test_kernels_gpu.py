@@ -951,6 +951,28 @@ def test_gemm_tn_group(C, shapes, K):
         assert _rel(o, w) < 1e-5
 
 
+@pytest.mark.parametrize("shapes,K0,K1", [([(2304, 768), (768, 768)], 16384, 16384),
+                                           ([(768, 2048), (4096, 768)], 8192, 8192),
+                                           ([(1000, 776), (96, 768), (256, 256)], 2048, 1024),
+                                           ([(384, 768), (768, 128)], 4096, 3072)])
+def test_gemm_tn_group_two_buffers(C, shapes, K0, K1):
+    """A chunked step's weight gradients as ONE grouped launch over both ping-pong chunks' rows
+    (the K-split length divides the first buffer's rows; items past it read the second
+    buffers) against the fp32 oracle, the first GEMM accumulating."""
+    torch.manual_seed(37)
+    A = [torch.randn(K0, m, device=DEV).bfloat16() for m, _ in shapes]
+    B = [torch.randn(K0, n, device=DEV).bfloat16() for _, n in shapes]
+    A2 = [torch.randn(K1, m, device=DEV).bfloat16() for m, _ in shapes]
+    B2 = [torch.randn(K1, n, device=DEV).bfloat16() for _, n in shapes]
+    outs = [torch.randn(m, n, device=DEV) for m, n in shapes]
+    acc = [1] + [0] * (len(shapes) - 1)
+    want = [(o.clone() if a_ else 0) + R.gemm_tn(a.float(), b.float()) + R.gemm_tn(a2.float(), b2.float())
+            for o, a, b, a2, b2, a_ in zip(outs, A, B, A2, B2, acc)]
+    assert C.gemm_tn_group(A, B, outs, acc, A2, B2)
+    for o, w in zip(outs, want):
+        assert _rel(o, w) < 1e-5
+
+
 def test_gemm_tn_group_declines(C):
     a = torch.randn(1000, 256, device=DEV).bfloat16()     # K % 64 != 0: not grouped
     outs = [torch.empty(256, 256, device=DEV)] * 2
