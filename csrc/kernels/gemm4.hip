@@ -1006,14 +1006,15 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   auto stage_rsrc_a = [&]() {
     if constexpr (FAST) {
       const unsigned off = (unsigned)p_t * sta;
-      const unsigned n = (p_t < nlive && p_it < total) ? na0 - off : 0u;
+      // (a two-buffer group's first buffer padded to whole splits: stages past its rows read zeros)
+      const unsigned n = (p_t < nlive && p_it < total && off < na0) ? na0 - off : 0u;
       sra = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ia + off), (short)0, (int)n, 0x00020000);
     }
   };
   auto stage_rsrc_b = [&]() {
     if constexpr (FAST) {
       const unsigned off = (unsigned)p_t * stb;
-      const unsigned n = (p_t < nlive && p_it < total) ? nb0 - off : 0u;
+      const unsigned n = (p_t < nlive && p_it < total && off < nb0) ? nb0 - off : 0u;
       srb = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ib + off), (short)0, (int)n, 0x00020000);
     }
   };
@@ -1697,25 +1698,43 @@ static int tn_group_splits(int n, const int* M, const int* N, int K, long long* 
   return best;
 }
 
-// The group's K-split plan: S splits of kps rows (a multiple of 64) over K = K0 + K1 rows; with
-// a second buffer (K1 > 0) kps also divides K0, so no work item straddles the two buffers.
-// Returns false where no plan fits.
-static bool tn_group_plan(int n, const int* M, const int* N, int K0, int K1, int* S_out, int* kps_out, long long* mn) {
+// The group's K-split plan: S splits of kps rows (a multiple of 64) over K = K0 + K1 rows.
+// With a second buffer (K1 > 0) each buffer is split on its own -- S0 splits over K0 and S1
+// over K1 with one kps -- and the kernel sees K0 padded to S0 kps (*kswitch): no work item
+// straddles the buffers, and the padding rows past K0 read zeros (past the first buffers'
+// descriptors).  S0 / S1 by the same makespan model as tn_group_splits.
+static bool tn_group_plan(int n, const int* M, const int* N, int K0, int K1, int* S_out, int* kps_out, long long* mn,
+                          int* kswitch) {
   const int K = K0 + K1;
   int S = tn_group_splits(n, M, N, K, mn);
   int kps = ((K + S - 1) / S + 63) / 64 * 64;
+  *kswitch = 0x7fffffff;
   if (K1 > 0) {
-    if (K0 % 64) return false;
-    // the multiple-of-64 divisor of K0 nearest the planned split length
-    int best = -1;
-    for (int m = 1; m <= K0 / 64; ++m) {
-      if (K0 % m || (K0 / m) % 64) continue;
-      const int c = K0 / m;
-      if (best < 0 || std::abs(c - kps) < std::abs(best - kps)) best = c;
+    if (K0 % 64 || K1 % 64) return false;
+    long long tiles = 0;
+    for (int g = 0; g < n; ++g) tiles += (long long)((M[g] + 255) / 256) * ((N[g] + 255) / 256);
+    const int cus = g4_cu_count();
+    double best_t = 1e300;
+    int bS = 0, bk = 0, bs0 = 0;
+    for (int S0 = 1; S0 <= 32; ++S0) {
+      const int S1 = std::max(1, (int)((double)S0 * K1 / K0 + 0.5));
+      const int k0 = ((K0 + S0 - 1) / S0 + 63) / 64 * 64, k1 = ((K1 + S1 - 1) / S1 + 63) / 64 * 64;
+      const int kp = std::max(k0, k1);
+      if (S0 + S1 > 2 && kp < 512) break;
+      const int s0 = (K0 + kp - 1) / kp, s1 = (K1 + kp - 1) / kp;
+      const long long rounds = (tiles * (s0 + s1) + cus - 1) / cus;
+      const double t = (double)rounds * kp * 1.95 + (double)(s0 + s1) * (*mn) * 8.0 / 4.0e6;
+      if (t < best_t * 0.97) {
+        best_t = t;
+        bS = s0 + s1;
+        bk = kp;
+        bs0 = s0;
+      }
     }
-    if (best <= 0) return false;
-    kps = best;
-    S = (K + kps - 1) / kps;
+    if (bS <= 0) return false;
+    S = bS;
+    kps = bk;
+    *kswitch = bs0 * bk;
   }
   *S_out = S;
   *kps_out = kps;
@@ -1742,8 +1761,8 @@ extern "C" long long dpfs_gemm_tn_group_ws(int n, const int* M, const int* N, co
     any_acc |= acc[g] != 0;
   }
   long long mn;
-  int S, kps;
-  if (!tn_group_plan(n, M, N, K, K1, &S, &kps, &mn)) return -1;
+  int S, kps, ksw;
+  if (!tn_group_plan(n, M, N, K, K1, &S, &kps, &mn, &ksw)) return -1;
   return (S > 1 || any_acc) ? (long long)S * mn : 0;
 }
 
@@ -1754,12 +1773,12 @@ extern "C" int dpfs_gemm_tn_group(int n, const void* const* A, const void* const
   const long long need = dpfs_gemm_tn_group_ws(n, M, N, lda, ldb, K, acc, lda2, ldb2, K1);
   if (need < 0 || (need > 0 && (ws == nullptr || ws_floats < need))) return 0;
   long long mn;
-  int S, kps;
-  if (!tn_group_plan(n, M, N, K, K1, &S, &kps, &mn)) return 0;
+  int S, kps, ksw;
+  if (!tn_group_plan(n, M, N, K, K1, &S, &kps, &mn, &ksw)) return 0;
   const bool slabs = need > 0;
   TnGroup grp{};
   grp.n = n;
-  grp.k_switch = K1 ? K : 0x7fffffff;
+  grp.k_switch = ksw;   // (K1 > 0: K0 padded to whole splits; else none)
   RedGroup red{};
   red.n = n;
   red.S = S;
@@ -1804,7 +1823,8 @@ extern "C" int dpfs_gemm_tn_group(int n, const void* const* A, const void* const
   const Rope rope = {nullptr, nullptr, 0, 64};
   const Dual dual = {nullptr, nullptr, 0x7fffffff, 0, 0, 0u, 0u};
   gemm4_k<false, false, 1, 0, true, 1, 256, 0, false, false, 0, 0, true, true><<<grid, 256, 0, s>>>(
-      grp.d[0].A, grp.d[0].B, grp.d[0].C, nullptr, 256, 256, K + K1, lda[0], ldb[0], N[0], kps, S, 0, grp.d[0].a_bytes,
+      grp.d[0].A, grp.d[0].B, grp.d[0].C, nullptr, 256, 256, K1 ? ksw + K1 : K, lda[0], ldb[0], N[0], kps, S, 0,
+      grp.d[0].a_bytes,
       grp.d[0].b_bytes, grp.d[0].c_bytes, rope, g_g4_group_m, dual, 0, nullptr, SwiOut{}, SwiBwd{}, grp);
   if (slabs) {
     long long gr = (mn / 4 + 255) / 256;

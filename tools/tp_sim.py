@@ -128,3 +128,7 @@ def main():
 
 if __name__ == "__main__":
     main()
+    if os.environ.get("DPFS_SHOW_GEMM") == "1":     # per-shape GEMM choices (ms)
+        from distributed_pytorch_from_scratch_amd.ops import gemm_select
+        for key, v in sorted(gemm_select.choices(with_times=True).items(), key=str):
+            print(f"[gemm] {key} -> {v}", file=sys.stderr, flush=True)
