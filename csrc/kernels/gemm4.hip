@@ -319,8 +319,8 @@ struct TnGemm {
 };
 struct TnGroup {
   int n, total;
-  int k_switch;   // rows of the first buffers (0x7fffffff: one buffer); a multiple of kps
-  int pad;
+  int k_switch;   // the first buffers' rows padded to whole splits (0x7fffffff: one buffer)
+  int k0;         // the first buffers' rows (0x7fffffff: one buffer)
   TnGemm d[4];
 };
 
@@ -903,6 +903,9 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
       const TnGemm& d = grp.d[g];
       Item x = decode<BN>(lin - d.item0, d.tiles_m * d.tiles_n, d.tiles_m, d.tiles_n, group_m, K, kps, grp.k_switch);
       x.g = g;
+      // a two-buffer group's first buffer is padded to whole splits: its last split ends at the
+      // buffer's rows (the padding stages are past nlive: zeros, no record-count underflow)
+      if (x.sel == 0 && x.ke > grp.k0) x.ke = grp.k0;
       return x;
     } else {
       return decode<BN>(lin, nwg, tiles_m, tiles_n, group_m, K, kps, dual.k_switch);
@@ -1006,15 +1009,14 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   auto stage_rsrc_a = [&]() {
     if constexpr (FAST) {
       const unsigned off = (unsigned)p_t * sta;
-      // (a two-buffer group's first buffer padded to whole splits: stages past its rows read zeros)
-      const unsigned n = (p_t < nlive && p_it < total && off < na0) ? na0 - off : 0u;
+      const unsigned n = (p_t < nlive && p_it < total) ? na0 - off : 0u;
       sra = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ia + off), (short)0, (int)n, 0x00020000);
     }
   };
   auto stage_rsrc_b = [&]() {
     if constexpr (FAST) {
       const unsigned off = (unsigned)p_t * stb;
-      const unsigned n = (p_t < nlive && p_it < total && off < nb0) ? nb0 - off : 0u;
+      const unsigned n = (p_t < nlive && p_it < total) ? nb0 - off : 0u;
       srb = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ib + off), (short)0, (int)n, 0x00020000);
     }
   };
@@ -1779,6 +1781,7 @@ extern "C" int dpfs_gemm_tn_group(int n, const void* const* A, const void* const
   TnGroup grp{};
   grp.n = n;
   grp.k_switch = ksw;   // (K1 > 0: K0 padded to whole splits; else none)
+  grp.k0 = K1 ? K : 0x7fffffff;
   RedGroup red{};
   red.n = n;
   red.S = S;
