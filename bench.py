@@ -69,7 +69,8 @@ def parse():
     ap.add_argument("--pg-timeout-s", type=float, default=240.0,
                     help="process-group (RCCL watchdog) timeout, well under the driver's lease")
     ap.add_argument("--fp8", action="store_true",
-                    help="fp8 (e4m3 / e5m2) forward and data-gradient GEMMs (ops/fp8.py); NOT the bf16 headline")
+                    help="fp8 (e4m3 / e5m2) forward and data-gradient GEMMs on hipBLASLt fp8 kernels (ops/fp8.py); "
+                         "NOT the bf16 headline")
     return ap.parse_args()
 
 
@@ -128,7 +129,8 @@ def measure(a, tp: int, world: int, dev, first: bool):
     # HBM plan (utils/memory.py) before anything is allocated: recompute on only where the
     # layout does not fit without it; a layout that does not fit at all is refused here.
     from distributed_pytorch_from_scratch_amd.utils import memory as MEM
-    lay = MEM.Layout(tp=tp, dp=p.dp_size, sp=False, seq=T, batch=lb, chunks=2 if tp > 1 else 1)
+    lay = MEM.Layout(tp=tp, dp=p.dp_size, sp=bool(args.sequence_parallel), seq=T, batch=lb,
+                     chunks=2 if tp > 1 else 1)
     want = {"auto": None, "on": True, "off": False}[a.recompute]
     free = MEM.device_free_bytes() if dev.type == "cuda" else None
     rc, est = MEM.plan(args, lay, free, want) if a.impl == "ours" else (False, MEM.estimate(args, lay))
@@ -240,7 +242,11 @@ def measure(a, tp: int, world: int, dev, first: bool):
         parallelism=f"tp{tp}" + (f"dp{p.dp_size}" if p.dp_size > 1 else "") + ("+sp" if sp_used else ""),
         final_loss=float(loss.float().item()), tp_comm=tp_comm.info(),
         chunks=model.overlap_chunks() if a.impl == "ours" else None, recompute=bool(rc),
-        peak_mem_gb_est=round(est.gb(), 2),
+        # the measured peak is the max over every engine configuration the trial ran: estimate
+        # each of them with its own SP / chunk setting and report the max alike
+        peak_mem_gb_est=round(max(MEM.estimate(args, MEM.Layout(**{**lay.__dict__, "sp": bool(k[0]),
+                                                                      "chunks": int(k[1]), "recompute": bool(rc)})).gb()
+                                  for k in (trial or [None])) if trial else est.gb(), 2),
         peak_mem_gb=round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2) if dev.type == "cuda" else None,
         trial={f"{'sp' if k[0] else 'nosp'}/c{k[1]}": round(1000 * v, 2) for k, v in trial.items()} or None)
     del model, opt, pool

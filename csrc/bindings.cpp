@@ -42,6 +42,8 @@ void dpfs_gemm_v2_sched(int);
 void dpfs_gemm_set_workspace(float*, long long);
 long long dpfs_gemm_bf16_ws(int, int, int);
 long long dpfs_gemm4_sk_ws(int, int, int);
+int dpfs_gemm4_sk_error(int);
+void dpfs_gemm4_sk_starve(int);
 void dpfs_gemm_tn(const void*, const void*, float*, float*, int, int, int, int, int, int, int, hipStream_t);
 int dpfs_gemm_tn2(const void*, const void*, const void*, const void*, float*, float*, int, int, int, int, int, int, int,
                   int, int, int, hipStream_t);
@@ -93,6 +95,12 @@ int dpfs_attn_bwd(const void*, const void*, const void*, const void*, const void
                    void*, int, int, int, int, long long, long long, long long, long long, long long, long long,
                    long long, long long, float, int, const int64_t*, const float*, hipStream_t, float*, float*, int);
 long long dpfs_attn_bias_ws(int, int, int, int);
+long long dpfs_attn_fused_ws(int, int, int, int);
+long long dpfs_attn_fused_bias_ws(int, int, int, int);
+int dpfs_attn_bwd_fused(const void*, const void*, const void*, const void*, const void*, const float*, float*, float*,
+                        void*, void*, void*, int, int, int, int, long long, long long, long long, long long, long long,
+                        long long, long long, long long, float, int, const int64_t*, const float*, hipStream_t, float*,
+                        float*);
 // kernels/decode.hip
 int dpfs_decode_nsplit(int);
 void dpfs_attn_decode(const void*, long long, const void*, const void*, const int*, void*, long long, float*, int, int,
@@ -761,6 +769,17 @@ bool attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tenso
     rt = rope_tab->data_ptr<float>();
   }
   auto delta = torch::empty({2, B, H, T}, lse.options());   // -delta | -lse/scale
+  if (impl == 6 && dpfs_attn_fused_ws((int)B, (int)T, (int)H, (int)hd) > 0) {
+    // fused backward (head_dim 64): fp32 dQ partials per (b, h, 256-key block, 64-query tile)
+    auto dqp = torch::empty({dpfs_attn_fused_ws((int)B, (int)T, (int)H, (int)hd)}, lse.options());
+    torch::Tensor fb;
+    if (db) fb = torch::empty({dpfs_attn_fused_bias_ws((int)B, (int)T, (int)H, (int)hd)}, lse.options());
+    return dpfs_attn_bwd_fused(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                               lse.data_ptr<float>(), delta.data_ptr<float>(), dqp.data_ptr<float>(), dq.data_ptr(),
+                               dk.data_ptr(), dv.data_ptr(), (int)B, (int)T, (int)H, (int)hd, vdo.ld, vq.ld, vk.ld,
+                               vv.ld, vo.ld, vdq.ld, vdk.ld, vdv.ld, (float)scale, causal ? 1 : 0, rp, rt, stream(), db,
+                               db ? fb.data_ptr<float>() : nullptr) > 0;
+  }
   torch::Tensor bws;
   if (db) bws = torch::empty({dpfs_attn_bias_ws((int)B, (int)T, (int)H, (int)hd)}, lse.options());
   return dpfs_attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
@@ -1357,6 +1376,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "head_dim-64 attention backward, next block's operands fetched ahead: bit 0 = dK/dV, bit 1 = dQ (3 default; A/B)");
   m.def("gemm4_swb_depth", [](int v) { dpfs_gemm4_swb_depth(v); },
         "SwiGLU-backward epilogue of the down-projection dgrad: gate / up row blocks in flight (2 default, 1 = A/B)");
+  m.def("gemm_sk_error", [](bool reset) { return dpfs_gemm4_sk_error(reset ? 1 : 0); }, py::arg("reset") = false,
+        "sticky host-mapped word: 1 when a stream-K consumer's bounded wait for its producer's partial timed out "
+        "(that GEMM's output is wrong); read without a device sync");
+  m.def("gemm_sk_starve", [](bool on) { dpfs_gemm4_sk_starve(on ? 1 : 0); },
+        "test hook: the next stream-K launch's producers never raise their flags, so every consumer wait times out");
   m.def("gemm_sk_applies", [](int64_t M, int64_t N, int64_t K) { return dpfs_gemm4_sk_ws((int)M, (int)N, (int)K) > 0; },
         "whether the stream-K bf16 kernel (variant 8 / 12) applies to an M x N x K NT / NN GEMM on this device");
   m.def("gemm4_m32k", [](int v) { dpfs_gemm4_m32k(v); },
@@ -1406,7 +1430,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rope_pos") = py::none(), py::arg("rope_tab") = py::none(), py::arg("dbias") = py::none(),
         py::arg("impl") = 0,
         "flash attention backward; impl (per call): 0 = auto (dq3 + dkdv3 at hd 64 / 128, dq + dkdv2 at hd 32), "
-        "2 = dq + dkdv2 (16x16x32), 4 = dq3 + dkdv3 (32x32x16), 5 = 4 with the dK/dV DIAG build");
+        "2 = dq + dkdv2 (16x16x32), 4 = dq3 + dkdv3 (32x32x16), 5 = 4 with the dK/dV DIAG build, 6 = the fused "
+        "head_dim-64 backward (delta pass, one dK/dV/dQ kernel, dQ partial reduction)");
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd_sorted", &embedding_bwd_sorted, py::arg("dout"), py::arg("ids"), py::arg("v_local"),
         py::arg("vocab_start"), py::arg("out") = py::none(), py::arg("accumulate") = false,

@@ -296,8 +296,9 @@ struct Item {
 struct SkArgs {
   float* part;        // [E][4 waves][64 x 64 lanes x 4] fp32, lane-linear per wave
   unsigned* flags;    // [E][4 waves], zeroed before the launch; 1 = partial written
-  unsigned* err;      // set to 1 when a wait timed out
+  unsigned* err;      // host-mapped, sticky: set to 1 when a wait timed out (dpfs_gemm4_sk_error)
   int extra;          // E
+  int starve;         // test hook: producers never raise their flags (every wait times out)
 };
 constexpr int kAuxSys = 1 | 16;   // sc0 | sc1: write-through stores, L2-bypassing loads
 
@@ -457,7 +458,7 @@ __device__ __forceinline__ void epilogue_sk_part(const SkArgs& sk, int e, int wa
     });
   });
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (l == 0) __hip_atomic_store(sk.flags + e * 4 + wave, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (l == 0 && !sk.starve) __hip_atomic_store(sk.flags + e * 4 + wave, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Stream-K, second K half (SK role 2): wait (bounded) for the first half's partial.
@@ -1460,6 +1461,39 @@ extern "C" void dpfs_gemm4_set_sk_ws(float* p, long long n) {
   g_g4_sk_ws = p;
   g_g4_sk_ws_floats = n;
 }
+// Sticky error word of the stream-K hand-off: host-mapped (the host reads it without a device
+// sync) and never cleared by a launch, so a consumer whose bounded wait for its producer's
+// partial timed out (its tile is then wrong) is reported by the next dpfs_gemm4_sk_error()
+// (ops.check_device_errors(), called by the engines after every step) instead of passing
+// silently.  Allocated on the first stream-K launch.
+static unsigned* g_g4_sk_err_host = nullptr;
+static unsigned* g_g4_sk_err_dev = nullptr;
+static unsigned* sk_err_word() {
+  if (!g_g4_sk_err_dev) {
+    unsigned* p = nullptr;
+    if (hipHostMalloc((void**)&p, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return nullptr;
+    *p = 0u;
+    unsigned* d = nullptr;
+    if (hipHostGetDevicePointer((void**)&d, p, 0) != hipSuccess) {
+      hipHostFree(p);
+      return nullptr;
+    }
+    g_g4_sk_err_host = p;
+    g_g4_sk_err_dev = d;
+  }
+  return g_g4_sk_err_dev;
+}
+extern "C" int dpfs_gemm4_sk_error(int reset) {
+  if (!g_g4_sk_err_host) return 0;
+  const int v = (int)__atomic_load_n(g_g4_sk_err_host, __ATOMIC_RELAXED);
+  if (reset) __atomic_store_n(g_g4_sk_err_host, 0u, __ATOMIC_RELAXED);
+  return v;
+}
+// Test hook: the next stream-K launch runs its consumers with their producers' flags never
+// set (the producers skip the flag store), so every consumer's wait times out.
+static int g_g4_sk_starve = 0;
+extern "C" void dpfs_gemm4_sk_starve(int on) { g_g4_sk_starve = on; }
 
 // Launch v4.  layout: 0 = NT (A K-major, B K-major), 1 = NN (B MN-major), 2 = TN (both
 // MN-major, fp32 out).  Returns false (nothing launched) when a span does not fit the 32-bit
@@ -1596,8 +1630,11 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
       SkArgs sk;
       sk.part = g_g4_sk_ws;
       sk.flags = reinterpret_cast<unsigned*>(g_g4_sk_ws + (long long)E * 4 * 16384);
-      sk.err = sk.flags + E * 4;
+      sk.err = sk_err_word();
+      if (!sk.err) return false;
       sk.extra = E;
+      sk.starve = g_g4_sk_starve;
+      g_g4_sk_starve = 0;
       if (hipMemsetAsync(sk.flags, 0, (size_t)(E * 4 + 1) * 4, s) != hipSuccess) return false;
 #define G4_SK(AK_, BK_, SA_)                                                                                  \
   gemm4_k<AK_, BK_, 0, 0, true, 1, 256, 0, false, 0, 0, SA_, false, false, true><<<cus, 256, 0, s>>>(       \

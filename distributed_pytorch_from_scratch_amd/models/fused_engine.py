@@ -40,6 +40,7 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
+from ..ops import _ext
 from ..ops import fp8 as F8
 from ..ops import gemm_select as GS
 from ..ops import reference
@@ -163,6 +164,7 @@ def collect_params(model) -> List[Optional[torch.Tensor]]:
 
 
 _LAYER_KEYS = ("s1", "wqkv", "bqkv", "wo", "bo", "s2", "wgu", "bgu", "wd", "bd")
+_SP_REP = ("s1", "bo", "s2", "bd")   # replicated under SP (layers.py sequence_parallel_grad)
 
 
 def arena_groups(model, layers, sp: bool):
@@ -174,8 +176,14 @@ def arena_groups(model, layers, sp: bool):
     lay = lambda li: (f"L{li}", list(zip(_LAYER_KEYS, layers[li].params())))
     nL = len(layers)
     if sp:
-        return ([("head", [("lm_w", head.weight), ("lm_b", head.bias)])] + [lay(li) for li in range(nL - 1, -1, -1)]
-                + [("tail", [("emb", model.embedding.weight), ("nf", model.norm.scale)])])
+        # the replicated gradients (norm scales, row-parallel biases: summed over TP after the
+        # step) are stored together in one trailing range, "sprep", so that sum is one in-place
+        # all-reduce of the arena (grad_sync.allreduce_sequence_parallel_grads)
+        rep = lambda li: [((f"L{li}", k), q) for k, q in zip(_LAYER_KEYS, layers[li].params()) if k in _SP_REP]
+        own = lambda li: (f"L{li}", [(k, q) for k, q in zip(_LAYER_KEYS, layers[li].params()) if k not in _SP_REP])
+        return ([("head", [("lm_w", head.weight), ("lm_b", head.bias)])] + [own(li) for li in range(nL - 1, -1, -1)]
+                + [("tail", [("emb", model.embedding.weight)])]
+                + [("sprep", [x for li in range(nL - 1, -1, -1) for x in rep(li)] + [(("tail", "nf"), model.norm.scale)])])
     return ([("head", [("nf", model.norm.scale), ("lm_w", head.weight), ("lm_b", head.bias)])]
             + [lay(li) for li in range(nL - 1, 0, -1)] + [("emb", [("emb", model.embedding.weight)]), lay(0)])
 
@@ -411,6 +419,13 @@ class DecoderTrainFn(torch.autograd.Function):
             dl = s["logits"]
             if s.pop("ce_done", False):     # d logits (and its column sums) came with the forward
                 db = s.pop("ce_db")
+                # the forward assumed a unit loss gradient (loss(unit_grad=True)); a caller that
+                # scaled the loss afterwards would get unscaled gradients.  Checking the value
+                # costs a host sync, so it runs in the debug modes (DPFS_SYNC_DEBUG / NAN_CHECK)
+                if ci == 0 and (_ext.debug_sync() or _ext.nan_check()) and not bool((gloss == 1).all()):
+                    raise RuntimeError("loss(unit_grad=True) was differentiated with a non-unit gradient "
+                                       f"({float(gloss.float().mean())}); call loss() without unit_grad when "
+                                       "scaling the loss")
             else:
                 gs = s["valid"].float() * gscale_all
                 db = first(g, "lm_b", dl, dl.size(1)) if head.bias is not None else None

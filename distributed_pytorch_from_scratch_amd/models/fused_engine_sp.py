@@ -362,6 +362,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
             del s["gfull"]
         g["emb"] = ev
         dp_reduce("tail")
+        dp_reduce("sprep")
         _defer_end()
         tp_comm.check()
         if dpb.finish():

@@ -65,6 +65,17 @@ def require():
     return _C
 
 
+def check_device_errors() -> None:
+    """Raise if a kernel reported an error through a host-mapped word (read without a device
+    sync): the stream-K GEMM's bounded producer wait timed out, so that GEMM's output is wrong
+    (``gemm4.hip`` ``sk_wait``).  The word is sticky; it is reset once reported."""
+    if _C is None or not hasattr(_C, "gemm_sk_error"):
+        return
+    if _C.gemm_sk_error(True):
+        raise RuntimeError("stream-K GEMM: a consumer workgroup's wait for its producer's fp32 partial timed out "
+                           "(2 s); the GEMM output of that launch is invalid")
+
+
 def so_path() -> str | None:
     _load()
     return getattr(_C, "__file__", None) if _C is not None else None

@@ -23,6 +23,12 @@ def K(t: torch.Tensor, dtype: "torch.dtype | None" = None):
     return reference
 
 
+def native_fp32() -> bool:
+    """Whether fp32 compute on the GPU runs on the native kernel set (fp32 MFMA GEMMs, fp32
+    flash attention) rather than the PyTorch oracle with materialised attention scores."""
+    return False
+
+
 def shadow(p: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     """Low-precision compute copy of an fp32 master parameter.
 

@@ -144,7 +144,9 @@ class GradArena:
             for key, p in items:
                 if p is None:
                     continue
-                self.slots[(name, key)] = (off, tuple(p.shape))
+                # a tuple key names the slot explicitly: (group, key) of another group whose
+                # gradient is stored in this group's range (the SP replicated gradients)
+                self.slots[key if isinstance(key, tuple) else (name, key)] = (off, tuple(p.shape))
                 off += p.numel()
             self.ranges[name] = (start, off)
         self.numel = off
@@ -213,8 +215,12 @@ class DPBucketer:
         if self.before_launch is not None:
             self.before_launch()
         sl = self.arena.buf[self._lo:self._hi]
-        h = dist.all_reduce(sl, group=self.group, async_op=True)
-        self._pending.append((h, sl))
+        # RCCL averages in the collective (ncclAvg): no separate pass over the gradients;
+        # gloo has no AVG, so it sums and the bucket is divided after the wait
+        avg = _has_avg(self.group)
+        h = dist.all_reduce(sl, op=dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM, group=self.group,
+                            async_op=True)
+        self._pending.append((h, sl, avg))
         self._lo = self._hi = None
         self.launches += 1
 
@@ -223,9 +229,10 @@ class DPBucketer:
         reduced."""
         self._launch()
         done = bool(self._pending)
-        for h, sl in self._pending:
+        for h, sl, avg in self._pending:
             h.wait()
-            sl.div_(self.dp)
+            if not avg:
+                sl.div_(self.dp)
         self._pending = []
         return done
 
@@ -242,10 +249,29 @@ def _flat_allreduce(tensors: List[torch.Tensor], group, average_by: int = 1) -> 
     torch._foreach_copy_(tensors, [q.view_as(t) for q, t in zip(parts, tensors)])
 
 
+def _has_avg(group) -> bool:
+    """``ReduceOp.AVG`` exists on the NCCL (= RCCL) backend only."""
+    try:
+        return dist.get_backend(group) == "nccl"
+    except Exception:
+        return False
+
+
 def allreduce_sequence_parallel_grads(model: torch.nn.Module) -> None:
     p = pm.pgm
     if p is None or p.tp_size == 1:
         return
+    a = getattr(model, "_dpfs_grad_arena", None)
+    if a is not None and "sprep" in a.ranges:
+        # the SP fused engine keeps every replicated gradient in one contiguous arena range
+        # ("sprep", fused_engine.arena_groups): one in-place all-reduce, no pack / copy back
+        lo, hi = a.ranges["sprep"]
+        rep = [q for q in model.parameters() if getattr(q, "sequence_parallel_grad", False) and q.grad is not None]
+        base, end = a.buf.data_ptr(), a.buf.data_ptr() + 4 * a.numel
+        if rep and all(base + 4 * lo <= q.grad.data_ptr() < base + 4 * hi for q in rep):
+            if hi > lo:
+                dist.all_reduce(a.buf[lo:hi], group=p.tp_group)
+            return
     grads = [q.grad for q in model.parameters()
              if getattr(q, "sequence_parallel_grad", False) and q.grad is not None]
     _flat_allreduce(grads, p.tp_group)

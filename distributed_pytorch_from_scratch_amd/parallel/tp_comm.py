@@ -519,7 +519,10 @@ def staging(slot: int, shape, dtype: torch.dtype, op: str = "all_reduce") -> Opt
 
 def check():
     """Raise if any xGMI call of this process timed out (one host-mapped word) or the native
-    RCCL communicator reported an asynchronous error."""
+    RCCL communicator reported an asynchronous error.  Also raises on the kernels' own
+    host-mapped error words (the stream-K GEMM hand-off, ``_ext.check_device_errors``)."""
+    from ..ops import _ext
+    _ext.check_device_errors()
     p = pm.pgm
     if p is None:
         return

@@ -30,6 +30,7 @@ from .constants import IGNORE_INDEX
 from .data.dataset import get_dataloader, get_synthetic_dataloader, resume_position, seek
 from .engine import TrainStep
 from .models import Transformer, get_preset
+from .ops.dispatch import native_fp32 as K_native_fp32
 from .ops.optim import FusedAdam
 from .parallel import process_manager as pm
 from .utils import checkpoint as ck
@@ -73,7 +74,8 @@ def get_train_args(argv=None) -> Namespace:
                    help="bf16 compute on the MI355X MFMA kernels (default fp32, as the reference: on the GPU the "
                         "fp32 PyTorch kernel set)")
     g.add_argument("--fp8", action="store_true",
-                   help="fp8 (e4m3 / e5m2) GEMMs for the large projections (ops/fp8.py); bf16 elsewhere")
+                   help="fp8 (e4m3 / e5m2) GEMMs for the large projections, run on hipBLASLt fp8 kernels "
+                        "(ops/fp8.py; quantisation on our HIP kernels); bf16 elsewhere")
     g.add_argument("--max_grad_norm", type=float, default=None)
     g.add_argument("--resume", type=str, default=None, help="checkpoint path, or 'latest'")
     g = p.add_argument_group("model")
@@ -121,8 +123,10 @@ def train(rank, args: Namespace):
     # does not fit without it; a layout that does not fit at all is refused with the numbers.
     rc = getattr(args, "recompute", "auto")
     rc = {"auto": None, "on": True, "off": False}.get(rc, rc if isinstance(rc, bool) else None)
+    fp32 = compute_dtype == torch.float32
     lay = MEM.Layout(tp=p.tp_size, dp=p.dp_size, sp=args.sp, seq=seq_len, batch=args.batch_size,
-                     chunks=2 if p.tp_size > 1 else 1)
+                     chunks=2 if p.tp_size > 1 else 1, compute="fp32" if fp32 else "bf16",
+                     materialized_attention=fp32 and not K_native_fp32())
     rc, est = MEM.plan(margs, lay, MEM.device_free_bytes(dev) if use_cuda else None, rc)
     margs = replace(margs, recompute=bool(rc))
     log0(f"HBM plan: peak {est.gb():.2f} GiB per rank estimated ({est.phase}), recompute={'on' if rc else 'off'}")

@@ -45,6 +45,19 @@ class Layout:
     chunks: int = 1            # ping-pong chunks of the fused engine
     recompute: bool = False
     tp_rank: int = 0           # the rank to size (uneven head / vocab shards: use the largest)
+    compute: str = "bf16"      # "bf16" | "fp32": activation bytes; fp32 keeps no bf16 shadows
+    materialized_attention: bool = False   # the PyTorch oracle path: (B, H, T, T) fp32 scores
+
+
+def xgmi_staging_bytes(tp: int, cap_mb: Optional[int] = None, nslots: int = 4) -> int:
+    """Bytes ``csrc/comm/xgmi.hip`` ``dpfs_xgmi_create`` allocates per rank: nslots staging
+    slots + the copy-in and temporary regions (nslots + 2 capacities) + two one-shot input
+    regions of min(capacity, 16 MiB); the capacity is ``DPFS_XGMI_CAP_MB`` (256 default)."""
+    if tp <= 1:
+        return 0
+    import os
+    cap = (cap_mb if cap_mb is not None else int(os.environ.get("DPFS_XGMI_CAP_MB", "256"))) << 20
+    return (nslots + 2) * cap + 2 * min(cap, 16 << 20)
 
 
 @dataclass
@@ -77,8 +90,11 @@ def _tn_splits(M: int, N: int, K: int) -> int:
     return best
 
 
-def estimate(args: ModelArgs, lay: Layout, act_bytes: int = 2) -> Estimate:
-    """Peak bytes allocated on one rank during a steady-state training step."""
+def estimate(args: ModelArgs, lay: Layout, act_bytes: Optional[int] = None) -> Estimate:
+    """Peak bytes allocated on one rank during a steady-state training step.  ``act_bytes``
+    defaults from ``lay.compute`` (2 for bf16, 4 for fp32)."""
+    if act_bytes is None:
+        act_bytes = 4 if lay.compute == "fp32" else 2
     n, r = lay.tp, min(lay.tp_rank, lay.tp - 1)
     d, F, L, hd = args.attn_dim, args.ffn_dim, args.num_layers, args.head_dim
     dl = partition_sizes(d, n, hd)[r]                  # this rank's attention width (heads x hd)
@@ -93,7 +109,7 @@ def estimate(args: ModelArgs, lay: Layout, act_bytes: int = 2) -> Estimate:
     P = L * p_layer + 2 * Vl * d + b * Vl + d * (2 if args.norm == "layernorm" else 1)
     parts: Dict[str, int] = {}
     parts["master_fp32"] = 4 * P
-    parts["shadow_bf16"] = 2 * w2d
+    parts["shadow_bf16"] = 2 * w2d if lay.compute != "fp32" else 0
     parts["adam_m_v_fp32"] = 8 * P
     parts["grad_arena_fp32"] = 4 * P
     static = parts["master_fp32"] + parts["shadow_bf16"] + parts["adam_m_v_fp32"] + parts["grad_arena_fp32"]
@@ -122,8 +138,16 @@ def estimate(args: ModelArgs, lay: Layout, act_bytes: int = 2) -> Estimate:
         _tn_splits(2 * Fl, d, M) * 2 * Fl * d, _tn_splits(3 * dl, d, M) * 3 * dl * d,
         _tn_splits(d, Fl, M) * d * Fl, _tn_splits(d, dl, M) * d * dl)
     rebuilt = per_layer if lay.recompute else 0
+    if lay.materialized_attention:
+        # the oracle keeps every layer's (tokens x T) fp32 probabilities for its backward, and
+        # one layer's scores + probabilities + their gradient transiently
+        heads_l = dl // hd
+        scores = 4 * M * lay.seq * heads_l
+        parts["attention_scores"] = L * scores
+        acts += L * scores
+        layer_tmp += 2 * scores
     parts["bwd_transient"] = max(lm_tn + a * M * d, layer_tmp + rebuilt)
-    parts["xgmi_staging"] = (4 * (256 << 20)) if n > 1 else 0
+    parts["xgmi_staging"] = xgmi_staging_bytes(n)
     fwd_peak = static + acts + head + parts["xgmi_staging"]
     bwd_peak = static + acts + head + parts["bwd_transient"] + parts["xgmi_staging"]
     est = Estimate(parts=parts)

@@ -314,6 +314,62 @@ def test_attention_bwd_cross_block_prefetch_is_bit_identical(C, B, T, H):
     assert _rel(dq, rq) < 3e-2 and _rel(dk, rk) < 3e-2 and _rel(dv, rv) < 3e-2
 
 
+@pytest.mark.parametrize("B,T,H,causal", [(2, 1024, 3, True), (1, 1000, 2, True), (3, 777, 1, True),
+                                           (1, 192, 2, True), (1, 64, 1, True), (2, 2048, 1, True),
+                                           (2, 256, 2, False), (1, 300, 2, False), (1, 130, 1, False)])
+def test_attention_bwd_fused6(C, B, T, H, causal):
+    """The fused head_dim-64 backward (impl 6: delta pass, one dK / dV / dQ kernel over 256-key
+    blocks with dS shared through LDS, deterministic fp32 dQ partial reduction) against the fp32
+    oracle, the dQ + dK/dV pair (impl 4) and itself (bitwise, two runs); causal and not,
+    ragged T (partial key blocks / query tiles), strided (packed QKV) views."""
+    torch.manual_seed(41)
+    hd = 64
+    qkv = torch.randn(B * T, 3 * H * hd, device=DEV).bfloat16()
+    q, k, v = (qkv[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+    o, lse = C.attn_fwd(q, k, v, 0.125, causal)
+    do = torch.randn_like(o)
+    outs = []
+    for impl in (6, 6, 4):
+        d = torch.full_like(qkv, float("nan"))
+        dq, dk, dv = (d[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+        C.attn_bwd(do, q, k, v, o, lse, 0.125, causal, dq, dk, dv, impl=impl)
+        outs.append((d, dq, dk, dv))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.isfinite(outs[0][0].float()).all()
+    rq, rk, rv = (torch.empty(B, T, H, hd, device=DEV) for _ in range(3))
+    R.attn_bwd(do.float(), q.float(), k.float(), v.float(), o.float(), lse, 0.125, causal, rq, rk, rv)
+    _, dq, dk, dv = outs[0]
+    assert _rel(dq, rq) < 3e-2 and _rel(dk, rk) < 3e-2 and _rel(dv, rv) < 3e-2, (_rel(dq, rq), _rel(dk, rk), _rel(dv, rv))
+    _, dq4, dk4, dv4 = outs[2]
+    assert _rel(dq, dq4) < 1e-2 and _rel(dk, dk4) < 1e-2 and _rel(dv, dv4) < 1e-2
+
+
+@pytest.mark.parametrize("T", [192, 1024, 333])
+def test_attention_bwd_fused6_rope_and_bias(C, T):
+    """impl 6 with the inverse RoPE (dK in the fused kernel's epilogue, dQ in the partial
+    reduction) and the QKV bias gradient (column sums from both) against the oracle."""
+    torch.manual_seed(42)
+    B, H, hd = 2, 3, 64
+    qkv = torch.randn(B * T, 3 * H * hd, device=DEV).bfloat16()
+    q, k, v = (qkv[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+    o, lse = C.attn_fwd(q, k, v, hd ** -0.5, True)
+    do = torch.randn_like(o)
+    pos = torch.randint(0, 2048, (B * T,), device=DEV)
+    tab = R.rope_table(2048, hd, 10000.0).to(DEV)
+    d = torch.empty_like(qkv)
+    dq, dk, dv = (d[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+    db = torch.full((3 * H * hd,), float("nan"), device=DEV)
+    assert C.attn_bwd(do, q, k, v, o, lse, hd ** -0.5, True, dq, dk, dv, pos, tab, dbias=db, impl=6)
+    assert _rel(db, d.float().sum(0)) < 5e-3
+    r = torch.empty(B * T, 3 * H * hd, device=DEV)
+    rq, rk, rv = (r[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+    rdb = torch.empty(3 * H * hd, device=DEV)
+    R.attn_bwd(do.float(), q.float(), k.float(), v.float(), o.float(), lse, hd ** -0.5, True, rq, rk, rv,
+               pos, tab, dbias=rdb)
+    assert _rel(d, r) < 3e-2
+    assert _rel(db, rdb) < 3e-2
+
+
 def test_adam_matches_torch(C):
     torch.manual_seed(11)
     ps = [torch.randn(n, device=DEV) for n in (1000, 16384 * 2 + 7, 4096)]
@@ -932,6 +988,29 @@ def test_gemm_stream_k(C, layout, K):
         wide = torch.zeros(M, N + 64, device=DEV, dtype=torch.bfloat16)
         C.gemm_nt(a, b, bias, out=wide[:, :N], variant=8)
         assert torch.equal(wide[:, :N], o) and not wide[:, N:].any()
+    assert C.gemm_sk_error(False) == 0
+
+
+def test_gemm_stream_k_starved_producer_raises(C):
+    """A stream-K consumer whose producer never raises its flag (test hook) times out after its
+    bounded wait; the sticky host-mapped error word then makes the step's error check raise,
+    instead of the wrong tile passing silently (gemm4.hip sk_wait)."""
+    from distributed_pytorch_from_scratch_amd.ops import _ext
+    M, N, K = 32768, 768, 768
+    if not C.gemm_sk_applies(M, N, K):
+        pytest.skip("stream-K needs 256 x 256 tiles at exactly 1.5 per CU on this device")
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = torch.randn(N, K, device=DEV).bfloat16()
+    C.gemm_sk_error(True)
+    C.gemm_sk_starve(True)
+    C.gemm_nt(a, b, None, variant=8)
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="stream-K"):
+        _ext.check_device_errors()
+    assert C.gemm_sk_error(False) == 0     # reported once, then reset
+    C.gemm_nt(a, b, None, variant=8)       # the hook is one-shot: the next launch is clean
+    torch.cuda.synchronize()
+    assert C.gemm_sk_error(False) == 0
 
 
 @pytest.mark.parametrize("shapes,K", [([(2304, 768), (768, 768)], 32768), ([(768, 2048), (4096, 768)], 32768),

@@ -74,3 +74,32 @@ def test_plan_refuses_what_does_not_fit_at_all():
 def test_plan_without_budget_never_refuses():
     rc, e = MEM.plan(get_preset("llama-13b"), MEM.Layout(tp=1, seq=8192, batch=8), None)
     assert rc is False and e.peak > 0
+
+
+def test_fp32_layout_counts_fp32_activations_and_no_shadows():
+    """the planner sized fp32 runs (train.py without --bf16) as bf16.  fp32 doubles
+    every activation byte and keeps no bf16 shadow; the oracle path's materialised attention
+    scores are counted too."""
+    a = get_preset("reference")
+    bf = MEM.estimate(a, MEM.Layout(tp=1, seq=1000, batch=32))
+    f32 = MEM.estimate(a, MEM.Layout(tp=1, seq=1000, batch=32, compute="fp32"))
+    f32m = MEM.estimate(a, MEM.Layout(tp=1, seq=1000, batch=32, compute="fp32", materialized_attention=True))
+    assert f32.parts["shadow_bf16"] == 0 and bf.parts["shadow_bf16"] > 0
+    assert 1.9 < f32.parts["activations"] / bf.parts["activations"] <= 2.01
+    # 12 layers x 8 heads x 32 x 1000 x 1000 fp32 probabilities kept for the backward
+    assert f32m.parts["attention_scores"] == 12 * 4 * 32 * 1000 * 1000 * 8
+    assert f32m.peak > f32.peak + f32m.parts["attention_scores"]
+    # and the plan picks recompute / refuses on that basis
+    rc, _ = MEM.plan(a, MEM.Layout(tp=1, seq=1000, batch=32, compute="fp32", materialized_attention=True),
+                     f32m.peak - (1 << 30), margin_frac=0.0, margin_bytes=0)
+    assert rc is True
+
+
+def test_xgmi_staging_follows_the_communicator_capacity(monkeypatch):
+    """xgmi_create allocates (nslots + 2) x cap + 2 x min(cap, 16 MiB) per rank."""
+    assert MEM.xgmi_staging_bytes(1) == 0
+    assert MEM.xgmi_staging_bytes(2, cap_mb=256) == 6 * (256 << 20) + 2 * (16 << 20)
+    assert MEM.xgmi_staging_bytes(8, cap_mb=8) == 6 * (8 << 20) + 2 * (8 << 20)
+    monkeypatch.setenv("DPFS_XGMI_CAP_MB", "64")
+    e = MEM.estimate(get_preset("gpt2-small"), MEM.Layout(tp=2, seq=1024, batch=32))
+    assert e.parts["xgmi_staging"] == 6 * (64 << 20) + 2 * (16 << 20)

@@ -31,6 +31,12 @@ PKG = os.path.join(ROOT, "distributed_pytorch_from_scratch_amd")
 ARCH = os.environ.get("DPFS_OFFLOAD_ARCH", "gfx950")
 
 
+# Per-translation-unit flags: the fused attention backward keeps its MFMA accumulators in VGPRs
+# (its long-lived ones are asm-owned AGPRs, csrc/kernels/attn_acc.inc), so the compiler must
+# not pick the AGPR form for its own MFMAs there; the other kernels keep the default heuristics.
+PER_FILE_FLAGS = {"attention_fused.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def _hipcc() -> str:
     for c in (os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc"), shutil.which("hipcc")):
         if c and os.path.exists(c):
@@ -72,8 +78,8 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True, kernel_asser
     jobs_list = []
     for k in kernels:
         o = os.path.join(obj_dir, os.path.basename(k) + ".o")
-        if force or _newer([k] + headers, o):
-            jobs_list.append([hipcc] + hip_flags + ["-c", k, "-o", o])
+        if force or _newer([k] + headers + glob.glob(os.path.join(CSRC, "kernels", "*.inc")), o):
+            jobs_list.append([hipcc] + hip_flags + PER_FILE_FLAGS.get(os.path.basename(k), []) + ["-c", k, "-o", o])
     # Host bindings: plain g++ against the torch headers (HIP runtime headers for types).
     rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
     py_inc = sysconfig.get_paths()["include"]
