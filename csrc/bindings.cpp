@@ -95,6 +95,9 @@ int dpfs_attn_bwd(const void*, const void*, const void*, const void*, const void
                    void*, int, int, int, int, long long, long long, long long, long long, long long, long long,
                    long long, long long, float, int, const int64_t*, const float*, hipStream_t, float*, float*, int);
 long long dpfs_attn_bias_ws(int, int, int, int);
+void dpfs_ce_finalize(const float*, const int64_t*, long long, float*, float*, float*, float*, int, int, int, int,
+                      hipStream_t);
+void dpfs_ce_valid_scale(const int64_t*, long long, float*, float*, int, hipStream_t);
 long long dpfs_attn_fused_ws(int, int, int, int);
 long long dpfs_attn_fused_bias_ws(int, int, int, int);
 int dpfs_attn_bwd_fused(const void*, const void*, const void*, const void*, const void*, const float*, float*, float*,
@@ -875,6 +878,41 @@ torch::Tensor embedding_bwd_sorted(torch::Tensor dout, torch::Tensor ids, int64_
   return dw;
 }
 
+// Loss bookkeeping of the vocab-parallel CE from the gathered statistics (nsh, M, 3): per-row
+// lse and validity (1.0 / 0.0), the running (loss sum, valid count) in acc[2] (overwritten when
+// `first`), and with `last` the mean loss into `loss` (0-d) and max(count, 1) into acc[1].
+std::vector<torch::Tensor> ce_finalize(torch::Tensor stats, torch::Tensor targets, int64_t ignore_index,
+                                       torch::Tensor acc, torch::Tensor loss, bool first, bool last) {
+  check_cuda(stats, "stats");
+  TORCH_CHECK(stats.scalar_type() == torch::kFloat32 && stats.is_contiguous() && stats.dim() == 3 &&
+                  stats.size(2) == 3, "ce_finalize: stats fp32 contiguous (nsh, M, 3)");
+  const int64_t M = stats.size(1);
+  TORCH_CHECK(targets.scalar_type() == torch::kInt64 && targets.is_contiguous() && targets.numel() == M,
+              "ce_finalize: targets int64 [M]");
+  TORCH_CHECK(acc.scalar_type() == torch::kFloat32 && acc.is_contiguous() && acc.numel() >= 2 &&
+                  loss.scalar_type() == torch::kFloat32 && loss.numel() == 1 && loss.is_contiguous(),
+              "ce_finalize: acc fp32 [>=2], loss fp32 scalar");
+  const at::DeviceGuard g(stats.device());
+  auto lse = torch::empty({M}, stats.options());
+  auto valid = torch::empty({M}, stats.options());
+  dpfs_ce_finalize(stats.data_ptr<float>(), targets.data_ptr<int64_t>(), ignore_index, lse.data_ptr<float>(),
+                   valid.data_ptr<float>(), acc.data_ptr<float>(), loss.data_ptr<float>(), (int)M,
+                   (int)stats.size(0), first ? 1 : 0, last ? 1 : 0, stream());
+  return {lse, valid};
+}
+
+std::vector<torch::Tensor> ce_valid_scale(torch::Tensor targets, int64_t ignore_index) {
+  check_cuda(targets, "targets");
+  TORCH_CHECK(targets.scalar_type() == torch::kInt64 && targets.is_contiguous(), "ce_valid_scale: int64 targets");
+  const at::DeviceGuard g(targets.device());
+  const int64_t M = targets.numel();
+  auto gs = torch::empty({M}, targets.options().dtype(torch::kFloat32));
+  auto n = torch::empty({}, targets.options().dtype(torch::kFloat32));
+  dpfs_ce_valid_scale(targets.data_ptr<int64_t>(), ignore_index, gs.data_ptr<float>(), n.data_ptr<float>(), (int)M,
+                      stream());
+  return {gs, n};
+}
+
 torch::Tensor ce_fwd_stats(torch::Tensor logits, torch::Tensor targets, int64_t vocab_start, int64_t vocab_valid) {
   check_rowmajor(logits, "logits");
   TORCH_CHECK(logits.is_contiguous(), "ce: logits contiguous");
@@ -1432,6 +1470,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "flash attention backward; impl (per call): 0 = auto (dq3 + dkdv3 at hd 64 / 128, dq + dkdv2 at hd 32), "
         "2 = dq + dkdv2 (16x16x32), 4 = dq3 + dkdv3 (32x32x16), 5 = 4 with the dK/dV DIAG build, 6 = the fused "
         "head_dim-64 backward (delta pass, one dK/dV/dQ kernel, dQ partial reduction)");
+  m.def("ce_finalize", &ce_finalize, py::arg("stats"), py::arg("targets"), py::arg("ignore_index"), py::arg("acc"),
+        py::arg("loss"), py::arg("first"), py::arg("last"),
+        "CE loss bookkeeping from gathered (nsh, M, 3) statistics: returns (lse, valid); running sums in acc");
+  m.def("ce_valid_scale", &ce_valid_scale, py::arg("targets"), py::arg("ignore_index"),
+        "(gs, n_valid): per-row 1 / max(#valid, 1) on valid rows (0 on ignored), and max(#valid, 1)");
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd_sorted", &embedding_bwd_sorted, py::arg("dout"), py::arg("ids"), py::arg("v_local"),
         py::arg("vocab_start"), py::arg("out") = py::none(), py::arg("accumulate") = false,

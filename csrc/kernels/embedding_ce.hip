@@ -454,6 +454,82 @@ static inline int cap_grid2(long long work, int block) {
   return (int)g;
 }
 
+
+// ---------------------------------------------------------------- CE loss bookkeeping --
+// The loss scalar and per-row terms of the vocab-parallel CE from the gathered statistics
+// (replaces ~15 small framework kernels per step: amax / log / exp / where / sums / casts).
+// One 1024-thread workgroup; every sum in a fixed order (per-thread strided rows, then a
+// fixed tree), so the loss is run-to-run bit-identical.
+//   stats (nsh, M, 3) = {max, sum exp(x - max), target logit or 0} per vocab shard;
+//   lse[r] = mx + log(sum_s se_s exp(m_s - mx)); valid[r] = (tgt[r] != ignore) as 1.0 / 0.0;
+//   acc[0] (+)= sum valid (lse - tl), acc[1] (+)= sum valid; with `last`: acc[1] = max(acc[1], 1),
+//   loss = acc[0] / acc[1].
+__global__ __launch_bounds__(1024) void ce_finalize_k(const float* __restrict__ stats, const int64_t* __restrict__ tgt,
+                                                     long long ignore, float* __restrict__ lse, float* __restrict__ valid,
+                                                     float* __restrict__ acc, float* __restrict__ loss, int M, int nsh,
+                                                     int first, int last) {
+  __shared__ float red[2][1024];
+  float ls = 0.f, cn = 0.f;
+  for (int r = threadIdx.x; r < M; r += 1024) {
+    float mx = -INFINITY;
+    for (int sh = 0; sh < nsh; ++sh) mx = fmaxf(mx, stats[((long long)sh * M + r) * 3]);
+    float se = 0.f, tl = 0.f;
+    for (int sh = 0; sh < nsh; ++sh) {
+      const float* st = stats + ((long long)sh * M + r) * 3;
+      se += st[1] * __expf(st[0] - mx);
+      tl += st[2];
+    }
+    const float l = mx + __logf(se);
+    const float v = tgt[r] != ignore ? 1.f : 0.f;
+    lse[r] = l;
+    valid[r] = v;
+    ls += v != 0.f ? l - tl : 0.f;
+    cn += v;
+  }
+  red[0][threadIdx.x] = ls;
+  red[1][threadIdx.x] = cn;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + o];
+      red[1][threadIdx.x] += red[1][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    float a0 = red[0][0], a1 = red[1][0];
+    if (!first) {
+      a0 += acc[0];
+      a1 += acc[1];
+    }
+    if (last) {
+      a1 = fmaxf(a1, 1.f);
+      loss[0] = a0 / a1;
+    }
+    acc[0] = a0;
+    acc[1] = a1;
+  }
+}
+
+// gs[r] = (tgt[r] != ignore) / max(count, 1) over all M rows (the one-pass TP-1 CE's per-row
+// gradient scale for a unit loss gradient); n_valid[0] = max(count, 1).  One workgroup.
+__global__ __launch_bounds__(1024) void ce_valid_scale_k(const int64_t* __restrict__ tgt, long long ignore,
+                                                        float* __restrict__ gs, float* __restrict__ n_valid, int M) {
+  __shared__ float red[1024];
+  float cn = 0.f;
+  for (int r = threadIdx.x; r < M; r += 1024) cn += tgt[r] != ignore ? 1.f : 0.f;
+  red[threadIdx.x] = cn;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  const float n = fmaxf(red[0], 1.f);
+  const float inv = 1.f / n;
+  for (int r = threadIdx.x; r < M; r += 1024) gs[r] = tgt[r] != ignore ? inv : 0.f;
+  if (threadIdx.x == 0) n_valid[0] = n;
+}
+
 }  // namespace dpfs
 
 using namespace dpfs;
@@ -594,4 +670,13 @@ extern "C" void dpfs_ce_bwd(int dtype, const void* logits, const int64_t* tgt, c
   else
     ce_bwd_k<float, 1><<<grid, 256, 0, s>>>((const float*)logits, tgt, lse, gscale, (float*)out, M, V, vstart,
                                             vvalid);
+}
+
+extern "C" void dpfs_ce_finalize(const float* stats, const int64_t* tgt, long long ignore, float* lse, float* valid,
+                                 float* acc, float* loss, int M, int nsh, int first, int last, hipStream_t s) {
+  ce_finalize_k<<<1, 1024, 0, s>>>(stats, tgt, ignore, lse, valid, acc, loss, M, nsh, first, last);
+}
+extern "C" void dpfs_ce_valid_scale(const int64_t* tgt, long long ignore, float* gs, float* n_valid, int M,
+                                    hipStream_t s) {
+  ce_valid_scale_k<<<1, 1024, 0, s>>>(tgt, ignore, gs, n_valid, M);
 }

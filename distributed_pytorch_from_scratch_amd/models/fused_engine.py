@@ -284,18 +284,20 @@ class DecoderTrainFn(torch.autograd.Function):
         # head: residual, final norm, lm_head shard, vocab-parallel CE statistics.  TP 1 with a
         # unit loss gradient (engine.TrainStep): d logits is written in the same pass over the
         # logits as the statistics (k.ce_fused), so backward does not read them again.
-        losses_sum = torch.zeros((), device=dev, dtype=torch.float32)
-        n_valid_total = torch.zeros((), device=dev, dtype=torch.float32)
+        # the loss bookkeeping (lse, validity, running sums, the mean) in one kernel per chunk
+        acc = torch.empty(2, device=dev, dtype=torch.float32)
+        loss = torch.empty((), device=dev, dtype=torch.float32)
         fuse_ce = CE_ONE_PASS and tp == 1 and getattr(model, "_ce_unit_grad", False) and hasattr(k, "ce_fused")
         if fuse_ce:
-            n_valid_all = (tgt != ignore_index).sum().float().clamp_min(1.0)
-        for s in st:
+            gs_all, _ = k.ce_valid_scale(tgt.reshape(-1).contiguous(), ignore_index)
+        row0 = 0
+        for ci, s in enumerate(st):
             _wait(s["h"])
             xf, hf, rf = k.add_rmsnorm_fwd(s["pend"], s["pend_bias"], s["x"], model.norm.scale, model.norm.eps)
             logits = GS.gemm_nt(k, hf, W(head.weight), head.bias)
             stats = None
             if fuse_ce:
-                gs = (s["tgt"] != ignore_index).float() / n_valid_all
+                gs = gs_all[row0:row0 + s["tgt"].numel()]
                 db = torch.empty(logits.size(1), device=dev, dtype=torch.float32) if head.bias is not None else None
                 stats = k.ce_fused(logits, s["tgt"], gs, vst, vvalid, db)
                 if stats is not None:
@@ -308,18 +310,12 @@ class DecoderTrainFn(torch.autograd.Function):
                 allst = allst.view(tp, -1, 3)
             else:
                 allst = stats.unsqueeze(0)
-            mx = allst[..., 0].amax(0)
-            lse = mx + torch.log((allst[..., 1] * torch.exp(allst[..., 0] - mx)).sum(0))
-            tl = allst[..., 2].sum(0)
-            valid = s["tgt"] != ignore_index
-            losses_sum = losses_sum + torch.where(valid, lse - tl, torch.zeros_like(lse)).sum()
-            n_valid_total = n_valid_total + valid.sum()
+            lse, valid = k.ce_finalize(allst, s["tgt"], ignore_index, acc, loss, ci == 0, ci == len(st) - 1)
+            row0 += s["tgt"].numel()
             s.update(xf=xf, hf=hf, rf=rf, logits=logits, ce_lse=lse, valid=valid)
             del s["pend"], s["h"]
-        n_valid_total = n_valid_total.clamp_min(1.0)
-        loss = losses_sum / n_valid_total
         ctx.model, ctx.st, ctx.layers, ctx.meta = model, st, layers, (T, dt, vst, vvalid, C, d)
-        ctx.n_valid = n_valid_total
+        ctx.n_valid = acc[1]
         ctx.tab = tab
         ctx.nparams = len(params)
         ctx.recompute = recompute
@@ -427,7 +423,7 @@ class DecoderTrainFn(torch.autograd.Function):
                                        f"({float(gloss.float().mean())}); call loss() without unit_grad when "
                                        "scaling the loss")
             else:
-                gs = s["valid"].float() * gscale_all
+                gs = s["valid"] * gscale_all
                 db = first(g, "lm_b", dl, dl.size(1)) if head.bias is not None else None
                 k.ce_bwd(dl, s["tgt"], s["ce_lse"], gs, vst, vvalid, dl, db)    # + lm_head bias grad
             dh = GS.gemm_nn(k, dl, W(head.weight), out=_slot(ci, dl.size(0), d, dt))

@@ -139,29 +139,23 @@ class DecoderTrainFnSP(torch.autograd.Function):
             hf, s["h"] = _ag(hfs, n)
             s.update(xf=xf, rf=rf, hf=hf)
             del s["pend"]
-        losses_sum = torch.zeros((), device=dev, dtype=torch.float32)
-        n_valid_total = torch.zeros((), device=dev, dtype=torch.float32)
-        for s in st:        # lm_head shard + vocab-parallel CE statistics
+        acc = torch.empty(2, device=dev, dtype=torch.float32)
+        loss = torch.empty((), device=dev, dtype=torch.float32)
+        for ci, s in enumerate(st):        # lm_head shard + vocab-parallel CE statistics
             _wait(s["h"])
             logits = GS.gemm_nt(k, s["hf"], W(head.weight), head.bias)
             stats = k.ce_fwd_stats(logits, s["tgt"], vst, vvalid)
             allst = stats.new_empty((n * stats.size(0), 3))
             dist.all_gather_into_tensor(allst, stats, group=p.tp_group)
             allst = allst.view(n, -1, 3)
-            mx = allst[..., 0].amax(0)
-            lse = mx + torch.log((allst[..., 1] * torch.exp(allst[..., 0] - mx)).sum(0))
-            tl = allst[..., 2].sum(0)
-            valid = s["tgt"] != ignore_index
-            losses_sum = losses_sum + torch.where(valid, lse - tl, torch.zeros_like(lse)).sum()
-            n_valid_total = n_valid_total + valid.sum()
+            lse, valid = k.ce_finalize(allst, s["tgt"], ignore_index, acc, loss, ci == 0, ci == len(st) - 1)
             s.update(logits=logits, ce_lse=lse, valid=valid, h=None)
-        n_valid_total = n_valid_total.clamp_min(1.0)
         ctx.model, ctx.st, ctx.layers, ctx.meta = model, st, layers, (T, dt, vst, vvalid, n)
         ctx.recompute = recompute
-        ctx.n_valid, ctx.tab = n_valid_total, tab
+        ctx.n_valid, ctx.tab = acc[1], tab
         ctx.f8map = f8map
         F8.activate(None)
-        return losses_sum / n_valid_total
+        return loss
 
     @staticmethod
     def backward(ctx, gloss):
@@ -241,7 +235,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
         d = model.args.attn_dim
         lm_p = []
         for ci, s in enumerate(st):    # CE backward in place, lm_head dgrad -> reduce-scatter, lm_head wgrad
-            gs = s["valid"].float() * gscale_all
+            gs = s["valid"] * gscale_all
             dl = s["logits"]
             db = first(g, "lm_b", dl, dl.size(1)) if head.bias is not None else None
             k.ce_bwd(dl, s["tgt"], s["ce_lse"], gs, vst, vvalid, dl, db)

@@ -433,6 +433,32 @@ def ce_combine(stats: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     return lse, tl
 
 
+def ce_finalize(stats: torch.Tensor, targets: torch.Tensor, ignore_index: int, acc: torch.Tensor,
+                loss: torch.Tensor, first: bool, last: bool) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Loss bookkeeping from the gathered (n_shards, M, 3) statistics: returns (lse[M], valid[M]
+    as 1.0 / 0.0); ``acc[0:2]`` holds the running (sum over valid rows of lse - target logit,
+    valid count), overwritten when ``first``; with ``last`` the count is clamped to >= 1 and
+    ``loss`` (0-d) gets the mean."""
+    lse, tl = ce_combine(stats)
+    valid = (targets != ignore_index).float()
+    part = torch.stack([torch.where(valid > 0, lse - tl, torch.zeros_like(lse)).sum(), valid.sum()])
+    if first:
+        acc[:2] = part
+    else:
+        acc[:2] += part
+    if last:
+        acc[1] = acc[1].clamp_min(1.0)
+        loss.copy_(acc[0] / acc[1])
+    return lse, valid
+
+
+def ce_valid_scale(targets: torch.Tensor, ignore_index: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(gs[M], n_valid): 1 / max(#valid, 1) on the valid rows, 0 on the ignored ones."""
+    valid = (targets != ignore_index).float()
+    n = valid.sum().clamp_min(1.0)
+    return valid / n, n
+
+
 def ce_bwd(logits: torch.Tensor, targets: torch.Tensor, lse: torch.Tensor, gscale: torch.Tensor,
            vocab_start: int, vocab_valid: int, out: torch.Tensor,
            dbias: Optional[torch.Tensor] = None) -> torch.Tensor:

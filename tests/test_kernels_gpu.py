@@ -370,6 +370,28 @@ def test_attention_bwd_fused6_rope_and_bias(C, T):
     assert _rel(db, rdb) < 3e-2
 
 
+@pytest.mark.parametrize("nsh,M", [(1, 32768), (2, 1000), (8, 4097)])
+def test_ce_finalize_and_valid_scale(C, nsh, M):
+    """The CE loss bookkeeping kernels (one workgroup, fixed-order sums) against the oracle:
+    per-row lse / validity, running sums over two chunks, the mean loss; and the one-pass
+    CE's per-row gradient scale."""
+    torch.manual_seed(43)
+    st = torch.stack([torch.randn(nsh, M, device=DEV) * 3, torch.rand(nsh, M, device=DEV) * 50 + 1,
+                      torch.randn(nsh, M, device=DEV)], dim=2).contiguous()
+    tgt = torch.randint(0, 100, (M,), device=DEV)
+    tgt[::7] = -1
+    acc, loss = torch.empty(2, device=DEV), torch.empty((), device=DEV)
+    racc, rloss = torch.empty(2, device=DEV), torch.empty((), device=DEV)
+    for first, last in ((True, False), (False, True)):
+        lse, valid = C.ce_finalize(st, tgt, -1, acc, loss, first, last)
+        rl, rv = R.ce_finalize(st, tgt, -1, racc, rloss, first, last)
+        assert _rel(lse, rl) < 1e-5 and torch.equal(valid, rv)
+    assert _rel(acc, racc) < 1e-5 and abs(loss.item() - rloss.item()) < 1e-4 * abs(rloss.item())
+    gs, n = C.ce_valid_scale(tgt, -1)
+    rg, rn = R.ce_valid_scale(tgt, -1)
+    assert torch.equal(n, rn) and _rel(gs, rg) < 1e-6
+
+
 def test_adam_matches_torch(C):
     torch.manual_seed(11)
     ps = [torch.randn(n, device=DEV) for n in (1000, 16384 * 2 + 7, 4096)]
