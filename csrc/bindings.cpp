@@ -98,6 +98,8 @@ long long dpfs_attn_bias_ws(int, int, int, int);
 void dpfs_ce_finalize(const float*, const int64_t*, long long, float*, float*, float*, float*, int, int, int, int,
                       hipStream_t);
 void dpfs_ce_valid_scale(const int64_t*, long long, float*, float*, int, hipStream_t);
+long long dpfs_emb_sort_ws(int);
+void dpfs_emb_sort(const int64_t*, int, long long, int, int*, int64_t*, int64_t*, hipStream_t);
 long long dpfs_attn_fused_ws(int, int, int, int);
 long long dpfs_attn_fused_bias_ws(int, int, int, int);
 int dpfs_attn_bwd_fused(const void*, const void*, const void*, const void*, const void*, const float*, float*, float*,
@@ -836,6 +838,24 @@ torch::Tensor embedding_bwd(torch::Tensor dout, torch::Tensor ids, int64_t v_loc
 // Deterministic embedding gradient (no atomics): the ids sorted (stable), each local vocab row's
 // segment found by binary search, one wave per vocab row sums its rows in row order and WRITES
 // dw (every row: no zero pass), or adds to it (`accumulate`).  D % 4 == 0 (else the atomic form).
+// Stable order of the ids by local vocab row (ids outside [vocab_start, vocab_start + v_local)
+// last) and each row's segment start: the deterministic embedding backward's index
+// (embedding_bwd_sorted); a two-pass radix sort on our kernels (embedding_ce.hip).
+std::vector<torch::Tensor> emb_sort(torch::Tensor ids, int64_t vocab_start, int64_t v_local) {
+  check_cuda(ids, "ids");
+  TORCH_CHECK(ids.scalar_type() == torch::kInt64 && ids.is_contiguous(), "emb_sort: ids int64 contiguous");
+  TORCH_CHECK(v_local >= 0 && v_local < 65535, "emb_sort: the local vocab must be below 65535 rows");
+  TORCH_CHECK(ids.numel() < (1LL << 31), "emb_sort: too many ids");
+  const at::DeviceGuard g(ids.device());
+  const int M = (int)ids.numel();
+  auto ws = torch::empty({dpfs_emb_sort_ws(M)}, ids.options().dtype(torch::kInt32));
+  auto perm = torch::empty({M}, ids.options());
+  auto seg = torch::empty({v_local + 1}, ids.options());
+  dpfs_emb_sort(ids.data_ptr<int64_t>(), M, vocab_start, (int)v_local, ws.data_ptr<int>(), perm.data_ptr<int64_t>(),
+                seg.data_ptr<int64_t>(), stream());
+  return {perm, seg};
+}
+
 torch::Tensor embedding_bwd_sorted(torch::Tensor dout, torch::Tensor ids, int64_t v_local, int64_t vocab_start,
                                    c10::optional<torch::Tensor> out, bool accumulate,
                                    c10::optional<torch::Tensor> perm_in, c10::optional<torch::Tensor> seg_in) {
@@ -868,10 +888,9 @@ torch::Tensor embedding_bwd_sorted(torch::Tensor dout, torch::Tensor ids, int64_
                     seg.scalar_type() == torch::kInt64 && seg.is_contiguous() && seg.numel() == v_local + 1,
                 "embedding_bwd_sorted: perm [M] / seg [v_local + 1] int64");
   } else {
-    auto sorted = at::sort(ids.view({-1}), /*stable=*/true, /*dim=*/0, /*descending=*/false);
-    perm = std::get<1>(sorted).contiguous();
-    const torch::Tensor bounds = at::arange(vocab_start, vocab_start + v_local + 1, ids.options());
-    seg = at::searchsorted(std::get<0>(sorted), bounds).contiguous();
+    auto ps = emb_sort(ids, vocab_start, v_local);
+    perm = ps[0];
+    seg = ps[1];
   }
   dpfs_embedding_bwd_seg(dcode(dout), dout.data_ptr(), perm.data_ptr<int64_t>(), seg.data_ptr<int64_t>(),
                          dw.data_ptr<float>(), (int)D, (int)v_local, accumulate ? 1 : 0, stream());
@@ -1475,6 +1494,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "CE loss bookkeeping from gathered (nsh, M, 3) statistics: returns (lse, valid); running sums in acc");
   m.def("ce_valid_scale", &ce_valid_scale, py::arg("targets"), py::arg("ignore_index"),
         "(gs, n_valid): per-row 1 / max(#valid, 1) on valid rows (0 on ignored), and max(#valid, 1)");
+  m.def("emb_sort", &emb_sort, py::arg("ids"), py::arg("vocab_start"), py::arg("v_local"),
+        "(perm, seg): the ids' stable order by local vocab row (out-of-shard ids last) and each row's segment "
+        "start, int64 (deterministic radix sort on HIP kernels)");
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd_sorted", &embedding_bwd_sorted, py::arg("dout"), py::arg("ids"), py::arg("v_local"),
         py::arg("vocab_start"), py::arg("out") = py::none(), py::arg("accumulate") = false,

@@ -156,17 +156,19 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_fused_k(
     int cur = 0;
     if (nq > 0) dma.issue(qbase, dobase, lsb, dlb, ldq, lddo, T, qstart, smem);
     if (nq > 1) dma.issue(qbase, dobase, lsb, dlb, ldq, lddo, T, qstart + BQ, smem + BUF);
-    // V B operands of dP (lane: key 32 kh + r32; d 16 ks + 8 hf + 0..7) in registers; K's
-    // (for S) are row reads of the block's K rows in LDS
-    bf16x8 vf[2][KS];
+    // K / V B operands of S / dP (lane: key 32 kh + r32; d 16 ks + 8 hf + 0..7) in registers
+    bf16x8 kf[2][KS], vf[2][KS];
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh) {
       const int key = kw0 + 32 * kh + r32;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        bf16x8 c_ = {};
-        if (key < T)
+        bf16x8 a_ = {}, c_ = {};
+        if (key < T) {
+          a_ = *reinterpret_cast<const bf16x8*>(K + ((long long)b * T + key) * ldk + (long long)h * HD + 16 * ks + 8 * hf);
           c_ = *reinterpret_cast<const bf16x8*>(V + ((long long)b * T + key) * ldv + (long long)h * HD + 16 * ks + 8 * hf);
+        }
+        kf[kh][ks] = a_;
         vf[kh][ks] = c_;
       }
     }
@@ -262,6 +264,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_fused_k(
         const int key = kw0 + 32 * kh + r32;
         vk[kh] = key >= T ? 0x7fffffff : (causal ? key - q0 - 4 * hf : -0x7fffffff);
       }
+      bf16x8 fa[KS], fb[KS];
       auto load_half = [&](int) __attribute__((always_inline)) {};
       // transposed dO^T / Q^T fragments of query half qt (A of dV^T / dK^T; shared by both key halves)
       s16x4 tho[16];
@@ -293,16 +296,19 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_fused_k(
             dp[j][4 * g + jj] = dd[jj];
           }
         }
-        // Q / dO row fragments (A; rows 32 qt + r32) and K row fragments (B; key rows 64 wave +
-        // 32 kh + r32 of the staged block: the same swizzle as row r32)
-        const char* kr = kst + (64 * wave + 32 * kh) * RB;
+        // Q / dO row fragments (A; rows 32 qt + r32): read once per query half (kh 0), issued
+        // together with the row constants before the chain
+        if (kh == 0) {
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            fa[ks] = *reinterpret_cast<const bf16x8*>(lq + roff[ks] + 32 * qt * RB);
+            fb[ks] = *reinterpret_cast<const bf16x8*>(ldo_ + roff[ks] + 32 * qt * RB);
+          }
+        }
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          const bf16x8 fa = *reinterpret_cast<const bf16x8*>(lq + roff[ks] + 32 * qt * RB);
-          const bf16x8 fk = *reinterpret_cast<const bf16x8*>(kr + roff[ks]);
-          const bf16x8 fb = *reinterpret_cast<const bf16x8*>(ldo_ + roff[ks] + 32 * qt * RB);
-          sc[j] = MFMA32(fa, fk, sc[j]);
-          dp[j] = MFMA32(fb, vf[kh][ks], dp[j]);
+          sc[j] = MFMA32(fa[ks], kf[kh][ks], sc[j]);
+          dp[j] = MFMA32(fb[ks], vf[kh][ks], dp[j]);
         }
       };
       // p = exp2(c2 S'), masked; dS = p dP'; P / dS packed (B operands of dV^T / dK^T); dS rows

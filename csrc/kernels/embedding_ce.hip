@@ -530,6 +530,135 @@ __global__ __launch_bounds__(1024) void ce_valid_scale_k(const int64_t* __restri
   if (threadIdx.x == 0) n_valid[0] = n;
 }
 
+
+// --------------------------------------------- deterministic counting sort of token ids --
+// The deterministic embedding backward needs the ids' stable order and each local vocab row's
+// segment (perm, seg).  A two-pass LSD radix sort on 8-bit digits of the 16-bit key (local id,
+// or 0xFFFF for an id outside this vocab shard), chunks of 1024 tokens (one 1024-thread
+// workgroup each), stable: within a wave the rank among equal digits comes from ballots (the
+// match mask of the 8 digit bits), across the 16 waves from per-wave digit counts in LDS, across
+// chunks from the (digit, chunk) count table.  Per pass: emb_digit_hist_k writes the chunk's 256
+// counts (no zeroing, no atomics), emb_digit_scatter_k derives the chunk's global offsets from
+// the whole table and moves (key, token) pairs; emb_seg_k then finds every row's segment start
+// by binary search.  Replaces the framework's sort + searchsorted (rocprim + ATen kernels).
+constexpr int kSortChunk = 1024;
+
+// rank of this lane among the active lanes of its wave with the same 8-bit digit, and the
+// mask of those lanes
+__device__ __forceinline__ unsigned long long digit_match(int d, bool active) {
+  unsigned long long m = __builtin_amdgcn_ballot_w64(active);
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const bool bit = (d >> b) & 1;
+    const unsigned long long bal = __builtin_amdgcn_ballot_w64(bit);
+    m &= bit ? bal : ~bal;
+  }
+  return m;
+}
+
+// Per-wave digit counts of the chunk into LDS wc[16][256] (zeroed here), then each thread
+// t < 256 turns column t into an exclusive prefix over the waves; returns the chunk total of
+// digit threadIdx.x (threads < 256).
+__device__ __forceinline__ int chunk_digit_prefix(int (&wc)[16][256], int d, bool active, unsigned long long m) {
+  for (int i = threadIdx.x; i < 16 * 256; i += 1024) (&wc[0][0])[i] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  if (active && (m & lt) == 0) wc[w][d] = __popcll(m);   // the first lane of each digit group
+  __syncthreads();
+  int tot = 0;
+  if (threadIdx.x < 256) {
+    for (int ww = 0; ww < 16; ++ww) {
+      const int c = wc[ww][threadIdx.x];
+      wc[ww][threadIdx.x] = tot;
+      tot += c;
+    }
+  }
+  __syncthreads();
+  return tot;
+}
+
+// key of token t: pass 0 reads the ids, pass 1 the previous pass's keys
+__device__ __forceinline__ int sort_key(const int64_t* ids, const int* kin, long long t, long long vstart, int vlocal) {
+  if (kin) return kin[t];
+  const long long l = ids[t] - vstart;
+  return (l >= 0 && l < vlocal) ? (int)l : 0xFFFF;
+}
+
+__global__ __launch_bounds__(1024) void emb_digit_hist_k(const int64_t* __restrict__ ids, const int* __restrict__ kin,
+                                                        long long vstart, int vlocal, int M, int shift,
+                                                        int* __restrict__ table) {
+  __shared__ int wc[16][256];
+  const long long t = (long long)blockIdx.x * kSortChunk + threadIdx.x;
+  const bool active = t < M;
+  const int d = active ? (sort_key(ids, kin, t, vstart, vlocal) >> shift) & 255 : 0;
+  const unsigned long long m = digit_match(d, active);
+  const int tot = chunk_digit_prefix(wc, d, active, m);
+  if (threadIdx.x < 256) table[threadIdx.x * gridDim.x + blockIdx.x] = tot;   // [digit][chunk]
+}
+
+__global__ __launch_bounds__(1024) void emb_digit_scatter_k(const int64_t* __restrict__ ids, const int* __restrict__ kin,
+                                                           const int* __restrict__ vin, long long vstart, int vlocal,
+                                                           int M, int shift, const int* __restrict__ table,
+                                                           int* __restrict__ kout, int* __restrict__ vout,
+                                                           int64_t* __restrict__ vout64) {
+  __shared__ int wc[16][256];
+  __shared__ int base[256];
+  const int NC = gridDim.x, c = blockIdx.x;
+  // the chunk's global offset of every digit: all chunks' counts of smaller digits, then this
+  // digit's counts in earlier chunks (fixed-order sums: thread t < 256 owns digit t)
+  __shared__ int dtot[256];
+  if (threadIdx.x < 256) {
+    int tot = 0, before = 0;
+    for (int cc = 0; cc < NC; ++cc) {
+      const int x = table[threadIdx.x * NC + cc];
+      if (cc < c) before += x;
+      tot += x;
+    }
+    dtot[threadIdx.x] = tot;
+    base[threadIdx.x] = before;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int dd = 0; dd < 256; ++dd) {
+      const int x = dtot[dd];
+      dtot[dd] = run;
+      run += x;
+    }
+  }
+  __syncthreads();
+  const long long t = (long long)c * kSortChunk + threadIdx.x;
+  const bool active = t < M;
+  const int key = active ? sort_key(ids, kin, t, vstart, vlocal) : 0;
+  const int d = (key >> shift) & 255;
+  const unsigned long long m = digit_match(d, active);
+  chunk_digit_prefix(wc, d, active, m);
+  if (active) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int pos = dtot[d] + base[d] + wc[w][d] + __popcll(m & lt);
+    const int val = vin ? vin[t] : (int)t;
+    kout[pos] = key;
+    if (vout) vout[pos] = val;
+    if (vout64) vout64[pos] = val;
+  }
+}
+
+// seg[v] = first position of key >= v in the sorted keys, v = 0 .. vlocal
+__global__ __launch_bounds__(256) void emb_seg_k(const int* __restrict__ keys, int M, int vlocal,
+                                                int64_t* __restrict__ seg) {
+  const int v = blockIdx.x * 256 + threadIdx.x;
+  if (v > vlocal) return;
+  int lo = 0, hi = M;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (keys[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  seg[v] = lo;
+}
+
 }  // namespace dpfs
 
 using namespace dpfs;
@@ -679,4 +808,20 @@ extern "C" void dpfs_ce_finalize(const float* stats, const int64_t* tgt, long lo
 extern "C" void dpfs_ce_valid_scale(const int64_t* tgt, long long ignore, float* gs, float* n_valid, int M,
                                     hipStream_t s) {
   ce_valid_scale_k<<<1, 1024, 0, s>>>(tgt, ignore, gs, n_valid, M);
+}
+
+// ws: 4 M + 256 * ceil(M / 1024) ints.  perm: int64 [M] (positions past seg[vlocal] hold the
+// ids outside this shard), seg: int64 [vlocal + 1].
+extern "C" long long dpfs_emb_sort_ws(int M) { return 4LL * M + 256LL * ((M + kSortChunk - 1) / kSortChunk); }
+extern "C" void dpfs_emb_sort(const int64_t* ids, int M, long long vstart, int vlocal, int* ws, int64_t* perm,
+                              int64_t* seg, hipStream_t s) {
+  const int NC = (M + kSortChunk - 1) / kSortChunk;
+  int *k1 = ws, *v1 = ws + M, *k2 = ws + 2LL * M, *table = ws + 4LL * M;
+  if (M > 0) {
+    emb_digit_hist_k<<<NC, 1024, 0, s>>>(ids, nullptr, vstart, vlocal, M, 0, table);
+    emb_digit_scatter_k<<<NC, 1024, 0, s>>>(ids, nullptr, nullptr, vstart, vlocal, M, 0, table, k1, v1, nullptr);
+    emb_digit_hist_k<<<NC, 1024, 0, s>>>(ids, k1, vstart, vlocal, M, 8, table);
+    emb_digit_scatter_k<<<NC, 1024, 0, s>>>(ids, k1, v1, vstart, vlocal, M, 8, table, k2, nullptr, perm);
+  }
+  emb_seg_k<<<(vlocal + 1 + 255) / 256, 256, 0, s>>>(k2, M, vlocal, seg);
 }

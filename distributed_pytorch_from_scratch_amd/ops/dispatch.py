@@ -72,8 +72,8 @@ def emb_sort_ahead(ids: torch.Tensor, vocab_start: int, v_local: int):
     cur = torch.cuda.current_stream(dev)
     side.wait_stream(cur)                       # the ids are ready
     with torch.cuda.stream(side):
-        sid, perm = torch.sort(ids.view(-1), stable=True)
-        seg = torch.searchsorted(sid, torch.arange(vocab_start, vocab_start + v_local + 1, device=dev))
+        # deterministic radix sort on our kernels (csrc/kernels/embedding_ce.hip emb_sort)
+        perm, seg = _ext.require().emb_sort(ids.view(-1), vocab_start, v_local)
         ev = torch.cuda.Event()
         ev.record(side)
     ids.record_stream(side)

@@ -400,6 +400,16 @@ def embedding_bwd_sorted(dout: torch.Tensor, ids: torch.Tensor, v_local: int, vo
     return embedding_bwd(dout, ids, v_local, vocab_start, out)
 
 
+def emb_sort(ids: torch.Tensor, vocab_start: int, v_local: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(perm, seg): the ids' stable order by local vocab row with the ids outside the shard last,
+    and each local row's segment start (seg[v_local] = number of in-shard ids)."""
+    local = ids.reshape(-1).long() - vocab_start
+    key = torch.where((local >= 0) & (local < v_local), local, torch.full_like(local, 0xFFFF))
+    sk, perm = torch.sort(key, stable=True)
+    seg = torch.searchsorted(sk, torch.arange(v_local + 1, device=ids.device))
+    return perm, seg
+
+
 def emb_sort_ahead(ids: torch.Tensor, vocab_start: int, v_local: int):
     """The embedding backward's sort (see ops.dispatch.emb_sort_ahead); nothing to do here."""
     return None

@@ -392,6 +392,27 @@ def test_ce_finalize_and_valid_scale(C, nsh, M):
     assert torch.equal(n, rn) and _rel(gs, rg) < 1e-6
 
 
+@pytest.mark.parametrize("M,V,start", [(32768, 50304, 0), (1000, 1024, 0), (4097, 6288, 6288), (5, 10, 0),
+                                       (70000, 12000, 24000)])
+def test_emb_sort_matches_stable_sort(C, M, V, start):
+    """The embedding backward's radix sort (two 8-bit LSD passes, ballot ranks): the same perm /
+    seg as a stable framework sort, with skewed ids (one very frequent row) and ids outside the
+    shard; and the sorted backward built on it equals the one built on the framework sort."""
+    torch.manual_seed(44)
+    ids = torch.randint(0, 3 * V, (M,), device=DEV) if start else torch.randint(0, V, (M,), device=DEV)
+    ids[::3] = start + V // 2          # a frequent token
+    perm, seg = C.emb_sort(ids, start, V)
+    rp, rs = R.emb_sort(ids, start, V)
+    assert torch.equal(seg, rs)
+    n = int(rs[-1])
+    assert torch.equal(perm[:n], rp[:n])
+    if M >= 1000:
+        d = torch.randn(M, 64, device=DEV).bfloat16()
+        a = C.embedding_bwd_sorted(d, ids, V, start, perm=perm, seg=seg)
+        b = R.embedding_bwd(d.float(), ids, V, start)
+        assert _rel(a, b) < 1e-5
+
+
 def test_adam_matches_torch(C):
     torch.manual_seed(11)
     ps = [torch.randn(n, device=DEV) for n in (1000, 16384 * 2 + 7, 4096)]
