@@ -68,6 +68,9 @@ def parse():
                          "exits with the headline and tp_pure = {error: timeout}")
     ap.add_argument("--pg-timeout-s", type=float, default=240.0,
                     help="process-group (RCCL watchdog) timeout, well under the driver's lease")
+    ap.add_argument("--fp32", action="store_true",
+                    help="fp32 compute (the reference's default without --bf16): the fp32-input MFMA kernel set "
+                         "(ops/fp32_native.py); with --impl reference, eager fp32 without autocast. NOT the headline")
     ap.add_argument("--fp8", action="store_true",
                     help="fp8 (e4m3 / e5m2) forward and data-gradient GEMMs on hipBLASLt fp8 kernels (ops/fp8.py); "
                          "NOT the bf16 headline")
@@ -130,7 +133,7 @@ def measure(a, tp: int, world: int, dev, first: bool):
     # layout does not fit without it; a layout that does not fit at all is refused here.
     from distributed_pytorch_from_scratch_amd.utils import memory as MEM
     lay = MEM.Layout(tp=tp, dp=p.dp_size, sp=bool(args.sequence_parallel), seq=T, batch=lb,
-                     chunks=2 if tp > 1 else 1)
+                     chunks=2 if tp > 1 else 1, compute="fp32" if a.fp32 else "bf16")
     want = {"auto": None, "on": True, "off": False}[a.recompute]
     free = MEM.device_free_bytes() if dev.type == "cuda" else None
     rc, est = MEM.plan(args, lay, free, want) if a.impl == "ours" else (False, MEM.estimate(args, lay))
@@ -148,6 +151,8 @@ def measure(a, tp: int, world: int, dev, first: bool):
     if a.impl == "ours":
         model = Transformer.from_args(args).to(dev)
         model.reset_parameters()
+        if a.fp32:
+            model.set_compute_dtype(torch.float32)
         opt = FusedAdam(model.parameters(), lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.0)
         step = TrainStep(model, opt)
 
@@ -167,7 +172,7 @@ def measure(a, tp: int, world: int, dev, first: bool):
 
         def run(i):
             b = pool[i % n_pool]
-            with torch.autocast("cuda", dtype=torch.bfloat16):
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=not a.fp32):
                 logits = model(b[:, :-1], pos)
                 loss = F.cross_entropy(logits.float().view(-1, V), b[:, 1:].reshape(-1), ignore_index=-1)
             opt.zero_grad()
@@ -398,7 +403,8 @@ def report(a, head, layouts, world, dev):
         "higher_is_better": True,
         "scaling": "strong" if a.global_batch else "weak",
         "vs_baseline": round(vs, 4) if vs else None,
-        "dtype": ("fp8-e4m3/e5m2 GEMMs + bf16" if a.fp8 else "bf16") if dev.type == "cuda" else "fp32",
+        "dtype": ("fp32" if a.fp32 else "fp8-e4m3/e5m2 GEMMs + bf16" if a.fp8 else "bf16") if dev.type == "cuda"
+                 else "fp32",
         "data": "synthetic (uniform random token ids), random-init weights",
         "config": {
             "model": a.model + (f"(L={a.layers})" if a.layers else ""),

@@ -99,6 +99,15 @@ void dpfs_ce_finalize(const float*, const int64_t*, long long, float*, float*, f
                       hipStream_t);
 void dpfs_ce_valid_scale(const int64_t*, long long, float*, float*, int, hipStream_t);
 long long dpfs_emb_sort_ws(int);
+void dpfs_gemm_f32(int, const float*, const float*, float*, const float*, int, int, int, long long, long long,
+                   long long, int, hipStream_t);
+int dpfs_attn_f32_supported_hd(int);
+void dpfs_attn_fwd_f32(const float*, const float*, const float*, float*, float*, int, int, int, int, long long,
+                       long long, long long, long long, float, int, hipStream_t);
+long long dpfs_attn_bwd_f32_ws(int, int, int, int, int);
+int dpfs_attn_bwd_f32(const float*, const float*, const float*, const float*, const float*, const float*, float*,
+                      float*, float*, float*, int, int, int, int, long long, long long, long long, long long, long long,
+                      long long, long long, long long, float, int, const int64_t*, const float*, float*, hipStream_t);
 void dpfs_emb_sort(const int64_t*, int, long long, int, int*, int64_t*, int64_t*, hipStream_t);
 long long dpfs_attn_fused_ws(int, int, int, int);
 long long dpfs_attn_fused_bias_ws(int, int, int, int);
@@ -791,6 +800,117 @@ bool attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tenso
                        delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), (int)B, (int)T, (int)H,
                        (int)hd, vdo.ld, vq.ld, vk.ld, vv.ld, vo.ld, vdq.ld, vdk.ld, vdv.ld, (float)scale, causal ? 1 : 0,
                        rp, rt, stream(), db, db ? bws.data_ptr<float>() : nullptr, (int)impl) != 0;
+}
+
+// ----------------------------------------------------------------------- fp32 path --
+// The reference's default (fp32) training on the device: fp32-input MFMA GEMMs and flash
+// attention (csrc/kernels/fp32.hip).  layout 0 = NT: c[M,N] = a[M,K] b[N,K]^T (+ bias);
+// 1 = NN: a[M,K] b[K,N]; 2 = TN: a[K,M]^T b[K,N] (+= into out with accumulate).
+torch::Tensor gemm_f32(torch::Tensor a, torch::Tensor b, int64_t layout, c10::optional<torch::Tensor> bias,
+                       c10::optional<torch::Tensor> out, bool accumulate) {
+  check_cuda(a, "a");
+  check_cuda(b, "b");
+  TORCH_CHECK(a.scalar_type() == torch::kFloat32 && b.scalar_type() == torch::kFloat32, "gemm_f32: fp32 operands");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1, "gemm_f32: row-major 2-D operands");
+  TORCH_CHECK(layout >= 0 && layout <= 2, "gemm_f32: layout 0 / 1 / 2");
+  const int64_t M = layout == 2 ? a.size(1) : a.size(0), K = layout == 2 ? a.size(0) : a.size(1);
+  const int64_t N = layout == 0 ? b.size(0) : b.size(1);
+  TORCH_CHECK((layout == 0 ? b.size(1) : b.size(0)) == K, "gemm_f32: inner dimensions differ");
+  const at::DeviceGuard g(a.device());
+  torch::Tensor c;
+  if (out.has_value() && out->defined()) {
+    c = *out;
+    TORCH_CHECK(c.scalar_type() == torch::kFloat32 && c.dim() == 2 && c.size(0) == M && c.size(1) == N &&
+                    c.stride(1) == 1, "gemm_f32: out fp32 [M, N] row-major");
+  } else {
+    c = torch::empty({M, N}, a.options());
+    accumulate = false;
+  }
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->is_contiguous() && bias->numel() == N,
+                "gemm_f32: bias fp32 [N]");
+    bp = bias->data_ptr<float>();
+  }
+  if (M && N) {
+    if (K == 0) {
+      if (!accumulate) c.zero_();
+      if (bp) c.add_(*bias);
+    } else {
+      dpfs_gemm_f32((int)layout, a.data_ptr<float>(), b.data_ptr<float>(), c.data_ptr<float>(), bp, (int)M, (int)N,
+                    (int)K, a.stride(0), b.stride(0), c.stride(0), accumulate ? 1 : 0, stream());
+    }
+  }
+  return c;
+}
+
+View4 check_bthd_f32(const torch::Tensor& t, const char* name, int64_t B, int64_t T, int64_t H, int64_t hd) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32, name, " must be fp32");
+  TORCH_CHECK(t.dim() == 4 && t.size(0) == B && t.size(1) == T && t.size(2) == H && t.size(3) == hd, name,
+              " must be (B, T, H, hd)");
+  TORCH_CHECK(t.stride(3) == 1 && t.stride(2) == hd && (B == 1 || t.stride(0) == T * t.stride(1)), name,
+              " must be a (B*T, ld) row view with packed heads");
+  TORCH_CHECK(t.stride(1) % 4 == 0 && (reinterpret_cast<uintptr_t>(t.data_ptr()) % 16) == 0, name,
+              " token stride must be a multiple of 4 floats (16-byte rows)");
+  return {(long long)t.stride(1)};
+}
+
+std::vector<torch::Tensor> attn_fwd_f32(torch::Tensor q, torch::Tensor k, torch::Tensor v, double scale, bool causal) {
+  const int64_t B = q.size(0), T = q.size(1), H = q.size(2), hd = q.size(3);
+  TORCH_CHECK(dpfs_attn_f32_supported_hd((int)hd), "attn_fwd_f32: head_dim ", hd, " not supported (32/64/128)");
+  auto vq = check_bthd_f32(q, "q", B, T, H, hd), vk = check_bthd_f32(k, "k", B, T, H, hd),
+       vv = check_bthd_f32(v, "v", B, T, H, hd);
+  const at::DeviceGuard g(q.device());
+  auto o = torch::empty({B, T, H, hd}, q.options());
+  auto lse = torch::empty({B, H, T}, q.options());
+  if (B * T * H)
+    dpfs_attn_fwd_f32(q.data_ptr<float>(), k.data_ptr<float>(), v.data_ptr<float>(), o.data_ptr<float>(),
+                      lse.data_ptr<float>(), (int)B, (int)T, (int)H, (int)hd, vq.ld, vk.ld, vv.ld, H * hd,
+                      (float)scale, causal ? 1 : 0, stream());
+  return {o, lse};
+}
+
+bool attn_bwd_f32(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Tensor o,
+                  torch::Tensor lse, double scale, bool causal, torch::Tensor dq, torch::Tensor dk, torch::Tensor dv,
+                  c10::optional<torch::Tensor> rope_pos, c10::optional<torch::Tensor> rope_tab,
+                  c10::optional<torch::Tensor> dbias) {
+  const int64_t B = q.size(0), T = q.size(1), H = q.size(2), hd = q.size(3);
+  TORCH_CHECK(dpfs_attn_f32_supported_hd((int)hd), "attn_bwd_f32: head_dim not supported");
+  auto vq = check_bthd_f32(q, "q", B, T, H, hd), vk = check_bthd_f32(k, "k", B, T, H, hd),
+       vv = check_bthd_f32(v, "v", B, T, H, hd);
+  auto vdo = check_bthd_f32(dout, "dout", B, T, H, hd), vo = check_bthd_f32(o, "o", B, T, H, hd);
+  auto vdq = check_bthd_f32(dq, "dq", B, T, H, hd), vdk = check_bthd_f32(dk, "dk", B, T, H, hd),
+       vdv = check_bthd_f32(dv, "dv", B, T, H, hd);
+  TORCH_CHECK(lse.is_cuda() && lse.scalar_type() == torch::kFloat32 && lse.is_contiguous() && lse.numel() == B * H * T,
+              "attn_bwd_f32: lse must be contiguous fp32 (B, H, T)");
+  const at::DeviceGuard g(q.device());
+  float* db = nullptr;
+  if (dbias.has_value() && dbias->defined()) {
+    TORCH_CHECK(dbias->is_cuda() && dbias->scalar_type() == torch::kFloat32 && dbias->is_contiguous() &&
+                    dbias->numel() == 3 * H * hd, "attn_bwd_f32: dbias must be contiguous fp32 [3 * H * hd]");
+    db = dbias->data_ptr<float>();
+  }
+  if (B * T * H == 0) {
+    if (db) dbias->zero_();
+    return db != nullptr;
+  }
+  const int64_t* rp = nullptr;
+  const float* rt = nullptr;
+  if (rope_pos.has_value() && rope_pos->defined()) {
+    TORCH_CHECK(rope_pos->scalar_type() == torch::kInt64 && rope_pos->is_contiguous() && rope_pos->numel() == B * T,
+                "attn_bwd_f32: rope_pos must be contiguous int64 [B*T]");
+    TORCH_CHECK(rope_tab.has_value() && rope_tab->scalar_type() == torch::kFloat32 && rope_tab->is_contiguous() &&
+                    rope_tab->dim() == 2 && rope_tab->size(1) == hd, "attn_bwd_f32: rope_tab fp32 [maxlen, hd]");
+    rp = rope_pos->data_ptr<int64_t>();
+    rt = rope_tab->data_ptr<float>();
+  }
+  auto ws = torch::empty({dpfs_attn_bwd_f32_ws((int)B, (int)T, (int)H, (int)hd, db ? 1 : 0)}, lse.options());
+  return dpfs_attn_bwd_f32(dout.data_ptr<float>(), q.data_ptr<float>(), k.data_ptr<float>(), v.data_ptr<float>(),
+                           o.data_ptr<float>(), lse.data_ptr<float>(), ws.data_ptr<float>(), dq.data_ptr<float>(),
+                           dk.data_ptr<float>(), dv.data_ptr<float>(), (int)B, (int)T, (int)H, (int)hd, vdo.ld, vq.ld,
+                           vk.ld, vv.ld, vo.ld, vdq.ld, vdk.ld, vdv.ld, (float)scale, causal ? 1 : 0, rp, rt, db,
+                           stream()) != 0;
 }
 
 // ------------------------------------------------------------------- embedding / CE --
@@ -1497,6 +1617,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("emb_sort", &emb_sort, py::arg("ids"), py::arg("vocab_start"), py::arg("v_local"),
         "(perm, seg): the ids' stable order by local vocab row (out-of-shard ids last) and each row's segment "
         "start, int64 (deterministic radix sort on HIP kernels)");
+  m.def("gemm_f32", &gemm_f32, py::arg("a"), py::arg("b"), py::arg("layout"), py::arg("bias") = py::none(),
+        py::arg("out") = py::none(), py::arg("accumulate") = false,
+        "fp32 MFMA GEMM (v_mfma_f32_32x32x2_f32, exact fp32): layout 0 = a b^T (+ bias), 1 = a b, 2 = a^T b (+=)");
+  m.def("attn_fwd_f32", &attn_fwd_f32, "fp32 causal flash attention forward: (o, lse)");
+  m.def("attn_bwd_f32", &attn_bwd_f32, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
+        py::arg("lse"), py::arg("scale"), py::arg("causal"), py::arg("dq"), py::arg("dk"), py::arg("dv"),
+        py::arg("rope_pos") = py::none(), py::arg("rope_tab") = py::none(), py::arg("dbias") = py::none(),
+        "fp32 flash attention backward (dQ kernel, then dK/dV), optional inverse RoPE and QKV bias gradient");
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd_sorted", &embedding_bwd_sorted, py::arg("dout"), py::arg("ids"), py::arg("v_local"),
         py::arg("vocab_start"), py::arg("out") = py::none(), py::arg("accumulate") = false,

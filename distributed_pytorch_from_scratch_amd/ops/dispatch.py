@@ -1,32 +1,44 @@
 """Device -> kernel-set selection.
 
 ``K(t)`` returns the module implementing the kernel API for tensor ``t``: the native HIP
-extension for GPU tensors (loud failure if it is not built), ``reference`` for CPU tensors and
-for fp32 compute on the GPU.
-Both expose identical function names/signatures (see ``ops/reference.py``).
+extension for bf16 compute on the GPU, ``ops/fp32_native.py`` (the native fp32 kernel set) for
+fp32 compute on the GPU -- both fail loudly if the extension is not built -- and
+``ops/reference.py`` (the PyTorch oracle) for CPU tensors.  All three expose the same
+function names / signatures.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
-from . import _ext, reference
+from . import _ext, fp32_native, reference
 
 
 def K(t: torch.Tensor, dtype: "torch.dtype | None" = None):
-    """Kernel set for tensor ``t`` computed in ``dtype`` (default: ``t.dtype``): the native
-    HIP extension for bf16 / fp16 / integer work on the GPU, ``reference`` on the CPU and for
-    fp32 compute on the GPU -- the reference's default fp32 training (``train.py`` without
-    ``--bf16``, ``/root/reference/train.py:58-63``) runs the fp32 PyTorch oracle on the
-    device, the MFMA kernels being bf16-in / fp32-accumulate."""
-    if t.is_cuda and (dtype or t.dtype) != torch.float32:
-        return _ext.require()
+    """Kernel set for tensor ``t`` computed in ``dtype`` (default: ``t.dtype``): on the GPU the
+    native HIP extension for bf16 work and ``fp32_native`` (fp32-input MFMA GEMMs and flash
+    attention + the shared fp32-capable kernels) for fp32 compute -- the reference's default
+    training (``train.py`` without ``--bf16``, ``/root/reference/train.py:58-63``); the
+    ``reference`` PyTorch oracle on the CPU (and on the GPU only with ``DPFS_FP32_ORACLE=1``,
+    an A/B switch)."""
+    if t.is_cuda:
+        if (dtype or t.dtype) != torch.float32:
+            return _ext.require()
+        if not _fp32_oracle():
+            _ext.require()
+            return fp32_native
     return reference
+
+
+def _fp32_oracle() -> bool:
+    return os.environ.get("DPFS_FP32_ORACLE", "0") == "1"
 
 
 def native_fp32() -> bool:
     """Whether fp32 compute on the GPU runs on the native kernel set (fp32 MFMA GEMMs, fp32
     flash attention) rather than the PyTorch oracle with materialised attention scores."""
-    return False
+    return not _fp32_oracle()
 
 
 def shadow(p: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:

@@ -44,6 +44,12 @@ _times: Dict[Tuple, Dict[str, float]] = {}   # key -> {candidate: ms} at selecti
 TN_GROUP = True
 
 
+def _direct(k) -> bool:
+    """A kernel set whose ops are called as they are, without per-shape candidate timing: the
+    CPU oracle (``reference``) and the fp32 kernel set (``fp32_native``, one kernel per op)."""
+    return k is reference or getattr(k, "DIRECT", False)
+
+
 def mode() -> str:
     return os.environ.get("DPFS_GEMM_BACKEND", "auto")
 
@@ -178,7 +184,7 @@ def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, out=None) -> torch.T
     if fw is not None:          # fp8 step (ModelArgs.fp8): e4m3 operands, hipBLASLt fp8 GEMM
         return F8.nt(x, fw, bias, out=out)
     m = mode()
-    if k is reference or not x.is_cuda or (m in ("ours", "auto") and _aligned(x.shape[1], w.shape[0])
+    if _direct(k) or not x.is_cuda or (m in ("ours", "auto") and _aligned(x.shape[1], w.shape[0])
                                            and x.shape[0] < _MIN_ROWS) or \
             (m == "ours" and _aligned(x.shape[1], w.shape[0])):
         return k.gemm_nt(x, w, bias, out=out)
@@ -224,7 +230,7 @@ def swiglu_epilogue(k, w: torch.Tensor, want: Optional[bool] = None) -> bool:
     turns it off."""
     if w.size(0) % 128 or want is False:
         return False
-    if k is reference or not w.is_cuda:
+    if _direct(k) or not w.is_cuda:
         return bool(want)
     return mode() in ("auto", "ours") and F8.lookup(w) is None and hasattr(k, "gemm_nt_swiglu")
 
@@ -254,7 +260,7 @@ def down_dgrad_swiglu(k, dy: torch.Tensor, w: torch.Tensor, gu: torch.Tensor, db
     gemm_nn + swiglu_bwd where the fused kernel declines the shape, for the fp8 step or a pinned
     library backend (profiles/r4_swiglu_bwd_epilogue_ab.txt: the fused form is 0.40 ms/step
     faster)."""
-    fused = (k is not reference and dy.is_cuda and mode() in ("auto", "ours") and F8.lookup(w, dgrad=True) is None
+    fused = (not _direct(k) and dy.is_cuda and mode() in ("auto", "ours") and F8.lookup(w, dgrad=True) is None
              and hasattr(k, "gemm_nn_swiglu_bwd"))
     if fused:
         r = k.gemm_nn_swiglu_bwd(dy, w, gu, dbias, perm)
@@ -269,7 +275,7 @@ def small_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, swiglu: bool = Fals
     csrc/kernels/decode.hip; SwiGLU fused into its operand load) wherever it applies, else
     hipBLASLt after a separate SwiGLU pass.  Not timed per shape: at these sizes a host-timed
     loop measures launch cost (see _MIN_ROWS); the kernel times are in profiles/."""
-    if k is reference or not x.is_cuda:
+    if _direct(k) or not x.is_cuda:
         return k.gemv_nt(x, w, bias, swiglu)
     if mode() != "blas" and k.gemv_nt_ok(x, w, swiglu):
         return k.gemv_nt(x, w, bias, swiglu)
@@ -282,7 +288,7 @@ def gemm_nn(k, a: torch.Tensor, b: torch.Tensor, out=None) -> torch.Tensor:
     if fw is not None:          # fp8 step: e5m2 gradient x e4m3 weight
         return F8.nn(a, fw, out=out)
     m = mode()
-    if k is reference or not a.is_cuda or (m in ("ours", "auto") and _aligned(a.shape[1], b.shape[1])
+    if _direct(k) or not a.is_cuda or (m in ("ours", "auto") and _aligned(a.shape[1], b.shape[1])
                                            and a.shape[0] < _MIN_ROWS) or \
             (m == "ours" and _aligned(a.shape[1], b.shape[1])):
         return k.gemm_nn(a, b, out=out)
@@ -325,7 +331,7 @@ def gemm_nt_rope(k, x: torch.Tensor, w: torch.Tensor, bias, pos, tab, rot_heads:
         k.rope_(y, pos, tab, rot_heads, hd, False)
         return y
     m = mode()
-    if k is reference or not x.is_cuda or m == "ours" or not _aligned(x.shape[1], w.shape[0]) \
+    if _direct(k) or not x.is_cuda or m == "ours" or not _aligned(x.shape[1], w.shape[0]) \
             or x.shape[0] < _MIN_ROWS:
         return k.gemm_nt(x, w, bias, pos, tab, rot_heads, hd)
     bb = shadow(bias, x.dtype) if bias is not None else None
@@ -416,7 +422,7 @@ def gemm_tn(k, a: torch.Tensor, b: torch.Tensor, out=None, accumulate: bool = Fa
     with ``DPFS_GEMM_LIB=1`` hipBLASLt through torch (fp32 output) or directly (accumulating
     in place, beta = 1), timed per (shape, accumulate) on a scratch output (an accumulating
     candidate must not be timed into the live gradient)."""
-    if k is reference or not a.is_cuda:
+    if _direct(k) or not a.is_cuda:
         return k.gemm_tn(a, b, out, accumulate) if out is not None else k.gemm_tn(a, b)
     if not _aligned(a.shape[1], b.shape[1]):
         c = torch.matmul(a.t(), b).float()
@@ -472,7 +478,7 @@ def gemm_tn_pair(k, a0: torch.Tensor, b0: torch.Tensor, a1: torch.Tensor, b1: to
         c = gemm_tn(k, a0, b0, dst, acc)
         return gemm_tn(k, a1, b1, c, True)
 
-    if k is reference or not a0.is_cuda or not hasattr(k, "gemm_tn2") or mode() not in ("auto", "ours"):
+    if _direct(k) or not a0.is_cuda or not hasattr(k, "gemm_tn2") or mode() not in ("auto", "ours"):
         return split(out, accumulate)
     M, N = a0.shape[1], b0.shape[1]
     if not _aligned(M, N) or min(a0.shape[0], a1.shape[0]) < _MIN_ROWS:
@@ -511,7 +517,7 @@ def gemm_tn_group(k, items) -> list:
             return [gemm_tn_pair(k, a, b, a1, b1, d, acc) for (a, b, _, acc, a1, b1), d in zip(items, dsts)]
         return [gemm_tn(k, a, b, d, acc) for (a, b, _, acc, _, _), d in zip(items, dsts)]
 
-    if (not TN_GROUP or k is reference or len(items) < 2 or any(o is None for o in outs) or not items[0][0].is_cuda
+    if (not TN_GROUP or _direct(k) or len(items) < 2 or any(o is None for o in outs) or not items[0][0].is_cuda
             or not hasattr(k, "gemm_tn_group") or mode() not in ("auto", "ours")
             or any((it[4] is not None) != two for it in items)):
         return each(outs)

@@ -71,8 +71,8 @@ def get_train_args(argv=None) -> Namespace:
     g.add_argument("--reserv_last_n_ckpts", type=int, default=-1)
     g.add_argument("--batch_size", "-b", type=int, default=32)
     g.add_argument("--bf16", action="store_true",
-                   help="bf16 compute on the MI355X MFMA kernels (default fp32, as the reference: on the GPU the "
-                        "fp32 PyTorch kernel set)")
+                   help="bf16 compute on the MI355X bf16 MFMA kernels (default fp32, as the reference: on the "
+                        "GPU the fp32-input MFMA kernel set)")
     g.add_argument("--fp8", action="store_true",
                    help="fp8 (e4m3 / e5m2) GEMMs for the large projections, run on hipBLASLt fp8 kernels "
                         "(ops/fp8.py; quantisation on our HIP kernels); bf16 elsewhere")
@@ -110,12 +110,14 @@ def train(rank, args: Namespace):
     grank = dist.get_rank()
     dev = torch.device("cuda", torch.cuda.current_device()) if use_cuda else torch.device("cpu")
     # the reference's flag semantics (train.py:58-63): fp32 unless --bf16.  On the GPU, fp32
-    # runs the fp32 PyTorch kernel set (ops.dispatch.K); --bf16 runs the MI355X MFMA kernels.
+    # runs the native fp32 kernel set (ops/fp32_native.py: fp32-input MFMA GEMMs and flash
+    # attention); --bf16 runs the bf16 MFMA kernels.
     compute_dtype = torch.bfloat16 if args.bf16 else torch.float32
     log0 = (lambda *a_: print(*a_, flush=True)) if grank == 0 else (lambda *a_: None)
     log0(f"{'Enable' if compute_dtype == torch.bfloat16 else 'Disable'} bf16 training  [{p}]")
     if use_cuda and compute_dtype == torch.float32:
-        log0("fp32 on the GPU: the fp32 PyTorch kernels (numerics reference); pass --bf16 for the MFMA kernels")
+        log0("fp32 on the GPU: fp32-input MFMA kernels (exact fp32, 1/16 of the bf16 MFMA rate); "
+             "pass --bf16 for the bf16 MFMA kernels")
 
     margs = replace(get_preset(args.model), sequence_parallel=args.sp, fp8=getattr(args, "fp8", False))
     seq_len = args.seq_len or margs.maxlen

@@ -1,13 +1,17 @@
 """fp32 training on the GPU (the reference's default without --bf16, /root/reference/train.py:
-58-63): the engines run the fp32 PyTorch kernel set on the device (ops.dispatch.K with an fp32
-compute dtype), and TP stays numerically transparent -- the SURVEY §0 invariant checked on the
-MI355X: TP = 1 / 2 / 4 (and SP) losses over Adam steps equal the vanilla fp32 model's on the
-CPU to 2e-5.  Ranks share one GPU over gloo."""
+58-63): the engines run the native fp32 kernel set on the device (ops.dispatch.K with an fp32
+compute dtype -> ops/fp32_native.py: fp32-input MFMA GEMMs and flash attention), and TP stays
+numerically transparent -- the SURVEY §0 invariant checked on the MI355X: TP = 1 / 2 / 4 (and
+SP) losses over Adam steps equal the vanilla fp32 model's on the CPU to 2e-5.  Ranks share one
+GPU over gloo."""
 import pytest
 import torch
 
 from dist_helpers import run_distributed
-from test_model_tp_equivalence import CFG, _batch, _train_vanilla
+from test_model_tp_equivalence import _batch, _train_vanilla
+
+# head_dim 32 (the native fp32 attention's smallest), 4 heads: one per rank at TP 4
+CFG = dict(attn_dim=128, ffn_dim=256, num_heads=4, num_layers=2, vocab_size=96, maxlen=64)
 
 pytestmark = pytest.mark.gpu
 
@@ -20,6 +24,8 @@ def _train_gpu(rank, world, cfg, steps, sp):
     set_seed(0)
     m.reset_parameters()            # on the CPU: the vanilla model's RNG order
     m = m.cuda().set_compute_dtype(torch.float32)
+    from distributed_pytorch_from_scratch_amd.ops import dispatch, fp32_native
+    assert dispatch.K(m.embedding.weight, torch.float32) is fp32_native   # the native fp32 kernels
     opt = torch.optim.Adam(m.parameters(), lr=1e-3)
     losses = []
     for s in range(steps):

@@ -413,6 +413,63 @@ def test_emb_sort_matches_stable_sort(C, M, V, start):
         assert _rel(a, b) < 1e-5
 
 
+@pytest.mark.parametrize("layout,M,N,K", [(0, 300, 200, 96), (0, 1024, 768, 512), (1, 257, 129, 64), (1, 512, 2048, 768),
+                                         (2, 768, 768, 1000), (2, 96, 130, 33), (0, 65, 67, 7)])
+def test_gemm_f32(C, layout, M, N, K):
+    """fp32-input MFMA GEMM (exact fp32 products, the fp32 training path) in the three layouts
+    against float64: bias (NT), accumulate into an existing output (TN), ragged / unaligned
+    shapes and a column-slice output."""
+    torch.manual_seed(45)
+    if layout == 0:
+        a, b = torch.randn(M, K, device=DEV), torch.randn(N, K, device=DEV)
+        ref = a.double() @ b.double().t()
+    elif layout == 1:
+        a, b = torch.randn(M, K, device=DEV), torch.randn(K, N, device=DEV)
+        ref = a.double() @ b.double()
+    else:
+        a, b = torch.randn(K, M, device=DEV), torch.randn(K, N, device=DEV)
+        ref = a.double().t() @ b.double()
+    bias = torch.randn(N, device=DEV) if layout == 0 else None
+    c = C.gemm_f32(a, b, layout, bias)
+    want = ref + (bias.double() if bias is not None else 0)
+    assert (c.double() - want).abs().max().item() < 1e-4 * max(1.0, K ** 0.5)
+    if layout == 2:
+        acc = torch.randn(M, N, device=DEV)
+        want2 = acc.double() + ref
+        C.gemm_f32(a, b, 2, None, acc, True)
+        assert (acc.double() - want2).abs().max().item() < 1e-4 * max(1.0, K ** 0.5)
+    wide = torch.zeros(M, N + 8, device=DEV)
+    C.gemm_f32(a, b, layout, bias, wide[:, :N])
+    assert torch.equal(wide[:, :N], c) and not wide[:, N:].any()
+
+
+@pytest.mark.parametrize("B,T,H,hd,causal", [(2, 256, 2, 64, True), (1, 300, 3, 64, True), (1, 130, 2, 128, True),
+                                             (2, 192, 2, 32, True), (1, 200, 2, 64, False)])
+def test_attention_f32(C, B, T, H, hd, causal):
+    """fp32 flash attention (fp32-input MFMAs) forward / backward against the fp32 oracle,
+    packed QKV views, with inverse RoPE and the QKV bias gradient in the backward."""
+    torch.manual_seed(46)
+    qkv = torch.randn(B * T, 3 * H * hd, device=DEV)
+    q, k, v = (qkv[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+    scale = hd ** -0.5
+    o, lse = C.attn_fwd_f32(q, k, v, scale, causal)
+    orf, lser = R.attn_fwd(q, k, v, scale, causal)
+    assert _rel(o, orf) < 1e-5 and (lse - lser).abs().max().item() < 1e-4
+    do = torch.randn_like(o)
+    pos = torch.randint(0, 1024, (B * T,), device=DEV)
+    tab = R.rope_table(1024, hd, 10000.0).to(DEV)
+    d = torch.empty_like(qkv)
+    dq, dk, dv = (d[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+    db = torch.full((3 * H * hd,), float("nan"), device=DEV)
+    assert C.attn_bwd_f32(do, q, k, v, o, lse, scale, causal, dq, dk, dv, pos, tab, db)
+    r = torch.empty(B * T, 3 * H * hd, device=DEV)
+    rq, rk, rv = (r[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+    rdb = torch.empty(3 * H * hd, device=DEV)
+    R.attn_bwd(do, q, k, v, o, lse, scale, causal, rq, rk, rv, pos, tab, dbias=rdb)
+    assert _rel(d, r) < 1e-4, _rel(d, r)
+    assert _rel(db, rdb) < 1e-4
+
+
 def test_adam_matches_torch(C):
     torch.manual_seed(11)
     ps = [torch.randn(n, device=DEV) for n in (1000, 16384 * 2 + 7, 4096)]
