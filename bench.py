@@ -145,7 +145,9 @@ def measure(a, tp: int, world: int, dev, first: bool):
     # same synthetic data on every rank of a TP group, a different stream per DP replica
     g = torch.Generator(device=dev).manual_seed(1234 + 7919 * p.dp_rank)
     n_pool = 4
+    # (ids, targets) as separate contiguous tensors, as a data loader hands them over
     pool = [torch.randint(0, V, (lb, T + 1), device=dev, generator=g) for _ in range(n_pool)]
+    pool = [(b[:, :-1].contiguous(), b[:, 1:].contiguous()) for b in pool]
     pos = torch.arange(T, device=dev).unsqueeze(0).expand(lb, T).contiguous()
 
     if a.impl == "ours":
@@ -157,8 +159,8 @@ def measure(a, tp: int, world: int, dev, first: bool):
         step = TrainStep(model, opt)
 
         def run(i):
-            b = pool[i % n_pool]
-            return step(b[:, :-1], pos, b[:, 1:])
+            ids, tgt = pool[i % n_pool]
+            return step(ids, pos, tgt)
     else:
         assert world == 1, "--impl reference is the single-GPU eager baseline"
         sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -171,10 +173,10 @@ def measure(a, tp: int, world: int, dev, first: bool):
         opt = torch.optim.Adam(model.parameters(), lr=3e-4)
 
         def run(i):
-            b = pool[i % n_pool]
+            ids, tgt = pool[i % n_pool]
             with torch.autocast("cuda", dtype=torch.bfloat16, enabled=not a.fp32):
-                logits = model(b[:, :-1], pos)
-                loss = F.cross_entropy(logits.float().view(-1, V), b[:, 1:].reshape(-1), ignore_index=-1)
+                logits = model(ids, pos)
+                loss = F.cross_entropy(logits.float().view(-1, V), tgt.reshape(-1), ignore_index=-1)
             opt.zero_grad()
             loss.backward()
             opt.step()

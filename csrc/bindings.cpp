@@ -95,12 +95,16 @@ int dpfs_attn_bwd(const void*, const void*, const void*, const void*, const void
                    void*, int, int, int, int, long long, long long, long long, long long, long long, long long,
                    long long, long long, float, int, const int64_t*, const float*, hipStream_t, float*, float*, int);
 long long dpfs_attn_bias_ws(int, int, int, int);
-void dpfs_ce_finalize(const float*, const int64_t*, long long, float*, float*, float*, float*, int, int, int, int,
-                      hipStream_t);
-void dpfs_ce_valid_scale(const int64_t*, long long, float*, float*, int, hipStream_t);
+int dpfs_ce_part_floats();
+void dpfs_ce_finalize(const float*, const int64_t*, long long, float*, float*, float*, float*, float*, int, int, int,
+                      int, hipStream_t);
+void dpfs_ce_valid_scale(const int64_t*, long long, float*, float*, float*, int, hipStream_t);
 long long dpfs_emb_sort_ws(int);
+void dpfs_occupy(int, double, hipStream_t);
+void dpfs_attn_stagger(int);
 void dpfs_gemm_f32(int, const float*, const float*, float*, const float*, int, int, int, long long, long long,
-                   long long, int, hipStream_t);
+                   long long, int, float*, hipStream_t);
+int dpfs_gemm_f32_splits(int, int, int);
 int dpfs_attn_f32_supported_hd(int);
 void dpfs_attn_fwd_f32(const float*, const float*, const float*, float*, float*, int, int, int, int, long long,
                        long long, long long, long long, float, int, hipStream_t);
@@ -837,8 +841,12 @@ torch::Tensor gemm_f32(torch::Tensor a, torch::Tensor b, int64_t layout, c10::op
       if (!accumulate) c.zero_();
       if (bp) c.add_(*bias);
     } else {
+      const int sp = dpfs_gemm_f32_splits((int)M, (int)N, (int)K);   // K-split slabs (weight gradients)
+      torch::Tensor ws;
+      if (sp > 1) ws = torch::empty({(int64_t)sp * M * N}, a.options());
       dpfs_gemm_f32((int)layout, a.data_ptr<float>(), b.data_ptr<float>(), c.data_ptr<float>(), bp, (int)M, (int)N,
-                    (int)K, a.stride(0), b.stride(0), c.stride(0), accumulate ? 1 : 0, stream());
+                    (int)K, a.stride(0), b.stride(0), c.stride(0), accumulate ? 1 : 0,
+                    sp > 1 ? ws.data_ptr<float>() : nullptr, stream());
     }
   }
   return c;
@@ -1034,9 +1042,10 @@ std::vector<torch::Tensor> ce_finalize(torch::Tensor stats, torch::Tensor target
   const at::DeviceGuard g(stats.device());
   auto lse = torch::empty({M}, stats.options());
   auto valid = torch::empty({M}, stats.options());
+  auto part = torch::empty({dpfs_ce_part_floats()}, stats.options());
   dpfs_ce_finalize(stats.data_ptr<float>(), targets.data_ptr<int64_t>(), ignore_index, lse.data_ptr<float>(),
-                   valid.data_ptr<float>(), acc.data_ptr<float>(), loss.data_ptr<float>(), (int)M,
-                   (int)stats.size(0), first ? 1 : 0, last ? 1 : 0, stream());
+                   valid.data_ptr<float>(), acc.data_ptr<float>(), loss.data_ptr<float>(), part.data_ptr<float>(),
+                   (int)M, (int)stats.size(0), first ? 1 : 0, last ? 1 : 0, stream());
   return {lse, valid};
 }
 
@@ -1047,8 +1056,9 @@ std::vector<torch::Tensor> ce_valid_scale(torch::Tensor targets, int64_t ignore_
   const int64_t M = targets.numel();
   auto gs = torch::empty({M}, targets.options().dtype(torch::kFloat32));
   auto n = torch::empty({}, targets.options().dtype(torch::kFloat32));
-  dpfs_ce_valid_scale(targets.data_ptr<int64_t>(), ignore_index, gs.data_ptr<float>(), n.data_ptr<float>(), (int)M,
-                      stream());
+  auto part = torch::empty({dpfs_ce_part_floats()}, targets.options().dtype(torch::kFloat32));
+  dpfs_ce_valid_scale(targets.data_ptr<int64_t>(), ignore_index, gs.data_ptr<float>(), n.data_ptr<float>(),
+                      part.data_ptr<float>(), (int)M, stream());
   return {gs, n};
 }
 
@@ -1625,6 +1635,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("lse"), py::arg("scale"), py::arg("causal"), py::arg("dq"), py::arg("dk"), py::arg("dv"),
         py::arg("rope_pos") = py::none(), py::arg("rope_tab") = py::none(), py::arg("dbias") = py::none(),
         "fp32 flash attention backward (dQ kernel, then dK/dV), optional inverse RoPE and QKV bias gradient");
+  m.def("occupy", [](int64_t blocks, double us) { dpfs_occupy((int)blocks, us, stream()); }, py::arg("blocks"),
+        py::arg("us"),
+        "collective stand-in on the current stream: `blocks` resident 1024-thread workgroups for `us` microseconds");
+  m.def("attn_stagger", [](int v) { dpfs_attn_stagger(v); },
+        "A/B hook: odd workgroups of the v3 attention backward kernels start v x 8k cycles late (0 default)");
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd_sorted", &embedding_bwd_sorted, py::arg("dout"), py::arg("ids"), py::arg("v_local"),
         py::arg("vocab_start"), py::arg("out") = py::none(), py::arg("accumulate") = false,

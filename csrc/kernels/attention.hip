@@ -1027,7 +1027,10 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
   const int key1 = kb1 * BK + 32 * wave + r32;
   const int nq0 = (T - (causal ? ((p * BK) / BQ) * BQ : 0) + BQ - 1) / BQ;
   // (head_dim 64 only: at 128 the one-wave-per-SIMD kernel has no register to spare for it)
-  const bool pre = HD == 64 && prefetch && kb1 != p && nq1 > 0 && nq0 >= 2;  // (uniform)
+  const bool pre = HD == 64 && (prefetch & 1) && kb1 != p && nq1 > 0 && nq0 >= 2;  // (uniform)
+  // A/B hook (prefetch >> 4 = n): odd workgroups start n x 8k cycles late, so the two workgroups
+  // sharing a CU's SIMDs run their MFMA-heavy and VALU-heavy phases offset
+  for (int sn = 0; sn < (blockIdx.x & 1) * (prefetch >> 4); ++sn) __builtin_amdgcn_s_sleep(127);
   bf16x8 kf[KS], vf[KS];
   auto load_kv = [&](int kk_) {
 #pragma unroll
@@ -1610,7 +1613,8 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
   const int qb1 = p;
   const int nkv0 = ((causal ? min(T, (nqb - p) * BQ) : T) + BKV - 1) / BKV;
   const int nkv1 = ((causal ? min(T, (qb1 + 1) * BQ) : T) + BKV - 1) / BKV;
-  const bool pre = HD == 64 && prefetch && qb1 != nqb - 1 - p && nkv0 >= 2 && nkv1 > 0;   // (uniform)
+  const bool pre = HD == 64 && (prefetch & 1) && qb1 != nqb - 1 - p && nkv0 >= 2 && nkv1 > 0;   // (uniform)
+  for (int sn = 0; sn < (blockIdx.x & 1) * (prefetch >> 4); ++sn) __builtin_amdgcn_s_sleep(127);
   bf16x8 qf[KS], df[KS], ovr[KS];   // Q^T / dO^T operands (lane: query), O for delta
   float lse_r = 0.f;
   auto load_qdo = [&](int qq) {
@@ -1826,6 +1830,9 @@ extern "C" void dpfs_attn_diag(void* p) { g_attn_diag = (unsigned long long*)p; 
 // bit 1 = dQ (3 default)
 static int g_attn_prefetch = 3;
 extern "C" void dpfs_attn_prefetch(int v) { g_attn_prefetch = v & 3; }
+// A/B hook: odd workgroups of the v3 backward kernels start v x 8k cycles late (0 default)
+static int g_attn_stagger = 0;
+extern "C" void dpfs_attn_stagger(int v) { g_attn_stagger = v & 15; }
 
 extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int T, int H,
                               int hd, long long ldq, long long ldk, long long ldv, long long ldo, float scale,
@@ -1880,7 +1887,7 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
   attn_bwd_dq3_k<HD_><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,   \
                                             (const bf16*)o, lse, delta, delta + (long long)B * H * T, (bf16*)dq, T, \
                                             H, B * H, ldq, ldk, ldv, lddo, ldo, lddq, scale, causal, rope_pos,     \
-                                            rope_tab, pq, (g_attn_prefetch >> 1) & 1)
+                                            rope_tab, pq, ((g_attn_prefetch >> 1) & 1) | (g_attn_stagger << 4))
     if (hd == 64) DQ3_LAUNCH(64);
     else DQ3_LAUNCH(128);
 #undef DQ3_LAUNCH
@@ -1896,7 +1903,7 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
   attn_bwd_dkdv3_k<HD_, DG_><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, \
                                                    delta + (long long)B * H * T, delta, (bf16*)dk, (bf16*)dv, T, H,     \
                                                    B * H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal, rope_pos,     \
-                                                   rope_tab, pk, pv, DG_ ? g_attn_diag : nullptr, g_attn_prefetch & 1)
+                                                   rope_tab, pk, pv, DG_ ? g_attn_diag : nullptr, (g_attn_prefetch & 1) | (g_attn_stagger << 4))
     if (hd == 64 && diag) DKDV3_LAUNCH(64, 1);
     else if (hd == 64) DKDV3_LAUNCH(64, 0);
     else DKDV3_LAUNCH(128, 0);

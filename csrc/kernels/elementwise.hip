@@ -495,3 +495,18 @@ extern "C" void dpfs_colsum_f32_split(const float* x, float* out, float* out2, i
   colsum_stage_k<float><<<dim3(cblocks, chunks), 256, 0, s>>>(x, ws, M, N, rpc);
   colsum_rows(ws, out, chunks, N, s, out2, split);
 }
+
+// ------------------------------------------------------------ collective emulation --
+// A stand-in for a TP collective on a side stream (tools/tp_sim.py --emulate-comm, and the
+// GEMM co-scheduling tests): `blocks` workgroups of 1024 threads -- the xGMI kernels' grid --
+// stay resident for `ticks` of the 100 MHz s_memrealtime clock (each wave sleeps between
+// polls, so what it takes from the CU is its residency, as a collective waiting on its peers
+// does), then exit.
+__global__ __launch_bounds__(1024) void occupy_k(unsigned long long ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
+}
+extern "C" void dpfs_occupy(int blocks, double us, hipStream_t s) {
+  if (blocks <= 0 || us <= 0) return;
+  occupy_k<<<blocks, 1024, 0, s>>>((unsigned long long)(us * 100.0));
+}

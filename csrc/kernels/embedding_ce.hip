@@ -14,6 +14,8 @@
 // target logit if owned; backward writes (softmax - onehot) * g in place over the logits.
 #include "common.h"
 
+#include <algorithm>
+
 namespace dpfs {
 
 template <typename TO>
@@ -458,19 +460,40 @@ static inline int cap_grid2(long long work, int block) {
 // ---------------------------------------------------------------- CE loss bookkeeping --
 // The loss scalar and per-row terms of the vocab-parallel CE from the gathered statistics
 // (replaces ~15 small framework kernels per step: amax / log / exp / where / sums / casts).
-// One 1024-thread workgroup; every sum in a fixed order (per-thread strided rows, then a
-// fixed tree), so the loss is run-to-run bit-identical.
+// Rows are split over kCeBlocks workgroups that write (loss, count) partials; a one-workgroup
+// pass adds them in block order.  Every sum has a fixed order, so the loss is run-to-run
+// bit-identical.
 //   stats (nsh, M, 3) = {max, sum exp(x - max), target logit or 0} per vocab shard;
 //   lse[r] = mx + log(sum_s se_s exp(m_s - mx)); valid[r] = (tgt[r] != ignore) as 1.0 / 0.0;
 //   acc[0] (+)= sum valid (lse - tl), acc[1] (+)= sum valid; with `last`: acc[1] = max(acc[1], 1),
 //   loss = acc[0] / acc[1].
-__global__ __launch_bounds__(1024) void ce_finalize_k(const float* __restrict__ stats, const int64_t* __restrict__ tgt,
-                                                     long long ignore, float* __restrict__ lse, float* __restrict__ valid,
-                                                     float* __restrict__ acc, float* __restrict__ loss, int M, int nsh,
-                                                     int first, int last) {
-  __shared__ float red[2][1024];
+constexpr int kCeBlocks = 64;
+
+// fixed-order block sum of (a, b) over 256 threads; thread 0 gets the totals
+__device__ __forceinline__ void block_sum2(float& a, float& b) {
+  __shared__ float red[2][256];
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + o];
+      red[1][threadIdx.x] += red[1][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  a = red[0][0];
+  b = red[1][0];
+}
+
+__global__ __launch_bounds__(256) void ce_finalize_rows_k(const float* __restrict__ stats,
+                                                          const int64_t* __restrict__ tgt, long long ignore,
+                                                          float* __restrict__ lse, float* __restrict__ valid,
+                                                          float* __restrict__ part, int M, int nsh) {
   float ls = 0.f, cn = 0.f;
-  for (int r = threadIdx.x; r < M; r += 1024) {
+  const int per = (M + gridDim.x - 1) / gridDim.x;
+  const int r0 = blockIdx.x * per, r1 = min(M, r0 + per);
+  for (int r = r0 + threadIdx.x; r < r1; r += 256) {
     float mx = -INFINITY;
     for (int sh = 0; sh < nsh; ++sh) mx = fmaxf(mx, stats[((long long)sh * M + r) * 3]);
     float se = 0.f, tl = 0.f;
@@ -486,50 +509,58 @@ __global__ __launch_bounds__(1024) void ce_finalize_k(const float* __restrict__ 
     ls += v != 0.f ? l - tl : 0.f;
     cn += v;
   }
-  red[0][threadIdx.x] = ls;
-  red[1][threadIdx.x] = cn;
-  __syncthreads();
-  for (int o = 512; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + o];
-      red[1][threadIdx.x] += red[1][threadIdx.x + o];
-    }
-    __syncthreads();
-  }
+  block_sum2(ls, cn);
   if (threadIdx.x == 0) {
-    float a0 = red[0][0], a1 = red[1][0];
-    if (!first) {
-      a0 += acc[0];
-      a1 += acc[1];
-    }
-    if (last) {
-      a1 = fmaxf(a1, 1.f);
-      loss[0] = a0 / a1;
-    }
-    acc[0] = a0;
-    acc[1] = a1;
+    part[2 * blockIdx.x] = ls;
+    part[2 * blockIdx.x + 1] = cn;
   }
+}
+
+__global__ __launch_bounds__(64) void ce_finalize_sum_k(const float* __restrict__ part, int nb,
+                                                        float* __restrict__ acc, float* __restrict__ loss, int first,
+                                                        int last) {
+  if (threadIdx.x != 0) return;
+  float a0 = 0.f, a1 = 0.f;
+  for (int b = 0; b < nb; ++b) {
+    a0 += part[2 * b];
+    a1 += part[2 * b + 1];
+  }
+  if (!first) {
+    a0 += acc[0];
+    a1 += acc[1];
+  }
+  if (last) {
+    a1 = fmaxf(a1, 1.f);
+    loss[0] = a0 / a1;
+  }
+  acc[0] = a0;
+  acc[1] = a1;
 }
 
 // gs[r] = (tgt[r] != ignore) / max(count, 1) over all M rows (the one-pass TP-1 CE's per-row
-// gradient scale for a unit loss gradient); n_valid[0] = max(count, 1).  One workgroup.
-__global__ __launch_bounds__(1024) void ce_valid_scale_k(const int64_t* __restrict__ tgt, long long ignore,
-                                                        float* __restrict__ gs, float* __restrict__ n_valid, int M) {
-  __shared__ float red[1024];
-  float cn = 0.f;
-  for (int r = threadIdx.x; r < M; r += 1024) cn += tgt[r] != ignore ? 1.f : 0.f;
-  red[threadIdx.x] = cn;
-  __syncthreads();
-  for (int o = 512; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
-  }
-  const float n = fmaxf(red[0], 1.f);
-  const float inv = 1.f / n;
-  for (int r = threadIdx.x; r < M; r += 1024) gs[r] = tgt[r] != ignore ? inv : 0.f;
-  if (threadIdx.x == 0) n_valid[0] = n;
+// gradient scale for a unit loss gradient); n_valid[0] = max(count, 1).  Per-block counts, then
+// every block adds them in block order and writes its rows.
+__global__ __launch_bounds__(256) void ce_valid_count_k(const int64_t* __restrict__ tgt, long long ignore,
+                                                        float* __restrict__ part, int M) {
+  float cn = 0.f, z = 0.f;
+  const int per = (M + gridDim.x - 1) / gridDim.x;
+  const int r0 = blockIdx.x * per, r1 = min(M, r0 + per);
+  for (int r = r0 + threadIdx.x; r < r1; r += 256) cn += tgt[r] != ignore ? 1.f : 0.f;
+  block_sum2(cn, z);
+  if (threadIdx.x == 0) part[blockIdx.x] = cn;
 }
-
+__global__ __launch_bounds__(256) void ce_valid_scale_k(const int64_t* __restrict__ tgt, long long ignore,
+                                                        const float* __restrict__ part, float* __restrict__ gs,
+                                                        float* __restrict__ n_valid, int M) {
+  float n = 0.f;
+  for (int b = 0; b < (int)gridDim.x; ++b) n += part[b];
+  n = fmaxf(n, 1.f);
+  const float inv = 1.f / n;
+  const int per = (M + gridDim.x - 1) / gridDim.x;
+  const int r0 = blockIdx.x * per, r1 = min(M, r0 + per);
+  for (int r = r0 + threadIdx.x; r < r1; r += 256) gs[r] = tgt[r] != ignore ? inv : 0.f;
+  if (blockIdx.x == 0 && threadIdx.x == 0) n_valid[0] = n;
+}
 
 // --------------------------------------------- deterministic counting sort of token ids --
 // The deterministic embedding backward needs the ids' stable order and each local vocab row's
@@ -801,13 +832,20 @@ extern "C" void dpfs_ce_bwd(int dtype, const void* logits, const int64_t* tgt, c
                                             vvalid);
 }
 
+// part: 2 * kCeBlocks floats of scratch
+extern "C" int dpfs_ce_part_floats() { return 2 * kCeBlocks; }
 extern "C" void dpfs_ce_finalize(const float* stats, const int64_t* tgt, long long ignore, float* lse, float* valid,
-                                 float* acc, float* loss, int M, int nsh, int first, int last, hipStream_t s) {
-  ce_finalize_k<<<1, 1024, 0, s>>>(stats, tgt, ignore, lse, valid, acc, loss, M, nsh, first, last);
+                                 float* acc, float* loss, float* part, int M, int nsh, int first, int last,
+                                 hipStream_t s) {
+  const int nb = std::max(1, std::min(kCeBlocks, (M + 255) / 256));
+  ce_finalize_rows_k<<<nb, 256, 0, s>>>(stats, tgt, ignore, lse, valid, part, M, nsh);
+  ce_finalize_sum_k<<<1, 64, 0, s>>>(part, nb, acc, loss, first, last);
 }
-extern "C" void dpfs_ce_valid_scale(const int64_t* tgt, long long ignore, float* gs, float* n_valid, int M,
-                                    hipStream_t s) {
-  ce_valid_scale_k<<<1, 1024, 0, s>>>(tgt, ignore, gs, n_valid, M);
+extern "C" void dpfs_ce_valid_scale(const int64_t* tgt, long long ignore, float* gs, float* n_valid, float* part,
+                                    int M, hipStream_t s) {
+  const int nb = std::max(1, std::min(kCeBlocks, (M + 255) / 256));
+  ce_valid_count_k<<<nb, 256, 0, s>>>(tgt, ignore, part, M);
+  ce_valid_scale_k<<<nb, 256, 0, s>>>(tgt, ignore, part, gs, n_valid, M);
 }
 
 // ws: 4 M + 256 * ceil(M / 1024) ints.  perm: int64 [M] (positions past seg[vlocal] hold the

@@ -18,6 +18,8 @@
 //    a row stride of HD + 1 floats (conflict-free column reads).  Only the log-sum-exp is saved.
 #include "common.h"
 
+#include <algorithm>
+
 namespace dpfs {
 
 #define MFMA_F32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x2f32((a), (b), (c), 0, 0, 0)
@@ -79,11 +81,23 @@ struct F32Tile {
 };
 
 // AK: A is K-major (a[m][k]); BK: B is K-major (b[n][k]).  C row-major fp32 with ldc.
+// Split-K (blockIdx.y = split s of gridDim.y): the K range [s kps, min(K, (s + 1) kps)) into the
+// fp32 slab C + s * slab (accumulate off); splitk_sum_f32_k adds the slabs in split order.
 template <bool AK, bool BK>
 __global__ __launch_bounds__(256) void gemm_f32_k(const float* __restrict__ A, const float* __restrict__ B,
                                                   float* __restrict__ C, const float* __restrict__ bias, int M, int N,
                                                   int K, long long lda, long long ldb, long long ldc, int accumulate,
-                                                  int vec_a, int vec_b) {
+                                                  int vec_a, int vec_b, int kps, long long slab) {
+  {
+    const int kb = blockIdx.y * kps;
+    const int ke = min(K, kb + kps);
+    if (gridDim.y > 1) {   // this split's operand panels and output slab
+      A += AK ? (long long)kb : (long long)kb * lda;
+      B += BK ? (long long)kb : (long long)kb * ldb;
+      C += blockIdx.y * slab;
+      K = ke - kb;
+    }
+  }
   __shared__ __attribute__((aligned(16))) float sa[2][kF32BK * kF32LD];
   __shared__ __attribute__((aligned(16))) float sb[2][kF32BK * kF32LD];
   const int tiles_n = (N + kF32BM - 1) / kF32BM;
@@ -274,16 +288,28 @@ __global__ __launch_bounds__(256) void attn_fwd_f32_k(const float* __restrict__ 
 template <int HD>
 __device__ __forceinline__ void inv_rope_tiles(f32x16 (&x)[HD / 32], const float* __restrict__ tr, int hf) {
   constexpr int DT = HD / 32;
+  if constexpr (DT == 1) {
+    // head_dim 32: column c < 16 (registers 0..7) pairs with c + 16 (register + 8), same tile
 #pragma unroll
-  for (int d = 0; d < DT / 2; ++d)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int c = 32 * d + 8 * (r >> 2) + 4 * hf + (r & 3);
+    for (int r = 0; r < 8; ++r) {
+      const int c = 8 * (r >> 2) + 4 * hf + (r & 3);
       const float cs = tr[c], sn = tr[HD / 2 + c];
-      const float x1 = x[d][r], x2 = x[d + DT / 2][r];
-      x[d][r] = x1 * cs + x2 * sn;
-      x[d + DT / 2][r] = x2 * cs - x1 * sn;
+      const float x1 = x[0][r], x2 = x[0][r + 8];
+      x[0][r] = x1 * cs + x2 * sn;
+      x[0][r + 8] = x2 * cs - x1 * sn;
     }
+  } else {
+#pragma unroll
+    for (int d = 0; d < DT / 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int c = 32 * d + 8 * (r >> 2) + 4 * hf + (r & 3);
+        const float cs = tr[c], sn = tr[HD / 2 + c];
+        const float x1 = x[d][r], x2 = x[d + DT / 2][r];
+        x[d][r] = x1 * cs + x2 * sn;
+        x[d + DT / 2][r] = x2 * cs - x1 * sn;
+      }
+  }
 }
 
 // dQ (query on the lane) + the row constants of dK/dV: NDEL = -delta, LSN = -lse (fp32 path:
@@ -496,6 +522,21 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_f32_k(
   }
 }
 
+// C (+)= sum over the S slabs (split order: deterministic); vectorised by 4 where aligned
+__global__ __launch_bounds__(256) void splitk_sum_f32_k(const float* __restrict__ ws, float* __restrict__ C,
+                                                        const float* __restrict__ bias, int M, int N, long long ldc,
+                                                        int S, int accumulate) {
+  const long long n = (long long)M * N;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    float acc = 0.f;
+    for (int sp = 0; sp < S; ++sp) acc += ws[sp * n + i];
+    const long long r = i / N, c = i % N;
+    if (bias) acc += bias[c];
+    float* p = C + r * ldc + c;
+    *p = accumulate ? *p + acc : acc;
+  }
+}
+
 // column sums of the per-wave partial rows: out[seg][h][c] = sum over R rows (fixed order)
 __global__ __launch_bounds__(256) void colsum_parts_f32_k(const float* __restrict__ P, float* __restrict__ out,
                                                           int R, int HD, int H) {
@@ -517,18 +558,43 @@ __global__ __launch_bounds__(256) void colsum_parts_f32_k(const float* __restric
 
 using namespace dpfs;
 
+// K-splits of an M x N x K fp32 GEMM: enough workgroups to fill the chip (~4 per CU) when the
+// output tiles alone do not, each split at least 512 deep.
+extern "C" int dpfs_gemm_f32_splits(int M, int N, int K) {
+  const long long tiles = (long long)((M + kF32BM - 1) / kF32BM) * ((N + kF32BM - 1) / kF32BM);
+  long long sp = (1024 + tiles - 1) / tiles;
+  sp = std::min<long long>(sp, std::max(1, K / 512));
+  return (int)std::max<long long>(1, std::min<long long>(sp, 64));
+}
+
 // layout: 0 = NT (a[M][K], b[N][K]), 1 = NN (a[M][K], b[K][N]), 2 = TN (a[K][M], b[K][N]).
+// ws: splits * M * N floats when dpfs_gemm_f32_splits > 1 (else unused, may be null).
 extern "C" void dpfs_gemm_f32(int layout, const float* A, const float* B, float* C, const float* bias, int M, int N,
-                              int K, long long lda, long long ldb, long long ldc, int accumulate, hipStream_t s) {
+                              int K, long long lda, long long ldb, long long ldc, int accumulate, float* ws,
+                              hipStream_t s) {
   if (M <= 0 || N <= 0) return;
-  const int grid = ((M + kF32BM - 1) / kF32BM) * ((N + kF32BM - 1) / kF32BM);
+  const int tiles = ((M + kF32BM - 1) / kF32BM) * ((N + kF32BM - 1) / kF32BM);
   const bool va = ((uintptr_t)A % 16 == 0) && lda % 4 == 0, vb = ((uintptr_t)B % 16 == 0) && ldb % 4 == 0;
+  const int S = ws ? dpfs_gemm_f32_splits(M, N, K) : 1;
+  const int kps = S > 1 ? ((K + S - 1) / S + kF32BK - 1) / kF32BK * kF32BK : K;
+  const int Sx = S > 1 ? (K + kps - 1) / kps : 1;
+  dim3 grid(tiles, Sx);
+  float* out = Sx > 1 ? ws : C;
+  const long long ldo = Sx > 1 ? N : ldc;
+  const float* bo = Sx > 1 ? nullptr : bias;
+  const int acc = Sx > 1 ? 0 : accumulate;
+  const long long slab = (long long)M * N;
   if (layout == 0)
-    gemm_f32_k<true, true><<<grid, 256, 0, s>>>(A, B, C, bias, M, N, K, lda, ldb, ldc, accumulate, va, vb);
+    gemm_f32_k<true, true><<<grid, 256, 0, s>>>(A, B, out, bo, M, N, K, lda, ldb, ldo, acc, va, vb, kps, slab);
   else if (layout == 1)
-    gemm_f32_k<true, false><<<grid, 256, 0, s>>>(A, B, C, bias, M, N, K, lda, ldb, ldc, accumulate, va, vb);
+    gemm_f32_k<true, false><<<grid, 256, 0, s>>>(A, B, out, bo, M, N, K, lda, ldb, ldo, acc, va, vb, kps, slab);
   else
-    gemm_f32_k<false, false><<<grid, 256, 0, s>>>(A, B, C, bias, M, N, K, lda, ldb, ldc, accumulate, va, vb);
+    gemm_f32_k<false, false><<<grid, 256, 0, s>>>(A, B, out, bo, M, N, K, lda, ldb, ldo, acc, va, vb, kps, slab);
+  if (Sx > 1) {
+    const long long n = (long long)M * N;
+    const int blocks = (int)std::min<long long>((n + 255) / 256, 4096);
+    splitk_sum_f32_k<<<blocks, 256, 0, s>>>(ws, C, bias, M, N, ldc, Sx, accumulate);
+  }
 }
 
 extern "C" int dpfs_attn_f32_supported_hd(int hd) { return hd == 32 || hd == 64 || hd == 128; }

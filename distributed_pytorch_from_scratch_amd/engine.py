@@ -77,7 +77,11 @@ class TrainStep:
         e1 = self._event()
         self.optimizer.zero_grad(set_to_none=True)
         with roctx("bwd"):
-            loss.backward()
+            # a cached unit gradient (autograd would fill a fresh ones tensor every step)
+            g1 = getattr(self, "_unit", None)
+            if g1 is None or g1.device != loss.device or g1.dtype != loss.dtype or g1.shape != loss.shape:
+                g1 = self._unit = torch.ones_like(loss)
+            loss.backward(g1)
             # DP first: finish() copies the DP-averaged buckets (packed during backward, before
             # any TP sum) back into .grad; the SP sum over TP must act on those copied-back grads.
             # The two sums commute, so this order gives sum_tp(mean_dp(g)).

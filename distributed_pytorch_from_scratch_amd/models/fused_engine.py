@@ -333,7 +333,12 @@ class DecoderTrainFn(torch.autograd.Function):
         F8.activate(ctx.f8map)
         _defer_begin()
         tab = ctx.tab
-        gscale_all = (gloss.float() / ctx.n_valid)
+        gscale = []   # d loss / d row-sum: only the CE backward that did not run in the forward needs it
+
+        def gscale_all():
+            if not gscale:
+                gscale.append(gloss.float() / ctx.n_valid)
+            return gscale[0]
         nL = len(layers)
         # fp32 gradients: every one is written straight into its slot of the model's gradient
         # arena (parallel/grad_sync.GradArena; the first chunk's contribution in place, later
@@ -405,7 +410,7 @@ class DecoderTrainFn(torch.autograd.Function):
         pg = pm.pgm
         dp = pg.dp_size if pg is not None else 1
         dpb = GSY.DPBucketer(arena, pg.dp_group if dp > 1 else None, dp,
-                             GSY.dp_bucket_bytes(pg.dp_group, gscale_all.device) if dp > 1 else 0,
+                             GSY.dp_bucket_bytes(pg.dp_group, gloss.device) if dp > 1 else 0,
                              before_launch=_defer_flush)
         dp_reduce = dpb.add
 
@@ -423,7 +428,7 @@ class DecoderTrainFn(torch.autograd.Function):
                                        f"({float(gloss.float().mean())}); call loss() without unit_grad when "
                                        "scaling the loss")
             else:
-                gs = s["valid"] * gscale_all
+                gs = s["valid"] * gscale_all()
                 db = first(g, "lm_b", dl, dl.size(1)) if head.bias is not None else None
                 k.ce_bwd(dl, s["tgt"], s["ce_lse"], gs, vst, vvalid, dl, db)    # + lm_head bias grad
             dh = GS.gemm_nn(k, dl, W(head.weight), out=_slot(ci, dl.size(0), d, dt))

@@ -228,7 +228,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
         # buckets of at least the measured knee of the DP group's all-reduce curve
         # (parallel/grad_sync.dp_bucket_bytes; small per-layer groups are merged)
         dpb = GSY.DPBucketer(arena, pg.dp_group if dp > 1 else None, dp,
-                             GSY.dp_bucket_bytes(pg.dp_group, gscale_all.device) if dp > 1 else 0,
+                             GSY.dp_bucket_bytes(pg.dp_group, gloss.device) if dp > 1 else 0,
                              before_launch=_defer_flush)
         dp_reduce = dpb.add
 

@@ -414,6 +414,7 @@ def test_emb_sort_matches_stable_sort(C, M, V, start):
 
 
 @pytest.mark.parametrize("layout,M,N,K", [(0, 300, 200, 96), (0, 1024, 768, 512), (1, 257, 129, 64), (1, 512, 2048, 768),
+                                         (2, 512, 512, 32000), (0, 128, 128, 8192),
                                          (2, 768, 768, 1000), (2, 96, 130, 33), (0, 65, 67, 7)])
 def test_gemm_f32(C, layout, M, N, K):
     """fp32-input MFMA GEMM (exact fp32 products, the fp32 training path) in the three layouts
@@ -468,6 +469,36 @@ def test_attention_f32(C, B, T, H, hd, causal):
     R.attn_bwd(do, q, k, v, o, lse, scale, causal, rq, rk, rv, pos, tab, dbias=rdb)
     assert _rel(d, r) < 1e-4, _rel(d, r)
     assert _rel(db, rdb) < 1e-4
+
+
+@pytest.mark.parametrize("layout,M,N,K,variant", [("nn", 32768, 768, 16384, 8), ("nn", 32768, 768, 3072, 0),
+                                                  ("nt", 32768, 2304, 768, 0), ("nt", 32768, 768, 2048, 8)])
+def test_gemm_beside_collective_standin_is_bitwise(C, layout, M, N, K, variant):
+    """The persistent v4 GEMM (static item striding over one workgroup per CU) and the stream-K
+    variant (consumers spin on their producer's flag) launched while a collective stand-in
+    (tools/tp_sim.py --emulate-comm: 64 resident 1024-thread workgroups, 3 ms) holds CUs on a
+    side stream: the output is bit-identical to the undisturbed run and no stream-K wait timed
+    out (the displaced workgroups start when the stand-in leaves)."""
+    if variant == 8 and not C.gemm_sk_applies(M, N, K):
+        pytest.skip("stream-K needs 256 x 256 tiles at exactly 1.5 per CU on this device")
+    torch.manual_seed(47)
+    a = (torch.randn(M, K, device=DEV) / 8).bfloat16()
+    b = (torch.randn(K, N, device=DEV) / 8).bfloat16() if layout == "nn" else (torch.randn(N, K, device=DEV) / 8).bfloat16()
+    run = (lambda: C.gemm_nn(a, b, variant=variant)) if layout == "nn" else (lambda: C.gemm_nt(a, b, None, variant=variant))
+    C.gemm_sk_error(True)
+    ref = run()
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    outs = []
+    for _ in range(3):
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            C.occupy(64, 3000.0)
+        outs.append(run())
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, ref)
+    assert C.gemm_sk_error(False) == 0
 
 
 def test_adam_matches_torch(C):

@@ -8,6 +8,15 @@ the replicated work (norms / residuals without SP) costs.  Numerics are meaningl
 sums are never combined); only timing is reported.
 
     python tools/tp_sim.py --tp 8 [--rank 0] [--steps 5]
+    python tools/tp_sim.py --tp 2 --emulate-comm 64 [--comm-blocks 32]
+
+``--emulate-comm GBPS`` replaces each no-op collective by a stand-in kernel on a high-priority
+side stream: the xGMI kernels' grid (``--comm-blocks`` workgroups of 1024 threads) resident
+for the collective's modelled duration at GBPS per link and direction (a W-rank two-shot
+all-reduce moves 2 x bytes / W over each link, a reduce-scatter or all-gather bytes / W), and
+the engine waits for it exactly as for the real collective.  The difference to the no-op floor
+is what losing those CUs to a collective costs the persistent / stream-K GEMMs and the rest of
+the step.
 """
 from __future__ import annotations
 
@@ -45,6 +54,12 @@ def main():
     ap.add_argument("--head-start-ms", type=float, default=0.0,
                     help="queue a GPU sleep of this length before each timed step and subtract it: "
                          "with the host that far ahead, launch latency cannot starve the GPU")
+    ap.add_argument("--emulate-comm", type=float, default=0.0,
+                    help="GB/s per xGMI link: collectives become CU-holding stand-ins of the modelled duration")
+    ap.add_argument("--comm-blocks", type=int, default=int(os.environ.get("DPFS_XGMI_BLOCKS", "32")))
+    ap.add_argument("--mem-check", action="store_true",
+                    help="also print the HBM planner's per-rank estimate of each layout (utils/memory.py; the "
+                         "xGMI staging term excluded: the simulation allocates none) against the measured peak")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -54,10 +69,39 @@ def main():
     from distributed_pytorch_from_scratch_amd.parallel import process_manager as pm, tp_comm
     from distributed_pytorch_from_scratch_amd.models import fused_engine_sp  # noqa: F401
     pm.pgm = SimPGM(a.tp, a.rank)
-    tp_comm.all_reduce = lambda t, async_op=True: None
-    tp_comm.reduce_scatter = lambda out, inp, async_op=True: None
-    tp_comm.all_gather = lambda out, inp, async_op=True: None
     n = a.tp
+    if a.emulate_comm > 0:
+        from distributed_pytorch_from_scratch_amd.ops import _ext
+        C = _ext.require()
+        side = torch.cuda.Stream(priority=-1)
+        stats = {"calls": 0, "us": 0.0}
+
+        class _Work:
+            def __init__(self, ev):
+                self.ev = ev
+
+            def wait(self):
+                torch.cuda.current_stream().wait_event(self.ev)
+
+        def _emulate(nbytes, per_link_factor):
+            us = per_link_factor * nbytes / n / (a.emulate_comm * 1e3)   # bytes / (GB/s) -> us
+            stats["calls"] += 1
+            stats["us"] += us
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                C.occupy(a.comm_blocks, us)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            return _Work(ev)
+
+        tp_comm.all_reduce = lambda t, async_op=True: _emulate(t.numel() * t.element_size(), 2.0)
+        tp_comm.reduce_scatter = lambda out, inp, async_op=True: _emulate(inp.numel() * inp.element_size(), 1.0)
+        tp_comm.all_gather = lambda out, inp, async_op=True: _emulate(out.numel() * out.element_size(), 1.0)
+    else:
+        stats = None
+        tp_comm.all_reduce = lambda t, async_op=True: None
+        tp_comm.reduce_scatter = lambda out, inp, async_op=True: None
+        tp_comm.all_gather = lambda out, inp, async_op=True: None
     dist.all_gather_into_tensor = lambda out, inp, group=None, async_op=False: out.view(n, -1).copy_(
         inp.reshape(1, -1).expand(n, -1))
     dist.all_reduce = lambda t, *args, **kw: None
@@ -121,9 +165,22 @@ def main():
             pr.disable()
             pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(25)
         torch.cuda.synchronize()
-        print(json.dumps({"tp": n, "rank": a.rank, "config": cfg, "ms_per_step": res[cfg],
-                          "tokens": B * T, "host_ms": host_ms,
-                          "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2)}), flush=True)
+        line = {"tp": n, "rank": a.rank, "config": cfg, "ms_per_step": res[cfg], "tokens": B * T,
+                "host_ms": host_ms, "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2)}
+        if a.mem_check:
+            from distributed_pytorch_from_scratch_amd.utils import memory as MEM
+            est = MEM.estimate(args, MEM.Layout(tp=n, sp=sp == "sp", seq=T, batch=B, chunks=int(c),
+                                                recompute="rc" in rest, tp_rank=a.rank))
+            est_b = est.peak - est.parts["xgmi_staging"]
+            meas = torch.cuda.max_memory_allocated()
+            line.update(est_gb=round(est_b / 2**30, 2), est_over_measured=round(est_b / meas, 3))
+        if stats is not None:
+            calls = stats["calls"] / max(1, a.steps + 3)
+            line.update(emulate_comm_gbps=a.emulate_comm, comm_blocks=a.comm_blocks,
+                        comm_ms_per_step_modelled=round(stats["us"] / max(1, a.steps + 3) / 1000, 2),
+                        comm_calls_per_step=round(calls, 1))
+            stats["calls"], stats["us"] = 0, 0.0
+        print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":
