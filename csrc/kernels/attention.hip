@@ -357,7 +357,9 @@ __device__ __forceinline__ bool fwd_cur_next(FwdCur& c, int n_items, int NP, int
 // >= T read as zeros) and its first two tiles, and the fetch flies under the softmax, P.V and
 // epilogue.  O / LSE go out as buffer stores (rows >= T dropped by the descriptor), so every
 // wave issues the same vector-memory operations and the counted vmcnt waits are exact.
-template <int HD, int DIAG = 0>
+// RSM: the row sum of P by one more MFMA per 16-key step (an all-ones A operand: O^T rows of
+// ones), in place of the per-element adds beside the MFMAs (A/B: impl 6).
+template <int HD, int DIAG = 0, bool RSM = false>
 __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ V, bf16* __restrict__ O,
                                                      float* __restrict__ LSE, int T, int H, int BH, long long ldq,
@@ -435,11 +437,13 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
     FwdCur n = c;
     n.t = nkv - 1;
     const bool nv = fwd_cur_next(n, n_items, NP, nqb, BH, T, causal);   // the next block, if any
-    f32x16 o[DTN];
+    f32x16 o[DTN], osum;
 #pragma unroll
     for (int d = 0; d < DTN; ++d)
 #pragma unroll
       for (int i = 0; i < 16; ++i) o[d][i] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) osum[i] = 0.f;
     float m = -INFINITY, lsum = 0.f;
     int slot = base;
     for (int t = 0; t < nkv; ++t) {
@@ -556,6 +560,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
           const float alpha = mnew == m ? 1.f : __builtin_amdgcn_exp2f(m - mnew);
           m = mnew;
           lsum *= alpha;
+          if constexpr (RSM) osum *= alpha;
 #pragma unroll
           for (int d = 0; d < DTN; ++d) o[d] *= alpha;
         }
@@ -569,10 +574,12 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
             const float e1 = __builtin_amdgcn_exp2f(fmaf(s[kh][i + 1], c2, -m));
             s[kh][i] = e0;
             s[kh][i + 1] = e1;
-            ps[(i >> 1) & 3] = vaddf(ps[(i >> 1) & 3], e0);
-            ps[((i >> 1) + 2) & 3] = vaddf(ps[((i >> 1) + 2) & 3], e1);
+            if constexpr (!RSM) {
+              ps[(i >> 1) & 3] = vaddf(ps[(i >> 1) & 3], e0);
+              ps[((i >> 1) + 2) & 3] = vaddf(ps[((i >> 1) + 2) & 3], e1);
+            }
           }
-        lsum += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+        if constexpr (!RSM) lsum += (ps[0] + ps[1]) + (ps[2] + ps[3]);
         bf16x8 pk[4];
 #pragma unroll
         for (int k4 = 0; k4 < 4; ++k4)
@@ -592,6 +599,13 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
             const bf16x8 vf = tr_join(vh[2 * (dt * 4 + k4)], vh[2 * (dt * 4 + k4) + 1]);
             o[dt] = MFMA32(vf, pk[k4], o[dt]);
           }
+        if constexpr (RSM) {
+          bf16x8 ones;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.f;
+#pragma unroll
+          for (int k4 = 0; k4 < 4; ++k4) osum = MFMA32(ones, pk[k4], osum);
+        }
         if constexpr (DIAG) d_acc[3] += stamp_dep(o[DTN - 1][15]) - d_t1;
       }
       slot = s1;
@@ -604,7 +618,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
           (void*)(O + (long long)b * T * ldo + (long long)h * HD), (short)0, (int)ospan, 0x00020000);
       const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
           (void*)(LSE + (long long)c.bh * T), (short)0, T * 4, 0x00020000);
-      const float ls = pair_sum(lsum);
+      const float ls = RSM ? osum[0] : pair_sum(lsum);   // (every osum row is the row sum)
       const float inv = 1.f / ls;
 #pragma unroll
       for (int dt = 0; dt < DTN; ++dt)
@@ -1838,6 +1852,16 @@ extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void*
                               int hd, long long ldq, long long ldk, long long ldv, long long ldo, float scale,
                               int causal, int impl_req, hipStream_t s) {
   const int impl = impl_req == 0 ? ((hd == 64 || hd == 128) ? 4 : 1) : impl_req;
+  if (impl == 6 && (hd == 64 || hd == 128)) {   // the row sum by MFMA (A/B)
+    const int nqb = (T + 127) / 128, grid = (B * H + 7) / 8 * 8 * ((nqb + 1) / 2);
+    if (hd == 64)
+      attn_fwd3_k<64, 0, true><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, T,
+                                                    H, B * H, ldq, ldk, ldv, ldo, scale, causal);
+    else
+      attn_fwd3_k<128, 0, true><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse,
+                                                     T, H, B * H, ldq, ldk, ldv, ldo, scale, causal);
+    return;
+  }
   if ((impl == 4 || (impl == 5 && g_attn_diag)) && (hd == 64 || hd == 128)) {
     // one workgroup per item (the dispatcher refills freed slots, which balances the end of
     // the kernel; a persistent grid measured slower)

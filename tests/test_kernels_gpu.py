@@ -219,11 +219,14 @@ def test_cross_entropy_kernels(C, V, valid, start):
 
 @pytest.mark.parametrize("B,T,H,hd", [(2, 256, 4, 64), (1, 300, 2, 64), (2, 130, 3, 128), (1, 64, 2, 32),
                                       (1, 1000, 2, 64), (1, 1000, 2, 128), (2, 384, 2, 128)])
-@pytest.mark.parametrize("impl", [1, 4])
+@pytest.mark.parametrize("impl", [1, 4, 6])
 def test_attention(C, B, T, H, hd, impl):
-    # per call: forward 16x16x32 register-staged / 32x32x16 LDS-DMA ring, backward pair
-    # 16x16x32 / 32x32x16 key-on-lane (hd 32 has only the first of each)
-    _check_attention(C, B, T, H, hd, impl, 4 if impl == 4 else 2)
+    # per call: forward 16x16x32 register-staged / 32x32x16 LDS-DMA ring (6: with the row sum by
+    # MFMA), backward pair 16x16x32 / 32x32x16 key-on-lane (hd 32 has only the first of each;
+    # impl 6 of the backward = the fused head_dim-64 kernel)
+    if impl == 6 and hd == 32:
+        pytest.skip("impl 6: head_dim 64 / 128")
+    _check_attention(C, B, T, H, hd, impl, {1: 2, 4: 4, 6: 6 if hd == 64 else 4}[impl])
 
 
 def _check_attention(C, B, T, H, hd, fimpl=0, bimpl=0):
@@ -248,7 +251,7 @@ def _check_attention(C, B, T, H, hd, fimpl=0, bimpl=0):
     assert _rel(dq, rq) < 3e-2 and _rel(dk, rk) < 3e-2 and _rel(dv, rv) < 3e-2
 
 
-@pytest.mark.parametrize("impl", [1, 4])
+@pytest.mark.parametrize("impl", [1, 4, 6])
 @pytest.mark.parametrize("hd", [64, 128])
 def test_attention_fwd_rescale_branch(C, impl, hd):
     """The online softmax's deferred rescale fires only when a row's max grows by > 2^8 between
