@@ -102,8 +102,8 @@ void dpfs_ce_valid_scale(const int64_t*, long long, float*, float*, float*, int,
 long long dpfs_emb_sort_ws(int);
 void dpfs_occupy(int, double, hipStream_t);
 void dpfs_attn_stagger(int);
-void dpfs_gemm_f32(int, const float*, const float*, float*, const float*, int, int, int, long long, long long,
-                   long long, int, float*, hipStream_t);
+void dpfs_gemm_f32(int, const void*, const void*, void*, const float*, int, int, int, long long, long long,
+                   long long, int, float*, int, int, hipStream_t);
 int dpfs_gemm_f32_splits(int, int, int);
 int dpfs_attn_f32_supported_hd(int);
 void dpfs_attn_fwd_f32(const float*, const float*, const float*, float*, float*, int, int, int, int, long long,
@@ -814,7 +814,9 @@ torch::Tensor gemm_f32(torch::Tensor a, torch::Tensor b, int64_t layout, c10::op
                        c10::optional<torch::Tensor> out, bool accumulate) {
   check_cuda(a, "a");
   check_cuda(b, "b");
-  TORCH_CHECK(a.scalar_type() == torch::kFloat32 && b.scalar_type() == torch::kFloat32, "gemm_f32: fp32 operands");
+  const bool in16 = a.scalar_type() == torch::kBFloat16;
+  TORCH_CHECK((a.scalar_type() == torch::kFloat32 || in16) && b.scalar_type() == a.scalar_type(),
+              "gemm_f32: fp32 or bf16 operands (both alike)");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1, "gemm_f32: row-major 2-D operands");
   TORCH_CHECK(layout >= 0 && layout <= 2, "gemm_f32: layout 0 / 1 / 2");
   const int64_t M = layout == 2 ? a.size(1) : a.size(0), K = layout == 2 ? a.size(0) : a.size(1);
@@ -824,12 +826,14 @@ torch::Tensor gemm_f32(torch::Tensor a, torch::Tensor b, int64_t layout, c10::op
   torch::Tensor c;
   if (out.has_value() && out->defined()) {
     c = *out;
-    TORCH_CHECK(c.scalar_type() == torch::kFloat32 && c.dim() == 2 && c.size(0) == M && c.size(1) == N &&
-                    c.stride(1) == 1, "gemm_f32: out fp32 [M, N] row-major");
+    TORCH_CHECK((c.scalar_type() == torch::kFloat32 || c.scalar_type() == torch::kBFloat16) && c.dim() == 2 &&
+                    c.size(0) == M && c.size(1) == N && c.stride(1) == 1, "gemm_f32: out fp32 / bf16 [M, N] row-major");
   } else {
-    c = torch::empty({M, N}, a.options());
+    // the bf16 API's output dtypes: a.dtype for NT / NN, fp32 for TN (weight gradients)
+    c = torch::empty({M, N}, a.options().dtype(layout == 2 ? torch::kFloat32 : a.scalar_type()));
     accumulate = false;
   }
+  TORCH_CHECK(in16 || c.scalar_type() == torch::kFloat32, "gemm_f32: fp32 operands give an fp32 output");
   const float* bp = nullptr;
   if (bias.has_value() && bias->defined()) {
     TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->is_contiguous() && bias->numel() == N,
@@ -844,9 +848,9 @@ torch::Tensor gemm_f32(torch::Tensor a, torch::Tensor b, int64_t layout, c10::op
       const int sp = dpfs_gemm_f32_splits((int)M, (int)N, (int)K);   // K-split slabs (weight gradients)
       torch::Tensor ws;
       if (sp > 1) ws = torch::empty({(int64_t)sp * M * N}, a.options());
-      dpfs_gemm_f32((int)layout, a.data_ptr<float>(), b.data_ptr<float>(), c.data_ptr<float>(), bp, (int)M, (int)N,
-                    (int)K, a.stride(0), b.stride(0), c.stride(0), accumulate ? 1 : 0,
-                    sp > 1 ? ws.data_ptr<float>() : nullptr, stream());
+      dpfs_gemm_f32((int)layout, a.data_ptr(), b.data_ptr(), c.data_ptr(), bp, (int)M, (int)N, (int)K, a.stride(0),
+                    b.stride(0), c.stride(0), accumulate ? 1 : 0, sp > 1 ? ws.data_ptr<float>() : nullptr,
+                    in16 ? 1 : 0, c.scalar_type() == torch::kBFloat16 ? 1 : 0, stream());
     }
   }
   return c;
@@ -1629,7 +1633,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "start, int64 (deterministic radix sort on HIP kernels)");
   m.def("gemm_f32", &gemm_f32, py::arg("a"), py::arg("b"), py::arg("layout"), py::arg("bias") = py::none(),
         py::arg("out") = py::none(), py::arg("accumulate") = false,
-        "fp32 MFMA GEMM (v_mfma_f32_32x32x2_f32, exact fp32): layout 0 = a b^T (+ bias), 1 = a b, 2 = a^T b (+=)");
+        "fp32-input MFMA GEMM (v_mfma_f32_32x32x2_f32, exact products): layout 0 = a b^T (+ bias), 1 = a b, 2 = a^T b "
+        "(+=); fp32 or bf16 operands of any alignment (bf16: the shapes the bf16 MFMA kernels decline)");
   m.def("attn_fwd_f32", &attn_fwd_f32, "fp32 causal flash attention forward: (o, lse)");
   m.def("attn_bwd_f32", &attn_bwd_f32, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("scale"), py::arg("causal"), py::arg("dq"), py::arg("dk"), py::arg("dv"),

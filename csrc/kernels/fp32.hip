@@ -28,11 +28,22 @@ namespace dpfs {
 constexpr int kF32BM = 128, kF32BK = 16, kF32LD = 128 + 4;   // LDS row: 128 floats + pad
 
 // One 128 x 16 operand tile: AKM = true when the operand is K-major in memory (x[r][k], ld
-// elements per row), false when it is MN-major (x[k][r]).  LDS image: s[k][r].
-template <bool AKM>
+// elements per row), false when it is MN-major (x[k][r]).  LDS image: s[k][r], fp32.  TI: the
+// operand's storage (fp32, or bf16 for the GEMMs whose contiguous dimension the bf16 MFMA
+// kernels cannot take: any alignment, converted to fp32 on the way in, exact products).
+template <typename TI>
+__device__ __forceinline__ f32x4 ld4(const TI* p) {
+  if constexpr (sizeof(TI) == 4) {
+    return *reinterpret_cast<const f32x4*>(p);
+  } else {
+    const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+    return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+  }
+}
+template <bool AKM, typename TI = float>
 struct F32Tile {
   f32x4 v[2];
-  __device__ __forceinline__ void load(const float* __restrict__ x, long long ld, int R, int Kd, int r0, int k0,
+  __device__ __forceinline__ void load(const TI* __restrict__ x, long long ld, int R, int Kd, int r0, int k0,
                                        bool vec) {
     const int t = threadIdx.x;
 #pragma unroll
@@ -43,10 +54,10 @@ struct F32Tile {
         const int gr = r0 + r, gk = k0 + k;
         if (gr < R) {
           if (vec && gk + 3 < Kd) {
-            q = *reinterpret_cast<const f32x4*>(x + (long long)gr * ld + gk);
+            q = ld4<TI>(x + (long long)gr * ld + gk);
           } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) q[j] = gk + j < Kd ? x[(long long)gr * ld + gk + j] : 0.f;
+            for (int j = 0; j < 4; ++j) q[j] = gk + j < Kd ? to_f(x[(long long)gr * ld + gk + j]) : 0.f;
           }
         }
       } else {
@@ -54,10 +65,10 @@ struct F32Tile {
         const int gr = r0 + r, gk = k0 + k;
         if (gk < Kd) {
           if (vec && gr + 3 < R) {
-            q = *reinterpret_cast<const f32x4*>(x + (long long)gk * ld + gr);
+            q = ld4<TI>(x + (long long)gk * ld + gr);
           } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) q[j] = gr + j < R ? x[(long long)gk * ld + gr + j] : 0.f;
+            for (int j = 0; j < 4; ++j) q[j] = gr + j < R ? to_f(x[(long long)gk * ld + gr + j]) : 0.f;
           }
         }
       }
@@ -83,9 +94,9 @@ struct F32Tile {
 // AK: A is K-major (a[m][k]); BK: B is K-major (b[n][k]).  C row-major fp32 with ldc.
 // Split-K (blockIdx.y = split s of gridDim.y): the K range [s kps, min(K, (s + 1) kps)) into the
 // fp32 slab C + s * slab (accumulate off); splitk_sum_f32_k adds the slabs in split order.
-template <bool AK, bool BK>
-__global__ __launch_bounds__(256) void gemm_f32_k(const float* __restrict__ A, const float* __restrict__ B,
-                                                  float* __restrict__ C, const float* __restrict__ bias, int M, int N,
+template <bool AK, bool BK, typename TI = float, typename TO = float>
+__global__ __launch_bounds__(256) void gemm_f32_k(const TI* __restrict__ A, const TI* __restrict__ B,
+                                                  TO* __restrict__ C, const float* __restrict__ bias, int M, int N,
                                                   int K, long long lda, long long ldb, long long ldc, int accumulate,
                                                   int vec_a, int vec_b, int kps, long long slab) {
   {
@@ -114,8 +125,8 @@ __global__ __launch_bounds__(256) void gemm_f32_k(const float* __restrict__ A, c
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  F32Tile<AK> ta;
-  F32Tile<BK> tb;
+  F32Tile<AK, TI> ta;
+  F32Tile<BK, TI> tb;
   const int nk = (K + kF32BK - 1) / kF32BK;
   ta.load(A, lda, M, K, m0, 0, vec_a);
   tb.load(B, ldb, N, K, n0, 0, vec_b);
@@ -158,9 +169,9 @@ __global__ __launch_bounds__(256) void gemm_f32_k(const float* __restrict__ A, c
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm + 32 * i + 8 * (r >> 2) + 4 * hf + (r & 3);
         if (row < M) {
-          float* p = C + (long long)row * ldc + col;
+          TO* p = C + (long long)row * ldc + col;
           const float v = acc[i][j][r] + bv;
-          *p = accumulate ? *p + v : v;
+          *p = from_f<TO>(accumulate ? to_f(*p) + v : v);
         }
       }
   }
@@ -523,7 +534,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_f32_k(
 }
 
 // C (+)= sum over the S slabs (split order: deterministic); vectorised by 4 where aligned
-__global__ __launch_bounds__(256) void splitk_sum_f32_k(const float* __restrict__ ws, float* __restrict__ C,
+template <typename TO>
+__global__ __launch_bounds__(256) void splitk_sum_f32_k(const float* __restrict__ ws, TO* __restrict__ C,
                                                         const float* __restrict__ bias, int M, int N, long long ldc,
                                                         int S, int accumulate) {
   const long long n = (long long)M * N;
@@ -532,8 +544,8 @@ __global__ __launch_bounds__(256) void splitk_sum_f32_k(const float* __restrict_
     for (int sp = 0; sp < S; ++sp) acc += ws[sp * n + i];
     const long long r = i / N, c = i % N;
     if (bias) acc += bias[c];
-    float* p = C + r * ldc + c;
-    *p = accumulate ? *p + acc : acc;
+    TO* p = C + r * ldc + c;
+    *p = from_f<TO>(accumulate ? to_f(*p) + acc : acc);
   }
 }
 
@@ -569,32 +581,50 @@ extern "C" int dpfs_gemm_f32_splits(int M, int N, int K) {
 
 // layout: 0 = NT (a[M][K], b[N][K]), 1 = NN (a[M][K], b[K][N]), 2 = TN (a[K][M], b[K][N]).
 // ws: splits * M * N floats when dpfs_gemm_f32_splits > 1 (else unused, may be null).
-extern "C" void dpfs_gemm_f32(int layout, const float* A, const float* B, float* C, const float* bias, int M, int N,
-                              int K, long long lda, long long ldb, long long ldc, int accumulate, float* ws,
-                              hipStream_t s) {
+template <typename TI, typename TO>
+static void gemm_generic(int layout, const TI* A, const TI* B, TO* C, const float* bias, int M, int N, int K,
+                         long long lda, long long ldb, long long ldc, int accumulate, float* ws, hipStream_t s) {
   if (M <= 0 || N <= 0) return;
   const int tiles = ((M + kF32BM - 1) / kF32BM) * ((N + kF32BM - 1) / kF32BM);
-  const bool va = ((uintptr_t)A % 16 == 0) && lda % 4 == 0, vb = ((uintptr_t)B % 16 == 0) && ldb % 4 == 0;
+  constexpr int VA = sizeof(TI) == 4 ? 16 : 8;   // bytes of a 4-element vector load
+  const bool va = ((uintptr_t)A % VA == 0) && lda % 4 == 0, vb = ((uintptr_t)B % VA == 0) && ldb % 4 == 0;
   const int S = ws ? dpfs_gemm_f32_splits(M, N, K) : 1;
   const int kps = S > 1 ? ((K + S - 1) / S + kF32BK - 1) / kF32BK * kF32BK : K;
   const int Sx = S > 1 ? (K + kps - 1) / kps : 1;
   dim3 grid(tiles, Sx);
-  float* out = Sx > 1 ? ws : C;
-  const long long ldo = Sx > 1 ? N : ldc;
-  const float* bo = Sx > 1 ? nullptr : bias;
-  const int acc = Sx > 1 ? 0 : accumulate;
   const long long slab = (long long)M * N;
-  if (layout == 0)
-    gemm_f32_k<true, true><<<grid, 256, 0, s>>>(A, B, out, bo, M, N, K, lda, ldb, ldo, acc, va, vb, kps, slab);
-  else if (layout == 1)
-    gemm_f32_k<true, false><<<grid, 256, 0, s>>>(A, B, out, bo, M, N, K, lda, ldb, ldo, acc, va, vb, kps, slab);
-  else
-    gemm_f32_k<false, false><<<grid, 256, 0, s>>>(A, B, out, bo, M, N, K, lda, ldb, ldo, acc, va, vb, kps, slab);
+#define GF32(AK_, BK_)                                                                                              \
+  do {                                                                                                              \
+    if (Sx > 1)                                                                                                     \
+      gemm_f32_k<AK_, BK_, TI, float><<<grid, 256, 0, s>>>(A, B, ws, nullptr, M, N, K, lda, ldb, N, 0, va, vb, kps,  \
+                                                            slab);                                                  \
+    else                                                                                                            \
+      gemm_f32_k<AK_, BK_, TI, TO><<<grid, 256, 0, s>>>(A, B, C, bias, M, N, K, lda, ldb, ldc, accumulate, va, vb,   \
+                                                         kps, slab);                                                \
+  } while (0)
+  if (layout == 0) GF32(true, true);
+  else if (layout == 1) GF32(true, false);
+  else GF32(false, false);
+#undef GF32
   if (Sx > 1) {
-    const long long n = (long long)M * N;
-    const int blocks = (int)std::min<long long>((n + 255) / 256, 4096);
-    splitk_sum_f32_k<<<blocks, 256, 0, s>>>(ws, C, bias, M, N, ldc, Sx, accumulate);
+    const int blocks = (int)std::min<long long>((slab + 255) / 256, 4096);
+    splitk_sum_f32_k<TO><<<blocks, 256, 0, s>>>(ws, C, bias, M, N, ldc, Sx, accumulate);
   }
+}
+
+// in_bf16 / out_bf16: operand / output storage (fp32 otherwise)
+extern "C" void dpfs_gemm_f32(int layout, const void* A, const void* B, void* C, const float* bias, int M, int N,
+                              int K, long long lda, long long ldb, long long ldc, int accumulate, float* ws,
+                              int in_bf16, int out_bf16, hipStream_t s) {
+  if (in_bf16 && out_bf16)
+    gemm_generic<bf16, bf16>(layout, (const bf16*)A, (const bf16*)B, (bf16*)C, bias, M, N, K, lda, ldb, ldc,
+                             accumulate, ws, s);
+  else if (in_bf16)
+    gemm_generic<bf16, float>(layout, (const bf16*)A, (const bf16*)B, (float*)C, bias, M, N, K, lda, ldb, ldc,
+                              accumulate, ws, s);
+  else
+    gemm_generic<float, float>(layout, (const float*)A, (const float*)B, (float*)C, bias, M, N, K, lda, ldb, ldc,
+                               accumulate, ws, s);
 }
 
 extern "C" int dpfs_attn_f32_supported_hd(int hd) { return hd == 32 || hd == 64 || hd == 128; }

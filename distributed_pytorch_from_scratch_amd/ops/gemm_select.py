@@ -164,9 +164,28 @@ _MIN_ROWS = 256
 
 
 def _aligned(*dims: int) -> bool:
-    """Our MFMA kernels stage 16-byte rows: every K / N (and TN's M) must be a multiple of 8.
-    Uneven vocab shards (e.g. 1000 over 2 ranks at vocab_pad_to=1) go to hipBLASLt."""
+    """Our bf16 MFMA kernels stage 16-byte rows: every K / N (and TN's M) must be a multiple of
+    8.  Other shapes (e.g. an uneven vocab shard, 1000 over 2 ranks at vocab_pad_to=1) run
+    :func:`_unaligned`."""
     return all(d % 8 == 0 for d in dims)
+
+
+def _rm(t: torch.Tensor) -> torch.Tensor:
+    return t if t.dim() == 2 and t.stride(1) == 1 else t.contiguous()
+
+
+def _unaligned(k, layout: int, a: torch.Tensor, b: torch.Tensor, bias=None, out=None, accumulate: bool = False):
+    """A GEMM whose K / N is not a multiple of 8: the fp32-input MFMA kernel (``gemm_f32``,
+    csrc/kernels/fp32.hip) reading the bf16 operands at any alignment (converted to fp32 as
+    they are staged; exact products, fp32 accumulate, fp32 bias in the epilogue, split-K for
+    the long-K weight gradients).  ``DPFS_GEMM_LIB=blas`` pins torch's library GEMM instead."""
+    if mode() == "blas":
+        return None
+    o = out if out is None or out.stride(-1) == 1 else None
+    c = k.gemm_f32(_rm(a), _rm(b), layout, bias, o, bool(accumulate and o is not None))
+    if out is not None and o is None:
+        return out.add_(c) if accumulate else out.copy_(c)
+    return c
 
 
 def _lt_operands_ok(*ts) -> bool:
@@ -197,7 +216,8 @@ def gemm_nt(k, x: torch.Tensor, w: torch.Tensor, bias=None, out=None) -> torch.T
             return torch.mm(x, w.t(), out=out)
         return torch.addmm(bb, x, w.t(), out=out)
     if not _aligned(x.shape[1], w.shape[0]):
-        return blas()
+        y = _unaligned(k, 0, x, w, bias, out)
+        return blas() if y is None else y
     M, N, K = x.shape[0], w.shape[0], x.shape[1]
     lt_ok = _lt_operands_ok(x, w, out) and _lt_bias_ok(bias)
 
@@ -296,7 +316,8 @@ def gemm_nn(k, a: torch.Tensor, b: torch.Tensor, out=None) -> torch.Tensor:
     def blas():
         return torch.matmul(a, b) if out is None else torch.matmul(a, b, out=out)
     if not _aligned(a.shape[1], b.shape[1]):
-        return blas()
+        y = _unaligned(k, 1, a, b, None, out)
+        return blas() if y is None else y
     M, N, K = a.shape[0], b.shape[1], a.shape[1]
     lt_ok = _lt_operands_ok(a, b, out)
 
@@ -331,8 +352,13 @@ def gemm_nt_rope(k, x: torch.Tensor, w: torch.Tensor, bias, pos, tab, rot_heads:
         k.rope_(y, pos, tab, rot_heads, hd, False)
         return y
     m = mode()
-    if _direct(k) or not x.is_cuda or m == "ours" or not _aligned(x.shape[1], w.shape[0]) \
-            or x.shape[0] < _MIN_ROWS:
+    if not _direct(k) and x.is_cuda and not _aligned(x.shape[1], w.shape[0]):
+        y = _unaligned(k, 0, x, w, bias)
+        if y is None:
+            y = F.linear(x, w, shadow(bias, x.dtype) if bias is not None else None)
+        k.rope_(y, pos, tab, rot_heads, hd, False)
+        return y
+    if _direct(k) or not x.is_cuda or m == "ours" or x.shape[0] < _MIN_ROWS:
         return k.gemm_nt(x, w, bias, pos, tab, rot_heads, hd)
     bb = shadow(bias, x.dtype) if bias is not None else None
     M, N, K = x.shape[0], w.shape[0], x.shape[1]
@@ -425,6 +451,9 @@ def gemm_tn(k, a: torch.Tensor, b: torch.Tensor, out=None, accumulate: bool = Fa
     if _direct(k) or not a.is_cuda:
         return k.gemm_tn(a, b, out, accumulate) if out is not None else k.gemm_tn(a, b)
     if not _aligned(a.shape[1], b.shape[1]):
+        c = _unaligned(k, 2, a, b, None, out, accumulate)
+        if c is not None:
+            return c
         c = torch.matmul(a.t(), b).float()
         if out is None:
             return c

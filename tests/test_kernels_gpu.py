@@ -447,6 +447,38 @@ def test_gemm_f32(C, layout, M, N, K):
     assert torch.equal(wide[:, :N], c) and not wide[:, N:].any()
 
 
+@pytest.mark.parametrize("layout,M,N,K", [(0, 300, 500, 777), (1, 257, 501, 999), (2, 1003, 501, 4097),
+                                          (0, 64, 1000, 768), (2, 768, 1000, 8192)])
+def test_gemm_unaligned_bf16(C, layout, M, N, K):
+    """bf16 GEMMs whose K / N is not a multiple of 8 (an uneven vocab shard): gemm_select routes
+    them to the fp32-input MFMA kernel reading bf16 at any alignment -- no torch matmul.
+    Against the fp32 product of the same bf16 values (exact products, fp32 accumulate)."""
+    from distributed_pytorch_from_scratch_amd.ops import gemm_select as G
+    torch.manual_seed(47)
+    bf = torch.bfloat16
+    if layout == 0:
+        a, b = torch.randn(M, K, device=DEV, dtype=bf), torch.randn(N, K, device=DEV, dtype=bf)
+        ref = a.double() @ b.double().t()
+        bias = torch.randn(N, device=DEV)
+        c = G.gemm_nt(C, a, b, bias)
+        ref = ref + bias.double()
+    elif layout == 1:
+        a, b = torch.randn(M, K, device=DEV, dtype=bf), torch.randn(K, N, device=DEV, dtype=bf)
+        ref = a.double() @ b.double()
+        c = G.gemm_nn(C, a, b)
+    else:
+        a, b = torch.randn(K, M, device=DEV, dtype=bf), torch.randn(K, N, device=DEV, dtype=bf)
+        ref = a.double().t() @ b.double()
+        c = G.gemm_tn(C, a, b)
+        assert c.dtype == torch.float32
+        acc = torch.randn(M, N, device=DEV)
+        want2 = acc.double() + ref
+        G.gemm_tn(C, a, b, acc, True)
+        assert (acc.double() - want2).abs().max().item() < 1e-4 * K ** 0.5
+    tol = (1e-4 if layout == 2 else 1e-2) * K ** 0.5   # bf16 output rounding for NT / NN
+    assert (c.double() - ref).abs().max().item() < tol * (1 if layout == 2 else ref.abs().max().item() / K ** 0.5)
+
+
 @pytest.mark.parametrize("B,T,H,hd,causal", [(2, 256, 2, 64, True), (1, 300, 3, 64, True), (1, 130, 2, 128, True),
                                              (2, 192, 2, 32, True), (1, 200, 2, 64, False)])
 def test_attention_f32(C, B, T, H, hd, causal):

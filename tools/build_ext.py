@@ -106,11 +106,15 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True, kernel_asser
     out = ext_path(kernel_assert)
     if force or jobs_list or not os.path.exists(out):
         tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
-        link = ["g++", "-shared", "-o", out] + objs + [
+        # link to a temporary name and rename: a tree snapshot taken during the build (a GPU
+        # run's upload) sees either the old or the new library, never a partial one
+        tmp_out = out + ".tmp"
+        link = ["g++", "-shared", "-o", tmp_out] + objs + [
             "-L" + tlib, "-Wl,-rpath," + tlib, "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python",
             "-lc10_hip", "-ltorch_hip", "-lamdhip64", "-lrccl",   # torch's own librccl.so (same instance)
             "-lhipblaslt"]                                       # and torch's own libhipblaslt.so
         _run(link)
+        os.replace(tmp_out, out)
         if verbose:
             print("[build_ext] linked", out, flush=True)
     return out
