@@ -847,7 +847,7 @@ torch::Tensor gemm_f32(torch::Tensor a, torch::Tensor b, int64_t layout, c10::op
     } else {
       const int sp = dpfs_gemm_f32_splits((int)M, (int)N, (int)K);   // K-split slabs (weight gradients)
       torch::Tensor ws;
-      if (sp > 1) ws = torch::empty({(int64_t)sp * M * N}, a.options());
+      if (sp > 1) ws = torch::empty({(int64_t)sp * M * N}, a.options().dtype(torch::kFloat32));
       dpfs_gemm_f32((int)layout, a.data_ptr(), b.data_ptr(), c.data_ptr(), bp, (int)M, (int)N, (int)K, a.stride(0),
                     b.stride(0), c.stride(0), accumulate ? 1 : 0, sp > 1 ? ws.data_ptr<float>() : nullptr,
                     in16 ? 1 : 0, c.scalar_type() == torch::kBFloat16 ? 1 : 0, stream());

@@ -1882,6 +1882,13 @@ extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void*
                                                             lse, T, H, ldq, ldk, ldv, ldo, scale, causal));
 }
 
+// attention_fused.hip (its own translation unit: asm-owned AGPR accumulators)
+extern "C" void dpfs_attn_bwd_dkdv4(int items, const void* q, const void* k, const void* v, const void* dout,
+                                    const float* lsn, const float* ndel, void* dk, void* dv, int T, int H, int BH,
+                                    long long ldq, long long ldk, long long ldv, long long lddo, long long lddk,
+                                    long long lddv, float scale, int causal, const int64_t* rope_pos,
+                                    const float* rope_tab, float* pk, float* pv, int prefetch, hipStream_t s);
+
 // delta: workspace [2][B, H, T] fp32: -delta (rowsum(dO*O)) and -lse/scale, written by the dQ kernel.
 // Backward kernel pair (`impl`): 0 = auto (4 at head_dim 64 / 128, 2 otherwise), 2 =
 // attn_bwd_dq_k + attn_bwd_dkdv2_k (16x16x32, LDS-DMA ring), 4 = attn_bwd_dq3_k +
@@ -1898,7 +1905,9 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
   // reduction kernel).
   const bool v3ok = hd == 64 || hd == 128;
   const bool diag = impl_req == 5 && g_attn_diag != nullptr;
-  const int bimpl = impl_req == 0 ? (v3ok ? 4 : 2) : (impl_req == 5 ? 4 : impl_req);
+  // 7 = attn_bwd_dq3_k + attn_bwd_dkdv4_k (64 keys per wave, head_dim 64; else 4)
+  const bool v4 = impl_req == 7 && hd == 64;
+  const int bimpl = impl_req == 0 ? (v3ok ? 4 : 2) : ((impl_req == 5 || impl_req == 7) ? 4 : impl_req);
   const bool bias = dbias != nullptr && bws != nullptr;
   const int nqb = (T + 127) / 128, nkb = (T + 63) / 64;
   float* pq = bias ? bws : nullptr;
@@ -1923,6 +1932,11 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
                                                              rope_pos, rope_tab, pq));
   if (bimpl == 4 && v3ok) {
     const int nkb3 = (T + 127) / 128, items = (B * H + 7) / 8 * 8 * ((nkb3 + 1) / 2);
+    const int nkb4 = (T + 255) / 256, items4 = (B * H + 7) / 8 * 8 * ((nkb4 + 1) / 2);
+    if (v4)
+      dpfs_attn_bwd_dkdv4(items4, q, k, v, dout, delta + (long long)B * H * T, delta, dk, dv, T, H, B * H, ldq, ldk,
+                          ldv, lddo, lddk, lddv, scale, causal, rope_pos, rope_tab, pk, pv, g_attn_prefetch & 1, s);
+    else {
 #define DKDV3_LAUNCH(HD_, DG_)                                                                                      \
   attn_bwd_dkdv3_k<HD_, DG_><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, \
                                                    delta + (long long)B * H * T, delta, (bf16*)dk, (bf16*)dv, T, H,     \
@@ -1932,6 +1946,7 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
     else if (hd == 64) DKDV3_LAUNCH(64, 0);
     else DKDV3_LAUNCH(128, 0);
 #undef DKDV3_LAUNCH
+    }
     if (bias) {
       if (hd == 64) attn_bias_grad_k<64><<<3 * H * 4, 1024, 0, s>>>(pq, pk, pv, dbias, H, B * nqb * 4, B * nkb3 * 4);
       else attn_bias_grad_k<128><<<3 * H * 8, 1024, 0, s>>>(pq, pk, pv, dbias, H, B * nqb * 4, B * nkb3 * 4);

@@ -542,6 +542,325 @@ using namespace dpfs;
 // (+ the bias-gradient reduction).  dqp: dpfs_attn_fused_ws floats of fp32 dQ partials;
 // delta: [2][B, H, T] fp32 (-delta | -lse/scale); bws: dpfs_attn_fused_bias_ws floats when
 // dbias is requested.
+// ================================= bwd: dK, dV, 64 keys per wave (one wave per SIMD) ==
+// attn_bwd_dkdv3_k with each wave owning 64 keys (two 32-key halves kh) instead of 32: every Q /
+// dO fragment read from LDS (rows for S / dP, transposed for dV^T / dK^T) feeds twice the MFMAs,
+// which halves the LDS traffic per MFMA (the v3 kernel moves as many LDS bytes per CU as its
+// MFMAs take cycles), and a workgroup's prologue (K / V to registers, the first two tiles) is
+// paid once per 256 keys.  The accumulators (dK^T / dV^T of 64 keys: 128 floats per lane) and
+// the K / V operands no longer leave room for a second wave per SIMD: a workgroup = 4 waves x 64
+// keys per CU, and the VALU softmax work of one key half overlaps the other half's MFMAs inside
+// the wave.  head_dim 64; same operands, row constants, ring and epilogue as v3.  dV^T / dK^T
+// of key half kh, d tile dt are the asm-owned AGPR blocks 2 kh + dt / 4 + 2 kh + dt
+// (attn_acc.inc), so the compiler's 256 VGPRs hold everything else.
+template <int HD>
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv4_k(
+    const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V, const bf16* __restrict__ dO,
+    const float* __restrict__ LSN, const float* __restrict__ NDEL, bf16* __restrict__ dK, bf16* __restrict__ dV,
+    int T, int H, int BH, long long ldq, long long ldk, long long ldv, long long lddo, long long lddk,
+    long long lddv, float scale, int causal, const int64_t* __restrict__ rpos, const float* __restrict__ rtab,
+    float* __restrict__ BPK, float* __restrict__ BPV, int prefetch = 1) {
+  static_assert(HD == 64, "dK/dV v4: head_dim 64");
+  constexpr int BK = 256, BQ = 64, KS = HD / 16, DTN = HD / 32, RB = HD * 2;
+  constexpr int TILE = BQ * RB, BUF = 2 * TILE + 1024, NST = 3;
+  constexpr int PWV = QdoDma3<HD>::PW + 1;
+  __shared__ __attribute__((aligned(1024))) char smem[NST * BUF + 4 * RowStage<HD>::BYTES];
+  const int nkb = (T + BK - 1) / BK;
+  const int NP = (nkb + 1) / 2;
+  const int nkb3 = (T + 127) / 128;   // the bias partials' 32-key rows (v3's layout)
+  const int it = blockIdx.x;
+  const int bh = (it >> 3) / NP * 8 + (it & 7), p = (it >> 3) % NP;
+  if (bh >= BH) return;
+  const int b = bh / H, h = bh % H;
+  const int wave = threadIdx.x >> 6, l = lane_id(), r32 = l & 31, hf = l >> 5, g16 = l >> 4, i16 = l & 15;
+  char* ep = smem + NST * BUF + wave * RowStage<HD>::BYTES;
+  const float c2 = scale * kLog2e;
+  const bf16* qbase = Q + (long long)b * T * ldq + (long long)h * HD;
+  const bf16* dobase = dO + (long long)b * T * lddo + (long long)h * HD;
+  const float* lsb = LSN + (long long)bh * T;
+  const float* dlb = NDEL + (long long)bh * T;
+  QdoDma3<HD> dma;
+  dma.init(ldq, lddo);
+  int roff[KS], toff[DTN][2];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) roff[ks] = r32 * RB + (swz_u<HD>(r32, 2 * ks + hf) << 4);
+#pragma unroll
+  for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int row = 4 * hf + (i16 >> 2) + 8 * e;
+      const int col = 32 * dt + 16 * (g16 & 1) + 4 * (i16 & 3);
+      toff[dt][e] = row * RB + (swz_u<HD>(row, col >> 3) << 4) + (col & 7) * 2;
+    }
+  const int kb1 = nkb - 1 - p;
+  const int qstart1 = causal ? ((kb1 * BK) / BQ) * BQ : 0;
+  const int nq1 = (T - qstart1 + BQ - 1) / BQ;
+  const int kw1 = kb1 * BK + 64 * wave;
+  const int nq0 = (T - (causal ? ((p * BK) / BQ) * BQ : 0) + BQ - 1) / BQ;
+  const bool pre = (prefetch & 1) && kb1 != p && nq1 > 0 && nq0 >= 2;  // (uniform)
+  bf16x8 kf[2][KS], vf[2][KS];
+  auto load_kv = [&](int kw_) {
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int kk_ = kw_ + 32 * kh + r32;
+        bf16x8 a_ = {}, c_ = {};
+        if (kk_ < T) {
+          a_ = *reinterpret_cast<const bf16x8*>(K + ((long long)b * T + kk_) * ldk + (long long)h * HD + 16 * ks + 8 * hf);
+          c_ = *reinterpret_cast<const bf16x8*>(V + ((long long)b * T + kk_) * ldv + (long long)h * HD + 16 * ks + 8 * hf);
+        }
+        kf[kh][ks] = a_;
+        vf[kh][ks] = c_;
+      }
+  };
+  int cur = 0;
+  for (int sub = 0; sub < 2; ++sub) {
+    const int kb = sub == 0 ? p : nkb - 1 - p;
+    if (sub == 1 && kb == p) break;
+    if (sub == 1) __syncthreads();
+    const int k0 = kb * BK, kw0 = k0 + 64 * wave;
+    const int qstart = causal ? (k0 / BQ) * BQ : 0;
+    const int nq = (T - qstart + BQ - 1) / BQ;
+    const bool fetched = sub == 1 && pre;
+    if (!fetched) {
+      const int c1 = cur + 1 == NST ? 0 : cur + 1;
+      if (nq > 0) dma.issue(qbase, dobase, lsb, dlb, ldq, lddo, T, qstart, smem + cur * BUF);
+      if (nq > 1) dma.issue(qbase, dobase, lsb, dlb, ldq, lddo, T, qstart + BQ, smem + c1 * BUF);
+      load_kv(kw0);
+    }
+    wait_vmcnt<0>();
+    acc32_zero<0>(); acc32_zero<1>(); acc32_zero<2>(); acc32_zero<3>();
+    acc32_zero<4>(); acc32_zero<5>(); acc32_zero<6>(); acc32_zero<7>();
+    const bool ahead = sub == 0 && pre;
+    for (int t = 0; t < nq; ++t) {
+      if (t + 1 < nq || ahead) wait_vmcnt<PWV>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      const char* lq = smem + cur * BUF;
+      const char* ldo_ = lq + TILE;
+      const float* ls = reinterpret_cast<const float*>(lq + 2 * TILE);
+      const float* ds = ls + 64;
+      int nb = cur + 2;
+      if (nb >= NST) nb -= NST;
+      cur = (cur + 1 == NST) ? 0 : cur + 1;
+      const int q0 = qstart + t * BQ;
+      if (t + 2 < nq) dma.issue(qbase, dobase, lsb, dlb, ldq, lddo, T, q0 + 2 * BQ, smem + nb * BUF);
+      else if (ahead && t + 2 - nq < nq1)
+        dma.issue(qbase, dobase, lsb, dlb, ldq, lddo, T, qstart1 + (t + 2 - nq) * BQ, smem + nb * BUF);
+      if (causal && q0 + BQ - 1 < kw0) {   // wave-uniform: every query of the tile < every key
+        if (ahead && t == nq - 1) load_kv(kw1);
+        continue;
+      }
+      // S / dP for both query halves qt and key halves kh (rows = queries, lane = key), the
+      // row constants as initial accumulators (as v3)
+      f32x16 sc[2][2], dp[2][2];
+      bf16x8 fa[KS], fb[KS];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 lv = *reinterpret_cast<const f32x4*>(ls + 8 * g + 4 * hf);
+        const f32x4 dd = *reinterpret_cast<const f32x4*>(ds + 8 * g + 4 * hf);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          sc[0][0][4 * g + j] = lv[j];
+          dp[0][0][4 * g + j] = dd[j];
+        }
+      }
+      sc[0][1] = sc[0][0];
+      dp[0][1] = dp[0][0];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        fa[ks] = *reinterpret_cast<const bf16x8*>(lq + roff[ks]);
+        fb[ks] = *reinterpret_cast<const bf16x8*>(ldo_ + roff[ks]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 ga[KS], gb[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        sc[0][0] = MFMA32(fa[ks], kf[0][ks], sc[0][0]);
+        sc[0][1] = MFMA32(fa[ks], kf[1][ks], sc[0][1]);
+        dp[0][0] = MFMA32(fb[ks], vf[0][ks], dp[0][0]);
+        dp[0][1] = MFMA32(fb[ks], vf[1][ks], dp[0][1]);
+        ga[ks] = *reinterpret_cast<const bf16x8*>(lq + roff[ks] + 32 * RB);
+        gb[ks] = *reinterpret_cast<const bf16x8*>(ldo_ + roff[ks] + 32 * RB);
+        if (ks < 2) {
+#pragma unroll
+          for (int g = 2 * ks; g < 2 * ks + 2; ++g) {
+            const f32x4 lv = *reinterpret_cast<const f32x4*>(ls + 32 + 8 * g + 4 * hf);
+            const f32x4 dd = *reinterpret_cast<const f32x4*>(ds + 32 + 8 * g + 4 * hf);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              sc[1][0][4 * g + j] = lv[j];
+              dp[1][0][4 * g + j] = dd[j];
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      sc[1][1] = sc[1][0];
+      dp[1][1] = dp[1][0];
+      // query half 1's MFMAs, half 0's exponentials under them (8 per k-step and key half)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        sc[1][0] = MFMA32(ga[ks], kf[0][ks], sc[1][0]);
+        sc[1][1] = MFMA32(ga[ks], kf[1][ks], sc[1][1]);
+        dp[1][0] = MFMA32(gb[ks], vf[0][ks], dp[1][0]);
+        dp[1][1] = MFMA32(gb[ks], vf[1][ks], dp[1][1]);
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int i = (16 / KS) * ks; i < (16 / KS) * (ks + 1); ++i)
+            sc[0][kh][i] = __builtin_amdgcn_exp2f(sc[0][kh][i] * c2);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (ahead && t == nq - 1) load_kv(kw1);
+      // dO^T fragments (A of dV^T), shared by both key halves
+      constexpr int NH = 2 * DTN * 4;
+      s16x4 th[NH];
+#pragma unroll
+      for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          th[2 * (dt * 4 + s4)] = ds_tr16_off(ldo_ + toff[dt][0], 16 * s4 * RB);
+          th[2 * (dt * 4 + s4) + 1] = ds_tr16_off(ldo_ + toff[dt][1], 16 * s4 * RB);
+        }
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[1][kh][i] = __builtin_amdgcn_exp2f(sc[1][kh][i] * c2);
+      const bool need_mask = __builtin_amdgcn_readfirstlane(
+          (int)((causal && kw0 + 63 > q0) || (q0 + BQ > T) || (kw0 + 64 > T)));
+      if (need_mask) {
+        const int uq = T - 1 - q0 - 4 * hf;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+          const int key = kw0 + 32 * kh + r32;
+          const int vk = key >= T ? 0x7fffffff : (causal ? key - q0 - 4 * hf : -0x7fffffff);
+#pragma unroll
+          for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int c = 32 * qt + 8 * (i >> 2) + (i & 3);
+              sc[qt][kh][i] = (c < vk || c > uq) ? 0.f : sc[qt][kh][i];
+            }
+        }
+      }
+      // P and dS = p (dP - delta) packed to bf16: operand pp[kh][s4] / pd[kh][s4] holds the
+      // 16-query k-step s4 = 2 qt + s1
+      bf16x8 pp[2][4], pd[2][4];
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+          for (int s1 = 0; s1 < 2; ++s1)
+#pragma unroll
+            for (int j = 0; j < 8; j += 2) {
+              const int i = 8 * s1 + j;
+              pp[kh][2 * qt + s1][j] = (bf16)sc[qt][kh][i];
+              pp[kh][2 * qt + s1][j + 1] = (bf16)sc[qt][kh][i + 1];
+              pd[kh][2 * qt + s1][j] = (bf16)vmulf(sc[qt][kh][i], dp[qt][kh][i]);
+              pd[kh][2 * qt + s1][j + 1] = (bf16)vmulf(sc[qt][kh][i + 1], dp[qt][kh][i + 1]);
+            }
+      tr_wait8(*reinterpret_cast<s16x4(*)[16]>(&th[0]));
+#pragma unroll
+      for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const bf16x8 a = tr_join(th[2 * (dt * 4 + s4)], th[2 * (dt * 4 + s4) + 1]);
+          acc32_mfma_i(dt, a, pp[0][s4]);
+          acc32_mfma_i(2 + dt, a, pp[1][s4]);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      // Q^T fragments (A of dK^T), read after the dV^T MFMAs are issued
+#pragma unroll
+      for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          th[2 * (dt * 4 + s4)] = ds_tr16_off(lq + toff[dt][0], 16 * s4 * RB);
+          th[2 * (dt * 4 + s4) + 1] = ds_tr16_off(lq + toff[dt][1], 16 * s4 * RB);
+        }
+      tr_wait8(*reinterpret_cast<s16x4(*)[16]>(&th[0]));
+#pragma unroll
+      for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const bf16x8 a = tr_join(th[2 * (dt * 4 + s4)], th[2 * (dt * 4 + s4) + 1]);
+          acc32_mfma_i(4 + dt, a, pd[0][s4]);
+          acc32_mfma_i(6 + dt, a, pd[1][s4]);
+        }
+    }
+    // epilogue per key half: dK *= scale, inverse RoPE, whole-row stores, bias partials
+    acc32_drain();
+    f32x16 dkt[2][DTN], dvt[2][DTN];
+    dvt[0][0] = acc32_read<0>(); dvt[0][1] = acc32_read<1>(); dvt[1][0] = acc32_read<2>(); dvt[1][1] = acc32_read<3>();
+    dkt[0][0] = acc32_read<4>(); dkt[0][1] = acc32_read<5>(); dkt[1][0] = acc32_read<6>(); dkt[1][1] = acc32_read<7>();
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      const int kwh = kw0 + 32 * kh, key = kwh + r32;
+#pragma unroll
+      for (int d = 0; d < DTN; ++d) dkt[kh][d] *= scale;
+      if (rpos && key < T) {
+        KASSERT(rpos[(long long)b * T + key] >= 0, "rope position at key %d", key);
+        const float* tr = rtab + rpos[(long long)b * T + key] * HD;
+#pragma unroll
+        for (int dt = 0; dt < DTN / 2; ++dt)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 cs = *reinterpret_cast<const f32x4*>(tr + 32 * dt + 8 * g + 4 * hf);
+            const f32x4 sn = *reinterpret_cast<const f32x4*>(tr + HD / 2 + 32 * dt + 8 * g + 4 * hf);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float x1 = dkt[kh][dt][4 * g + j], x2 = dkt[kh][dt + DTN / 2][4 * g + j];
+              dkt[kh][dt][4 * g + j] = x1 * cs[j] + x2 * sn[j];
+              dkt[kh][dt + DTN / 2][4 * g + j] = x2 * cs[j] - x1 * sn[j];
+            }
+          }
+      }
+      {
+        u32x4 rk[RowStage<HD>::NI], rv[RowStage<HD>::NI];
+        RowStage<HD>::put(ep, dkt[kh]);
+        RowStage<HD>::get(ep, rk);
+        RowStage<HD>::put(ep, dvt[kh]);
+        RowStage<HD>::get(ep, rv);
+        RowStage<HD>::put_rows(rk, dK + (long long)b * T * lddk + (long long)h * HD, lddk, kwh, T);
+        RowStage<HD>::put_rows(rv, dV + (long long)b * T * lddv + (long long)h * HD, lddv, kwh, T);
+      }
+      const int u = kwh >> 5;   // the 32-key row of the bias partials (v3 layout)
+      if (BPK && u < 4 * nkb3) {
+        const long long row = (((long long)h * (BH / H) + b) * nkb3 + (u >> 2)) * 4 + (u & 3);
+#pragma unroll
+        for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            float a = key < T ? dkt[kh][dt][i] : 0.f, c = key < T ? dvt[kh][dt][i] : 0.f;
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) {
+              a += __shfl_xor(a, o, 64);
+              c += __shfl_xor(c, o, 64);
+            }
+            if (r32 == 0) {
+              const int d = 32 * dt + 8 * (i >> 2) + 4 * hf + (i & 3);
+              BPK[row * HD + d] = a;
+              BPV[row * HD + d] = c;
+            }
+          }
+      }
+    }
+  }
+}
+
+
+extern "C" void dpfs_attn_bwd_dkdv4(int items, const void* q, const void* k, const void* v, const void* dout,
+                                    const float* lsn, const float* ndel, void* dk, void* dv, int T, int H, int BH,
+                                    long long ldq, long long ldk, long long ldv, long long lddo, long long lddk,
+                                    long long lddv, float scale, int causal, const int64_t* rope_pos,
+                                    const float* rope_tab, float* pk, float* pv, int prefetch, hipStream_t s) {
+  attn_bwd_dkdv4_k<64><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lsn,
+                                              ndel, (bf16*)dk, (bf16*)dv, T, H, BH, ldq, ldk, ldv, lddo, lddk, lddv,
+                                              scale, causal, rope_pos, rope_tab, pk, pv, prefetch);
+}
+
 extern "C" long long dpfs_attn_fused_ws(int B, int T, int H, int hd) {
   if (hd != 64) return -1;
   const long long nkb = (T + 255) / 256, nqt = (T + 63) / 64;

@@ -47,3 +47,43 @@ def test_fp32_gpu_tp_transparent(world, sp):
     res = run_distributed(_train_gpu, world, CFG, 3, sp, timeout=240)
     for r in range(world):
         assert torch.allclose(torch.tensor(res[r]), torch.tensor(van), atol=2e-5), (res[r], van)
+
+
+def _train_gpu_bf16_no_lib(rank, world, cfg, steps):
+    """bf16 compute with every torch GEMM entry point poisoned: an uneven vocab shard (501 / 500
+    rows at TP 2) must run on our kernels (gemm_select -> the any-alignment gemm_f32 path)."""
+    import torch.nn.functional as F
+    torch.cuda.set_device(0)
+    from distributed_pytorch_from_scratch_amd.models import Transformer, ModelArgs
+    from distributed_pytorch_from_scratch_amd.utils.dist import set_seed
+    m = Transformer.from_args(ModelArgs(**cfg, vocab_pad_to=1))
+    set_seed(0)
+    m.reset_parameters()
+    m = m.cuda().set_compute_dtype(torch.bfloat16)
+
+    def poisoned(*a, **k):
+        raise AssertionError("torch GEMM reached in the bf16 step")
+    saved = (F.linear, torch.mm, torch.matmul, torch.addmm)
+    F.linear = torch.mm = torch.matmul = torch.addmm = poisoned
+    try:
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+        losses = []
+        for s in range(steps):
+            ids, pos, tgt = (t.cuda() for t in _batch(cfg["vocab_size"], 2, 16, seed=100 + s))
+            loss = m.loss(ids, pos, tgt)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            losses.append(loss.item())
+    finally:
+        F.linear, torch.mm, torch.matmul, torch.addmm = saved
+    return losses
+
+
+def test_bf16_uneven_vocab_native_gemms():
+    cfg = dict(attn_dim=128, ffn_dim=256, num_heads=2, num_layers=2, vocab_size=1001, maxlen=64)
+    van, _ = _train_vanilla(cfg, 3)
+    res = run_distributed(_train_gpu_bf16_no_lib, 2, cfg, 3, timeout=240)
+    for r in range(2):
+        assert all(x == x and abs(x) < 20 for x in res[r]), res[r]
+        assert torch.allclose(torch.tensor(res[r]), torch.tensor(van), atol=5e-2), (res[r], van)   # bf16

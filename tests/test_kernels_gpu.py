@@ -1324,3 +1324,38 @@ def test_gemm_nn_swiglu_bwd_epilogue(C, M, F_, K, perm):
         assert torch.equal(db1, db)
     finally:
         C.gemm4_swb_depth(2)
+
+
+@pytest.mark.parametrize("B,T,H,causal", [(2, 1024, 3, True), (1, 1000, 2, True), (3, 777, 1, True),
+                                           (1, 192, 2, True), (1, 64, 1, True), (2, 2048, 1, True),
+                                           (1, 1100, 1, True), (2, 256, 2, False), (1, 300, 2, False)])
+def test_attention_bwd_dkdv4(C, B, T, H, causal):
+    """impl 7: the dQ kernel + the 64-keys-per-wave dK/dV kernel (one wave per SIMD, asm-owned
+    AGPR accumulators).  Same products in the same order as impl 4: bit-identical to it, incl.
+    the inverse RoPE and the QKV bias gradient (32-key partial rows); ragged T (partial 256-key
+    blocks, bias rows past the last key), non-causal, strided views; and the fp32 oracle."""
+    torch.manual_seed(48)
+    hd = 64
+    qkv = torch.randn(B * T, 3 * H * hd, device=DEV).bfloat16()
+    q, k, v = (qkv[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+    o, lse = C.attn_fwd(q, k, v, 0.125, causal)
+    do = torch.randn_like(o)
+    pos = torch.randint(0, 4096, (B * T,), device=DEV)
+    tab = R.rope_table(4096, hd, 10000.0).to(DEV)
+    outs = []
+    for impl in (7, 4):
+        for rope in (False, True):
+            d = torch.full_like(qkv, float("nan"))
+            dq, dk, dv = (d[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+            db = torch.full((3 * H * hd,), float("nan"), device=DEV)
+            C.attn_bwd(do, q, k, v, o, lse, 0.125, causal, dq, dk, dv, pos if rope else None, tab if rope else None,
+                       dbias=db, impl=impl)
+            outs.append((d, db))
+    for i in range(2):
+        assert torch.equal(outs[i][0], outs[2 + i][0]) and torch.equal(outs[i][1], outs[2 + i][1])
+    d = outs[0][0]
+    assert torch.isfinite(d.float()).all()
+    rq, rk, rv = (torch.empty(B, T, H, hd, device=DEV) for _ in range(3))
+    R.attn_bwd(do.float(), q.float(), k.float(), v.float(), o.float(), lse, 0.125, causal, rq, rk, rv)
+    dq, dk, dv = (d[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
+    assert _rel(dq, rq) < 3e-2 and _rel(dk, rk) < 3e-2 and _rel(dv, rv) < 3e-2

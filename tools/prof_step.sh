@@ -11,5 +11,6 @@ for kv in "$@"; do export "$kv"; done
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/p_$tag -o run -- python3 $R/bench.py --steps 10 --warmup 5 ${BENCH_ARGS:-} > $R/gpurun_out/p_$tag.log 2>&1 || exit $?
 python3 $R/tools/prof_summary.py $R/gpurun_out/p_$tag/run_results.db --after adam_k --skip 5 --steps 10 --top 60 \
     ${DPFS_PROF_SEQ:+--sequence "$DPFS_PROF_SEQ"} > $R/gpurun_out/sum_$tag.txt 2>&1
+python3 $R/tools/gap_analysis.py $R/gpurun_out/p_$tag/run_results.db --last-ms 150 --top 12 >> $R/gpurun_out/sum_$tag.txt 2>&1
 rm -rf $R/gpurun_out/p_$tag
 head -30 $R/gpurun_out/sum_$tag.txt
