@@ -68,6 +68,9 @@ def parse():
                          "exits with the headline and tp_pure = {error: timeout}")
     ap.add_argument("--pg-timeout-s", type=float, default=240.0,
                     help="process-group (RCCL watchdog) timeout, well under the driver's lease")
+    ap.add_argument("--graph", choices=["on", "off"], default=os.environ.get("DPFS_GRAPH", "off"),
+                    help="one rank: replay the forward + backward from a HIP graph captured after the "
+                         "warmup (engine.GraphTrainStep; the same kernels, launched by the graph)")
     ap.add_argument("--fp32", action="store_true",
                     help="fp32 compute (the reference's default without --bf16): the fp32-input MFMA kernel set "
                          "(ops/fp32_native.py); with --impl reference, eager fp32 without autocast. NOT the headline")
@@ -228,6 +231,18 @@ def measure(a, tp: int, world: int, dev, first: bool):
     for _ in range(a.warmup - i):
         loss = run(i)
         i += 1
+    graphed = False
+    if a.impl == "ours" and world == 1 and dev.type == "cuda" and a.graph == "on":
+        # forward + backward replayed from one HIP graph (engine.GraphTrainStep); captured here,
+        # in one more untimed warmup step
+        from distributed_pytorch_from_scratch_amd.engine import GraphTrainStep
+        gstep = GraphTrainStep(step)
+
+        def run(i):
+            ids, tgt = pool[i % n_pool]
+            return gstep(ids, pos, tgt)
+        loss = run(i)
+        graphed = True
     sp_used = bool(a.impl == "ours" and model.args.sequence_parallel)
     sync()
     dist.barrier()
@@ -255,7 +270,8 @@ def measure(a, tp: int, world: int, dev, first: bool):
                                                                       "chunks": int(k[1]), "recompute": bool(rc)})).gb()
                                   for k in (trial or [None])) if trial else est.gb(), 2),
         peak_mem_gb=round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2) if dev.type == "cuda" else None,
-        trial={f"{'sp' if k[0] else 'nosp'}/c{k[1]}": round(1000 * v, 2) for k, v in trial.items()} or None)
+        trial={f"{'sp' if k[0] else 'nosp'}/c{k[1]}": round(1000 * v, 2) for k, v in trial.items()} or None,
+        graph=graphed)
     del model, opt, pool
     if a.impl == "ours":
         del step
@@ -420,6 +436,7 @@ def report(a, head, layouts, world, dev):
             "tp_comm": head["tp_comm"],
             "chunks": head["chunks"],
             "engine_trial_ms": head["trial"],
+            "hip_graph": head["graph"],
         },
         "tflops_per_gpu": round(value * mflops / world / 1e12, 2),
         "mfu_vs_2.5pf_dense_bf16": round(value * mflops / world / 2.5e15, 4),

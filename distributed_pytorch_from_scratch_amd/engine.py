@@ -108,3 +108,61 @@ class TrainStep:
         e0, e1, e2, e3 = self._ev
         e3.synchronize()
         return {"fwd_ms": e0.elapsed_time(e1), "bwd_ms": e1.elapsed_time(e2), "opt_ms": e2.elapsed_time(e3)}
+
+
+class GraphTrainStep:
+    """A :class:`TrainStep` whose forward + backward replay from one HIP graph.
+
+    The step is ~300 kernel launches (GEMMs with fused epilogues, attention, norms, CE,
+    embedding sort on a side stream); eagerly the host issues them one by one, and wherever the
+    host falls behind the GPU idles between kernels.  After the eager warmup steps (per-shape
+    GEMM selection, workspaces, the Adam descriptor table) the first call captures the forward
+    and backward into a graph (``torch.cuda.graph``: the activations live in the graph's private
+    pool at fixed addresses, the gradients stay where the eager steps put them); every call then
+    copies the batch into the captured input buffers, replays the graph and runs the fused Adam
+    (one kernel, eagerly: its learning rate / bias corrections change per step).
+
+    Single-process steps only (no DP / TP group: their collectives and bucket hooks stay eager).
+    The work per step is identical to :class:`TrainStep`'s -- only the launch path changes.
+    """
+
+    def __init__(self, step: TrainStep):
+        p = pm.pgm
+        assert p is None or (p.dp_size == 1 and p.tp_size == 1), "GraphTrainStep: single-rank steps only"
+        self.step = step
+        self.graph = None
+        self.loss = None
+        self.steps = 0
+
+    def _capture(self, input_ids, position_ids, target_ids):
+        st = self.step
+        self.ids, self.pos, self.tgt = input_ids.clone(), position_ids.clone(), target_ids.clone()
+        self.unit = torch.ones((), device=input_ids.device, dtype=torch.float32)
+        torch.cuda.synchronize()
+        # no .grad before the capture: the engine's backward assigns its gradient-arena views as
+        # the parameters' .grad (a host-side assignment that outlives the capture) and writes,
+        # rather than accumulates, them -- every replay refreshes the same tensors in place
+        st.optimizer.zero_grad(set_to_none=True)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            loss = st.model.loss(self.ids, self.pos, self.tgt, unit_grad=True)
+            loss.backward(self.unit.to(loss.dtype).expand_as(loss))
+        torch.cuda.synchronize()
+        self.graph, self.loss = g, loss.detach()
+
+    def __call__(self, input_ids: torch.Tensor, position_ids: torch.Tensor,
+                 target_ids: torch.Tensor) -> torch.Tensor:
+        st = self.step
+        if self.graph is None:
+            self._capture(input_ids, position_ids, target_ids)
+        if input_ids.data_ptr() != self.ids.data_ptr():
+            self.ids.copy_(input_ids, non_blocking=True)
+            self.tgt.copy_(target_ids, non_blocking=True)
+            if position_ids.data_ptr() != self.pos.data_ptr():
+                self.pos.copy_(position_ids, non_blocking=True)
+        self.graph.replay()
+        st.optimizer.step()
+        if st.scheduler is not None:
+            st.scheduler.step()
+        self.steps += 1
+        return self.loss
