@@ -359,7 +359,11 @@ __device__ __forceinline__ bool fwd_cur_next(FwdCur& c, int n_items, int NP, int
 // wave issues the same vector-memory operations and the counted vmcnt waits are exact.
 // RSM: the row sum of P by one more MFMA per 16-key step (an all-ones A operand: O^T rows of
 // ones), in place of the per-element adds beside the MFMAs (A/B: impl 6).
-template <int HD, int DIAG = 0, bool RSM = false>
+// MF: the softmax scale and the running max folded into the MFMAs (impl 8): Q is scaled by
+// scale * log2(e) once per block in registers, and one more 32x32x16 MFMA per key half adds
+// -m (a B column [-m, 0, ...] against an A column of ones) to the score accumulator, so
+// p = exp2(s) needs no per-element fma; m is kept bf16-exact (it is only a shift).
+template <int HD, int DIAG = 0, bool RSM = false, bool MF = false>
 __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ V, bf16* __restrict__ O,
                                                      float* __restrict__ LSE, int T, int H, int BH, long long ldq,
@@ -444,7 +448,13 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
       for (int i = 0; i < 16; ++i) o[d][i] = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) osum[i] = 0.f;
-    float m = -INFINITY, lsum = 0.f;
+    float m = MF ? 0.f : -INFINITY, lsum = 0.f;
+    // MF: the extra k-step's operands (A: lanes 0-31 hold k = 0 of a key row = 1; B: lanes 0-31
+    // hold k = 0 of a query column = -m)
+    bf16x8 kx = {}, qx = {};
+    if constexpr (MF) {
+      if (hf == 0) kx[0] = (bf16)1.f;
+    }
     int slot = base;
     for (int t = 0; t < nkv; ++t) {
       // tile t landed; what was issued after its DMA may still fly: the next tile (PW) and,
@@ -467,6 +477,18 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
       const char* lv = lk + TILE;
       const int s1 = slot + 1 == NST ? 0 : slot + 1, s2 = s1 + 1 == NST ? 0 : s1 + 1;
       if (t + 2 < nkv) dma.issue(kb, vb, ldk, ldv, T, (t + 2) * BKV, smem + s2 * STAGE);
+      if constexpr (MF) {
+        if (t == 0) {
+          // this block's Q landed (the wait above): Q' = bf16(Q scale log2 e).  (The empty asm
+          // orders the reads of the asm-loaded registers after the wait.)
+          asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]));
+          if constexpr (KS > 4) asm volatile("" : "+v"(qf[KS - 4]), "+v"(qf[KS - 3]), "+v"(qf[KS - 2]), "+v"(qf[KS - 1]));
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qf[ks][j] = (bf16)((float)qf[ks][j] * c2);
+        }
+      }
       const int kv0 = t * BKV;
       const bool last = t + 1 == nkv;
       const bool active = !causal || kv0 <= wq0 + 31;   // wave-uniform
@@ -482,6 +504,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int i = 0; i < 16; ++i) s[0][i] = 0.f;
+          if constexpr (MF) s[0] = MFMA32(kx, qx, s[0]);
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks) {
             s[0] = MFMA32(ka[ks], qf[ks], s[0]);
@@ -490,6 +513,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
           }
 #pragma unroll
           for (int i = 0; i < 16; ++i) s[1][i] = 0.f;
+          if constexpr (MF) s[1] = MFMA32(kx, qx, s[1]);
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks) s[1] = MFMA32(kb[ks], qf[ks], s[1]);
         } else {
@@ -497,6 +521,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
           for (int kh = 0; kh < 2; ++kh) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) s[kh][i] = 0.f;
+            if constexpr (MF) s[kh] = MFMA32(kx, qx, s[kh]);
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
               const bf16x8 kf = *reinterpret_cast<const bf16x8*>(lk + koff[kh][ks]);
@@ -554,7 +579,25 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
         // every visited tile has a valid key for every query row (kv0 <= wq0), so m is finite
         // after the first tile
         constexpr float kDefer = 8.f;
-        if (__builtin_amdgcn_ballot_w64(mx * c2 > m + kDefer) != 0) {
+        if constexpr (MF) {
+          // s = S' - m already; the first tile sets m (the plain form's -inf start), later ones
+          // move it only past the defer threshold.  m stays bf16-exact (the B column's -m).
+          if (t == 0 || __builtin_amdgcn_ballot_w64(mx > kDefer) != 0) {
+            const float mr = pair_max(mx);
+            const float mnew = (t == 0 || mr > kDefer) ? (float)(bf16)(m + mr) : m;
+            const float d = mnew - m;
+            if (t > 0) {
+              const float alpha = __builtin_amdgcn_exp2f(-d);
+              lsum *= alpha;
+#pragma unroll
+              for (int dd = 0; dd < DTN; ++dd) o[dd] *= alpha;
+            }
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh) s[kh] -= d;
+            m = mnew;
+            if (hf == 0) qx[0] = (bf16)(-m);
+          }
+        } else if (__builtin_amdgcn_ballot_w64(mx * c2 > m + kDefer) != 0) {
           const float mr = pair_max(mx) * c2;   // both lanes of a row decide together
           const float mnew = mr > m + kDefer ? mr : m;
           const float alpha = mnew == m ? 1.f : __builtin_amdgcn_exp2f(m - mnew);
@@ -570,8 +613,8 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_fwd3_k(const bf16
         for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
           for (int i = 0; i < 16; i += 2) {
-            const float e0 = __builtin_amdgcn_exp2f(fmaf(s[kh][i], c2, -m));
-            const float e1 = __builtin_amdgcn_exp2f(fmaf(s[kh][i + 1], c2, -m));
+            const float e0 = __builtin_amdgcn_exp2f(MF ? s[kh][i] : fmaf(s[kh][i], c2, -m));
+            const float e1 = __builtin_amdgcn_exp2f(MF ? s[kh][i + 1] : fmaf(s[kh][i + 1], c2, -m));
             s[kh][i] = e0;
             s[kh][i + 1] = e1;
             if constexpr (!RSM) {
@@ -981,7 +1024,10 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv2_k(
 // exp half / second exp half + mask + dS + packs / dO^T reads + dV^T / Q^T reads + dK^T /
 // epilogues / prologues (K, V to registers) / tiles computed / start / end (timing build only:
 // each stamp waits for the value it depends on).
-template <int HD, int DIAG = 0>
+// KSC: K scaled by scale log2(e) once per key block in registers and LSN = -lse log2(e) (the
+// dQ kernel's KSC convention), so p = exp2(S') with no per-element multiply (impl 9, A/B:
+// -1.5 % per call, nothing measurable per step, K rounded once more; impl 4 = the unscaled form).
+template <int HD, int DIAG = 0, bool KSC = false>
 __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
     const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V, const bf16* __restrict__ dO,
     const float* __restrict__ LSN, const float* __restrict__ NDEL, bf16* __restrict__ dK, bf16* __restrict__ dV,
@@ -1076,6 +1122,12 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
       load_kv(key);
     }
     wait_vmcnt<0>();
+    if constexpr (KSC) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) kf[ks][j] = (bf16)((float)kf[ks][j] * c2);
+    }
     if constexpr (DIAG) d_acc[6] += stamp_dep(__builtin_bit_cast(float, __builtin_bit_cast(u32x4, vf[KS - 1])[3])) - d_t0;
     f32x16 dkt[DTN], dvt[DTN];
 #pragma unroll
@@ -1168,7 +1220,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
         dp[1] = MFMA32(gb[ks], vf[ks], dp[1]);
 #pragma unroll
         for (int i = (16 / KS) * ks; i < (16 / KS) * (ks + 1); ++i)
-          sc[0][i] = __builtin_amdgcn_exp2f(sc[0][i] * c2);
+          sc[0][i] = __builtin_amdgcn_exp2f(KSC ? sc[0][i] : sc[0][i] * c2);
         __builtin_amdgcn_sched_barrier(0);
       }
       // the block's last tile: K / V are consumed, load the next block's
@@ -1189,7 +1241,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
       // dS = p (dP - delta)
       bf16x8 pp[4];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) sc[1][i] = __builtin_amdgcn_exp2f(sc[1][i] * c2);
+      for (int i = 0; i < 16; ++i) sc[1][i] = __builtin_amdgcn_exp2f(KSC ? sc[1][i] : sc[1][i] * c2);
       const bool need_mask = __builtin_amdgcn_readfirstlane(
           (int)((causal && kw0 + 31 > q0) || (q0 + BQ > T) || (kw0 + 32 > T)));
       if (need_mask) {
@@ -1573,7 +1625,7 @@ struct KvDmaU {   // K / V tile rows [kv0, kv0 + 64) into a stage (K at 0, V at 
   }
 };
 
-template <int HD>
+template <int HD, bool KSC = false>
 __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
     const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V, const bf16* __restrict__ dO,
     const bf16* __restrict__ Og, const float* __restrict__ LSE, float* __restrict__ NDEL_OUT,
@@ -1671,7 +1723,8 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
     const float lc = qi < T ? -lse_r * kLog2e : 0.f;   // p = exp2(c2 S + lc)
     const float ndel = -pair_sum(dsum);                                      // dP' = dP - delta
     if (hf == 0 && qi < T) {
-      LSN_OUT[(long long)bh * T + qi] = -lse_r / scale;   // dK/dV: S' = S - lse / scale
+      // dK/dV: S' = S - lse / scale (KSC: S' = S scale log2 e - lse log2 e, K pre-scaled)
+      LSN_OUT[(long long)bh * T + qi] = KSC ? -lse_r * kLog2e : -lse_r / scale;
       NDEL_OUT[(long long)bh * T + qi] = ndel;
     }
     f32x16 dq[DTN];
@@ -1852,6 +1905,16 @@ extern "C" void dpfs_attn_fwd(const void* q, const void* k, const void* v, void*
                               int hd, long long ldq, long long ldk, long long ldv, long long ldo, float scale,
                               int causal, int impl_req, hipStream_t s) {
   const int impl = impl_req == 0 ? ((hd == 64 || hd == 128) ? 4 : 1) : impl_req;
+  if (impl == 8 && (hd == 64 || hd == 128)) {   // scale and max folded into the MFMAs (A/B)
+    const int nqb = (T + 127) / 128, grid = (B * H + 7) / 8 * 8 * ((nqb + 1) / 2);
+    if (hd == 64)
+      attn_fwd3_k<64, 0, false, true><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o,
+                                                           lse, T, H, B * H, ldq, ldk, ldv, ldo, scale, causal);
+    else
+      attn_fwd3_k<128, 0, false, true><<<grid, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o,
+                                                            lse, T, H, B * H, ldq, ldk, ldv, ldo, scale, causal);
+    return;
+  }
   if (impl == 6 && (hd == 64 || hd == 128)) {   // the row sum by MFMA (A/B)
     const int nqb = (T + 127) / 128, grid = (B * H + 7) / 8 * 8 * ((nqb + 1) / 2);
     if (hd == 64)
@@ -1907,7 +1970,9 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
   const bool diag = impl_req == 5 && g_attn_diag != nullptr;
   // 7 = attn_bwd_dq3_k + attn_bwd_dkdv4_k (64 keys per wave, head_dim 64; else 4)
   const bool v4 = impl_req == 7 && hd == 64;
-  const int bimpl = impl_req == 0 ? (v3ok ? 4 : 2) : ((impl_req == 5 || impl_req == 7) ? 4 : impl_req);
+  // 9 = impl 4 with the K pre-scale (KSC, A/B; the 64-keys-per-wave dK/dV of impl 7 uses it too)
+  const bool ksc = impl_req == 9 || impl_req == 7;
+  const int bimpl = impl_req == 0 ? (v3ok ? 4 : 2) : ((impl_req == 5 || impl_req == 7 || impl_req == 9) ? 4 : impl_req);
   const bool bias = dbias != nullptr && bws != nullptr;
   const int nqb = (T + 127) / 128, nkb = (T + 63) / 64;
   float* pq = bias ? bws : nullptr;
@@ -1917,10 +1982,14 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
   if (bimpl == 4 && v3ok) {   // (attn_bwd_dkdv3_k reads the -lse / scale this kernel writes)
     const int items = (B * H + 7) / 8 * 8 * ((nqb + 1) / 2);
 #define DQ3_LAUNCH(HD_)                                                                                             \
-  attn_bwd_dq3_k<HD_><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,   \
+  do { if (ksc) attn_bwd_dq3_k<HD_, true><<<items, 256, 0, s>>>(                                                         \
+      (const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, (const bf16*)o, lse, delta,                \
+      delta + (long long)B * H * T, (bf16*)dq, T, H, B * H, ldq, ldk, ldv, lddo, ldo, lddq, scale, causal, rope_pos,  \
+      rope_tab, pq, ((g_attn_prefetch >> 1) & 1) | (g_attn_stagger << 4));                                           \
+  else attn_bwd_dq3_k<HD_, false><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout,   \
                                             (const bf16*)o, lse, delta, delta + (long long)B * H * T, (bf16*)dq, T, \
                                             H, B * H, ldq, ldk, ldv, lddo, ldo, lddq, scale, causal, rope_pos,     \
-                                            rope_tab, pq, ((g_attn_prefetch >> 1) & 1) | (g_attn_stagger << 4))
+                                            rope_tab, pq, ((g_attn_prefetch >> 1) & 1) | (g_attn_stagger << 4)); } while (0)
     if (hd == 64) DQ3_LAUNCH(64);
     else DQ3_LAUNCH(128);
 #undef DQ3_LAUNCH
@@ -1938,10 +2007,14 @@ extern "C" int dpfs_attn_bwd(const void* dout, const void* q, const void* k, con
                           ldv, lddo, lddk, lddv, scale, causal, rope_pos, rope_tab, pk, pv, g_attn_prefetch & 1, s);
     else {
 #define DKDV3_LAUNCH(HD_, DG_)                                                                                      \
-  attn_bwd_dkdv3_k<HD_, DG_><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, \
+  do { if (ksc) attn_bwd_dkdv3_k<HD_, DG_, true><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,       \
+      (const bf16*)dout, delta + (long long)B * H * T, delta, (bf16*)dk, (bf16*)dv, T, H, B * H, ldq, ldk, ldv, lddo,  \
+      lddk, lddv, scale, causal, rope_pos, rope_tab, pk, pv, DG_ ? g_attn_diag : nullptr,                              \
+      (g_attn_prefetch & 1) | (g_attn_stagger << 4));                                                                  \
+  else attn_bwd_dkdv3_k<HD_, DG_, false><<<items, 256, 0, s>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, \
                                                    delta + (long long)B * H * T, delta, (bf16*)dk, (bf16*)dv, T, H,     \
                                                    B * H, ldq, ldk, ldv, lddo, lddk, lddv, scale, causal, rope_pos,     \
-                                                   rope_tab, pk, pv, DG_ ? g_attn_diag : nullptr, (g_attn_prefetch & 1) | (g_attn_stagger << 4))
+                                                   rope_tab, pk, pv, DG_ ? g_attn_diag : nullptr, (g_attn_prefetch & 1) | (g_attn_stagger << 4)); } while (0)
     if (hd == 64 && diag) DKDV3_LAUNCH(64, 1);
     else if (hd == 64) DKDV3_LAUNCH(64, 0);
     else DKDV3_LAUNCH(128, 0);

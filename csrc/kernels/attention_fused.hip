@@ -630,6 +630,13 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv4_k(
       load_kv(kw0);
     }
     wait_vmcnt<0>();
+    // K pre-scaled by scale log2(e) (the dQ kernel's LSN = -lse log2(e) convention, as v3's KSC)
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) kf[kh][ks][j] = (bf16)((float)kf[kh][ks][j] * c2);
     acc32_zero<0>(); acc32_zero<1>(); acc32_zero<2>(); acc32_zero<3>();
     acc32_zero<4>(); acc32_zero<5>(); acc32_zero<6>(); acc32_zero<7>();
     const bool ahead = sub == 0 && pre;
@@ -710,7 +717,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv4_k(
         for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
           for (int i = (16 / KS) * ks; i < (16 / KS) * (ks + 1); ++i)
-            sc[0][kh][i] = __builtin_amdgcn_exp2f(sc[0][kh][i] * c2);
+            sc[0][kh][i] = __builtin_amdgcn_exp2f(sc[0][kh][i]);
         __builtin_amdgcn_sched_barrier(0);
       }
       if (ahead && t == nq - 1) load_kv(kw1);
@@ -727,7 +734,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv4_k(
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sc[1][kh][i] = __builtin_amdgcn_exp2f(sc[1][kh][i] * c2);
+        for (int i = 0; i < 16; ++i) sc[1][kh][i] = __builtin_amdgcn_exp2f(sc[1][kh][i]);
       const bool need_mask = __builtin_amdgcn_readfirstlane(
           (int)((causal && kw0 + 63 > q0) || (q0 + BQ > T) || (kw0 + 64 > T)));
       if (need_mask) {

@@ -219,14 +219,16 @@ def test_cross_entropy_kernels(C, V, valid, start):
 
 @pytest.mark.parametrize("B,T,H,hd", [(2, 256, 4, 64), (1, 300, 2, 64), (2, 130, 3, 128), (1, 64, 2, 32),
                                       (1, 1000, 2, 64), (1, 1000, 2, 128), (2, 384, 2, 128)])
-@pytest.mark.parametrize("impl", [1, 4, 6])
+@pytest.mark.parametrize("impl", [1, 4, 6, 8, 9])
 def test_attention(C, B, T, H, hd, impl):
     # per call: forward 16x16x32 register-staged / 32x32x16 LDS-DMA ring (6: with the row sum by
     # MFMA), backward pair 16x16x32 / 32x32x16 key-on-lane (hd 32 has only the first of each;
     # impl 6 of the backward = the fused head_dim-64 kernel)
-    if impl == 6 and hd == 32:
-        pytest.skip("impl 6: head_dim 64 / 128")
-    _check_attention(C, B, T, H, hd, impl, {1: 2, 4: 4, 6: 6 if hd == 64 else 4}[impl])
+    # (impl 8: the forward with the scale and running max folded into its MFMAs)
+    # (impl 9 of the backward: the v3 pair with K pre-scaled by scale log2 e)
+    if impl in (6, 8, 9) and hd == 32:
+        pytest.skip("impl 6 / 8 / 9: head_dim 64 / 128")
+    _check_attention(C, B, T, H, hd, 4 if impl == 9 else impl, {1: 2, 4: 4, 6: 6 if hd == 64 else 4, 8: 4, 9: 9}[impl])
 
 
 def _check_attention(C, B, T, H, hd, fimpl=0, bimpl=0):
@@ -251,7 +253,7 @@ def _check_attention(C, B, T, H, hd, fimpl=0, bimpl=0):
     assert _rel(dq, rq) < 3e-2 and _rel(dk, rk) < 3e-2 and _rel(dv, rv) < 3e-2
 
 
-@pytest.mark.parametrize("impl", [1, 4, 6])
+@pytest.mark.parametrize("impl", [1, 4, 6, 8])
 @pytest.mark.parametrize("hd", [64, 128])
 def test_attention_fwd_rescale_branch(C, impl, hd):
     """The online softmax's deferred rescale fires only when a row's max grows by > 2^8 between
@@ -1331,7 +1333,8 @@ def test_gemm_nn_swiglu_bwd_epilogue(C, M, F_, K, perm):
                                            (1, 1100, 1, True), (2, 256, 2, False), (1, 300, 2, False)])
 def test_attention_bwd_dkdv4(C, B, T, H, causal):
     """impl 7: the dQ kernel + the 64-keys-per-wave dK/dV kernel (one wave per SIMD, asm-owned
-    AGPR accumulators).  Same products in the same order as impl 4: bit-identical to it, incl.
+    AGPR accumulators, K pre-scaled).  Same products in the same order as impl 9 (the v3 pair
+    with the K pre-scale): bit-identical to it, incl.
     the inverse RoPE and the QKV bias gradient (32-key partial rows); ragged T (partial 256-key
     blocks, bias rows past the last key), non-causal, strided views; and the fp32 oracle."""
     torch.manual_seed(48)
@@ -1343,7 +1346,7 @@ def test_attention_bwd_dkdv4(C, B, T, H, causal):
     pos = torch.randint(0, 4096, (B * T,), device=DEV)
     tab = R.rope_table(4096, hd, 10000.0).to(DEV)
     outs = []
-    for impl in (7, 4):
+    for impl in (7, 9):
         for rope in (False, True):
             d = torch.full_like(qkv, float("nan"))
             dq, dk, dv = (d[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
