@@ -31,6 +31,8 @@ def _load():
     # The attention kernel generation is a per-call argument (``impl`` of attn_fwd / attn_bwd,
     # 0 = the per-head-dim default, the measured winner).  For same-box A/B runs of whole models
     # DPFS_ATTN_IMPL = "<fwd>[,<bwd>]", read once here, becomes the default of that argument.
+    if os.environ.get("DPFS_GEMM_GROUP_M"):   # A/B: tile-row group of the GEMMs' item order (4)
+        _C.gemm4_group_m(int(os.environ["DPFS_GEMM_GROUP_M"]))
     spec = (os.environ.get("DPFS_ATTN_IMPL") or "0").split(",")
     fi, bi = int(spec[0] or 0), int(spec[1] if len(spec) > 1 and spec[1] else 0)
     if fi or bi:

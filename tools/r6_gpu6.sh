@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
-  "240|t_dkdv4|python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k 'dkdv4 or (test_attention and 4)'" \
+  "240|t_dkdv4|python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k 'dkdv4 or (test_attention and 4) or gemm_unaligned or gemm_f32'" \
   "240|probe_dkdv4|python -u tools/attn_probe.py --bwd --impl 4 7 4 7 --iters 20" \
   "300|prof_dkdv4|cd /tmp && timeout -k 10 120 rocprofv3 --kernel-trace --stats -d \$GRAFT_REPO_ROOT/gpurun_out/pk4 -o run -- python3 \$GRAFT_REPO_ROOT/tools/attn_probe.py --bwd --impl 7 --iters 10 && python3 \$GRAFT_REPO_ROOT/tools/prof_summary.py \$GRAFT_REPO_ROOT/gpurun_out/pk4/run_results.db --top 8 > \$GRAFT_REPO_ROOT/gpurun_out/sum_dkdv4.txt; rm -rf \$GRAFT_REPO_ROOT/gpurun_out/pk4" \
   "400|ab_bwd7|bash tools/ab_env.sh DPFS_ATTN_IMPL '0,4 0,7 0,4 0,7'" \
