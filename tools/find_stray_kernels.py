@@ -50,15 +50,28 @@ def main():
             step(pool[i % 4][0], pos, pool[i % 4][1])
         torch.cuda.synchronize()
     print(f"CPU ops that launched GPU work over {a.steps} steps ({'fp32' if a.fp32 else 'bf16'}), our bindings excluded:")
-    for ev in prof.key_averages(group_by_stack_n=10):
+    for ev in prof.key_averages():
         dt = getattr(ev, "self_device_time_total", None)
         if dt is None:
             dt = getattr(ev, "self_cuda_time_total", 0)
         if not ev.key.startswith("aten::") or dt <= 0:
             continue
-        stack = [s for s in (ev.stack or []) if "site-packages" not in s and "/torch/" not in s][:6]
         print(f"  {ev.count / a.steps:5.2f}/step  {ev.key}  ({dt / a.steps:.1f} us/step on the GPU)")
-        for s in stack:
+    # call sites: the Python frames (ours) of every such op that has device work of its own
+    sites = {}
+    for e in prof.events():
+        if e.device_type.name != "CPU" or not e.name.startswith("aten::"):
+            continue
+        kids = [k for k in e.kernels] if hasattr(e, "kernels") else []
+        if not kids:
+            continue
+        st = tuple(s for s in (e.stack or []) if "distributed_pytorch_from_scratch_amd" in s or "tools/" in s)[:4]
+        key = (e.name, st, tuple(sorted(set(k.name[:60] for k in kids))))
+        sites[key] = sites.get(key, 0) + 1
+    print("call sites (op, our frames, kernels launched):")
+    for (name, st, ks), n in sorted(sites.items(), key=lambda kv: -kv[1]):
+        print(f"  {n / a.steps:5.2f}/step  {name}  kernels {list(ks)}")
+        for s in st:
             print(f"      at {s}")
 
 
