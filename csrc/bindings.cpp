@@ -99,6 +99,7 @@ int dpfs_ce_part_floats();
 void dpfs_ce_finalize(const float*, const int64_t*, long long, float*, float*, float*, float*, float*, int, int, int,
                       int, hipStream_t);
 void dpfs_ce_valid_scale(const int64_t*, long long, float*, float*, float*, int, hipStream_t);
+void dpfs_ce_grad_scale(const float*, const void*, int, const float*, float*, int, hipStream_t);
 long long dpfs_emb_sort_ws(int);
 void dpfs_occupy(int, double, hipStream_t);
 void dpfs_attn_stagger(int);
@@ -1066,6 +1067,22 @@ std::vector<torch::Tensor> ce_valid_scale(torch::Tensor targets, int64_t ignore_
   return {gs, n};
 }
 
+torch::Tensor ce_grad_scale(torch::Tensor valid, torch::Tensor gloss, torch::Tensor n_valid) {
+  check_cuda(valid, "valid");
+  TORCH_CHECK(valid.scalar_type() == torch::kFloat32 && valid.is_contiguous(), "ce_grad_scale: fp32 valid [M]");
+  TORCH_CHECK((gloss.scalar_type() == torch::kFloat32 || gloss.scalar_type() == torch::kBFloat16) && gloss.numel() == 1 &&
+                  gloss.is_cuda(), "ce_grad_scale: gloss fp32 / bf16 scalar on the device");
+  TORCH_CHECK(n_valid.scalar_type() == torch::kFloat32 && n_valid.numel() == 1 && n_valid.is_cuda(),
+              "ce_grad_scale: n_valid fp32 scalar on the device");
+  const at::DeviceGuard g(valid.device());
+  auto gs = torch::empty_like(valid);
+  auto gl = gloss.contiguous();
+  auto nv = n_valid.contiguous();
+  dpfs_ce_grad_scale(valid.data_ptr<float>(), gl.data_ptr(), gl.scalar_type() == torch::kBFloat16 ? 1 : 0,
+                     nv.data_ptr<float>(), gs.data_ptr<float>(), (int)valid.numel(), stream());
+  return gs;
+}
+
 torch::Tensor ce_fwd_stats(torch::Tensor logits, torch::Tensor targets, int64_t vocab_start, int64_t vocab_valid) {
   check_rowmajor(logits, "logits");
   TORCH_CHECK(logits.is_contiguous(), "ce: logits contiguous");
@@ -1643,6 +1660,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("occupy", [](int64_t blocks, double us) { dpfs_occupy((int)blocks, us, stream()); }, py::arg("blocks"),
         py::arg("us"),
         "collective stand-in on the current stream: `blocks` resident 1024-thread workgroups for `us` microseconds");
+  m.def("ce_grad_scale", &ce_grad_scale, py::arg("valid"), py::arg("gloss"), py::arg("n_valid"),
+        "gs = valid * gloss / n_valid (the CE backward's per-row loss gradient; device scalars, one launch)");
   m.def("attn_stagger", [](int v) { dpfs_attn_stagger(v); },
         "A/B hook: odd workgroups of the v3 attention backward kernels start v x 8k cycles late (0 default)");
   m.def("embedding_fwd", &embedding_fwd);

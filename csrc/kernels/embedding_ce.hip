@@ -562,6 +562,16 @@ __global__ __launch_bounds__(256) void ce_valid_scale_k(const int64_t* __restric
   if (blockIdx.x == 0 && threadIdx.x == 0) n_valid[0] = n;
 }
 
+// d loss / d row of the CE backward: gs[r] = valid[r] * gloss / n_valid (gloss: the loss's
+// incoming gradient, fp32 or bf16 scalar; n_valid: the fp32 valid-row count of ce_finalize), one
+// launch instead of a framework divide + multiply.
+template <typename TG>
+__global__ __launch_bounds__(256) void ce_grad_scale_k(const float* __restrict__ valid, const TG* __restrict__ gloss,
+                                                       const float* __restrict__ n_valid, float* __restrict__ gs, int M) {
+  const float c = (float)gloss[0] / n_valid[0];
+  for (int r = blockIdx.x * 256 + threadIdx.x; r < M; r += gridDim.x * 256) gs[r] = valid[r] * c;
+}
+
 // --------------------------------------------- deterministic counting sort of token ids --
 // The deterministic embedding backward needs the ids' stable order and each local vocab row's
 // segment (perm, seg).  A two-pass LSD radix sort on 8-bit digits of the 16-bit key (local id,
@@ -846,6 +856,16 @@ extern "C" void dpfs_ce_valid_scale(const int64_t* tgt, long long ignore, float*
   const int nb = std::max(1, std::min(kCeBlocks, (M + 255) / 256));
   ce_valid_count_k<<<nb, 256, 0, s>>>(tgt, ignore, part, M);
   ce_valid_scale_k<<<nb, 256, 0, s>>>(tgt, ignore, part, gs, n_valid, M);
+}
+
+extern "C" void dpfs_ce_grad_scale(const float* valid, const void* gloss, int gloss_bf16, const float* n_valid,
+                                   float* gs, int M, hipStream_t s) {
+  if (M <= 0) return;
+  const int nb = std::min(1024, (M + 255) / 256);
+  if (gloss_bf16)
+    ce_grad_scale_k<bf16><<<nb, 256, 0, s>>>(valid, (const bf16*)gloss, n_valid, gs, M);
+  else
+    ce_grad_scale_k<float><<<nb, 256, 0, s>>>(valid, (const float*)gloss, n_valid, gs, M);
 }
 
 // ws: 4 M + 256 * ceil(M / 1024) ints.  perm: int64 [M] (positions past seg[vlocal] hold the

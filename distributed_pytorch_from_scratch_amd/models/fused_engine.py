@@ -333,12 +333,8 @@ class DecoderTrainFn(torch.autograd.Function):
         F8.activate(ctx.f8map)
         _defer_begin()
         tab = ctx.tab
-        gscale = []   # d loss / d row-sum: only the CE backward that did not run in the forward needs it
-
-        def gscale_all():
-            if not gscale:
-                gscale.append(gloss.float() / ctx.n_valid)
-            return gscale[0]
+        # d loss / d row (valid * gloss / n_valid, one native launch per chunk): only the CE
+        # backward that did not run in the forward needs it
         nL = len(layers)
         # fp32 gradients: every one is written straight into its slot of the model's gradient
         # arena (parallel/grad_sync.GradArena; the first chunk's contribution in place, later
@@ -428,7 +424,7 @@ class DecoderTrainFn(torch.autograd.Function):
                                        f"({float(gloss.float().mean())}); call loss() without unit_grad when "
                                        "scaling the loss")
             else:
-                gs = s["valid"] * gscale_all()
+                gs = k.ce_grad_scale(s["valid"], gloss, ctx.n_valid)
                 db = first(g, "lm_b", dl, dl.size(1)) if head.bias is not None else None
                 k.ce_bwd(dl, s["tgt"], s["ce_lse"], gs, vst, vvalid, dl, db)    # + lm_head bias grad
             dh = GS.gemm_nn(k, dl, W(head.weight), out=_slot(ci, dl.size(0), d, dt))

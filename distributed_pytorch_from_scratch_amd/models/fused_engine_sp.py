@@ -167,7 +167,6 @@ class DecoderTrainFnSP(torch.autograd.Function):
         F8.activate(ctx.f8map)
         _defer_begin()
         tab = ctx.tab
-        gscale_all = gloss.float() / ctx.n_valid
         nL = len(layers)
         # fp32 gradients straight into the model's gradient arena (parallel/grad_sync.GradArena):
         # DP all-reduces run on contiguous slices of it, no pack / copy back
@@ -235,7 +234,7 @@ class DecoderTrainFnSP(torch.autograd.Function):
         d = model.args.attn_dim
         lm_p = []
         for ci, s in enumerate(st):    # CE backward in place, lm_head dgrad -> reduce-scatter, lm_head wgrad
-            gs = s["valid"] * gscale_all
+            gs = k.ce_grad_scale(s["valid"], gloss, ctx.n_valid)
             dl = s["logits"]
             db = first(g, "lm_b", dl, dl.size(1)) if head.bias is not None else None
             k.ce_bwd(dl, s["tgt"], s["ce_lse"], gs, vst, vvalid, dl, db)

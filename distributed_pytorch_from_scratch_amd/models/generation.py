@@ -209,6 +209,7 @@ class DecodeGraph:
             decode_step(model, self.ids, self.pos, cache)
         torch.cuda.current_stream().wait_stream(s)
         cache.len_t.copy_(saved)
+        _graph_rng_state_normal(dev)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             for i in range(nsteps):
@@ -225,6 +226,26 @@ class DecodeGraph:
         self.ids.copy_(ids.view(-1, 1))
         self.graph.replay()
         return self.outs
+
+
+_RNG_GRAPH_STATE = set()
+
+
+def _graph_rng_state_normal(dev) -> None:
+    """The first graph capture of a process creates the CUDA generator's graph-safe RNG state;
+    created under inference mode (this module's decode paths) those tensors are inference
+    tensors, and every later capture outside inference mode (engine.GraphTrainStep) fails on
+    their in-place update.  So the state is created by a one-op capture with inference mode off
+    before the first decode capture."""
+    if dev.index in _RNG_GRAPH_STATE:
+        return
+    with torch.inference_mode(False):
+        x = torch.zeros(1, device=dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            x.add_(1)
+        del g, x
+    _RNG_GRAPH_STATE.add(dev.index)
 
 
 def _use_graph(dev) -> bool:

@@ -469,6 +469,11 @@ def ce_valid_scale(targets: torch.Tensor, ignore_index: int) -> Tuple[torch.Tens
     return valid / n, n
 
 
+def ce_grad_scale(valid: torch.Tensor, gloss: torch.Tensor, n_valid: torch.Tensor) -> torch.Tensor:
+    """Per-row gradient scale of the CE backward: valid * gloss / n_valid."""
+    return valid * (gloss.float().reshape(()) / n_valid.reshape(()))
+
+
 def ce_bwd(logits: torch.Tensor, targets: torch.Tensor, lse: torch.Tensor, gscale: torch.Tensor,
            vocab_start: int, vocab_valid: int, out: torch.Tensor,
            dbias: Optional[torch.Tensor] = None) -> torch.Tensor:

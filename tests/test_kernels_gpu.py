@@ -1362,3 +1362,17 @@ def test_attention_bwd_dkdv4(C, B, T, H, causal):
     R.attn_bwd(do.float(), q.float(), k.float(), v.float(), o.float(), lse, 0.125, causal, rq, rk, rv)
     dq, dk, dv = (d[:, i * H * hd:(i + 1) * H * hd].view(B, T, H, hd) for i in range(3))
     assert _rel(dq, rq) < 3e-2 and _rel(dk, rk) < 3e-2 and _rel(dv, rv) < 3e-2
+
+
+@pytest.mark.parametrize("M", [1, 1000, 32768, 70001])
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
+def test_ce_grad_scale(C, M, gdt):
+    """The CE backward's per-row loss gradient valid * gloss / n_valid in one launch (device
+    scalars, no host sync) against the oracle."""
+    torch.manual_seed(49)
+    valid = (torch.rand(M, device=DEV) > 0.2).float()
+    gloss = torch.tensor(0.37, device=DEV).to(gdt)
+    n = valid.sum().clamp_min(1.0)
+    acc = torch.stack([torch.tensor(3.0, device=DEV), n])     # n_valid as a view, as the engine passes it
+    gs = C.ce_grad_scale(valid, gloss, acc[1])
+    assert torch.allclose(gs, R.ce_grad_scale(valid, gloss, acc[1]), rtol=1e-6, atol=0)
