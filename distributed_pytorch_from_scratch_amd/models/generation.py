@@ -228,15 +228,16 @@ class DecodeGraph:
         return self.outs
 
 
-_RNG_GRAPH_STATE = set()
+_RNG_GRAPH_STATE = {}
 
 
 def _graph_rng_state_normal(dev) -> None:
-    """The first graph capture of a process creates the CUDA generator's graph-safe RNG state;
-    created under inference mode (this module's decode paths) those tensors are inference
-    tensors, and every later capture outside inference mode (engine.GraphTrainStep) fails on
-    their in-place update.  So the state is created by a one-op capture with inference mode off
-    before the first decode capture."""
+    """The CUDA generator's graph-safe RNG state is allocated when the first graph registers with
+    the generator (and freed when the last one is destroyed); allocated under inference mode
+    (this module's decode paths) those tensors are inference tensors, and every later capture
+    outside inference mode (engine.GraphTrainStep) fails on their in-place update.  So a
+    one-op graph built with inference mode off is kept alive for the process: the state is
+    allocated once, as normal tensors, before the first decode capture."""
     if dev.index in _RNG_GRAPH_STATE:
         return
     with torch.inference_mode(False):
@@ -244,8 +245,7 @@ def _graph_rng_state_normal(dev) -> None:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             x.add_(1)
-        del g, x
-    _RNG_GRAPH_STATE.add(dev.index)
+    _RNG_GRAPH_STATE[dev.index] = (g, x)
 
 
 def _use_graph(dev) -> bool:
