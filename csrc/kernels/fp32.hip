@@ -25,7 +25,7 @@ namespace dpfs {
 #define MFMA_F32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x2f32((a), (b), (c), 0, 0, 0)
 
 // ------------------------------------------------------------------------------ GEMM --
-constexpr int kF32BM = 128, kF32BK = 16, kF32LD = 128 + 4;   // LDS row: 128 floats + pad
+constexpr int kF32BM = 128, kF32BK = 32, kF32LD = 128 + 4;   // LDS row: 128 floats + pad
 
 // One 128 x 16 operand tile: AKM = true when the operand is K-major in memory (x[r][k], ld
 // elements per row), false when it is MN-major (x[k][r]).  LDS image: s[k][r], fp32.  TI: the
@@ -42,15 +42,17 @@ __device__ __forceinline__ f32x4 ld4(const TI* p) {
 }
 template <bool AKM, typename TI = float>
 struct F32Tile {
-  f32x4 v[2];
+  static constexpr int NI = kF32BK / 8;       // 16-byte pieces per thread (128 x BK floats / 256)
+  static constexpr int TPR = kF32BK / 4;      // K-major: threads per row
+  f32x4 v[NI];
   __device__ __forceinline__ void load(const TI* __restrict__ x, long long ld, int R, int Kd, int r0, int k0,
                                        bool vec) {
     const int t = threadIdx.x;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NI; ++i) {
       f32x4 q = {0.f, 0.f, 0.f, 0.f};
       if constexpr (AKM) {
-        const int r = t / 4 + 64 * i, k = (t & 3) * 4;
+        const int r = t / TPR + (256 / TPR) * i, k = (t % TPR) * 4;
         const int gr = r0 + r, gk = k0 + k;
         if (gr < R) {
           if (vec && gk + 3 < Kd) {
@@ -78,9 +80,9 @@ struct F32Tile {
   __device__ __forceinline__ void store(float* s) const {
     const int t = threadIdx.x;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NI; ++i) {
       if constexpr (AKM) {
-        const int r = t / 4 + 64 * i, k = (t & 3) * 4;
+        const int r = t / TPR + (256 / TPR) * i, k = (t % TPR) * 4;
 #pragma unroll
         for (int j = 0; j < 4; ++j) s[(k + j) * kF32LD + r] = v[i][j];
       } else {
@@ -182,6 +184,37 @@ __global__ __launch_bounds__(256) void gemm_f32_k(const TI* __restrict__ A, cons
 template <int HD>
 struct F32Rows {
   static constexpr int LD = HD + 1;
+  // the same tile in two halves: fetch = the global loads into registers (issued a tile ahead,
+  // so their latency hides under the current tile's MFMAs -- these kernels run one or two waves
+  // per SIMD, nothing else covers it), put = the LDS writes
+  template <int R>
+  struct Regs {
+    static constexpr int N = (R * HD / 4 + 255) / 256;
+    f32x4 v[N];
+  };
+  template <int R>
+  __device__ __forceinline__ static void fetch(Regs<R>& g, const float* __restrict__ x, long long ld, int r0, int T) {
+#pragma unroll
+    for (int n = 0; n < Regs<R>::N; ++n) {
+      const int i = threadIdx.x + 256 * n;
+      const int r = i / (HD / 4), c = (i % (HD / 4)) * 4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (i < R * HD / 4 && r0 + r < T) v = *reinterpret_cast<const f32x4*>(x + (long long)(r0 + r) * ld + c);
+      g.v[n] = v;
+    }
+  }
+  template <int R>
+  __device__ __forceinline__ static void put(float* s, const Regs<R>& g) {
+#pragma unroll
+    for (int n = 0; n < Regs<R>::N; ++n) {
+      const int i = threadIdx.x + 256 * n;
+      const int r = i / (HD / 4), c = (i % (HD / 4)) * 4;
+      if (i < R * HD / 4) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[r * LD + c + j] = g.v[n][j];
+      }
+    }
+  }
   // rows [r0, r0 + R) of a (B, T, H, HD) view (row stride ld elements) into s; rows >= T zero
   template <int R>
   __device__ __forceinline__ static void load(float* s, const float* __restrict__ x, long long ld, int r0, int T) {
@@ -232,11 +265,25 @@ __global__ __launch_bounds__(256) void attn_fwd_f32_k(const float* __restrict__ 
   const float c2 = scale * kF32Log2e;
   float m = -INFINITY, lsum = 0.f;
   const int kv_end = causal ? min(T, q0 + BQ) : T;
+  typename F32Rows<HD>::template Regs<BKV> gk, gv;
+  constexpr bool PF = HD == 64;   // (at 32 the prefetch registers cost a wave per SIMD)
+  if (PF) {
+    F32Rows<HD>::fetch(gk, kb_, ldk, 0, T);
+    F32Rows<HD>::fetch(gv, vb_, ldv, 0, T);
+  }
   for (int kv0 = 0; kv0 < kv_end; kv0 += BKV) {
     __syncthreads();
-    F32Rows<HD>::template load<BKV>(sk, kb_, ldk, kv0, T);
-    F32Rows<HD>::template load<BKV>(sv, vb_, ldv, kv0, T);
+    if (!PF) {
+      F32Rows<HD>::fetch(gk, kb_, ldk, kv0, T);
+      F32Rows<HD>::fetch(gv, vb_, ldv, kv0, T);
+    }
+    F32Rows<HD>::put(sk, gk);
+    F32Rows<HD>::put(sv, gv);
     __syncthreads();
+    if (PF && kv0 + BKV < kv_end) {   // the next tile's loads fly under this tile's MFMAs
+      F32Rows<HD>::fetch(gk, kb_, ldk, kv0 + BKV, T);
+      F32Rows<HD>::fetch(gv, vb_, ldv, kv0 + BKV, T);
+    }
     if (causal && kv0 > q0 + 32 * wave + 31) continue;   // wave-uniform: every key after every query
     f32x16 s[2];
 #pragma unroll
@@ -359,11 +406,26 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_f32_k(
 #pragma unroll
     for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
   const int kv_end = causal ? min(T, q0 + BQ) : T;
+  const float lse2 = lse * kF32Log2e, c2 = scale * kF32Log2e;   // p = exp2(c2 S - lse log2 e)
+  typename F32Rows<HD>::template Regs<BKV> gk, gv;
+  constexpr bool PF = HD == 64;
+  if (PF) {
+    F32Rows<HD>::fetch(gk, kb_, ldk, 0, T);
+    F32Rows<HD>::fetch(gv, vb_, ldv, 0, T);
+  }
   for (int kv0 = 0; kv0 < kv_end; kv0 += BKV) {
     __syncthreads();
-    F32Rows<HD>::template load<BKV>(sk, kb_, ldk, kv0, T);
-    F32Rows<HD>::template load<BKV>(sv, vb_, ldv, kv0, T);
+    if (!PF) {
+      F32Rows<HD>::fetch(gk, kb_, ldk, kv0, T);
+      F32Rows<HD>::fetch(gv, vb_, ldv, kv0, T);
+    }
+    F32Rows<HD>::put(sk, gk);
+    F32Rows<HD>::put(sv, gv);
     __syncthreads();
+    if (PF && kv0 + BKV < kv_end) {
+      F32Rows<HD>::fetch(gk, kb_, ldk, kv0 + BKV, T);
+      F32Rows<HD>::fetch(gv, vb_, ldv, kv0 + BKV, T);
+    }
     if (causal && kv0 > q0 + 32 * wave + 31) continue;
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh) {
@@ -383,7 +445,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_f32_k(
       for (int r = 0; r < 16; ++r) {
         const int key = kv0 + 32 * kh + 8 * (r >> 2) + 4 * hf + (r & 3);
         const bool ok = key < T && qi < T && (!causal || key <= qi);
-        const float p = ok ? expf(s[r] * scale - lse) : 0.f;
+        const float p = ok ? exp2f(s[r] * c2 - lse2) : 0.f;
         s[r] = p * (dp[r] - delta);
       }
       // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
@@ -453,16 +515,33 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_f32_k(
       dv[d][r] = 0.f;
     }
   const int qstart = causal ? (k0 / BQ) * BQ : 0;
+  const float c2 = scale * kF32Log2e;   // p = exp2(c2 S - lse log2 e)
+  typename F32Rows<HD>::template Regs<BQ> gq, gd;
+  float gl = 0.f, gdl = 0.f;
+  auto fetch_tile = [&](int q0_) {
+    F32Rows<HD>::fetch(gq, qb_, ldq, q0_, T);
+    F32Rows<HD>::fetch(gd, dob_, lddo, q0_, T);
+    if (threadIdx.x < BQ) {
+      const int q = q0_ + threadIdx.x;
+      gl = q < T ? LSE[(long long)bh * T + q] * kF32Log2e : 0.f;
+      gdl = q < T ? -NDEL[(long long)bh * T + q] : 0.f;
+    }
+  };
+  // (head_dim 64 only: at 32 the prefetch registers cost the second wave per SIMD, at 128
+  // they spill)
+  constexpr bool PF = HD == 64;
+  if (PF && qstart < T) fetch_tile(qstart);
   for (int q0 = qstart; q0 < T; q0 += BQ) {
     __syncthreads();
-    F32Rows<HD>::template load<BQ>(sq, qb_, ldq, q0, T);
-    F32Rows<HD>::template load<BQ>(sdo, dob_, lddo, q0, T);
+    if (!PF) fetch_tile(q0);
+    F32Rows<HD>::put(sq, gq);
+    F32Rows<HD>::put(sdo, gd);
     if (threadIdx.x < BQ) {
-      const int q = q0 + threadIdx.x;
-      sl[threadIdx.x] = q < T ? LSE[(long long)bh * T + q] : 0.f;
-      sd[threadIdx.x] = q < T ? -NDEL[(long long)bh * T + q] : 0.f;
+      sl[threadIdx.x] = gl;
+      sd[threadIdx.x] = gdl;
     }
     __syncthreads();
+    if (PF && q0 + BQ < T) fetch_tile(q0 + BQ);   // the next tile's loads fly under this tile's MFMAs
     if (causal && q0 + BQ - 1 < k0 + 32 * wave) continue;   // every query before every key
 #pragma unroll
     for (int qh = 0; qh < 2; ++qh) {
@@ -482,7 +561,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_f32_k(
       for (int r = 0; r < 16; ++r) {
         const int ql = 32 * qh + 8 * (r >> 2) + 4 * hf + (r & 3), q = q0 + ql;
         const bool ok = key < T && q < T && (!causal || key <= q);
-        const float p = ok ? expf(s[r] * scale - sl[ql]) : 0.f;
+        const float p = ok ? exp2f(s[r] * c2 - sl[ql]) : 0.f;
         s[r] = p;
         pd[r] = p * (dp[r] - sd[ql]);
       }
