@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 validation: the whole GPU suite (the N-rank rehearsal test separately, with a progress
 # ticker), smoke(), the headline bench and its kernel trace.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 ( while sleep 50; do date >> gpurun_out/tick.log; done ) &

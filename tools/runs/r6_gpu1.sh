@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-6 GPU check 1: fused attention backward numerics + timing, stream-K error word, bench A/B.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
   "300|t_fused|python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k 'fused6 or stream_k'" \

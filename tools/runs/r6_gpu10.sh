@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU check 10: backward with K pre-scaled (impl 4 now; 9 = the old form): tests, per-call
 # A/B, headline A/B; forward impl 8 combined.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
   "300|t_ksc|python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k 'attention'" \

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-6 GPU check 16: stray kernel call sites; TP-2 collective/compute overlap under emulated collectives.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
   "200|stray16c|python -u tools/find_stray_kernels.py" \

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU check 18: where a short-K NT GEMM tile's time goes (gemm4 DIAG split: step-entry
 # wait / body / epilogue per tile) for lm_head and gate|up, default schedule.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
   "300|gdiag|python -u tools/gemm4_probe.py --layouts nt --shapes lmhead gateup qkv --scheds 0 --rounds 1 --iters 5 --diag --no-blas"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU check 2: fp32 native kernels + training, CE bookkeeping, embedding sort, bench,
 # step traces (bf16 headline and fp32 reference preset).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
   "400|t_new|python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k 'f32 or ce_finalize or emb_sort or fused6 or stream_k'" \

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU check 21: fp32 attention with the next tile's loads in flight under the MFMAs and
 # exp2: tests, fp32 bench vs the reference's eager fp32 on the same box, step trace.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
   "300|t_f32|python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_kernels_gpu.py -k 'attention_f32 or gemm_f32' tests/test_fp32_gpu.py" \

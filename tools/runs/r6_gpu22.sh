@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-6 GPU check 22: fp32 GEMM with 32-deep K stages; fp32 model tests; fp32 bench + trace.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
   "300|t_f32b|python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_kernels_gpu.py -k 'attention_f32 or gemm_f32 or gemm_unaligned'" \

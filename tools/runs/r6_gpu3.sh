@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU check 3: fp32 fixes + split-K, CE bookkeeping, GEMM beside a collective stand-in,
 # planner at TP 2/4/8, bench, stagger A/B, TP floors with emulated collectives, fp32 bench.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
   "300|t_k|python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k 'f32 or ce_finalize or emb_sort or beside_collective'" \

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU check 4: forward row-sum-by-MFMA A/B, fp32 (ours vs the reference's eager fp32) on one
 # box + its step trace, TP-2 emulated collectives at 153 GB/s, one- vs two-chunk kernel traces.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
   "200|t_att6|python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k 'test_attention and 6'" \

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU check 6: the 64-keys-per-wave dK/dV kernel (impl 7): bitwise vs impl 4, per-call
 # A/B at the GPT-2 small and LLaMA-like shapes, kernel trace; the headline step with gap analysis.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
   "240|t_dkdv4|python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k 'dkdv4 or (test_attention and 4) or gemm_unaligned or gemm_f32'" \

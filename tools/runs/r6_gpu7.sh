@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU check 7: HIP-graph train step (bitwise test + bench A/B); TP 2 / 8 chunk counts
 # under emulated collectives (1 / 2 / 4 chunks).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
   "240|t_graph|python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_model_gpu.py -k graph_train_step" \

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU check 9: forward with scale + running max folded into the MFMAs (impl 8): oracle /
 # rescale tests, per-call A/B, headline A/B.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
   "240|t_fwd8|python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k 'test_attention'" \
