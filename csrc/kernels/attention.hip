@@ -1223,8 +1223,6 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
           sc[0][i] = __builtin_amdgcn_exp2f(KSC ? sc[0][i] : sc[0][i] * c2);
         __builtin_amdgcn_sched_barrier(0);
       }
-      // the block's last tile: K / V are consumed, load the next block's
-      if (ahead && t == nq - 1) load_kv(key1);
       if constexpr (DIAG) {
         const unsigned long long t1 = stamp_dep(sc[0][15] + dp[1][15]);
         d_acc[1] += t1 - d_t0;
@@ -1269,6 +1267,10 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
             pd[2 * qt + s1][j] = (bf16)vmulf(sc[qt][i], dp[qt][i]);
             pd[2 * qt + s1][j + 1] = (bf16)vmulf(sc[qt][i + 1], dp[qt][i + 1]);
           }
+      // the block's last tile: K / V are consumed, load the next block's.  Issued here, after
+      // every exp / dS of the tile, not between the S / dP MFMAs and the exps: a branch there
+      // lets the compiler sink query tile 0's exps below it, out from under tile 1's MFMAs.
+      if (ahead && t == nq - 1) load_kv(key1);
       if constexpr (DIAG) {
         const unsigned long long t1 = stamp_dep(__builtin_bit_cast(float, __builtin_bit_cast(u32x4, pd[3])[3]));
         d_acc[2] += t1 - d_t0;
@@ -1787,8 +1789,6 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
           sc[0][i] = __builtin_amdgcn_exp2f(fmaf(sc[0][i], c2, lc));
         __builtin_amdgcn_sched_barrier(0);
       }
-      // the block's last tile: Q / dO are consumed, load the next block's rows
-      if (ahead && t == nkv - 1) load_qdo(qi1);
       // K^T fragments (A of dQ^T: lane d = 32 dt + r32, keys 16 s + 4 hf + 0..3 / 8..11)
       constexpr int NH = 2 * DTN * 4;
       s16x4 th[(NH + 15) / 16 * 16];
@@ -1820,6 +1820,10 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
           pd[s4][j] = (bf16)vmulf(sc[kh][i], dp[kh][i]);
           pd[s4][j + 1] = (bf16)vmulf(sc[kh][i + 1], dp[kh][i + 1]);
         }
+      // the block's last tile: Q / dO are consumed, load the next block's rows (after the exps
+      // and dS: a branch between the S / dP MFMAs and the exps lets the compiler sink key half
+      // 0's exps out from under half 1's MFMAs)
+      if (ahead && t == nkv - 1) load_qdo(qi1);
 #pragma unroll
       for (int w = 0; w < (NH + 15) / 16; ++w) tr_wait8(*reinterpret_cast<s16x4(*)[16]>(&th[16 * w]));
 #pragma unroll
