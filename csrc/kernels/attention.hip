@@ -1340,25 +1340,27 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
       RowStage<HD>::put_rows(rv, dV + (long long)b * T * lddv + (long long)h * HD, lddv, kw0, T);
     }
     if (BPK) {
-      // per-wave column sums over the 32 keys: registers summed across the 32 lanes of each half
-      // (keys >= T hold zeros), then the two halves hold disjoint d rows.
+      // per-wave column sums over the 32 keys (keys >= T hold zeros): a transpose reduction over
+      // the 32 lanes of each half (lane32_sums; the two halves hold disjoint d rows), after which
+      // lane r32 holds the sums of registers r32 DTN / 2 + j and stores them
       const long long row = (((long long)h * (BH / H) + b) * nkb + kb) * 4 + wave;
+      float wk[DTN * 16], wv[DTN * 16];
 #pragma unroll
       for (int dt = 0; dt < DTN; ++dt)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float a = key < T ? dkt[dt][i] : 0.f, c = key < T ? dvt[dt][i] : 0.f;
-#pragma unroll
-          for (int o = 1; o < 32; o <<= 1) {
-            a += __shfl_xor(a, o, 64);
-            c += __shfl_xor(c, o, 64);
-          }
-          if (r32 == 0) {
-            const int d = 32 * dt + 8 * (i >> 2) + 4 * hf + (i & 3);
-            BPK[row * HD + d] = a;
-            BPV[row * HD + d] = c;
-          }
+          wk[16 * dt + i] = key < T ? dkt[dt][i] : 0.f;
+          wv[16 * dt + i] = key < T ? dvt[dt][i] : 0.f;
         }
+      lane32_sums(wk, r32);
+      lane32_sums(wv, r32);
+#pragma unroll
+      for (int j = 0; j < DTN / 2; ++j) {
+        const int rr = r32 * (DTN / 2) + j, i = rr & 15;
+        const int d = 32 * (rr >> 4) + 8 * (i >> 2) + 4 * hf + (i & 3);
+        BPK[row * HD + d] = wk[j];
+        BPV[row * HD + d] = wv[j];
+      }
     }
     if constexpr (DIAG) d_acc[5] += stamp_dep(0.f) - d_t0;
   }
@@ -1858,17 +1860,19 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
       RowStage<HD>::get(ep, rq);
       RowStage<HD>::put_rows(rq, dQ + (long long)b * T * lddq + (long long)h * HD, lddq, wq0, T);
     }
-    if (BPQ) {
+    if (BPQ) {   // per-wave column sums over the 32 queries (lane32_sums, as dK / dV's)
       const long long prow = (((long long)h * (BH / H) + b) * nqb + qb) * 4 + wave;
+      float wq[DTN * 16];
 #pragma unroll
       for (int dt = 0; dt < DTN; ++dt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float a = qi < T ? dq[dt][i] : 0.f;
+        for (int i = 0; i < 16; ++i) wq[16 * dt + i] = qi < T ? dq[dt][i] : 0.f;
+      lane32_sums(wq, r32);
 #pragma unroll
-          for (int o = 1; o < 32; o <<= 1) a += __shfl_xor(a, o, 64);
-          if (r32 == 0) BPQ[prow * HD + 32 * dt + 8 * (i >> 2) + 4 * hf + (i & 3)] = a;
-        }
+      for (int j = 0; j < DTN / 2; ++j) {
+        const int rr = r32 * (DTN / 2) + j, i = rr & 15;
+        BPQ[prow * HD + 32 * (rr >> 4) + 8 * (i >> 2) + 4 * hf + (i & 3)] = wq[j];
+      }
     }
   }
 }

@@ -438,6 +438,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_fused_k(
       // per-wave column sums over its 64 keys (keys >= T hold zeros): both key halves, then the
       // 32 lanes of each half; the two lane halves hold disjoint d rows
       const long long row = (((long long)h * (BH / H) + b) * nkb + kb) * 4 + wave;
+      float wk[DTN * 16], wv[DTN * 16];
 #pragma unroll
       for (int dt = 0; dt < DTN; ++dt)
 #pragma unroll
@@ -449,17 +450,18 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_fused_k(
             a += kv ? dkt[kh][dt][i] : 0.f;
             c += kv ? dvt[kh][dt][i] : 0.f;
           }
-#pragma unroll
-          for (int o = 1; o < 32; o <<= 1) {
-            a += __shfl_xor(a, o, 64);
-            c += __shfl_xor(c, o, 64);
-          }
-          if (r32 == 0) {
-            const int d = 32 * dt + 8 * (i >> 2) + 4 * hf + (i & 3);
-            BPK[row * HD + d] = a;
-            BPV[row * HD + d] = c;
-          }
+          wk[16 * dt + i] = a;
+          wv[16 * dt + i] = c;
         }
+      lane32_sums(wk, r32);   // transpose reduction over the 32 lanes of each half
+      lane32_sums(wv, r32);
+#pragma unroll
+      for (int j = 0; j < DTN / 2; ++j) {
+        const int rr = r32 * (DTN / 2) + j, i = rr & 15;
+        const int d = 32 * (rr >> 4) + 8 * (i >> 2) + 4 * hf + (i & 3);
+        BPK[row * HD + d] = wk[j];
+        BPV[row * HD + d] = wv[j];
+      }
     }
   }
 }
@@ -836,22 +838,23 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv4_k(
       const int u = kwh >> 5;   // the 32-key row of the bias partials (v3 layout)
       if (BPK && u < 4 * nkb3) {
         const long long row = (((long long)h * (BH / H) + b) * nkb3 + (u >> 2)) * 4 + (u & 3);
+        float wk[DTN * 16], wv[DTN * 16];   // the v3 kernel's transpose reduction (lane32_sums)
 #pragma unroll
         for (int dt = 0; dt < DTN; ++dt)
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            float a = key < T ? dkt[kh][dt][i] : 0.f, c = key < T ? dvt[kh][dt][i] : 0.f;
-#pragma unroll
-            for (int o = 1; o < 32; o <<= 1) {
-              a += __shfl_xor(a, o, 64);
-              c += __shfl_xor(c, o, 64);
-            }
-            if (r32 == 0) {
-              const int d = 32 * dt + 8 * (i >> 2) + 4 * hf + (i & 3);
-              BPK[row * HD + d] = a;
-              BPV[row * HD + d] = c;
-            }
+            wk[16 * dt + i] = key < T ? dkt[kh][dt][i] : 0.f;
+            wv[16 * dt + i] = key < T ? dvt[kh][dt][i] : 0.f;
           }
+        lane32_sums(wk, r32);
+        lane32_sums(wv, r32);
+#pragma unroll
+        for (int j = 0; j < DTN / 2; ++j) {
+          const int rr = r32 * (DTN / 2) + j, i = rr & 15;
+          const int d = 32 * (rr >> 4) + 8 * (i >> 2) + 4 * hf + (i & 3);
+          BPK[row * HD + d] = wk[j];
+          BPV[row * HD + d] = wv[j];
+        }
       }
     }
   }

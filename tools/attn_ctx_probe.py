@@ -4,6 +4,7 @@ The step trace prices the backward at ~0.37 ms per layer, back-to-back timing at
 Arms (each call bracketed by its own events, median over --n calls):
   hot        back-to-back calls (the operands stay in the 256 MiB infinity cache / L2)
   hot_rope   + inverse RoPE and the QKV bias gradient, as the training step calls it
+  rope_only / bias_only  one of the two
   cold       a 1 GiB memset before each call (infinity cache / L2 flushed)
   after_gemm a bf16 GEMM (~1 ms) before each call (chip under MFMA load, as between the step's GEMMs)
 
@@ -43,11 +44,10 @@ def main():
     ga = torch.randn(8192, 8192, device="cuda").bfloat16()
     gb = torch.randn(8192, 8192, device="cuda").bfloat16()
 
-    def bwd(rope=False):
-        if rope:
-            C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv, pos, tab, db)
-        else:
-            C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv)
+    def bwd(rope=False, bias=None):
+        bias = rope if bias is None else bias
+        C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv, pos if rope else None, tab if rope else None,
+                   db if bias else None)
 
     def fwd():
         C.attn_fwd(q, k, v, scale, True)
@@ -56,6 +56,8 @@ def main():
     arms = {
         "hot": (None, op),
         "hot_rope": (None, (lambda: bwd(True)) if not a.fwd else op),
+        "rope_only": (None, (lambda: bwd(True, False)) if not a.fwd else op),
+        "bias_only": (None, (lambda: bwd(False, True)) if not a.fwd else op),
         "cold": (lambda: flush.zero_(), op),
         "after_gemm": (lambda: torch.mm(ga, gb), op),
         "cold_rope": (lambda: flush.zero_(), (lambda: bwd(True)) if not a.fwd else op),
