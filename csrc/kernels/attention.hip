@@ -1308,12 +1308,41 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
     }
     if constexpr (DIAG) d_t0 = stamp_dep(0.f);
     // epilogue: lane = key, registers = d rows 32 dt + 8 g + 4 hf + j.  dK *= scale, inverse
-    // RoPE (d pairs with d + HD/2: tile dt with dt + DTN/2, same register), 8-byte stores.
+    // RoPE (d pairs with d + HD/2: tile dt with dt + DTN/2, same register), 8-byte stores.  The
+    // key's RoPE position is loaded first and dV's row stores and column sums run under that
+    // load; then the rotation's table loads and dK's.
+    const bool rope = rpos && key < T;
+    const int kpos = rope ? reinterpret_cast<const int*>(rpos)[2 * ((long long)b * T + key)] : 0;   // (low word)
+    // whole-row stores through the wave's LDS rows (dV, then dK in the same rows: one wave's
+    // LDS operations run in order)
+    {
+      u32x4 rv[RowStage<HD>::NI];
+      RowStage<HD>::put(ep, dvt);
+      RowStage<HD>::get(ep, rv);
+      RowStage<HD>::put_rows(rv, dV + (long long)b * T * lddv + (long long)h * HD, lddv, kw0, T);
+    }
+    // per-wave column sums over the 32 keys (keys >= T hold zeros): a transpose reduction over
+    // the 32 lanes of each half (lane32_sums; the two halves hold disjoint d rows), after which
+    // lane r32 holds the sums of registers r32 DTN / 2 + j and stores them
+    const long long brow = (((long long)h * (BH / H) + b) * nkb + kb) * 4 + wave;
+    if (BPV) {
+      float wv[DTN * 16];
+#pragma unroll
+      for (int dt = 0; dt < DTN; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wv[16 * dt + i] = key < T ? dvt[dt][i] : 0.f;
+      lane32_sums(wv, r32);
+#pragma unroll
+      for (int j = 0; j < DTN / 2; ++j) {
+        const int rr = r32 * (DTN / 2) + j, i = rr & 15;
+        BPV[brow * HD + 32 * (rr >> 4) + 8 * (i >> 2) + 4 * hf + (i & 3)] = wv[j];
+      }
+    }
 #pragma unroll
     for (int d = 0; d < DTN; ++d) dkt[d] *= scale;
-    if (rpos && key < T) {
-      KASSERT(rpos[(long long)b * T + key] >= 0, "rope position at key %d", key);
-      const float* tr = rtab + rpos[(long long)b * T + key] * HD;
+    if (rope) {
+      KASSERT(kpos >= 0, "rope position at key %d", key);
+      const float* tr = rtab + (long long)kpos * HD;
 #pragma unroll
       for (int dt = 0; dt < DTN / 2; ++dt)
 #pragma unroll
@@ -1328,38 +1357,23 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dkdv3_k(
           }
         }
     }
-    // whole-row stores through the wave's LDS rows (dK, then dV in the same rows: one wave's
-    // LDS operations run in order)
     {
-      u32x4 rk[RowStage<HD>::NI], rv[RowStage<HD>::NI];
+      u32x4 rk[RowStage<HD>::NI];
       RowStage<HD>::put(ep, dkt);
       RowStage<HD>::get(ep, rk);
-      RowStage<HD>::put(ep, dvt);
-      RowStage<HD>::get(ep, rv);
       RowStage<HD>::put_rows(rk, dK + (long long)b * T * lddk + (long long)h * HD, lddk, kw0, T);
-      RowStage<HD>::put_rows(rv, dV + (long long)b * T * lddv + (long long)h * HD, lddv, kw0, T);
     }
     if (BPK) {
-      // per-wave column sums over the 32 keys (keys >= T hold zeros): a transpose reduction over
-      // the 32 lanes of each half (lane32_sums; the two halves hold disjoint d rows), after which
-      // lane r32 holds the sums of registers r32 DTN / 2 + j and stores them
-      const long long row = (((long long)h * (BH / H) + b) * nkb + kb) * 4 + wave;
-      float wk[DTN * 16], wv[DTN * 16];
+      float wk[DTN * 16];
 #pragma unroll
       for (int dt = 0; dt < DTN; ++dt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          wk[16 * dt + i] = key < T ? dkt[dt][i] : 0.f;
-          wv[16 * dt + i] = key < T ? dvt[dt][i] : 0.f;
-        }
+        for (int i = 0; i < 16; ++i) wk[16 * dt + i] = key < T ? dkt[dt][i] : 0.f;
       lane32_sums(wk, r32);
-      lane32_sums(wv, r32);
 #pragma unroll
       for (int j = 0; j < DTN / 2; ++j) {
         const int rr = r32 * (DTN / 2) + j, i = rr & 15;
-        const int d = 32 * (rr >> 4) + 8 * (i >> 2) + 4 * hf + (i & 3);
-        BPK[row * HD + d] = wk[j];
-        BPV[row * HD + d] = wv[j];
+        BPK[brow * HD + 32 * (rr >> 4) + 8 * (i >> 2) + 4 * hf + (i & 3)] = wk[j];
       }
     }
     if constexpr (DIAG) d_acc[5] += stamp_dep(0.f) - d_t0;
@@ -1708,6 +1722,8 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
     if (sub == 1 && qb == nqb - 1 - p) break;
     if (sub == 1) __syncthreads();
     const int q0 = qb * BQ, wq0 = q0 + 32 * wave, qi = wq0 + r32;
+    // the query's RoPE position (low word of the int64), loaded with the block's prologue
+    const int qpos = (rpos && qi < T) ? reinterpret_cast<const int*>(rpos)[2 * ((long long)b * T + qi)] : 0;
     const int kv_end = causal ? min(T, q0 + BQ) : T;
     const int nkv = (kv_end + BKV - 1) / BKV;
     const bool fetched = sub == 1 && pre;   // tiles 0 / 1 and the Q / dO / O rows already on their way
@@ -1719,6 +1735,7 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
       load_qdo(qi);
     }
     wait_vmcnt<0>();
+    asm volatile("" ::"v"(qpos));   // (keeps the position load here, not sunk to its use)
     float dsum = 0.f;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
@@ -1838,8 +1855,8 @@ __global__ __launch_bounds__(256, (HD > 64 ? 1 : 2)) void attn_bwd_dq3_k(
 #pragma unroll
     for (int d = 0; d < DTN; ++d) dq[d] *= scale;
     if (rpos && qi < T) {
-      KASSERT(rpos[(long long)b * T + qi] >= 0, "rope position at query %d", qi);
-      const float* tr = rtab + rpos[(long long)b * T + qi] * HD;
+      KASSERT(qpos >= 0, "rope position at query %d", qi);
+      const float* tr = rtab + (long long)qpos * HD;
 #pragma unroll
       for (int dt = 0; dt < DTN / 2; ++dt)
 #pragma unroll

@@ -171,37 +171,6 @@ __device__ __forceinline__ float pair_sum(float x) {
 }
 
 
-// Sums over the 32 lanes of each wave half of N per-lane values (N a multiple of 32), as a
-// transpose reduction: at each halving step (partner lane l ^ m, m = 16, 8, 4, 2, 1) a lane
-// keeps the half of its values that its lane bit m selects and adds the partner's copy of that
-// half -- N - N/32 lane exchanges for the whole reduction instead of 5 N for a butterfly per
-// value.  m = 16 is v_permlane16_swap (VALU; called with (lower half, upper half) the swap hands
-// an even-row lane the partner's lower half and an odd-row lane the partner's upper half, so no
-// select); m = 8 .. 1 are ds_swizzle xor exchanges of the half the partner keeps.  On return lane
-// r32 holds in w[j] the sum of value r32 (N / 32) + j, j < N / 32 (the rest of w is scratch).
-template <int N>
-__device__ __forceinline__ void lane32_sums(float (&w)[N], int r32) {
-  static_assert(N % 32 == 0, "lane32_sums: N must be a multiple of 32");
-#pragma unroll
-  for (int k = 0; k < N / 2; ++k) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(w[k]), __float_as_uint(w[k + N / 2]), false, false);
-    w[k] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  }
-#define LANE32_STEP(M_, n_)                                                                        \
-  {                                                                                                \
-    const bool hi = r32 & (M_);                                                                    \
-    _Pragma("unroll") for (int k = 0; k < (n_) / 2; ++k) {                                         \
-      const float send = hi ? w[k] : w[k + (n_) / 2], keep = hi ? w[k + (n_) / 2] : w[k];          \
-      w[k] = keep + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(send), 0x1F | ((M_) << 10))); \
-    }                                                                                              \
-  }
-  LANE32_STEP(8, N / 2)
-  LANE32_STEP(4, N / 4)
-  LANE32_STEP(2, N / 8)
-  LANE32_STEP(1, N / 16)
-#undef LANE32_STEP
-}
-
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n (jump over the immediates 0..63).
 __device__ __forceinline__ void wait_vm_rt(int n) {
   switch (n) {

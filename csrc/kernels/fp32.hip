@@ -467,17 +467,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_f32_k(
 #pragma unroll
       for (int r = 0; r < 16; ++r) p[32 * d + 8 * (r >> 2) + 4 * hf + (r & 3)] = dq[d][r];
   }
-  if (BPQ) {   // column sums over the wave's 32 queries (fixed order)
+  if (BPQ) {   // column sums over the wave's 32 queries (transpose reduction, fixed order)
     const long long prow = (((long long)h * (gridDim.y / H) + b) * gridDim.x + qb) * 4 + wave;
+    constexpr int NV = DT * 16, NP = NV < 32 ? 32 : NV;   // (head_dim 32: padded with zeros)
+    float w[NP];
 #pragma unroll
-    for (int d = 0; d < DT; ++d)
+    for (int i = 0; i < NP; ++i) w[i] = (i < NV && qi < T) ? dq[i / 16 % DT][i % 16] : 0.f;
+    lane32_sums(w, r32);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float a = qi < T ? dq[d][r] : 0.f;
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) a += __shfl_xor(a, o, 64);
-        if (r32 == 0) BPQ[prow * HD + 32 * d + 8 * (r >> 2) + 4 * hf + (r & 3)] = a;
-      }
+    for (int j = 0; j < NP / 32; ++j) {
+      const int rr = r32 * (NP / 32) + j, r = rr & 15;
+      if (rr < NV) BPQ[prow * HD + 32 * (rr >> 4) + 8 * (r >> 2) + 4 * hf + (r & 3)] = w[j];
+    }
   }
 }
 
@@ -591,24 +592,26 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_f32_k(
         pv[c] = dv[d][r];
       }
   }
-  if (BPK) {
+  if (BPK) {   // column sums over the wave's 32 keys (transpose reduction, fixed order)
     const long long row = (((long long)h * (gridDim.y / H) + b) * gridDim.x + kb) * 4 + wave;
+    constexpr int NV = DT * 16, NP = NV < 32 ? 32 : NV;   // (head_dim 32: padded with zeros)
+    float wk[NP], wv[NP];
 #pragma unroll
-    for (int d = 0; d < DT; ++d)
+    for (int i = 0; i < NP; ++i) {
+      wk[i] = (i < NV && key < T) ? dk[i / 16 % DT][i % 16] : 0.f;
+      wv[i] = (i < NV && key < T) ? dv[i / 16 % DT][i % 16] : 0.f;
+    }
+    lane32_sums(wk, r32);
+    lane32_sums(wv, r32);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float a = key < T ? dk[d][r] : 0.f, c = key < T ? dv[d][r] : 0.f;
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
-          a += __shfl_xor(a, o, 64);
-          c += __shfl_xor(c, o, 64);
-        }
-        if (r32 == 0) {
-          const int cc = 32 * d + 8 * (r >> 2) + 4 * hf + (r & 3);
-          BPK[row * HD + cc] = a;
-          BPV[row * HD + cc] = c;
-        }
+    for (int j = 0; j < NP / 32; ++j) {
+      const int rr = r32 * (NP / 32) + j, r = rr & 15;
+      if (rr < NV) {
+        const int cc = 32 * (rr >> 4) + 8 * (r >> 2) + 4 * hf + (r & 3);
+        BPK[row * HD + cc] = wk[j];
+        BPV[row * HD + cc] = wv[j];
       }
+    }
   }
 }
 
