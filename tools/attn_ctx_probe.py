@@ -25,6 +25,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=30)
     ap.add_argument("--fwd", action="store_true")
+    ap.add_argument("--impls", type=int, nargs="*", default=[],
+                    help="backward implementations to compare as the step calls them (RoPE + bias), e.g. 4 6 7 9")
     a = ap.parse_args()
     C = _ext.require()
     B, T, H, hd = 32, 1024, 12, 64
@@ -53,7 +55,12 @@ def main():
         C.attn_fwd(q, k, v, scale, True)
 
     op = fwd if a.fwd else bwd
-    arms = {
+    if a.impls:   # implementation comparison only: every arm with RoPE + bias, as the step calls it
+        arms = {f"impl{i}": (None, (lambda i=i: C.attn_bwd(do, q, k, v, o, lse, scale, True, dq, dk, dv, pos, tab, db,
+                                                              impl=i))) for i in a.impls}
+    else:
+        arms = {}
+    arms = arms or {
         "hot": (None, op),
         "hot_rope": (None, (lambda: bwd(True)) if not a.fwd else op),
         "rope_only": (None, (lambda: bwd(True, False)) if not a.fwd else op),
