@@ -133,11 +133,20 @@ def _ours_variants(call: Callable[[int], torch.Tensor], widths: bool = False, sk
     is no longer a candidate; it remains the fallback for shapes the v4 launcher declines."""
     out = {"ours": lambda: call(0)}
     if widths:
-        out.update({"ours256": lambda: call(1), "ours192": lambda: call(2), "ours_nt": lambda: call(4),
-                    "ours256_nt": lambda: call(5), "ours192_nt": lambda: call(6)})
+        out.update({"ours256": lambda: call(1), "ours192": lambda: call(2)})
+        if NT_STORES:
+            out.update({"ours_nt": lambda: call(4), "ours256_nt": lambda: call(5), "ours192_nt": lambda: call(6)})
     if widths and sk:
-        out.update({"ours_sk": lambda: call(8), "ours_sk_nt": lambda: call(12)})
+        out.update({"ours_sk": lambda: call(8)})
+        if NT_STORES:
+            out["ours_sk_nt"] = lambda: call(12)
     return out
+
+
+# A/B hook (tools/ab_attr.py): the non-temporal-store variants among the per-shape candidates.
+# They are timed alone, where an output that streams past the caches can only help; in the
+# step the next kernel then reads that output from HBM instead of the infinity cache.
+NT_STORES = True
 
 
 def _sk_ok(k, M: int, N: int, K: int) -> bool:
