@@ -1597,7 +1597,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm4_m32", [](int v) { dpfs_gemm4_m32(v); },
         "TN main loop of the v4 GEMM: 1 = 32x32x16 MFMAs (default), 0 = 16x16x32 (A/B probes)");
   m.def("gemm4_br", [](int v) { dpfs_gemm4_br(v); },
-        "rows of MFMAs before each step's barrier in the plain v4 kernels (0, 1, 2; A/B runs)");
+        "rows of MFMAs before each step's barrier in the plain v4 kernels (0, 1, 2 = default; A/B runs)");
   m.def("gemm4_sched", [](int v) { dpfs_gemm4_sched(v); },
         "v4 main-loop variant: 0 = default (descriptor-advancing DMA where K ranges allow, one piece per MFMA "
         "row), 1 = two pieces per row in rows 4-7, 2 = per-lane K checks everywhere (the pre-FAST stream)");

@@ -1383,7 +1383,9 @@ extern "C" void dpfs_gemm4_diag(void* p) { g_g4_diag = (unsigned long long*)p; }
 static int g_g4_sched = 0;
 extern "C" void dpfs_gemm4_sched(int v) { g_g4_sched = v; }
 // Rows of MFMAs before each step's barrier (gemm4_k's BR) of the plain FAST kernels: 0, 1, 2.
-static int g_g4_br = 0;
+// 2 (default since the end of round 6): -0.18 ms per training step against 0 in 6 of 6
+// same-box interleaved rounds (profiles/r6_gemm_br_ab.txt); 1 is within 0.01 ms of 2.
+static int g_g4_br = 2;
 extern "C" void dpfs_gemm4_br(int v) { g_g4_br = (v >= 0 && v <= 2) ? v : 0; }
 extern "C" void dpfs_gemm4_group_m(int g) { g_g4_group_m = g > 0 ? g : 4; }
 // TN main loop: 1 = the 32x32x16 form (gemm4_k's M32, default), 0 = 16x16x32 (A/B probes).
