@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-6 GPU check 42: barrier row 2 in the SwiGLU / SwiGLU-backward / RoPE / non-temporal-store
+# Round-6 GPU check 42: barrier row 1 in the SwiGLU / SwiGLU-backward / RoPE forms and 2 in the non-temporal-store forms (was: barrier row 2 in the SwiGLU / SwiGLU-backward / RoPE / non-temporal-store
 # GEMM forms too -- GEMM + model GPU tests (fused forms checked bitwise against the separate
 # kernels), step A/B against the plain-forms-only build (same box, interleaved).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
