@@ -29,6 +29,7 @@ void dpfs_gemm_nt_rope(const void*, const void*, void*, const float*, int, int, 
                        const float*, int, int, int, hipStream_t);
 void dpfs_gemm4_sched(int);
 void dpfs_gemm4_br(int);
+void dpfs_gemm4_br_tn(int);
 void dpfs_gemm4_m32(int);
 void dpfs_attn_prefetch(int);
 void dpfs_gemm4_swb_depth(int);
@@ -1601,6 +1602,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm4_sched", [](int v) { dpfs_gemm4_sched(v); },
         "v4 main-loop variant: 0 = default (descriptor-advancing DMA where K ranges allow, one piece per MFMA "
         "row), 1 = two pieces per row in rows 4-7, 2 = per-lane K checks everywhere (the pre-FAST stream)");
+  m.def("gemm4_br_tn", [](int v) { dpfs_gemm4_br_tn(v); },
+        "blocks of 4 MFMAs before each step's barrier in the 32x32x16 (TN weight-gradient) main loop (0 default, 1, 2; A/B)");
   m.def("gemm4_group_m", [](int v) { dpfs_gemm4_group_m(v); }, "v4 tile-row group size of the item order (default 4)");
   m.def("gemm_v2_sched", [](int v) { dpfs_gemm_v2_sched(v); }, "v2 256x256 schedule (-1 per-layout default, 0..4 see gemm2_k SCHED)");
   m.def("gemm_set_impl", [](int v) { dpfs_gemm_set_impl(v); }, "1 = v1 (128x128 register-staged), 2 = v2 (LDS-DMA, one tile per workgroup), 3 = v3 (persistent v2, default)");

@@ -871,7 +871,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
   static_assert(!SWB || (OUT == 0 && BN == 256 && ROPE == 0 && !SWIGLU), "SwiGLU-backward epilogue: bf16 256-wide tiles");
   static_assert(BN == 256 || BN == 192, "tile width");
   static_assert(BR >= 0 && BR <= 4 && (BR == 0 || DIAG == 0), "barrier row");
-  static_assert(!M32 || ((AK ? true : (!BKM && OUT == 1)) && BN == 256 && BR == 0 && SCHED == 1 && ROPE == 0 &&
+  static_assert(!M32 || ((AK ? true : (!BKM && OUT == 1)) && BN == 256 && SCHED == 1 && ROPE == 0 &&
                           !SWIGLU && !SWB),
                 "32x32x16 main loop: TN fp32, NN / NT fp32 or bf16 (+ bias), 256-wide");
   static_assert(!GRP || (M32 && FAST), "grouped TN: the 32x32x16 FAST kernel");
@@ -1156,22 +1156,26 @@ __global__ __launch_bounds__(256, 1) void gemm4_k(const bf16* __restrict__ A, co
     const char* src = smem + c_slot * SLOT;
     if constexpr (M32) {
       // 32 MFMAs t = 16 kk + 4 bi + bj; after MFMA t < 16 the next step's fragment t (A for
-      // t < 8, B after: two transposed reads each); DMA piece q after MFMA 4 q + 2.
+      // t < 8, B after: two transposed reads each); DMA piece q after MFMA 4 q + 2.  BR > 0:
+      // the wait + barrier after MFMA 4 BR - 1 (BR blocks of 4 MFMAs on fragments already in
+      // registers ahead of it) and the next step's reads shifted behind it by 4 BR MFMAs.
       static_for<0, 32>([&](auto T) {
         constexpr int t = decltype(T)::value;
         constexpr int kk = t >> 4, bi = (t >> 2) & 3, bj = t & 3;
+        constexpr int tr = t - 4 * BR;   // read slot of this MFMA
         acc32_mfma<bi, bj, ZR && kk == 0>(cur.b.get(2 * bj + kk), cur.a.get(2 * bi + kk));
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (t == 0) stage_rsrc_a();
         if constexpr (t == 1) stage_rsrc_b();
-        // next step's fragments: block nb of A after MFMA 2 nb, of B after MFMA 8 + 2 nb
-        if constexpr (!NOPF && t < 8 && (t & 1) == 0) {
-          if constexpr (AK) nxt.a.load_nb(t >> 1, src + k32a[0], src + k32a[1]);
-          else nxt.a.load_nb(t >> 1, src + m32a[t >> 1]);
+        if constexpr (BR > 0 && t == 4 * BR - 1) sync();
+        // next step's fragments: block nb of A after MFMA 4 BR + 2 nb, of B after 4 BR + 8 + 2 nb
+        if constexpr (!NOPF && tr >= 0 && tr < 8 && (tr & 1) == 0) {
+          if constexpr (AK) nxt.a.load_nb(tr >> 1, src + k32a[0], src + k32a[1]);
+          else nxt.a.load_nb(tr >> 1, src + m32a[tr >> 1]);
         }
-        if constexpr (!NOPF && t >= 8 && t < 16 && (t & 1) == 0) {
-          if constexpr (BKM) nxt.b.load_nb((t - 8) >> 1, src + k32b[0], src + k32b[1]);
-          else nxt.b.load_nb((t - 8) >> 1, src + m32b[(t - 8) >> 1]);
+        if constexpr (!NOPF && tr >= 8 && tr < 16 && (tr & 1) == 0) {
+          if constexpr (BKM) nxt.b.load_nb((tr - 8) >> 1, src + k32b[0], src + k32b[1]);
+          else nxt.b.load_nb((tr - 8) >> 1, src + m32b[(tr - 8) >> 1]);
         }
         if constexpr ((t & 3) == 2 && (t >> 2) < NQ) issue(t >> 2);
         __builtin_amdgcn_sched_barrier(0);
@@ -1374,6 +1378,10 @@ static int g_g4_group_m = 4;
 // returns zeros, no memory traffic), 4 = no DMA wait, 8 = no step barrier (wrong results).
 // Bits 4 / 8 (and 1024: none) run the DIAG-3 build of the NT 256-wide kernel, the only one
 // that reads them.
+// Blocks of 4 MFMAs ahead of each step's wait + barrier in the 32x32x16 (TN weight-gradient)
+// main loop: 0 (default), 1, 2 (A/B hook).
+static int g_g4_br_tn = 0;
+extern "C" void dpfs_gemm4_br_tn(int v) { g_g4_br_tn = (v >= 0 && v <= 2) ? v : 0; }
 static int g_g4_ablate = 0;
 static unsigned long long* g_g4_diag = nullptr;   // [grid][4 waves][wait, body, epilogue, valid]
 extern "C" void dpfs_gemm4_ablate(int v) { g_g4_ablate = v; }
@@ -1580,8 +1588,15 @@ extern "C" bool dpfs_gemm4_launch(int layout, int out_f32, const void* A, const 
     }                                                                                             \
     if constexpr (!AK_ && !BK_ && OUT_ == 1) {                                                    \
       if (fast && sched == 1 && g_g4_m32) {                                                       \
-        gemm4_k<false, false, 1, 0, true, 1, 256, 0, false, false, 0, 0, true>                    \
-            <<<grid, 256, 0, s>>>(G4_ARGS);                                                       \
+        if (g_g4_br_tn == 1)                                                                      \
+          gemm4_k<false, false, 1, 0, true, 1, 256, 0, false, false, 1, 0, true>                  \
+              <<<grid, 256, 0, s>>>(G4_ARGS);                                                     \
+        else if (g_g4_br_tn == 2)                                                                 \
+          gemm4_k<false, false, 1, 0, true, 1, 256, 0, false, false, 2, 0, true>                  \
+              <<<grid, 256, 0, s>>>(G4_ARGS);                                                     \
+        else                                                                                      \
+          gemm4_k<false, false, 1, 0, true, 1, 256, 0, false, false, 0, 0, true>                  \
+              <<<grid, 256, 0, s>>>(G4_ARGS);                                                     \
         break;                                                                                    \
       }                                                                                           \
     }                                                                                             \
@@ -1875,10 +1890,15 @@ extern "C" int dpfs_gemm_tn_group(int n, const void* const* A, const void* const
   const int grid = (int)std::min<long long>(items, g4_cu_count());
   const Rope rope = {nullptr, nullptr, 0, 64};
   const Dual dual = {nullptr, nullptr, 0x7fffffff, 0, 0, 0u, 0u};
-  gemm4_k<false, false, 1, 0, true, 1, 256, 0, false, false, 0, 0, true, true><<<grid, 256, 0, s>>>(
-      grp.d[0].A, grp.d[0].B, grp.d[0].C, nullptr, 256, 256, K1 ? ksw + K1 : K, lda[0], ldb[0], N[0], kps, S, 0,
-      grp.d[0].a_bytes,
-      grp.d[0].b_bytes, grp.d[0].c_bytes, rope, g_g4_group_m, dual, 0, nullptr, SwiOut{}, SwiBwd{}, grp);
+#define G4_GRP(BR_)                                                                                         \
+  gemm4_k<false, false, 1, 0, true, 1, 256, 0, false, false, BR_, 0, true, true><<<grid, 256, 0, s>>>(       \
+      grp.d[0].A, grp.d[0].B, grp.d[0].C, nullptr, 256, 256, K1 ? ksw + K1 : K, lda[0], ldb[0], N[0], kps, S, 0, \
+      grp.d[0].a_bytes, grp.d[0].b_bytes, grp.d[0].c_bytes, rope, g_g4_group_m, dual, 0, nullptr, SwiOut{},     \
+      SwiBwd{}, grp)
+  if (g_g4_br_tn == 1) G4_GRP(1);
+  else if (g_g4_br_tn == 2) G4_GRP(2);
+  else G4_GRP(0);
+#undef G4_GRP
   if (slabs) {
     long long gr = (mn / 4 + 255) / 256;
     if (gr > 4096) gr = 4096;
