@@ -486,18 +486,6 @@ __device__ __forceinline__ void epilogue(const char* bias_lds, const Item& ci, v
   const int g = l >> 4;
   const int wcol0 = ci.n0 + wn * (BN / 2);
   const int row0 = ci.m0 + wm * 128 + (l & 15);
-  // RoPE: the 8 row blocks' positions (low words of the int64s) are loaded before the drain, so
-  // each block's table loads below are one dependent load away instead of two
-  constexpr int HDR = (OUT == 0 && BN == 256) ? ROPE : 0;
-  int rpos8[HDR ? 8 : 1];
-  if constexpr (HDR != 0) {
-    const bool rope_here = rope.cols > 0 && wcol0 < rope.cols;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = row0 + 16 * i;
-      rpos8[i] = (rope_here && m < M) ? reinterpret_cast<const int*>(rope.pos)[2 * (long long)m] : 0;
-    }
-  }
   acc_drain();
   if constexpr (OUT == 0) {
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(C, (short)0, (int)c_bytes, 0x00020000);
@@ -515,8 +503,9 @@ __device__ __forceinline__ void epilogue(const char* bias_lds, const Item& ci, v
     const bool do_rope = HD && rope.cols > 0 && wcol0 < rope.cols;
     f32x4 cs[HJ], sn[HJ];
     auto rope_load = [&](int i) {
-      const long long pp = rpos8[HD ? i : 0];
-      KASSERT(row0 + 16 * i >= M || pp >= 0, "rope position %lld at row %d", pp, row0 + 16 * i);
+      const int m = row0 + 16 * i;
+      const long long pp = m < M ? rope.pos[m] : 0;
+      KASSERT(m >= M || pp >= 0, "rope position %lld at row %d", pp, m);
       const float* tr = rope.tab + pp * HD;
 #pragma unroll
       for (int jh = 0; jh < HJ; ++jh) {
