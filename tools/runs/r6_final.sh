@@ -11,7 +11,7 @@ bash tools/gpu_steps.sh \
   "700|suite_rh|python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -k rehearsal -p no:cacheprovider" \
   "300|smoke|python -u -c 'import __graft_entry__ as g; g.smoke()'" \
   "300|bench|python -u bench.py" \
-  "300|prof_final|bash tools/prof_step.sh r6final5"
+  "300|prof_final|bash tools/prof_step.sh r6final6"
 rc=$?
 kill $TICK
 exit $rc
